@@ -1,0 +1,579 @@
+/* pd_oracle.c -- scalar CPU restatement of the reference env (TEST INFRASTRUCTURE, see pd_oracle.h).
+ * Build: oracle/Makefile (gcc -O2 -ffp-contract=off: no FMA contraction, like CPython).
+ * Every function names the reference file:line it restates. */
+#include "pd_oracle.h"
+#include <math.h>
+#include <string.h>
+#include <stdlib.h>
+
+#define N_NB 50
+#define N_SYS (N_NB + 3)
+
+/* CPython math.radians / math.degrees (mathmodule.c: x * (pi/180), x * (180/pi)) */
+static const double DEG2RAD = 3.141592653589793 / 180.0;
+static const double RAD2DEG = 180.0 / 3.141592653589793;
+static double radians(double x) { return x * DEG2RAD; }
+static double degrees(double x) { return x * RAD2DEG; }
+static const double PI = 3.141592653589793;
+
+/* ---------------------------------------------------------------- atmosphere
+ * atmosphere_dynamics.py:5-27 -> ambiance.Atmosphere (third-party, absent here; its
+ * published ISA/US-1976 layer model restated: geopotential H = r h/(r+h), layer base
+ * table, T = Tb + beta (H-Hb), p = pb (1+beta/Tb (H-Hb))^(-g0/(beta R)) or
+ * pb exp(-g0/(R T) (H-Hb)), rho = p/(R T), a = sqrt(kappa R T)). */
+void orc_atmosphere(const orc_params* P, double alt, double* rho, double* p, double* a) {
+    if (alt < 0) alt = 0.0;
+    if (alt < P->isa_alt_max) {
+        double H = P->isa_r * alt / (P->isa_r + alt);
+        int i = 0;
+        for (int k = 0; k < 9; ++k) if (P->isa_Hb[k] <= H) i = k;  /* searchsorted(side=right)-1 */
+        double Hb = P->isa_Hb[i], Tb = P->isa_Tb[i], b = P->isa_beta[i], pb = P->isa_pb[i];
+        double T = Tb + b * (H - Hb);
+        double pp;
+        if (b != 0.0) pp = pb * pow(1.0 + b / Tb * (H - Hb), -P->isa_g0 / (b * P->isa_R));
+        else pp = pb * exp(-P->isa_g0 / (P->isa_R * T) * (H - Hb));
+        *p = pp;
+        *rho = pp / (P->isa_R * T);
+        *a = sqrt(P->isa_kappa * P->isa_R * T);
+    } else {
+        *rho = 0.0; *p = 0.0; *a = 0.0;
+    }
+}
+
+/* atmosphere_dynamics.py:29-33 */
+double orc_gravity(const orc_params* P, double alt) {
+    double q = P->grav_R / (P->grav_R + alt);
+    return P->grav_g0 * (q * q);
+}
+
+/* ---------------------------------------------------------------- RBF
+ * scipy.interpolate.RBFInterpolator(points, coef, kernel='thin_plate_spline',
+ * neighbors=50) as called by aerodynamic_coefficients.py:57-66: per query a 50-NN
+ * search (euclidean, raw (Mach, AoA-deg) space), neighbourhood sorted by index,
+ * 53x53 system [[K, P],[P^T, 0]] with K_ij = r^2 log r, P = [1, (y-shift)/scale],
+ * shift = (min+max)/2, scale = (max-min)/2 (0 -> 1); solved by LU with partial pivoting
+ * (LAPACK dgesv); value = sum phi(|x-y_j|) c_j + [1, xhat] . c_poly. */
+static double tps(double r) { return r == 0.0 ? 0.0 : r * r * log(r); }
+
+static int lu_solve(double* A, double* b, int n) {
+    int piv[N_SYS];
+    for (int k = 0; k < n; ++k) {
+        int p = k; double best = fabs(A[k * n + k]);
+        for (int i = k + 1; i < n; ++i) { double v = fabs(A[i * n + k]); if (v > best) { best = v; p = i; } }
+        if (best == 0.0) return -1;
+        piv[k] = p;
+        if (p != k) {
+            for (int j = 0; j < n; ++j) { double t = A[k * n + j]; A[k * n + j] = A[p * n + j]; A[p * n + j] = t; }
+            double t = b[k]; b[k] = b[p]; b[p] = t;
+        }
+        double r = 1.0 / A[k * n + k];
+        for (int i = k + 1; i < n; ++i) {
+            double l = A[i * n + k] * r;
+            A[i * n + k] = l;
+            if (l != 0.0) for (int j = k + 1; j < n; ++j) A[i * n + j] -= l * A[k * n + j];
+            b[i] -= l * b[k];
+        }
+    }
+    for (int i = n - 1; i >= 0; --i) {
+        double s = b[i];
+        for (int j = i + 1; j < n; ++j) s -= A[i * n + j] * b[j];
+        b[i] = s / A[i * n + i];
+    }
+    (void)piv;
+    return 0;
+}
+
+double orc_rbf(const orc_params* P, int which, double mach, double aoa) {
+    const double *pm = which ? P->cl_m : P->cd_m, *pa = which ? P->cl_a : P->cd_a,
+                 *pc = which ? P->cl_c : P->cd_c;
+    int n = which ? P->cl_n : P->cd_n;
+    /* 50 nearest: selection by (d2, index) */
+    double bd[N_NB]; int bi[N_NB]; int cnt = 0;
+    for (int i = 0; i < n; ++i) {
+        double dm = mach - pm[i], da = aoa - pa[i];
+        double d2 = dm * dm + da * da;
+        if (cnt < N_NB || d2 < bd[cnt - 1]) {
+            int pos = cnt < N_NB ? cnt : N_NB - 1;
+            while (pos > 0 && bd[pos - 1] > d2) { if (pos < N_NB) { bd[pos] = bd[pos - 1]; bi[pos] = bi[pos - 1]; } --pos; }
+            bd[pos] = d2; bi[pos] = i;
+            if (cnt < N_NB) ++cnt;
+        }
+    }
+    /* sort neighbour indices ascending (np.sort(yindices)) */
+    for (int i = 1; i < N_NB; ++i) { int v = bi[i], j = i; while (j > 0 && bi[j - 1] > v) { bi[j] = bi[j - 1]; --j; } bi[j] = v; }
+    double ym[N_NB], ya[N_NB], yd[N_NB];
+    double mn0 = 1e300, mx0 = -1e300, mn1 = 1e300, mx1 = -1e300;
+    for (int j = 0; j < N_NB; ++j) {
+        ym[j] = pm[bi[j]]; ya[j] = pa[bi[j]]; yd[j] = pc[bi[j]];
+        if (ym[j] < mn0) mn0 = ym[j]; if (ym[j] > mx0) mx0 = ym[j];
+        if (ya[j] < mn1) mn1 = ya[j]; if (ya[j] > mx1) mx1 = ya[j];
+    }
+    double sh0 = (mx0 + mn0) / 2, sc0 = (mx0 - mn0) / 2, sh1 = (mx1 + mn1) / 2, sc1 = (mx1 - mn1) / 2;
+    if (sc0 == 0.0) sc0 = 1.0;
+    if (sc1 == 0.0) sc1 = 1.0;
+    double A[N_SYS * N_SYS];
+    double b[N_SYS];
+    for (int i = 0; i < N_NB; ++i) {
+        for (int j = 0; j < N_NB; ++j) {
+            double d0 = ym[i] - ym[j], d1 = ya[i] - ya[j];
+            A[i * N_SYS + j] = tps(sqrt(d0 * d0 + d1 * d1));
+        }
+        double h0 = (ym[i] - sh0) / sc0, h1 = (ya[i] - sh1) / sc1;
+        A[i * N_SYS + N_NB] = 1.0; A[i * N_SYS + N_NB + 1] = h0; A[i * N_SYS + N_NB + 2] = h1;
+        A[N_NB * N_SYS + i] = 1.0; A[(N_NB + 1) * N_SYS + i] = h0; A[(N_NB + 2) * N_SYS + i] = h1;
+        b[i] = yd[i];
+    }
+    for (int i = N_NB; i < N_SYS; ++i) { for (int j = N_NB; j < N_SYS; ++j) A[i * N_SYS + j] = 0.0; b[i] = 0.0; }
+    if (lu_solve(A, b, N_SYS) != 0) return NAN;
+    double v = 0.0;
+    for (int j = 0; j < N_NB; ++j) {
+        double d0 = mach - ym[j], d1 = aoa - ya[j];
+        v += tps(sqrt(d0 * d0 + d1 * d1)) * b[j];
+    }
+    v += 1.0 * b[N_NB];
+    v += (mach - sh0) / sc0 * b[N_NB + 1];
+    v += (aoa - sh1) / sc1 * b[N_NB + 2];
+    return v;
+}
+
+/* rockets_physics.py:712 CD_func = rocket_CD(M, degrees(alpha)); aerodynamic_coefficients.py:105-115
+ * (the clamp compares the DEGREE value against radians(10): bug kept) */
+double orc_CD(const orc_params* P, double mach, double alpha_rad) {
+    double aoa = degrees(alpha_rad);
+    double r10 = radians(10.0);
+    if (aoa > r10) return orc_rbf(P, 0, mach, r10);
+    else if (aoa < radians(-10.0)) return orc_rbf(P, 0, mach, radians(-10.0));
+    return orc_rbf(P, 0, mach, aoa);
+}
+
+/* rockets_physics.py:711 CL_func = rocket_CL(M, degrees(alpha)) and rocket_CL converts to
+ * degrees AGAIN (aerodynamic_coefficients.py:117-132): a = deg(deg(alpha)) */
+double orc_CL(const orc_params* P, double mach, double alpha_rad) {
+    double a = degrees(degrees(alpha_rad));
+    if (a > 10) return orc_rbf(P, 1, mach, 10.0);
+    else if (a < -10) return orc_rbf(P, 1, mach, -10.0);
+    else if (fabs(a) < 1e-6) return 0.0;
+    else if (a < 0) return -orc_rbf(P, 1, mach, fabs(a));
+    return orc_rbf(P, 1, mach, a);
+}
+
+/* ---------------------------------------------------------------- grid fins
+ * grid_fin_aerodynamics.py:7-18: interp1d(kind='linear', fill_value='extrapolate')
+ * -> scipy _call_linear: idx = searchsorted(x, M).clip(1, n-1) */
+double orc_Ca(const orc_params* P, double mach) {
+    if (mach < P->ca_min_mach) return P->ca_min_val;
+    int n = P->ca_n, idx = 0;
+    while (idx < n && P->ca_x[idx] < mach) ++idx;   /* searchsorted side='left' */
+    if (idx < 1) idx = 1;
+    if (idx > n - 1) idx = n - 1;
+    double xl = P->ca_x[idx - 1], xh = P->ca_x[idx], yl = P->ca_y[idx - 1], yh = P->ca_y[idx];
+    double slope = (yh - yl) / (xh - xl);
+    return slope * (mach - xl) + yl;
+}
+
+/* np.interp (numpy compiled_base.c arr_interp) for one in-range query */
+static double np_interp(const double* x, const double* y, int n, double v) {
+    if (v < x[0]) return y[0];
+    if (v > x[n - 1]) return y[n - 1];
+    if (v == x[n - 1]) return y[n - 1];
+    int j = 0;
+    while (j + 1 < n && x[j + 1] <= v) ++j;
+    if (x[j] == v) return y[j];
+    double slope = (y[j + 1] - y[j]) / (x[j + 1] - x[j]);
+    return slope * (v - x[j]) + y[j];
+}
+
+/* grid_fin_aerodynamics.py:21-46 */
+double orc_Cn(const orc_params* P, double mach, double alpha_rad) {
+    double ad = degrees(alpha_rad);
+    double cna;
+    if (mach < P->cn_min_mach) cna = P->cn_min_val;
+    else if (mach <= P->cn_max_mach) cna = np_interp(P->cn_x, P->cn_y, P->cn_n, mach);
+    else cna = P->cn_max_val + P->cn_slope * (mach - P->cn_max_mach);
+    return cna * ad;
+}
+
+/* ---------------------------------------------------------------- mass properties
+ * stage_inertia closure (rocket_dimensions.py:167-196), stage-2 constants */
+void orc_inertia(const orc_params* P, double fill, double* x_cog, double* inertia) {
+    double h_ox_t = P->h_ox * fill, h_f_t = P->h_f * fill, m_ox_t = P->m_ox * fill, m_f_t = P->m_f * fill;
+    double x_prop = (m_ox_t * (P->h_lower + h_ox_t / 2) + m_f_t * (P->h_lower + P->h_ox + h_f_t / 2)) / (m_ox_t + m_f_t);
+    double t1 = P->h_lower + h_ox_t / 2 - x_prop;
+    double I_ox = 1.0 / 12 * m_ox_t * (h_ox_t * h_ox_t) + m_ox_t * (t1 * t1);
+    double t2 = P->h_lower + P->h_ox + h_f_t / 2 - x_prop;
+    double I_f = 1.0 / 12 * m_f_t * (h_f_t * h_f_t) + m_f_t * (t2 * t2);
+    double I_prop = I_ox + I_f;
+    double x_wet = (P->m_dry * P->x_dry + (m_ox_t + m_f_t) * x_prop) / (P->m_dry + m_ox_t + m_f_t);
+    double t3 = P->x_dry - x_wet, t4 = x_prop - x_wet;
+    double I_dry_hat = P->I_dry + P->m_dry * (t3 * t3);
+    double I_prop_hat = I_prop + (m_ox_t + m_f_t) * (t4 * t4);
+    *x_cog = x_wet;
+    *inertia = I_dry_hat + I_prop_hat;
+}
+
+/* ---------------------------------------------------------------- ACS (acs_model.py:13-87) */
+typedef struct { double f_perp, f_par, m_z, dcmd_l, dcmd_r, ca, cn_l; } acs_res;
+static acs_res acs(const orc_params* P, double alpha_eff, double q, double mach, double x_cog,
+                   double cmd_l_deg, double cmd_r_deg, double prev_l, double prev_r, double dt) {
+    acs_res r;
+    r.dcmd_l = radians(cmd_l_deg);   /* caller already multiplied by 60 (f32 or f64 path) */
+    r.dcmd_r = radians(cmd_r_deg);
+    double dl = prev_l + dt * ((-prev_l + r.dcmd_l) / 0.5);
+    double dr = prev_r + dt * ((-prev_r + r.dcmd_r) / 0.5);
+    double all = alpha_eff - dl, alr = alpha_eff - dr;
+    double qS = q * P->S_gf;
+    double Ca = orc_Ca(P, mach), CnL = orc_Cn(P, mach, all), CnR = orc_Cn(P, mach, alr);
+    double cl = cos(dl), cr = cos(dr), sl = sin(dl), sr = sin(dr);
+    r.f_perp = qS * (CnR * cr - CnL * cl - Ca * (sl - sr));
+    r.f_par = qS * (Ca * (2 + cl + cr) - CnL * sl + CnR * sr);
+    r.m_z = -(P->d_base_gf - x_cog) * r.f_perp + P->R_rocket * qS * (Ca * (sr - sl) - CnL * cl + CnR * cr);
+    r.ca = Ca; r.cn_l = CnL;
+    return r;
+}
+
+/* ---------------------------------------------------------------- wind (full_wind_model.py:35-43) */
+static double wind_profile(const orc_params* P, double y) {
+    /* HorizontalWindSpeed.py:58-68: interp1d(alt_km, speed, fill_value=(first,last)) */
+    double km = y / 1000.0;
+    int n = P->wind_n;
+    if (km < P->wind_alt_km[0]) return P->wind_speed[0];
+    if (km > P->wind_alt_km[n - 1]) return P->wind_speed[n - 1];
+    return np_interp(P->wind_alt_km, P->wind_speed, n, km);
+}
+
+static void vk_step(const double* Ad, const double* Bd, double sigma, double* s, double w) {
+    /* vonkarman.py:33-36: state = Ad @ state + Bd * w, Bd = sigma * Bd(sigma=1) */
+    double n0 = (Ad[0] * s[0] + Ad[1] * s[1]) + (sigma * Bd[0]) * w;
+    double n1 = (Ad[2] * s[0] + Ad[3] * s[1]) + (sigma * Bd[1]) * w;
+    s[0] = n0; s[1] = n1;
+}
+
+/* ---------------------------------------------------------------- one physics sub-step
+ * rocket_physics_fcn (rockets_physics.py:455-704) with the landing-burn control laws
+ * force_moment_decomposer_landing_burn_throttle_only (:340-400) and
+ * force_moment_decomposer_landing_burn_gimballed (:168-269). */
+static void substep(const orc_params* P, orc_env* E, int phase, const double* u, int f32,
+                    double dt, double dt_act, const double* noise2, double* info) {
+    double* s = E->s;
+    double x = s[0], y = s[1], vx = s[2], vy = s[3], th = s[4], thd = s[5], ga = s[6], al = s[7];
+    double m = s[8], mp = s[9], t = s[10];
+    double rho, patm, a;
+    orc_atmosphere(P, y, &rho, &patm, &a);
+    double speed = sqrt(vx * vx + vy * vy);
+    double mach = 0.0;
+    if (a != 0.0) { double mr = speed / a; mach = (10.0 < mr) ? 10.0 : mr; }   /* min(speed/a, 10.0) */
+    double q = 0.5 * rho * (speed * speed);
+    double fpc = (P->m_prop0 - mp) / P->m_prop0;
+    if (fpc == 0.0) fpc = 1e-6;
+    double x_cog, inertia;
+    orc_inertia(P, 1 - fpc, &x_cog, &inertia);
+    double d_thrust = x_cog + P->engine_height;
+    double ae = (vy < 0) ? ga - th - PI : al;
+    double d_cp_cg = x_cog - P->cop;
+    double ug = 0.0, vg = 0.0;
+    if (E->wind_on) {
+        ug = wind_profile(P, y);
+        if (y < P->vk_y_threshold && E->wind_stoch) {
+            /* vonkarman.py:34: one np.random.randn() per filter step, u first then v */
+            double w0 = 0.0, w1 = 0.0;
+            if (noise2) {
+                int off = E->noise_slotted ? 0 : E->noise_used;
+                w0 = noise2[off]; w1 = noise2[off + 1];
+            }
+            E->noise_used += 2;
+            vk_step(P->vk_Ad_u, P->vk_Bd_u, E->sigma_u, E->fu, w0);
+            vk_step(P->vk_Ad_v, P->vk_Bd_v, E->sigma_v, E->fv, w1);
+            ug = ug + E->fu[1];
+            vg = E->fv[1];
+        }
+    }
+    double Fwx = 0.5 * rho * (ug * ug) * P->A_front * P->C_gust_x;
+    double Fwy = 0.5 * rho * (vg * vg) * P->A_front * P->C_gust_y;
+    double Mw = -d_cp_cg * Fwy;
+    double CL = 0.0, CD = 0.0;
+    if (a != 0.0) { CL = orc_CL(P, mach, ae); CD = orc_CD(P, mach, ae); }
+    double drag = 0.5 * rho * (speed * speed) * CD * P->A_front;
+    double lift = 0.5 * rho * (speed * speed) * CL * P->A_front;
+    double apar, aperp;
+    if (vy >= 0.0) { apar = lift * sin(ae) - drag * cos(ae); aperp = -lift * cos(ae) - drag * sin(ae); }
+    else { apar = drag * cos(ae) - lift * sin(ae); aperp = -drag * sin(ae) - lift * cos(ae); }
+    double aero_x = apar * cos(th) + aperp * sin(th);
+    double aero_y = apar * sin(th) - aperp * cos(th);
+    double aero_m = aperp * d_cp_cg;
+
+    double T_full = P->T_e + (P->p_e - patm) * P->A_e;
+    double cfp, cfperp, cm, mdot_dt, mdot_info, throttle_info, gimbal_deg_out = 0.0;
+    acs_res ac;
+    if (phase == ORC_PHASE_PURE_THROTTLE) {
+        const double nominal = (0 * 0.4) / (double)P->n_eng;
+        if (f32) {
+            float u0 = (float)u[0];
+            float nnt = (u0 + 1.0f) / 2.0f;
+            float thr = nnt * (float)(1 - nominal) + (float)nominal;
+            float tg = (float)(T_full * P->n_eng) * thr;
+            float ntot = tg / (float)T_full;
+            float md = (float)(P->T_e / P->v_ex) * ntot;
+            ac = acs(P, ae, q, mach, x_cog, 0.0, 0.0, 0.0, 0.0, dt_act);
+            cfp = (double)tg + ac.f_par;
+            cfperp = ac.f_perp; cm = ac.m_z;
+            mdot_dt = (double)(md * (float)dt);
+            mdot_info = md; throttle_info = thr;
+        } else {
+            double u0 = u[0];
+            double nnt = (u0 + 1) / 2;
+            double thr = nnt * (1 - nominal) + nominal;
+            double tg = T_full * P->n_eng * thr;
+            double ntot = tg / T_full;
+            double md = (P->T_e / P->v_ex) * ntot;
+            ac = acs(P, ae, q, mach, x_cog, 0.0, 0.0, 0.0, 0.0, dt_act);
+            cfp = tg + ac.f_par; cfperp = ac.f_perp; cm = ac.m_z;
+            mdot_dt = md * dt; mdot_info = md; throttle_info = thr;
+        }
+    } else {
+        /* landing_burn: 18 gimballed engines, nominal 3*0.4/16, gimbal 5 deg, fins radians(20) */
+        const int n_eng = P->n_eng + 2;
+        const double nominal = (3 * 0.4) / (double)P->n_eng;
+        const double max_gimbal_rad = radians(5.0), max_defl = radians(20.0);
+        const double max_gimbal_deg = degrees(max_gimbal_rad);
+        double gdeg_cmd, thr_d, tg_d, tpar, tperp, mz, md_d, cmd_l, cmd_r;
+        float thr_f = 0.0f, md_f = 0.0f;
+        if (f32) {
+            float u0 = (float)u[0], u1 = (float)u[1], u2 = (float)u[2], u3 = (float)u[3];
+            float grad = u0 * (float)max_gimbal_rad;
+            gdeg_cmd = degrees((double)grad);
+            double gd = E->gimbal_prev + dt_act * ((-E->gimbal_prev + gdeg_cmd) / 1.0);
+            if (gd < -max_gimbal_deg) gd = -max_gimbal_deg;
+            if (gd > max_gimbal_deg) gd = max_gimbal_deg;
+            double grad2 = radians(gd);
+            float nnt = (u1 + 1.0f) / 2.0f;
+            thr_f = nnt * (float)(1 - nominal) + (float)nominal;
+            float tg = (float)(T_full * n_eng) * thr_f;
+            float fpar = tg * (float)cos(grad2);
+            float fperp = (-tg) * (float)sin(grad2);
+            /* (-T sin d) * d_thrust_cg: d_thrust_cg is np.float64 (x_cog derives from the
+             * np.float64 state), so this last product promotes to binary64 */
+            float fm = (-tg) * (float)sin(grad2);
+            float tot = sqrtf(fpar * fpar + fperp * fperp);
+            float ntot = tot / (float)T_full;
+            md_f = (float)(P->T_e / P->v_ex) * ntot;
+            gimbal_deg_out = degrees(grad2);
+            float dl = u2 * (float)max_defl, dr = u3 * (float)max_defl;
+            cmd_l = (double)(dl * (float)60); cmd_r = (double)(dr * (float)60);
+            tpar = fpar; tperp = fperp; mz = (double)fm * d_thrust;
+            thr_d = thr_f; md_d = md_f; (void)tg_d;
+        } else {
+            double grad = u[0] * max_gimbal_rad;
+            gdeg_cmd = degrees(grad);
+            double gd = E->gimbal_prev + dt_act * ((-E->gimbal_prev + gdeg_cmd) / 1.0);
+            if (gd < -max_gimbal_deg) gd = -max_gimbal_deg;
+            if (gd > max_gimbal_deg) gd = max_gimbal_deg;
+            double grad2 = radians(gd);
+            double nnt = (u[1] + 1) / 2;
+            thr_d = nnt * (1 - nominal) + nominal;
+            tg_d = T_full * n_eng * thr_d;
+            tpar = tg_d * cos(grad2);
+            tperp = -tg_d * sin(grad2);
+            mz = -tg_d * sin(grad2) * d_thrust;
+            double tot = sqrt(tpar * tpar + tperp * tperp);
+            md_d = (P->T_e / P->v_ex) * (tot / T_full);
+            gimbal_deg_out = degrees(grad2);
+            cmd_l = u[2] * max_defl * 60; cmd_r = u[3] * max_defl * 60;
+        }
+        ac = acs(P, ae, q, mach, x_cog, cmd_l, cmd_r, E->dl_prev, E->dr_prev, dt_act);
+        cfp = tpar + ac.f_par; cfperp = tperp + ac.f_perp; cm = mz + ac.m_z;
+        if (f32) mdot_dt = (double)(md_f * (float)dt); else mdot_dt = md_d * dt;
+        mdot_info = md_d; throttle_info = thr_d;
+    }
+    /* NaN guard (rockets_physics.py:599-607): an elif chain */
+    if (isnan(cfp)) cfp = 0.0;
+    else if (isnan(cfperp)) cfperp = 0.0;
+    else if (isnan(cm)) cm = 0.0;
+    double cfx = cfp * cos(th) + cfperp * sin(th);
+    double cfy = cfp * sin(th) - cfperp * cos(th);
+    double g = orc_gravity(P, y);
+    double fx = aero_x + cfx + Fwx, fy = aero_y + cfy + Fwy;
+    double vxd = fx / m, vyd = fy / m - g;
+    vx += vxd * dt; vy += vyd * dt; x += vx * dt; y += vy * dt;
+    double mz_tot = cm + aero_m + Mw;
+    double thdd = mz_tot / inertia;
+    thd += thdd * dt; th += thd * dt;
+    ga = atan2(vy, vx);
+    if (th > 2 * PI) th -= 2 * PI;
+    if (ga < 0) ga = 2 * PI + ga;
+    al = th - ga;
+    mp -= mdot_dt; m -= mdot_dt; t += dt;
+    s[0] = x; s[1] = y; s[2] = vx; s[3] = vy; s[4] = th; s[5] = thd; s[6] = ga; s[7] = al;
+    s[8] = m; s[9] = mp; s[10] = t;
+    if (info) {
+        info[ORC_I_RHO] = rho; info[ORC_I_P] = patm; info[ORC_I_A] = a; info[ORC_I_MACH] = mach;
+        info[ORC_I_Q] = q; info[ORC_I_CL] = CL; info[ORC_I_CD] = CD; info[ORC_I_MDOT] = mdot_info;
+        info[ORC_I_XCOG] = x_cog; info[ORC_I_INERTIA] = inertia; info[ORC_I_DTHRUST] = d_thrust;
+        info[ORC_I_ALPHA_EFF] = ae; info[ORC_I_THROTTLE] = throttle_info; info[ORC_I_CFPAR] = cfp;
+        info[ORC_I_CFPERP] = cfperp; info[ORC_I_CM] = cm; info[ORC_I_AERO_X] = aero_x; info[ORC_I_AERO_Y] = aero_y;
+        info[ORC_I_UG] = ug; info[ORC_I_VG] = vg; info[ORC_I_CA] = ac.ca; info[ORC_I_CNL] = ac.cn_l;
+        info[ORC_I_GIMBAL_DEG] = gimbal_deg_out; info[ORC_I_DCMD_L] = ac.dcmd_l; info[ORC_I_DCMD_R] = ac.dcmd_r;
+        info[ORC_I_DRAG] = drag; info[ORC_I_LIFT] = lift;
+    }
+}
+
+int orc_physics(const orc_params* P, orc_env* E, int phase, const double* u, int f32,
+                const double* noise, double* info) {
+    /* compile_physics: pure throttle dt_temp = 0.025 x4 (rockets_physics.py:909-957);
+     * landing_burn physics dt = 0.1 x4 with actuator dt 0.025 (:803-861) */
+    double dt = phase == ORC_PHASE_PURE_THROTTLE ? 0.025 : 0.1;
+    E->noise_used = 0;
+    for (int k = 0; k < 4; ++k)
+        substep(P, E, phase, u, f32, dt, 0.025, noise ? (E->noise_slotted ? noise + 2 * k : noise) : NULL, info);
+    if (phase == ORC_PHASE_LANDING_BURN && info) {
+        /* base_environment.py:122-124: prevs <- filtered gimbal, fin COMMANDS */
+        E->gimbal_prev = info[ORC_I_GIMBAL_DEG];
+        E->dl_prev = info[ORC_I_DCMD_L];
+        E->dr_prev = info[ORC_I_DCMD_R];
+    }
+    return 0;
+}
+
+void orc_reset(const orc_params* P, orc_env* E, const double* s0, int wind_on, int wind_stoch,
+               double sigma_u, double sigma_v) {
+    memset(E, 0, sizeof(*E));
+    memcpy(E->s, s0 ? s0 : P->state0, sizeof(E->s));
+    memcpy(E->prev_s, E->s, sizeof(E->s));
+    E->wind_on = wind_on; E->wind_stoch = wind_stoch; E->sigma_u = sigma_u; E->sigma_v = sigma_v;
+}
+
+/* ---------------------------------------------------------------- rtd */
+static void rtd_rl_pure_throttle(const orc_params* P, const orc_env* E, double gl, orc_out* o) {
+    /* rtd_rl.py:190-336 */
+    const double* s = E->s;
+    double x = s[0], y = s[1], vx = s[2], vy = s[3], th = s[4], mp = s[9];
+    (void)x;
+    double rho, pa, a;
+    orc_atmosphere(P, y, &rho, &pa, &a);
+    double speed = sqrt(vx * vx + vy * vy);
+    double q = 0.5 * rho * (speed * speed);
+    int tr = 0, id = 0;
+    if (y < -10) { tr = 1; id = 1; }
+    else if (mp <= 0) { tr = 1; id = 2; }
+    else if (th > PI + radians(2)) { tr = 1; id = 3; }
+    else if (q > 65000) { tr = 1; id = 4; }
+    else if (gl > 6.0) { tr = 1; id = 5; }
+    else if (vy > 0.0) { tr = 1; id = 6; }
+    else if (vx > 0.01) { tr = 1; id = 7; }
+    int done = (y > 0 && y < 1 && speed < 5.0);
+    double y0 = P->state0[1], m0 = P->state0[8];
+    double sp = hypot(vx, vy);
+    double r = 0.0;
+    if (q > 60000.0) { double e = (q - 60000.0) / (65000.0 - 60000.0); r -= 1.0 * fmin(e * e, 1.0); }
+    if (gl > 5.5) { double e = (gl - 5.5) / (6.0 - 5.5); r -= 1.0 * fmin(e * e, 1.0); }
+    double prog = (y0 - y) / y0;
+    double wp = (q <= 60000.0 && gl <= 5.5) ? 0.5 : 0.5 * 0.1;
+    r += wp * prog;
+    if (y < 100.0) r += 5.5 * (1.0 - fabs(vy) / 50.0);
+    if (done && !tr) r += 400.0 * mp / m0;
+    else if (tr && y > 0) r -= 50.0 * (fabs(y) / y0);
+    else if (tr && y < 0) r -= 50.0 * (fabs(vy) / 10);
+    if (!done || !(tr && y < 0)) { if (r < -10.0) r = -10.0; if (r > 10.0) r = 10.0; }
+    (void)sp;
+    o->reward = r; o->done = done; o->trunc = tr; o->trunc_id = id;
+}
+
+static void rtd_pso(const orc_params* P, const orc_env* E, int phase, double gl, orc_out* o) {
+    const double* s = E->s;
+    double x = s[0], y = s[1], vx = s[2], vy = s[3], th = s[4], ga = s[6], mp = s[9];
+    double rho, pa, a;
+    orc_atmosphere(P, y, &rho, &pa, &a);
+    double speed = sqrt(vx * vx + vy * vy);
+    double q = 0.5 * rho * (speed * speed);
+    int tr = 0, id = 0, done = 0;
+    double r = 0.0;
+    if (phase == ORC_PHASE_PURE_THROTTLE) {   /* rtd_pso.py:172-230 */
+        if (y < 0.0) { tr = 1; id = 1; }
+        else if (mp <= 0) { tr = 1; id = 2; }
+        else if (th > PI + radians(2)) { tr = 1; id = 3; }
+        else if (q > 65000) { tr = 1; id = 4; }
+        else if (vy > 0.0) { tr = 1; id = 6; }
+        else if (gl > 6.0) { tr = 1; id = 7; }
+        done = (y > 0 && y < 1 && speed < 5.5);
+        if (tr && y > 0) r = -fabs(y);
+        else if (tr && y < 0) r = 200 - fabs(speed);
+        else if (done) r = mp;
+    } else {                                   /* rtd_pso.py:234-317 */
+        double dist = sqrt(x * x + y * y);
+        double over;
+        if (x < 0 && y < 0) over = sqrt(x * x + y * y);
+        else if (x < 0) over = -x;
+        else if (y < 0) over = -y;
+        else over = 0;
+        double aeff = (vy < 0) ? fabs(ga - th - PI) : fabs(th - ga);
+        if (over > 0.5) { tr = 1; id = 1; }
+        else if (mp <= 0) { tr = 1; id = 2; }
+        else if (aeff > radians(10)) { tr = 1; id = 3; }
+        else if (q > 65000) { tr = 1; id = 4; }
+        else if (vy > 0.0) { tr = 1; id = 6; }
+        else if (gl > 6.0) { tr = 1; id = 7; }
+        else if (y > 1000 && vx > 0.0) { tr = 1; id = 8; }
+        done = (dist > 0 && dist < 1 && speed < 2.5);
+        if (tr && over < 0.5) r = -fabs(dist);
+        else if (tr) r = 200 - fabs(speed);
+        else if (done) r = mp;
+    }
+    o->reward = r; o->done = done; o->trunc = tr; o->trunc_id = id;
+}
+
+/* ---------------------------------------------------------------- env step
+ * rocket_environment_pre_wrap.step (base_environment.py:99-154) */
+int orc_step(const orc_params* P, orc_env* E, int phase, int rtd, const double* u, int f32,
+             const double* noise, orc_out* o) {
+    memset(o, 0, sizeof(*o));
+    orc_physics(P, E, phase, u, f32, noise, o->info);
+    const double *s = E->s, *ps = E->prev_s;
+    double v = sqrt(s[2] * s[2] + s[3] * s[3]);
+    double vp = sqrt(ps[2] * ps[2] + ps[3] * ps[3]);
+    double gload = fabs(v - vp) / 0.1 * 1 / 9.81;
+    if (E->gwin_len < 10) E->gwin[E->gwin_len++] = gload;
+    else { memmove(E->gwin, E->gwin + 1, 9 * sizeof(double)); E->gwin[9] = gload; }
+    double sum = 0.0;
+    for (int i = 0; i < E->gwin_len; ++i) sum += E->gwin[i];
+    double gl = sum / 10;
+    o->info[ORC_I_GLOAD] = gl;
+    if (rtd == ORC_RTD_RL) rtd_rl_pure_throttle(P, E, gl, o);
+    else rtd_pso(P, E, phase, gl, o);
+    E->trunc_id = o->trunc_id;
+    memcpy(E->prev_s, E->s, sizeof(E->s));
+    /* observations: RL pure throttle (env_wrapped_rl_pytorch.py:195-198), PSO (env_wrapped_ea.py:108-122) */
+    if (rtd == ORC_RTD_RL) {
+        o->obs[0] = (1 - s[1] / P->norm_y) * 2 - 1;
+        o->obs[1] = (1 - s[3] / P->norm_vy) * 2 - 1;
+    } else if (phase == ORC_PHASE_PURE_THROTTLE) {
+        o->obs[0] = s[1] / P->norm_y; o->obs[1] = s[3] / P->norm_vy;
+    } else {
+        double k = atanh(0.75) / radians(25);
+        o->obs[0] = s[0] / P->norm_x; o->obs[1] = s[1] / P->norm_y;
+        o->obs[2] = s[2] / P->norm_vx; o->obs[3] = s[3] / P->norm_vy;
+        o->obs[4] = tanh(k * (s[4] - PI / 2));
+    }
+    return 0;
+}
+
+/* CPU baseline driver: n_env independent envs, static loop (the reference runs one env per
+ * process; this is its scalar port).  Returns wall seconds is measured by the caller. */
+double orc_rollout(const orc_params* P, int phase, int rtd, int n_env, int n_steps,
+                   const float* actions, int auto_reset, int64_t* env_steps_out) {
+    int A = phase == ORC_PHASE_PURE_THROTTLE ? 1 : 4;
+    orc_env* envs = (orc_env*)malloc(sizeof(orc_env) * (size_t)n_env);
+    for (int i = 0; i < n_env; ++i) orc_reset(P, &envs[i], NULL, 0, 0, 0, 0);
+    double acc = 0.0; int64_t steps = 0;
+    orc_out o;
+    for (int t = 0; t < n_steps; ++t) {
+        for (int i = 0; i < n_env; ++i) {
+            double u[4];
+            for (int k = 0; k < A; ++k) u[k] = actions[((size_t)t * n_env + i) * A + k];
+            orc_step(P, &envs[i], phase, rtd, u, 1, NULL, &o);
+            acc += o.reward; ++steps;
+            if (auto_reset && (o.done || o.trunc)) orc_reset(P, &envs[i], NULL, 0, 0, 0, 0);
+        }
+    }
+    free(envs);
+    if (env_steps_out) *env_steps_out = steps;
+    return acc;
+}

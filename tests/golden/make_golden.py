@@ -1,0 +1,287 @@
+#!/usr/bin/env python3
+"""Generate the golden fixtures under tests/golden/ (build container only).
+
+Two kinds of fixtures, both plain data (npz):
+
+1. recorded_*.npz -- columns lifted from the reference's OWN recorded runs
+   (data/reference_trajectory, data/agent_saves/PyTorchSAC, data/pso_saves):
+   the de-facto golden data of the reference.
+2. ref_*.npz -- produced by importing the reference (/root/reference, read-only)
+   and running its own functions on seeded inputs.  The reference needs two
+   absent third-party packages; tests/golden/shims provides `ambiance` (ISA
+   restated, pinned by the recorded atmosphere columns) and a `gymnasium`
+   annotation stub.  `dill.load` is replaced BEFORE the reference is imported:
+   the reference's rocket_functions.pkl is never unpickled.  Instead the closures
+   are rebuilt from the reference's own stage_inertia / d_cg_thrusters / cop_func
+   with the constants tools/make_param_pack.py read statically from the pickle.
+
+Nothing here ships to the GPU box: only the .npz outputs are committed.
+Run:  python tests/golden/make_golden.py
+"""
+import contextlib
+import io
+import json
+import os
+import random
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.abspath(os.path.join(HERE, "..", ".."))
+REF = os.environ.get("PDENV_REFERENCE", "/root/reference")
+PACK = os.path.join(REPO, "psso-sac-for-powered-descent_amd", "data", "param_pack.json")
+STATE_COLS = ["x", "y", "vx", "vy", "theta", "theta_dot", "gamma", "alpha", "mass", "mass_propellant", "time"]
+
+
+def save(name, **arrays):
+    path = os.path.join(HERE, name)
+    np.savez_compressed(path, **arrays)
+    print(f"  {name}: " + ", ".join(f"{k}{tuple(np.shape(v))}" for k, v in arrays.items()), file=sys.stderr)
+
+
+# --------------------------------------------------------------------------- recorded data
+def recorded():
+    import pandas as pd
+    d = pd.read_csv(os.path.join(REF, "data/reference_trajectory/landing_burn_controls_pure_throttle/"
+                                      "state_action_landing_burn_pure_throttle_control.csv"))
+    cols = ["x[m]", "y[m]", "vx[m/s]", "vy[m/s]", "theta[rad]", "theta_dot[rad/s]", "gamma[rad]",
+            "alpha[rad]", "mass[kg]", "masspropellant[kg]", "time[s]"]
+    save("recorded_reference_trajectory.npz", state=d[cols].values, u0=d["u0"].values)
+
+    root = os.path.join(REF, "data/agent_saves/PyTorchSAC/LandingBurnPureThrottle")
+    runs = sorted(r for r in os.listdir(root) if os.path.exists(os.path.join(root, r, "trajectories/trajectory.csv")))
+    keep = ["air_density", "atmospheric_pressure", "speed_of_sound", "CD", "CL", "mach_number",
+            "mass_flow", "dynamic_pressure", "x_cog", "inertia", "d_thrust_cg", "alpha_effective",
+            "g_load_1_sec_window", "control_force_parallel", "throttle"]
+    out = {}
+    for k, r in enumerate(runs[:4]):
+        t = pd.read_csv(os.path.join(root, r, "trajectories/trajectory.csv"))
+        out[f"run{k}_state"] = t[STATE_COLS].values
+        out[f"run{k}_action"] = t["action"].values.astype(np.float64)
+        out[f"run{k}_info"] = t[keep].values
+    out["info_names"] = np.array(keep)
+    out["runs"] = np.array(runs[:4])
+    save("recorded_sac_trajectories.npz", **out)
+
+    p = os.path.join(REF, "data/pso_saves/landing_burn_pure_throttle/Landed/trajectory_data")
+    tr = pd.read_csv(os.path.join(p, "trajectory.csv"))
+    ac = pd.read_csv(os.path.join(p, "actions.csv"))
+    rw = pd.read_csv(os.path.join(p, "rewards.csv"))
+    info = pd.read_csv(os.path.join(p, "info_data.csv"))
+    cols2 = ["x[m]", "y[m]", "vx[m/s]", "vy[m/s]", "theta[rad]", "theta_dot[rad/s]", "gamma[rad]",
+             "alpha[rad]", "mass[kg]", "mass_propellant[kg]", "time[s]"]
+    save("recorded_pso_landed.npz", state=tr[cols2].values, action=ac.values[:, 0].astype(np.float64),
+         reward=rw.values[:, 0], mass_flow=info["mass_flow"].values, air_density=info["air_density"].values,
+         CD=info["CD"].values, CL=info["CL"].values)
+
+
+# --------------------------------------------------------------------------- reference import
+def import_reference():
+    sys.path[:0] = [os.path.join(HERE, "shims"), REF]
+    os.chdir(REF)
+    pack = json.load(open(PACK))
+    import dill
+
+    def _no_unpickle(_f, *a, **k):
+        from src.RocketSizing.functions.rocket_dimensions import stage_inertia, d_cg_thrusters
+        from src.RocketSizing.functions.cop_estimation import cop_func
+        c = pack["inertia"]
+        inert = stage_inertia(h_ox=c["h_ox"], h_f=c["h_f"], m_ox=c["m_ox"], m_f=c["m_f"],
+                              h_lower=c["h_lower"], m_dry=c["m_dry"], x_dry=c["x_dry"], I_dry=c["I_dry"])
+        L = pack["sizing"]["stage_1_height"]
+        return {"x_cog_inertia_subrocket_2_lambda": inert,
+                "d_cg_thrusters_subrocket_2_lambda": lambda x: d_cg_thrusters(x, c["engine_height"]),
+                "cop_subrocket_2_lambda": lambda alpha, M: cop_func(L, alpha, M, d_0=0.75),
+                "cop_subrocket_0_lambda": None, "cop_subrocket_1_lambda": None}
+
+    dill.load = _no_unpickle
+    with contextlib.redirect_stdout(io.StringIO()):
+        import src.envs.rockets_physics as rp
+        from src.envs.utils import acs_model, atmosphere_dynamics
+        from src.envs.rl.env_wrapped_rl_pytorch import rl_wrapped_env_pytorch
+        from src.envs.pso.env_wrapped_ea import pso_wrapper
+    return rp, acs_model, atmosphere_dynamics, rl_wrapped_env_pytorch, pso_wrapper
+
+
+def kats(rp, acs_model, atm):
+    rng = np.random.default_rng(1234)
+    # rocket_CD(M, aoa_deg): clamps at +-radians(10) in "degree" units
+    M = np.concatenate([np.linspace(0.0, 10.0, 101), rng.uniform(0, 4, 400)])
+    Acd = np.concatenate([np.linspace(-0.2, 0.2, 41), rng.uniform(-0.2, 0.2, 60)])
+    cd_q = np.array([(m, a) for m in M[::5] for a in Acd[::4]] + [(m, a) for m, a in zip(rng.uniform(0, 4, 300), rng.uniform(-0.2, 0.2, 300))])
+    cd_v = np.array([rp.rocket_CD(m, a) for m, a in cd_q])
+    # rocket_CL(M, x): x is converted to degrees once more inside
+    Xcl = np.concatenate([np.linspace(-0.25, 0.25, 51), rng.uniform(-0.2, 0.2, 80), np.radians([1e-7, 2.0, 10.0, 11.0])])
+    cl_q = np.array([(m, x) for m in M[::5] for x in Xcl[::3]] + [(m, x) for m, x in zip(rng.uniform(0, 4, 300), rng.uniform(-0.2, 0.2, 300))])
+    cl_v = np.array([rp.rocket_CL(m, x) for m, x in cl_q])
+    ca_q = np.concatenate([np.linspace(0, 5, 201), rng.uniform(0, 4, 100)])
+    ca_v = np.array([float(acs_model.Ca_func(m)) for m in ca_q])
+    cn_q = np.stack([np.concatenate([np.linspace(0, 5, 101), rng.uniform(0, 4, 100)]),
+                     rng.uniform(-0.3, 0.3, 201)], 1)
+    cn_v = np.array([float(acs_model.Cn_func(m, a)) for m, a in cn_q])
+    alt = np.concatenate([np.linspace(-100, 90000, 3000), [0, 11000, 20000, 32000, 47000, 51000, 71000, 80000, 81019.9, 81020]])
+    isa = np.array([atm.endo_atmospheric_model(h) for h in alt])
+    grav = np.array([atm.gravity_model_endo(h) for h in alt])
+    save("ref_kat.npz", cd_q=cd_q, cd_v=cd_v, cl_q=cl_q, cl_v=cl_v, ca_q=ca_q, ca_v=ca_v,
+         cn_q=cn_q, cn_v=cn_v, alt=alt, isa=isa, grav=grav)
+
+
+def sample_states(rng, n):
+    sac = np.load(os.path.join(HERE, "recorded_sac_trajectories.npz"))
+    ref = np.load(os.path.join(HERE, "recorded_reference_trajectory.npz"))["state"]
+    pool = np.concatenate([sac[f"run{k}_state"] for k in range(4)] + [ref])
+    pool = pool[pool[:, 1] > 5.0]
+    return pool[rng.choice(len(pool), n, replace=False)]
+
+
+def teacher_forced(rp):
+    rng = np.random.default_rng(99)
+    step_pt = rp.compile_physics(0.1, "landing_burn_pure_throttle")
+    step_lb = rp.compile_physics(0.1, "landing_burn")
+    S = sample_states(rng, 600)
+    out = {}
+    for tag, fn, A in (("pt", step_pt, 1), ("lb", step_lb, 4)):
+        acts = rng.uniform(-1, 1, (len(S), A)).astype(np.float32)
+        prevs = np.stack([rng.uniform(-5, 5, len(S)), rng.uniform(-0.3, 0.3, len(S)), rng.uniform(-0.3, 0.3, len(S))], 1)
+        res, info_keep = [], []
+        for i in range(len(S)):
+            st = [np.float64(v) for v in S[i]]
+            with contextlib.redirect_stdout(io.StringIO()):
+                if A == 1:
+                    s2, info = fn(st, acts[i], wind_generator=None)
+                else:
+                    s2, info = fn(st, acts[i], prevs[i, 0], prevs[i, 1], prevs[i, 2], wind_generator=None)
+            res.append([float(v) for v in s2])
+            ai = info["action_info"]
+            info_keep.append([info["air_density"], info["mach_number"], info["CL"], info["CD"],
+                              float(info["mass_flow"]), info["dynamic_pressure"], info["x_cog"], info["inertia"],
+                              float(ai.get("gimbal_angle_deg", 0.0)), float(ai.get("delta_command_left_rad", 0.0)),
+                              float(ai.get("delta_command_right_rad", 0.0))])
+        out[f"{tag}_state_in"] = S
+        out[f"{tag}_action"] = acts
+        out[f"{tag}_prevs"] = prevs
+        out[f"{tag}_state_out"] = np.array(res)
+        out[f"{tag}_info"] = np.array(info_keep)
+    out["info_names"] = np.array(["air_density", "mach_number", "CL", "CD", "mass_flow", "dynamic_pressure",
+                                  "x_cog", "inertia", "gimbal_angle_deg", "delta_command_left_rad",
+                                  "delta_command_right_rad"])
+    save("ref_teacher_forced.npz", **out)
+
+
+def run_episode(env, actions, max_steps, obs_of_step):
+    rec = {k: [] for k in ("state", "reward", "done", "trunc", "trunc_id", "obs")}
+    with contextlib.redirect_stdout(io.StringIO()):
+        env.reset()
+        for k in range(max_steps):
+            obs, r, d, tr, info = obs_of_step(env, actions[k])
+            rec["state"].append([float(v) for v in info["state"]])
+            rec["reward"].append(float(r)); rec["done"].append(bool(d)); rec["trunc"].append(bool(tr))
+            rec["trunc_id"].append(int(env.truncation_id() if callable(getattr(env, "truncation_id", None)) else env.env.truncation_id))
+            rec["obs"].append(np.asarray(obs, dtype=np.float64).ravel().tolist())
+            if d or tr:
+                break
+    return {k: np.array(v) for k, v in rec.items()}
+
+
+def episodes(rl_env_cls, pso_wrapper_cls):
+    ref_u0 = np.load(os.path.join(HERE, "recorded_reference_trajectory.npz"))["u0"]
+    out = {}
+    # (a) SAC wrapper, pure throttle, the SAC driver's configuration (sac_pytorch_powered_descent.py:22-28)
+    with contextlib.redirect_stdout(io.StringIO()):
+        env = rl_env_cls(flight_phase="landing_burn_pure_throttle", enable_wind=False, stochastic_wind=False,
+                         trajectory_length=1, discount_factor=0.99)
+    sac_step = lambda e, a: e.step(a)
+    seqs = {
+        "rl_land": ref_u0.astype(np.float32)[:, None],              # the classical controller's throttle, as f32
+        "rl_rand0": np.random.default_rng(7).uniform(-1, 1, (2200, 1)).astype(np.float32),
+        "rl_rand1": np.random.default_rng(8).uniform(0.2, 1, (2200, 1)).astype(np.float32),
+        "rl_hi": np.full((2200, 1), 0.95, np.float32),
+    }
+    for name, acts in seqs.items():
+        ep = run_episode(env, acts, min(2200, len(acts)), sac_step)
+        for k, v in ep.items():
+            out[f"{name}_{k}"] = v
+        out[f"{name}_actions"] = acts[:len(ep["reward"])]
+    # (b) PSO wrapper, pure throttle and landing_burn (env_wrapped_ea.py:77-134)
+    import torch
+    pso_step = lambda e, a: e.step(torch.tensor(a))
+    with contextlib.redirect_stdout(io.StringIO()):
+        pt = pso_wrapper_cls(flight_phase="landing_burn_pure_throttle", enable_wind=False, stochastic_wind=False,
+                             horiontal_wind_percentile=50)
+        lb = pso_wrapper_cls(flight_phase="landing_burn", enable_wind=False, stochastic_wind=False,
+                             horiontal_wind_percentile=50)
+    seqs = {
+        ("pso_pt_land", pt): ref_u0.astype(np.float32)[:, None],
+        ("pso_pt_rand", pt): np.random.default_rng(11).uniform(-1, 1, (2200, 1)).astype(np.float32),
+        ("pso_lb_rand0", lb): np.random.default_rng(12).uniform(-1, 1, (2200, 4)).astype(np.float32),
+        ("pso_lb_rand1", lb): np.concatenate([np.random.default_rng(13).uniform(-0.2, 0.2, (2200, 1)),
+                                              np.random.default_rng(14).uniform(0.3, 1.0, (2200, 1)),
+                                              np.random.default_rng(15).uniform(-0.3, 0.3, (2200, 2))], 1).astype(np.float32),
+    }
+    for (name, env), acts in seqs.items():
+        ep = run_episode(env, acts, 2200, pso_step)
+        for k, v in ep.items():
+            out[f"{name}_{k}"] = v
+        out[f"{name}_actions"] = acts[:len(ep["reward"])]
+    save("ref_episodes.npz", **out)
+
+
+def wind_episodes(rl_env_cls):
+    """Stochastic wind with an INJECTED noise stream: vonkarman.py draws np.random.randn()
+    per filter step and random.uniform per reset; both are replaced by recorded streams."""
+    out = {}
+    ref_u0 = np.load(os.path.join(HERE, "recorded_reference_trajectory.npz"))["u0"]
+    for ep_i, seed in enumerate((21, 22)):
+        rng = np.random.default_rng(seed)
+        normals = rng.standard_normal(2200 * 8)
+        uniforms = [0.5 + (2.25 - 0.5) * rng.random(), 1.25 + (2.0 - 1.25) * rng.random()]
+        state = {"n": 0, "u": 0}
+        orig_randn, orig_uniform = np.random.randn, random.uniform
+
+        def fake_randn(*a):
+            v = normals[state["n"]]; state["n"] += 1
+            return v
+
+        def fake_uniform(a, b):
+            if state["u"] < 2:
+                v = uniforms[state["u"]]
+            else:
+                v = a + (b - a) * 0.5
+            state["u"] += 1
+            return v
+
+        np.random.randn, random.uniform = fake_randn, fake_uniform
+        try:
+            with contextlib.redirect_stdout(io.StringIO()):
+                env = rl_env_cls(flight_phase="landing_burn_pure_throttle", enable_wind=True, stochastic_wind=True,
+                                 horiontal_wind_percentile=50, trajectory_length=1, discount_factor=0.99)
+                state["n"] = 0; state["u"] = 0
+                # reset() draws the per-episode sigmas (VKDisturbanceGenerator._new_filters)
+                acts = ref_u0.astype(np.float32)[:, None] if ep_i == 0 else np.full((2200, 1), 0.9, np.float32)
+                ep = run_episode(env, acts, min(2200, len(acts)), lambda e, a: e.step(a))
+                su = env.env.wind_generator.von_karman_generator_class.sigma_u
+                sv = env.env.wind_generator.von_karman_generator_class.sigma_v
+        finally:
+            np.random.randn, random.uniform = orig_randn, orig_uniform
+        for k, v in ep.items():
+            out[f"w{ep_i}_{k}"] = v
+        out[f"w{ep_i}_actions"] = acts[:len(ep["reward"])]
+        out[f"w{ep_i}_normals"] = normals[:state["n"]]
+        out[f"w{ep_i}_sigma"] = np.array([su, sv])
+    save("ref_wind_episodes.npz", **out)
+
+
+def main():
+    print("recorded fixtures", file=sys.stderr)
+    recorded()
+    print("importing the reference (shims: ambiance, gymnasium; dill.load replaced)", file=sys.stderr)
+    rp, acs_model, atm, rl_env_cls, pso_wrapper_cls = import_reference()
+    print("KATs", file=sys.stderr); kats(rp, acs_model, atm)
+    print("teacher-forced steps", file=sys.stderr); teacher_forced(rp)
+    print("episodes", file=sys.stderr); episodes(rl_env_cls, pso_wrapper_cls)
+    print("wind episodes", file=sys.stderr); wind_episodes(rl_env_cls)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,172 @@
+"""Pin the CPU oracle (oracle/pd_oracle.c) against the reference's own recorded runs and
+against fixtures produced by importing the reference (tests/golden/make_golden.py)."""
+import numpy as np
+import pytest
+
+from conftest import golden
+
+ST = ["x", "y", "vx", "vy", "theta", "theta_dot", "gamma", "alpha", "mass", "mass_propellant", "time"]
+# full-episode fp64 tolerance, fraction of per-channel range: the attitude channels
+# (x, vx, theta, theta_dot, gamma, alpha) are chaotic and amplify ulp-level
+# differences (LAPACK vs our LU in the RBF); y, vy, masses, time are not.
+TOL_EPISODE = np.array([1e-6, 1e-9, 1e-6, 1e-9, 1e-6, 1e-6, 1e-6, 1e-6, 1e-12, 1e-12, 1e-12])
+
+
+def rel(a, b, floor=1e-300):
+    return np.abs(a - b) / np.maximum(np.abs(b), floor)
+
+
+def test_isa_matches_recorded_atmosphere(oracle_mod):
+    """recorded air_density/pressure/speed_of_sound columns (SAC runs) pin ambiance."""
+    d = golden("recorded_sac_trajectories.npz")
+    names = list(d["info_names"])
+    for k in range(4):
+        st, info = d[f"run{k}_state"], d[f"run{k}_info"]
+        # info is from the LAST sub-step: pre-sub-step altitude = y - vy*0.025
+        y_pre = st[:, 1] - st[:, 3] * 0.025
+        got = np.array([oracle_mod.atmosphere(y) for y in y_pre])
+        for j, n in enumerate(("air_density", "atmospheric_pressure", "speed_of_sound")):
+            ref = info[:, names.index(n)]
+            assert rel(got[:, j], ref).max() < 1e-9, n
+
+
+def test_isa_kat(oracle_mod):
+    d = golden("ref_kat.npz")
+    got = np.array([oracle_mod.atmosphere(h) for h in d["alt"]])
+    assert np.abs(got - d["isa"]).max() <= 1e-12 * np.abs(d["isa"]).max()
+    # the reference's own KAT (atmosphere_dynamics.py:35-56), 5 % / 1 %
+    for alt, rho, p, a in [(0.0, 1.225, 101325.0, 340.3), (11000.0, 0.36391, 22632.0, 295.1),
+                           (20000.0, 0.08803, 5474.9, 295.1), (32000.0, 0.01322, 868.02, 301.6),
+                           (47000.0, 0.00143, 110.91, 329.8)]:
+        r, pp, aa = oracle_mod.atmosphere(alt)
+        assert abs(r - rho) / rho < 5e-2 and abs(pp - p) / p < 5e-2 and abs(aa - a) / a < 1e-2
+
+
+def test_rbf_cd_cl_kat(oracle_mod):
+    """scipy RBFInterpolator(TPS, neighbors=50) via the reference's rocket_CD/rocket_CL."""
+    d = golden("ref_kat.npz")
+    cd = np.array([oracle_mod.rbf(0, m, a) if abs(a) <= np.radians(10) else
+                   oracle_mod.rbf(0, m, np.sign(a) * np.radians(10)) for m, a in d["cd_q"]])
+    assert np.abs(cd - d["cd_v"]).max() < 1e-11
+    # rocket_CL(M, x) converts x to degrees inside; the oracle's CL() adds the physics-level
+    # degrees() too, so feed radians(x)
+    cl = np.array([oracle_mod.CL(m, np.radians(x)) for m, x in d["cl_q"]])
+    assert np.abs(cl - d["cl_v"]).max() < 1e-10
+
+
+def test_grid_fin_kat(oracle_mod):
+    import ctypes as C
+    d = golden("ref_kat.npz")
+    L, P = oracle_mod.lib(), oracle_mod.params()
+    ca = np.array([L.orc_Ca(C.byref(P), m) for m in d["ca_q"]])
+    cn = np.array([L.orc_Cn(C.byref(P), m, a) for m, a in d["cn_q"]])
+    assert np.abs(ca - d["ca_v"]).max() < 1e-15
+    assert np.abs(cn - d["cn_v"]).max() < 1e-13
+
+
+@pytest.mark.parametrize("tag,phase", [("pt", 0), ("lb", 1)])
+def test_teacher_forced_physics(oracle_mod, tag, phase):
+    d = golden("ref_teacher_forced.npz")
+    o = oracle_mod.Oracle(phase=phase)
+    names = list(d["info_names"])
+    worst = np.zeros(11)
+    for i in range(len(d[f"{tag}_state_in"])):
+        s, info = o.physics(d[f"{tag}_state_in"][i], d[f"{tag}_action"][i], f32=True,
+                            prevs=tuple(d[f"{tag}_prevs"][i]))
+        worst = np.maximum(worst, rel(s, d[f"{tag}_state_out"][i], 1e-3))
+        assert abs(info["mass_flow"] - d[f"{tag}_info"][i][names.index("mass_flow")]) == 0.0
+    # fp64 per step: <= 1e-12 relative on every channel but theta_dot (its moment is a
+    # difference of large aero/ACS terms; RBF ulps from LAPACK vs our LU show up at 1e-10)
+    tol = np.full(11, 1e-10); tol[5] = 1e-8
+    assert (worst < tol).all(), dict(zip(ST, worst))
+
+
+def test_recorded_pso_landed_teacher_forced(oracle_mod):
+    """PSO 'Landed' run (float32 actions): every step from the recorded previous state."""
+    d = golden("recorded_pso_landed.npz")
+    o = oracle_mod.Oracle(phase=0, rtd=1)
+    st, act = d["state"], d["action"]
+    # the run started from an older initial state (not recorded): start from row 0
+    prev = st[0]
+    worst = np.zeros(11)
+    for k in range(1, len(act)):
+        s, info = o.physics(prev, [act[k]], f32=True)
+        worst = np.maximum(worst, np.abs(s - st[k]) / (np.ptp(st, 0) + 1e-300))
+        assert info["mass_flow"] == pytest.approx(d["mass_flow"][k], rel=1e-7)
+        prev = st[k]
+    assert worst.max() < 1e-9, dict(zip(ST, worst))
+    assert d["reward"][-1] == pytest.approx(st[-1, 9], rel=1e-15)
+
+
+def test_reference_trajectory_open_loop(oracle_mod):
+    """Config 1: replay u0 (f64 [[u0]]) from the nominal initial state, all 1281 rows."""
+    d = golden("recorded_reference_trajectory.npz")
+    o = oracle_mod.Oracle(phase=0, rtd=1)
+    got = []
+    for u in d["u0"]:
+        s, r, done, tr, tid, obs, info = o.step([u], f32=False)
+        got.append(s)
+    got = np.array(got)
+    err = np.abs(got - d["state"]).max(0) / np.ptp(d["state"], 0)
+    tol = np.full(11, 1e-8); tol[5] = 1e-6       # theta_dot: chaotic
+    assert (err < tol).all(), dict(zip(ST, err))
+    assert done and not tr and r == pytest.approx(474318.950426, rel=1e-9)
+
+
+def _replay(o, acts, f32=True, noise=None):
+    rec = []
+    for k, a in enumerate(acts):
+        nz = None if noise is None else noise[k]
+        s, r, d, tr, tid, obs, info = o.step(a, f32=f32, noise=nz)
+        rec.append((s, r, d, tr, tid, obs))
+        if d or tr:
+            break
+    return rec
+
+
+@pytest.mark.parametrize("name,phase,rtd", [
+    ("rl_land", 0, 0), ("rl_rand0", 0, 0), ("rl_rand1", 0, 0), ("rl_hi", 0, 0),
+    ("pso_pt_land", 0, 1), ("pso_pt_rand", 0, 1), ("pso_lb_rand0", 1, 1), ("pso_lb_rand1", 1, 1)])
+def test_episodes_match_reference(oracle_mod, name, phase, rtd):
+    d = golden("ref_episodes.npz")
+    o = oracle_mod.Oracle(phase=phase, rtd=rtd)
+    rec = _replay(o, d[f"{name}_actions"])
+    assert len(rec) == len(d[f"{name}_reward"])
+    S = np.array([r[0] for r in rec]); R = np.array([r[1] for r in rec])
+    rs = d[f"{name}_state"]
+    err = np.abs(S - rs).max(0) / (np.ptp(rs, 0) + 1e-12)
+    tol = TOL_EPISODE if phase == 0 else np.maximum(TOL_EPISODE, 1e-6 * (TOL_EPISODE > 1e-12))
+    assert (err < tol).all(), dict(zip(ST, err))
+    assert np.abs(R - d[f"{name}_reward"]).max() <= 1e-9 * max(1.0, np.abs(d[f"{name}_reward"]).max())
+    assert [r[2] for r in rec] == list(d[f"{name}_done"])
+    assert [r[3] for r in rec] == list(d[f"{name}_trunc"])
+    assert [r[4] for r in rec][-1] == d[f"{name}_trunc_id"][-1]
+    obs = np.array([r[5][:d[f"{name}_obs"].shape[1]] for r in rec])
+    ref_obs = d[f"{name}_obs"]
+    if rtd == 0:   # the SAC wrapper casts observations to float32
+        obs = obs.astype(np.float32).astype(np.float64)
+    assert np.abs(obs - ref_obs).max() < 1e-6
+
+
+@pytest.mark.parametrize("ep", [0, 1])
+def test_wind_episode_injected_noise(oracle_mod, ep):
+    """Stochastic wind: the reference's np.random stream was injected and recorded; the
+    oracle consumes it in the same order (2 normals per sub-step below 15 km)."""
+    d = golden("ref_wind_episodes.npz")
+    su, sv = d[f"w{ep}_sigma"]
+    o = oracle_mod.Oracle(phase=0, rtd=0, wind=True, stochastic=True, sigma_u=su, sigma_v=sv)
+    normals = np.concatenate([d[f"w{ep}_normals"], np.zeros(8)])
+    rs = d[f"w{ep}_state"]
+    k = 0
+    S = []
+    for a in d[f"w{ep}_actions"]:
+        s, r, dn, tr, tid, obs, info = o.step(a, f32=True, noise=normals[k:k + 8])
+        k += o.noise_used
+        S.append(s)
+        if dn or tr:
+            break
+    S = np.array(S)
+    assert len(S) == len(rs)
+    assert k == len(d[f"w{ep}_normals"])
+    err = np.abs(S - rs).max(0) / (np.ptp(rs, 0) + 1e-12)
+    assert (err < TOL_EPISODE).all(), dict(zip(ST, err))
