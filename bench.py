@@ -1,0 +1,166 @@
+#!/usr/bin/env python3
+"""Benchmark: env-steps/s of the MI355X powered-descent env (BASELINE.json metric).
+
+Workload (BASELINE config c3, one GPU): 65 536 parallel envs per GPU, phase
+landing_burn_pure_throttle with the SAC driver's reward (rtd_rl), the horizontal wind
+profile + von Karman gusts (percentile drawn per reset, as WindModel(given_percentile=None)),
+initial pitch perturbation N(0, 1 deg), synthetic uniform float32 random actions resident in
+HBM, auto-reset on done/truncated.  One timed "step" = one env.step() of all envs (one
+k_step launch; 4 physics sub-steps + g-load window + truncated/done/reward + obs each).
+
+Multi-GPU: one process per GPU (torchrun), each rank steps its own contiguous env shard
+(env_offset = rank * N); the env batch shards with no data-path collective, so scaling is
+weak; the timed region is bracketed by barriers and the max over ranks is reported.
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "psso-sac-for-powered-descent_amd"))
+
+
+def algorithmic_bytes(precision, phase, wind, obs_dim, act_dim):
+    """HBM bytes one env-step must move (SoA state in/out + caches + I/O), DESIGN.md s3."""
+    r = 8 if precision == "f64" else 4
+    rd = 11 * r + r + 10 * r + 2 + 16 + 8 + 4 + 4 + 4 * act_dim
+    wr = 11 * r + r + r + 2 + 1 + 4 + 16 + 8 + obs_dim * r + r + 3
+    if phase == "landing_burn":
+        rd += 3 * r; wr += 3 * r
+    if wind:
+        rd += 6 * r + 1; wr += 4 * r
+    return rd + wr
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--envs", type=int, default=65536, help="envs per GPU")
+    ap.add_argument("--precision", choices=["f64", "f32"], default="f64")
+    ap.add_argument("--phase", default="landing_burn_pure_throttle")
+    ap.add_argument("--no-wind", action="store_true")
+    ap.add_argument("--cpu-baseline", type=int, default=1)
+    ap.add_argument("--secondary", type=int, default=1, help="also time the other precision")
+    args = ap.parse_args()
+
+    import torch
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+    import pdenv
+
+    def run(precision):
+        n = args.envs
+        mode = "rl" if args.phase == "landing_burn_pure_throttle" else "pso"
+        env = pdenv.PoweredDescentEnv(
+            n, flight_phase=args.phase, mode=mode, precision=precision, device=local,
+            enable_wind=not args.no_wind, stochastic_wind=not args.no_wind, wind_percentile=None,
+            auto_reset=True, tilt_sigma_rad=math.radians(1.0), seed=1234, env_offset=rank * n)
+        env.flush_every = 16
+        T = args.warmup + args.steps
+        g = torch.Generator(device=env.device).manual_seed(42 + rank)
+        acts = (torch.rand(T, n, env.action_dim, generator=g, device=env.device) * 2 - 1).contiguous()
+        for t in range(args.warmup):
+            env.step(acts[t])
+        torch.cuda.synchronize()
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for k in range(args.steps):
+            ev[k][0].record()
+            env.step(acts[args.warmup + k])
+            ev[k][1].record()
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        wall = time.perf_counter() - t0
+        kern_ms = sorted(a.elapsed_time(b) for a, b in ev)
+        w = torch.tensor([wall], device=env.device, dtype=torch.float64)
+        if dist:
+            dist.all_reduce(w, op=dist.ReduceOp.MAX)
+        wall = float(w.item())
+        c = env.counters()
+        res = dict(wall=wall, kern_avg_ms=sum(kern_ms) / len(kern_ms), kern_med_ms=kern_ms[len(kern_ms) // 2],
+                   n=n, obs_dim=env.obs_dim, act_dim=env.action_dim, counters=c)
+        env.close()
+        return res
+
+    main_res = run(args.precision)
+    other = None
+    if args.secondary:
+        other = run("f32" if args.precision == "f64" else "f64")
+    if rank != 0:
+        if dist:
+            dist.destroy_process_group()
+        return
+    n_total = main_res["n"] * world
+    value = n_total * args.steps / main_res["wall"]
+    wind = not args.no_wind
+    bpe = algorithmic_bytes(args.precision, args.phase, wind, main_res["obs_dim"], main_res["act_dim"])
+    achieved = bpe * main_res["n"] / (main_res["kern_avg_ms"] * 1e-3) / 1e9
+    traffic = None
+    pmc = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    if os.path.exists(pmc):
+        try:
+            traffic = json.load(open(pmc)).get(f"{args.precision}_bytes_per_launch")
+        except Exception:
+            traffic = None
+    out = {
+        "metric": "env-steps/sec at 65 536 parallel envs; achieved HBM GB/s vs peak",
+        "value": value,
+        "unit": "env-steps/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": main_res["wall"] / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": args.precision,
+        "data": "synthetic (uniform float32 random actions in HBM; reference initial state + N(0,1deg) pitch tilt)",
+        "config": {"workload": "c3: 65536 envs/GPU, landing_burn_pure_throttle, rtd_rl reward, wind (VK gusts + "
+                               "percentile profile) + tilt, auto-reset",
+                   "envs_per_gpu": main_res["n"], "global_envs": n_total, "parallelism": f"env-shard x{world}"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": 8000.0, "unit": "GB/s",
+                     "frac": achieved / 8000.0, "traffic": traffic,
+                     "bytes_per_env_step": bpe, "kernel": "k_step", "kernel_avg_ms": main_res["kern_avg_ms"],
+                     "note": "VALU/transcendental-bound elementwise ODE (no MFMA); see DESIGN.md"},
+        "rbf_table_misses": main_res["counters"]["rbf_misses"],
+    }
+    if other is not None:
+        op = "f32" if args.precision == "f64" else "f64"
+        out["secondary"] = {"dtype": op, "value": other["n"] * world * args.steps / other["wall"],
+                            "kernel_avg_ms": other["kern_avg_ms"]}
+    if args.cpu_baseline and world == 1:
+        sys.path.insert(0, os.path.join(REPO, "oracle"))
+        import numpy as np
+        import oracle
+        ne, ns = 32, 200
+        acts = np.random.default_rng(0).uniform(-1, 1, (ns, ne, 1)).astype(np.float32)
+        oracle.rollout(0, 0, 2, 2, acts[:2, :2], True, wind, math.radians(1.0))
+        t0 = time.perf_counter()
+        _, nsteps = oracle.rollout(0, 0, ne, ns, acts, True, wind, math.radians(1.0))
+        dt = time.perf_counter() - t0
+        out["cpu_baseline"] = {"value": nsteps / dt, "unit": "env-steps/s", "cores": 1, "kind": "port",
+                               "sample": f"oracle/pd_oracle.c scalar port, {ne} envs x {ns} steps of the same "
+                                         f"workload (wind+tilt+auto-reset), 1 host thread, {dt:.1f} s"}
+    print(json.dumps(out))
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,159 @@
+/* pdenv.h -- C ABI of the MI355X-native vectorised powered-descent environment (libpdenv.so).
+ *
+ * Drop-in boundary for the hot path of JvanZyl1/PSSO-SAC-for-powered-descent.  The reference
+ * has no FFI: its seam is the Python object API, which this ABI replaces one-for-one for a
+ * batch of N environments living in HBM:
+ *
+ *   pd_create   <- rocket_environment_pre_wrap.__init__ + compile_physics + compile_rtd_{rl,pso}
+ *                  (src/envs/base_environment.py:13-78, src/envs/rockets_physics.py:707-998,
+ *                   src/envs/rl/rtd_rl.py:537-604, src/envs/pso/rtd_pso.py:320-383)
+ *   pd_reset    <- rocket_environment_pre_wrap.reset (base_environment.py:80-97)
+ *   pd_step     <- rocket_environment_pre_wrap.step  (base_environment.py:99-154), i.e.
+ *                  physics_step x4 sub-steps (rockets_physics.py:455-704, :857-860, :953-956),
+ *                  g-load window, truncated_func -> done_func -> reward_func, plus the wrapper's
+ *                  observation (env_wrapped_rl_pytorch.py:167-202 / env_wrapped_ea.py:97-123)
+ *   pd_get_state/pd_set_state <- .state attribute (teacher forcing, checkpoint, perturbation)
+ *   pd_truncation_ids <- rl_wrapped_env_pytorch.truncation_id (env_wrapped_rl_pytorch.py:117-118)
+ *
+ * Conventions: plain C, no torch types.  All array arguments are DEVICE pointers (HBM) owned by
+ * the caller, laid out env-major [N] or [N][k]; `stream` is a hipStream_t (NULL = default).
+ * Calls are asynchronous and stream-ordered; a handle is not thread-safe (one per GPU/shard).
+ * Floating point buffers use the handle's precision: double for PD_F64, float for PD_F32.
+ * Errors are returned as pd_status codes; pd_last_error() gives a thread-local message.
+ */
+#ifndef PDENV_H
+#define PDENV_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PD_ABI_VERSION 1
+#define PD_MAX_PTS 256      /* aero scatter points per table */
+#define PD_MAX_COLS 5       /* AoA columns per aero table */
+#define PD_MAX_TAB 64       /* grid-fin table length */
+#define PD_MAX_WIND 16      /* nodes per wind profile */
+#define PD_N_WIND_PROFILES 50   /* integer percentiles 50..99 */
+#define PD_N_STATE 11       /* x y vx vy theta theta_dot gamma alpha mass mass_propellant time */
+#define PD_N_INFO 16        /* see pd_info_field */
+
+typedef enum { PD_OK = 0, PD_ERR_INVALID = 1, PD_ERR_HIP = 2, PD_ERR_NOMEM = 3, PD_ERR_UNSUPPORTED = 4 } pd_status;
+typedef enum { PD_PHASE_PURE_THROTTLE = 0, PD_PHASE_LANDING_BURN = 1 } pd_phase;   /* 1 resp. 4 actions */
+typedef enum { PD_RTD_RL = 0, PD_RTD_PSO = 1 } pd_rtd;                             /* rtd_rl.py / rtd_pso.py */
+typedef enum { PD_F64 = 0, PD_F32 = 1 } pd_precision;
+
+/* One neighbourhood-aero table: scatter points grouped by AoA column, Mach-sorted inside. */
+typedef struct {
+    int32_t n_cols, n_pts;
+    double col_aoa[PD_MAX_COLS];
+    int32_t col_start[PD_MAX_COLS], col_len[PD_MAX_COLS];
+    double mach[PD_MAX_PTS];
+    double coef[PD_MAX_PTS];
+} pd_aero_table;
+
+/* Physical parameter pack (host memory); filled from data/param_pack.json by the loader. */
+typedef struct {
+    /* sizing_results.csv (rockets_physics.py:714-719, size_gust_coefficients.py:3-22) */
+    double thrust_per_engine, nozzle_exit_pressure, nozzle_exit_area, v_exhaust;
+    int32_t n_engines_gimballed, pad0;
+    double grid_fin_area, d_base_grid_fin, rocket_radius, frontal_area, m_prop0, C_gust_x, C_gust_y;
+    /* stage-2 stage_inertia closure constants (rocket_dimensions.py:158-197) */
+    double h_ox, h_f, m_ox, m_f, h_lower, m_dry, x_dry, I_dry, engine_height, cop;
+    /* ISA layer table (ambiance) + gravity (atmosphere_dynamics.py:5-33) */
+    double isa_Hb[9], isa_Tb[9], isa_beta[9], isa_pb[9];
+    double isa_g0, isa_R, isa_kappa, isa_r, isa_alt_max, grav_R, grav_g0;
+    /* V2 aero (aerodynamic_coefficients.py:8-66) */
+    pd_aero_table cd, cl;
+    /* grid fins (grid_fin_aerodynamics.py:7-46), x sorted */
+    int32_t ca_n, cn_n;
+    double ca_x[PD_MAX_TAB], ca_y[PD_MAX_TAB], ca_min_mach, ca_min_val;
+    double cn_x[PD_MAX_TAB], cn_y[PD_MAX_TAB], cn_min_mach, cn_max_mach, cn_min_val, cn_max_val, cn_slope;
+    /* wind (HorizontalWindSpeed.py, vonkarman.py): profiles for percentiles 50..99 */
+    int32_t wind_n[PD_N_WIND_PROFILES];
+    double wind_alt_km[PD_N_WIND_PROFILES][PD_MAX_WIND], wind_speed[PD_N_WIND_PROFILES][PD_MAX_WIND];
+    double vk_Ad_u[4], vk_Bd_u[2], vk_Ad_v[4], vk_Bd_v[2], vk_y_threshold;
+    double sigma_u_lo, sigma_u_hi, sigma_v_lo, sigma_v_hi;
+    /* initial state (load_initial_states.py:236-242) and observation normalisers */
+    double state0[PD_N_STATE];
+    double norm_y, norm_vy, norm_x, norm_vx;
+    /* pre-enumerated neighbourhood keys of the two aero tables (host arrays, may be NULL) */
+    const uint64_t* keys_cd; int64_t n_keys_cd;
+    const uint64_t* keys_cl; int64_t n_keys_cl;
+} pd_params;
+
+typedef struct {
+    int64_t n_envs;
+    int32_t device;            /* HIP device ordinal */
+    int32_t phase;             /* pd_phase */
+    int32_t rtd;               /* pd_rtd */
+    int32_t precision;         /* pd_precision */
+    uint64_t seed;             /* Philox key (wind normals, sigmas, percentiles, tilt) */
+    uint64_t env_offset;       /* global index of env 0 (multi-GPU shards draw disjoint streams) */
+    int32_t enable_wind, stochastic_wind;
+    int32_t wind_percentile;   /* 50..99, or -1 = float(randint(50, 99)) per reset */
+    int32_t auto_reset;        /* reset envs in-kernel when done|truncated */
+    double tilt_sigma_rad;     /* initial pitch perturbation N(0, s) (0 = reference) */
+    int32_t action_f64;        /* actions are double (f64 path, no float32 islands) */
+    int32_t pad;
+} pd_config;
+
+typedef enum {
+    PD_INFO_AIR_DENSITY = 0, PD_INFO_PRESSURE, PD_INFO_SPEED_OF_SOUND, PD_INFO_MACH, PD_INFO_Q,
+    PD_INFO_CL, PD_INFO_CD, PD_INFO_MASS_FLOW, PD_INFO_X_COG, PD_INFO_INERTIA, PD_INFO_ALPHA_EFF,
+    PD_INFO_THROTTLE, PD_INFO_GLOAD, PD_INFO_UG, PD_INFO_VG, PD_INFO_GIMBAL_DEG
+} pd_info_field;
+
+typedef struct pd_env pd_env;
+
+int pd_abi_version(void);
+/* sizeof(pd_params) / sizeof(pd_config) as compiled, for binding-layout checks */
+size_t pd_sizeof_params(void);
+size_t pd_sizeof_config(void);
+const char* pd_last_error(void);
+/* Number of HIP devices visible (0 without a GPU); never aborts. */
+int pd_device_count(void);
+
+pd_status pd_create(const pd_params* params, const pd_config* cfg, pd_env** out);
+pd_status pd_destroy(pd_env* env);
+/* Reset envs (mask: device uint8[N], NULL = all).  obs may be NULL. */
+pd_status pd_reset(pd_env* env, const uint8_t* mask, void* obs, void* stream);
+/* One env step for all N envs.
+ *  actions : [N][A] float32 (or double when cfg.action_f64), A = 1 or 4
+ *  obs     : [N][O] (O = 2 pure throttle, 5 PSO landing_burn), post-step (pre-auto-reset)
+ *  reward  : [N]; done, truncated: uint8 [N]; trunc_id: int8 [N]   (any output may be NULL)
+ *  noise   : optional [N][8] double standard normals replacing the Philox wind stream
+ *            (sub-step k uses noise[2k], noise[2k+1]; test injection), NULL = Philox
+ *  info    : optional [PD_N_INFO][N] (last sub-step values), NULL = not written */
+pd_status pd_step(pd_env* env, const void* actions, void* obs, void* reward, uint8_t* done,
+                  uint8_t* truncated, int8_t* trunc_id, const double* noise, void* info, void* stream);
+/* Multi-step rollout with device-resident actions [T][N][A]: T launches of the step kernel,
+ * rewards accumulated into reward_sum [N] (may be NULL).  No host synchronisation. */
+pd_status pd_rollout(pd_env* env, const void* actions, int32_t n_steps, void* reward_sum,
+                     void* stream);
+/* Insert the aero neighbourhoods solved on device since the last flush into the handle's
+ * tables (one tiny kernel; a no-op when nothing missed).  Call every few steps: a missed
+ * neighbourhood is solved exactly on every lookup until it is flushed. */
+pd_status pd_flush_misses(pd_env* env, void* stream);
+/* Current observation (post-reset) [N][O]. */
+pd_status pd_observe(pd_env* env, void* obs, void* stream);
+/* State SoA [11][N] in the handle's precision. */
+pd_status pd_get_state(pd_env* env, void* state, void* stream);
+pd_status pd_set_state(pd_env* env, const void* state, void* stream);
+/* Landing-burn actuator memory [3][N] (gimbal deg, left/right fin command rad). */
+pd_status pd_get_actuators(pd_env* env, void* act, void* stream);
+pd_status pd_set_actuators(pd_env* env, const void* act, void* stream);
+/* Per-env wind state: sigma_u, sigma_v [2][N] (double). */
+pd_status pd_set_wind_sigmas(pd_env* env, const double* sig, void* stream);
+/* Counters since create: aero-table misses solved on device, NaN guard hits. Host sync. */
+pd_status pd_counters(pd_env* env, int64_t* rbf_misses, int64_t* table_entries_cd,
+                      int64_t* table_entries_cl, int64_t* nan_events);
+/* Observation / action widths of the handle. */
+int pd_obs_dim(const pd_env* env);
+int pd_action_dim(const pd_env* env);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -100,6 +100,9 @@ def lib():
         L.orc_step.argtypes = [P(OrcParams), P(OrcEnv), C.c_int, C.c_int, P(D), C.c_int, P(D), P(OrcOut)]
         L.orc_physics.restype = C.c_int
         L.orc_physics.argtypes = [P(OrcParams), P(OrcEnv), C.c_int, P(D), C.c_int, P(D), P(D)]
+        L.orc_rollout_ex.restype = D
+        L.orc_rollout_ex.argtypes = [P(OrcParams), C.c_int, C.c_int, C.c_int, C.c_int, P(C.c_float),
+                                     C.c_int, C.c_int, D, C.c_uint64, P(C.c_int64)]
         L.orc_rollout.restype = D
         L.orc_rollout.argtypes = [P(OrcParams), C.c_int, C.c_int, C.c_int, C.c_int, P(C.c_float),
                                   C.c_int, P(C.c_int64)]
@@ -235,9 +238,12 @@ def atmosphere(alt):
     return r.value, p.value, a.value
 
 
-def rollout(phase, rtd, n_env, n_steps, actions_f32, auto_reset=True):
+def rollout(phase, rtd, n_env, n_steps, actions_f32, auto_reset=True, wind=False, tilt=0.0, seed=1,
+            wind_percentile=50):
+    """Scalar CPU rollout (the cpu_baseline port): returns (sum of rewards, env-steps)."""
     acts = np.ascontiguousarray(actions_f32, dtype=np.float32)
     steps = C.c_int64()
-    acc = lib().orc_rollout(C.byref(params()), phase, rtd, n_env, n_steps,
-                            acts.ctypes.data_as(C.POINTER(C.c_float)), int(auto_reset), C.byref(steps))
+    acc = lib().orc_rollout_ex(C.byref(params(wind_percentile)), phase, rtd, n_env, n_steps,
+                               acts.ctypes.data_as(C.POINTER(C.c_float)), int(auto_reset), int(wind),
+                               float(tilt), int(seed), C.byref(steps))
     return acc, steps.value

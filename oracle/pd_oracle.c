@@ -555,22 +555,44 @@ int orc_step(const orc_params* P, orc_env* E, int phase, int rtd, const double* 
     return 0;
 }
 
-/* CPU baseline driver: n_env independent envs, static loop (the reference runs one env per
- * process; this is its scalar port).  Returns wall seconds is measured by the caller. */
+/* CPU baseline driver: n_env independent envs stepped in a static loop (the reference runs
+ * one env per process; this is its scalar port).  Optional stochastic wind (sigmas and
+ * normals from a xorshift64* + Box-Muller stream) and initial tilt N(0, tilt_sigma). */
+static uint64_t xs_next(uint64_t* s) { uint64_t x = *s; x ^= x >> 12; x ^= x << 25; x ^= x >> 27; *s = x; return x * 2685821657736338717ull; }
+static double xs_u01(uint64_t* s) { return (double)(xs_next(s) >> 11) * (1.0 / 9007199254740992.0); }
+static double xs_normal(uint64_t* s) {
+    double u1 = 1.0 - xs_u01(s), u2 = xs_u01(s);
+    return sqrt(-2.0 * log(u1)) * cos(2.0 * PI * u2);
+}
+static void rollout_reset(const orc_params* P, orc_env* E, int wind, double tilt, uint64_t* rng) {
+    double s0[11];
+    memcpy(s0, P->state0, sizeof(s0));
+    if (tilt > 0) { s0[4] += tilt * xs_normal(rng); s0[7] = s0[4] - s0[6]; }
+    orc_reset(P, E, s0, wind, wind, 0.5 + 1.75 * xs_u01(rng), 1.25 + 0.75 * xs_u01(rng));
+    E->noise_slotted = 1;
+}
 double orc_rollout(const orc_params* P, int phase, int rtd, int n_env, int n_steps,
                    const float* actions, int auto_reset, int64_t* env_steps_out) {
+    return orc_rollout_ex(P, phase, rtd, n_env, n_steps, actions, auto_reset, 0, 0.0, 1, env_steps_out);
+}
+double orc_rollout_ex(const orc_params* P, int phase, int rtd, int n_env, int n_steps,
+                      const float* actions, int auto_reset, int wind, double tilt, uint64_t seed,
+                      int64_t* env_steps_out) {
     int A = phase == ORC_PHASE_PURE_THROTTLE ? 1 : 4;
+    uint64_t rng = seed ? seed : 1;
     orc_env* envs = (orc_env*)malloc(sizeof(orc_env) * (size_t)n_env);
-    for (int i = 0; i < n_env; ++i) orc_reset(P, &envs[i], NULL, 0, 0, 0, 0);
+    for (int i = 0; i < n_env; ++i) rollout_reset(P, &envs[i], wind, tilt, &rng);
     double acc = 0.0; int64_t steps = 0;
     orc_out o;
+    double nz[8];
     for (int t = 0; t < n_steps; ++t) {
         for (int i = 0; i < n_env; ++i) {
             double u[4];
             for (int k = 0; k < A; ++k) u[k] = actions[((size_t)t * n_env + i) * A + k];
-            orc_step(P, &envs[i], phase, rtd, u, 1, NULL, &o);
+            if (wind) for (int k = 0; k < 8; ++k) nz[k] = xs_normal(&rng);
+            orc_step(P, &envs[i], phase, rtd, u, 1, wind ? nz : NULL, &o);
             acc += o.reward; ++steps;
-            if (auto_reset && (o.done || o.trunc)) orc_reset(P, &envs[i], NULL, 0, 0, 0, 0);
+            if (auto_reset && (o.done || o.trunc)) rollout_reset(P, &envs[i], wind, tilt, &rng);
         }
     }
     free(envs);

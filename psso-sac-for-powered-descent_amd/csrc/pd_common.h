@@ -1,0 +1,150 @@
+// pd_common.h -- host+device helpers of libpdenv (product code; independent of oracle/).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define PD_HD __host__ __device__ __forceinline__
+
+namespace pd {
+
+constexpr int kNbr = 50;            // RBFInterpolator(neighbors=50), aerodynamic_coefficients.py:59
+constexpr int kSys = kNbr + 3;      // + degree-1 polynomial tail (TPS default degree)
+constexpr int kCols = 5;            // AoA columns of each V2 table
+constexpr int kPay = 64;            // payload stride: 50 kernel coefs, 3 poly, shift0/1, scale0/1
+constexpr int kKeyLoBits = 6, kKeyLenBits = 6, kKeyField = kKeyLoBits + kKeyLenBits;
+constexpr uint64_t kEmptyKey = ~0ull;
+
+// CPython math.radians / math.degrees: x * (pi/180), x * (180/pi)
+constexpr double kPi = 3.141592653589793;
+constexpr double kDeg2Rad = kPi / 180.0;
+constexpr double kRad2Deg = 180.0 / kPi;
+
+PD_HD uint64_t key_pack(const int lo[kCols], const int len[kCols]) {
+    uint64_t k = 0;
+    for (int c = 0; c < kCols; ++c) {
+        uint64_t f = (uint64_t)(len[c] > 0 ? lo[c] : 0) | ((uint64_t)len[c] << kKeyLoBits);
+        k |= f << (kKeyField * c);
+    }
+    return k;
+}
+PD_HD void key_unpack(uint64_t k, int lo[kCols], int len[kCols]) {
+    for (int c = 0; c < kCols; ++c) {
+        uint64_t f = (k >> (kKeyField * c)) & ((1ull << kKeyField) - 1);
+        lo[c] = (int)(f & ((1u << kKeyLoBits) - 1));
+        len[c] = (int)(f >> kKeyLoBits);
+    }
+}
+PD_HD uint32_t key_hash(uint64_t k, int log2cap) {
+    return (uint32_t)((k * 0x9E3779B97F4A7C15ull) >> (64 - log2cap));
+}
+
+PD_HD double tps(double r) { return r == 0.0 ? 0.0 : r * r * log(r); }
+
+// Build and solve the thin-plate-spline system of ONE 50-point neighbourhood, exactly the
+// system scipy's RBFInterpolator builds (scipy/interpolate/_rbfinterp.py _build_system:
+// shift=(min+max)/2, scale=(max-min)/2 (0->1), K_ij = r^2 log r, P = [1, (y-shift)/scale],
+// [[K, P], [P^T, 0]] c = [d, 0]) and solve it by LU with partial pivoting (LAPACK dgesv's
+// algorithm).  Points are taken in window order (column by column, Mach-ascending).
+//   mach/coef: table arrays (column-grouped); col_start/col_aoa: column geometry
+//   work: >= kSys*kSys + kSys + 3*kNbr doubles of scratch;  payload: kPay doubles out.
+// Returns 0 on success, -1 on a singular system.
+PD_HD int solve_neighbourhood(const double* mach, const double* coef, const int* col_start,
+                              const double* col_aoa, uint64_t key, double* work, double* payload) {
+    int lo[kCols], len[kCols];
+    key_unpack(key, lo, len);
+    double* A = work;
+    double* b = A + kSys * kSys;
+    double* ym = b + kSys;
+    double* ya = ym + kNbr;
+    double* yd = ya + kNbr;
+    int n = 0;
+    for (int c = 0; c < kCols; ++c)
+        for (int i = 0; i < len[c]; ++i) {
+            if (n >= kNbr) return -1;
+            ym[n] = mach[col_start[c] + lo[c] + i];
+            ya[n] = col_aoa[c];
+            yd[n] = coef[col_start[c] + lo[c] + i];
+            ++n;
+        }
+    if (n != kNbr) return -1;
+    double mn0 = ym[0], mx0 = ym[0], mn1 = ya[0], mx1 = ya[0];
+    for (int j = 1; j < kNbr; ++j) {
+        mn0 = ym[j] < mn0 ? ym[j] : mn0; mx0 = ym[j] > mx0 ? ym[j] : mx0;
+        mn1 = ya[j] < mn1 ? ya[j] : mn1; mx1 = ya[j] > mx1 ? ya[j] : mx1;
+    }
+    double sh0 = (mx0 + mn0) / 2, sc0 = (mx0 - mn0) / 2, sh1 = (mx1 + mn1) / 2, sc1 = (mx1 - mn1) / 2;
+    if (sc0 == 0.0) sc0 = 1.0;
+    if (sc1 == 0.0) sc1 = 1.0;
+    for (int i = 0; i < kNbr; ++i) {
+        for (int j = 0; j < kNbr; ++j) {
+            double d0 = ym[i] - ym[j], d1 = ya[i] - ya[j];
+            A[i * kSys + j] = tps(sqrt(d0 * d0 + d1 * d1));
+        }
+        double h0 = (ym[i] - sh0) / sc0, h1 = (ya[i] - sh1) / sc1;
+        A[i * kSys + kNbr] = 1.0; A[i * kSys + kNbr + 1] = h0; A[i * kSys + kNbr + 2] = h1;
+        A[kNbr * kSys + i] = 1.0; A[(kNbr + 1) * kSys + i] = h0; A[(kNbr + 2) * kSys + i] = h1;
+        b[i] = yd[i];
+    }
+    for (int i = kNbr; i < kSys; ++i) {
+        for (int j = kNbr; j < kSys; ++j) A[i * kSys + j] = 0.0;
+        b[i] = 0.0;
+    }
+    for (int k = 0; k < kSys; ++k) {
+        int p = k;
+        double best = fabs(A[k * kSys + k]);
+        for (int i = k + 1; i < kSys; ++i) {
+            double v = fabs(A[i * kSys + k]);
+            if (v > best) { best = v; p = i; }
+        }
+        if (best == 0.0) return -1;
+        if (p != k) {
+            for (int j = 0; j < kSys; ++j) { double t = A[k * kSys + j]; A[k * kSys + j] = A[p * kSys + j]; A[p * kSys + j] = t; }
+            double t = b[k]; b[k] = b[p]; b[p] = t;
+        }
+        double r = 1.0 / A[k * kSys + k];
+        for (int i = k + 1; i < kSys; ++i) {
+            double l = A[i * kSys + k] * r;
+            if (l != 0.0)
+                for (int j = k + 1; j < kSys; ++j) A[i * kSys + j] -= l * A[k * kSys + j];
+            b[i] -= l * b[k];
+        }
+    }
+    for (int i = kSys - 1; i >= 0; --i) {
+        double s = b[i];
+        for (int j = i + 1; j < kSys; ++j) s -= A[i * kSys + j] * b[j];
+        b[i] = s / A[i * kSys + i];
+    }
+    for (int j = 0; j < kSys; ++j) payload[j] = b[j];
+    payload[kSys + 0] = sh0; payload[kSys + 1] = sh1;
+    payload[kSys + 2] = sc0; payload[kSys + 3] = sc1;
+    for (int j = kSys + 4; j < kPay; ++j) payload[j] = 0.0;
+    return 0;
+}
+
+// ---------------------------------------------------------------- Philox4x32-10
+struct u32x4 { uint32_t x, y, z, w; };
+PD_HD u32x4 philox(u32x4 c, uint32_t k0, uint32_t k1) {
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        uint64_t p0 = (uint64_t)0xD2511F53u * c.x;
+        uint64_t p1 = (uint64_t)0xCD9E8D57u * c.z;
+        u32x4 n;
+        n.x = (uint32_t)(p1 >> 32) ^ c.y ^ k0;
+        n.y = (uint32_t)p1;
+        n.z = (uint32_t)(p0 >> 32) ^ c.w ^ k1;
+        n.w = (uint32_t)p0;
+        c = n;
+        k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+    }
+    return c;
+}
+// 53-bit uniform in [0, 1)
+PD_HD double u01(uint32_t hi, uint32_t lo) {
+    return ((double)(hi >> 5) * 67108864.0 + (double)(lo >> 6)) * (1.0 / 9007199254740992.0);
+}
+// Philox purpose tags (4th counter word)
+constexpr uint32_t kTagWindSub = 0;   // +substep 0..3
+constexpr uint32_t kTagReset = 16;
+constexpr uint32_t kTagTilt = 17;
+
+}  // namespace pd

@@ -1,0 +1,217 @@
+// pd_physics.h -- device physics of the landing burn, templated on the state precision.
+//
+// One lane = one environment.  Every function restates a reference function (file:line)
+// with the same operation order, so that the binary64 instantiation reproduces the
+// reference's IEEE results (up to libm ulps); the float instantiation is the throughput mode.
+#pragma once
+#include "pd_common.h"
+
+namespace pd {
+
+template <typename R> struct Cst;
+template <> struct Cst<double> {
+    static constexpr double deg2rad = kDeg2Rad, rad2deg = kRad2Deg, pi = kPi, two_pi = 2 * kPi;
+    static constexpr double inf = __builtin_huge_val();
+};
+template <> struct Cst<float> {
+    static constexpr float deg2rad = (float)kDeg2Rad, rad2deg = (float)kRad2Deg, pi = (float)kPi,
+                           two_pi = (float)(2 * kPi);
+    static constexpr float inf = __builtin_huge_valf();
+};
+
+// Device parameter block (one per handle, in HBM, read with uniform scalar loads).
+template <typename R> struct DevParams {
+    // sizing
+    R T_e, p_e, A_e, v_ex, S_gf, d_base_gf, R_rocket, A_front, m_prop0, C_gust_x, C_gust_y;
+    int n_eng, pad0;
+    // float32 islands: constants as NumPy casts them (weak Python scalars -> float32)
+    float f_Te_over_vex, f_one_minus_nom_pt, f_nom_pt, f_one_minus_nom_lb, f_nom_lb, f_dt_pt, f_dt_lb,
+        f_max_gimbal_rad, f_max_defl_rad, pad1;
+    R Te_over_vex, one_minus_nom_pt, nom_pt, one_minus_nom_lb, nom_lb, max_gimbal_rad, max_gimbal_deg,
+        max_defl_rad;
+    // mass properties
+    R h_ox, h_f, m_ox, m_f, h_lower, m_dry, x_dry, I_dry, engine_height, cop;
+    // ISA: per layer base, T, p, beta, beta/Tb, exponent -g0/(beta R), isothermal -g0/(R Tb)
+    R isa_Hb[9], isa_Tb[9], isa_beta[9], isa_pb[9], isa_bt[9], isa_ex[9], isa_iso[9];
+    R isa_r, isa_R, isa_kappaR, isa_alt_max, grav_R, grav_g0;
+    // aero tables: geometry (the Mach arrays are staged into LDS)
+    int cd_start[kCols], cd_len[kCols], cl_start[kCols], cl_len[kCols];
+    R cd_aoa[kCols], cl_aoa[kCols];
+    int cd_n, cl_n;
+    R cd_mach[256], cl_mach[256];
+    // binary64 copies for on-device neighbourhood solves
+    double cd_mach_d[256], cd_coef_d[256], cl_mach_d[256], cl_coef_d[256], cd_aoa_d[kCols], cl_aoa_d[kCols];
+    // grid fins
+    int ca_n, cn_n;
+    R ca_x[64], ca_y[64], ca_min_mach, ca_min_val;
+    R cn_x[64], cn_y[64], cn_min_mach, cn_max_mach, cn_min_val, cn_max_val, cn_slope;
+    // wind
+    int wind_n[50];
+    R wind_alt_km[50][16], wind_speed[50][16];
+    R vk_Ad_u[4], vk_Bd_u[2], vk_Ad_v[4], vk_Bd_v[2], vk_y_threshold;
+    double sigma_u_lo, sigma_u_hi, sigma_v_lo, sigma_v_hi;
+    // initial state, observation normalisers
+    R state0[11];
+    double state0_d[11];
+    R norm_y, norm_vy, norm_x, norm_vx, k_theta_pso;
+    R y0_rl, m0_rl;
+    // neighbourhood hash tables
+    const unsigned long long* keys_cd;
+    const unsigned long long* keys_cl;
+    const R* pay_cd;
+    const R* pay_cl;
+    int logcap_cd, logcap_cl;
+    unsigned long long init_key_cd, init_key_cl;
+};
+
+// ---------------------------------------------------------------- atmosphere
+// atmosphere_dynamics.py:5-27 (ambiance ISA restated)
+template <typename R>
+__device__ __forceinline__ void atmosphere(const DevParams<R>& P, R y, R& rho, R& p, R& a) {
+    R alt = y < R(0) ? R(0) : y;
+    if (alt < P.isa_alt_max) {
+        R H = P.isa_r * alt / (P.isa_r + alt);
+        int i = 0;
+#pragma unroll
+        for (int k = 1; k < 9; ++k) i = (P.isa_Hb[k] <= H) ? k : i;
+        R Hb = P.isa_Hb[i], Tb = P.isa_Tb[i], b = P.isa_beta[i], pb = P.isa_pb[i];
+        R dH = H - Hb;
+        R T = Tb + b * dH;
+        R pp;
+        if (b != R(0)) pp = pb * pow(R(1) + P.isa_bt[i] * dH, P.isa_ex[i]);
+        else pp = pb * exp(P.isa_iso[i] * dH);
+        p = pp;
+        rho = pp / (P.isa_R * T);
+        a = sqrt(P.isa_kappaR * T);
+    } else {
+        rho = R(0); p = R(0); a = R(0);
+    }
+}
+
+template <typename R> __device__ __forceinline__ R gravity(const DevParams<R>& P, R y) {
+    R q = P.grav_R / (P.grav_R + y);      // atmosphere_dynamics.py:29-33
+    return P.grav_g0 * (q * q);
+}
+
+// stage_inertia closure (rocket_dimensions.py:167-196)
+template <typename R>
+__device__ __forceinline__ void inertia(const DevParams<R>& P, R fill, R& x_cog, R& I) {
+    R h_ox_t = P.h_ox * fill, h_f_t = P.h_f * fill, m_ox_t = P.m_ox * fill, m_f_t = P.m_f * fill;
+    R x_prop = (m_ox_t * (P.h_lower + h_ox_t / R(2)) + m_f_t * (P.h_lower + P.h_ox + h_f_t / R(2))) / (m_ox_t + m_f_t);
+    R t1 = P.h_lower + h_ox_t / R(2) - x_prop;
+    R I_ox = R(1.0 / 12) * m_ox_t * (h_ox_t * h_ox_t) + m_ox_t * (t1 * t1);
+    R t2 = P.h_lower + P.h_ox + h_f_t / R(2) - x_prop;
+    R I_f = R(1.0 / 12) * m_f_t * (h_f_t * h_f_t) + m_f_t * (t2 * t2);
+    R mp_t = m_ox_t + m_f_t;
+    R x_wet = (P.m_dry * P.x_dry + mp_t * x_prop) / (P.m_dry + mp_t);
+    R t3 = P.x_dry - x_wet, t4 = x_prop - x_wet;
+    x_cog = x_wet;
+    I = (P.I_dry + P.m_dry * (t3 * t3)) + ((I_ox + I_f) + mp_t * (t4 * t4));
+}
+
+// ---------------------------------------------------------------- tables in LDS
+// scipy interp1d._call_linear with fill_value='extrapolate' (grid_fin_aerodynamics.py:7-18)
+template <typename R>
+__device__ __forceinline__ R grid_fin_ca(const DevParams<R>& P, const R* sx, const R* sy, R mach) {
+    if (mach < P.ca_min_mach) return P.ca_min_val;
+    int n = P.ca_n;
+    int lo = 0, hi = n;                       // lower_bound: first x >= mach
+    while (lo < hi) { int mid = (lo + hi) >> 1; if (sx[mid] < mach) lo = mid + 1; else hi = mid; }
+    int idx = lo < 1 ? 1 : (lo > n - 1 ? n - 1 : lo);
+    R xl = sx[idx - 1], xh = sx[idx], yl = sy[idx - 1], yh = sy[idx];
+    R slope = (yh - yl) / (xh - xl);
+    return slope * (mach - xl) + yl;
+}
+
+// np.interp for an in-range query (numpy compiled_base.c arr_interp)
+template <typename R>
+__device__ __forceinline__ R np_interp(const R* x, const R* y, int n, R v) {
+    if (v < x[0]) return y[0];
+    if (v >= x[n - 1]) return y[n - 1];
+    int lo = 0, hi = n;                       // upper_bound: first x > v
+    while (lo < hi) { int mid = (lo + hi) >> 1; if (x[mid] <= v) lo = mid + 1; else hi = mid; }
+    int j = lo - 1;
+    if (x[j] == v) return y[j];
+    R slope = (y[j + 1] - y[j]) / (x[j + 1] - x[j]);
+    return slope * (v - x[j]) + y[j];
+}
+
+// grid_fin_aerodynamics.py:21-46: cn_alpha(M) * degrees(alpha)
+template <typename R>
+__device__ __forceinline__ R grid_fin_cn_alpha(const DevParams<R>& P, const R* sx, const R* sy, R mach) {
+    if (mach < P.cn_min_mach) return P.cn_min_val;
+    if (mach <= P.cn_max_mach) return np_interp(sx, sy, P.cn_n, mach);
+    return P.cn_max_val + P.cn_slope * (mach - P.cn_max_mach);
+}
+
+// ---------------------------------------------------------------- exact local-RBF aero
+// Incremental 50-NN maintenance on the per-column Mach windows.  Within one AoA column the
+// squared distance is convex in the Mach-sorted index, so a neighbourhood is one contiguous
+// window per column; the 50-NN set is the unique window set with
+//      max(included endpoint distance) <= min(adjacent excluded distance).
+// Starting from the env's cached window set we swap (worst included) <-> (best adjacent
+// excluded) until that holds; each swap strictly lowers the sum of included distances.
+template <typename R> struct RbfCache {
+    unsigned long long key;
+    int slot;
+};
+
+template <typename R>
+__device__ __forceinline__ R d2_at(const R* mach, int start, int i, R M, R dz) {
+    R dm = M - mach[start + i];
+    return dm * dm + dz;
+}
+
+template <typename R>
+__device__ __forceinline__ void knn_windows(const R* smach, const int* start, const int* n,
+                                            const R* aoa, R M, R a, int lo[kCols], int len[kCols]) {
+    R dz[kCols];
+    int p[kCols];
+#pragma unroll
+    for (int c = 0; c < kCols; ++c) {
+        R da = a - aoa[c];
+        dz[c] = da * da;
+        // insertion point of M (used for empty columns)
+        int l = 0, h = n[c];
+        while (l < h) { int mid = (l + h) >> 1; if (smach[start[c] + mid] < M) l = mid + 1; else h = mid; }
+        p[c] = l;
+    }
+    for (int it = 0; it < 256; ++it) {
+        R maxin = R(-1); int maxc = -1, maxi = 0;
+        R minex = Cst<R>::inf; int minc = -1, mini = 0;
+#pragma unroll
+        for (int c = 0; c < kCols; ++c) {
+            if (len[c] > 0) {
+                int l0 = lo[c], l1 = lo[c] + len[c] - 1;
+                R da0 = d2_at(smach, start[c], l0, M, dz[c]);
+                R da1 = d2_at(smach, start[c], l1, M, dz[c]);
+                if (da0 > maxin) { maxin = da0; maxc = c; maxi = l0; }
+                if (da1 > maxin) { maxin = da1; maxc = c; maxi = l1; }
+                if (l0 > 0) { R d = d2_at(smach, start[c], l0 - 1, M, dz[c]); if (d < minex) { minex = d; minc = c; mini = l0 - 1; } }
+                if (l1 + 1 < n[c]) { R d = d2_at(smach, start[c], l1 + 1, M, dz[c]); if (d < minex) { minex = d; minc = c; mini = l1 + 1; } }
+            } else {
+                if (p[c] > 0) { R d = d2_at(smach, start[c], p[c] - 1, M, dz[c]); if (d < minex) { minex = d; minc = c; mini = p[c] - 1; } }
+                if (p[c] < n[c]) { R d = d2_at(smach, start[c], p[c], M, dz[c]); if (d < minex) { minex = d; minc = c; mini = p[c]; } }
+            }
+        }
+        if (!(maxin > minex)) break;          // also exits on NaN queries
+        // add the best excluded point, then drop the worst included one
+#pragma unroll
+        for (int c = 0; c < kCols; ++c) {
+            if (c == minc) {
+                if (len[c] == 0) { lo[c] = mini; len[c] = 1; }
+                else if (mini < lo[c]) { lo[c] = mini; len[c] += 1; }
+                else { len[c] += 1; }
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < kCols; ++c) {
+            if (c == maxc) {
+                if (maxi == lo[c]) { lo[c] += 1; len[c] -= 1; }
+                else { len[c] -= 1; }
+            }
+        }
+    }
+}
+
+}  // namespace pd

@@ -1,0 +1,1125 @@
+// pdenv.hip -- MI355X (gfx950) kernels and C ABI of the vectorised powered-descent env.
+//
+// Layout in HBM: struct-of-arrays, one lane per env.  A step launch reads each env's state
+// (11 words), its g-load window and caches, runs the 4 physics sub-steps of
+// rocket_environment_pre_wrap.step in registers, and writes state + outputs once.
+// Parameter tables are staged into LDS per workgroup; scalar parameters are uniform loads
+// from a per-handle parameter block.  See DESIGN.md for the roofline of each kernel.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/pdenv.h"
+#include "pd_physics.h"
+
+using namespace pd;
+
+namespace {
+
+thread_local std::string g_err;
+pd_status fail(pd_status s, const std::string& m) { g_err = m; return s; }
+
+#define PD_HIP(expr)                                                                   \
+    do {                                                                               \
+        hipError_t e_ = (expr);                                                        \
+        if (e_ != hipSuccess)                                                          \
+            return fail(PD_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+constexpr int kBlock = 256;
+constexpr int kScratch = kSys * kSys + kSys + 3 * kNbr + kPay;   // doubles per wave
+constexpr int kPendingCap = 1024;
+
+// ---------------------------------------------------------------- per-env device buffers
+template <typename R> struct EnvBufs {
+    R* st;            // [11][N]
+    R* vprev;         // [N]   |v| of the previous state (base_environment.py:137-139)
+    R* gwin;          // [10][N] g-load ring
+    uint8_t* ghead;   // [N]
+    uint8_t* glen;    // [N]
+    R* act;           // [3][N] landing_burn actuator memory
+    R* wind;          // [6][N] fu0 fu1 fv0 fv1 sigma_u sigma_v
+    uint8_t* wprof;   // [N] wind profile (percentile-50)
+    unsigned long long* key;   // [2][N] cached neighbourhood keys (cd, cl)
+    int* slot;                 // [2][N] cached table slots
+    int8_t* tid;      // [N] truncation id
+    uint32_t* epi;    // [N] episode counter
+    uint32_t* tstep;  // [N] step within episode
+};
+
+struct Pending {
+    unsigned long long* count;   // [1] entries appended this launch
+    unsigned long long* keys;    // [cap] (table id in bit 63)
+    double* pay;                 // [cap][kPay]
+    unsigned long long* stats;   // [4] misses, nan events, inserted cd, inserted cl
+};
+
+template <typename R> struct StepArgs {
+    const DevParams<R>* P;
+    EnvBufs<R> b;
+    Pending pend;
+    double* scratch;             // [n_waves][kScratch]
+    int64_t n;
+    uint64_t env_offset;
+    uint32_t seed_lo, seed_hi;
+    int act_f64, auto_reset, stochastic, fixed_prof, use_tilt;
+    double tilt_sigma;
+    const void* actions;
+    R* obs; R* reward; uint8_t* done; uint8_t* trunc; int8_t* trunc_id;
+    const double* noise;
+    R* info;
+    R* reward_sum;
+};
+
+// ---------------------------------------------------------------- reset of one env
+template <typename R>
+__device__ void reset_env(const StepArgs<R>& a, int64_t i, uint32_t episode, bool reset_cache) {
+    const DevParams<R>& P = *a.P;
+    const int64_t N = a.n;
+    R s[11];
+#pragma unroll
+    for (int k = 0; k < 11; ++k) s[k] = P.state0[k];
+    uint64_t g = a.env_offset + (uint64_t)i;
+    if (a.use_tilt) {
+        u32x4 r = philox({(uint32_t)g, (uint32_t)(g >> 32) ^ episode, 0u, kTagTilt}, a.seed_lo, a.seed_hi);
+        double u1 = 1.0 - u01(r.x, r.y), u2 = u01(r.z, r.w);
+        double z = sqrt(-2.0 * log(u1)) * cos(2.0 * kPi * u2);
+        s[4] = s[4] + (R)(a.tilt_sigma * z);
+        s[7] = s[4] - s[6];
+    }
+#pragma unroll
+    for (int k = 0; k < 11; ++k) a.b.st[k * N + i] = s[k];
+    a.b.vprev[i] = sqrt(s[2] * s[2] + s[3] * s[3]);
+    a.b.ghead[i] = 0; a.b.glen[i] = 0;
+    a.b.act[i] = R(0); a.b.act[N + i] = R(0); a.b.act[2 * N + i] = R(0);
+    a.b.tid[i] = 0;
+    a.b.epi[i] = episode; a.b.tstep[i] = 0;
+    // wind: VKDisturbanceGenerator._new_filters (vonkarman.py:60-66): sigmas drawn per reset,
+    // filter state zeroed; WindModel.compile_horizontal_fixed_wind: percentile per reset
+    u32x4 r = philox({(uint32_t)g, (uint32_t)(g >> 32) ^ episode, 0u, kTagReset}, a.seed_lo, a.seed_hi);
+    double su = P.sigma_u_lo + (P.sigma_u_hi - P.sigma_u_lo) * u01(r.x, r.y);
+    double sv = P.sigma_v_lo + (P.sigma_v_hi - P.sigma_v_lo) * u01(r.z, r.w);
+    a.b.wind[i] = R(0); a.b.wind[N + i] = R(0); a.b.wind[2 * N + i] = R(0); a.b.wind[3 * N + i] = R(0);
+    a.b.wind[4 * N + i] = (R)su; a.b.wind[5 * N + i] = (R)sv;
+    a.b.wprof[i] = a.fixed_prof >= 0 ? (uint8_t)a.fixed_prof : (uint8_t)((r.x ^ r.w) % 49u);  // randint(50, 99)
+    if (reset_cache) {   // any valid 50-set is a correct start for the swap search
+        a.b.key[i] = P.init_key_cd; a.b.key[N + i] = P.init_key_cl;
+        a.b.slot[i] = -1; a.b.slot[N + i] = -1;
+    }
+}
+
+template <typename R>
+__global__ __launch_bounds__(kBlock) void k_reset(StepArgs<R> a, const uint8_t* mask) {
+    int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= a.n) return;
+    if (mask && !mask[i]) return;
+    uint32_t ep = a.b.epi[i] + 1;
+    reset_env(a, i, ep, true);
+}
+
+// ---------------------------------------------------------------- RBF lookup + evaluation
+template <typename R>
+__device__ __forceinline__ R rbf_eval(const R* __restrict__ pay, const R* smach, const int* start,
+                                      const R* aoa, const int lo[kCols], const int len[kCols], R M, R a) {
+    R s = R(0);
+    int j = 0;
+#pragma unroll
+    for (int c = 0; c < kCols; ++c) {
+        R da = a - aoa[c];
+        R da2 = da * da;
+        const R* m = smach + start[c] + lo[c];
+        for (int k = 0; k < len[c]; ++k) {
+            R dm = M - m[k];
+            R r = sqrt(dm * dm + da2);
+            R phi = r == R(0) ? R(0) : r * r * log(r);
+            s += phi * pay[j + k];
+        }
+        j += len[c];
+    }
+    s += R(1) * pay[kNbr];
+    s += (M - pay[kSys + 0]) / pay[kSys + 2] * pay[kNbr + 1];
+    s += (a - pay[kSys + 1]) / pay[kSys + 3] * pay[kNbr + 2];
+    return s;
+}
+
+// slow path: the neighbourhood is not in the table -> solve it here, exactly, on one lane
+// (rare: the table is pre-enumerated over the reachable domain), and queue it for insertion.
+template <typename R>
+__device__ __noinline__ R rbf_miss(const StepArgs<R>& a, int table, unsigned long long key, R M, R aq,
+                                   const R* smach) {
+    const DevParams<R>& P = *a.P;
+    int64_t wave = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
+    double* work = a.scratch + wave * kScratch;
+    double* pay = work + (kScratch - kPay);
+    const double* mach = table ? P.cl_mach_d : P.cd_mach_d;
+    const double* coef = table ? P.cl_coef_d : P.cd_coef_d;
+    const int* start = table ? P.cl_start : P.cd_start;
+    const double* aoa = table ? P.cl_aoa_d : P.cd_aoa_d;
+    int rc = solve_neighbourhood(mach, coef, start, aoa, key, work, pay);
+    atomicAdd(&a.pend.stats[0], 1ull);
+    if (rc != 0) return (R)NAN;
+    unsigned long long idx = atomicAdd(a.pend.count, 1ull);
+    if (idx < (unsigned long long)kPendingCap) {
+        for (int j = 0; j < kPay; ++j) a.pend.pay[idx * kPay + j] = pay[j];
+        a.pend.keys[idx] = key | ((unsigned long long)table << 63);
+    }
+    int lo[kCols], len[kCols];
+    key_unpack(key, lo, len);
+    R* payR = (R*)work;   // the matrix area is free again: payload in the kernel's precision
+    for (int j = 0; j < kPay; ++j) payR[j] = (R)pay[j];
+    const R* aoaR = table ? P.cl_aoa : P.cd_aoa;
+    return rbf_eval<R>(payR, smach, start, aoaR, lo, len, M, aq);
+}
+
+template <typename R>
+__device__ __forceinline__ R rbf(const StepArgs<R>& a, int table, const R* smach, RbfCache<R>& cache,
+                                 R M, R aq) {
+    const DevParams<R>& P = *a.P;
+    const int* start = table ? P.cl_start : P.cd_start;
+    const int* n = table ? P.cl_len : P.cd_len;
+    const R* aoa = table ? P.cl_aoa : P.cd_aoa;
+    int lo[kCols], len[kCols];
+    key_unpack(cache.key, lo, len);
+    // keys store lo=0 for empty columns; knn_windows uses insertion points for those
+    knn_windows<R>(smach, start, n, aoa, M, aq, lo, len);
+    unsigned long long key = key_pack(lo, len);
+    int slot = cache.slot;
+    if (key != cache.key || slot < 0) {
+        const unsigned long long* keys = table ? P.keys_cl : P.keys_cd;
+        int lc = table ? P.logcap_cl : P.logcap_cd;
+        uint32_t mask = (1u << lc) - 1u;
+        uint32_t h = key_hash(key, lc);
+        slot = -1;
+        for (uint32_t probe = 0; probe <= mask; ++probe) {
+            unsigned long long k = keys[h];
+            if (k == key) { slot = (int)h; break; }
+            if (k == kEmptyKey) break;
+            h = (h + 1) & mask;
+        }
+        cache.key = key;
+        cache.slot = slot;
+    }
+    R val = R(0);
+    if (slot >= 0) {
+        const R* pay = (table ? P.pay_cl : P.pay_cd) + (int64_t)slot * kPay;
+        val = rbf_eval<R>(pay, smach, start, aoa, lo, len, M, aq);
+    }
+    // misses share the wave's scratch: serialise them over the active lanes (the wave runs
+    // divergent branches one after another, so lanes of other call sites never overlap)
+    unsigned long long mm = __ballot(slot < 0);
+    while (mm) {
+        int leader = __ffsll((long long)mm) - 1;
+        if ((int)__lane_id() == leader) val = rbf_miss<R>(a, table, key, M, aq, smach);
+        mm &= mm - 1;
+    }
+    return val;
+}
+
+// rocket_CD: CD_func = rocket_CD(M, degrees(alpha)); clamp of the DEGREE value at
+// +-radians(10) (rockets_physics.py:712, aerodynamic_coefficients.py:105-115)
+template <typename R>
+__device__ __forceinline__ R coef_CD(const StepArgs<R>& a, const R* smach, RbfCache<R>& c, R M, R ae) {
+    R aoa = ae * Cst<R>::rad2deg;
+    const R r10 = (R)(10.0 * kDeg2Rad);
+    if (aoa > r10) aoa = r10;
+    else if (aoa < (R)(-10.0 * kDeg2Rad)) aoa = (R)(-10.0 * kDeg2Rad);
+    return rbf<R>(a, 0, smach, c, M, aoa);
+}
+// rocket_CL: degrees applied twice (rockets_physics.py:711 + aerodynamic_coefficients.py:117-132);
+// the clamp/sign cases are resolved first so that one inlined RBF serves all of them.
+template <typename R>
+__device__ __forceinline__ R coef_CL(const StepArgs<R>& a, const R* smach, RbfCache<R>& c, R M, R ae) {
+    R aq = (ae * Cst<R>::rad2deg) * Cst<R>::rad2deg;
+    R sgn = R(1);
+    bool zero = false;
+    if (aq > R(10)) aq = R(10);
+    else if (aq < R(-10)) aq = R(-10);
+    else if (fabs(aq) < R(1e-6)) zero = true;
+    else if (aq < R(0)) { aq = fabs(aq); sgn = R(-1); }
+    if (zero) return R(0);
+    R v = rbf<R>(a, 1, smach, c, M, aq);
+    return sgn < R(0) ? -v : v;
+}
+
+// ---------------------------------------------------------------- the step kernel
+template <typename R, int PHASE, int RTD, bool WIND> struct Lds {
+    static constexpr int kCd = 0, kCl = 256, kCaX = 512, kCaY = 576, kCnX = 640, kCnY = 704,
+                         kWAlt = 768, kWSp = kWAlt + 800, kTotal = WIND ? kWSp + 800 : kWAlt;
+};
+
+template <typename R, int PHASE, int RTD, bool WIND>
+__global__ __launch_bounds__(kBlock) void k_step(StepArgs<R> a) {
+    using L = Lds<R, PHASE, RTD, WIND>;
+    __shared__ R lds[L::kTotal];
+    const DevParams<R>& P = *a.P;
+    for (int t = threadIdx.x; t < 256; t += kBlock) { lds[L::kCd + t] = P.cd_mach[t]; lds[L::kCl + t] = P.cl_mach[t]; }
+    if (threadIdx.x < 64) {
+        lds[L::kCaX + threadIdx.x] = P.ca_x[threadIdx.x]; lds[L::kCaY + threadIdx.x] = P.ca_y[threadIdx.x];
+        lds[L::kCnX + threadIdx.x] = P.cn_x[threadIdx.x]; lds[L::kCnY + threadIdx.x] = P.cn_y[threadIdx.x];
+    }
+    if constexpr (WIND) {
+        for (int t = threadIdx.x; t < 800; t += kBlock) {
+            lds[L::kWAlt + t] = (&P.wind_alt_km[0][0])[t];
+            lds[L::kWSp + t] = (&P.wind_speed[0][0])[t];
+        }
+    }
+    __syncthreads();
+    const int64_t N = a.n;
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= N) return;
+    const R* s_cd = lds + L::kCd;
+    const R* s_cl = lds + L::kCl;
+
+    R s[11];
+#pragma unroll
+    for (int k = 0; k < 11; ++k) s[k] = a.b.st[k * N + i];
+    RbfCache<R> ccd{a.b.key[i], a.b.slot[i]}, ccl{a.b.key[N + i], a.b.slot[N + i]};
+    R gprev = R(0), dlprev = R(0), drprev = R(0);
+    if constexpr (PHASE == 1) { gprev = a.b.act[i]; dlprev = a.b.act[N + i]; drprev = a.b.act[2 * N + i]; }
+    R fu0 = R(0), fu1 = R(0), fv0 = R(0), fv1 = R(0), sgu = R(0), sgv = R(0);
+    int prof = 0;
+    if constexpr (WIND) {
+        fu0 = a.b.wind[i]; fu1 = a.b.wind[N + i]; fv0 = a.b.wind[2 * N + i]; fv1 = a.b.wind[3 * N + i];
+        sgu = a.b.wind[4 * N + i]; sgv = a.b.wind[5 * N + i];
+        prof = a.b.wprof[i];
+    }
+    const uint32_t ep = a.b.epi[i], ts = a.b.tstep[i];
+    const uint64_t g = a.env_offset + (uint64_t)i;
+
+    // actions (float32 unless act_f64)
+    float uf[4] = {0.f, 0.f, 0.f, 0.f};
+    double ud[4] = {0.0, 0.0, 0.0, 0.0};
+    constexpr int A = PHASE == 0 ? 1 : 4;
+    if (a.act_f64) {
+        const double* ap = (const double*)a.actions + i * A;
+#pragma unroll
+        for (int k = 0; k < A; ++k) ud[k] = ap[k];
+    } else {
+        const float* ap = (const float*)a.actions + i * A;
+#pragma unroll
+        for (int k = 0; k < A; ++k) uf[k] = ap[k];
+    }
+
+    const R dt = PHASE == 0 ? R(0.025) : R(0.1);
+    const R dt_act = R(0.025);
+    R gdeg_out = gprev, dcmdl_out = dlprev, dcmdr_out = drprev;
+    bool nan_hit = false;
+
+#pragma unroll 1
+    for (int sub = 0; sub < 4; ++sub) {
+        R x = s[0], y = s[1], vx = s[2], vy = s[3], th = s[4], thd = s[5], ga = s[6], al = s[7];
+        R m = s[8], mp = s[9];
+        // rocket_physics_fcn (rockets_physics.py:455-704)
+        R rho, patm, asnd;
+        atmosphere<R>(P, y, rho, patm, asnd);
+        R speed = sqrt(vx * vx + vy * vy);
+        R mach = R(0);
+        if (asnd != R(0)) { R mr = speed / asnd; mach = (R(10) < mr) ? R(10) : mr; }
+        R q = R(0.5) * rho * (speed * speed);
+        R fpc = (P.m_prop0 - mp) / P.m_prop0;
+        if (fpc == R(0)) fpc = R(1e-6);
+        R x_cog, I;
+        inertia<R>(P, R(1) - fpc, x_cog, I);
+        R d_thrust = x_cog + P.engine_height;
+        R ae = (vy < R(0)) ? ga - th - Cst<R>::pi : al;
+        R d_cp_cg = x_cog - P.cop;
+        R ug = R(0), vg = R(0);
+        if constexpr (WIND) {
+            // WindModel.__call__ (full_wind_model.py:35-43)
+            const R* walt = lds + L::kWAlt + prof * 16;
+            const R* wsp = lds + L::kWSp + prof * 16;
+            R km = y / R(1000);
+            int wn = P.wind_n[prof];
+            ug = np_interp<R>(walt, wsp, wn, km);
+            if (y < P.vk_y_threshold && a.stochastic) {
+                double w0, w1;
+                if (a.noise) { w0 = a.noise[i * 8 + 2 * sub]; w1 = a.noise[i * 8 + 2 * sub + 1]; }
+                else {
+                    u32x4 r = philox({(uint32_t)g, (uint32_t)(g >> 32) ^ ep, ts, kTagWindSub + (uint32_t)sub},
+                                     a.seed_lo, a.seed_hi);
+                    double u1 = 1.0 - u01(r.x, r.y), u2 = u01(r.z, r.w);
+                    double rad = sqrt(-2.0 * log(u1));
+                    w0 = rad * cos(2.0 * kPi * u2); w1 = rad * sin(2.0 * kPi * u2);
+                }
+                // vonkarman.py:33-36: state = Ad @ state + Bd * w  (Bd = sigma * Bd(sigma=1))
+                R n0 = (P.vk_Ad_u[0] * fu0 + P.vk_Ad_u[1] * fu1) + (sgu * P.vk_Bd_u[0]) * (R)w0;
+                R n1 = (P.vk_Ad_u[2] * fu0 + P.vk_Ad_u[3] * fu1) + (sgu * P.vk_Bd_u[1]) * (R)w0;
+                fu0 = n0; fu1 = n1;
+                n0 = (P.vk_Ad_v[0] * fv0 + P.vk_Ad_v[1] * fv1) + (sgv * P.vk_Bd_v[0]) * (R)w1;
+                n1 = (P.vk_Ad_v[2] * fv0 + P.vk_Ad_v[3] * fv1) + (sgv * P.vk_Bd_v[1]) * (R)w1;
+                fv0 = n0; fv1 = n1;
+                ug = ug + fu1;
+                vg = fv1;
+            }
+        }
+        R Fwx = R(0.5) * rho * (ug * ug) * P.A_front * P.C_gust_x;
+        R Fwy = R(0.5) * rho * (vg * vg) * P.A_front * P.C_gust_y;
+        R Mw = -d_cp_cg * Fwy;
+        R CL = R(0), CD = R(0);
+        if (asnd != R(0)) {
+            CL = coef_CL<R>(a, s_cl, ccl, mach, ae);
+            CD = coef_CD<R>(a, s_cd, ccd, mach, ae);
+        }
+        R drag = R(0.5) * rho * (speed * speed) * CD * P.A_front;
+        R lift = R(0.5) * rho * (speed * speed) * CL * P.A_front;
+        R sae = sin(ae), cae = cos(ae);
+        R apar, aperp;
+        if (vy >= R(0)) { apar = lift * sae - drag * cae; aperp = -lift * cae - drag * sae; }
+        else { apar = drag * cae - lift * sae; aperp = -drag * sae - lift * cae; }
+        R sth = sin(th), cth = cos(th);
+        R aero_x = apar * cth + aperp * sth;
+        R aero_y = apar * sth - aperp * cth;
+        R aero_m = aperp * d_cp_cg;
+
+        R T_full = P.T_e + (P.p_e - patm) * P.A_e;
+        R qS = q * P.S_gf;
+        R Ca = grid_fin_ca<R>(P, lds + L::kCaX, lds + L::kCaY, mach);
+        R cfp, cfperp, cm, mdot_dt, md_info, thr_info;
+        if constexpr (PHASE == 0) {
+            // force_moment_decomposer_landing_burn_throttle_only (:340-400); ACS with zero
+            // deflection: F_perp = M = 0 exactly, F_par = qS * (Ca * (2 + 1 + 1))
+            R acs_par = qS * (Ca * R(4));
+            if (a.act_f64) {
+                R u0 = (R)ud[0];
+                R nnt = (u0 + R(1)) / R(2);
+                R thr = nnt * P.one_minus_nom_pt + P.nom_pt;
+                R tg = T_full * (R)P.n_eng * thr;
+                R md = P.Te_over_vex * (tg / T_full);
+                cfp = tg + acs_par; mdot_dt = md * dt; md_info = md; thr_info = thr;
+            } else {
+                float nnt = (uf[0] + 1.0f) / 2.0f;
+                float thr = nnt * P.f_one_minus_nom_pt + P.f_nom_pt;
+                float tg = (float)(T_full * (R)P.n_eng) * thr;
+                float md = P.f_Te_over_vex * (tg / (float)T_full);
+                cfp = (R)tg + acs_par; mdot_dt = (R)(md * P.f_dt_pt); md_info = (R)md; thr_info = (R)thr;
+            }
+            cfperp = R(0); cm = R(0);
+        } else {
+            // force_moment_decomposer_landing_burn_gimballed (:168-269)
+            R gdeg_cmd, tpar, tperp, tmz, cmd_l, cmd_r, md, thr;
+            R gd;
+            if (a.act_f64) {
+                R grad = (R)ud[0] * P.max_gimbal_rad;
+                gdeg_cmd = grad * Cst<R>::rad2deg;
+                gd = gprev + dt_act * ((-gprev + gdeg_cmd) / R(1));
+                gd = gd < -P.max_gimbal_deg ? -P.max_gimbal_deg : gd;
+                gd = gd > P.max_gimbal_deg ? P.max_gimbal_deg : gd;
+                R grad2 = gd * Cst<R>::deg2rad;
+                R nnt = ((R)ud[1] + R(1)) / R(2);
+                thr = nnt * P.one_minus_nom_lb + P.nom_lb;
+                R tg = T_full * (R)(P.n_eng + 2) * thr;
+                R cg = cos(grad2), sg = sin(grad2);
+                tpar = tg * cg; tperp = -tg * sg; tmz = -tg * sg * d_thrust;
+                R tot = sqrt(tpar * tpar + tperp * tperp);
+                md = P.Te_over_vex * (tot / T_full);
+                gdeg_out = grad2 * Cst<R>::rad2deg;
+                cmd_l = (R)ud[2] * P.max_defl_rad * R(60); cmd_r = (R)ud[3] * P.max_defl_rad * R(60);
+                mdot_dt = md * dt;
+            } else {
+                float grad = uf[0] * P.f_max_gimbal_rad;
+                gdeg_cmd = (R)grad * Cst<R>::rad2deg;
+                gd = gprev + dt_act * ((-gprev + gdeg_cmd) / R(1));
+                gd = gd < -P.max_gimbal_deg ? -P.max_gimbal_deg : gd;
+                gd = gd > P.max_gimbal_deg ? P.max_gimbal_deg : gd;
+                R grad2 = gd * Cst<R>::deg2rad;
+                float nnt = (uf[1] + 1.0f) / 2.0f;
+                float thrf = nnt * P.f_one_minus_nom_lb + P.f_nom_lb;
+                float tg = (float)(T_full * (R)(P.n_eng + 2)) * thrf;
+                float cg = (float)cos(grad2), sg = (float)sin(grad2);
+                float fpar = tg * cg, fperp = (-tg) * sg, fm = (-tg) * sg;
+                float tot = sqrtf(fpar * fpar + fperp * fperp);
+                float mdf = P.f_Te_over_vex * (tot / (float)T_full);
+                tpar = (R)fpar; tperp = (R)fperp; tmz = (R)fm * d_thrust;   // d_thrust_cg is float64
+                md = (R)mdf; thr = (R)thrf;
+                gdeg_out = grad2 * Cst<R>::rad2deg;
+                float dlf = uf[2] * P.f_max_defl_rad, drf = uf[3] * P.f_max_defl_rad;
+                cmd_l = (R)(dlf * 60.0f); cmd_r = (R)(drf * 60.0f);
+                mdot_dt = (R)(mdf * P.f_dt_lb);
+            }
+            // ACS (acs_model.py:13-87)
+            R dcl = cmd_l * Cst<R>::deg2rad, dcr = cmd_r * Cst<R>::deg2rad;
+            R dl = dlprev + dt_act * ((-dlprev + dcl) / R(0.5));
+            R dr = drprev + dt_act * ((-drprev + dcr) / R(0.5));
+            R cna = grid_fin_cn_alpha<R>(P, lds + L::kCnX, lds + L::kCnY, mach);
+            R CnL = cna * ((ae - dl) * Cst<R>::rad2deg);
+            R CnR = cna * ((ae - dr) * Cst<R>::rad2deg);
+            R cl_ = cos(dl), cr_ = cos(dr), sl_ = sin(dl), sr_ = sin(dr);
+            R f_perp = qS * (CnR * cr_ - CnL * cl_ - Ca * (sl_ - sr_));
+            R f_par = qS * (Ca * (R(2) + cl_ + cr_) - CnL * sl_ + CnR * sr_);
+            R m_z = -(P.d_base_gf - x_cog) * f_perp + P.R_rocket * qS * (Ca * (sr_ - sl_) - CnL * cl_ + CnR * cr_);
+            cfp = tpar + f_par; cfperp = tperp + f_perp; cm = tmz + m_z;
+            dcmdl_out = dcl; dcmdr_out = dcr;
+            md_info = md; thr_info = thr;
+        }
+        // NaN guard (rockets_physics.py:599-607), an elif chain
+        if (isnan(cfp)) { cfp = R(0); nan_hit = true; }
+        else if (isnan(cfperp)) { cfperp = R(0); nan_hit = true; }
+        else if (isnan(cm)) { cm = R(0); nan_hit = true; }
+        R cfx = cfp * cth + cfperp * sth;
+        R cfy = cfp * sth - cfperp * cth;
+        R gr = gravity<R>(P, y);
+        R fx = aero_x + cfx + Fwx, fy = aero_y + cfy + Fwy;
+        R vxd = fx / m, vyd = fy / m - gr;
+        vx += vxd * dt; vy += vyd * dt; x += vx * dt; y += vy * dt;
+        R thdd = (cm + aero_m + Mw) / I;
+        thd += thdd * dt; th += thd * dt;
+        ga = atan2(vy, vx);
+        if (th > Cst<R>::two_pi) th -= Cst<R>::two_pi;
+        if (ga < R(0)) ga = Cst<R>::two_pi + ga;
+        al = th - ga;
+        mp -= mdot_dt; m -= mdot_dt;
+        s[0] = x; s[1] = y; s[2] = vx; s[3] = vy; s[4] = th; s[5] = thd; s[6] = ga; s[7] = al;
+        s[8] = m; s[9] = mp; s[10] = s[10] + dt;
+        if (sub == 3 && a.info) {   // info of the last sub-step (rockets_physics.py:649-702)
+            R vals[PD_N_INFO - 1] = {rho, patm, asnd, mach, q, CL, CD, md_info, x_cog, I, ae, thr_info, ug, vg, gdeg_out};
+#pragma unroll
+            for (int k = 0; k < PD_N_INFO - 1; ++k) a.info[(k < PD_INFO_GLOAD ? k : k + 1) * N + i] = vals[k];
+        }
+    }
+    if (nan_hit) atomicAdd(&a.pend.stats[1], 1ull);
+
+    // ---- g-load window (base_environment.py:136-149)
+    R v = sqrt(s[2] * s[2] + s[3] * s[3]);
+    R vp = a.b.vprev[i];
+    R gl_new = fabs(v - vp) / R(0.1) * R(1) / R(9.81);
+    int glen = a.b.glen[i], ghead = a.b.ghead[i];
+    R w[10];
+#pragma unroll
+    for (int k = 0; k < 10; ++k) w[k] = a.b.gwin[k * N + i];
+    int wslot;
+    if (glen < 10) { wslot = glen; glen += 1; }
+    else { wslot = ghead; ghead = ghead == 9 ? 0 : ghead + 1; }
+#pragma unroll
+    for (int k = 0; k < 10; ++k) w[k] = (k == wslot) ? gl_new : w[k];
+    // Python sum() from the oldest entry: ring order ghead, ghead+1, ... (glen < 10: 0..glen-1)
+    R gsum = R(0);
+    int start = glen < 10 ? 0 : ghead;
+#pragma unroll
+    for (int k = 0; k < 10; ++k) {
+        int idx = start + k; idx = idx >= 10 ? idx - 10 : idx;
+        R vk = w[0];
+#pragma unroll
+        for (int q2 = 1; q2 < 10; ++q2) vk = (idx == q2) ? w[q2] : vk;
+        gsum = (k < glen) ? gsum + vk : gsum;
+    }
+    R gl = gsum / R(10);
+
+    // ---- truncated -> done -> reward (rtd_rl.py:190-336 / rtd_pso.py:172-317)
+    R x = s[0], y = s[1], vx = s[2], vy = s[3], th = s[4], ga = s[6], mp = s[9];
+    R rho, pa_, as_;
+    atmosphere<R>(P, y, rho, pa_, as_);
+    R speed = v;
+    R q = R(0.5) * rho * (speed * speed);
+    int tr = 0, id = 0, dn = 0;
+    R rew = R(0);
+    const R r2 = (R)(2.0 * kDeg2Rad);
+    if constexpr (RTD == 0) {
+        if (y < R(-10)) { tr = 1; id = 1; }
+        else if (mp <= R(0)) { tr = 1; id = 2; }
+        else if (th > Cst<R>::pi + r2) { tr = 1; id = 3; }
+        else if (q > R(65000)) { tr = 1; id = 4; }
+        else if (gl > R(6)) { tr = 1; id = 5; }
+        else if (vy > R(0)) { tr = 1; id = 6; }
+        else if (vx > R(0.01)) { tr = 1; id = 7; }
+        dn = (y > R(0) && y < R(1) && speed < R(5));
+        R sp = hypot(vx, vy);
+        R qr = R(0.5) * rho * (sp * sp);
+        if (qr > R(60000)) { R e = (qr - R(60000)) / (R(65000) - R(60000)); R e2 = e * e; rew -= R(1) * (e2 > R(1) ? R(1) : e2); }
+        if (gl > R(5.5)) { R e = (gl - R(5.5)) / (R(6) - R(5.5)); R e2 = e * e; rew -= R(1) * (e2 > R(1) ? R(1) : e2); }
+        R prog = (P.y0_rl - y) / P.y0_rl;
+        R wp = (qr <= R(60000) && gl <= R(5.5)) ? R(0.5) : R(0.5) * R(0.1);
+        rew += wp * prog;
+        if (y < R(100)) rew += R(5.5) * (R(1) - fabs(vy) / R(50));
+        if (dn && !tr) rew += R(400) * mp / P.m0_rl;
+        else if (tr && y > R(0)) rew -= R(50) * (fabs(y) / P.y0_rl);
+        else if (tr && y < R(0)) rew -= R(50) * (fabs(vy) / R(10));
+        if (!dn || !(tr && y < R(0))) rew = rew < R(-10) ? R(-10) : (rew > R(10) ? R(10) : rew);
+    } else {
+        if constexpr (PHASE == 0) {
+            if (y < R(0)) { tr = 1; id = 1; }
+            else if (mp <= R(0)) { tr = 1; id = 2; }
+            else if (th > Cst<R>::pi + r2) { tr = 1; id = 3; }
+            else if (q > R(65000)) { tr = 1; id = 4; }
+            else if (vy > R(0)) { tr = 1; id = 6; }
+            else if (gl > R(6)) { tr = 1; id = 7; }
+            dn = (y > R(0) && y < R(1) && speed < R(5.5));
+            if (tr && y > R(0)) rew = -fabs(y);
+            else if (tr && y < R(0)) rew = R(200) - fabs(speed);
+            else if (dn) rew = mp;
+        } else {
+            R dist = sqrt(x * x + y * y);
+            R over;
+            if (x < R(0) && y < R(0)) over = sqrt(x * x + y * y);
+            else if (x < R(0)) over = -x;
+            else if (y < R(0)) over = -y;
+            else over = R(0);
+            R aeff = (vy < R(0)) ? fabs(ga - th - Cst<R>::pi) : fabs(th - ga);
+            if (over > R(0.5)) { tr = 1; id = 1; }
+            else if (mp <= R(0)) { tr = 1; id = 2; }
+            else if (aeff > (R)(10.0 * kDeg2Rad)) { tr = 1; id = 3; }
+            else if (q > R(65000)) { tr = 1; id = 4; }
+            else if (vy > R(0)) { tr = 1; id = 6; }
+            else if (gl > R(6)) { tr = 1; id = 7; }
+            else if (y > R(1000) && vx > R(0)) { tr = 1; id = 8; }
+            dn = (dist > R(0) && dist < R(1) && speed < R(2.5));
+            if (tr && over < R(0.5)) rew = -fabs(dist);
+            else if (tr) rew = R(200) - fabs(speed);
+            else if (dn) rew = mp;
+        }
+    }
+
+    // ---- outputs
+    if (a.obs) {
+        if constexpr (RTD == 0) {
+            a.obs[i * 2 + 0] = (R(1) - y / P.norm_y) * R(2) - R(1);
+            a.obs[i * 2 + 1] = (R(1) - vy / P.norm_vy) * R(2) - R(1);
+        } else if constexpr (PHASE == 0) {
+            a.obs[i * 2 + 0] = y / P.norm_y; a.obs[i * 2 + 1] = vy / P.norm_vy;
+        } else {
+            a.obs[i * 5 + 0] = x / P.norm_x; a.obs[i * 5 + 1] = y / P.norm_y;
+            a.obs[i * 5 + 2] = vx / P.norm_vx; a.obs[i * 5 + 3] = vy / P.norm_vy;
+            a.obs[i * 5 + 4] = tanh(P.k_theta_pso * (th - Cst<R>::pi / R(2)));
+        }
+    }
+    if (a.reward) a.reward[i] = rew;
+    if (a.reward_sum) a.reward_sum[i] += rew;
+    if (a.done) a.done[i] = (uint8_t)dn;
+    if (a.trunc) a.trunc[i] = (uint8_t)tr;
+    if (a.trunc_id) a.trunc_id[i] = (int8_t)id;
+    if (a.info) a.info[PD_INFO_GLOAD * N + i] = gl;
+
+    if (a.auto_reset && (dn || tr)) {
+        reset_env(a, i, ep + 1, false);
+        a.b.key[i] = ccd.key; a.b.key[N + i] = ccl.key;
+        a.b.slot[i] = ccd.slot; a.b.slot[N + i] = ccl.slot;
+        return;
+    }
+    // ---- state write-back
+#pragma unroll
+    for (int k = 0; k < 11; ++k) a.b.st[k * N + i] = s[k];
+    a.b.vprev[i] = v;
+    a.b.gwin[wslot * N + i] = gl_new;
+    a.b.glen[i] = (uint8_t)glen; a.b.ghead[i] = (uint8_t)ghead;
+    a.b.tid[i] = (int8_t)id;
+    a.b.tstep[i] = ts + 1;
+    a.b.key[i] = ccd.key; a.b.key[N + i] = ccl.key;
+    a.b.slot[i] = ccd.slot; a.b.slot[N + i] = ccl.slot;
+    if constexpr (PHASE == 1) { a.b.act[i] = gdeg_out; a.b.act[N + i] = dcmdl_out; a.b.act[2 * N + i] = dcmdr_out; }
+    if constexpr (WIND) {
+        a.b.wind[i] = fu0; a.b.wind[N + i] = fu1; a.b.wind[2 * N + i] = fv0; a.b.wind[3 * N + i] = fv1;
+    }
+}
+
+// Insert the neighbourhoods solved on device during the last launch (single block; the only
+// writer of the tables, stream-ordered between step launches, so readers never race it).
+template <typename R>
+__global__ void k_insert(Pending pend, unsigned long long* keys_cd, R* pay_cd, int lc_cd,
+                         unsigned long long* keys_cl, R* pay_cl, int lc_cl) {
+    __shared__ int s_slot;
+    unsigned long long cnt = *pend.count;
+    if (cnt == 0) return;
+    if (cnt > (unsigned long long)kPendingCap) cnt = kPendingCap;
+    for (unsigned long long e = 0; e < cnt; ++e) {
+        if (threadIdx.x == 0) {
+            unsigned long long kk = pend.keys[e];
+            int table = (int)(kk >> 63);
+            unsigned long long key = kk & ~(1ull << 63);
+            unsigned long long* keys = table ? keys_cl : keys_cd;
+            int lc = table ? lc_cl : lc_cd;
+            uint32_t mask = (1u << lc) - 1u, h = key_hash(key, lc);
+            int slot = -1;
+            uint32_t used = 0;
+            for (uint32_t p = 0; p <= mask; ++p) {
+                unsigned long long k = keys[h];
+                if (k == key) { slot = -1; break; }
+                if (k == kEmptyKey) { slot = (int)h; break; }
+                h = (h + 1) & mask; ++used;
+            }
+            // keep the load factor <= 1/2
+            if (slot >= 0 && pend.stats[2 + table] * 2 + 2 > (1ull << lc)) slot = -1;
+            if (slot >= 0) { pend.stats[2 + table] += 1; }
+            s_slot = slot >= 0 ? (slot | (table << 30)) : -1;
+            if (slot >= 0) keys[slot] = key;
+        }
+        __syncthreads();
+        int sl = s_slot;
+        if (sl >= 0) {
+            int table = sl >> 30, slot = sl & ((1 << 30) - 1);
+            R* pay = (table ? pay_cl : pay_cd) + (int64_t)slot * kPay;
+            if (threadIdx.x < kPay) pay[threadIdx.x] = (R)pend.pay[e * kPay + threadIdx.x];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) *pend.count = 0;
+}
+
+template <typename R>
+__global__ __launch_bounds__(kBlock) void k_observe(StepArgs<R> a, int obs_kind) {
+    const DevParams<R>& P = *a.P;
+    int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const int64_t N = a.n;
+    if (i >= N) return;
+    R x = a.b.st[i], y = a.b.st[N + i], vx = a.b.st[2 * N + i], vy = a.b.st[3 * N + i], th = a.b.st[4 * N + i];
+    if (obs_kind == 0) {
+        a.obs[i * 2] = (R(1) - y / P.norm_y) * R(2) - R(1);
+        a.obs[i * 2 + 1] = (R(1) - vy / P.norm_vy) * R(2) - R(1);
+    } else if (obs_kind == 1) {
+        a.obs[i * 2] = y / P.norm_y; a.obs[i * 2 + 1] = vy / P.norm_vy;
+    } else {
+        a.obs[i * 5] = x / P.norm_x; a.obs[i * 5 + 1] = y / P.norm_y;
+        a.obs[i * 5 + 2] = vx / P.norm_vx; a.obs[i * 5 + 3] = vy / P.norm_vy;
+        a.obs[i * 5 + 4] = tanh(P.k_theta_pso * (th - Cst<R>::pi / R(2)));
+    }
+}
+
+template <typename R>
+__global__ __launch_bounds__(kBlock) void k_set_sigmas(StepArgs<R> a, const double* sig) {
+    int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= a.n) return;
+    a.b.wind[4 * a.n + i] = (R)sig[i];
+    a.b.wind[5 * a.n + i] = (R)sig[a.n + i];
+}
+
+// ---------------------------------------------------------------- host side
+int log2ceil(int64_t v) { int l = 0; while ((1ll << l) < v) ++l; return l; }
+
+template <typename R> struct Table {
+    int logcap = 0;
+    std::vector<unsigned long long> keys;
+    std::vector<R> pay;
+    int64_t entries = 0;
+};
+
+// brute-force 50-NN key at a query (host), used for the initial cache and key checks
+uint64_t host_knn_key(const pd_aero_table& t, double M, double a) {
+    std::vector<std::pair<double, int>> d;
+    for (int c = 0; c < t.n_cols; ++c)
+        for (int k = 0; k < t.col_len[c]; ++k) {
+            double dm = M - t.mach[t.col_start[c] + k], da = a - t.col_aoa[c];
+            d.push_back({dm * dm + da * da, t.col_start[c] + k});
+        }
+    std::stable_sort(d.begin(), d.end(), [](auto& x, auto& y) { return x.first < y.first; });
+    int lo[kCols], hi[kCols];
+    for (int c = 0; c < kCols; ++c) { lo[c] = 1 << 20; hi[c] = -1; }
+    for (int j = 0; j < kNbr; ++j) {
+        int p = d[j].second, c = 0;
+        while (c + 1 < t.n_cols && p >= t.col_start[c + 1]) ++c;
+        int k = p - t.col_start[c];
+        lo[c] = std::min(lo[c], k); hi[c] = std::max(hi[c], k);
+    }
+    int L[kCols], N[kCols];
+    for (int c = 0; c < kCols; ++c) {
+        if (hi[c] < 0) { L[c] = 0; N[c] = 0; } else { L[c] = lo[c]; N[c] = hi[c] - lo[c] + 1; }
+    }
+    return key_pack(L, N);
+}
+
+template <typename R>
+pd_status build_table(const pd_aero_table& t, const uint64_t* keys, int64_t nk, Table<R>& T) {
+    int64_t cap_need = std::max<int64_t>(4 * std::max<int64_t>(nk, 64), 1024);
+    T.logcap = log2ceil(cap_need);
+    int64_t cap = 1ll << T.logcap;
+    T.keys.assign(cap, kEmptyKey);
+    T.pay.assign(cap * kPay, R(0));
+    std::vector<double> work(kScratch), pay(kPay);
+    double aoa[kCols];
+    for (int c = 0; c < kCols; ++c) aoa[c] = t.col_aoa[c];
+    for (int64_t e = 0; e < nk; ++e) {
+        uint64_t key = keys[e];
+        if (solve_neighbourhood(t.mach, t.coef, t.col_start, aoa, key, work.data(), pay.data()) != 0)
+            return fail(PD_ERR_INVALID, "invalid/singular neighbourhood key in param pack");
+        uint32_t mask = (uint32_t)(cap - 1), h = key_hash(key, T.logcap);
+        while (T.keys[h] != kEmptyKey && T.keys[h] != key) h = (h + 1) & mask;
+        if (T.keys[h] == key) continue;
+        T.keys[h] = key;
+        for (int j = 0; j < kPay; ++j) T.pay[h * kPay + j] = (R)pay[j];
+        ++T.entries;
+    }
+    return PD_OK;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------- the handle
+struct pd_env {
+    pd_config cfg{};
+    int device = 0;
+    int obs_dim = 2, act_dim = 1;
+    size_t rsize = 8;
+    void* dparams = nullptr;
+    std::vector<void*> allocs;
+    // per-env buffers (typed views in the precision of the handle)
+    void* st = nullptr; void* vprev = nullptr; void* gwin = nullptr; void* act = nullptr; void* wind = nullptr;
+    uint8_t *ghead = nullptr, *glen = nullptr, *wprof = nullptr;
+    unsigned long long* key = nullptr; int* slot = nullptr;
+    int8_t* tid = nullptr; uint32_t *epi = nullptr, *tstep = nullptr;
+    Pending pend{};
+    double* scratch = nullptr;
+    unsigned long long *keys_cd = nullptr, *keys_cl = nullptr;
+    void *pay_cd = nullptr, *pay_cl = nullptr;
+    int logcap_cd = 0, logcap_cl = 0;
+    int64_t entries_cd = 0, entries_cl = 0;
+};
+
+namespace {
+
+pd_status dalloc(pd_env* e, void** p, size_t bytes) {
+    if (bytes == 0) bytes = 8;
+    PD_HIP(hipMalloc(p, bytes));
+    e->allocs.push_back(*p);
+    return PD_OK;
+}
+
+template <typename R> StepArgs<R> make_args(pd_env* e) {
+    StepArgs<R> a{};
+    a.P = (const DevParams<R>*)e->dparams;
+    a.b.st = (R*)e->st; a.b.vprev = (R*)e->vprev; a.b.gwin = (R*)e->gwin; a.b.ghead = e->ghead; a.b.glen = e->glen;
+    a.b.act = (R*)e->act; a.b.wind = (R*)e->wind; a.b.wprof = e->wprof; a.b.key = e->key; a.b.slot = e->slot;
+    a.b.tid = e->tid; a.b.epi = e->epi; a.b.tstep = e->tstep;
+    a.pend = e->pend;
+    a.scratch = e->scratch;
+    a.n = e->cfg.n_envs;
+    a.env_offset = e->cfg.env_offset;
+    a.seed_lo = (uint32_t)e->cfg.seed; a.seed_hi = (uint32_t)(e->cfg.seed >> 32);
+    a.act_f64 = e->cfg.action_f64;
+    a.auto_reset = e->cfg.auto_reset;
+    a.stochastic = e->cfg.stochastic_wind;
+    a.fixed_prof = e->cfg.wind_percentile >= 50 ? e->cfg.wind_percentile - 50 : -1;
+    a.use_tilt = e->cfg.tilt_sigma_rad > 0.0;
+    a.tilt_sigma = e->cfg.tilt_sigma_rad;
+    return a;
+}
+
+template <typename R> void fill_params(const pd_params* p, const pd_config* c, DevParams<R>& D) {
+    std::memset(&D, 0, sizeof(D));
+    D.T_e = (R)p->thrust_per_engine; D.p_e = (R)p->nozzle_exit_pressure; D.A_e = (R)p->nozzle_exit_area;
+    D.v_ex = (R)p->v_exhaust; D.S_gf = (R)p->grid_fin_area; D.d_base_gf = (R)p->d_base_grid_fin;
+    D.R_rocket = (R)p->rocket_radius; D.A_front = (R)p->frontal_area; D.m_prop0 = (R)p->m_prop0;
+    D.C_gust_x = (R)p->C_gust_x; D.C_gust_y = (R)p->C_gust_y; D.n_eng = p->n_engines_gimballed;
+    // compile_physics constants (rockets_physics.py:808-835, 914-916), in binary64 as Python does
+    double nom_pt = (0 * 0.4) / (double)p->n_engines_gimballed;
+    double nom_lb = (3 * 0.4) / (double)p->n_engines_gimballed;
+    double te_vex = p->thrust_per_engine / p->v_exhaust;
+    double mg = 5.0 * kDeg2Rad, md = 20.0 * kDeg2Rad;
+    D.f_Te_over_vex = (float)te_vex; D.f_one_minus_nom_pt = (float)(1 - nom_pt); D.f_nom_pt = (float)nom_pt;
+    D.f_one_minus_nom_lb = (float)(1 - nom_lb); D.f_nom_lb = (float)nom_lb; D.f_dt_pt = (float)0.025;
+    D.f_dt_lb = (float)0.1; D.f_max_gimbal_rad = (float)mg; D.f_max_defl_rad = (float)md;
+    D.Te_over_vex = (R)te_vex; D.one_minus_nom_pt = (R)(1 - nom_pt); D.nom_pt = (R)nom_pt;
+    D.one_minus_nom_lb = (R)(1 - nom_lb); D.nom_lb = (R)nom_lb; D.max_gimbal_rad = (R)mg;
+    D.max_gimbal_deg = (R)(mg * kRad2Deg); D.max_defl_rad = (R)md;
+    D.h_ox = (R)p->h_ox; D.h_f = (R)p->h_f; D.m_ox = (R)p->m_ox; D.m_f = (R)p->m_f; D.h_lower = (R)p->h_lower;
+    D.m_dry = (R)p->m_dry; D.x_dry = (R)p->x_dry; D.I_dry = (R)p->I_dry; D.engine_height = (R)p->engine_height;
+    D.cop = (R)p->cop;
+    for (int k = 0; k < 9; ++k) {
+        double b = p->isa_beta[k], Tb = p->isa_Tb[k];
+        D.isa_Hb[k] = (R)p->isa_Hb[k]; D.isa_Tb[k] = (R)Tb; D.isa_beta[k] = (R)b; D.isa_pb[k] = (R)p->isa_pb[k];
+        D.isa_bt[k] = (R)(b / Tb);
+        D.isa_ex[k] = (R)(b != 0.0 ? -p->isa_g0 / (b * p->isa_R) : 0.0);
+        D.isa_iso[k] = (R)(-p->isa_g0 / (p->isa_R * Tb));
+    }
+    D.isa_r = (R)p->isa_r; D.isa_R = (R)p->isa_R; D.isa_kappaR = (R)(p->isa_kappa * p->isa_R);
+    D.isa_alt_max = (R)p->isa_alt_max; D.grav_R = (R)p->grav_R; D.grav_g0 = (R)p->grav_g0;
+    for (int cc = 0; cc < kCols; ++cc) {
+        D.cd_start[cc] = p->cd.col_start[cc]; D.cd_len[cc] = p->cd.col_len[cc]; D.cd_aoa[cc] = (R)p->cd.col_aoa[cc];
+        D.cl_start[cc] = p->cl.col_start[cc]; D.cl_len[cc] = p->cl.col_len[cc]; D.cl_aoa[cc] = (R)p->cl.col_aoa[cc];
+        D.cd_aoa_d[cc] = p->cd.col_aoa[cc]; D.cl_aoa_d[cc] = p->cl.col_aoa[cc];
+    }
+    D.cd_n = p->cd.n_pts; D.cl_n = p->cl.n_pts;
+    for (int k = 0; k < 256; ++k) {
+        D.cd_mach[k] = (R)p->cd.mach[k]; D.cl_mach[k] = (R)p->cl.mach[k];
+        D.cd_mach_d[k] = p->cd.mach[k]; D.cl_mach_d[k] = p->cl.mach[k];
+        D.cd_coef_d[k] = p->cd.coef[k]; D.cl_coef_d[k] = p->cl.coef[k];
+    }
+    D.ca_n = p->ca_n; D.cn_n = p->cn_n;
+    for (int k = 0; k < 64; ++k) {
+        D.ca_x[k] = (R)p->ca_x[k]; D.ca_y[k] = (R)p->ca_y[k]; D.cn_x[k] = (R)p->cn_x[k]; D.cn_y[k] = (R)p->cn_y[k];
+    }
+    D.ca_min_mach = (R)p->ca_min_mach; D.ca_min_val = (R)p->ca_min_val;
+    D.cn_min_mach = (R)p->cn_min_mach; D.cn_max_mach = (R)p->cn_max_mach; D.cn_min_val = (R)p->cn_min_val;
+    D.cn_max_val = (R)p->cn_max_val; D.cn_slope = (R)p->cn_slope;
+    for (int w = 0; w < 50; ++w) {
+        D.wind_n[w] = p->wind_n[w];
+        for (int k = 0; k < 16; ++k) { D.wind_alt_km[w][k] = (R)p->wind_alt_km[w][k]; D.wind_speed[w][k] = (R)p->wind_speed[w][k]; }
+    }
+    for (int k = 0; k < 4; ++k) { D.vk_Ad_u[k] = (R)p->vk_Ad_u[k]; D.vk_Ad_v[k] = (R)p->vk_Ad_v[k]; }
+    for (int k = 0; k < 2; ++k) { D.vk_Bd_u[k] = (R)p->vk_Bd_u[k]; D.vk_Bd_v[k] = (R)p->vk_Bd_v[k]; }
+    D.vk_y_threshold = (R)p->vk_y_threshold;
+    D.sigma_u_lo = p->sigma_u_lo; D.sigma_u_hi = p->sigma_u_hi; D.sigma_v_lo = p->sigma_v_lo; D.sigma_v_hi = p->sigma_v_hi;
+    for (int k = 0; k < 11; ++k) { D.state0[k] = (R)p->state0[k]; D.state0_d[k] = p->state0[k]; }
+    D.norm_y = (R)p->norm_y; D.norm_vy = (R)p->norm_vy; D.norm_x = (R)p->norm_x; D.norm_vx = (R)p->norm_vx;
+    D.k_theta_pso = (R)(std::atanh(0.75) / (25.0 * kDeg2Rad));
+    D.y0_rl = (R)p->state0[1]; D.m0_rl = (R)p->state0[8];
+    (void)c;
+}
+
+pd_status validate(const pd_params* p, const pd_config* c) {
+    if (!p || !c) return fail(PD_ERR_INVALID, "null params/config");
+    if (c->n_envs <= 0 || c->n_envs > (int64_t)1 << 31) return fail(PD_ERR_INVALID, "n_envs out of range");
+    if (c->phase != PD_PHASE_PURE_THROTTLE && c->phase != PD_PHASE_LANDING_BURN) return fail(PD_ERR_INVALID, "bad phase");
+    if (c->rtd != PD_RTD_RL && c->rtd != PD_RTD_PSO) return fail(PD_ERR_INVALID, "bad rtd");
+    if (c->rtd == PD_RTD_RL && c->phase != PD_PHASE_PURE_THROTTLE)
+        return fail(PD_ERR_UNSUPPORTED, "RL reward is implemented for landing_burn_pure_throttle (the SAC driver's phase)");
+    if (c->precision != PD_F64 && c->precision != PD_F32) return fail(PD_ERR_INVALID, "bad precision");
+    if (c->action_f64 && c->precision != PD_F64) return fail(PD_ERR_INVALID, "f64 actions need PD_F64");
+    if (c->enable_wind && !(c->wind_percentile == -1 || (c->wind_percentile >= 50 && c->wind_percentile <= 99)))
+        return fail(PD_ERR_INVALID, "wind_percentile must be 50..99 or -1");
+    const pd_aero_table* ts[2] = {&p->cd, &p->cl};
+    for (auto t : ts) {
+        if (t->n_cols != kCols || t->n_pts < kNbr || t->n_pts > PD_MAX_PTS) return fail(PD_ERR_INVALID, "aero table shape");
+        int s = 0;
+        for (int k = 0; k < kCols; ++k) {
+            if (t->col_start[k] != s || t->col_len[k] < 1 || t->col_len[k] >= (1 << kKeyLoBits))
+                return fail(PD_ERR_INVALID, "aero column layout");
+            s += t->col_len[k];
+        }
+        if (s != t->n_pts) return fail(PD_ERR_INVALID, "aero column count");
+    }
+    if (p->ca_n < 2 || p->ca_n > PD_MAX_TAB || p->cn_n < 2 || p->cn_n > PD_MAX_TAB) return fail(PD_ERR_INVALID, "grid fin tables");
+    for (int w = 0; w < PD_N_WIND_PROFILES; ++w)
+        if (c->enable_wind && (p->wind_n[w] < 1 || p->wind_n[w] > PD_MAX_WIND)) return fail(PD_ERR_INVALID, "wind profile");
+    return PD_OK;
+}
+
+template <typename R> pd_status create_impl(const pd_params* p, const pd_config* c, pd_env* e) {
+    const int64_t N = c->n_envs;
+    DevParams<R> D;
+    fill_params<R>(p, c, D);
+    Table<R> tcd, tcl;
+    pd_status st;
+    if ((st = build_table<R>(p->cd, p->keys_cd, p->n_keys_cd, tcd)) != PD_OK) return st;
+    if ((st = build_table<R>(p->cl, p->keys_cl, p->n_keys_cl, tcl)) != PD_OK) return st;
+    e->logcap_cd = tcd.logcap; e->logcap_cl = tcl.logcap;
+    e->entries_cd = tcd.entries; e->entries_cl = tcl.entries;
+    if ((st = dalloc(e, (void**)&e->keys_cd, tcd.keys.size() * 8)) || (st = dalloc(e, &e->pay_cd, tcd.pay.size() * sizeof(R))) ||
+        (st = dalloc(e, (void**)&e->keys_cl, tcl.keys.size() * 8)) || (st = dalloc(e, &e->pay_cl, tcl.pay.size() * sizeof(R))))
+        return st;
+    PD_HIP(hipMemcpy(e->keys_cd, tcd.keys.data(), tcd.keys.size() * 8, hipMemcpyHostToDevice));
+    PD_HIP(hipMemcpy(e->pay_cd, tcd.pay.data(), tcd.pay.size() * sizeof(R), hipMemcpyHostToDevice));
+    PD_HIP(hipMemcpy(e->keys_cl, tcl.keys.data(), tcl.keys.size() * 8, hipMemcpyHostToDevice));
+    PD_HIP(hipMemcpy(e->pay_cl, tcl.pay.data(), tcl.pay.size() * sizeof(R), hipMemcpyHostToDevice));
+    D.keys_cd = e->keys_cd; D.keys_cl = e->keys_cl; D.pay_cd = (const R*)e->pay_cd; D.pay_cl = (const R*)e->pay_cl;
+    D.logcap_cd = tcd.logcap; D.logcap_cl = tcl.logcap;
+    // initial neighbourhood caches: the 50-NN at the initial state's clamped query points
+    // (any valid 50-set works; the in-kernel swap search repairs it)
+    D.init_key_cd = host_knn_key(p->cd, 3.0, 0.0);
+    D.init_key_cl = host_knn_key(p->cl, 3.0, 10.0);
+    if ((st = dalloc(e, &e->dparams, sizeof(D)))) return st;
+    PD_HIP(hipMemcpy(e->dparams, &D, sizeof(D), hipMemcpyHostToDevice));
+    size_t R_ = sizeof(R);
+    if ((st = dalloc(e, &e->st, 11 * N * R_)) || (st = dalloc(e, &e->vprev, N * R_)) ||
+        (st = dalloc(e, &e->gwin, 10 * N * R_)) || (st = dalloc(e, &e->act, 3 * N * R_)) ||
+        (st = dalloc(e, &e->wind, 6 * N * R_)) || (st = dalloc(e, (void**)&e->ghead, N)) ||
+        (st = dalloc(e, (void**)&e->glen, N)) || (st = dalloc(e, (void**)&e->wprof, N)) ||
+        (st = dalloc(e, (void**)&e->key, 2 * N * 8)) || (st = dalloc(e, (void**)&e->slot, 2 * N * 4)) ||
+        (st = dalloc(e, (void**)&e->tid, N)) || (st = dalloc(e, (void**)&e->epi, N * 4)) ||
+        (st = dalloc(e, (void**)&e->tstep, N * 4)))
+        return st;
+    PD_HIP(hipMemset(e->gwin, 0, 10 * N * R_));
+    PD_HIP(hipMemset(e->epi, 0xff, N * 4));   // first reset -> episode 0
+    int64_t n_waves = (N + 63) / 64;
+    if ((st = dalloc(e, (void**)&e->scratch, (size_t)n_waves * kScratch * 8))) return st;
+    if ((st = dalloc(e, (void**)&e->pend.count, 8)) || (st = dalloc(e, (void**)&e->pend.keys, kPendingCap * 8)) ||
+        (st = dalloc(e, (void**)&e->pend.pay, (size_t)kPendingCap * kPay * 8)) || (st = dalloc(e, (void**)&e->pend.stats, 4 * 8)))
+        return st;
+    PD_HIP(hipMemset(e->pend.count, 0, 8));
+    unsigned long long stats0[4] = {0, 0, (unsigned long long)tcd.entries, (unsigned long long)tcl.entries};
+    PD_HIP(hipMemcpy(e->pend.stats, stats0, sizeof(stats0), hipMemcpyHostToDevice));
+    StepArgs<R> a = make_args<R>(e);
+    unsigned grid = (unsigned)((N + kBlock - 1) / kBlock);
+    hipLaunchKernelGGL(k_reset<R>, dim3(grid), dim3(kBlock), 0, 0, a, (const uint8_t*)nullptr);
+    PD_HIP(hipGetLastError());
+    PD_HIP(hipDeviceSynchronize());
+    return PD_OK;
+}
+
+template <typename R, int PH, int RT, bool W> void launch_step(const StepArgs<R>& a, hipStream_t s) {
+    unsigned grid = (unsigned)((a.n + kBlock - 1) / kBlock);
+    hipLaunchKernelGGL((k_step<R, PH, RT, W>), dim3(grid), dim3(kBlock), 0, s, a);
+}
+
+template <typename R> void dispatch_step(const pd_env* e, const StepArgs<R>& a, hipStream_t s) {
+    int ph = e->cfg.phase, rt = e->cfg.rtd;
+    bool w = e->cfg.enable_wind != 0;
+    if (ph == 0 && rt == 0) { if (w) launch_step<R, 0, 0, true>(a, s); else launch_step<R, 0, 0, false>(a, s); }
+    else if (ph == 0 && rt == 1) { if (w) launch_step<R, 0, 1, true>(a, s); else launch_step<R, 0, 1, false>(a, s); }
+    else { if (w) launch_step<R, 1, 1, true>(a, s); else launch_step<R, 1, 1, false>(a, s); }
+}
+
+template <typename R> void launch_insert(pd_env* e, hipStream_t s) {
+    hipLaunchKernelGGL(k_insert<R>, dim3(1), dim3(kPay), 0, s, e->pend, e->keys_cd, (R*)e->pay_cd, e->logcap_cd,
+                       e->keys_cl, (R*)e->pay_cl, e->logcap_cl);
+}
+
+template <typename R>
+pd_status step_impl(pd_env* e, const void* actions, void* obs, void* reward, uint8_t* done, uint8_t* trunc,
+                    int8_t* tid, const double* noise, void* info, void* reward_sum, hipStream_t s) {
+    StepArgs<R> a = make_args<R>(e);
+    a.actions = actions; a.obs = (R*)obs; a.reward = (R*)reward; a.done = done; a.trunc = trunc; a.trunc_id = tid;
+    a.noise = noise; a.info = (R*)info; a.reward_sum = (R*)reward_sum;
+    dispatch_step<R>(e, a, s);
+    PD_HIP(hipGetLastError());
+    return PD_OK;
+}
+
+}  // namespace
+
+// ================================================================ C ABI
+extern "C" {
+
+int pd_abi_version(void) { return PD_ABI_VERSION; }
+size_t pd_sizeof_params(void) { return sizeof(pd_params); }
+size_t pd_sizeof_config(void) { return sizeof(pd_config); }
+const char* pd_last_error(void) { return g_err.c_str(); }
+
+int pd_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+pd_status pd_create(const pd_params* params, const pd_config* cfg, pd_env** out) {
+    if (!out) return fail(PD_ERR_INVALID, "out is null");
+    *out = nullptr;
+    pd_status st = validate(params, cfg);
+    if (st != PD_OK) return st;
+    int ndev = pd_device_count();
+    if (ndev <= 0) return fail(PD_ERR_HIP, "no HIP device visible");
+    if (cfg->device < 0 || cfg->device >= ndev) return fail(PD_ERR_INVALID, "device ordinal out of range");
+    PD_HIP(hipSetDevice(cfg->device));
+    pd_env* e = new pd_env();
+    e->cfg = *cfg;
+    e->device = cfg->device;
+    e->act_dim = cfg->phase == PD_PHASE_PURE_THROTTLE ? 1 : 4;
+    e->obs_dim = (cfg->phase == PD_PHASE_LANDING_BURN) ? 5 : 2;
+    e->rsize = cfg->precision == PD_F64 ? 8 : 4;
+    st = cfg->precision == PD_F64 ? create_impl<double>(params, cfg, e) : create_impl<float>(params, cfg, e);
+    if (st != PD_OK) { pd_destroy(e); return st; }
+    *out = e;
+    return PD_OK;
+}
+
+pd_status pd_destroy(pd_env* e) {
+    if (!e) return PD_OK;
+    (void)hipSetDevice(e->device);
+    for (void* p : e->allocs) (void)hipFree(p);
+    delete e;
+    return PD_OK;
+}
+
+pd_status pd_reset(pd_env* e, const uint8_t* mask, void* obs, void* stream) {
+    if (!e) return fail(PD_ERR_INVALID, "null env");
+    PD_HIP(hipSetDevice(e->device));
+    hipStream_t s = (hipStream_t)stream;
+    unsigned grid = (unsigned)((e->cfg.n_envs + kBlock - 1) / kBlock);
+    if (e->rsize == 8) hipLaunchKernelGGL(k_reset<double>, dim3(grid), dim3(kBlock), 0, s, make_args<double>(e), mask);
+    else hipLaunchKernelGGL(k_reset<float>, dim3(grid), dim3(kBlock), 0, s, make_args<float>(e), mask);
+    PD_HIP(hipGetLastError());
+    if (obs) return pd_observe(e, obs, stream);
+    return PD_OK;
+}
+
+pd_status pd_step(pd_env* e, const void* actions, void* obs, void* reward, uint8_t* done, uint8_t* truncated,
+                  int8_t* trunc_id, const double* noise, void* info, void* stream) {
+    if (!e || !actions) return fail(PD_ERR_INVALID, "null env/actions");
+    PD_HIP(hipSetDevice(e->device));
+    if (e->rsize == 8)
+        return step_impl<double>(e, actions, obs, reward, done, truncated, trunc_id, noise, info, nullptr, (hipStream_t)stream);
+    return step_impl<float>(e, actions, obs, reward, done, truncated, trunc_id, noise, info, nullptr, (hipStream_t)stream);
+}
+
+pd_status pd_rollout(pd_env* e, const void* actions, int32_t n_steps, void* reward_sum, void* stream) {
+    if (!e || !actions || n_steps < 0) return fail(PD_ERR_INVALID, "bad rollout args");
+    PD_HIP(hipSetDevice(e->device));
+    size_t stride = (size_t)e->cfg.n_envs * e->act_dim * (e->cfg.action_f64 ? 8 : 4);
+    for (int32_t t = 0; t < n_steps; ++t) {
+        const void* at = (const char*)actions + stride * t;
+        pd_status st = e->rsize == 8
+            ? step_impl<double>(e, at, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, reward_sum, (hipStream_t)stream)
+            : step_impl<float>(e, at, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, reward_sum, (hipStream_t)stream);
+        if (st != PD_OK) return st;
+        if ((t & 15) == 15 || t + 1 == n_steps) { if ((st = pd_flush_misses(e, stream)) != PD_OK) return st; }
+    }
+    return PD_OK;
+}
+
+pd_status pd_flush_misses(pd_env* e, void* stream) {
+    if (!e) return fail(PD_ERR_INVALID, "null env");
+    PD_HIP(hipSetDevice(e->device));
+    if (e->rsize == 8) launch_insert<double>(e, (hipStream_t)stream);
+    else launch_insert<float>(e, (hipStream_t)stream);
+    PD_HIP(hipGetLastError());
+    return PD_OK;
+}
+
+pd_status pd_observe(pd_env* e, void* obs, void* stream) {
+    if (!e || !obs) return fail(PD_ERR_INVALID, "null env/obs");
+    PD_HIP(hipSetDevice(e->device));
+    int kind = e->cfg.rtd == PD_RTD_RL ? 0 : (e->cfg.phase == PD_PHASE_PURE_THROTTLE ? 1 : 2);
+    unsigned grid = (unsigned)((e->cfg.n_envs + kBlock - 1) / kBlock);
+    hipStream_t s = (hipStream_t)stream;
+    if (e->rsize == 8) { auto a = make_args<double>(e); a.obs = (double*)obs; hipLaunchKernelGGL(k_observe<double>, dim3(grid), dim3(kBlock), 0, s, a, kind); }
+    else { auto a = make_args<float>(e); a.obs = (float*)obs; hipLaunchKernelGGL(k_observe<float>, dim3(grid), dim3(kBlock), 0, s, a, kind); }
+    PD_HIP(hipGetLastError());
+    return PD_OK;
+}
+
+pd_status pd_get_state(pd_env* e, void* state, void* stream) {
+    if (!e || !state) return fail(PD_ERR_INVALID, "null env/state");
+    PD_HIP(hipSetDevice(e->device));
+    PD_HIP(hipMemcpyAsync(state, e->st, 11 * e->cfg.n_envs * e->rsize, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+    return PD_OK;
+}
+
+pd_status pd_set_state(pd_env* e, const void* state, void* stream) {
+    if (!e || !state) return fail(PD_ERR_INVALID, "null env/state");
+    PD_HIP(hipSetDevice(e->device));
+    PD_HIP(hipMemcpyAsync(e->st, state, 11 * e->cfg.n_envs * e->rsize, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+    return PD_OK;
+}
+
+pd_status pd_get_actuators(pd_env* e, void* act, void* stream) {
+    if (!e || !act) return fail(PD_ERR_INVALID, "null env/act");
+    PD_HIP(hipSetDevice(e->device));
+    PD_HIP(hipMemcpyAsync(act, e->act, 3 * e->cfg.n_envs * e->rsize, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+    return PD_OK;
+}
+
+pd_status pd_set_actuators(pd_env* e, const void* act, void* stream) {
+    if (!e || !act) return fail(PD_ERR_INVALID, "null env/act");
+    PD_HIP(hipSetDevice(e->device));
+    PD_HIP(hipMemcpyAsync(e->act, act, 3 * e->cfg.n_envs * e->rsize, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+    return PD_OK;
+}
+
+pd_status pd_set_wind_sigmas(pd_env* e, const double* sig, void* stream) {
+    if (!e || !sig) return fail(PD_ERR_INVALID, "null env/sig");
+    PD_HIP(hipSetDevice(e->device));
+    unsigned grid = (unsigned)((e->cfg.n_envs + kBlock - 1) / kBlock);
+    hipStream_t s = (hipStream_t)stream;
+    if (e->rsize == 8) hipLaunchKernelGGL(k_set_sigmas<double>, dim3(grid), dim3(kBlock), 0, s, make_args<double>(e), sig);
+    else hipLaunchKernelGGL(k_set_sigmas<float>, dim3(grid), dim3(kBlock), 0, s, make_args<float>(e), sig);
+    PD_HIP(hipGetLastError());
+    return PD_OK;
+}
+
+pd_status pd_counters(pd_env* e, int64_t* misses, int64_t* ecd, int64_t* ecl, int64_t* nans) {
+    if (!e) return fail(PD_ERR_INVALID, "null env");
+    PD_HIP(hipSetDevice(e->device));
+    unsigned long long st[4];
+    PD_HIP(hipMemcpy(st, e->pend.stats, sizeof(st), hipMemcpyDeviceToHost));
+    if (misses) *misses = (int64_t)st[0];
+    if (nans) *nans = (int64_t)st[1];
+    if (ecd) *ecd = (int64_t)st[2];
+    if (ecl) *ecl = (int64_t)st[3];
+    return PD_OK;
+}
+
+int pd_obs_dim(const pd_env* e) { return e ? e->obs_dim : 0; }
+int pd_action_dim(const pd_env* e) { return e ? e->act_dim : 0; }
+
+}  // extern "C"

@@ -1,0 +1,122 @@
+"""ctypes binding of libpdenv.so (include/pdenv.h).
+
+The product path: every call goes to the HIP library.  There is no CPU fallback; loading
+fails loudly when the library is missing or when no HIP device is visible.
+"""
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libpdenv.so")
+
+D, I32, I64, U64 = C.c_double, C.c_int32, C.c_int64, C.c_uint64
+MAX_PTS, MAX_COLS, MAX_TAB, MAX_WIND, N_PROF = 256, 5, 64, 16, 50
+N_STATE, N_INFO = 11, 16
+
+PD_OK, PD_ERR_INVALID, PD_ERR_HIP, PD_ERR_NOMEM, PD_ERR_UNSUPPORTED = range(5)
+PURE_THROTTLE, LANDING_BURN = 0, 1
+RTD_RL, RTD_PSO = 0, 1
+F64, F32 = 0, 1
+
+INFO_FIELDS = ["air_density", "atmospheric_pressure", "speed_of_sound", "mach_number",
+               "dynamic_pressure", "CL", "CD", "mass_flow", "x_cog", "inertia",
+               "alpha_effective", "throttle", "g_load_1_sec_window", "ug", "vg", "gimbal_angle_deg"]
+
+
+class PdAeroTable(C.Structure):
+    _fields_ = [("n_cols", I32), ("n_pts", I32), ("col_aoa", D * MAX_COLS),
+                ("col_start", I32 * MAX_COLS), ("col_len", I32 * MAX_COLS),
+                ("mach", D * MAX_PTS), ("coef", D * MAX_PTS)]
+
+
+class PdParams(C.Structure):
+    _fields_ = [
+        ("thrust_per_engine", D), ("nozzle_exit_pressure", D), ("nozzle_exit_area", D), ("v_exhaust", D),
+        ("n_engines_gimballed", I32), ("pad0", I32),
+        ("grid_fin_area", D), ("d_base_grid_fin", D), ("rocket_radius", D), ("frontal_area", D),
+        ("m_prop0", D), ("C_gust_x", D), ("C_gust_y", D),
+        ("h_ox", D), ("h_f", D), ("m_ox", D), ("m_f", D), ("h_lower", D), ("m_dry", D), ("x_dry", D),
+        ("I_dry", D), ("engine_height", D), ("cop", D),
+        ("isa_Hb", D * 9), ("isa_Tb", D * 9), ("isa_beta", D * 9), ("isa_pb", D * 9),
+        ("isa_g0", D), ("isa_R", D), ("isa_kappa", D), ("isa_r", D), ("isa_alt_max", D),
+        ("grav_R", D), ("grav_g0", D),
+        ("cd", PdAeroTable), ("cl", PdAeroTable),
+        ("ca_n", I32), ("cn_n", I32),
+        ("ca_x", D * MAX_TAB), ("ca_y", D * MAX_TAB), ("ca_min_mach", D), ("ca_min_val", D),
+        ("cn_x", D * MAX_TAB), ("cn_y", D * MAX_TAB), ("cn_min_mach", D), ("cn_max_mach", D),
+        ("cn_min_val", D), ("cn_max_val", D), ("cn_slope", D),
+        ("wind_n", I32 * N_PROF),
+        ("wind_alt_km", (D * MAX_WIND) * N_PROF), ("wind_speed", (D * MAX_WIND) * N_PROF),
+        ("vk_Ad_u", D * 4), ("vk_Bd_u", D * 2), ("vk_Ad_v", D * 4), ("vk_Bd_v", D * 2), ("vk_y_threshold", D),
+        ("sigma_u_lo", D), ("sigma_u_hi", D), ("sigma_v_lo", D), ("sigma_v_hi", D),
+        ("state0", D * N_STATE), ("norm_y", D), ("norm_vy", D), ("norm_x", D), ("norm_vx", D),
+        ("keys_cd", C.POINTER(U64)), ("n_keys_cd", I64),
+        ("keys_cl", C.POINTER(U64)), ("n_keys_cl", I64),
+    ]
+
+
+class PdConfig(C.Structure):
+    _fields_ = [("n_envs", I64), ("device", I32), ("phase", I32), ("rtd", I32), ("precision", I32),
+                ("seed", U64), ("env_offset", U64), ("enable_wind", I32), ("stochastic_wind", I32),
+                ("wind_percentile", I32), ("auto_reset", I32), ("tilt_sigma_rad", D),
+                ("action_f64", I32), ("pad", I32)]
+
+
+EXPORTS = ["pd_abi_version", "pd_sizeof_params", "pd_sizeof_config", "pd_last_error", "pd_device_count", "pd_create", "pd_destroy", "pd_reset",
+           "pd_step", "pd_rollout", "pd_flush_misses", "pd_observe", "pd_get_state", "pd_set_state", "pd_get_actuators",
+           "pd_set_actuators", "pd_set_wind_sigmas", "pd_counters", "pd_obs_dim", "pd_action_dim"]
+
+_lib = None
+
+
+class PdError(RuntimeError):
+    pass
+
+
+def load(path=None):
+    """Load libpdenv.so (built in-tree by pdenv.build)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    path = path or LIB_PATH
+    if not os.path.exists(path):
+        raise PdError(f"libpdenv.so not found at {path}: run __graft_entry__.build() "
+                      "(the HIP extension is required; there is no CPU fallback)")
+    L = C.CDLL(path)
+    vp, P = C.c_void_p, C.POINTER
+    L.pd_abi_version.restype = C.c_int
+    L.pd_last_error.restype = C.c_char_p
+    L.pd_device_count.restype = C.c_int
+    L.pd_create.argtypes = [P(PdParams), P(PdConfig), P(vp)]
+    L.pd_destroy.argtypes = [vp]
+    L.pd_reset.argtypes = [vp, vp, vp, vp]
+    L.pd_step.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
+    L.pd_rollout.argtypes = [vp, vp, I32, vp, vp]
+    L.pd_observe.argtypes = [vp, vp, vp]
+    L.pd_flush_misses.argtypes = [vp, vp]
+    L.pd_get_state.argtypes = [vp, vp, vp]
+    L.pd_set_state.argtypes = [vp, vp, vp]
+    L.pd_get_actuators.argtypes = [vp, vp, vp]
+    L.pd_set_actuators.argtypes = [vp, vp, vp]
+    L.pd_set_wind_sigmas.argtypes = [vp, vp, vp]
+    L.pd_counters.argtypes = [vp, P(I64), P(I64), P(I64), P(I64)]
+    L.pd_obs_dim.argtypes = [vp]; L.pd_obs_dim.restype = C.c_int
+    L.pd_action_dim.argtypes = [vp]; L.pd_action_dim.restype = C.c_int
+    for name in ("pd_create", "pd_destroy", "pd_reset", "pd_step", "pd_rollout", "pd_flush_misses", "pd_observe",
+                 "pd_get_state", "pd_set_state", "pd_get_actuators", "pd_set_actuators",
+                 "pd_set_wind_sigmas", "pd_counters"):
+        getattr(L, name).restype = C.c_int
+    L.pd_sizeof_params.restype = C.c_size_t
+    L.pd_sizeof_config.restype = C.c_size_t
+    if L.pd_abi_version() != 1:
+        raise PdError("libpdenv ABI version mismatch")
+    if L.pd_sizeof_params() != C.sizeof(PdParams) or L.pd_sizeof_config() != C.sizeof(PdConfig):
+        raise PdError("pd_params/pd_config layout mismatch between ctypes and libpdenv.so")
+    _lib = L
+    return L
+
+
+def check(status):
+    if status != PD_OK:
+        msg = load().pd_last_error().decode(errors="replace")
+        raise PdError(f"libpdenv error {status}: {msg}")

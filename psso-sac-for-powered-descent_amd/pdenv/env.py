@@ -1,0 +1,164 @@
+"""Batched powered-descent environment over HBM-resident torch tensors.
+
+`PoweredDescentEnv(n_envs, ...)` is the vectorised counterpart of the reference's
+`rocket_environment_pre_wrap` (src/envs/base_environment.py:12-154) for the two phases the
+north-star drivers use: 'landing_burn_pure_throttle' (SAC driver) and 'landing_burn' (PSO
+driver).  All compute runs in libpdenv.so (HIP kernels); torch only provides device memory
+and the current stream.
+"""
+import ctypes as C
+
+import torch
+
+from . import _lib as L
+from .params import Params
+
+PHASES = {"landing_burn_pure_throttle": L.PURE_THROTTLE, "landing_burn": L.LANDING_BURN}
+MODES = {"rl": L.RTD_RL, "pso": L.RTD_PSO}
+
+
+def _stream(device):
+    return C.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def _ptr(t):
+    return None if t is None else C.c_void_p(t.data_ptr())
+
+
+class PoweredDescentEnv:
+    def __init__(self, n_envs, flight_phase="landing_burn_pure_throttle", mode="rl", precision="f64",
+                 device=0, enable_wind=False, stochastic_wind=False, wind_percentile=50,
+                 auto_reset=False, tilt_sigma_rad=0.0, seed=0, env_offset=0, action_f64=False,
+                 params=None):
+        if flight_phase not in PHASES:
+            raise ValueError(f"flight_phase must be one of {list(PHASES)} (got {flight_phase!r})")
+        if mode not in MODES:
+            raise ValueError(f"mode must be 'rl' or 'pso' (got {mode!r})")
+        self.lib = L.load()
+        if self.lib.pd_device_count() <= 0 or not torch.cuda.is_available():
+            raise L.PdError("no HIP device visible: the powered-descent env runs on MI355X only")
+        self.device = torch.device("cuda", device) if isinstance(device, int) else torch.device(device)
+        self.n = int(n_envs)
+        self.flight_phase, self.mode = flight_phase, mode
+        self.dtype = torch.float64 if precision == "f64" else torch.float32
+        self.params = params or Params()
+        cfg = L.PdConfig()
+        cfg.n_envs = self.n
+        cfg.device = self.device.index or 0
+        cfg.phase = PHASES[flight_phase]
+        cfg.rtd = MODES[mode]
+        cfg.precision = L.F64 if precision == "f64" else L.F32
+        cfg.seed = int(seed)
+        cfg.env_offset = int(env_offset)
+        cfg.enable_wind = int(bool(enable_wind))
+        cfg.stochastic_wind = int(bool(stochastic_wind))
+        cfg.wind_percentile = -1 if wind_percentile is None else int(wind_percentile)
+        cfg.auto_reset = int(bool(auto_reset))
+        cfg.tilt_sigma_rad = float(tilt_sigma_rad)
+        cfg.action_f64 = int(bool(action_f64))
+        self.cfg = cfg
+        handle = C.c_void_p()
+        with torch.cuda.device(self.device):
+            L.check(self.lib.pd_create(C.byref(self.params.struct), C.byref(cfg), C.byref(handle)))
+        self.h = handle
+        self.obs_dim = self.lib.pd_obs_dim(self.h)
+        self.action_dim = self.lib.pd_action_dim(self.h)
+        self.action_dtype = torch.float64 if action_f64 else torch.float32
+        kw = dict(device=self.device)
+        self._obs = torch.empty(self.n, self.obs_dim, dtype=self.dtype, **kw)
+        self._rew = torch.empty(self.n, dtype=self.dtype, **kw)
+        self._done = torch.empty(self.n, dtype=torch.uint8, **kw)
+        self._trunc = torch.empty(self.n, dtype=torch.uint8, **kw)
+        self._tid = torch.empty(self.n, dtype=torch.int8, **kw)
+        self._steps = 0
+        self.flush_every = 1
+
+    # ------------------------------------------------------------------ reference surface
+    def reset(self, mask=None):
+        """base_environment.py:80-97 for all envs (or a bool/uint8 mask [N]); returns obs [N, O]."""
+        m = None
+        if mask is not None:
+            m = mask.to(device=self.device, dtype=torch.uint8).contiguous()
+        L.check(self.lib.pd_reset(self.h, _ptr(m), _ptr(self._obs), _stream(self.device)))
+        return self._obs.clone()
+
+    def step(self, actions, noise=None, info=False):
+        """base_environment.py:99-154 for every env.  actions: [N, A] float32 (float64 with
+        action_f64).  Returns (obs, reward, done, truncated, extras) as device tensors; with
+        auto_reset the obs is the post-step (terminal) observation."""
+        a = actions.to(device=self.device, dtype=self.action_dtype).reshape(self.n, self.action_dim).contiguous()
+        nz = None
+        if noise is not None:
+            nz = noise.to(device=self.device, dtype=torch.float64).reshape(self.n, 8).contiguous()
+        inf = torch.empty(L.N_INFO, self.n, dtype=self.dtype, device=self.device) if info else None
+        L.check(self.lib.pd_step(self.h, _ptr(a), _ptr(self._obs), _ptr(self._rew), _ptr(self._done),
+                                 _ptr(self._trunc), _ptr(self._tid), _ptr(nz), _ptr(inf), _stream(self.device)))
+        self._steps += 1
+        if self._steps % self.flush_every == 0:
+            self.flush()
+        extras = {"trunc_id": self._tid.clone()}
+        if info:
+            extras.update({k: inf[j] for j, k in enumerate(L.INFO_FIELDS)})
+        return self._obs.clone(), self._rew.clone(), self._done.bool(), self._trunc.bool(), extras
+
+    def rollout(self, actions, reward_sum=None):
+        """T step launches over device-resident actions [T, N, A]; returns summed rewards [N]."""
+        a = actions.to(device=self.device, dtype=self.action_dtype).contiguous()
+        T = a.shape[0]
+        rs = reward_sum if reward_sum is not None else torch.zeros(self.n, dtype=self.dtype, device=self.device)
+        L.check(self.lib.pd_rollout(self.h, _ptr(a), int(T), _ptr(rs), _stream(self.device)))
+        return rs
+
+    def flush(self):
+        """Insert device-solved aero neighbourhoods into the tables (pd_flush_misses)."""
+        L.check(self.lib.pd_flush_misses(self.h, _stream(self.device)))
+
+    def observe(self):
+        L.check(self.lib.pd_observe(self.h, _ptr(self._obs), _stream(self.device)))
+        return self._obs.clone()
+
+    @property
+    def state(self):
+        """[N, 11] x y vx vy theta theta_dot gamma alpha mass mass_propellant time."""
+        soa = torch.empty(11, self.n, dtype=self.dtype, device=self.device)
+        L.check(self.lib.pd_get_state(self.h, _ptr(soa), _stream(self.device)))
+        return soa.t().contiguous()
+
+    def set_state(self, state):
+        soa = state.to(device=self.device, dtype=self.dtype).reshape(self.n, 11).t().contiguous()
+        L.check(self.lib.pd_set_state(self.h, _ptr(soa), _stream(self.device)))
+        torch.cuda.current_stream(self.device).synchronize()
+
+    @property
+    def actuators(self):
+        soa = torch.empty(3, self.n, dtype=self.dtype, device=self.device)
+        L.check(self.lib.pd_get_actuators(self.h, _ptr(soa), _stream(self.device)))
+        return soa.t().contiguous()
+
+    def set_actuators(self, act):
+        soa = act.to(device=self.device, dtype=self.dtype).reshape(self.n, 3).t().contiguous()
+        L.check(self.lib.pd_set_actuators(self.h, _ptr(soa), _stream(self.device)))
+        torch.cuda.current_stream(self.device).synchronize()
+
+    def set_wind_sigmas(self, sigma_u, sigma_v):
+        sig = torch.stack([torch.as_tensor(sigma_u, dtype=torch.float64).expand(self.n),
+                           torch.as_tensor(sigma_v, dtype=torch.float64).expand(self.n)]).to(self.device).contiguous()
+        L.check(self.lib.pd_set_wind_sigmas(self.h, _ptr(sig), _stream(self.device)))
+        torch.cuda.current_stream(self.device).synchronize()
+
+    def counters(self):
+        v = [L.I64() for _ in range(4)]
+        L.check(self.lib.pd_counters(self.h, *[C.byref(x) for x in v]))
+        return {"rbf_misses": v[0].value, "table_entries_cd": v[1].value, "table_entries_cl": v[2].value,
+                "nan_events": v[3].value}
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.pd_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

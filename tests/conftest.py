@@ -25,3 +25,13 @@ def oracle_mod():
     import oracle
     oracle.build()
     return oracle
+
+
+def pytest_sessionstart(session):
+    # keep the in-tree HIP library current (no-op when up to date; hipcc cross-compiles)
+    try:
+        from pdenv import build as b
+        if not b.up_to_date():
+            b.build()
+    except Exception as e:  # the ABI tests report the failure precisely
+        print(f"[conftest] libpdenv build skipped: {e}")

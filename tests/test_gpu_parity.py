@@ -1,0 +1,197 @@
+"""GPU parity: the HIP kernels (through the C ABI) against the reference's recorded runs,
+the fixtures made by importing the reference, and the CPU oracle.
+
+Tolerances (fp64 handle): teacher-forced single env-step <= 1e-10 relative per channel
+(theta_dot: 1e-8 with a 1e-3 rad/s floor); full episodes: TOL_EPISODE (fraction of
+per-channel range; the attitude channels are chaotic).  fp32 handle:
+teacher-forced <= 1e-4 relative on non-attitude channels.
+"""
+import numpy as np
+import pytest
+
+from conftest import golden
+
+pytestmark = pytest.mark.gpu
+
+ST = ["x", "y", "vx", "vy", "theta", "theta_dot", "gamma", "alpha", "mass", "mass_propellant", "time"]
+TOL_EPISODE = np.array([1e-6, 1e-9, 1e-6, 1e-9, 1e-6, 1e-6, 1e-6, 1e-6, 1e-12, 1e-12, 1e-12])
+
+
+@pytest.fixture(scope="module")
+def pd():
+    import torch
+    import pdenv
+    assert torch.cuda.is_available(), "GPU tests need a HIP device"
+    return pdenv
+
+
+def make(pd, n, phase="landing_burn_pure_throttle", mode="rl", **kw):
+    return pd.PoweredDescentEnv(n, flight_phase=phase, mode=mode, **kw)
+
+
+@pytest.mark.parametrize("tag,phase", [("pt", "landing_burn_pure_throttle"), ("lb", "landing_burn")])
+def test_teacher_forced_step_vs_reference(pd, tag, phase):
+    import torch
+    d = golden("ref_teacher_forced.npz")
+    S0, A = d[f"{tag}_state_in"], d[f"{tag}_action"]
+    env = make(pd, len(S0), phase, mode="pso")
+    env.set_state(torch.tensor(S0))
+    if phase == "landing_burn":
+        env.set_actuators(torch.tensor(d[f"{tag}_prevs"]))
+    obs, r, dn, tr, ex = env.step(torch.tensor(A), info=True)
+    S = env.state.cpu().numpy()
+    ref = d[f"{tag}_state_out"]
+    err = np.abs(S - ref) / np.maximum(np.abs(ref), 1e-3)
+    tol = np.full(11, 1e-10); tol[5] = 1e-8
+    assert (err.max(0) < tol).all(), dict(zip(ST, err.max(0)))
+    names = list(d["info_names"])
+    md = ex["mass_flow"].cpu().numpy()
+    assert np.array_equal(md, d[f"{tag}_info"][:, names.index("mass_flow")]), "float32 mass-flow island"
+    cd = ex["CD"].cpu().numpy(); cl = ex["CL"].cpu().numpy()
+    assert np.abs(cd - d[f"{tag}_info"][:, names.index("CD")]).max() < 1e-11
+    assert np.abs(cl - d[f"{tag}_info"][:, names.index("CL")]).max() < 1e-10
+
+
+def test_reference_trajectory_config1(pd):
+    """Config c1: the classical controller's u0 as f64 [[u0]] from the nominal initial state."""
+    import torch
+    d = golden("recorded_reference_trajectory.npz")
+    env = make(pd, 1, mode="pso", action_f64=True)
+    got, last = [], None
+    for u in d["u0"]:
+        obs, r, dn, tr, ex = env.step(torch.tensor([[u]], dtype=torch.float64))
+        got.append(env.state.cpu().numpy()[0])
+        last = (float(r[0]), bool(dn[0]), bool(tr[0]))
+    got = np.array(got)
+    err = np.abs(got - d["state"]).max(0) / np.ptp(d["state"], 0)
+    tol = np.full(11, 1e-8); tol[5] = 1e-6
+    assert (err < tol).all(), dict(zip(ST, err))
+    assert last[1] and not last[2] and last[0] == pytest.approx(474318.950426, rel=1e-9)
+
+
+EPISODES = [("rl_land", "landing_burn_pure_throttle", "rl"), ("rl_rand0", "landing_burn_pure_throttle", "rl"),
+            ("rl_rand1", "landing_burn_pure_throttle", "rl"), ("rl_hi", "landing_burn_pure_throttle", "rl"),
+            ("pso_pt_land", "landing_burn_pure_throttle", "pso"), ("pso_pt_rand", "landing_burn_pure_throttle", "pso"),
+            ("pso_lb_rand0", "landing_burn", "pso"), ("pso_lb_rand1", "landing_burn", "pso")]
+
+
+@pytest.mark.parametrize("name,phase,mode", EPISODES)
+def test_episode_vs_reference(pd, name, phase, mode):
+    """Whole episodes with float32 actions, as the SAC / PSO wrappers feed them."""
+    import torch
+    d = golden("ref_episodes.npz")
+    acts = d[f"{name}_actions"]
+    T = len(acts)
+    env = make(pd, 1, phase, mode=mode)
+    S, R, DN, TR, TID, OBS = [], [], [], [], [], []
+    at = torch.tensor(acts, dtype=torch.float32).cuda()
+    for t in range(T):
+        obs, r, dn, tr, ex = env.step(at[t:t + 1])
+        S.append(env.state); R.append(r); DN.append(dn); TR.append(tr); TID.append(ex["trunc_id"]); OBS.append(obs)
+    S = torch.cat(S).cpu().numpy(); R = torch.cat(R).cpu().numpy()
+    DN = torch.cat(DN).cpu().numpy(); TR = torch.cat(TR).cpu().numpy(); TID = torch.cat(TID).cpu().numpy()
+    OBS = torch.cat(OBS).cpu().numpy()
+    rs = d[f"{name}_state"]
+    err = np.abs(S - rs).max(0) / (np.ptp(rs, 0) + 1e-12)
+    tol = TOL_EPISODE if phase == "landing_burn_pure_throttle" else np.maximum(TOL_EPISODE, 1e-6 * (TOL_EPISODE > 1e-12))
+    assert (err < tol).all(), dict(zip(ST, err))
+    assert np.abs(R - d[f"{name}_reward"]).max() <= 1e-9 * max(1.0, np.abs(d[f"{name}_reward"]).max())
+    assert list(DN.astype(bool)) == list(d[f"{name}_done"])
+    assert list(TR.astype(bool)) == list(d[f"{name}_trunc"])
+    assert TID[-1] == d[f"{name}_trunc_id"][-1]
+    ref_obs = d[f"{name}_obs"]
+    if mode == "rl":
+        OBS = OBS.astype(np.float32).astype(np.float64)
+    assert np.abs(OBS - ref_obs).max() < 1e-6
+
+
+def test_batched_random_vs_oracle(pd, oracle_mod):
+    """4096 envs (config c2 size), random float32 actions, 40 steps: every env against the
+    scalar oracle on a sampled subset, and batch-invariance (env i does not depend on N)."""
+    import torch
+    rng = np.random.default_rng(5)
+    N, T = 4096, 40
+    A = rng.uniform(-1, 1, (T, N, 1)).astype(np.float32)
+    env = make(pd, N, mode="rl")
+    at = torch.tensor(A).cuda()
+    rews = []
+    for t in range(T):
+        obs, r, dn, tr, ex = env.step(at[t])
+        rews.append(r.cpu().numpy())
+    S = env.state.cpu().numpy()
+    rews = np.array(rews)
+    for i in rng.choice(N, 16, replace=False):
+        o = oracle_mod.Oracle(phase=0, rtd=0)
+        rr = []
+        for t in range(T):
+            s, r, dn_, tr_, tid, ob, info = o.step(A[t, i], f32=True)
+            rr.append(r)
+        err = np.abs(o.state - S[i]) / (np.abs(o.state) + 1e-3)
+        assert err.max() < 1e-8, (i, dict(zip(ST, err)))
+        assert np.abs(np.array(rr) - rews[:, i]).max() < 1e-9
+
+
+def test_auto_reset_and_full_size_properties(pd):
+    """65 536 envs (config c3 size): auto-reset keeps every env in a valid episode; time
+    advances by exactly 0.1 s per step; mass never increases; counters sane."""
+    import torch
+    N = 65536
+    env = make(pd, N, mode="rl", auto_reset=True, seed=3)
+    g = torch.Generator(device="cuda").manual_seed(0)
+    s0 = env.state
+    done_total = 0
+    for t in range(60):
+        a = torch.rand(N, 1, device="cuda", generator=g) * 2 - 1
+        prev = env.state
+        obs, r, dn, tr, ex = env.step(a)
+        cur = env.state
+        ended = (dn | tr)
+        done_total += int(ended.sum())
+        live = ~ended
+        dt = (cur[live, 10] - prev[live, 10]).cpu().numpy()
+        assert np.allclose(dt, 0.1, rtol=0, atol=1e-9)
+        assert bool((cur[live, 9] <= prev[live, 9]).all())
+        if ended.any():
+            assert torch.equal(cur[ended], s0[ended])
+    assert done_total > 0
+    c = env.counters()
+    assert c["nan_events"] == 0
+
+
+def test_wind_injected_noise_vs_oracle(pd, oracle_mod):
+    """Stochastic wind with the same injected normals (slotted per sub-step) on both sides.
+    The oracle's own reference parity on the reference's recorded noise stream is
+    tests/test_oracle_golden.py::test_wind_episode_injected_noise."""
+    import torch
+    d = golden("ref_episodes.npz")
+    acts = d["rl_land_actions"][:500]
+    rng = np.random.default_rng(17)
+    noise = rng.standard_normal((len(acts), 8))
+    su, sv = 1.3, 1.7
+    env = make(pd, 1, mode="rl", enable_wind=True, stochastic_wind=True, wind_percentile=50)
+    env.set_wind_sigmas(su, sv)
+    o = oracle_mod.Oracle(phase=0, rtd=0, wind=True, stochastic=True, sigma_u=su, sigma_v=sv)
+    o.E.noise_slotted = 1
+    for t, a in enumerate(acts):
+        obs, r, dn, tr, ex = env.step(torch.tensor(a[None]), noise=torch.tensor(noise[t][None]))
+        s_o, r_o, dn_o, tr_o, tid, ob, info = o.step(a, f32=True, noise=noise[t])
+        if dn_o or tr_o:
+            break
+    s = env.state.cpu().numpy()[0]
+    err = np.abs(s - s_o) / (np.abs(s_o) + 1e-3)
+    assert err.max() < 1e-8, dict(zip(ST, err))
+
+
+def test_f32_teacher_forced(pd):
+    """fp32 handle: one step from recorded states vs the reference (fp32 tolerance)."""
+    import torch
+    d = golden("ref_teacher_forced.npz")
+    S0, A = d["pt_state_in"], d["pt_action"]
+    env = make(pd, len(S0), mode="pso", precision="f32")
+    env.set_state(torch.tensor(S0))
+    env.step(torch.tensor(A))
+    S = env.state.double().cpu().numpy()
+    ref = d["pt_state_out"]
+    err = np.abs(S - ref) / np.maximum(np.abs(ref), 1.0)
+    keep = [1, 3, 8, 9, 10]   # y, vy, m, m_prop, t
+    assert err[:, keep].max() < 1e-5, dict(zip([ST[k] for k in keep], err[:, keep].max(0)))

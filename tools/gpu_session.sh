@@ -1,0 +1,29 @@
+#!/bin/bash
+# One GPU session: parity tests, smoke, bench, rocprof kernel trace.  Every GPU step has its
+# own time limit; a crash/timeout/abort stops the session (no further GPU work).
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+stage() {  # name, seconds, command...
+  local name=$1 secs=$2; shift 2
+  echo "=== $name ($(date +%T))"
+  timeout -k 10 "$secs" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "    rc=$rc"; tail -n 5 "gpurun_out/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
+  return 0
+}
+STAGES=${STAGES:-"tests smoke bench prof"}
+for s in $STAGES; do
+  case $s in
+    tests) stage gpu_tests 900 python -m pytest tests/ -m gpu -x -q ;;
+    testsall) stage gpu_tests 900 python -m pytest tests/ -m gpu -q ;;
+    smoke) stage smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) stage bench 600 python bench.py ;;
+    bench32) stage bench32 600 python bench.py --precision f32 ;;
+    prof) stage prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- python3 bench.py --steps 100 --warmup 10 --cpu-baseline 0 --secondary 0 ;;
+    prof32) stage prof32 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof32 -o run -- python3 bench.py --steps 100 --warmup 10 --cpu-baseline 0 --secondary 0 --precision f32 ;;
+    pmc) stage pmc 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/pmc_fetch -o run -- python3 bench.py --steps 20 --warmup 5 --cpu-baseline 0 --secondary 0 ;;
+  esac
+done
+echo "=== done"
