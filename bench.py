@@ -72,7 +72,7 @@ def main():
         g = torch.Generator(device=env.device).manual_seed(42 + rank)
         acts = (torch.rand(T, n, env.action_dim, generator=g, device=env.device) * 2 - 1).contiguous()
         for t in range(args.warmup):
-            env.step(acts[t])
+            env.step_raw(acts[t])
         torch.cuda.synchronize()
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
         if dist:
@@ -81,7 +81,7 @@ def main():
         t0 = time.perf_counter()
         for k in range(args.steps):
             ev[k][0].record()
-            env.step(acts[args.warmup + k])
+            env.step_raw(acts[args.warmup + k])
             ev[k][1].record()
         torch.cuda.synchronize()
         if dist:

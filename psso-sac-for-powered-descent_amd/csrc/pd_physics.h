@@ -19,6 +19,8 @@ template <> struct Cst<float> {
     static constexpr float inf = __builtin_huge_valf();
 };
 
+constexpr int kLineMax = 96;   // breakpoints per clamped query line
+
 // Device parameter block (one per handle, in HBM, read with uniform scalar loads).
 template <typename R> struct DevParams {
     // sizing
@@ -62,6 +64,19 @@ template <typename R> struct DevParams {
     const R* pay_cl;
     int logcap_cd, logcap_cl;
     unsigned long long init_key_cd, init_key_cl;
+    // neighbourhood intervals along the four clamped query lines (C_D at +-radians(10) "deg",
+    // C_L at +-10): breakpoints in Mach, and the key/slot of each interval
+    R line_a[4];
+    int line_nbp[4];
+    // 2-D candidate grids over the interior query domain (Mach x AoA-abscissa), one per table:
+    // the key/slot of the 50-NN set at each cell centre
+    int grid_nm[2], grid_na[2];
+    R grid_a0[2], grid_inv_da[2], grid_inv_dm[2];
+    const unsigned long long* grid_key[2];
+    const int* grid_slot[2];
+    R line_bp[4][kLineMax];
+    int line_slot[4][kLineMax + 1];
+    unsigned long long line_key[4][kLineMax + 1];
 };
 
 // ---------------------------------------------------------------- atmosphere
@@ -163,20 +178,13 @@ __device__ __forceinline__ R d2_at(const R* mach, int start, int i, R M, R dz) {
 }
 
 template <typename R>
-__device__ __forceinline__ void knn_windows(const R* smach, const int* start, const int* n,
-                                            const R* aoa, R M, R a, int lo[kCols], int len[kCols]) {
+__device__ __forceinline__ int knn_windows(const R* smach, const int* start, const int* n,
+                                           const R* aoa, R M, R a, int lo[kCols], int len[kCols]) {
     R dz[kCols];
-    int p[kCols];
 #pragma unroll
-    for (int c = 0; c < kCols; ++c) {
-        R da = a - aoa[c];
-        dz[c] = da * da;
-        // insertion point of M (used for empty columns)
-        int l = 0, h = n[c];
-        while (l < h) { int mid = (l + h) >> 1; if (smach[start[c] + mid] < M) l = mid + 1; else h = mid; }
-        p[c] = l;
-    }
-    for (int it = 0; it < 256; ++it) {
+    for (int c = 0; c < kCols; ++c) { R da = a - aoa[c]; dz[c] = da * da; }
+    int it = 0;
+    for (; it < 256; ++it) {
         R maxin = R(-1); int maxc = -1, maxi = 0;
         R minex = Cst<R>::inf; int minc = -1, mini = 0;
 #pragma unroll
@@ -189,9 +197,17 @@ __device__ __forceinline__ void knn_windows(const R* smach, const int* start, co
                 if (da1 > maxin) { maxin = da1; maxc = c; maxi = l1; }
                 if (l0 > 0) { R d = d2_at(smach, start[c], l0 - 1, M, dz[c]); if (d < minex) { minex = d; minc = c; mini = l0 - 1; } }
                 if (l1 + 1 < n[c]) { R d = d2_at(smach, start[c], l1 + 1, M, dz[c]); if (d < minex) { minex = d; minc = c; mini = l1 + 1; } }
-            } else {
-                if (p[c] > 0) { R d = d2_at(smach, start[c], p[c] - 1, M, dz[c]); if (d < minex) { minex = d; minc = c; mini = p[c] - 1; } }
-                if (p[c] < n[c]) { R d = d2_at(smach, start[c], p[c], M, dz[c]); if (d < minex) { minex = d; minc = c; mini = p[c]; } }
+            }
+        }
+        // empty columns: every point is at distance >= dz[c]; only columns that could hold a
+        // point closer than the worst included one need their nearest point (binary search)
+#pragma unroll
+        for (int c = 0; c < kCols; ++c) {
+            if (len[c] == 0 && dz[c] < maxin) {
+                int l = 0, h = n[c];
+                while (l < h) { int mid = (l + h) >> 1; if (smach[start[c] + mid] < M) l = mid + 1; else h = mid; }
+                if (l > 0) { R d = d2_at(smach, start[c], l - 1, M, dz[c]); if (d < minex) { minex = d; minc = c; mini = l - 1; } }
+                if (l < n[c]) { R d = d2_at(smach, start[c], l, M, dz[c]); if (d < minex) { minex = d; minc = c; mini = l; } }
             }
         }
         if (!(maxin > minex)) break;          // also exits on NaN queries
@@ -212,6 +228,7 @@ __device__ __forceinline__ void knn_windows(const R* smach, const int* start, co
             }
         }
     }
+    return it;
 }
 
 }  // namespace pd

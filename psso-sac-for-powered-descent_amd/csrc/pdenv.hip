@@ -10,6 +10,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -122,28 +123,110 @@ __global__ __launch_bounds__(kBlock) void k_reset(StepArgs<R> a, const uint8_t* 
     reset_env(a, i, ep, true);
 }
 
+// Opaque copy of a uniform pointer: loads through it cannot be hoisted above this point.
+// The step kernel re-launders its parameter block per sub-step, so that the ~150 uniform
+// parameters are re-read (scalar loads, cheap) instead of being kept live in registers
+// across the whole kernel (which cost >200 VGPRs and occupancy).
+template <typename T> __device__ __forceinline__ const T* launder(const T* p) {
+    uint64_t v = (uint64_t)p;
+    uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+    uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    asm volatile("" : "+s"(lo), "+s"(hi));
+    return (const T*)(((uint64_t)hi << 32) | lo);
+}
+
 // ---------------------------------------------------------------- RBF lookup + evaluation
+// Lanes-per-env (LPE) decomposition: with LPE = 1 one lane evaluates both tables; with
+// LPE = 2 lane role 0 owns C_D and role 1 owns C_L; with LPE = 4/8 each table is owned by a
+// pair/quad of lanes that split its 50-term thin-plate sum (terms k = part, part + nparts..).
+template <typename R> struct TabView {
+    const R* smach;
+    const int* start;
+    const int* n;
+    const R* aoa;
+    const unsigned long long* keys;
+    const R* pay;
+    int logcap;
+    int line0;                 // index of this table's first clamped line (0: C_D, 2: C_L)
+    const unsigned long long* grid_key;
+    const int* grid_slot;
+    int grid_nm, grid_na;
+    R grid_a0, grid_inv_da, grid_inv_dm;
+};
+
+// LDS copy of the clamped-line interval tables
+template <typename R> struct LineLds {
+    R bp[4][kLineMax];
+    int slot[4][kLineMax + 1];
+    unsigned long long key[4][kLineMax + 1];
+    R a[4];
+    int nbp[4];
+};
+
+template <typename R>
+__device__ __forceinline__ TabView<R> tab_view(const DevParams<R>& P, const R* s_cd, const R* s_cl, int table) {
+    TabView<R> t;
+    t.smach = table ? s_cl : s_cd;
+    t.start = table ? P.cl_start : P.cd_start;
+    t.n = table ? P.cl_len : P.cd_len;
+    t.aoa = table ? P.cl_aoa : P.cd_aoa;
+    t.keys = table ? P.keys_cl : P.keys_cd;
+    t.pay = table ? P.pay_cl : P.pay_cd;
+    t.logcap = table ? P.logcap_cl : P.logcap_cd;
+    t.line0 = table ? 2 : 0;
+    t.grid_key = P.grid_key[table];
+    t.grid_slot = P.grid_slot[table];
+    t.grid_nm = P.grid_nm[table];
+    t.grid_na = P.grid_na[table];
+    t.grid_a0 = P.grid_a0[table];
+    t.grid_inv_da = P.grid_inv_da[table];
+    t.grid_inv_dm = P.grid_inv_dm[table];
+    return t;
+}
+
 template <typename R>
 __device__ __forceinline__ R rbf_eval(const R* __restrict__ pay, const R* smach, const int* start,
-                                      const R* aoa, const int lo[kCols], const int len[kCols], R M, R a) {
-    R s = R(0);
-    int j = 0;
+                                      const R* aoa, const int lo[kCols], const int len[kCols], R M, R a,
+                                      int part, int nparts) {
+    // phi(r) = r^2 log r = d2 * log(d2) / 2 with d2 = |x - y|^2 (thin_plate_spline, phi(0) = 0).
+    // The 50 terms are flattened over the column windows and evaluated in chunks of 10
+    // independent terms, so that the payload loads (HBM/L2) and LDS reads of a chunk are all
+    // in flight together and the 10 log() chains interleave.
+    const int c1 = len[0], c2 = c1 + len[1], c3 = c2 + len[2], c4 = c3 + len[3];
+    const int b0 = start[0] + lo[0], b1 = start[1] + lo[1] - c1, b2 = start[2] + lo[2] - c2,
+              b3 = start[3] + lo[3] - c3, b4 = start[4] + lo[4] - c4;
+    R dz[kCols];
 #pragma unroll
-    for (int c = 0; c < kCols; ++c) {
-        R da = a - aoa[c];
-        R da2 = da * da;
-        const R* m = smach + start[c] + lo[c];
-        for (int k = 0; k < len[c]; ++k) {
-            R dm = M - m[k];
-            R r = sqrt(dm * dm + da2);
-            R phi = r == R(0) ? R(0) : r * r * log(r);
-            s += phi * pay[j + k];
+    for (int c = 0; c < kCols; ++c) { R da = a - aoa[c]; dz[c] = da * da; }
+    R s0 = R(0), s1 = R(0);
+    constexpr int kChunk = 10;
+#pragma unroll 1
+    for (int j0 = part; j0 < kNbr; j0 += kChunk * nparts) {
+        R mm[kChunk], pp[kChunk], zz[kChunk];
+#pragma unroll
+        for (int u = 0; u < kChunk; ++u) {
+            int j = j0 + u * nparts;
+            bool ok = j < kNbr;
+            int jj = ok ? j : 0;
+            int b = jj < c1 ? b0 : (jj < c2 ? b1 : (jj < c3 ? b2 : (jj < c4 ? b3 : b4)));
+            zz[u] = jj < c1 ? dz[0] : (jj < c2 ? dz[1] : (jj < c3 ? dz[2] : (jj < c4 ? dz[3] : dz[4])));
+            mm[u] = smach[b + jj];
+            pp[u] = ok ? pay[jj] : R(0);
         }
-        j += len[c];
+#pragma unroll
+        for (int u = 0; u < kChunk; ++u) {
+            R dm = M - mm[u];
+            R d2 = dm * dm + zz[u];
+            R f = d2 == R(0) ? R(0) : R(0.5) * d2 * log(d2);
+            if (u & 1) s1 += f * pp[u]; else s0 += f * pp[u];
+        }
     }
-    s += R(1) * pay[kNbr];
-    s += (M - pay[kSys + 0]) / pay[kSys + 2] * pay[kNbr + 1];
-    s += (a - pay[kSys + 1]) / pay[kSys + 3] * pay[kNbr + 2];
+    R s = s0 + s1;
+    if (part == 0) {
+        s += R(1) * pay[kNbr];
+        s += (M - pay[kSys + 0]) / pay[kSys + 2] * pay[kNbr + 1];
+        s += (a - pay[kSys + 1]) / pay[kSys + 3] * pay[kNbr + 2];
+    }
     return s;
 }
 
@@ -173,89 +256,111 @@ __device__ __noinline__ R rbf_miss(const StepArgs<R>& a, int table, unsigned lon
     R* payR = (R*)work;   // the matrix area is free again: payload in the kernel's precision
     for (int j = 0; j < kPay; ++j) payR[j] = (R)pay[j];
     const R* aoaR = table ? P.cl_aoa : P.cd_aoa;
-    return rbf_eval<R>(payR, smach, start, aoaR, lo, len, M, aq);
+    return rbf_eval<R>(payR, smach, start, aoaR, lo, len, M, aq, 0, 1);
 }
 
+// This lane's share of the RBF value of `table` at (M, aq).
+// Candidate neighbourhood: on a clamped query line (the common case: |alpha_eff| > 0.003 rad
+// clamps both tables) the interval table of that line (binary search over <= 96 Mach
+// breakpoints in LDS); elsewhere the env's cached set.  Either way the candidate is VERIFIED
+// (and repaired by the swap search) against the exact distances before it is used.
 template <typename R>
-__device__ __forceinline__ R rbf(const StepArgs<R>& a, int table, const R* smach, RbfCache<R>& cache,
-                                 R M, R aq) {
-    const DevParams<R>& P = *a.P;
-    const int* start = table ? P.cl_start : P.cd_start;
-    const int* n = table ? P.cl_len : P.cd_len;
-    const R* aoa = table ? P.cl_aoa : P.cd_aoa;
+__device__ __forceinline__ R rbf(const StepArgs<R>& a, int table, const TabView<R>& t, const LineLds<R>& ln,
+                                 RbfCache<R>& cache, R M, R aq, int part, int nparts) {
+    unsigned long long ckey = cache.key;
+    int cslot = cache.slot;
+    int li = aq == ln.a[t.line0] ? t.line0 : (aq == ln.a[t.line0 + 1] ? t.line0 + 1 : -1);
+    if (li >= 0 && ln.nbp[li] >= 0) {
+        int l = 0, h = ln.nbp[li];
+        while (l < h) { int mid = (l + h) >> 1; if (ln.bp[li][mid] < M) l = mid + 1; else h = mid; }
+        ckey = ln.key[li][l];
+        cslot = ln.slot[li][l];
+    } else if (t.grid_key) {
+        R fm = M * t.grid_inv_dm, fa = (aq - t.grid_a0) * t.grid_inv_da;
+        int im = fm < R(0) ? 0 : (fm >= R(t.grid_nm) ? t.grid_nm - 1 : (int)fm);
+        int ia = fa < R(0) ? 0 : (fa >= R(t.grid_na) ? t.grid_na - 1 : (int)fa);
+        if (!(fm == fm) || !(fa == fa)) { im = 0; ia = 0; }   // NaN queries
+        int cell = im * t.grid_na + ia;
+        ckey = t.grid_key[cell];
+        cslot = t.grid_slot[cell];
+    }
     int lo[kCols], len[kCols];
-    key_unpack(cache.key, lo, len);
+    key_unpack(ckey, lo, len);
     // keys store lo=0 for empty columns; knn_windows uses insertion points for those
-    knn_windows<R>(smach, start, n, aoa, M, aq, lo, len);
+#ifndef PD_EXP_NOKNN
+#ifdef PD_EXP_COUNT
+    int iters = knn_windows<R>(t.smach, t.start, t.n, t.aoa, M, aq, lo, len);
+    atomicAdd(&a.pend.stats[4], 1ull);
+    atomicAdd(&a.pend.stats[5], (unsigned long long)(li >= 0));
+    atomicAdd(&a.pend.stats[6], (unsigned long long)iters);
+#else
+    knn_windows<R>(t.smach, t.start, t.n, t.aoa, M, aq, lo, len);
+#endif
+#endif
     unsigned long long key = key_pack(lo, len);
-    int slot = cache.slot;
-    if (key != cache.key || slot < 0) {
-        const unsigned long long* keys = table ? P.keys_cl : P.keys_cd;
-        int lc = table ? P.logcap_cl : P.logcap_cd;
-        uint32_t mask = (1u << lc) - 1u;
-        uint32_t h = key_hash(key, lc);
-        slot = -1;
+    int slot = key == ckey ? cslot : -1;
+#ifdef PD_EXP_COUNT
+    atomicAdd(&a.pend.stats[7], (unsigned long long)(slot < 0));
+#endif
+    if (slot < 0) {
+        uint32_t mask = (1u << t.logcap) - 1u;
+        uint32_t h = key_hash(key, t.logcap);
         for (uint32_t probe = 0; probe <= mask; ++probe) {
-            unsigned long long k = keys[h];
+            unsigned long long k = t.keys[h];
             if (k == key) { slot = (int)h; break; }
             if (k == kEmptyKey) break;
             h = (h + 1) & mask;
         }
-        cache.key = key;
-        cache.slot = slot;
     }
+    cache.key = key;
+    cache.slot = slot;
     R val = R(0);
-    if (slot >= 0) {
-        const R* pay = (table ? P.pay_cl : P.pay_cd) + (int64_t)slot * kPay;
-        val = rbf_eval<R>(pay, smach, start, aoa, lo, len, M, aq);
-    }
-    // misses share the wave's scratch: serialise them over the active lanes (the wave runs
-    // divergent branches one after another, so lanes of other call sites never overlap)
-    unsigned long long mm = __ballot(slot < 0);
+    if (slot >= 0) val = rbf_eval<R>(t.pay + (int64_t)slot * kPay, t.smach, t.start, t.aoa, lo, len, M, aq, part, nparts);
+    // misses share the wave's scratch: serialise them over the active part-0 lanes (the wave
+    // runs divergent branches one after another, so lanes of other call sites never overlap);
+    // the part-0 lane returns the whole value, the other parts of the group return 0
+    unsigned long long mm = __ballot(slot < 0 && part == 0);
     while (mm) {
         int leader = __ffsll((long long)mm) - 1;
-        if ((int)__lane_id() == leader) val = rbf_miss<R>(a, table, key, M, aq, smach);
+        if ((int)__lane_id() == leader) val = rbf_miss<R>(a, table, key, M, aq, t.smach);
         mm &= mm - 1;
     }
     return val;
 }
 
-// rocket_CD: CD_func = rocket_CD(M, degrees(alpha)); clamp of the DEGREE value at
+// rocket_CD query: CD_func = rocket_CD(M, degrees(alpha)); clamp of the DEGREE value at
 // +-radians(10) (rockets_physics.py:712, aerodynamic_coefficients.py:105-115)
-template <typename R>
-__device__ __forceinline__ R coef_CD(const StepArgs<R>& a, const R* smach, RbfCache<R>& c, R M, R ae) {
+template <typename R> __device__ __forceinline__ R cd_query(R ae) {
     R aoa = ae * Cst<R>::rad2deg;
     const R r10 = (R)(10.0 * kDeg2Rad);
     if (aoa > r10) aoa = r10;
     else if (aoa < (R)(-10.0 * kDeg2Rad)) aoa = (R)(-10.0 * kDeg2Rad);
-    return rbf<R>(a, 0, smach, c, M, aoa);
+    return aoa;
 }
-// rocket_CL: degrees applied twice (rockets_physics.py:711 + aerodynamic_coefficients.py:117-132);
-// the clamp/sign cases are resolved first so that one inlined RBF serves all of them.
-template <typename R>
-__device__ __forceinline__ R coef_CL(const StepArgs<R>& a, const R* smach, RbfCache<R>& c, R M, R ae) {
+// rocket_CL query: degrees applied twice (rockets_physics.py:711 + aerodynamic_coefficients.py:117-132)
+// returns the RBF abscissa, the sign to apply, and whether C_L is exactly 0
+template <typename R> __device__ __forceinline__ R cl_query(R ae, R& sgn, bool& zero) {
     R aq = (ae * Cst<R>::rad2deg) * Cst<R>::rad2deg;
-    R sgn = R(1);
-    bool zero = false;
+    sgn = R(1);
+    zero = false;
     if (aq > R(10)) aq = R(10);
     else if (aq < R(-10)) aq = R(-10);
     else if (fabs(aq) < R(1e-6)) zero = true;
     else if (aq < R(0)) { aq = fabs(aq); sgn = R(-1); }
-    if (zero) return R(0);
-    R v = rbf<R>(a, 1, smach, c, M, aq);
-    return sgn < R(0) ? -v : v;
+    return aq;
 }
 
 // ---------------------------------------------------------------- the step kernel
-template <typename R, int PHASE, int RTD, bool WIND> struct Lds {
+template <bool WIND> struct Lds {
     static constexpr int kCd = 0, kCl = 256, kCaX = 512, kCaY = 576, kCnX = 640, kCnY = 704,
                          kWAlt = 768, kWSp = kWAlt + 800, kTotal = WIND ? kWSp + 800 : kWAlt;
 };
 
-template <typename R, int PHASE, int RTD, bool WIND>
+template <typename R, int PHASE, int RTD, bool WIND, int LPE>
 __global__ __launch_bounds__(kBlock) void k_step(StepArgs<R> a) {
-    using L = Lds<R, PHASE, RTD, WIND>;
+    using L = Lds<WIND>;
     __shared__ R lds[L::kTotal];
+    __shared__ LineLds<R> lines;
     const DevParams<R>& P = *a.P;
     for (int t = threadIdx.x; t < 256; t += kBlock) { lds[L::kCd + t] = P.cd_mach[t]; lds[L::kCl + t] = P.cl_mach[t]; }
     if (threadIdx.x < 64) {
@@ -268,17 +373,33 @@ __global__ __launch_bounds__(kBlock) void k_step(StepArgs<R> a) {
             lds[L::kWSp + t] = (&P.wind_speed[0][0])[t];
         }
     }
+    for (int t = threadIdx.x; t < 4 * kLineMax; t += kBlock) (&lines.bp[0][0])[t] = (&P.line_bp[0][0])[t];
+    for (int t = threadIdx.x; t < 4 * (kLineMax + 1); t += kBlock) {
+        (&lines.slot[0][0])[t] = (&P.line_slot[0][0])[t];
+        (&lines.key[0][0])[t] = (&P.line_key[0][0])[t];
+    }
+    if (threadIdx.x < 4) { lines.a[threadIdx.x] = P.line_a[threadIdx.x]; lines.nbp[threadIdx.x] = P.line_nbp[threadIdx.x]; }
     __syncthreads();
     const int64_t N = a.n;
-    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const int64_t gt = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const int64_t i = gt / LPE;
+    const int role = (int)(gt % LPE);
     if (i >= N) return;
+    // role -> (table, part): LPE 1: both tables on one lane; else table = role / (LPE/2)
+    constexpr int nparts = LPE >= 2 ? LPE / 2 : 1;
+    const int my_table = LPE >= 2 ? role / nparts : 0;   // 0 = C_D, 1 = C_L
+    const int part = LPE >= 2 ? role % nparts : 0;
+    const int gbase = (int)__lane_id() & ~(LPE - 1);
     const R* s_cd = lds + L::kCd;
     const R* s_cl = lds + L::kCl;
 
     R s[11];
 #pragma unroll
     for (int k = 0; k < 11; ++k) s[k] = a.b.st[k * N + i];
-    RbfCache<R> ccd{a.b.key[i], a.b.slot[i]}, ccl{a.b.key[N + i], a.b.slot[N + i]};
+    RbfCache<R> cA, cB;   // LPE 1: A = C_D, B = C_L; LPE >= 2: A = own table
+    cA.key = a.b.key[my_table * N + i]; cA.slot = a.b.slot[my_table * N + i];
+    if constexpr (LPE == 1) { cB.key = a.b.key[N + i]; cB.slot = a.b.slot[N + i]; }
+    else { cB.key = 0; cB.slot = -1; }
     R gprev = R(0), dlprev = R(0), drprev = R(0);
     if constexpr (PHASE == 1) { gprev = a.b.act[i]; dlprev = a.b.act[N + i]; drprev = a.b.act[2 * N + i]; }
     R fu0 = R(0), fu1 = R(0), fv0 = R(0), fv1 = R(0), sgu = R(0), sgv = R(0);
@@ -292,9 +413,11 @@ __global__ __launch_bounds__(kBlock) void k_step(StepArgs<R> a) {
     const uint64_t g = a.env_offset + (uint64_t)i;
 
     // actions (float32 unless act_f64)
-    float uf[4] = {0.f, 0.f, 0.f, 0.f};
-    double ud[4] = {0.0, 0.0, 0.0, 0.0};
     constexpr int A = PHASE == 0 ? 1 : 4;
+    float uf[A];
+    double ud[A];
+#pragma unroll
+    for (int k = 0; k < A; ++k) { uf[k] = 0.f; ud[k] = 0.0; }
     if (a.act_f64) {
         const double* ap = (const double*)a.actions + i * A;
 #pragma unroll
@@ -312,6 +435,7 @@ __global__ __launch_bounds__(kBlock) void k_step(StepArgs<R> a) {
 
 #pragma unroll 1
     for (int sub = 0; sub < 4; ++sub) {
+        const DevParams<R>& P = *launder(a.P);
         R x = s[0], y = s[1], vx = s[2], vy = s[3], th = s[4], thd = s[5], ga = s[6], al = s[7];
         R m = s[8], mp = s[9];
         // rocket_physics_fcn (rockets_physics.py:455-704)
@@ -361,9 +485,31 @@ __global__ __launch_bounds__(kBlock) void k_step(StepArgs<R> a) {
         R Fwy = R(0.5) * rho * (vg * vg) * P.A_front * P.C_gust_y;
         R Mw = -d_cp_cg * Fwy;
         R CL = R(0), CD = R(0);
+#ifdef PD_EXP_NORBF
+        if (false) {
+#else
         if (asnd != R(0)) {
-            CL = coef_CL<R>(a, s_cl, ccl, mach, ae);
-            CD = coef_CD<R>(a, s_cd, ccd, mach, ae);
+#endif
+            R cl_sgn; bool cl_zero;
+            R aq_cl = cl_query<R>(ae, cl_sgn, cl_zero);
+            R aq_cd = cd_query<R>(ae);
+            if constexpr (LPE == 1) {
+                if (!cl_zero) {
+                    R v = rbf<R>(a, 1, tab_view<R>(P, s_cd, s_cl, 1), lines, cB, mach, aq_cl, 0, 1);
+                    CL = cl_sgn < R(0) ? -v : v;
+                }
+                CD = rbf<R>(a, 0, tab_view<R>(P, s_cd, s_cl, 0), lines, cA, mach, aq_cd, 0, 1);
+            } else {
+                R v = R(0);
+                if (my_table == 0 || !cl_zero)
+                    v = rbf<R>(a, my_table, tab_view<R>(P, s_cd, s_cl, my_table), lines, cA, mach,
+                               my_table ? aq_cl : aq_cd, part, nparts);
+                if constexpr (nparts >= 2) v += __shfl_xor(v, 1);
+                if constexpr (nparts >= 4) v += __shfl_xor(v, 2);
+                CD = __shfl(v, gbase);
+                R vcl = __shfl(v, gbase + nparts);
+                CL = cl_zero ? R(0) : (cl_sgn < R(0) ? -vcl : vcl);
+            }
         }
         R drag = R(0.5) * rho * (speed * speed) * CD * P.A_front;
         R lift = R(0.5) * rho * (speed * speed) * CL * P.A_front;
@@ -475,44 +621,35 @@ __global__ __launch_bounds__(kBlock) void k_step(StepArgs<R> a) {
         mp -= mdot_dt; m -= mdot_dt;
         s[0] = x; s[1] = y; s[2] = vx; s[3] = vy; s[4] = th; s[5] = thd; s[6] = ga; s[7] = al;
         s[8] = m; s[9] = mp; s[10] = s[10] + dt;
-        if (sub == 3 && a.info) {   // info of the last sub-step (rockets_physics.py:649-702)
+        if (sub == 3 && a.info && role == 0) {   // info of the last sub-step (rockets_physics.py:649-702)
             R vals[PD_N_INFO - 1] = {rho, patm, asnd, mach, q, CL, CD, md_info, x_cog, I, ae, thr_info, ug, vg, gdeg_out};
 #pragma unroll
             for (int k = 0; k < PD_N_INFO - 1; ++k) a.info[(k < PD_INFO_GLOAD ? k : k + 1) * N + i] = vals[k];
         }
     }
-    if (nan_hit) atomicAdd(&a.pend.stats[1], 1ull);
+    if (nan_hit && role == 0) atomicAdd(&a.pend.stats[1], 1ull);
 
-    // ---- g-load window (base_environment.py:136-149)
+    // ---- g-load window (base_environment.py:136-149): ring of 10, Python sum() from the oldest
+    const DevParams<R>& P2 = *launder(a.P);
     R v = sqrt(s[2] * s[2] + s[3] * s[3]);
     R vp = a.b.vprev[i];
     R gl_new = fabs(v - vp) / R(0.1) * R(1) / R(9.81);
     int glen = a.b.glen[i], ghead = a.b.ghead[i];
-    R w[10];
-#pragma unroll
-    for (int k = 0; k < 10; ++k) w[k] = a.b.gwin[k * N + i];
     int wslot;
     if (glen < 10) { wslot = glen; glen += 1; }
     else { wslot = ghead; ghead = ghead == 9 ? 0 : ghead + 1; }
-#pragma unroll
-    for (int k = 0; k < 10; ++k) w[k] = (k == wslot) ? gl_new : w[k];
-    // Python sum() from the oldest entry: ring order ghead, ghead+1, ... (glen < 10: 0..glen-1)
     R gsum = R(0);
-    int start = glen < 10 ? 0 : ghead;
-#pragma unroll
-    for (int k = 0; k < 10; ++k) {
-        int idx = start + k; idx = idx >= 10 ? idx - 10 : idx;
-        R vk = w[0];
-#pragma unroll
-        for (int q2 = 1; q2 < 10; ++q2) vk = (idx == q2) ? w[q2] : vk;
-        gsum = (k < glen) ? gsum + vk : gsum;
+    int idx = glen < 10 ? 0 : ghead;
+    for (int k = 0; k < glen; ++k) {
+        gsum += idx == wslot ? gl_new : a.b.gwin[idx * N + i];
+        idx = idx == 9 ? 0 : idx + 1;
     }
     R gl = gsum / R(10);
 
     // ---- truncated -> done -> reward (rtd_rl.py:190-336 / rtd_pso.py:172-317)
     R x = s[0], y = s[1], vx = s[2], vy = s[3], th = s[4], ga = s[6], mp = s[9];
     R rho, pa_, as_;
-    atmosphere<R>(P, y, rho, pa_, as_);
+    atmosphere<R>(P2, y, rho, pa_, as_);
     R speed = v;
     R q = R(0.5) * rho * (speed * speed);
     int tr = 0, id = 0, dn = 0;
@@ -531,12 +668,12 @@ __global__ __launch_bounds__(kBlock) void k_step(StepArgs<R> a) {
         R qr = R(0.5) * rho * (sp * sp);
         if (qr > R(60000)) { R e = (qr - R(60000)) / (R(65000) - R(60000)); R e2 = e * e; rew -= R(1) * (e2 > R(1) ? R(1) : e2); }
         if (gl > R(5.5)) { R e = (gl - R(5.5)) / (R(6) - R(5.5)); R e2 = e * e; rew -= R(1) * (e2 > R(1) ? R(1) : e2); }
-        R prog = (P.y0_rl - y) / P.y0_rl;
+        R prog = (P2.y0_rl - y) / P2.y0_rl;
         R wp = (qr <= R(60000) && gl <= R(5.5)) ? R(0.5) : R(0.5) * R(0.1);
         rew += wp * prog;
         if (y < R(100)) rew += R(5.5) * (R(1) - fabs(vy) / R(50));
-        if (dn && !tr) rew += R(400) * mp / P.m0_rl;
-        else if (tr && y > R(0)) rew -= R(50) * (fabs(y) / P.y0_rl);
+        if (dn && !tr) rew += R(400) * mp / P2.m0_rl;
+        else if (tr && y > R(0)) rew -= R(50) * (fabs(y) / P2.y0_rl);
         else if (tr && y < R(0)) rew -= R(50) * (fabs(vy) / R(10));
         if (!dn || !(tr && y < R(0))) rew = rew < R(-10) ? R(-10) : (rew > R(10) ? R(10) : rew);
     } else {
@@ -573,45 +710,50 @@ __global__ __launch_bounds__(kBlock) void k_step(StepArgs<R> a) {
         }
     }
 
-    // ---- outputs
-    if (a.obs) {
-        if constexpr (RTD == 0) {
-            a.obs[i * 2 + 0] = (R(1) - y / P.norm_y) * R(2) - R(1);
-            a.obs[i * 2 + 1] = (R(1) - vy / P.norm_vy) * R(2) - R(1);
-        } else if constexpr (PHASE == 0) {
-            a.obs[i * 2 + 0] = y / P.norm_y; a.obs[i * 2 + 1] = vy / P.norm_vy;
+    // ---- outputs (role 0 of the env's lane group)
+    const bool ended = a.auto_reset && (dn || tr);
+    if (role == 0) {
+        if (a.obs) {
+            if constexpr (RTD == 0) {
+                a.obs[i * 2 + 0] = (R(1) - y / P2.norm_y) * R(2) - R(1);
+                a.obs[i * 2 + 1] = (R(1) - vy / P2.norm_vy) * R(2) - R(1);
+            } else if constexpr (PHASE == 0) {
+                a.obs[i * 2 + 0] = y / P2.norm_y; a.obs[i * 2 + 1] = vy / P2.norm_vy;
+            } else {
+                a.obs[i * 5 + 0] = x / P2.norm_x; a.obs[i * 5 + 1] = y / P2.norm_y;
+                a.obs[i * 5 + 2] = vx / P2.norm_vx; a.obs[i * 5 + 3] = vy / P2.norm_vy;
+                a.obs[i * 5 + 4] = tanh(P2.k_theta_pso * (th - Cst<R>::pi / R(2)));
+            }
+        }
+        if (a.reward) a.reward[i] = rew;
+        if (a.reward_sum) a.reward_sum[i] += rew;
+        if (a.done) a.done[i] = (uint8_t)dn;
+        if (a.trunc) a.trunc[i] = (uint8_t)tr;
+        if (a.trunc_id) a.trunc_id[i] = (int8_t)id;
+        if (a.info) a.info[PD_INFO_GLOAD * N + i] = gl;
+        if (ended) {
+            reset_env(a, i, ep + 1, false);
         } else {
-            a.obs[i * 5 + 0] = x / P.norm_x; a.obs[i * 5 + 1] = y / P.norm_y;
-            a.obs[i * 5 + 2] = vx / P.norm_vx; a.obs[i * 5 + 3] = vy / P.norm_vy;
-            a.obs[i * 5 + 4] = tanh(P.k_theta_pso * (th - Cst<R>::pi / R(2)));
+            a.b.vprev[i] = v;
+            a.b.gwin[wslot * N + i] = gl_new;
+            a.b.glen[i] = (uint8_t)glen; a.b.ghead[i] = (uint8_t)ghead;
+            a.b.tid[i] = (int8_t)id;
+            a.b.tstep[i] = ts + 1;
+            if constexpr (PHASE == 1) { a.b.act[i] = gdeg_out; a.b.act[N + i] = dcmdl_out; a.b.act[2 * N + i] = dcmdr_out; }
+            if constexpr (WIND) {
+                a.b.wind[i] = fu0; a.b.wind[N + i] = fu1; a.b.wind[2 * N + i] = fv0; a.b.wind[3 * N + i] = fv1;
+            }
         }
     }
-    if (a.reward) a.reward[i] = rew;
-    if (a.reward_sum) a.reward_sum[i] += rew;
-    if (a.done) a.done[i] = (uint8_t)dn;
-    if (a.trunc) a.trunc[i] = (uint8_t)tr;
-    if (a.trunc_id) a.trunc_id[i] = (int8_t)id;
-    if (a.info) a.info[PD_INFO_GLOAD * N + i] = gl;
-
-    if (a.auto_reset && (dn || tr)) {
-        reset_env(a, i, ep + 1, false);
-        a.b.key[i] = ccd.key; a.b.key[N + i] = ccl.key;
-        a.b.slot[i] = ccd.slot; a.b.slot[N + i] = ccl.slot;
-        return;
+    // neighbourhood caches survive resets (any valid 50-set is a correct start)
+    if (part == 0) {
+        a.b.key[my_table * N + i] = cA.key; a.b.slot[my_table * N + i] = cA.slot;
+        if constexpr (LPE == 1) { a.b.key[N + i] = cB.key; a.b.slot[N + i] = cB.slot; }
     }
-    // ---- state write-back
+    if (!ended) {
 #pragma unroll
-    for (int k = 0; k < 11; ++k) a.b.st[k * N + i] = s[k];
-    a.b.vprev[i] = v;
-    a.b.gwin[wslot * N + i] = gl_new;
-    a.b.glen[i] = (uint8_t)glen; a.b.ghead[i] = (uint8_t)ghead;
-    a.b.tid[i] = (int8_t)id;
-    a.b.tstep[i] = ts + 1;
-    a.b.key[i] = ccd.key; a.b.key[N + i] = ccl.key;
-    a.b.slot[i] = ccd.slot; a.b.slot[N + i] = ccl.slot;
-    if constexpr (PHASE == 1) { a.b.act[i] = gdeg_out; a.b.act[N + i] = dcmdl_out; a.b.act[2 * N + i] = dcmdr_out; }
-    if constexpr (WIND) {
-        a.b.wind[i] = fu0; a.b.wind[N + i] = fu1; a.b.wind[2 * N + i] = fv0; a.b.wind[3 * N + i] = fv1;
+        for (int k = 0; k < 11; ++k)
+            if (k % LPE == role) a.b.st[k * N + i] = s[k];
     }
 }
 
@@ -720,6 +862,22 @@ uint64_t host_knn_key(const pd_aero_table& t, double M, double a) {
 }
 
 template <typename R>
+int table_insert(const pd_aero_table& t, Table<R>& T, uint64_t key, std::vector<double>& work, std::vector<double>& pay) {
+    int64_t cap = 1ll << T.logcap;
+    uint32_t mask = (uint32_t)(cap - 1), h = key_hash(key, T.logcap);
+    while (T.keys[h] != kEmptyKey && T.keys[h] != key) h = (h + 1) & mask;
+    if (T.keys[h] == key) return (int)h;
+    double aoa[kCols];
+    for (int c = 0; c < kCols; ++c) aoa[c] = t.col_aoa[c];
+    if (solve_neighbourhood(t.mach, t.coef, t.col_start, aoa, key, work.data(), pay.data()) != 0) return -1;
+    if ((T.entries + 1) * 2 > cap) return -1;
+    T.keys[h] = key;
+    for (int j = 0; j < kPay; ++j) T.pay[h * kPay + j] = (R)pay[j];
+    ++T.entries;
+    return (int)h;
+}
+
+template <typename R>
 pd_status build_table(const pd_aero_table& t, const uint64_t* keys, int64_t nk, Table<R>& T) {
     int64_t cap_need = std::max<int64_t>(4 * std::max<int64_t>(nk, 64), 1024);
     T.logcap = log2ceil(cap_need);
@@ -727,19 +885,72 @@ pd_status build_table(const pd_aero_table& t, const uint64_t* keys, int64_t nk, 
     T.keys.assign(cap, kEmptyKey);
     T.pay.assign(cap * kPay, R(0));
     std::vector<double> work(kScratch), pay(kPay);
-    double aoa[kCols];
-    for (int c = 0; c < kCols; ++c) aoa[c] = t.col_aoa[c];
-    for (int64_t e = 0; e < nk; ++e) {
-        uint64_t key = keys[e];
-        if (solve_neighbourhood(t.mach, t.coef, t.col_start, aoa, key, work.data(), pay.data()) != 0)
+    for (int64_t e = 0; e < nk; ++e)
+        if (table_insert<R>(t, T, keys[e], work, pay) < 0)
             return fail(PD_ERR_INVALID, "invalid/singular neighbourhood key in param pack");
-        uint32_t mask = (uint32_t)(cap - 1), h = key_hash(key, T.logcap);
-        while (T.keys[h] != kEmptyKey && T.keys[h] != key) h = (h + 1) & mask;
-        if (T.keys[h] == key) continue;
-        T.keys[h] = key;
-        for (int j = 0; j < kPay; ++j) T.pay[h * kPay + j] = (R)pay[j];
-        ++T.entries;
+    return PD_OK;
+}
+
+// Exact neighbourhood intervals along one horizontal query line a = const: the 50-NN set only
+// changes where two points swap distance order, i.e. at pair-bisector crossings; evaluate the
+// set between consecutive crossings and merge equal neighbours.  (The device still verifies
+// every looked-up set, so a query exactly on a breakpoint stays exact.)
+template <typename R>
+pd_status build_line(const pd_aero_table& t, double a, Table<R>& T, int li, DevParams<R>& D) {
+    std::vector<double> m(t.n_pts), dz(t.n_pts);
+    for (int c = 0; c < kCols; ++c)
+        for (int k = 0; k < t.col_len[c]; ++k) {
+            m[t.col_start[c] + k] = t.mach[t.col_start[c] + k];
+            double da = a - t.col_aoa[c];
+            dz[t.col_start[c] + k] = da * da;
+        }
+    std::vector<double> xs;
+    for (int i = 0; i < t.n_pts; ++i)
+        for (int j = i + 1; j < t.n_pts; ++j) {
+            double den = 2.0 * (m[j] - m[i]);
+            if (den == 0.0) continue;
+            double x = (m[j] * m[j] - m[i] * m[i] + dz[j] - dz[i]) / den;
+            if (x > 0.0 && x < 10.0) xs.push_back(x);
+        }
+    std::sort(xs.begin(), xs.end());
+    xs.erase(std::unique(xs.begin(), xs.end()), xs.end());
+    std::vector<double> bps;
+    bps.push_back(0.0);
+    bps.insert(bps.end(), xs.begin(), xs.end());
+    bps.push_back(10.0);
+    std::vector<double> B;
+    std::vector<uint64_t> K;
+    for (size_t k = 0; k + 1 < bps.size(); ++k) {
+        uint64_t key = host_knn_key(t, 0.5 * (bps[k] + bps[k + 1]), a);
+        if (K.empty()) K.push_back(key);
+        else if (key != K.back()) { B.push_back(bps[k]); K.push_back(key); }
     }
+    D.line_a[li] = (R)a;
+    if ((int)B.size() > kLineMax) { D.line_nbp[li] = -1; return PD_OK; }   // too fine: cache path only
+    std::vector<double> work(kScratch), pay(kPay);
+    D.line_nbp[li] = (int)B.size();
+    for (size_t k = 0; k < B.size(); ++k) D.line_bp[li][k] = (R)B[k];
+    for (size_t k = 0; k < K.size(); ++k) {
+        D.line_key[li][k] = K[k];
+        D.line_slot[li][k] = table_insert<R>(t, T, K[k], work, pay);
+    }
+    return PD_OK;
+}
+
+// Candidate grid over the interior query domain [0, 10] Mach x [a0, a1]: the 50-NN key at
+// every cell centre (brute force), inserted into the table.  Device lookups verify it.
+template <typename R>
+pd_status build_grid(const pd_aero_table& t, double a0, double a1, int nm, int na, Table<R>& T,
+                     std::vector<unsigned long long>& gk, std::vector<int>& gs) {
+    gk.assign((size_t)nm * na, 0); gs.assign((size_t)nm * na, -1);
+    std::vector<double> work(kScratch), pay(kPay);
+    double dm = 10.0 / nm, da = (a1 - a0) / na;
+    for (int im = 0; im < nm; ++im)
+        for (int ia = 0; ia < na; ++ia) {
+            uint64_t key = host_knn_key(t, (im + 0.5) * dm, a0 + (ia + 0.5) * da);
+            gk[(size_t)im * na + ia] = key;
+            gs[(size_t)im * na + ia] = table_insert<R>(t, T, key, work, pay);
+        }
     return PD_OK;
 }
 
@@ -764,6 +975,7 @@ struct pd_env {
     void *pay_cd = nullptr, *pay_cl = nullptr;
     int logcap_cd = 0, logcap_cl = 0;
     int64_t entries_cd = 0, entries_cl = 0;
+    int lpe = 2;   // lanes per env of the step kernel
 };
 
 namespace {
@@ -893,6 +1105,28 @@ template <typename R> pd_status create_impl(const pd_params* p, const pd_config*
     pd_status st;
     if ((st = build_table<R>(p->cd, p->keys_cd, p->n_keys_cd, tcd)) != PD_OK) return st;
     if ((st = build_table<R>(p->cl, p->keys_cl, p->n_keys_cl, tcl)) != PD_OK) return st;
+    // clamped query lines: C_D at +-radians(10) (aerodynamic_coefficients.py:108-114), C_L at
+    // +-10 (:122-125); the device computes these abscissae with the same expressions
+    if ((st = build_line<R>(p->cd, 10.0 * kDeg2Rad, tcd, 0, D)) != PD_OK) return st;
+    if ((st = build_line<R>(p->cd, -10.0 * kDeg2Rad, tcd, 1, D)) != PD_OK) return st;
+    if ((st = build_line<R>(p->cl, 10.0, tcl, 2, D)) != PD_OK) return st;
+    if ((st = build_line<R>(p->cl, -10.0, tcl, 3, D)) != PD_OK) return st;
+    // interior candidate grids: C_D abscissa in [-radians(10), radians(10)], C_L in [0, 10]
+    std::vector<unsigned long long> gk[2];
+    std::vector<int> gs[2];
+    const int gnm[2] = {400, 400}, gna[2] = {16, 200};
+    const double ga0[2] = {-10.0 * kDeg2Rad, 0.0}, ga1[2] = {10.0 * kDeg2Rad, 10.0};
+    if ((st = build_grid<R>(p->cd, ga0[0], ga1[0], gnm[0], gna[0], tcd, gk[0], gs[0])) != PD_OK) return st;
+    if ((st = build_grid<R>(p->cl, ga0[1], ga1[1], gnm[1], gna[1], tcl, gk[1], gs[1])) != PD_OK) return st;
+    for (int tb = 0; tb < 2; ++tb) {
+        void *dk, *ds;
+        if ((st = dalloc(e, &dk, gk[tb].size() * 8)) || (st = dalloc(e, &ds, gs[tb].size() * 4))) return st;
+        PD_HIP(hipMemcpy(dk, gk[tb].data(), gk[tb].size() * 8, hipMemcpyHostToDevice));
+        PD_HIP(hipMemcpy(ds, gs[tb].data(), gs[tb].size() * 4, hipMemcpyHostToDevice));
+        D.grid_key[tb] = (const unsigned long long*)dk; D.grid_slot[tb] = (const int*)ds;
+        D.grid_nm[tb] = gnm[tb]; D.grid_na[tb] = gna[tb]; D.grid_a0[tb] = (R)ga0[tb];
+        D.grid_inv_da[tb] = (R)(gna[tb] / (ga1[tb] - ga0[tb])); D.grid_inv_dm[tb] = (R)(gnm[tb] / 10.0);
+    }
     e->logcap_cd = tcd.logcap; e->logcap_cl = tcl.logcap;
     e->entries_cd = tcd.entries; e->entries_cl = tcl.entries;
     if ((st = dalloc(e, (void**)&e->keys_cd, tcd.keys.size() * 8)) || (st = dalloc(e, &e->pay_cd, tcd.pay.size() * sizeof(R))) ||
@@ -921,13 +1155,13 @@ template <typename R> pd_status create_impl(const pd_params* p, const pd_config*
         return st;
     PD_HIP(hipMemset(e->gwin, 0, 10 * N * R_));
     PD_HIP(hipMemset(e->epi, 0xff, N * 4));   // first reset -> episode 0
-    int64_t n_waves = (N + 63) / 64;
+    int64_t n_waves = (N * e->lpe + 63) / 64;
     if ((st = dalloc(e, (void**)&e->scratch, (size_t)n_waves * kScratch * 8))) return st;
     if ((st = dalloc(e, (void**)&e->pend.count, 8)) || (st = dalloc(e, (void**)&e->pend.keys, kPendingCap * 8)) ||
-        (st = dalloc(e, (void**)&e->pend.pay, (size_t)kPendingCap * kPay * 8)) || (st = dalloc(e, (void**)&e->pend.stats, 4 * 8)))
+        (st = dalloc(e, (void**)&e->pend.pay, (size_t)kPendingCap * kPay * 8)) || (st = dalloc(e, (void**)&e->pend.stats, 8 * 8)))
         return st;
     PD_HIP(hipMemset(e->pend.count, 0, 8));
-    unsigned long long stats0[4] = {0, 0, (unsigned long long)tcd.entries, (unsigned long long)tcl.entries};
+    unsigned long long stats0[8] = {0, 0, (unsigned long long)tcd.entries, (unsigned long long)tcl.entries, 0, 0, 0, 0};
     PD_HIP(hipMemcpy(e->pend.stats, stats0, sizeof(stats0), hipMemcpyHostToDevice));
     StepArgs<R> a = make_args<R>(e);
     unsigned grid = (unsigned)((N + kBlock - 1) / kBlock);
@@ -937,17 +1171,26 @@ template <typename R> pd_status create_impl(const pd_params* p, const pd_config*
     return PD_OK;
 }
 
-template <typename R, int PH, int RT, bool W> void launch_step(const StepArgs<R>& a, hipStream_t s) {
-    unsigned grid = (unsigned)((a.n + kBlock - 1) / kBlock);
-    hipLaunchKernelGGL((k_step<R, PH, RT, W>), dim3(grid), dim3(kBlock), 0, s, a);
+template <typename R, int PH, int RT, bool W, int LPE> void launch_step(const StepArgs<R>& a, hipStream_t s) {
+    unsigned grid = (unsigned)((a.n * LPE + kBlock - 1) / kBlock);
+    hipLaunchKernelGGL((k_step<R, PH, RT, W, LPE>), dim3(grid), dim3(kBlock), 0, s, a);
+}
+
+template <typename R, int PH, int RT, bool W> void launch_lpe(int lpe, const StepArgs<R>& a, hipStream_t s) {
+    switch (lpe) {
+        case 1: launch_step<R, PH, RT, W, 1>(a, s); break;
+        case 2: launch_step<R, PH, RT, W, 2>(a, s); break;
+        case 8: launch_step<R, PH, RT, W, 8>(a, s); break;
+        default: launch_step<R, PH, RT, W, 4>(a, s); break;
+    }
 }
 
 template <typename R> void dispatch_step(const pd_env* e, const StepArgs<R>& a, hipStream_t s) {
-    int ph = e->cfg.phase, rt = e->cfg.rtd;
+    int ph = e->cfg.phase, rt = e->cfg.rtd, l = e->lpe;
     bool w = e->cfg.enable_wind != 0;
-    if (ph == 0 && rt == 0) { if (w) launch_step<R, 0, 0, true>(a, s); else launch_step<R, 0, 0, false>(a, s); }
-    else if (ph == 0 && rt == 1) { if (w) launch_step<R, 0, 1, true>(a, s); else launch_step<R, 0, 1, false>(a, s); }
-    else { if (w) launch_step<R, 1, 1, true>(a, s); else launch_step<R, 1, 1, false>(a, s); }
+    if (ph == 0 && rt == 0) { if (w) launch_lpe<R, 0, 0, true>(l, a, s); else launch_lpe<R, 0, 0, false>(l, a, s); }
+    else if (ph == 0 && rt == 1) { if (w) launch_lpe<R, 0, 1, true>(l, a, s); else launch_lpe<R, 0, 1, false>(l, a, s); }
+    else { if (w) launch_lpe<R, 1, 1, true>(l, a, s); else launch_lpe<R, 1, 1, false>(l, a, s); }
 }
 
 template <typename R> void launch_insert(pd_env* e, hipStream_t s) {
@@ -997,6 +1240,8 @@ pd_status pd_create(const pd_params* params, const pd_config* cfg, pd_env** out)
     e->act_dim = cfg->phase == PD_PHASE_PURE_THROTTLE ? 1 : 4;
     e->obs_dim = (cfg->phase == PD_PHASE_LANDING_BURN) ? 5 : 2;
     e->rsize = cfg->precision == PD_F64 ? 8 : 4;
+    e->lpe = cfg->lanes_per_env == 0 ? 2 : cfg->lanes_per_env;
+    if (e->lpe != 1 && e->lpe != 2 && e->lpe != 4 && e->lpe != 8) { delete e; return fail(PD_ERR_INVALID, "lanes_per_env must be 0, 1, 2, 4 or 8"); }
     st = cfg->precision == PD_F64 ? create_impl<double>(params, cfg, e) : create_impl<float>(params, cfg, e);
     if (st != PD_OK) { pd_destroy(e); return st; }
     *out = e;
@@ -1110,8 +1355,10 @@ pd_status pd_set_wind_sigmas(pd_env* e, const double* sig, void* stream) {
 pd_status pd_counters(pd_env* e, int64_t* misses, int64_t* ecd, int64_t* ecl, int64_t* nans) {
     if (!e) return fail(PD_ERR_INVALID, "null env");
     PD_HIP(hipSetDevice(e->device));
-    unsigned long long st[4];
+    unsigned long long st[8];
     PD_HIP(hipMemcpy(st, e->pend.stats, sizeof(st), hipMemcpyDeviceToHost));
+    if (getenv("PDENV_DEBUG_COUNTERS"))
+        fprintf(stderr, "[pdenv] knn calls %llu line-candidates %llu iterations %llu probes %llu\n", st[4], st[5], st[6], st[7]);
     if (misses) *misses = (int64_t)st[0];
     if (nans) *nans = (int64_t)st[1];
     if (ecd) *ecd = (int64_t)st[2];

@@ -59,7 +59,7 @@ class PdConfig(C.Structure):
     _fields_ = [("n_envs", I64), ("device", I32), ("phase", I32), ("rtd", I32), ("precision", I32),
                 ("seed", U64), ("env_offset", U64), ("enable_wind", I32), ("stochastic_wind", I32),
                 ("wind_percentile", I32), ("auto_reset", I32), ("tilt_sigma_rad", D),
-                ("action_f64", I32), ("pad", I32)]
+                ("action_f64", I32), ("lanes_per_env", I32)]
 
 
 EXPORTS = ["pd_abi_version", "pd_sizeof_params", "pd_sizeof_config", "pd_last_error", "pd_device_count", "pd_create", "pd_destroy", "pd_reset",
@@ -78,7 +78,7 @@ def load(path=None):
     global _lib
     if _lib is not None:
         return _lib
-    path = path or LIB_PATH
+    path = path or os.environ.get("PDENV_LIB") or LIB_PATH
     if not os.path.exists(path):
         raise PdError(f"libpdenv.so not found at {path}: run __graft_entry__.build() "
                       "(the HIP extension is required; there is no CPU fallback)")

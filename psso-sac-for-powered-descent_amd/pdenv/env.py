@@ -29,7 +29,7 @@ class PoweredDescentEnv:
     def __init__(self, n_envs, flight_phase="landing_burn_pure_throttle", mode="rl", precision="f64",
                  device=0, enable_wind=False, stochastic_wind=False, wind_percentile=50,
                  auto_reset=False, tilt_sigma_rad=0.0, seed=0, env_offset=0, action_f64=False,
-                 params=None):
+                 params=None, lanes_per_env=0):
         if flight_phase not in PHASES:
             raise ValueError(f"flight_phase must be one of {list(PHASES)} (got {flight_phase!r})")
         if mode not in MODES:
@@ -56,6 +56,7 @@ class PoweredDescentEnv:
         cfg.auto_reset = int(bool(auto_reset))
         cfg.tilt_sigma_rad = float(tilt_sigma_rad)
         cfg.action_f64 = int(bool(action_f64))
+        cfg.lanes_per_env = int(lanes_per_env)
         self.cfg = cfg
         handle = C.c_void_p()
         with torch.cuda.device(self.device):
@@ -100,6 +101,37 @@ class PoweredDescentEnv:
         if info:
             extras.update({k: inf[j] for j, k in enumerate(L.INFO_FIELDS)})
         return self._obs.clone(), self._rew.clone(), self._done.bool(), self._trunc.bool(), extras
+
+    def step_raw(self, actions):
+        """Hot-loop step: launches pd_step into the handle's preallocated output buffers
+        (obs_buf, reward_buf, done_buf, trunc_buf, trunc_id_buf) without copies or syncs.
+        actions must already be a contiguous [N, A] tensor of action_dtype on the device."""
+        L.check(self.lib.pd_step(self.h, C.c_void_p(actions.data_ptr()), _ptr(self._obs), _ptr(self._rew),
+                                 _ptr(self._done), _ptr(self._trunc), _ptr(self._tid), None, None,
+                                 _stream(self.device)))
+        self._steps += 1
+        if self._steps % self.flush_every == 0:
+            self.flush()
+
+    @property
+    def obs_buf(self):
+        return self._obs
+
+    @property
+    def reward_buf(self):
+        return self._rew
+
+    @property
+    def done_buf(self):
+        return self._done
+
+    @property
+    def trunc_buf(self):
+        return self._trunc
+
+    @property
+    def trunc_id_buf(self):
+        return self._tid
 
     def rollout(self, actions, reward_sum=None):
         """T step launches over device-resident actions [T, N, A]; returns summed rewards [N]."""

@@ -21,8 +21,9 @@ for s in $STAGES; do
     smoke) stage smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) stage bench 600 python bench.py ;;
     bench32) stage bench32 600 python bench.py --precision f32 ;;
-    prof) stage prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- python3 bench.py --steps 100 --warmup 10 --cpu-baseline 0 --secondary 0 ;;
-    prof32) stage prof32 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof32 -o run -- python3 bench.py --steps 100 --warmup 10 --cpu-baseline 0 --secondary 0 --precision f32 ;;
+    prof) stage prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 100 --warmup 10 --cpu-baseline 0 --secondary 0 ;;
+    prof32) stage prof32 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof32 -o run -- python3 bench.py --steps 100 --warmup 10 --cpu-baseline 0 --secondary 0 --precision f32 ;;
+    sweep) stage sweep 600 python tools/sweep.py ;;
     pmc) stage pmc 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/pmc_fetch -o run -- python3 bench.py --steps 20 --warmup 5 --cpu-baseline 0 --secondary 0 ;;
   esac
 done
