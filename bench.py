@@ -148,7 +148,7 @@ def main():
         sys.path.insert(0, os.path.join(REPO, "oracle"))
         import numpy as np
         import oracle
-        ne, ns = 32, 200
+        ne, ns = 64, 600
         acts = np.random.default_rng(0).uniform(-1, 1, (ns, ne, 1)).astype(np.float32)
         oracle.rollout(0, 0, 2, 2, acts[:2, :2], True, wind, math.radians(1.0))
         t0 = time.perf_counter()

@@ -461,19 +461,19 @@ static void rtd_rl_pure_throttle(const orc_params* P, const orc_env* E, double g
     else if (vx > 0.01) { tr = 1; id = 7; }
     int done = (y > 0 && y < 1 && speed < 5.0);
     double y0 = P->state0[1], m0 = P->state0[8];
-    double sp = hypot(vx, vy);
+    double sp = hypot(vx, vy);          /* reward_func uses math.hypot (rtd_rl.py:292) */
+    double qr = 0.5 * rho * (sp * sp);
     double r = 0.0;
-    if (q > 60000.0) { double e = (q - 60000.0) / (65000.0 - 60000.0); r -= 1.0 * fmin(e * e, 1.0); }
+    if (qr > 60000.0) { double e = (qr - 60000.0) / (65000.0 - 60000.0); r -= 1.0 * fmin(e * e, 1.0); }
     if (gl > 5.5) { double e = (gl - 5.5) / (6.0 - 5.5); r -= 1.0 * fmin(e * e, 1.0); }
     double prog = (y0 - y) / y0;
-    double wp = (q <= 60000.0 && gl <= 5.5) ? 0.5 : 0.5 * 0.1;
+    double wp = (qr <= 60000.0 && gl <= 5.5) ? 0.5 : 0.5 * 0.1;
     r += wp * prog;
     if (y < 100.0) r += 5.5 * (1.0 - fabs(vy) / 50.0);
     if (done && !tr) r += 400.0 * mp / m0;
     else if (tr && y > 0) r -= 50.0 * (fabs(y) / y0);
     else if (tr && y < 0) r -= 50.0 * (fabs(vy) / 10);
     if (!done || !(tr && y < 0)) { if (r < -10.0) r = -10.0; if (r > 10.0) r = 10.0; }
-    (void)sp;
     o->reward = r; o->done = done; o->trunc = tr; o->trunc_id = id;
 }
 
@@ -541,9 +541,9 @@ int orc_step(const orc_params* P, orc_env* E, int phase, int rtd, const double* 
     E->trunc_id = o->trunc_id;
     memcpy(E->prev_s, E->s, sizeof(E->s));
     /* observations: RL pure throttle (env_wrapped_rl_pytorch.py:195-198), PSO (env_wrapped_ea.py:108-122) */
-    if (rtd == ORC_RTD_RL) {
-        o->obs[0] = (1 - s[1] / P->norm_y) * 2 - 1;
-        o->obs[1] = (1 - s[3] / P->norm_vy) * 2 - 1;
+    if (rtd == ORC_RTD_RL) {   /* the SAC wrapper casts the state to float32 first */
+        o->obs[0] = (1 - (double)(float)s[1] / P->norm_y) * 2 - 1;
+        o->obs[1] = (1 - (double)(float)s[3] / P->norm_vy) * 2 - 1;
     } else if (phase == ORC_PHASE_PURE_THROTTLE) {
         o->obs[0] = s[1] / P->norm_y; o->obs[1] = s[3] / P->norm_vy;
     } else {

@@ -38,7 +38,52 @@ PD_HD uint32_t key_hash(uint64_t k, int log2cap) {
     return (uint32_t)((k * 0x9E3779B97F4A7C15ull) >> (64 - log2cap));
 }
 
-PD_HD double tps(double r) { return r == 0.0 ? 0.0 : r * r * log(r); }
+// Natural log for the neighbourhood solves, evaluated with plain IEEE arithmetic only so that
+// the host-built and the device-built (wave-cooperative) payloads are bit-identical; libm's and
+// the device library's log differ in the last ulp.  Classic argument reduction
+// x = 2^k (1 + f), sqrt(2)/2 <= 1+f < sqrt(2); s = f / (2 + f); log(1+f) = f - hfsq + s (hfsq + R(s^2))
+// with the degree-14 minimax R of the public-domain fdlibm e_log.c; error < 1 ulp.
+// Valid for positive normal finite x (distances between distinct table points).
+PD_HD double pd_log(double x) {
+    const double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10;
+    const double Lg1 = 6.666666666666735130e-01, Lg2 = 3.999999999940941908e-01,
+                 Lg3 = 2.857142874366239149e-01, Lg4 = 2.222219843214978396e-01,
+                 Lg5 = 1.818357216161805012e-01, Lg6 = 1.531383769920937332e-01,
+                 Lg7 = 1.479819860511658591e-01;
+    uint64_t bits;
+    __builtin_memcpy(&bits, &x, 8);
+    int32_t hx = (int32_t)(bits >> 32);
+    int k = (hx >> 20) - 1023;
+    hx &= 0x000fffff;
+    int32_t i = (hx + 0x95f64) & 0x100000;
+    bits = ((uint64_t)(uint32_t)(hx | (i ^ 0x3ff00000)) << 32) | (bits & 0xffffffffull);
+    double xn;
+    __builtin_memcpy(&xn, &bits, 8);
+    k += i >> 20;
+    double f = xn - 1.0;
+    double dk = (double)k;
+    if ((0x000fffff & (2 + hx)) < 3) {
+        if (f == 0.0) return k == 0 ? 0.0 : dk * ln2_hi + dk * ln2_lo;
+        double R = f * f * (0.5 - 0.33333333333333333 * f);
+        return k == 0 ? f - R : dk * ln2_hi - ((R - dk * ln2_lo) - f);
+    }
+    double s = f / (2.0 + f);
+    double z = s * s;
+    int32_t i2 = hx - 0x6147a;
+    double w = z * z;
+    int32_t j = 0x6b851 - hx;
+    double t1 = w * (Lg2 + w * (Lg4 + w * Lg6));
+    double t2 = z * (Lg1 + w * (Lg3 + w * (Lg5 + w * Lg7)));
+    i2 |= j;
+    double R = t2 + t1;
+    if (i2 > 0) {
+        double hfsq = 0.5 * f * f;
+        return k == 0 ? f - (hfsq - s * (hfsq + R)) : dk * ln2_hi - ((hfsq - (s * (hfsq + R) + dk * ln2_lo)) - f);
+    }
+    return k == 0 ? f - s * (f - R) : dk * ln2_hi - ((s * (f - R) - dk * ln2_lo) - f);
+}
+
+PD_HD double tps(double r) { return r == 0.0 ? 0.0 : r * r * pd_log(r); }
 
 // Build and solve the thin-plate-spline system of ONE 50-point neighbourhood, exactly the
 // system scipy's RBFInterpolator builds (scipy/interpolate/_rbfinterp.py _build_system:
@@ -109,10 +154,12 @@ PD_HD int solve_neighbourhood(const double* mach, const double* coef, const int*
             b[i] -= l * b[k];
         }
     }
+    // column-oriented back substitution (the device's wave-cooperative solve does the same
+    // operations in the same order, so host-built and device-built payloads agree bit-for-bit)
     for (int i = kSys - 1; i >= 0; --i) {
-        double s = b[i];
-        for (int j = i + 1; j < kSys; ++j) s -= A[i * kSys + j] * b[j];
-        b[i] = s / A[i * kSys + i];
+        double xi = b[i] / A[i * kSys + i];
+        b[i] = xi;
+        for (int r = 0; r < i; ++r) b[r] -= A[r * kSys + i] * xi;
     }
     for (int j = 0; j < kSys; ++j) payload[j] = b[j];
     payload[kSys + 0] = sh0; payload[kSys + 1] = sh1;

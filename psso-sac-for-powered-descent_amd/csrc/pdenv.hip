@@ -64,7 +64,6 @@ template <typename R> struct StepArgs {
     const DevParams<R>* P;
     EnvBufs<R> b;
     Pending pend;
-    double* scratch;             // [n_waves][kScratch]
     int64_t n;
     uint64_t env_offset;
     uint32_t seed_lo, seed_hi;
@@ -154,6 +153,14 @@ template <typename R> struct TabView {
     R grid_a0, grid_inv_da, grid_inv_dm;
 };
 
+// Per-workgroup LDS scratch for the rare exact on-device neighbourhood solve, guarded by a
+// spin lock taken by lane 0 of the solving wave (a wave never waits on itself: it releases the
+// lock before its next miss).
+struct SolveLds {
+    double work[kScratch];
+    int lock;
+};
+
 // LDS copy of the clamped-line interval tables
 template <typename R> struct LineLds {
     R bp[4][kLineMax];
@@ -232,31 +239,151 @@ __device__ __forceinline__ R rbf_eval(const R* __restrict__ pay, const R* smach,
 
 // slow path: the neighbourhood is not in the table -> solve it here, exactly, on one lane
 // (rare: the table is pre-enumerated over the reachable domain), and queue it for insertion.
+__device__ __forceinline__ void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+// Wave-cooperative exact solve of one neighbourhood into the workgroup's LDS scratch: lane r
+// owns row r of the 53x53 system; LU with partial pivoting (pivot by a wave max-reduction,
+// smallest row index on ties) and column-oriented back substitution -- the operations and
+// their order per element are those of solve_neighbourhood(), so the payload is bit-identical
+// to the host-built one.  Must be called by a converged wave (all 64 lanes active).
 template <typename R>
-__device__ __noinline__ R rbf_miss(const StepArgs<R>& a, int table, unsigned long long key, R M, R aq,
-                                   const R* smach) {
-    const DevParams<R>& P = *a.P;
-    int64_t wave = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
-    double* work = a.scratch + wave * kScratch;
-    double* pay = work + (kScratch - kPay);
+__device__ __noinline__ void solve_wave(const DevParams<R>& P, int table, unsigned long long key, SolveLds* sl) {
+    const int lane = (int)__lane_id();
+    double* A = sl->work;
+    double* b = A + kSys * kSys;
+    double* ym = b + kSys;
+    double* ya = ym + kNbr;
+    double* yd = ya + kNbr;
+    double* pay = sl->work + (kScratch - kPay);
     const double* mach = table ? P.cl_mach_d : P.cd_mach_d;
     const double* coef = table ? P.cl_coef_d : P.cd_coef_d;
     const int* start = table ? P.cl_start : P.cd_start;
     const double* aoa = table ? P.cl_aoa_d : P.cd_aoa_d;
-    int rc = solve_neighbourhood(mach, coef, start, aoa, key, work, pay);
-    atomicAdd(&a.pend.stats[0], 1ull);
-    if (rc != 0) return (R)NAN;
-    unsigned long long idx = atomicAdd(a.pend.count, 1ull);
-    if (idx < (unsigned long long)kPendingCap) {
-        for (int j = 0; j < kPay; ++j) a.pend.pay[idx * kPay + j] = pay[j];
-        a.pend.keys[idx] = key | ((unsigned long long)table << 63);
-    }
     int lo[kCols], len[kCols];
     key_unpack(key, lo, len);
-    R* payR = (R*)work;   // the matrix area is free again: payload in the kernel's precision
-    for (int j = 0; j < kPay; ++j) payR[j] = (R)pay[j];
-    const R* aoaR = table ? P.cl_aoa : P.cd_aoa;
-    return rbf_eval<R>(payR, smach, start, aoaR, lo, len, M, aq, 0, 1);
+    if (lane < kNbr) {
+        int c = 0, off = lane, acc = 0;
+#pragma unroll
+        for (int q = 0; q < kCols; ++q) {
+            if (lane >= acc && lane < acc + len[q]) { c = q; off = lane - acc; }
+            acc += len[q];
+        }
+        int idx = start[c] + lo[c] + off;
+        ym[lane] = mach[idx]; ya[lane] = aoa[c]; yd[lane] = coef[idx];
+    }
+    lds_sync();
+    double mn0 = ym[0], mx0 = ym[0], mn1 = ya[0], mx1 = ya[0];
+    for (int j = 1; j < kNbr; ++j) {
+        double u = ym[j], w = ya[j];
+        mn0 = u < mn0 ? u : mn0; mx0 = u > mx0 ? u : mx0;
+        mn1 = w < mn1 ? w : mn1; mx1 = w > mx1 ? w : mx1;
+    }
+    double sh0 = (mx0 + mn0) / 2, sc0 = (mx0 - mn0) / 2, sh1 = (mx1 + mn1) / 2, sc1 = (mx1 - mn1) / 2;
+    if (sc0 == 0.0) sc0 = 1.0;
+    if (sc1 == 0.0) sc1 = 1.0;
+    if (lane < kNbr) {
+        double yi = ym[lane], ai = ya[lane];
+        for (int j = 0; j < kNbr; ++j) {
+            double d0 = yi - ym[j], d1 = ai - ya[j];
+            A[lane * kSys + j] = tps(sqrt(d0 * d0 + d1 * d1));
+        }
+        A[lane * kSys + kNbr] = 1.0;
+        A[lane * kSys + kNbr + 1] = (yi - sh0) / sc0;
+        A[lane * kSys + kNbr + 2] = (ai - sh1) / sc1;
+        b[lane] = yd[lane];
+    } else if (lane < kSys) {
+        for (int j = 0; j < kNbr; ++j)
+            A[lane * kSys + j] = lane == kNbr ? 1.0 : (lane == kNbr + 1 ? (ym[j] - sh0) / sc0 : (ya[j] - sh1) / sc1);
+        for (int j = kNbr; j < kSys; ++j) A[lane * kSys + j] = 0.0;
+        b[lane] = 0.0;
+    }
+    lds_sync();
+    bool singular = false;
+    for (int k = 0; k < kSys; ++k) {
+        double v = (lane >= k && lane < kSys) ? fabs(A[lane * kSys + k]) : -1.0;
+        int p = lane;
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {
+            double ov = __shfl_xor(v, o);
+            int op = __shfl_xor(p, o);
+            if (ov > v || (ov == v && op < p)) { v = ov; p = op; }
+        }
+        if (v == 0.0) { singular = true; break; }
+        if (p != k) {
+            if (lane < kSys) { double t = A[k * kSys + lane]; A[k * kSys + lane] = A[p * kSys + lane]; A[p * kSys + lane] = t; }
+            if (lane == 0) { double t = b[k]; b[k] = b[p]; b[p] = t; }
+            lds_sync();
+        }
+        double r = 1.0 / A[k * kSys + k];
+        if (lane > k && lane < kSys) {
+            double l = A[lane * kSys + k] * r;
+            if (l != 0.0)
+                for (int j = k + 1; j < kSys; ++j) A[lane * kSys + j] -= l * A[k * kSys + j];
+            b[lane] -= l * b[k];
+        }
+        lds_sync();
+    }
+    if (!singular) {
+        for (int i = kSys - 1; i >= 0; --i) {
+            double xi = b[i] / A[i * kSys + i];
+            lds_sync();
+            if (lane == i) b[i] = xi;
+            if (lane < i) b[lane] -= A[lane * kSys + i] * xi;
+            lds_sync();
+        }
+    }
+    if (lane < kSys) pay[lane] = singular ? (double)NAN : b[lane];
+    else if (lane == kSys) pay[kSys] = sh0;
+    else if (lane == kSys + 1) pay[kSys + 1] = sh1;
+    else if (lane == kSys + 2) pay[kSys + 2] = sc0;
+    else if (lane == kSys + 3) pay[kSys + 3] = sc1;
+    else if (lane < kPay) pay[lane] = 0.0;
+    lds_sync();
+    // payload in the kernel's precision, in the (now free) matrix area
+    if (lane < kPay) ((R*)sl->work)[lane] = (R)pay[lane];
+    lds_sync();
+}
+
+// Each distinct (table, key) missed by the wave is solved cooperatively into the workgroup's LDS
+// scratch (under its lock), evaluated by the lanes that need it, and queued for insertion into
+// the device table (pd_flush_misses).  Called by the converged wave.
+template <typename R>
+__device__ __forceinline__ R rbf_miss_wave(const StepArgs<R>& a, SolveLds* sl, int table, const R* smach,
+                                        const int* start, const R* aoa, unsigned long long key, R M, R aq,
+                                        int part, int nparts, bool need) {
+    R val = R(0);
+    unsigned long long mm = __ballot(need);
+    while (mm) {
+        int leader = __ffsll((long long)mm) - 1;
+        unsigned long long lk = ((unsigned long long)(unsigned int)__shfl((int)(key >> 32), leader) << 32) |
+                                (unsigned int)__shfl((int)key, leader);
+        int lt = __shfl(table, leader);
+        if (__lane_id() == 0) {
+            while (atomicCAS(&sl->lock, 0, 1) != 0) __builtin_amdgcn_s_sleep(2);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        solve_wave<R>(*a.P, lt, lk, sl);
+        if (need && key == lk && table == lt) {
+            int lo[kCols], len[kCols];
+            key_unpack(key, lo, len);
+            val = rbf_eval<R>((const R*)sl->work, smach, start, aoa, lo, len, M, aq, part, nparts);
+            need = false;
+        }
+        if ((int)__lane_id() == leader) {
+            atomicAdd(&a.pend.stats[0], 1ull);
+            unsigned long long idx = atomicAdd(a.pend.count, 1ull);
+            const double* pay = sl->work + (kScratch - kPay);
+            if (idx < (unsigned long long)kPendingCap) {
+                for (int j = 0; j < kPay; ++j) a.pend.pay[idx * kPay + j] = pay[j];
+                a.pend.keys[idx] = lk | ((unsigned long long)lt << 63);
+            }
+        }
+        lds_sync();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        if (__lane_id() == 0) atomicExch(&sl->lock, 0);
+        mm = __ballot(need);
+    }
+    return val;
 }
 
 // This lane's share of the RBF value of `table` at (M, aq).
@@ -265,8 +392,8 @@ __device__ __noinline__ R rbf_miss(const StepArgs<R>& a, int table, unsigned lon
 // breakpoints in LDS); elsewhere the env's cached set.  Either way the candidate is VERIFIED
 // (and repaired by the swap search) against the exact distances before it is used.
 template <typename R>
-__device__ __forceinline__ R rbf(const StepArgs<R>& a, int table, const TabView<R>& t, const LineLds<R>& ln,
-                                 RbfCache<R>& cache, R M, R aq, int part, int nparts) {
+__device__ __forceinline__ R rbf(const StepArgs<R>& a, SolveLds* sl, int table, const TabView<R>& t,
+                                 const LineLds<R>& ln, RbfCache<R>& cache, R M, R aq, int part, int nparts) {
     unsigned long long ckey = cache.key;
     int cslot = cache.slot;
     int li = aq == ln.a[t.line0] ? t.line0 : (aq == ln.a[t.line0 + 1] ? t.line0 + 1 : -1);
@@ -316,14 +443,14 @@ __device__ __forceinline__ R rbf(const StepArgs<R>& a, int table, const TabView<
     cache.slot = slot;
     R val = R(0);
     if (slot >= 0) val = rbf_eval<R>(t.pay + (int64_t)slot * kPay, t.smach, t.start, t.aoa, lo, len, M, aq, part, nparts);
-    // misses share the wave's scratch: serialise them over the active part-0 lanes (the wave
-    // runs divergent branches one after another, so lanes of other call sites never overlap);
-    // the part-0 lane returns the whole value, the other parts of the group return 0
-    unsigned long long mm = __ballot(slot < 0 && part == 0);
-    while (mm) {
-        int leader = __ffsll((long long)mm) - 1;
-        if ((int)__lane_id() == leader) val = rbf_miss<R>(a, table, key, M, aq, t.smach);
-        mm &= mm - 1;
+    // Misses (a neighbourhood outside the pre-enumerated tables): the converged wave solves
+    // each distinct (table, key) cooperatively in the workgroup's LDS scratch, evaluates the
+    // lanes that need it, and queues the payload for insertion (pd_flush_misses).
+    // Misses (a neighbourhood outside the pre-enumerated tables) take the wave-cooperative
+    // exact solve; the loop in rbf_miss_wave runs only when some lane of the wave missed
+    if (__ballot(slot < 0)) {
+        R mv = rbf_miss_wave<R>(a, sl, table, t.smach, t.start, t.aoa, key, M, aq, part, nparts, slot < 0);
+        if (slot < 0) val = mv;
     }
     return val;
 }
@@ -357,10 +484,13 @@ template <bool WIND> struct Lds {
 };
 
 template <typename R, int PHASE, int RTD, bool WIND, int LPE>
-__global__ __launch_bounds__(kBlock) void k_step(StepArgs<R> a) {
+// waves_per_eu(2): the f64 kernel would otherwise spill its last VGPRs into AGPRs and run at one
+// wave per SIMD; two waves with a small scratch spill measured 20% faster (LPE 2, c3 workload).
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) void k_step(StepArgs<R> a) {
     using L = Lds<WIND>;
     __shared__ R lds[L::kTotal];
     __shared__ LineLds<R> lines;
+    __shared__ SolveLds solve;
     const DevParams<R>& P = *a.P;
     for (int t = threadIdx.x; t < 256; t += kBlock) { lds[L::kCd + t] = P.cd_mach[t]; lds[L::kCl + t] = P.cl_mach[t]; }
     if (threadIdx.x < 64) {
@@ -379,12 +509,15 @@ __global__ __launch_bounds__(kBlock) void k_step(StepArgs<R> a) {
         (&lines.key[0][0])[t] = (&P.line_key[0][0])[t];
     }
     if (threadIdx.x < 4) { lines.a[threadIdx.x] = P.line_a[threadIdx.x]; lines.nbp[threadIdx.x] = P.line_nbp[threadIdx.x]; }
+    if (threadIdx.x == 0) solve.lock = 0;
     __syncthreads();
     const int64_t N = a.n;
     const int64_t gt = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    const int64_t i = gt / LPE;
+    // every lane stays active (the cooperative miss solve needs converged waves): lanes past
+    // the end recompute the last env and write nothing
+    const bool valid = gt / LPE < N;
+    const int64_t i = valid ? gt / LPE : N - 1;
     const int role = (int)(gt % LPE);
-    if (i >= N) return;
     // role -> (table, part): LPE 1: both tables on one lane; else table = role / (LPE/2)
     constexpr int nparts = LPE >= 2 ? LPE / 2 : 1;
     const int my_table = LPE >= 2 ? role / nparts : 0;   // 0 = C_D, 1 = C_L
@@ -485,32 +618,31 @@ __global__ __launch_bounds__(kBlock) void k_step(StepArgs<R> a) {
         R Fwy = R(0.5) * rho * (vg * vg) * P.A_front * P.C_gust_y;
         R Mw = -d_cp_cg * Fwy;
         R CL = R(0), CD = R(0);
-#ifdef PD_EXP_NORBF
-        if (false) {
-#else
-        if (asnd != R(0)) {
-#endif
+#ifndef PD_EXP_NORBF
+        {
+            // evaluated convergently by every lane; results of lanes that need none (speed of
+            // sound 0 above 81 km, |deg(deg(alpha))| < 1e-6 for C_L) are discarded
             R cl_sgn; bool cl_zero;
             R aq_cl = cl_query<R>(ae, cl_sgn, cl_zero);
             R aq_cd = cd_query<R>(ae);
+            const bool have = asnd != R(0);
             if constexpr (LPE == 1) {
-                if (!cl_zero) {
-                    R v = rbf<R>(a, 1, tab_view<R>(P, s_cd, s_cl, 1), lines, cB, mach, aq_cl, 0, 1);
-                    CL = cl_sgn < R(0) ? -v : v;
-                }
-                CD = rbf<R>(a, 0, tab_view<R>(P, s_cd, s_cl, 0), lines, cA, mach, aq_cd, 0, 1);
+                R v = rbf<R>(a, &solve, 1, tab_view<R>(P, s_cd, s_cl, 1), lines, cB, mach, aq_cl, 0, 1);
+                CL = (!have || cl_zero) ? R(0) : (cl_sgn < R(0) ? -v : v);
+                R w = rbf<R>(a, &solve, 0, tab_view<R>(P, s_cd, s_cl, 0), lines, cA, mach, aq_cd, 0, 1);
+                CD = have ? w : R(0);
             } else {
-                R v = R(0);
-                if (my_table == 0 || !cl_zero)
-                    v = rbf<R>(a, my_table, tab_view<R>(P, s_cd, s_cl, my_table), lines, cA, mach,
-                               my_table ? aq_cl : aq_cd, part, nparts);
+                R v = rbf<R>(a, &solve, my_table, tab_view<R>(P, s_cd, s_cl, my_table), lines, cA, mach,
+                             my_table ? aq_cl : aq_cd, part, nparts);
                 if constexpr (nparts >= 2) v += __shfl_xor(v, 1);
                 if constexpr (nparts >= 4) v += __shfl_xor(v, 2);
-                CD = __shfl(v, gbase);
+                R vcd = __shfl(v, gbase);
                 R vcl = __shfl(v, gbase + nparts);
-                CL = cl_zero ? R(0) : (cl_sgn < R(0) ? -vcl : vcl);
+                CD = have ? vcd : R(0);
+                CL = (!have || cl_zero) ? R(0) : (cl_sgn < R(0) ? -vcl : vcl);
             }
         }
+#endif
         R drag = R(0.5) * rho * (speed * speed) * CD * P.A_front;
         R lift = R(0.5) * rho * (speed * speed) * CL * P.A_front;
         R sae = sin(ae), cae = cos(ae);
@@ -621,13 +753,13 @@ __global__ __launch_bounds__(kBlock) void k_step(StepArgs<R> a) {
         mp -= mdot_dt; m -= mdot_dt;
         s[0] = x; s[1] = y; s[2] = vx; s[3] = vy; s[4] = th; s[5] = thd; s[6] = ga; s[7] = al;
         s[8] = m; s[9] = mp; s[10] = s[10] + dt;
-        if (sub == 3 && a.info && role == 0) {   // info of the last sub-step (rockets_physics.py:649-702)
+        if (sub == 3 && a.info && role == 0 && valid) {   // info of the last sub-step (rockets_physics.py:649-702)
             R vals[PD_N_INFO - 1] = {rho, patm, asnd, mach, q, CL, CD, md_info, x_cog, I, ae, thr_info, ug, vg, gdeg_out};
 #pragma unroll
             for (int k = 0; k < PD_N_INFO - 1; ++k) a.info[(k < PD_INFO_GLOAD ? k : k + 1) * N + i] = vals[k];
         }
     }
-    if (nan_hit && role == 0) atomicAdd(&a.pend.stats[1], 1ull);
+    if (nan_hit && role == 0 && valid) atomicAdd(&a.pend.stats[1], 1ull);
 
     // ---- g-load window (base_environment.py:136-149): ring of 10, Python sum() from the oldest
     const DevParams<R>& P2 = *launder(a.P);
@@ -712,11 +844,13 @@ __global__ __launch_bounds__(kBlock) void k_step(StepArgs<R> a) {
 
     // ---- outputs (role 0 of the env's lane group)
     const bool ended = a.auto_reset && (dn || tr);
-    if (role == 0) {
+    if (role == 0 && valid) {
         if (a.obs) {
             if constexpr (RTD == 0) {
-                a.obs[i * 2 + 0] = (R(1) - y / P2.norm_y) * R(2) - R(1);
-                a.obs[i * 2 + 1] = (R(1) - vy / P2.norm_vy) * R(2) - R(1);
+                // GymnasiumWrapperPyTorch._process_state casts the raw state to float32 BEFORE
+                // augment_state (env_wrapped_rl_pytorch.py:42-47, 195-198)
+                a.obs[i * 2 + 0] = (R(1) - (R)(float)y / P2.norm_y) * R(2) - R(1);
+                a.obs[i * 2 + 1] = (R(1) - (R)(float)vy / P2.norm_vy) * R(2) - R(1);
             } else if constexpr (PHASE == 0) {
                 a.obs[i * 2 + 0] = y / P2.norm_y; a.obs[i * 2 + 1] = vy / P2.norm_vy;
             } else {
@@ -746,11 +880,11 @@ __global__ __launch_bounds__(kBlock) void k_step(StepArgs<R> a) {
         }
     }
     // neighbourhood caches survive resets (any valid 50-set is a correct start)
-    if (part == 0) {
+    if (part == 0 && valid) {
         a.b.key[my_table * N + i] = cA.key; a.b.slot[my_table * N + i] = cA.slot;
         if constexpr (LPE == 1) { a.b.key[N + i] = cB.key; a.b.slot[N + i] = cB.slot; }
     }
-    if (!ended) {
+    if (!ended && valid) {
 #pragma unroll
         for (int k = 0; k < 11; ++k)
             if (k % LPE == role) a.b.st[k * N + i] = s[k];
@@ -808,8 +942,8 @@ __global__ __launch_bounds__(kBlock) void k_observe(StepArgs<R> a, int obs_kind)
     if (i >= N) return;
     R x = a.b.st[i], y = a.b.st[N + i], vx = a.b.st[2 * N + i], vy = a.b.st[3 * N + i], th = a.b.st[4 * N + i];
     if (obs_kind == 0) {
-        a.obs[i * 2] = (R(1) - y / P.norm_y) * R(2) - R(1);
-        a.obs[i * 2 + 1] = (R(1) - vy / P.norm_vy) * R(2) - R(1);
+        a.obs[i * 2] = (R(1) - (R)(float)y / P.norm_y) * R(2) - R(1);
+        a.obs[i * 2 + 1] = (R(1) - (R)(float)vy / P.norm_vy) * R(2) - R(1);
     } else if (obs_kind == 1) {
         a.obs[i * 2] = y / P.norm_y; a.obs[i * 2 + 1] = vy / P.norm_vy;
     } else {
@@ -970,7 +1104,6 @@ struct pd_env {
     unsigned long long* key = nullptr; int* slot = nullptr;
     int8_t* tid = nullptr; uint32_t *epi = nullptr, *tstep = nullptr;
     Pending pend{};
-    double* scratch = nullptr;
     unsigned long long *keys_cd = nullptr, *keys_cl = nullptr;
     void *pay_cd = nullptr, *pay_cl = nullptr;
     int logcap_cd = 0, logcap_cl = 0;
@@ -994,7 +1127,6 @@ template <typename R> StepArgs<R> make_args(pd_env* e) {
     a.b.act = (R*)e->act; a.b.wind = (R*)e->wind; a.b.wprof = e->wprof; a.b.key = e->key; a.b.slot = e->slot;
     a.b.tid = e->tid; a.b.epi = e->epi; a.b.tstep = e->tstep;
     a.pend = e->pend;
-    a.scratch = e->scratch;
     a.n = e->cfg.n_envs;
     a.env_offset = e->cfg.env_offset;
     a.seed_lo = (uint32_t)e->cfg.seed; a.seed_hi = (uint32_t)(e->cfg.seed >> 32);
@@ -1155,8 +1287,6 @@ template <typename R> pd_status create_impl(const pd_params* p, const pd_config*
         return st;
     PD_HIP(hipMemset(e->gwin, 0, 10 * N * R_));
     PD_HIP(hipMemset(e->epi, 0xff, N * 4));   // first reset -> episode 0
-    int64_t n_waves = (N * e->lpe + 63) / 64;
-    if ((st = dalloc(e, (void**)&e->scratch, (size_t)n_waves * kScratch * 8))) return st;
     if ((st = dalloc(e, (void**)&e->pend.count, 8)) || (st = dalloc(e, (void**)&e->pend.keys, kPendingCap * 8)) ||
         (st = dalloc(e, (void**)&e->pend.pay, (size_t)kPendingCap * kPay * 8)) || (st = dalloc(e, (void**)&e->pend.stats, 8 * 8)))
         return st;

@@ -84,6 +84,16 @@ class Params:
         self.struct = p
         self.pack = pk
 
+    def restrict_keys(self, n_cd, n_cl):
+        """Keep only the first n_cd / n_cl pre-enumerated neighbourhoods (tests: forces the
+        on-device exact solve for everything else)."""
+        self.keys_cd = np.ascontiguousarray(self.keys_cd[:n_cd])
+        self.keys_cl = np.ascontiguousarray(self.keys_cl[:n_cl])
+        p = self.struct
+        p.keys_cd = self.keys_cd.ctypes.data_as(C.POINTER(U64)); p.n_keys_cd = len(self.keys_cd)
+        p.keys_cl = self.keys_cl.ctypes.data_as(C.POINTER(U64)); p.n_keys_cl = len(self.keys_cl)
+        return self
+
     @property
     def state0(self):
         return np.array(self.pack["state0"])

@@ -143,9 +143,7 @@ def test_episodes_match_reference(oracle_mod, name, phase, rtd):
     assert [r[4] for r in rec][-1] == d[f"{name}_trunc_id"][-1]
     obs = np.array([r[5][:d[f"{name}_obs"].shape[1]] for r in rec])
     ref_obs = d[f"{name}_obs"]
-    if rtd == 0:   # the SAC wrapper casts observations to float32
-        obs = obs.astype(np.float32).astype(np.float64)
-    assert np.abs(obs - ref_obs).max() < 1e-6
+    assert np.abs(obs - ref_obs).max() < 1e-6   # bounded by the (chaotic) state drift
 
 
 @pytest.mark.parametrize("ep", [0, 1])

@@ -24,7 +24,9 @@ for s in $STAGES; do
     prof) stage prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 100 --warmup 10 --cpu-baseline 0 --secondary 0 ;;
     prof32) stage prof32 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof32 -o run -- python3 bench.py --steps 100 --warmup 10 --cpu-baseline 0 --secondary 0 --precision f32 ;;
     sweep) stage sweep 600 python tools/sweep.py ;;
-    pmc) stage pmc 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/pmc_fetch -o run -- python3 bench.py --steps 20 --warmup 5 --cpu-baseline 0 --secondary 0 ;;
+    pmc) stage pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run -- python3 bench.py --steps 20 --warmup 5 --cpu-baseline 0 --secondary 0
+         stage pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o run -- python3 bench.py --steps 20 --warmup 5 --cpu-baseline 0 --secondary 0 ;;
+    pmcv) stage pmc_valu 600 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES --output-format csv -d gpurun_out/pmc_valu -o run -- python3 bench.py --steps 20 --warmup 5 --cpu-baseline 0 --secondary 0 ;;
   esac
 done
 echo "=== done"

@@ -178,10 +178,30 @@ def sweep_line_keys(table, a, mlo=0.0, mhi=10.0):
     return knn_keys(table, mids, np.full(len(mids), a))
 
 
-def enumerate_keys(table, a_lo, a_hi, n_lines, extra_lines):
+def vsweep_line_keys(table, M, a_lo, a_hi):
+    """Exact enumeration along the vertical line Mach=M, a in [a_lo, a_hi]: bisectors of
+    points in different AoA columns cross it once; same-column pairs never swap along it."""
+    pm = np.array(table["mach"])
+    pa = np.concatenate([[c["aoa"]] * c["len"] for c in table["cols"]])
+    dm2 = (M - pm) ** 2
+    i, j = np.triu_indices(len(pm), 1)
+    den = 2.0 * (pa[j] - pa[i])
+    ok = den != 0
+    x = (dm2[j][ok] - dm2[i][ok] + pa[j][ok] ** 2 - pa[i][ok] ** 2) / den[ok]
+    x = np.unique(x[(x > a_lo) & (x < a_hi)])
+    bps = np.concatenate([[a_lo], x, [a_hi]])
+    mids = np.concatenate([[a_lo], 0.5 * (bps[:-1] + bps[1:]), [a_hi]])
+    return knn_keys(table, np.full(len(mids), M), mids)
+
+
+def enumerate_keys(table, a_lo, a_hi, n_lines, extra_lines, n_vlines=2001, n_random=2000000):
     keys = set()
     for a in list(np.linspace(a_lo, a_hi, n_lines)) + list(extra_lines):
         keys.update(int(k) for k in sweep_line_keys(table, float(a)))
+    for M in np.linspace(0.0, 10.0, n_vlines):
+        keys.update(int(k) for k in vsweep_line_keys(table, float(M), a_lo, a_hi))
+    rng = np.random.default_rng(1)
+    keys.update(int(k) for k in knn_keys(table, rng.uniform(0, 10, n_random), rng.uniform(a_lo, a_hi, n_random)))
     # dense 2-D grid on top (cheap insurance for slivers between lines)
     M = np.linspace(0.0, 10.0, 2001)
     Aq = np.linspace(a_lo, a_hi, 4 * n_lines + 1)
