@@ -76,11 +76,21 @@ template <typename R> struct StepArgs {
     R* reward_sum;
 };
 
+// Per-env element `i` of a wave-uniform base pointer, addressed as base + zero-extended 32-bit
+// byte offset: the compiler keeps the bases in SGPRs (global_load ... saddr) instead of one
+// 64-bit VGPR address per SoA field.
+template <typename T> __device__ __forceinline__ T& ev(T* base, uint32_t i) {
+    using B = typename std::conditional<std::is_const<T>::value, const char, char>::type;
+    return *(T*)((B*)base + (uint32_t)(i * (uint32_t)sizeof(T)));
+}
+
 // ---------------------------------------------------------------- reset of one env
 template <typename R>
 __device__ void reset_env(const StepArgs<R>& a, int64_t i, uint32_t episode, bool reset_cache) {
     const DevParams<R>& P = *a.P;
     const int64_t N = a.n;
+    uint32_t ui = (uint32_t)i;
+    asm volatile("" : "+v"(ui));   // addresses recomputed here, not kept live by the caller
     R s[11];
 #pragma unroll
     for (int k = 0; k < 11; ++k) s[k] = P.state0[k];
@@ -93,23 +103,23 @@ __device__ void reset_env(const StepArgs<R>& a, int64_t i, uint32_t episode, boo
         s[7] = s[4] - s[6];
     }
 #pragma unroll
-    for (int k = 0; k < 11; ++k) a.b.st[k * N + i] = s[k];
-    a.b.vprev[i] = sqrt(s[2] * s[2] + s[3] * s[3]);
-    a.b.ghead[i] = 0; a.b.glen[i] = 0;
-    a.b.act[i] = R(0); a.b.act[N + i] = R(0); a.b.act[2 * N + i] = R(0);
-    a.b.tid[i] = 0;
-    a.b.epi[i] = episode; a.b.tstep[i] = 0;
+    for (int k = 0; k < 11; ++k) ev(a.b.st + (k) * N, ui) = s[k];
+    ev(a.b.vprev, ui) = sqrt(s[2] * s[2] + s[3] * s[3]);
+    ev(a.b.ghead, ui) = 0; ev(a.b.glen, ui) = 0;
+    ev(a.b.act, ui) = R(0); ev(a.b.act + N, ui) = R(0); ev(a.b.act + (2) * N, ui) = R(0);
+    ev(a.b.tid, ui) = 0;
+    ev(a.b.epi, ui) = episode; ev(a.b.tstep, ui) = 0;
     // wind: VKDisturbanceGenerator._new_filters (vonkarman.py:60-66): sigmas drawn per reset,
     // filter state zeroed; WindModel.compile_horizontal_fixed_wind: percentile per reset
     u32x4 r = philox({(uint32_t)g, (uint32_t)(g >> 32) ^ episode, 0u, kTagReset}, a.seed_lo, a.seed_hi);
     double su = P.sigma_u_lo + (P.sigma_u_hi - P.sigma_u_lo) * u01(r.x, r.y);
     double sv = P.sigma_v_lo + (P.sigma_v_hi - P.sigma_v_lo) * u01(r.z, r.w);
-    a.b.wind[i] = R(0); a.b.wind[N + i] = R(0); a.b.wind[2 * N + i] = R(0); a.b.wind[3 * N + i] = R(0);
-    a.b.wind[4 * N + i] = (R)su; a.b.wind[5 * N + i] = (R)sv;
-    a.b.wprof[i] = a.fixed_prof >= 0 ? (uint8_t)a.fixed_prof : (uint8_t)((r.x ^ r.w) % 49u);  // randint(50, 99)
+    ev(a.b.wind, ui) = R(0); ev(a.b.wind + N, ui) = R(0); ev(a.b.wind + (2) * N, ui) = R(0); ev(a.b.wind + (3) * N, ui) = R(0);
+    ev(a.b.wind + (4) * N, ui) = (R)su; ev(a.b.wind + (5) * N, ui) = (R)sv;
+    ev(a.b.wprof, ui) = a.fixed_prof >= 0 ? (uint8_t)a.fixed_prof : (uint8_t)((r.x ^ r.w) % 49u);  // randint(50, 99)
     if (reset_cache) {   // any valid 50-set is a correct start for the swap search
-        a.b.key[i] = P.init_key_cd; a.b.key[N + i] = P.init_key_cl;
-        a.b.slot[i] = -1; a.b.slot[N + i] = -1;
+        ev(a.b.key, ui) = P.init_key_cd; ev(a.b.key + N, ui) = P.init_key_cl;
+        ev(a.b.slot, ui) = -1; ev(a.b.slot + N, ui) = -1;
     }
 }
 
@@ -518,6 +528,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
     const bool valid = gt / LPE < N;
     const int64_t i = valid ? gt / LPE : N - 1;
     const int role = (int)(gt % LPE);
+    const uint32_t ui = (uint32_t)i;   // N <= 2^25 (validated): 32-bit per-lane byte offsets
     // role -> (table, part): LPE 1: both tables on one lane; else table = role / (LPE/2)
     constexpr int nparts = LPE >= 2 ? LPE / 2 : 1;
     const int my_table = LPE >= 2 ? role / nparts : 0;   // 0 = C_D, 1 = C_L
@@ -528,21 +539,21 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
 
     R s[11];
 #pragma unroll
-    for (int k = 0; k < 11; ++k) s[k] = a.b.st[k * N + i];
+    for (int k = 0; k < 11; ++k) s[k] = ev(a.b.st + (k) * N, ui);
     RbfCache<R> cA, cB;   // LPE 1: A = C_D, B = C_L; LPE >= 2: A = own table
-    cA.key = a.b.key[my_table * N + i]; cA.slot = a.b.slot[my_table * N + i];
-    if constexpr (LPE == 1) { cB.key = a.b.key[N + i]; cB.slot = a.b.slot[N + i]; }
+    cA.key = ev(a.b.key + (my_table) * N, ui); cA.slot = ev(a.b.slot + (my_table) * N, ui);
+    if constexpr (LPE == 1) { cB.key = ev(a.b.key + N, ui); cB.slot = ev(a.b.slot + N, ui); }
     else { cB.key = 0; cB.slot = -1; }
     R gprev = R(0), dlprev = R(0), drprev = R(0);
-    if constexpr (PHASE == 1) { gprev = a.b.act[i]; dlprev = a.b.act[N + i]; drprev = a.b.act[2 * N + i]; }
+    if constexpr (PHASE == 1) { gprev = ev(a.b.act, ui); dlprev = ev(a.b.act + N, ui); drprev = ev(a.b.act + (2) * N, ui); }
     R fu0 = R(0), fu1 = R(0), fv0 = R(0), fv1 = R(0), sgu = R(0), sgv = R(0);
     int prof = 0;
     if constexpr (WIND) {
-        fu0 = a.b.wind[i]; fu1 = a.b.wind[N + i]; fv0 = a.b.wind[2 * N + i]; fv1 = a.b.wind[3 * N + i];
-        sgu = a.b.wind[4 * N + i]; sgv = a.b.wind[5 * N + i];
-        prof = a.b.wprof[i];
+        fu0 = ev(a.b.wind, ui); fu1 = ev(a.b.wind + N, ui); fv0 = ev(a.b.wind + (2) * N, ui); fv1 = ev(a.b.wind + (3) * N, ui);
+        sgu = ev(a.b.wind + (4) * N, ui); sgv = ev(a.b.wind + (5) * N, ui);
+        prof = ev(a.b.wprof, ui);
     }
-    const uint32_t ep = a.b.epi[i], ts = a.b.tstep[i];
+    const uint32_t ep = ev(a.b.epi, ui), ts = ev(a.b.tstep, ui);
     const uint64_t g = a.env_offset + (uint64_t)i;
 
     // actions (float32 unless act_f64)
@@ -552,13 +563,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
 #pragma unroll
     for (int k = 0; k < A; ++k) { uf[k] = 0.f; ud[k] = 0.0; }
     if (a.act_f64) {
-        const double* ap = (const double*)a.actions + i * A;
 #pragma unroll
-        for (int k = 0; k < A; ++k) ud[k] = ap[k];
+        for (int k = 0; k < A; ++k) ud[k] = ev((const double*)a.actions + k, ui * A);
     } else {
-        const float* ap = (const float*)a.actions + i * A;
 #pragma unroll
-        for (int k = 0; k < A; ++k) uf[k] = ap[k];
+        for (int k = 0; k < A; ++k) uf[k] = ev((const float*)a.actions + k, ui * A);
     }
 
     const R dt = PHASE == 0 ? R(0.025) : R(0.1);
@@ -595,7 +604,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
             ug = np_interp<R>(walt, wsp, wn, km);
             if (y < P.vk_y_threshold && a.stochastic) {
                 double w0, w1;
-                if (a.noise) { w0 = a.noise[i * 8 + 2 * sub]; w1 = a.noise[i * 8 + 2 * sub + 1]; }
+                if (a.noise) { w0 = ev(a.noise + 2 * sub, ui * 8); w1 = ev(a.noise + 2 * sub + 1, ui * 8); }
                 else {
                     u32x4 r = philox({(uint32_t)g, (uint32_t)(g >> 32) ^ ep, ts, kTagWindSub + (uint32_t)sub},
                                      a.seed_lo, a.seed_hi);
@@ -756,7 +765,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
         if (sub == 3 && a.info && role == 0 && valid) {   // info of the last sub-step (rockets_physics.py:649-702)
             R vals[PD_N_INFO - 1] = {rho, patm, asnd, mach, q, CL, CD, md_info, x_cog, I, ae, thr_info, ug, vg, gdeg_out};
 #pragma unroll
-            for (int k = 0; k < PD_N_INFO - 1; ++k) a.info[(k < PD_INFO_GLOAD ? k : k + 1) * N + i] = vals[k];
+            for (int k = 0; k < PD_N_INFO - 1; ++k) ev(a.info + ((k < PD_INFO_GLOAD ? k : k + 1)) * N, ui) = vals[k];
         }
     }
     if (nan_hit && role == 0 && valid) atomicAdd(&a.pend.stats[1], 1ull);
@@ -764,16 +773,16 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
     // ---- g-load window (base_environment.py:136-149): ring of 10, Python sum() from the oldest
     const DevParams<R>& P2 = *launder(a.P);
     R v = sqrt(s[2] * s[2] + s[3] * s[3]);
-    R vp = a.b.vprev[i];
+    R vp = ev(a.b.vprev, ui);
     R gl_new = fabs(v - vp) / R(0.1) * R(1) / R(9.81);
-    int glen = a.b.glen[i], ghead = a.b.ghead[i];
+    int glen = ev(a.b.glen, ui), ghead = ev(a.b.ghead, ui);
     int wslot;
     if (glen < 10) { wslot = glen; glen += 1; }
     else { wslot = ghead; ghead = ghead == 9 ? 0 : ghead + 1; }
     R gsum = R(0);
     int idx = glen < 10 ? 0 : ghead;
     for (int k = 0; k < glen; ++k) {
-        gsum += idx == wslot ? gl_new : a.b.gwin[idx * N + i];
+        gsum += idx == wslot ? gl_new : ev(a.b.gwin + (idx) * N, ui);
         idx = idx == 9 ? 0 : idx + 1;
     }
     R gl = gsum / R(10);
@@ -843,51 +852,55 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
     }
 
     // ---- outputs (role 0 of the env's lane group)
+    // fresh copy of the offset: the store addresses are recomputed here from the SGPR bases
+    // instead of keeping the load addresses live (spilled) across the sub-step loop
+    uint32_t ui_out = ui;
+    asm volatile("" : "+v"(ui_out));
     const bool ended = a.auto_reset && (dn || tr);
     if (role == 0 && valid) {
         if (a.obs) {
             if constexpr (RTD == 0) {
                 // GymnasiumWrapperPyTorch._process_state casts the raw state to float32 BEFORE
                 // augment_state (env_wrapped_rl_pytorch.py:42-47, 195-198)
-                a.obs[i * 2 + 0] = (R(1) - (R)(float)y / P2.norm_y) * R(2) - R(1);
-                a.obs[i * 2 + 1] = (R(1) - (R)(float)vy / P2.norm_vy) * R(2) - R(1);
+                ev(a.obs + 0, ui_out * 2) = (R(1) - (R)(float)y / P2.norm_y) * R(2) - R(1);
+                ev(a.obs + 1, ui_out * 2) = (R(1) - (R)(float)vy / P2.norm_vy) * R(2) - R(1);
             } else if constexpr (PHASE == 0) {
-                a.obs[i * 2 + 0] = y / P2.norm_y; a.obs[i * 2 + 1] = vy / P2.norm_vy;
+                ev(a.obs + 0, ui_out * 2) = y / P2.norm_y; ev(a.obs + 1, ui_out * 2) = vy / P2.norm_vy;
             } else {
-                a.obs[i * 5 + 0] = x / P2.norm_x; a.obs[i * 5 + 1] = y / P2.norm_y;
-                a.obs[i * 5 + 2] = vx / P2.norm_vx; a.obs[i * 5 + 3] = vy / P2.norm_vy;
-                a.obs[i * 5 + 4] = tanh(P2.k_theta_pso * (th - Cst<R>::pi / R(2)));
+                ev(a.obs + 0, ui_out * 5) = x / P2.norm_x; ev(a.obs + 1, ui_out * 5) = y / P2.norm_y;
+                ev(a.obs + 2, ui_out * 5) = vx / P2.norm_vx; ev(a.obs + 3, ui_out * 5) = vy / P2.norm_vy;
+                ev(a.obs + 4, ui_out * 5) = tanh(P2.k_theta_pso * (th - Cst<R>::pi / R(2)));
             }
         }
-        if (a.reward) a.reward[i] = rew;
-        if (a.reward_sum) a.reward_sum[i] += rew;
-        if (a.done) a.done[i] = (uint8_t)dn;
-        if (a.trunc) a.trunc[i] = (uint8_t)tr;
-        if (a.trunc_id) a.trunc_id[i] = (int8_t)id;
-        if (a.info) a.info[PD_INFO_GLOAD * N + i] = gl;
+        if (a.reward) ev(a.reward, ui_out) = rew;
+        if (a.reward_sum) ev(a.reward_sum, ui_out) += rew;
+        if (a.done) ev(a.done, ui_out) = (uint8_t)dn;
+        if (a.trunc) ev(a.trunc, ui_out) = (uint8_t)tr;
+        if (a.trunc_id) ev(a.trunc_id, ui_out) = (int8_t)id;
+        if (a.info) ev(a.info + (PD_INFO_GLOAD) * N, ui_out) = gl;
         if (ended) {
             reset_env(a, i, ep + 1, false);
         } else {
-            a.b.vprev[i] = v;
-            a.b.gwin[wslot * N + i] = gl_new;
-            a.b.glen[i] = (uint8_t)glen; a.b.ghead[i] = (uint8_t)ghead;
-            a.b.tid[i] = (int8_t)id;
-            a.b.tstep[i] = ts + 1;
-            if constexpr (PHASE == 1) { a.b.act[i] = gdeg_out; a.b.act[N + i] = dcmdl_out; a.b.act[2 * N + i] = dcmdr_out; }
+            ev(a.b.vprev, ui_out) = v;
+            ev(a.b.gwin + (wslot) * N, ui_out) = gl_new;
+            ev(a.b.glen, ui_out) = (uint8_t)glen; ev(a.b.ghead, ui_out) = (uint8_t)ghead;
+            ev(a.b.tid, ui_out) = (int8_t)id;
+            ev(a.b.tstep, ui_out) = ts + 1;
+            if constexpr (PHASE == 1) { ev(a.b.act, ui_out) = gdeg_out; ev(a.b.act + N, ui_out) = dcmdl_out; ev(a.b.act + (2) * N, ui_out) = dcmdr_out; }
             if constexpr (WIND) {
-                a.b.wind[i] = fu0; a.b.wind[N + i] = fu1; a.b.wind[2 * N + i] = fv0; a.b.wind[3 * N + i] = fv1;
+                ev(a.b.wind, ui_out) = fu0; ev(a.b.wind + N, ui_out) = fu1; ev(a.b.wind + (2) * N, ui_out) = fv0; ev(a.b.wind + (3) * N, ui_out) = fv1;
             }
         }
     }
     // neighbourhood caches survive resets (any valid 50-set is a correct start)
     if (part == 0 && valid) {
-        a.b.key[my_table * N + i] = cA.key; a.b.slot[my_table * N + i] = cA.slot;
-        if constexpr (LPE == 1) { a.b.key[N + i] = cB.key; a.b.slot[N + i] = cB.slot; }
+        ev(a.b.key + (my_table) * N, ui_out) = cA.key; ev(a.b.slot + (my_table) * N, ui_out) = cA.slot;
+        if constexpr (LPE == 1) { ev(a.b.key + N, ui_out) = cB.key; ev(a.b.slot + N, ui_out) = cB.slot; }
     }
     if (!ended && valid) {
 #pragma unroll
         for (int k = 0; k < 11; ++k)
-            if (k % LPE == role) a.b.st[k * N + i] = s[k];
+            if (k % LPE == role) ev(a.b.st + (k) * N, ui_out) = s[k];
     }
 }
 
@@ -1203,7 +1216,8 @@ template <typename R> void fill_params(const pd_params* p, const pd_config* c, D
 
 pd_status validate(const pd_params* p, const pd_config* c) {
     if (!p || !c) return fail(PD_ERR_INVALID, "null params/config");
-    if (c->n_envs <= 0 || c->n_envs > (int64_t)1 << 31) return fail(PD_ERR_INVALID, "n_envs out of range");
+    // per-lane byte offsets in k_step are 32-bit (largest per-env row: noise, 64 B)
+    if (c->n_envs <= 0 || c->n_envs > (int64_t)1 << 25) return fail(PD_ERR_INVALID, "n_envs out of range (1 .. 2^25 per handle)");
     if (c->phase != PD_PHASE_PURE_THROTTLE && c->phase != PD_PHASE_LANDING_BURN) return fail(PD_ERR_INVALID, "bad phase");
     if (c->rtd != PD_RTD_RL && c->rtd != PD_RTD_PSO) return fail(PD_ERR_INVALID, "bad rtd");
     if (c->rtd == PD_RTD_RL && c->phase != PD_PHASE_PURE_THROTTLE)

@@ -26,6 +26,9 @@ for s in $STAGES; do
     sweep) stage sweep 600 python tools/sweep.py ;;
     pmc) stage pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run -- python3 bench.py --steps 20 --warmup 5 --cpu-baseline 0 --secondary 0
          stage pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o run -- python3 bench.py --steps 20 --warmup 5 --cpu-baseline 0 --secondary 0 ;;
+    pmc32) stage pmc_fetch32 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch32 -o run -- python3 bench.py --steps 20 --warmup 5 --cpu-baseline 0 --secondary 0 --precision f32
+         stage pmc_write32 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write32 -o run -- python3 bench.py --steps 20 --warmup 5 --cpu-baseline 0 --secondary 0 --precision f32 ;;
+    avail) stage avail 300 rocprofv3 --list-avail ;;
     pmcv) stage pmc_valu 600 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES --output-format csv -d gpurun_out/pmc_valu -o run -- python3 bench.py --steps 20 --warmup 5 --cpu-baseline 0 --secondary 0 ;;
   esac
 done
