@@ -494,8 +494,8 @@ template <bool WIND> struct Lds {
 };
 
 template <typename R, int PHASE, int RTD, bool WIND, int LPE>
-// waves_per_eu(2): the f64 kernel would otherwise spill its last VGPRs into AGPRs and run at one
-// wave per SIMD; two waves with a small scratch spill measured 20% faster (LPE 2, c3 workload).
+// waves_per_eu(2): caps VGPR+AGPR at 256 so the f64 kernel keeps two waves per SIMD (without it
+// the allocator spilled into AGPRs and ran one wave per SIMD, 20% slower on the c3 workload).
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) void k_step(StepArgs<R> a) {
     using L = Lds<WIND>;
     __shared__ R lds[L::kTotal];
