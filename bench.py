@@ -35,6 +35,36 @@ def algorithmic_bytes(precision, phase, wind, obs_dim, act_dim):
     return rd + wr
 
 
+def shard_offset(rank, n_per_rank):
+    """Global index of a rank's first env: contiguous shards, disjoint Philox streams."""
+    return rank * n_per_rank
+
+
+def whole_job_rate(n_per_rank, world, steps, wall_max):
+    """env-steps/s of the whole job: every rank's envs x steps over the slowest rank's time."""
+    return n_per_rank * world * steps / wall_max
+
+
+def timed_region(step_fn, steps, sync, dist=None, device="cpu"):
+    """barrier + sync, exactly `steps` calls of step_fn(k), sync + barrier; max wall over ranks."""
+    import torch
+    if dist:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for k in range(steps):
+        step_fn(k)
+    sync()
+    if dist:
+        dist.barrier()
+    wall = time.perf_counter() - t0
+    if dist:
+        w = torch.tensor([wall], device=device, dtype=torch.float64)
+        dist.all_reduce(w, op=dist.ReduceOp.MAX)
+        wall = float(w.item())
+    return wall
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -66,7 +96,7 @@ def main():
         env = pdenv.PoweredDescentEnv(
             n, flight_phase=args.phase, mode=mode, precision=precision, device=local,
             enable_wind=not args.no_wind, stochastic_wind=not args.no_wind, wind_percentile=None,
-            auto_reset=True, tilt_sigma_rad=math.radians(1.0), seed=1234, env_offset=rank * n)
+            auto_reset=True, tilt_sigma_rad=math.radians(1.0), seed=1234, env_offset=shard_offset(rank, n))
         env.flush_every = 16
         T = args.warmup + args.steps
         g = torch.Generator(device=env.device).manual_seed(42 + rank)
@@ -75,23 +105,13 @@ def main():
             env.step_raw(acts[t])
         torch.cuda.synchronize()
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-        if dist:
-            dist.barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for k in range(args.steps):
+
+        def one(k):
             ev[k][0].record()
             env.step_raw(acts[args.warmup + k])
             ev[k][1].record()
-        torch.cuda.synchronize()
-        if dist:
-            dist.barrier()
-        wall = time.perf_counter() - t0
+        wall = timed_region(one, args.steps, torch.cuda.synchronize, dist, env.device)
         kern_ms = sorted(a.elapsed_time(b) for a, b in ev)
-        w = torch.tensor([wall], device=env.device, dtype=torch.float64)
-        if dist:
-            dist.all_reduce(w, op=dist.ReduceOp.MAX)
-        wall = float(w.item())
         c = env.counters()
         res = dict(wall=wall, kern_avg_ms=sum(kern_ms) / len(kern_ms), kern_med_ms=kern_ms[len(kern_ms) // 2],
                    n=n, obs_dim=env.obs_dim, act_dim=env.action_dim, counters=c)
@@ -107,7 +127,7 @@ def main():
             dist.destroy_process_group()
         return
     n_total = main_res["n"] * world
-    value = n_total * args.steps / main_res["wall"]
+    value = whole_job_rate(main_res["n"], world, args.steps, main_res["wall"])
     wind = not args.no_wind
     bpe = algorithmic_bytes(args.precision, args.phase, wind, main_res["obs_dim"], main_res["act_dim"])
     achieved = bpe * main_res["n"] / (main_res["kern_avg_ms"] * 1e-3) / 1e9
@@ -142,21 +162,24 @@ def main():
     }
     if other is not None:
         op = "f32" if args.precision == "f64" else "f64"
-        out["secondary"] = {"dtype": op, "value": other["n"] * world * args.steps / other["wall"],
+        out["secondary"] = {"dtype": op, "value": whole_job_rate(other["n"], world, args.steps, other["wall"]),
                             "kernel_avg_ms": other["kern_avg_ms"]}
     if args.cpu_baseline and world == 1:
         sys.path.insert(0, os.path.join(REPO, "oracle"))
         import numpy as np
         import oracle
-        ne, ns = 64, 600
+        # all host threads this job may use (the GPU box exports OMP_NUM_THREADS = its CPU share)
+        thr = max(1, min(int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)), os.cpu_count() or 1, 64))
+        ne, ns = 64 * thr, 600
         acts = np.random.default_rng(0).uniform(-1, 1, (ns, ne, 1)).astype(np.float32)
         oracle.rollout(0, 0, 2, 2, acts[:2, :2], True, wind, math.radians(1.0))
         t0 = time.perf_counter()
-        _, nsteps = oracle.rollout(0, 0, ne, ns, acts, True, wind, math.radians(1.0))
+        _, nsteps = oracle.rollout(0, 0, ne, ns, acts, True, wind, math.radians(1.0), threads=thr)
         dt = time.perf_counter() - t0
-        out["cpu_baseline"] = {"value": nsteps / dt, "unit": "env-steps/s", "cores": 1, "kind": "port",
-                               "sample": f"oracle/pd_oracle.c scalar port, {ne} envs x {ns} steps of the same "
-                                         f"workload (wind+tilt+auto-reset), 1 host thread, {dt:.1f} s"}
+        out["cpu_baseline"] = {"value": nsteps / dt, "unit": "env-steps/s", "cores": thr, "kind": "port",
+                               "sample": f"oracle/pd_oracle.c scalar port on {thr} host threads (static env "
+                                         f"partition), {ne} envs x {ns} steps of the same workload "
+                                         f"(wind+tilt+auto-reset), {dt:.1f} s"}
     print(json.dumps(out))
     if dist:
         dist.destroy_process_group()

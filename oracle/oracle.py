@@ -103,6 +103,9 @@ def lib():
         L.orc_rollout_ex.restype = D
         L.orc_rollout_ex.argtypes = [P(OrcParams), C.c_int, C.c_int, C.c_int, C.c_int, P(C.c_float),
                                      C.c_int, C.c_int, D, C.c_uint64, P(C.c_int64)]
+        L.orc_rollout_mt.restype = D
+        L.orc_rollout_mt.argtypes = [P(OrcParams), C.c_int, C.c_int, C.c_int, C.c_int, P(C.c_float),
+                                     C.c_int, C.c_int, D, C.c_uint64, C.c_int, P(C.c_int64)]
         L.orc_rollout.restype = D
         L.orc_rollout.argtypes = [P(OrcParams), C.c_int, C.c_int, C.c_int, C.c_int, P(C.c_float),
                                   C.c_int, P(C.c_int64)]
@@ -239,11 +242,12 @@ def atmosphere(alt):
 
 
 def rollout(phase, rtd, n_env, n_steps, actions_f32, auto_reset=True, wind=False, tilt=0.0, seed=1,
-            wind_percentile=50):
-    """Scalar CPU rollout (the cpu_baseline port): returns (sum of rewards, env-steps)."""
+            wind_percentile=50, threads=1):
+    """Scalar CPU rollout (the cpu_baseline port), on `threads` host threads over a static env
+    partition: returns (sum of rewards, env-steps)."""
     acts = np.ascontiguousarray(actions_f32, dtype=np.float32)
     steps = C.c_int64()
-    acc = lib().orc_rollout_ex(C.byref(params(wind_percentile)), phase, rtd, n_env, n_steps,
+    acc = lib().orc_rollout_mt(C.byref(params(wind_percentile)), phase, rtd, n_env, n_steps,
                                acts.ctypes.data_as(C.POINTER(C.c_float)), int(auto_reset), int(wind),
-                               float(tilt), int(seed), C.byref(steps))
+                               float(tilt), int(seed), int(threads), C.byref(steps))
     return acc, steps.value

@@ -5,6 +5,7 @@
 #include <math.h>
 #include <string.h>
 #include <stdlib.h>
+#include <pthread.h>
 
 #define N_NB 50
 #define N_SYS (N_NB + 3)
@@ -575,20 +576,22 @@ double orc_rollout(const orc_params* P, int phase, int rtd, int n_env, int n_ste
                    const float* actions, int auto_reset, int64_t* env_steps_out) {
     return orc_rollout_ex(P, phase, rtd, n_env, n_steps, actions, auto_reset, 0, 0.0, 1, env_steps_out);
 }
-double orc_rollout_ex(const orc_params* P, int phase, int rtd, int n_env, int n_steps,
-                      const float* actions, int auto_reset, int wind, double tilt, uint64_t seed,
-                      int64_t* env_steps_out) {
+/* Envs [i0, i1) of a rollout over n_env envs (actions [T][n_env][A]); own RNG stream. */
+static double rollout_range(const orc_params* P, int phase, int rtd, int i0, int i1, int n_env, int n_steps,
+                            const float* actions, int auto_reset, int wind, double tilt, uint64_t seed,
+                            int64_t* env_steps_out) {
     int A = phase == ORC_PHASE_PURE_THROTTLE ? 1 : 4;
+    int n = i1 - i0;
     uint64_t rng = seed ? seed : 1;
-    orc_env* envs = (orc_env*)malloc(sizeof(orc_env) * (size_t)n_env);
-    for (int i = 0; i < n_env; ++i) rollout_reset(P, &envs[i], wind, tilt, &rng);
+    orc_env* envs = (orc_env*)malloc(sizeof(orc_env) * (size_t)(n > 0 ? n : 1));
+    for (int i = 0; i < n; ++i) rollout_reset(P, &envs[i], wind, tilt, &rng);
     double acc = 0.0; int64_t steps = 0;
     orc_out o;
     double nz[8];
     for (int t = 0; t < n_steps; ++t) {
-        for (int i = 0; i < n_env; ++i) {
+        for (int i = 0; i < n; ++i) {
             double u[4];
-            for (int k = 0; k < A; ++k) u[k] = actions[((size_t)t * n_env + i) * A + k];
+            for (int k = 0; k < A; ++k) u[k] = actions[((size_t)t * n_env + i0 + i) * A + k];
             if (wind) for (int k = 0; k < 8; ++k) nz[k] = xs_normal(&rng);
             orc_step(P, &envs[i], phase, rtd, u, 1, wind ? nz : NULL, &o);
             acc += o.reward; ++steps;
@@ -596,6 +599,52 @@ double orc_rollout_ex(const orc_params* P, int phase, int rtd, int n_env, int n_
         }
     }
     free(envs);
+    if (env_steps_out) *env_steps_out = steps;
+    return acc;
+}
+
+double orc_rollout_ex(const orc_params* P, int phase, int rtd, int n_env, int n_steps,
+                      const float* actions, int auto_reset, int wind, double tilt, uint64_t seed,
+                      int64_t* env_steps_out) {
+    return rollout_range(P, phase, rtd, 0, n_env, n_env, n_steps, actions, auto_reset, wind, tilt, seed,
+                         env_steps_out);
+}
+
+typedef struct {
+    const orc_params* P; int phase, rtd, i0, i1, n_env, n_steps; const float* actions;
+    int auto_reset, wind; double tilt; uint64_t seed; double acc; int64_t steps;
+} rollout_job;
+
+static void* rollout_worker(void* p) {
+    rollout_job* j = (rollout_job*)p;
+    j->acc = rollout_range(j->P, j->phase, j->rtd, j->i0, j->i1, j->n_env, j->n_steps, j->actions,
+                           j->auto_reset, j->wind, j->tilt, j->seed, &j->steps);
+    return NULL;
+}
+
+/* The same rollout on n_threads host threads over a static contiguous env partition (the
+ * multi-core CPU baseline); thread k draws its wind noise from seed + k. */
+double orc_rollout_mt(const orc_params* P, int phase, int rtd, int n_env, int n_steps,
+                      const float* actions, int auto_reset, int wind, double tilt, uint64_t seed,
+                      int n_threads, int64_t* env_steps_out) {
+    if (n_threads < 1) n_threads = 1;
+    if (n_threads > n_env) n_threads = n_env;
+    rollout_job* jobs = (rollout_job*)calloc((size_t)n_threads, sizeof(rollout_job));
+    pthread_t* th = (pthread_t*)calloc((size_t)n_threads, sizeof(pthread_t));
+    for (int k = 0; k < n_threads; ++k) {
+        rollout_job* j = &jobs[k];
+        j->P = P; j->phase = phase; j->rtd = rtd; j->n_env = n_env; j->n_steps = n_steps;
+        j->i0 = (int)((int64_t)n_env * k / n_threads); j->i1 = (int)((int64_t)n_env * (k + 1) / n_threads);
+        j->actions = actions; j->auto_reset = auto_reset; j->wind = wind; j->tilt = tilt;
+        j->seed = seed + (uint64_t)k;
+        pthread_create(&th[k], NULL, rollout_worker, j);
+    }
+    double acc = 0.0; int64_t steps = 0;
+    for (int k = 0; k < n_threads; ++k) {
+        pthread_join(th[k], NULL);
+        acc += jobs[k].acc; steps += jobs[k].steps;
+    }
+    free(jobs); free(th);
     if (env_steps_out) *env_steps_out = steps;
     return acc;
 }

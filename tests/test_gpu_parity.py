@@ -154,6 +154,27 @@ def test_device_solve_bit_identical(pd, precision, lpe):
     assert full.counters()["rbf_misses"] < cut.counters()["rbf_misses"]
 
 
+def test_env_shards_equal_single_handle(pd):
+    """Multi-GPU layout on one device: two handles over contiguous shards (env_offset = rank*n,
+    as bench.py assigns them) reproduce the single N-env handle bit for bit, wind + tilt +
+    random percentile + auto-reset included (the Philox streams depend on the global env)."""
+    import torch
+    N, T = 4096, 50
+    g = torch.Generator(device="cuda").manual_seed(3)
+    A = torch.rand(T, N, 1, device="cuda", generator=g) * 2 - 1
+    kw = dict(enable_wind=True, stochastic_wind=True, wind_percentile=None, auto_reset=True,
+              tilt_sigma_rad=0.02, seed=77)
+    whole = make(pd, N, **kw)
+    half = N // 2
+    shards = [make(pd, half, env_offset=r * half, **kw) for r in range(2)]
+    for t in range(T):
+        o, r, d, *_ = whole.step(A[t])
+        parts = [s.step(A[t, k * half:(k + 1) * half]) for k, s in enumerate(shards)]
+        assert torch.equal(r, torch.cat([p[1] for p in parts])), t
+        assert torch.equal(d, torch.cat([p[2] for p in parts])), t
+    assert torch.equal(whole.state, torch.cat([s.state for s in shards], dim=0))
+
+
 def test_auto_reset_and_full_size_properties(pd):
     """65 536 envs (config c3 size): auto-reset keeps every env in a valid episode; time
     advances by exactly 0.1 s per step; mass never increases; counters sane."""

@@ -1,0 +1,93 @@
+"""The N > 1 path on CPU: world_size-2 `gloo` process groups (no GPU).
+
+bench.py shards the env batch contiguously (`shard_offset`), steps each shard with no data-path
+collective, brackets the timed region with barriers and reports the max over ranks
+(`timed_region`, `whole_job_rate`).  These tests run those helpers on two gloo ranks, and
+check with the CPU oracle that sharding does not change any env's result: the per-rank shards,
+all-gathered (the transition gather of SURVEY config c5), equal the single-process batch.
+"""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "oracle"))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _init(rank, world, port):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+
+
+def _timing_worker(rank, world, port, out):
+    import time
+    import bench
+    _init(rank, world, port)
+    wall = bench.timed_region(lambda k: time.sleep(0.004 * (rank + 1)), 5, lambda: None, dist, "cpu")
+    out[rank] = wall
+    dist.destroy_process_group()
+
+
+def test_timed_region_reports_max_over_ranks():
+    world, port = 2, _free_port()
+    with mp.Manager() as m:
+        out = m.dict()
+        mp.spawn(_timing_worker, args=(world, port, out), nprocs=world, join=True)
+        walls = [out[r] for r in range(world)]
+    import bench
+    assert walls[0] == walls[1]                 # every rank reports the same (max) time
+    assert walls[0] >= 5 * 0.008                # at least the slow rank's own work
+    assert bench.whole_job_rate(100, world, 5, walls[0]) == pytest.approx(1000 / walls[0])
+    assert [bench.shard_offset(r, 100) for r in range(world)] == [0, 100]
+
+
+def _episode(global_env, n_steps):
+    """The oracle run of one env whose actions depend only on its GLOBAL index."""
+    import oracle
+    rng = np.random.default_rng(1000 + global_env)
+    acts = rng.uniform(-1, 1, (n_steps, 1)).astype(np.float32)
+    o = oracle.Oracle(phase=0, rtd=0)
+    rew = 0.0
+    for t in range(n_steps):
+        s, r, d, tr, tid, ob, info = o.step(acts[t], f32=True)
+        rew += r
+        if d or tr:
+            break
+    return np.concatenate([o.state, [rew]])
+
+
+def _shard_worker(rank, world, port, n_per_rank, n_steps, out):
+    import bench
+    _init(rank, world, port)
+    off = bench.shard_offset(rank, n_per_rank)
+    mine = torch.tensor(np.stack([_episode(off + i, n_steps) for i in range(n_per_rank)]))
+    gathered = [torch.empty_like(mine) for _ in range(world)]
+    dist.all_gather(gathered, mine)
+    if rank == 0:
+        out["all"] = torch.cat(gathered).numpy()
+    dist.destroy_process_group()
+
+
+def test_sharded_envs_equal_single_batch(oracle_mod):
+    world, n_per_rank, n_steps = 2, 3, 25
+    port = _free_port()
+    with mp.Manager() as m:
+        out = m.dict()
+        mp.spawn(_shard_worker, args=(world, port, n_per_rank, n_steps, out), nprocs=world, join=True)
+        got = out["all"]
+    ref = np.stack([_episode(g, n_steps) for g in range(world * n_per_rank)])
+    assert np.array_equal(got, ref)
