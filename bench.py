@@ -65,6 +65,62 @@ def timed_region(step_fn, steps, sync, dist=None, device="cpu"):
     return wall
 
 
+def bench_pso(args, world, rank, local, dist):
+    """Config c4: PSO generations of pso_wrapped_env.objective_function over P particles per GPU
+    (phase landing_burn, 372-parameter simple_actor per particle, positions U(-1.5, 1.5) as the
+    swarm is initialised), the actor fused into the step kernel (pd_rollout_policy).  One timed
+    step = one generation: every particle's episode until done/truncated (cap 2200)."""
+    import torch
+    import pdenv
+    P = args.particles
+    env = pdenv.PoweredDescentEnv(P, flight_phase="landing_burn", mode="pso", precision=args.precision,
+                                  device=local, seed=1234, env_offset=shard_offset(rank, P))
+    g = torch.Generator(device=env.device).manual_seed(7 + rank)
+    T = args.warmup + args.steps
+    W = (torch.rand(T, P, 372, generator=g, device=env.device) * 3 - 1.5).contiguous()
+    for t in range(args.warmup):
+        env.rollout_policy(W[t], max_steps=2200, check_every=16)
+    torch.cuda.synchronize()
+    tot = torch.zeros((), dtype=torch.int64, device=env.device)
+
+    def one(k):
+        fit, steps = env.rollout_policy(W[args.warmup + k], max_steps=2200, check_every=16)
+        tot.add_(steps.sum())
+    wall = timed_region(one, args.steps, torch.cuda.synchronize, dist, env.device)
+    if dist:
+        dist.all_reduce(tot)
+    if rank != 0:
+        if dist:
+            dist.destroy_process_group()
+        return
+    env_steps = int(tot.item())
+    eps = whole_job_rate(P, world, args.steps, wall)
+    out = {
+        "metric": "PSO particle-episodes/sec (c4, fused actor)", "value": eps, "unit": "particle-episodes/s",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": wall / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": args.precision,
+        "data": "synthetic (actor parameters U(-1.5,1.5) per particle, nominal initial state, no wind)",
+        "config": {"workload": "c4: PSO generation, landing_burn, 372-param simple_actor fused in k_step",
+                   "particles_per_gpu": P, "global_particles": P * world, "parallelism": f"particle-shard x{world}"},
+        "env_steps_per_s": env_steps / wall, "mean_episode_len": env_steps / (P * world * args.steps),
+    }
+    if args.cpu_baseline and world == 1:
+        sys.path.insert(0, os.path.join(REPO, "oracle"))
+        import numpy as np
+        import oracle
+        Wc = np.random.default_rng(0).uniform(-1.5, 1.5, (2048, 372)).astype(np.float32)
+        t0 = time.perf_counter()
+        _, st = oracle.rollout_policy(1, Wc, 2200)
+        dt = time.perf_counter() - t0
+        out["cpu_baseline"] = {"value": len(Wc) / dt, "unit": "particle-episodes/s", "cores": 1, "kind": "port",
+                               "sample": f"oracle/pd_oracle.c orc_rollout_policy, {len(Wc)} particles "
+                                         f"({int(st.sum())} env-steps), 1 host thread, {dt:.1f} s"}
+    print(json.dumps(out))
+    if dist:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -76,6 +132,9 @@ def main():
     ap.add_argument("--no-wind", action="store_true")
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--secondary", type=int, default=1, help="also time the other precision")
+    ap.add_argument("--workload", choices=["c3", "c4"], default="c3",
+                    help="c3: env-steps/s headline; c4: PSO generations with the fused actor")
+    ap.add_argument("--particles", type=int, default=32768, help="c4: particles per GPU")
     args = ap.parse_args()
 
     import torch
@@ -89,6 +148,8 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     torch.cuda.set_device(local)
     import pdenv
+    if args.workload == "c4":
+        return bench_pso(args, world, rank, local, dist)
 
     def run(precision):
         n = args.envs

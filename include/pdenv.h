@@ -13,7 +13,9 @@
  *                  g-load window, truncated_func -> done_func -> reward_func, plus the wrapper's
  *                  observation (env_wrapped_rl_pytorch.py:167-202 / env_wrapped_ea.py:97-123)
  *   pd_get_state/pd_set_state <- .state attribute (teacher forcing, checkpoint, perturbation)
- *   pd_truncation_ids <- rl_wrapped_env_pytorch.truncation_id (env_wrapped_rl_pytorch.py:117-118)
+ *   trunc_id output of pd_step <- rl_wrapped_env_pytorch.truncation_id (env_wrapped_rl_pytorch.py:117-118)
+ *   pd_rollout_policy <- pso_wrapped_env.objective_function + simple_actor.forward for a batch of
+ *                  particles (env_wrapped_ea.py:18-44, 200-222; particle_swarm_optimisation.py:334-350)
  *
  * Conventions: plain C, no torch types.  All array arguments are DEVICE pointers (HBM) owned by
  * the caller, laid out env-major [N] or [N][k]; `stream` is a hipStream_t (NULL = default).
@@ -38,6 +40,10 @@ extern "C" {
 #define PD_N_WIND_PROFILES 50   /* integer percentiles 50..99 */
 #define PD_N_STATE 11       /* x y vx vy theta theta_dot gamma alpha mass mass_propellant time */
 #define PD_N_INFO 16        /* see pd_info_field */
+/* simple_actor sizes of the PSO drivers (env_wrapped_ea.py:18-36, 174-185):
+ * pure throttle 2-8-(8-8)x3-1, landing_burn 5-8-(8-8)x4-4 */
+#define PD_ACTOR_PARAMS_PURE_THROTTLE 249
+#define PD_ACTOR_PARAMS_LANDING_BURN 372
 
 typedef enum { PD_OK = 0, PD_ERR_INVALID = 1, PD_ERR_HIP = 2, PD_ERR_NOMEM = 3, PD_ERR_UNSUPPORTED = 4 } pd_status;
 typedef enum { PD_PHASE_PURE_THROTTLE = 0, PD_PHASE_LANDING_BURN = 1 } pd_phase;   /* 1 resp. 4 actions */
@@ -132,6 +138,17 @@ pd_status pd_step(pd_env* env, const void* actions, void* obs, void* reward, uin
  * rewards accumulated into reward_sum [N] (may be NULL).  No host synchronisation. */
 pd_status pd_rollout(pd_env* env, const void* actions, int32_t n_steps, void* reward_sum,
                      void* stream);
+/* PSO objective for a batch of particles, one env per particle, on the device:
+ * pso_wrapped_env.objective_function (env_wrapped_ea.py:200-222) driven by simple_actor
+ * (env_wrapped_ea.py:18-44) evaluated inside the step kernel.  Resets every env, then steps
+ * each until done or truncated (or max_steps), accumulating fitness = -sum(reward).
+ *  weights : [n_params][N] float32, parameter-major (named_parameters() order per particle)
+ *  n_params: PD_ACTOR_PARAMS_* for the handle's phase; the handle must have rtd = PD_RTD_PSO
+ *  fitness : [N] (handle precision); steps: [N] int32 episode lengths (may be NULL)
+ *  check_every: >0 = read the finished-env count every that many steps and stop early when all
+ *            envs are done (one host sync per check); 0 = always run max_steps launches. */
+pd_status pd_rollout_policy(pd_env* env, const float* weights, int32_t n_params, int32_t max_steps,
+                            void* fitness, int32_t* steps, int32_t check_every, void* stream);
 /* Insert the aero neighbourhoods solved on device since the last flush into the handle's
  * tables (one tiny kernel; a no-op when nothing missed).  Call every few steps: a missed
  * neighbourhood is solved exactly on every lookup until it is flushed. */

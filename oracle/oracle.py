@@ -106,6 +106,9 @@ def lib():
         L.orc_rollout_mt.restype = D
         L.orc_rollout_mt.argtypes = [P(OrcParams), C.c_int, C.c_int, C.c_int, C.c_int, P(C.c_float),
                                      C.c_int, C.c_int, D, C.c_uint64, C.c_int, P(C.c_int64)]
+        L.orc_actor.argtypes = [P(OrcParams), C.c_int, P(C.c_float), P(D), P(C.c_float)]
+        L.orc_rollout_policy.argtypes = [P(OrcParams), C.c_int, C.c_int, P(C.c_float), C.c_int, P(D),
+                                         P(C.c_int32)]
         L.orc_rollout.restype = D
         L.orc_rollout.argtypes = [P(OrcParams), C.c_int, C.c_int, C.c_int, C.c_int, P(C.c_float),
                                   C.c_int, P(C.c_int64)]
@@ -251,3 +254,24 @@ def rollout(phase, rtd, n_env, n_steps, actions_f32, auto_reset=True, wind=False
                                acts.ctypes.data_as(C.POINTER(C.c_float)), int(auto_reset), int(wind),
                                float(tilt), int(seed), int(threads), C.byref(steps))
     return acc, steps.value
+
+
+def actor(phase, w, state):
+    """simple_actor.forward on the PSO observation of `state` (oracle restatement)."""
+    w = np.ascontiguousarray(w, dtype=np.float32)
+    s = np.ascontiguousarray(state, dtype=np.float64)
+    out = np.zeros(4, dtype=np.float32)
+    lib().orc_actor(C.byref(params()), phase, w.ctypes.data_as(C.POINTER(C.c_float)),
+                    s.ctypes.data_as(C.POINTER(C.c_double)), out.ctypes.data_as(C.POINTER(C.c_float)))
+    return out[:1] if phase == 0 else out
+
+
+def rollout_policy(phase, W, max_steps=2200):
+    """PSO objective of every particle row of W (no wind): (fitness, steps)."""
+    W = np.ascontiguousarray(W, dtype=np.float32)
+    n = W.shape[0]
+    fit = np.zeros(n)
+    steps = np.zeros(n, dtype=np.int32)
+    lib().orc_rollout_policy(C.byref(params()), phase, n, W.ctypes.data_as(C.POINTER(C.c_float)), int(max_steps),
+                             fit.ctypes.data_as(C.POINTER(C.c_double)), steps.ctypes.data_as(C.POINTER(C.c_int32)))
+    return fit, steps

@@ -648,3 +648,70 @@ double orc_rollout_mt(const orc_params* P, int phase, int rtd, int n_env, int n_
     if (env_steps_out) *env_steps_out = steps;
     return acc;
 }
+
+/* ---------------------------------------------------------------- PSO actor (test oracle)
+ * simple_actor.forward (env_wrapped_ea.py:18-44) on pso_wrapper.augment_state
+ * (env_wrapped_ea.py:97-123): Linear(IN,8)-ReLU-[Linear(8,8)-ReLU]xNL-Linear(8,OUT)-Tanh in
+ * binary32, parameters in named_parameters() order.  Summation order: sequential over the
+ * inputs, then + bias; tanh in binary64 rounded to binary32 (the order the GPU kernel uses;
+ * torch's CPU sgemv may round differently in the last ulp). */
+static void actor_layer(const float* w, const float* b, int in, int out, const float* x, float* y, int act) {
+    for (int j = 0; j < out; ++j) {
+        float acc = 0.f;
+        for (int k = 0; k < in; ++k) acc = acc + w[j * in + k] * x[k];
+        acc = acc + b[j];
+        if (act == 0) y[j] = acc < 0.f ? 0.f : acc;
+        else y[j] = (float)tanh((double)acc);
+    }
+}
+
+void orc_actor(const orc_params* P, int phase, const float* w, const double* s, float* out) {
+    float x[5], h[8], g[8];
+    int in, nl, nout;
+    if (phase == ORC_PHASE_PURE_THROTTLE) {
+        in = 2; nl = 3; nout = 1;
+        x[0] = (float)(s[1] / P->norm_y); x[1] = (float)(s[3] / P->norm_vy);
+    } else {
+        double k = atanh(0.75) / radians(25);
+        in = 5; nl = 4; nout = 4;
+        x[0] = (float)(s[0] / P->norm_x); x[1] = (float)(s[1] / P->norm_y);
+        x[2] = (float)(s[2] / P->norm_vx); x[3] = (float)(s[3] / P->norm_vy);
+        x[4] = (float)tanh(k * (s[4] - PI / 2));
+    }
+    const float* p = w;
+    actor_layer(p, p + 8 * in, in, 8, x, h, 0); p += 8 * in + 8;
+    for (int l = 0; l < nl; ++l) {
+        actor_layer(p, p + 64, 8, 8, h, g, 0); p += 72;
+        memcpy(h, g, sizeof(h));
+    }
+    actor_layer(p, p + 8 * nout, 8, nout, h, out, 1);
+}
+
+int orc_actor_params(int phase) { return phase == ORC_PHASE_PURE_THROTTLE ? 249 : 372; }
+
+/* pso_wrapped_env.objective_function (env_wrapped_ea.py:200-222) for n particles (weights
+ * [n][orc_actor_params(phase)]), each from the nominal initial state, no wind, until done or
+ * truncated or max_steps: fitness[i] = -sum(reward), steps[i] = episode length. */
+void orc_rollout_policy(const orc_params* P, int phase, int n, const float* w, int max_steps,
+                        double* fitness, int32_t* steps) {
+    int np_ = orc_actor_params(phase);
+    for (int i = 0; i < n; ++i) {
+        orc_env E;
+        orc_out o;
+        orc_reset(P, &E, NULL, 0, 0, 1.0, 1.0);
+        double fit = 0.0;
+        int t = 0;
+        while (t < max_steps) {
+            float a[4];
+            double u[4];
+            orc_actor(P, phase, w + (size_t)i * np_, E.s, a);
+            for (int k = 0; k < 4; ++k) u[k] = a[k];
+            orc_step(P, &E, phase, ORC_RTD_PSO, u, 1, NULL, &o);
+            fit -= o.reward;
+            ++t;
+            if (o.done || o.trunc) break;
+        }
+        fitness[i] = fit;
+        steps[i] = t;
+    }
+}

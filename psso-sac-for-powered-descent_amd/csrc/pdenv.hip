@@ -51,6 +51,7 @@ template <typename R> struct EnvBufs {
     int8_t* tid;      // [N] truncation id
     uint32_t* epi;    // [N] episode counter
     uint32_t* tstep;  // [N] step within episode
+    uint8_t* fin;     // [N] episode finished (policy rollouts: the env is frozen until reset)
 };
 
 struct Pending {
@@ -74,6 +75,8 @@ template <typename R> struct StepArgs {
     const double* noise;
     R* info;
     R* reward_sum;
+    const float* policy_w;           // policy rollouts: actor parameters [P][N] float32
+    unsigned long long* n_done;      // policy rollouts: envs whose episode has ended
 };
 
 // Per-env element `i` of a wave-uniform base pointer, addressed as base + zero-extended 32-bit
@@ -109,6 +112,7 @@ __device__ void reset_env(const StepArgs<R>& a, int64_t i, uint32_t episode, boo
     ev(a.b.act, ui) = R(0); ev(a.b.act + N, ui) = R(0); ev(a.b.act + (2) * N, ui) = R(0);
     ev(a.b.tid, ui) = 0;
     ev(a.b.epi, ui) = episode; ev(a.b.tstep, ui) = 0;
+    ev(a.b.fin, ui) = 0;
     // wind: VKDisturbanceGenerator._new_filters (vonkarman.py:60-66): sigmas drawn per reset,
     // filter state zeroed; WindModel.compile_horizontal_fixed_wind: percentile per reset
     u32x4 r = philox({(uint32_t)g, (uint32_t)(g >> 32) ^ episode, 0u, kTagReset}, a.seed_lo, a.seed_hi);
@@ -488,12 +492,57 @@ template <typename R> __device__ __forceinline__ R cl_query(R ae, R& sgn, bool& 
 }
 
 // ---------------------------------------------------------------- the step kernel
+// simple_actor.forward (env_wrapped_ea.py:18-44): Linear(IN,8)-ReLU-[Linear(8,8)-ReLU]xNL-
+// Linear(8,OUT)-Tanh in binary32 on the float32-cast observation.  Parameters are in
+// named_parameters() order (weight [out][in] row-major, then bias, layer by layer), stored
+// parameter-major [P][N] so that every load is coalesced across the envs of a wave.
+// Each output is the sequential sum over inputs (no FMA) plus the bias; tanh is evaluated in
+// binary64 and rounded (the oracle restates the same order: oracle/pd_oracle.c orc_actor).
+template <int IN, int NL, int OUT>
+__device__ __forceinline__ void actor_forward(const float* __restrict__ W, int64_t N, uint32_t ui,
+                                              const float* x, float* y) {
+    constexpr int H = 8;
+    float h[H], g[H];
+    int64_t p = 0;
+#pragma unroll
+    for (int j = 0; j < H; ++j) {
+        float acc = 0.f;
+#pragma unroll
+        for (int k = 0; k < IN; ++k) acc = acc + ev(W + (p + j * IN + k) * N, ui) * x[k];
+        acc = acc + ev(W + (p + H * IN + j) * N, ui);
+        h[j] = acc < 0.f ? 0.f : acc;
+    }
+    p += H * IN + H;
+#pragma unroll
+    for (int l = 0; l < NL; ++l) {
+#pragma unroll
+        for (int j = 0; j < H; ++j) {
+            float acc = 0.f;
+#pragma unroll
+            for (int k = 0; k < H; ++k) acc = acc + ev(W + (p + j * H + k) * N, ui) * h[k];
+            acc = acc + ev(W + (p + H * H + j) * N, ui);
+            g[j] = acc < 0.f ? 0.f : acc;
+        }
+#pragma unroll
+        for (int j = 0; j < H; ++j) h[j] = g[j];
+        p += H * H + H;
+    }
+#pragma unroll
+    for (int j = 0; j < OUT; ++j) {
+        float acc = 0.f;
+#pragma unroll
+        for (int k = 0; k < H; ++k) acc = acc + ev(W + (p + j * H + k) * N, ui) * h[k];
+        acc = acc + ev(W + (p + H * OUT + j) * N, ui);
+        y[j] = (float)tanh((double)acc);
+    }
+}
+
 template <bool WIND> struct Lds {
     static constexpr int kCd = 0, kCl = 256, kCaX = 512, kCaY = 576, kCnX = 640, kCnY = 704,
                          kWAlt = 768, kWSp = kWAlt + 800, kTotal = WIND ? kWSp + 800 : kWAlt;
 };
 
-template <typename R, int PHASE, int RTD, bool WIND, int LPE>
+template <typename R, int PHASE, int RTD, bool WIND, int LPE, int POL = 0>
 // waves_per_eu(2): caps VGPR+AGPR at 256 so the f64 kernel keeps two waves per SIMD (without it
 // the allocator spilled into AGPRs and ran one wave per SIMD, 20% slower on the c3 workload).
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) void k_step(StepArgs<R> a) {
@@ -529,6 +578,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
     const int64_t i = valid ? gt / LPE : N - 1;
     const int role = (int)(gt % LPE);
     const uint32_t ui = (uint32_t)i;   // N <= 2^25 (validated): 32-bit per-lane byte offsets
+    // POL (policy rollout): envs whose episode ended stay frozen; a wave with none left exits
+    // (wave-uniform, after the only workgroup barrier)
+    bool live_ = valid;
+    if constexpr (POL) {
+        live_ = live_ && ev(a.b.fin, ui) == 0;
+        if (__ballot(live_) == 0) return;
+    }
+    const bool live = live_;
     // role -> (table, part): LPE 1: both tables on one lane; else table = role / (LPE/2)
     constexpr int nparts = LPE >= 2 ? LPE / 2 : 1;
     const int my_table = LPE >= 2 ? role / nparts : 0;   // 0 = C_D, 1 = C_L
@@ -562,7 +619,19 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
     double ud[A];
 #pragma unroll
     for (int k = 0; k < A; ++k) { uf[k] = 0.f; ud[k] = 0.0; }
-    if (a.act_f64) {
+    if constexpr (POL) {
+        // pso_wrapper.augment_state (env_wrapped_ea.py:97-123) of the current state in the
+        // handle's precision, cast to float32 (simple_actor.forward), then the actor
+        const DevParams<R>& Q = *a.P;
+        if constexpr (PHASE == 0) {
+            float x[2] = {(float)(s[1] / Q.norm_y), (float)(s[3] / Q.norm_vy)};
+            actor_forward<2, 3, 1>(a.policy_w, N, ui, x, uf);
+        } else {
+            float x[5] = {(float)(s[0] / Q.norm_x), (float)(s[1] / Q.norm_y), (float)(s[2] / Q.norm_vx),
+                          (float)(s[3] / Q.norm_vy), (float)tanh(Q.k_theta_pso * (s[4] - Cst<R>::pi / R(2)))};
+            actor_forward<5, 4, 4>(a.policy_w, N, ui, x, uf);
+        }
+    } else if (a.act_f64) {
 #pragma unroll
         for (int k = 0; k < A; ++k) ud[k] = ev((const double*)a.actions + k, ui * A);
     } else {
@@ -762,13 +831,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
         mp -= mdot_dt; m -= mdot_dt;
         s[0] = x; s[1] = y; s[2] = vx; s[3] = vy; s[4] = th; s[5] = thd; s[6] = ga; s[7] = al;
         s[8] = m; s[9] = mp; s[10] = s[10] + dt;
-        if (sub == 3 && a.info && role == 0 && valid) {   // info of the last sub-step (rockets_physics.py:649-702)
+        if (sub == 3 && a.info && role == 0 && live) {   // info of the last sub-step (rockets_physics.py:649-702)
             R vals[PD_N_INFO - 1] = {rho, patm, asnd, mach, q, CL, CD, md_info, x_cog, I, ae, thr_info, ug, vg, gdeg_out};
 #pragma unroll
             for (int k = 0; k < PD_N_INFO - 1; ++k) ev(a.info + ((k < PD_INFO_GLOAD ? k : k + 1)) * N, ui) = vals[k];
         }
     }
-    if (nan_hit && role == 0 && valid) atomicAdd(&a.pend.stats[1], 1ull);
+    if (nan_hit && role == 0 && live) atomicAdd(&a.pend.stats[1], 1ull);
 
     // ---- g-load window (base_environment.py:136-149): ring of 10, Python sum() from the oldest
     const DevParams<R>& P2 = *launder(a.P);
@@ -856,8 +925,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
     // instead of keeping the load addresses live (spilled) across the sub-step loop
     uint32_t ui_out = ui;
     asm volatile("" : "+v"(ui_out));
-    const bool ended = a.auto_reset && (dn || tr);
-    if (role == 0 && valid) {
+    const bool ended = !POL && a.auto_reset && (dn || tr);
+    if (role == 0 && live) {
         if (a.obs) {
             if constexpr (RTD == 0) {
                 // GymnasiumWrapperPyTorch._process_state casts the raw state to float32 BEFORE
@@ -873,7 +942,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
             }
         }
         if (a.reward) ev(a.reward, ui_out) = rew;
-        if (a.reward_sum) ev(a.reward_sum, ui_out) += rew;
+        if constexpr (POL) {
+            // objective_function: episode_reward -= reward until done or truncated (env_wrapped_ea.py:200-222)
+            ev(a.reward_sum, ui_out) -= rew;
+            if (dn || tr) { ev(a.b.fin, ui_out) = 1; atomicAdd(a.n_done, 1ull); }
+        } else if (a.reward_sum) {
+            ev(a.reward_sum, ui_out) += rew;
+        }
         if (a.done) ev(a.done, ui_out) = (uint8_t)dn;
         if (a.trunc) ev(a.trunc, ui_out) = (uint8_t)tr;
         if (a.trunc_id) ev(a.trunc_id, ui_out) = (int8_t)id;
@@ -893,11 +968,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
         }
     }
     // neighbourhood caches survive resets (any valid 50-set is a correct start)
-    if (part == 0 && valid) {
+    if (part == 0 && live) {
         ev(a.b.key + (my_table) * N, ui_out) = cA.key; ev(a.b.slot + (my_table) * N, ui_out) = cA.slot;
         if constexpr (LPE == 1) { ev(a.b.key + N, ui_out) = cB.key; ev(a.b.slot + N, ui_out) = cB.slot; }
     }
-    if (!ended && valid) {
+    if (!ended && live) {
 #pragma unroll
         for (int k = 0; k < 11; ++k)
             if (k % LPE == role) ev(a.b.st + (k) * N, ui_out) = s[k];
@@ -1116,6 +1191,7 @@ struct pd_env {
     uint8_t *ghead = nullptr, *glen = nullptr, *wprof = nullptr;
     unsigned long long* key = nullptr; int* slot = nullptr;
     int8_t* tid = nullptr; uint32_t *epi = nullptr, *tstep = nullptr;
+    uint8_t* fin = nullptr; unsigned long long* n_done = nullptr;
     Pending pend{};
     unsigned long long *keys_cd = nullptr, *keys_cl = nullptr;
     void *pay_cd = nullptr, *pay_cl = nullptr;
@@ -1138,7 +1214,8 @@ template <typename R> StepArgs<R> make_args(pd_env* e) {
     a.P = (const DevParams<R>*)e->dparams;
     a.b.st = (R*)e->st; a.b.vprev = (R*)e->vprev; a.b.gwin = (R*)e->gwin; a.b.ghead = e->ghead; a.b.glen = e->glen;
     a.b.act = (R*)e->act; a.b.wind = (R*)e->wind; a.b.wprof = e->wprof; a.b.key = e->key; a.b.slot = e->slot;
-    a.b.tid = e->tid; a.b.epi = e->epi; a.b.tstep = e->tstep;
+    a.b.tid = e->tid; a.b.epi = e->epi; a.b.tstep = e->tstep; a.b.fin = e->fin;
+    a.n_done = e->n_done;
     a.pend = e->pend;
     a.n = e->cfg.n_envs;
     a.env_offset = e->cfg.env_offset;
@@ -1297,7 +1374,8 @@ template <typename R> pd_status create_impl(const pd_params* p, const pd_config*
         (st = dalloc(e, (void**)&e->glen, N)) || (st = dalloc(e, (void**)&e->wprof, N)) ||
         (st = dalloc(e, (void**)&e->key, 2 * N * 8)) || (st = dalloc(e, (void**)&e->slot, 2 * N * 4)) ||
         (st = dalloc(e, (void**)&e->tid, N)) || (st = dalloc(e, (void**)&e->epi, N * 4)) ||
-        (st = dalloc(e, (void**)&e->tstep, N * 4)))
+        (st = dalloc(e, (void**)&e->tstep, N * 4)) || (st = dalloc(e, (void**)&e->fin, N)) ||
+        (st = dalloc(e, (void**)&e->n_done, 8)))
         return st;
     PD_HIP(hipMemset(e->gwin, 0, 10 * N * R_));
     PD_HIP(hipMemset(e->epi, 0xff, N * 4));   // first reset -> episode 0
@@ -1337,6 +1415,11 @@ template <typename R> void dispatch_step(const pd_env* e, const StepArgs<R>& a, 
     else { if (w) launch_lpe<R, 1, 1, true>(l, a, s); else launch_lpe<R, 1, 1, false>(l, a, s); }
 }
 
+template <typename R, int PH, bool W> void launch_policy(const StepArgs<R>& a, hipStream_t s) {
+    unsigned grid = (unsigned)((a.n * 2 + kBlock - 1) / kBlock);
+    hipLaunchKernelGGL((k_step<R, PH, 1, W, 2, 1>), dim3(grid), dim3(kBlock), 0, s, a);
+}
+
 template <typename R> void launch_insert(pd_env* e, hipStream_t s) {
     hipLaunchKernelGGL(k_insert<R>, dim3(1), dim3(kPay), 0, s, e->pend, e->keys_cd, (R*)e->pay_cd, e->logcap_cd,
                        e->keys_cl, (R*)e->pay_cl, e->logcap_cl);
@@ -1349,6 +1432,35 @@ pd_status step_impl(pd_env* e, const void* actions, void* obs, void* reward, uin
     a.actions = actions; a.obs = (R*)obs; a.reward = (R*)reward; a.done = done; a.trunc = trunc; a.trunc_id = tid;
     a.noise = noise; a.info = (R*)info; a.reward_sum = (R*)reward_sum;
     dispatch_step<R>(e, a, s);
+    PD_HIP(hipGetLastError());
+    return PD_OK;
+}
+
+template <typename R>
+pd_status rollout_policy_impl(pd_env* e, const float* w, int32_t max_steps, void* fitness, int32_t* steps,
+                              int32_t check_every, hipStream_t s) {
+    const int64_t N = e->cfg.n_envs;
+    unsigned grid = (unsigned)((N + kBlock - 1) / kBlock);
+    hipLaunchKernelGGL(k_reset<R>, dim3(grid), dim3(kBlock), 0, s, make_args<R>(e), (const uint8_t*)nullptr);
+    PD_HIP(hipMemsetAsync(fitness, 0, (size_t)N * sizeof(R), s));
+    PD_HIP(hipMemsetAsync(e->n_done, 0, 8, s));
+    StepArgs<R> a = make_args<R>(e);
+    a.policy_w = w; a.reward_sum = (R*)fitness; a.auto_reset = 0;
+    const bool wind = e->cfg.enable_wind != 0;
+    for (int32_t t = 0; t < max_steps; ++t) {
+        if (e->cfg.phase == PD_PHASE_PURE_THROTTLE) { if (wind) launch_policy<R, 0, true>(a, s); else launch_policy<R, 0, false>(a, s); }
+        else { if (wind) launch_policy<R, 1, true>(a, s); else launch_policy<R, 1, false>(a, s); }
+        PD_HIP(hipGetLastError());
+        if ((t & 15) == 15) launch_insert<R>(e, s);
+        if (check_every > 0 && (t + 1) % check_every == 0 && t + 1 < max_steps) {
+            unsigned long long done = 0;
+            PD_HIP(hipMemcpyAsync(&done, e->n_done, 8, hipMemcpyDeviceToHost, s));
+            PD_HIP(hipStreamSynchronize(s));
+            if ((int64_t)done >= N) break;
+        }
+    }
+    launch_insert<R>(e, s);
+    if (steps) PD_HIP(hipMemcpyAsync(steps, e->tstep, (size_t)N * 4, hipMemcpyDeviceToDevice, s));
     PD_HIP(hipGetLastError());
     return PD_OK;
 }
@@ -1434,6 +1546,17 @@ pd_status pd_rollout(pd_env* e, const void* actions, int32_t n_steps, void* rewa
         if ((t & 15) == 15 || t + 1 == n_steps) { if ((st = pd_flush_misses(e, stream)) != PD_OK) return st; }
     }
     return PD_OK;
+}
+
+pd_status pd_rollout_policy(pd_env* e, const float* weights, int32_t n_params, int32_t max_steps, void* fitness,
+                            int32_t* steps, int32_t check_every, void* stream) {
+    if (!e || !weights || !fitness || max_steps < 0) return fail(PD_ERR_INVALID, "bad policy rollout args");
+    if (e->cfg.rtd != PD_RTD_PSO) return fail(PD_ERR_UNSUPPORTED, "policy rollouts need rtd = PD_RTD_PSO");
+    int want = e->cfg.phase == PD_PHASE_PURE_THROTTLE ? PD_ACTOR_PARAMS_PURE_THROTTLE : PD_ACTOR_PARAMS_LANDING_BURN;
+    if (n_params != want) return fail(PD_ERR_INVALID, "n_params does not match the phase's actor");
+    PD_HIP(hipSetDevice(e->device));
+    return e->rsize == 8 ? rollout_policy_impl<double>(e, weights, max_steps, fitness, steps, check_every, (hipStream_t)stream)
+                         : rollout_policy_impl<float>(e, weights, max_steps, fitness, steps, check_every, (hipStream_t)stream);
 }
 
 pd_status pd_flush_misses(pd_env* e, void* stream) {

@@ -17,6 +17,7 @@ PD_OK, PD_ERR_INVALID, PD_ERR_HIP, PD_ERR_NOMEM, PD_ERR_UNSUPPORTED = range(5)
 PURE_THROTTLE, LANDING_BURN = 0, 1
 RTD_RL, RTD_PSO = 0, 1
 F64, F32 = 0, 1
+ACTOR_PARAMS = {0: 249, 1: 372}   # PD_ACTOR_PARAMS_PURE_THROTTLE / _LANDING_BURN
 
 INFO_FIELDS = ["air_density", "atmospheric_pressure", "speed_of_sound", "mach_number",
                "dynamic_pressure", "CL", "CD", "mass_flow", "x_cog", "inertia",
@@ -63,7 +64,7 @@ class PdConfig(C.Structure):
 
 
 EXPORTS = ["pd_abi_version", "pd_sizeof_params", "pd_sizeof_config", "pd_last_error", "pd_device_count", "pd_create", "pd_destroy", "pd_reset",
-           "pd_step", "pd_rollout", "pd_flush_misses", "pd_observe", "pd_get_state", "pd_set_state", "pd_get_actuators",
+           "pd_step", "pd_rollout", "pd_rollout_policy", "pd_flush_misses", "pd_observe", "pd_get_state", "pd_set_state", "pd_get_actuators",
            "pd_set_actuators", "pd_set_wind_sigmas", "pd_counters", "pd_obs_dim", "pd_action_dim"]
 
 _lib = None
@@ -92,6 +93,7 @@ def load(path=None):
     L.pd_reset.argtypes = [vp, vp, vp, vp]
     L.pd_step.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
     L.pd_rollout.argtypes = [vp, vp, I32, vp, vp]
+    L.pd_rollout_policy.argtypes = [vp, vp, I32, I32, vp, vp, I32, vp]
     L.pd_observe.argtypes = [vp, vp, vp]
     L.pd_flush_misses.argtypes = [vp, vp]
     L.pd_get_state.argtypes = [vp, vp, vp]
@@ -102,7 +104,7 @@ def load(path=None):
     L.pd_counters.argtypes = [vp, P(I64), P(I64), P(I64), P(I64)]
     L.pd_obs_dim.argtypes = [vp]; L.pd_obs_dim.restype = C.c_int
     L.pd_action_dim.argtypes = [vp]; L.pd_action_dim.restype = C.c_int
-    for name in ("pd_create", "pd_destroy", "pd_reset", "pd_step", "pd_rollout", "pd_flush_misses", "pd_observe",
+    for name in ("pd_create", "pd_destroy", "pd_reset", "pd_step", "pd_rollout", "pd_rollout_policy", "pd_flush_misses", "pd_observe",
                  "pd_get_state", "pd_set_state", "pd_get_actuators", "pd_set_actuators",
                  "pd_set_wind_sigmas", "pd_counters"):
         getattr(L, name).restype = C.c_int

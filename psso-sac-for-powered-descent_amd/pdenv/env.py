@@ -178,6 +178,22 @@ class PoweredDescentEnv:
         L.check(self.lib.pd_set_wind_sigmas(self.h, _ptr(sig), _stream(self.device)))
         torch.cuda.current_stream(self.device).synchronize()
 
+    def rollout_policy(self, weights, max_steps=2200, check_every=64):
+        """PSO objective of N particles on the device (pd_rollout_policy): every env is reset and
+        driven by its own simple_actor until done/truncated or max_steps.
+        weights: [N, P] per-particle parameter vectors (named_parameters() order).
+        Returns (fitness [N] = -sum(reward), steps [N] int32) device tensors."""
+        w = torch.as_tensor(weights, dtype=torch.float32, device=self.device)
+        if w.dim() != 2 or w.shape[0] != self.n:
+            raise ValueError(f"weights must be [{self.n}, P]")
+        wt = w.t().contiguous()                       # parameter-major [P][N]: coalesced loads
+        fit = torch.empty(self.n, dtype=self.dtype, device=self.device)
+        steps = torch.empty(self.n, dtype=torch.int32, device=self.device)
+        L.check(self.lib.pd_rollout_policy(self.h, _ptr(wt), int(w.shape[1]), int(max_steps), _ptr(fit),
+                                           _ptr(steps), int(check_every), _stream(self.device)))
+        self._keep = wt                               # alive until the stream has consumed it
+        return fit, steps
+
     def counters(self):
         v = [L.I64() for _ in range(4)]
         L.check(self.lib.pd_counters(self.h, *[C.byref(x) for x in v]))

@@ -181,7 +181,8 @@ class pso_wrapped_env:
         return total
 
     def objective_function_batch(self, individuals, max_steps=2200):
-        """individuals [P, D] -> fitness [P] (device tensor), one episode per particle."""
+        """individuals [P, D] -> fitness [P] (device tensor), one episode per particle, with the
+        actor evaluated inside the step kernel (pd_rollout_policy)."""
         X = torch.as_tensor(np.asarray(individuals), dtype=torch.float32, device=f"cuda:{self.device}")
         P = X.shape[0]
         if self._batch_env is None or self._batch_env.n != P:
@@ -189,7 +190,18 @@ class pso_wrapped_env:
             self._batch_env = PoweredDescentEnv(P, self.flight_phase, mode="pso", precision=self.precision,
                                                 device=self.device, enable_wind=w[0], stochastic_wind=w[1],
                                                 wind_percentile=w[2], seed=self.seed)
-        env = self._batch_env
+        fit, steps = self._batch_env.rollout_policy(X, max_steps=max_steps)
+        self.last_batch_steps = steps
+        return fit
+
+    def objective_function_batch_torch(self, individuals, max_steps=2200):
+        """The same objective with the actor as batched torch.bmm between env steps (reference
+        check for the fused path; one kernel round trip per step)."""
+        X = torch.as_tensor(np.asarray(individuals), dtype=torch.float32, device=f"cuda:{self.device}")
+        P = X.shape[0]
+        w = self.wind
+        env = PoweredDescentEnv(P, self.flight_phase, mode="pso", precision=self.precision, device=self.device,
+                                enable_wind=w[0], stochastic_wind=w[1], wind_percentile=w[2], seed=self.seed)
         shapes = self.actor.shapes()
         Ws, idx = [], 0
         for (o, i) in shapes:
@@ -210,6 +222,7 @@ class pso_wrapped_env:
             obs = o2.float()
             if t % 32 == 31 and not bool(alive.any()):
                 break
+        env.close()
         return fit
 
     @property

@@ -100,7 +100,8 @@ def import_reference():
         import src.envs.rockets_physics as rp
         from src.envs.utils import acs_model, atmosphere_dynamics
         from src.envs.rl.env_wrapped_rl_pytorch import rl_wrapped_env_pytorch
-        from src.envs.pso.env_wrapped_ea import pso_wrapper
+        from src.envs.pso.env_wrapped_ea import pso_wrapper, pso_wrapped_env
+    import_reference.pso_wrapped_env = pso_wrapped_env
     return rp, acs_model, atmosphere_dynamics, rl_wrapped_env_pytorch, pso_wrapper
 
 
@@ -272,6 +273,45 @@ def wind_episodes(rl_env_cls):
     save("ref_wind_episodes.npz", **out)
 
 
+def pso_objective(pso_wrapped_env_cls):
+    """pso_wrapped_env.objective_function (env_wrapped_ea.py:200-222) on seeded particles of both
+    PSO phases: fitness, episode length, and per step the raw env state the actor saw and the
+    float32 action it returned (teacher-forced check of the fused actor)."""
+    import torch
+    torch.manual_seed(0)
+    out = {}
+    for tag, phase in (("pt", "landing_burn_pure_throttle"), ("lb", "landing_burn")):
+        with contextlib.redirect_stdout(io.StringIO()):
+            model = pso_wrapped_env_cls(flight_phase=phase, enable_wind=False, stochastic_wind=False,
+                                        horiontal_wind_percentile=50)
+        D = len(model.bounds)
+        rng = np.random.default_rng(11)
+        inds = np.concatenate([rng.uniform(-1.5, 1.5, (4, D)), rng.uniform(-0.5, 0.5, (4, D))])
+        base = model.env.env
+        fits, lens, states, acts, owner = [], [], [], [], []
+        for k, ind in enumerate(inds):
+            rec_s, rec_a = [], []
+            orig = model.env.step
+
+            def step(action, _orig=orig, _rs=rec_s, _ra=rec_a):
+                _rs.append(np.array(base.state, dtype=np.float64))
+                _ra.append(action.detach().numpy().astype(np.float32).reshape(-1))
+                return _orig(action)
+            model.env.step = step
+            with contextlib.redirect_stdout(io.StringIO()):
+                f = model.objective_function(ind)
+            model.env.step = orig
+            fits.append(f); lens.append(len(rec_a))
+            states += rec_s; acts += rec_a; owner += [k] * len(rec_a)
+        out[f"{tag}_individuals"] = inds
+        out[f"{tag}_fitness"] = np.array(fits)
+        out[f"{tag}_length"] = np.array(lens)
+        out[f"{tag}_states"] = np.array(states)
+        out[f"{tag}_actions"] = np.array(acts)
+        out[f"{tag}_owner"] = np.array(owner)
+    save("ref_pso_objective.npz", **out)
+
+
 def main():
     print("recorded fixtures", file=sys.stderr)
     recorded()
@@ -281,7 +321,12 @@ def main():
     print("teacher-forced steps", file=sys.stderr); teacher_forced(rp)
     print("episodes", file=sys.stderr); episodes(rl_env_cls, pso_wrapper_cls)
     print("wind episodes", file=sys.stderr); wind_episodes(rl_env_cls)
+    print("PSO objective", file=sys.stderr); pso_objective(import_reference.pso_wrapped_env)
 
 
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) > 1 and sys.argv[1] == "pso":     # only the PSO-objective fixture
+        _, _, _, _, _ = import_reference()
+        pso_objective(import_reference.pso_wrapped_env)
+    else:
+        main()

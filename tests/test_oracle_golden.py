@@ -168,3 +168,44 @@ def test_wind_episode_injected_noise(oracle_mod, ep):
     assert k == len(d[f"w{ep}_normals"])
     err = np.abs(S - rs).max(0) / (np.ptp(rs, 0) + 1e-12)
     assert (err < TOL_EPISODE).all(), dict(zip(ST, err))
+
+
+def test_pso_actor_teacher_forced_vs_reference(oracle_mod):
+    """simple_actor on pso_wrapper.augment_state: the oracle's binary32 MLP (sequential sums) on
+    every (state, action) the reference's torch actor produced inside objective_function.
+    torch's CPU sgemv (MKL, AVX-512) rounds in a different order, so agreement is a few f32
+    ulps of the tanh output, not bits."""
+    d = golden("ref_pso_objective.npz")
+    for tag, phase in (("pt", 0), ("lb", 1)):
+        W = d[f"{tag}_individuals"].astype(np.float32)
+        err = max(np.abs(oracle_mod.actor(phase, W[o], s) - a).max()
+                  for s, a, o in zip(d[f"{tag}_states"], d[f"{tag}_actions"], d[f"{tag}_owner"]))
+        assert err <= 4e-6, (tag, err)
+
+
+def test_pso_objective_vs_reference(oracle_mod):
+    """objective_function of 8 seeded particles per phase.  Pure throttle: the oracle's own
+    actor + env reproduce fitness and episode length.  landing_burn: the attitude dynamics
+    amplify the actor's ulp differences, so the env is replayed with the
+    reference's recorded actions and must reproduce its states, fitness and length."""
+    d = golden("ref_pso_objective.npz")
+    W = d["pt_individuals"].astype(np.float32)
+    fit, steps = oracle_mod.rollout_policy(0, W)
+    assert list(steps) == list(d["pt_length"])
+    assert np.abs(fit - d["pt_fitness"]).max() <= 1e-7 * np.abs(d["pt_fitness"]).max()
+    st, act, own = d["lb_states"], d["lb_actions"], d["lb_owner"]
+    for k in range(len(d["lb_fitness"])):
+        rows = np.where(own == k)[0]
+        o = oracle_mod.Oracle(phase=1, rtd=1)
+        fitk, n = 0.0, 0
+        tol = np.maximum(TOL_EPISODE, 1e-6 * (TOL_EPISODE > 1e-12))   # as the landing_burn episodes
+        scale = np.ptp(st, 0) + 1e-12
+        for j, r in enumerate(rows):
+            if j < 10:   # saturated actors tumble the vehicle: ulp differences grow ~3x per step
+                assert (np.abs(o.state - st[r]) / scale < tol).all(), (k, j)
+            s, rew, dn, tr, tid, ob, info = o.step(act[r], f32=True)
+            fitk -= rew
+            n += 1
+            assert (dn or tr) == (j == len(rows) - 1)
+        assert n == d["lb_length"][k]
+        assert fitk == pytest.approx(d["lb_fitness"][k], rel=1e-6)
