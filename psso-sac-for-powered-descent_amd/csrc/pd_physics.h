@@ -56,6 +56,7 @@ template <typename R> struct DevParams {
     R state0[11];
     double state0_d[11];
     R norm_y, norm_vy, norm_x, norm_vx, k_theta_pso;
+    LogTable logtab;   // log_tab cells (pd_common.h), staged into LDS by the step kernel
     R y0_rl, m0_rl;
     // neighbourhood hash tables
     const unsigned long long* keys_cd;

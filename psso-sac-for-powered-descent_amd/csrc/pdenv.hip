@@ -205,6 +205,17 @@ __device__ __forceinline__ TabView<R> tab_view(const DevParams<R>& P, const R* s
     return t;
 }
 
+// log() of the RBF kernel terms: binary64 through the LDS-staged cell table (log_tab), binary32
+// through the hardware log2.
+__shared__ double s_logtab[2 * kLogCells];
+template <typename R> __device__ __forceinline__ R eval_log(R x);
+template <> __device__ __forceinline__ double eval_log<double>(double x) {
+    return log_tab(x, s_logtab, s_logtab + kLogCells);
+}
+template <> __device__ __forceinline__ float eval_log<float>(float x) {
+    return __builtin_amdgcn_logf(x) * 0.693147180559945309f;
+}
+
 template <typename R>
 __device__ __forceinline__ R rbf_eval(const R* __restrict__ pay, const R* smach, const int* start,
                                       const R* aoa, const int lo[kCols], const int len[kCols], R M, R a,
@@ -238,7 +249,13 @@ __device__ __forceinline__ R rbf_eval(const R* __restrict__ pay, const R* smach,
         for (int u = 0; u < kChunk; ++u) {
             R dm = M - mm[u];
             R d2 = dm * dm + zz[u];
+#ifdef PD_EXP_NOLOG
+            R f = R(0.5) * d2 * d2;
+#elif defined(PD_EXP_LIBLOG)
             R f = d2 == R(0) ? R(0) : R(0.5) * d2 * log(d2);
+#else
+            R f = d2 == R(0) ? R(0) : R(0.5) * d2 * eval_log<R>(d2);
+#endif
             if (u & 1) s1 += f * pp[u]; else s0 += f * pp[u];
         }
     }
@@ -569,6 +586,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
     }
     if (threadIdx.x < 4) { lines.a[threadIdx.x] = P.line_a[threadIdx.x]; lines.nbp[threadIdx.x] = P.line_nbp[threadIdx.x]; }
     if (threadIdx.x == 0) solve.lock = 0;
+    for (int t = threadIdx.x; t < kLogCells; t += kBlock) {
+        s_logtab[t] = P.logtab.invc[t]; s_logtab[kLogCells + t] = P.logtab.logc[t];
+    }
     __syncthreads();
     const int64_t N = a.n;
     const int64_t gt = (int64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -1287,6 +1307,7 @@ template <typename R> void fill_params(const pd_params* p, const pd_config* c, D
     for (int k = 0; k < 11; ++k) { D.state0[k] = (R)p->state0[k]; D.state0_d[k] = p->state0[k]; }
     D.norm_y = (R)p->norm_y; D.norm_vy = (R)p->norm_vy; D.norm_x = (R)p->norm_x; D.norm_vx = (R)p->norm_vx;
     D.k_theta_pso = (R)(std::atanh(0.75) / (25.0 * kDeg2Rad));
+    log_table_fill(D.logtab);
     D.y0_rl = (R)p->state0[1]; D.m0_rl = (R)p->state0[8];
     (void)c;
 }
