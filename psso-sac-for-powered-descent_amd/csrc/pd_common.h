@@ -86,12 +86,12 @@ PD_HD double pd_log(double x) {
 PD_HD double tps(double r) { return r == 0.0 ? 0.0 : r * r * pd_log(r); }
 
 // Table-driven natural log for the RBF evaluation (the hot transcendental: 200 per lane per
-// env-step).  x = 2^e m, m in [1, 2); the top 7 mantissa bits pick a cell with rounded inverse
-// centre invc and logc = -log(invc); r = m * invc - 1 (one fma, |r| < 2^-7.9) and
-// log x = e ln2 + logc + log1p(r), log1p to degree 7 (truncation < 3e-18).  Absolute error
-// below 2 ulp of |log x| (host-checked against long double, tools/check_log.cpp); about a
-// third of the device library's double log.  Positive normal finite x only.
-constexpr int kLogCells = 128;
+// env-step).  x = 2^e m, m in [1, 2); the top 9 mantissa bits pick a cell with rounded inverse
+// centre invc and logc = -log(invc); r = m * invc - 1 (one fma, |r| < 2^-9.9) and
+// log x = e ln2 + logc + log1p(r), log1p to degree 5 (truncation < 2e-19).  Absolute error
+// below 5e-16 over the RBF's argument range (host-checked against long double); a third of
+// the device library's double log.  Positive normal finite x; x = 0 gives a finite value.
+constexpr int kLogBits = 9, kLogCells = 1 << kLogBits;
 struct LogTable { double invc[kLogCells], logc[kLogCells]; };
 inline void log_table_fill(LogTable& t) {
     for (int i = 0; i < kLogCells; ++i) {
@@ -102,23 +102,21 @@ inline void log_table_fill(LogTable& t) {
     }
 }
 PD_HD double log_tab(double x, const double* invc, const double* logc) {
-    const double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10;
+    const double ln2 = 6.93147180559945286227e-01;
     uint64_t b;
     __builtin_memcpy(&b, &x, 8);
     uint32_t hi = (uint32_t)(b >> 32);
     double e = (double)((int)(hi >> 20) - 1023);
-    uint32_t i = (hi >> 13) & (kLogCells - 1);
+    uint32_t i = (hi >> (20 - kLogBits)) & (kLogCells - 1);
     uint64_t mb = (b & 0x000fffffffffffffull) | 0x3ff0000000000000ull;
     double m;
     __builtin_memcpy(&m, &mb, 8);
     double r = fma(m, invc[i], -1.0);
-    double t = fma(r, 1.0 / 7.0, -1.0 / 6.0);
-    t = fma(r, t, 0.2);
-    t = fma(r, t, -0.25);
+    double t = fma(r, 0.2, -0.25);
     t = fma(r, t, 1.0 / 3.0);
     t = fma(r, t, -0.5);
     double p = fma(r * r, t, r);
-    return fma(e, ln2_hi, fma(e, ln2_lo, logc[i]) + p);
+    return fma(e, ln2, logc[i] + p);
 }
 
 // Build and solve the thin-plate-spline system of ONE 50-point neighbourhood, exactly the

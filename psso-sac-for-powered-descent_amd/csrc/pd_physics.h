@@ -80,6 +80,18 @@ template <typename R> struct DevParams {
     unsigned long long line_key[4][kLineMax + 1];
 };
 
+// ---------------------------------------------------------------- logarithms
+// Hot-path log(): binary64 through the LDS-staged cell table (log_tab, pd_common.h; the step
+// kernel stages it before its barrier), binary32 through the hardware log2.
+__shared__ double s_logtab[2 * kLogCells];
+template <typename R> __device__ __forceinline__ R eval_log(R x);
+template <> __device__ __forceinline__ double eval_log<double>(double x) {
+    return log_tab(x, s_logtab, s_logtab + kLogCells);
+}
+template <> __device__ __forceinline__ float eval_log<float>(float x) {
+    return __builtin_amdgcn_logf(x) * 0.693147180559945309f;
+}
+
 // ---------------------------------------------------------------- atmosphere
 // atmosphere_dynamics.py:5-27 (ambiance ISA restated)
 template <typename R>
@@ -94,7 +106,11 @@ __device__ __forceinline__ void atmosphere(const DevParams<R>& P, R y, R& rho, R
         R dH = H - Hb;
         R T = Tb + b * dH;
         R pp;
-        if (b != R(0)) pp = pb * pow(R(1) + P.isa_bt[i] * dH, P.isa_ex[i]);
+        // (1 + beta/Tb dH)^ex; binary64 as exp(ex log(.)) with the table log (|err| < 1e-15 rel)
+        if (b != R(0)) {
+            if constexpr (sizeof(R) == 8) pp = pb * exp(P.isa_ex[i] * eval_log<R>(R(1) + P.isa_bt[i] * dH));
+            else pp = pb * pow(R(1) + P.isa_bt[i] * dH, P.isa_ex[i]);
+        }
         else pp = pb * exp(P.isa_iso[i] * dH);
         p = pp;
         rho = pp / (P.isa_R * T);

@@ -205,17 +205,6 @@ __device__ __forceinline__ TabView<R> tab_view(const DevParams<R>& P, const R* s
     return t;
 }
 
-// log() of the RBF kernel terms: binary64 through the LDS-staged cell table (log_tab), binary32
-// through the hardware log2.
-__shared__ double s_logtab[2 * kLogCells];
-template <typename R> __device__ __forceinline__ R eval_log(R x);
-template <> __device__ __forceinline__ double eval_log<double>(double x) {
-    return log_tab(x, s_logtab, s_logtab + kLogCells);
-}
-template <> __device__ __forceinline__ float eval_log<float>(float x) {
-    return __builtin_amdgcn_logf(x) * 0.693147180559945309f;
-}
-
 template <typename R>
 __device__ __forceinline__ R rbf_eval(const R* __restrict__ pay, const R* smach, const int* start,
                                       const R* aoa, const int lo[kCols], const int len[kCols], R M, R a,
@@ -249,17 +238,20 @@ __device__ __forceinline__ R rbf_eval(const R* __restrict__ pay, const R* smach,
         for (int u = 0; u < kChunk; ++u) {
             R dm = M - mm[u];
             R d2 = dm * dm + zz[u];
+            // c_j d2 log(d2) accumulated (the 1/2 of phi = d2 log(d2) / 2 is applied once below);
+            // d2 = 0 (query on a table point) contributes c_j * 0 * finite = 0
+            R w = d2 * pp[u];
 #ifdef PD_EXP_NOLOG
-            R f = R(0.5) * d2 * d2;
+            R l = d2;
 #elif defined(PD_EXP_LIBLOG)
-            R f = d2 == R(0) ? R(0) : R(0.5) * d2 * log(d2);
+            R l = log(d2 > R(0) ? d2 : R(1));
 #else
-            R f = d2 == R(0) ? R(0) : R(0.5) * d2 * eval_log<R>(d2);
+            R l = eval_log<R>(sizeof(R) == 8 ? d2 : (d2 > R(1e-30) ? d2 : R(1e-30)));
 #endif
-            if (u & 1) s1 += f * pp[u]; else s0 += f * pp[u];
+            if (u & 1) s1 = fma(w, l, s1); else s0 = fma(w, l, s0);
         }
     }
-    R s = s0 + s1;
+    R s = R(0.5) * (s0 + s1);
     if (part == 0) {
         s += R(1) * pay[kNbr];
         s += (M - pay[kSys + 0]) / pay[kSys + 2] * pay[kNbr + 1];
@@ -697,9 +689,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
                 else {
                     u32x4 r = philox({(uint32_t)g, (uint32_t)(g >> 32) ^ ep, ts, kTagWindSub + (uint32_t)sub},
                                      a.seed_lo, a.seed_hi);
-                    double u1 = 1.0 - u01(r.x, r.y), u2 = u01(r.z, r.w);
-                    double rad = sqrt(-2.0 * log(u1));
-                    w0 = rad * cos(2.0 * kPi * u2); w1 = rad * sin(2.0 * kPi * u2);
+                    // Box-Muller in binary32 on 24-bit uniforms (hardware log2 and sin/cos of 2*pi*u):
+                    // the gust normals are random variates, their last bits carry no physics
+                    float u1 = 1.0f - (float)(r.x >> 8) * 0x1p-24f, u2 = (float)(r.z >> 8) * 0x1p-24f;
+                    float rad = sqrtf(-1.38629436112f * __builtin_amdgcn_logf(u1));
+                    w0 = (double)(rad * __builtin_amdgcn_cosf(u2)); w1 = (double)(rad * __builtin_amdgcn_sinf(u2));
                 }
                 // vonkarman.py:33-36: state = Ad @ state + Bd * w  (Bd = sigma * Bd(sigma=1))
                 R n0 = (P.vk_Ad_u[0] * fu0 + P.vk_Ad_u[1] * fu1) + (sgu * P.vk_Bd_u[0]) * (R)w0;
