@@ -10,7 +10,8 @@ namespace pd {
 constexpr int kNbr = 50;            // RBFInterpolator(neighbors=50), aerodynamic_coefficients.py:59
 constexpr int kSys = kNbr + 3;      // + degree-1 polynomial tail (TPS default degree)
 constexpr int kCols = 5;            // AoA columns of each V2 table
-constexpr int kPay = 64;            // payload stride: 50 kernel coefs, 3 poly, shift0/1, scale0/1
+constexpr int kPay = 64;            // payload (binary64): 50 kernel coefs, 3 poly, shift0/1, scale0/1,
+constexpr int kPayIdx = kNbr + 3 + 4;   // then from slot 57 the 50 points' table indices as bytes
 constexpr int kKeyLoBits = 6, kKeyLenBits = 6, kKeyField = kKeyLoBits + kKeyLenBits;
 constexpr uint64_t kEmptyKey = ~0ull;
 
@@ -125,7 +126,8 @@ PD_HD double log_tab(double x, const double* invc, const double* logc) {
 // [[K, P], [P^T, 0]] c = [d, 0]) and solve it by LU with partial pivoting (LAPACK dgesv's
 // algorithm).  Points are taken in window order (column by column, Mach-ascending).
 //   mach/coef: table arrays (column-grouped); col_start/col_aoa: column geometry
-//   work: >= kSys*kSys + kSys + 3*kNbr doubles of scratch;  payload: kPay doubles out.
+//   work: >= kSys*kSys + kSys + 3*kNbr doubles of scratch;  payload: kPay doubles out (the
+//   last 7 hold the points' table indices as bytes, see pay_store).
 // Returns 0 on success, -1 on a singular system.
 PD_HD int solve_neighbourhood(const double* mach, const double* coef, const int* col_start,
                               const double* col_aoa, uint64_t key, double* work, double* payload) {
@@ -137,9 +139,11 @@ PD_HD int solve_neighbourhood(const double* mach, const double* coef, const int*
     double* ya = ym + kNbr;
     double* yd = ya + kNbr;
     int n = 0;
+    uint8_t idx[kNbr];
     for (int c = 0; c < kCols; ++c)
         for (int i = 0; i < len[c]; ++i) {
             if (n >= kNbr) return -1;
+            idx[n] = (uint8_t)(col_start[c] + lo[c] + i);
             ym[n] = mach[col_start[c] + lo[c] + i];
             ya[n] = col_aoa[c];
             yd[n] = coef[col_start[c] + lo[c] + i];
@@ -199,7 +203,17 @@ PD_HD int solve_neighbourhood(const double* mach, const double* coef, const int*
     payload[kSys + 0] = sh0; payload[kSys + 1] = sh1;
     payload[kSys + 2] = sc0; payload[kSys + 3] = sc1;
     for (int j = kSys + 4; j < kPay; ++j) payload[j] = 0.0;
+    __builtin_memcpy((uint8_t*)(payload + kPayIdx), idx, kNbr);
     return 0;
+}
+
+// Payload in a handle's precision: coefficients converted, index bytes copied.  Stride in R
+// units: 64 (binary64) or 72 (binary32: 57 coefficients + 50 bytes = 13 floats + padding).
+template <typename R> constexpr int pay_stride() { return sizeof(R) == 8 ? kPay : 72; }
+template <typename R> PD_HD void pay_store(const double* src, R* dst) {
+    for (int j = 0; j < kPayIdx; ++j) dst[j] = (R)src[j];
+    for (int j = kPayIdx; j < pay_stride<R>(); ++j) dst[j] = R(0);
+    __builtin_memcpy((uint8_t*)(dst + kPayIdx), (const uint8_t*)(src + kPayIdx), kNbr);
 }
 
 // ---------------------------------------------------------------- Philox4x32-10

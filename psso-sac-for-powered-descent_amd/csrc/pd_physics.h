@@ -41,6 +41,7 @@ template <typename R> struct DevParams {
     R cd_aoa[kCols], cl_aoa[kCols];
     int cd_n, cl_n;
     R cd_mach[256], cl_mach[256];
+    R cd_pt_aoa[256], cl_pt_aoa[256];   // AoA of every table point (its column's)
     // binary64 copies for on-device neighbourhood solves
     double cd_mach_d[256], cd_coef_d[256], cl_mach_d[256], cl_coef_d[256], cd_aoa_d[kCols], cl_aoa_d[kCols];
     // grid fins

@@ -154,6 +154,7 @@ template <typename T> __device__ __forceinline__ const T* launder(const T* p) {
 // pair/quad of lanes that split its 50-term thin-plate sum (terms k = part, part + nparts..).
 template <typename R> struct TabView {
     const R* smach;
+    const R* saoa;             // per-point AoA (LDS)
     const int* start;
     const int* n;
     const R* aoa;
@@ -188,6 +189,7 @@ template <typename R>
 __device__ __forceinline__ TabView<R> tab_view(const DevParams<R>& P, const R* s_cd, const R* s_cl, int table) {
     TabView<R> t;
     t.smach = table ? s_cl : s_cd;
+    t.saoa = (table ? s_cl : s_cd) + 512;   // Lds: kCdA = kCd + 512, kClA = kCl + 512
     t.start = table ? P.cl_start : P.cd_start;
     t.n = table ? P.cl_len : P.cd_len;
     t.aoa = table ? P.cl_aoa : P.cd_aoa;
@@ -205,41 +207,36 @@ __device__ __forceinline__ TabView<R> tab_view(const DevParams<R>& P, const R* s
     return t;
 }
 
+// This lane's share of sum_j c_j phi(|x - y_j|) + poly of one neighbourhood payload.
+// phi(r) = r^2 log r = d2 log(d2) / 2 with d2 = |x - y|^2 (thin_plate_spline, phi(0) = 0).
+// The payload names each term's table point by a byte index, whose (Mach, AoA) sit in LDS; the
+// terms are evaluated in chunks of 10 independent terms so that the loads of a chunk are in
+// flight together and the 10 log chains interleave.
 template <typename R>
-__device__ __forceinline__ R rbf_eval(const R* __restrict__ pay, const R* smach, const int* start,
-                                      const R* aoa, const int lo[kCols], const int len[kCols], R M, R a,
+__device__ __forceinline__ R rbf_eval(const R* __restrict__ pay, const R* smach, const R* saoa, R M, R a,
                                       int part, int nparts) {
-    // phi(r) = r^2 log r = d2 * log(d2) / 2 with d2 = |x - y|^2 (thin_plate_spline, phi(0) = 0).
-    // The 50 terms are flattened over the column windows and evaluated in chunks of 10
-    // independent terms, so that the payload loads (HBM/L2) and LDS reads of a chunk are all
-    // in flight together and the 10 log() chains interleave.
-    const int c1 = len[0], c2 = c1 + len[1], c3 = c2 + len[2], c4 = c3 + len[3];
-    const int b0 = start[0] + lo[0], b1 = start[1] + lo[1] - c1, b2 = start[2] + lo[2] - c2,
-              b3 = start[3] + lo[3] - c3, b4 = start[4] + lo[4] - c4;
-    R dz[kCols];
-#pragma unroll
-    for (int c = 0; c < kCols; ++c) { R da = a - aoa[c]; dz[c] = da * da; }
+    const uint8_t* ib = (const uint8_t*)(pay + kPayIdx);
     R s0 = R(0), s1 = R(0);
     constexpr int kChunk = 10;
 #pragma unroll 1
     for (int j0 = part; j0 < kNbr; j0 += kChunk * nparts) {
-        R mm[kChunk], pp[kChunk], zz[kChunk];
+        R mm[kChunk], aa[kChunk], pp[kChunk];
 #pragma unroll
         for (int u = 0; u < kChunk; ++u) {
             int j = j0 + u * nparts;
             bool ok = j < kNbr;
             int jj = ok ? j : 0;
-            int b = jj < c1 ? b0 : (jj < c2 ? b1 : (jj < c3 ? b2 : (jj < c4 ? b3 : b4)));
-            zz[u] = jj < c1 ? dz[0] : (jj < c2 ? dz[1] : (jj < c3 ? dz[2] : (jj < c4 ? dz[3] : dz[4])));
-            mm[u] = smach[b + jj];
+            int ix = ib[jj];
+            mm[u] = smach[ix];
+            aa[u] = saoa[ix];
             pp[u] = ok ? pay[jj] : R(0);
         }
 #pragma unroll
         for (int u = 0; u < kChunk; ++u) {
-            R dm = M - mm[u];
-            R d2 = dm * dm + zz[u];
-            // c_j d2 log(d2) accumulated (the 1/2 of phi = d2 log(d2) / 2 is applied once below);
-            // d2 = 0 (query on a table point) contributes c_j * 0 * finite = 0
+            R dm = M - mm[u], da = a - aa[u];
+            R d2 = dm * dm + da * da;
+            // c_j d2 log(d2) accumulated (the 1/2 of phi is applied once below); d2 = 0 (query
+            // on a table point) contributes c_j * 0 * finite = 0
             R w = d2 * pp[u];
 #ifdef PD_EXP_NOLOG
             R l = d2;
@@ -284,6 +281,7 @@ __device__ __noinline__ void solve_wave(const DevParams<R>& P, int table, unsign
     const double* aoa = table ? P.cl_aoa_d : P.cd_aoa_d;
     int lo[kCols], len[kCols];
     key_unpack(key, lo, len);
+    int my_idx = 0;
     if (lane < kNbr) {
         int c = 0, off = lane, acc = 0;
 #pragma unroll
@@ -292,6 +290,7 @@ __device__ __noinline__ void solve_wave(const DevParams<R>& P, int table, unsign
             acc += len[q];
         }
         int idx = start[c] + lo[c] + off;
+        my_idx = idx;
         ym[lane] = mach[idx]; ya[lane] = aoa[c]; yd[lane] = coef[idx];
     }
     lds_sync();
@@ -362,8 +361,14 @@ __device__ __noinline__ void solve_wave(const DevParams<R>& P, int table, unsign
     else if (lane == kSys + 3) pay[kSys + 3] = sc1;
     else if (lane < kPay) pay[lane] = 0.0;
     lds_sync();
-    // payload in the kernel's precision, in the (now free) matrix area
-    if (lane < kPay) ((R*)sl->work)[lane] = (R)pay[lane];
+    if (lane < kNbr) ((uint8_t*)(pay + kPayIdx))[lane] = (uint8_t)my_idx;
+    lds_sync();
+    // payload in the kernel's precision, in the (now free) matrix area (pay_store, by lanes)
+    R* pr = (R*)sl->work;
+    if (lane < kPayIdx) pr[lane] = (R)pay[lane];
+    else if (lane < pay_stride<R>()) pr[lane] = R(0);
+    lds_sync();
+    if (lane < kNbr) ((uint8_t*)(pr + kPayIdx))[lane] = (uint8_t)my_idx;
     lds_sync();
 }
 
@@ -372,7 +377,7 @@ __device__ __noinline__ void solve_wave(const DevParams<R>& P, int table, unsign
 // the device table (pd_flush_misses).  Called by the converged wave.
 template <typename R>
 __device__ __forceinline__ R rbf_miss_wave(const StepArgs<R>& a, SolveLds* sl, int table, const R* smach,
-                                        const int* start, const R* aoa, unsigned long long key, R M, R aq,
+                                        const R* saoa, unsigned long long key, R M, R aq,
                                         int part, int nparts, bool need) {
     R val = R(0);
     unsigned long long mm = __ballot(need);
@@ -387,9 +392,7 @@ __device__ __forceinline__ R rbf_miss_wave(const StepArgs<R>& a, SolveLds* sl, i
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         solve_wave<R>(*a.P, lt, lk, sl);
         if (need && key == lk && table == lt) {
-            int lo[kCols], len[kCols];
-            key_unpack(key, lo, len);
-            val = rbf_eval<R>((const R*)sl->work, smach, start, aoa, lo, len, M, aq, part, nparts);
+            val = rbf_eval<R>((const R*)sl->work, smach, saoa, M, aq, part, nparts);
             need = false;
         }
         if ((int)__lane_id() == leader) {
@@ -465,14 +468,14 @@ __device__ __forceinline__ R rbf(const StepArgs<R>& a, SolveLds* sl, int table, 
     cache.key = key;
     cache.slot = slot;
     R val = R(0);
-    if (slot >= 0) val = rbf_eval<R>(t.pay + (int64_t)slot * kPay, t.smach, t.start, t.aoa, lo, len, M, aq, part, nparts);
+    if (slot >= 0) val = rbf_eval<R>(t.pay + (int64_t)slot * pay_stride<R>(), t.smach, t.saoa, M, aq, part, nparts);
     // Misses (a neighbourhood outside the pre-enumerated tables): the converged wave solves
     // each distinct (table, key) cooperatively in the workgroup's LDS scratch, evaluates the
     // lanes that need it, and queues the payload for insertion (pd_flush_misses).
     // Misses (a neighbourhood outside the pre-enumerated tables) take the wave-cooperative
     // exact solve; the loop in rbf_miss_wave runs only when some lane of the wave missed
     if (__ballot(slot < 0)) {
-        R mv = rbf_miss_wave<R>(a, sl, table, t.smach, t.start, t.aoa, key, M, aq, part, nparts, slot < 0);
+        R mv = rbf_miss_wave<R>(a, sl, table, t.smach, t.saoa, key, M, aq, part, nparts, slot < 0);
         if (slot < 0) val = mv;
     }
     return val;
@@ -547,8 +550,9 @@ __device__ __forceinline__ void actor_forward(const float* __restrict__ W, int64
 }
 
 template <bool WIND> struct Lds {
-    static constexpr int kCd = 0, kCl = 256, kCaX = 512, kCaY = 576, kCnX = 640, kCnY = 704,
-                         kWAlt = 768, kWSp = kWAlt + 800, kTotal = WIND ? kWSp + 800 : kWAlt;
+    // table Mach values and, 512 further on, each point's AoA (tab_view relies on that offset)
+    static constexpr int kCd = 0, kCl = 256, kCdA = 512, kClA = 768, kCaX = 1024, kCaY = 1088, kCnX = 1152,
+                         kCnY = 1216, kWAlt = 1280, kWSp = kWAlt + 800, kTotal = WIND ? kWSp + 800 : kWAlt;
 };
 
 template <typename R, int PHASE, int RTD, bool WIND, int LPE, int POL = 0>
@@ -560,7 +564,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
     __shared__ LineLds<R> lines;
     __shared__ SolveLds solve;
     const DevParams<R>& P = *a.P;
-    for (int t = threadIdx.x; t < 256; t += kBlock) { lds[L::kCd + t] = P.cd_mach[t]; lds[L::kCl + t] = P.cl_mach[t]; }
+    for (int t = threadIdx.x; t < 256; t += kBlock) {
+        lds[L::kCd + t] = P.cd_mach[t]; lds[L::kCl + t] = P.cl_mach[t];
+        lds[L::kCdA + t] = P.cd_pt_aoa[t]; lds[L::kClA + t] = P.cl_pt_aoa[t];
+    }
     if (threadIdx.x < 64) {
         lds[L::kCaX + threadIdx.x] = P.ca_x[threadIdx.x]; lds[L::kCaY + threadIdx.x] = P.ca_y[threadIdx.x];
         lds[L::kCnX + threadIdx.x] = P.cn_x[threadIdx.x]; lds[L::kCnY + threadIdx.x] = P.cn_y[threadIdx.x];
@@ -1028,8 +1035,8 @@ __global__ void k_insert(Pending pend, unsigned long long* keys_cd, R* pay_cd, i
         int sl = s_slot;
         if (sl >= 0) {
             int table = sl >> 30, slot = sl & ((1 << 30) - 1);
-            R* pay = (table ? pay_cl : pay_cd) + (int64_t)slot * kPay;
-            if (threadIdx.x < kPay) pay[threadIdx.x] = (R)pend.pay[e * kPay + threadIdx.x];
+            R* pay = (table ? pay_cl : pay_cd) + (int64_t)slot * pay_stride<R>();
+            if (threadIdx.x == 0) pay_store<R>(pend.pay + e * kPay, pay);
         }
         __syncthreads();
     }
@@ -1108,7 +1115,7 @@ int table_insert(const pd_aero_table& t, Table<R>& T, uint64_t key, std::vector<
     if (solve_neighbourhood(t.mach, t.coef, t.col_start, aoa, key, work.data(), pay.data()) != 0) return -1;
     if ((T.entries + 1) * 2 > cap) return -1;
     T.keys[h] = key;
-    for (int j = 0; j < kPay; ++j) T.pay[h * kPay + j] = (R)pay[j];
+    pay_store<R>(pay.data(), T.pay.data() + h * pay_stride<R>());
     ++T.entries;
     return (int)h;
 }
@@ -1119,7 +1126,7 @@ pd_status build_table(const pd_aero_table& t, const uint64_t* keys, int64_t nk, 
     T.logcap = log2ceil(cap_need);
     int64_t cap = 1ll << T.logcap;
     T.keys.assign(cap, kEmptyKey);
-    T.pay.assign(cap * kPay, R(0));
+    T.pay.assign(cap * pay_stride<R>(), R(0));
     std::vector<double> work(kScratch), pay(kPay);
     for (int64_t e = 0; e < nk; ++e)
         if (table_insert<R>(t, T, keys[e], work, pay) < 0)
@@ -1278,6 +1285,10 @@ template <typename R> void fill_params(const pd_params* p, const pd_config* c, D
         D.cd_aoa_d[cc] = p->cd.col_aoa[cc]; D.cl_aoa_d[cc] = p->cl.col_aoa[cc];
     }
     D.cd_n = p->cd.n_pts; D.cl_n = p->cl.n_pts;
+    for (int cc = 0; cc < kCols; ++cc) {
+        for (int k = 0; k < p->cd.col_len[cc]; ++k) D.cd_pt_aoa[p->cd.col_start[cc] + k] = (R)p->cd.col_aoa[cc];
+        for (int k = 0; k < p->cl.col_len[cc]; ++k) D.cl_pt_aoa[p->cl.col_start[cc] + k] = (R)p->cl.col_aoa[cc];
+    }
     for (int k = 0; k < 256; ++k) {
         D.cd_mach[k] = (R)p->cd.mach[k]; D.cl_mach[k] = (R)p->cl.mach[k];
         D.cd_mach_d[k] = p->cd.mach[k]; D.cl_mach_d[k] = p->cl.mach[k];
