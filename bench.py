@@ -65,6 +65,46 @@ def timed_region(step_fn, steps, sync, dist=None, device="cpu"):
     return wall
 
 
+def bench_sac(args, world, rank, local, dist):
+    """Config c5: SAC data collection, 4096 envs per GPU (32 768 on 8 GPUs), pure throttle, RL
+    reward, auto-reset.  One timed step = the reference's Actor (256x2, sampled, PyTorch-ROCm)
+    on every env's observation + one env step + transition slab + all_gather over RCCL + append
+    to the learner rank's device replay buffer."""
+    import torch
+    import pdenv
+    from pdenv.sac import Actor, DeviceReplayBuffer, SACCollector
+    n = args.envs if args.envs != 65536 else 4096
+    env = pdenv.PoweredDescentEnv(n, flight_phase="landing_burn_pure_throttle", mode="rl",
+                                  precision=args.precision, device=local, auto_reset=True, seed=1234,
+                                  env_offset=shard_offset(rank, n))
+    env.flush_every = 16
+    torch.manual_seed(0)
+    actor = Actor(2, 1).to(env.device)
+    buf = DeviceReplayBuffer(1_000_000, 2, 1, env.device) if rank == 0 else None
+    col = SACCollector(env, actor, buf, dist, generator=torch.Generator(device=env.device).manual_seed(rank))
+    for _ in range(args.warmup):
+        col.step()
+    wall = timed_region(lambda k: col.step(), args.steps, torch.cuda.synchronize, dist, env.device)
+    if rank != 0:
+        if dist:
+            dist.destroy_process_group()
+        return
+    out = {
+        "metric": "SAC collection env-steps/sec (c5: actor + env + RCCL gather + replay buffer)",
+        "value": whole_job_rate(n, world, args.steps, wall), "unit": "env-steps/s",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": wall / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": args.precision,
+        "data": "synthetic (random-init SAC actor 2-256-256-1, reference initial state, no wind)",
+        "config": {"workload": "c5: SAC collection, landing_burn_pure_throttle, rtd_rl, auto-reset",
+                   "envs_per_gpu": n, "global_envs": n * world, "parallelism": f"env-shard x{world} + all_gather"},
+        "replay_buffer_size": len(buf),
+    }
+    print(json.dumps(out))
+    if dist:
+        dist.destroy_process_group()
+
+
 def bench_pso(args, world, rank, local, dist):
     """Config c4: PSO generations of pso_wrapped_env.objective_function over P particles per GPU
     (phase landing_burn, 372-parameter simple_actor per particle, positions U(-1.5, 1.5) as the
@@ -132,8 +172,9 @@ def main():
     ap.add_argument("--no-wind", action="store_true")
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--secondary", type=int, default=1, help="also time the other precision")
-    ap.add_argument("--workload", choices=["c3", "c4"], default="c3",
-                    help="c3: env-steps/s headline; c4: PSO generations with the fused actor")
+    ap.add_argument("--workload", choices=["c3", "c4", "c5"], default="c3",
+                    help="c3: env-steps/s headline; c4: PSO generations with the fused actor; "
+                         "c5: SAC collection (actor + env + RCCL transition gather + replay buffer)")
     ap.add_argument("--particles", type=int, default=32768, help="c4: particles per GPU")
     args = ap.parse_args()
 
@@ -150,6 +191,8 @@ def main():
     import pdenv
     if args.workload == "c4":
         return bench_pso(args, world, rank, local, dist)
+    if args.workload == "c5":
+        return bench_sac(args, world, rank, local, dist)
 
     def run(precision):
         n = args.envs

@@ -1,0 +1,130 @@
+"""SAC data path on the device (SURVEY config c5): the reference's actor drives N envs per GPU,
+transitions are all-gathered over RCCL into a device replay buffer on the learner rank.
+
+The reference steps ONE env per process and adds one transition per step to a numpy buffer
+(sac_pytorch_powered_descent.py:160-183, sac_pytorch.py:12-49).  Here every rank steps its own
+env shard through libpdenv, builds the transition slab [n_local, s|a|r|s'|done] (28 B per env
+for the pure-throttle task), and `all_gather_into_tensor` (backend "nccl" = RCCL over xGMI)
+concatenates the slabs in rank order; the learner rank appends them to its ring buffer.  The
+learner itself (critic/actor updates) is the caller's, as in the reference.
+"""
+import torch
+import torch.nn as nn
+
+
+class Actor(nn.Module):
+    """sac_pytorch.py:129-179: shared MLP (ReLU), mean and log_std heads, tanh squashing."""
+
+    def __init__(self, state_dim, action_dim, hidden_dim=256, n_hidden_layers=2, max_action=1.0,
+                 log_std_min=-20.0, log_std_max=2.0):
+        super().__init__()
+        self.max_action, self.log_std_min, self.log_std_max = max_action, log_std_min, log_std_max
+        layers = [nn.Linear(state_dim, hidden_dim), nn.ReLU()]
+        for _ in range(n_hidden_layers - 1):
+            layers += [nn.Linear(hidden_dim, hidden_dim), nn.ReLU()]
+        self.shared_net = nn.Sequential(*layers)
+        self.mean = nn.Linear(hidden_dim, action_dim)
+        self.log_std = nn.Linear(hidden_dim, action_dim)
+
+    def forward(self, state):
+        f = self.shared_net(state)
+        return self.mean(f), torch.clamp(self.log_std(f), self.log_std_min, self.log_std_max)
+
+    def sample(self, state, deterministic=False, generator=None):
+        mean, log_std = self(state)
+        if deterministic:
+            return torch.tanh(mean) * self.max_action, None
+        std = log_std.exp()
+        eps = torch.randn(mean.shape, device=mean.device, dtype=mean.dtype, generator=generator)
+        x = mean + std * eps                                   # Normal(mean, std).rsample()
+        action = torch.tanh(x)
+        log_prob = (-((x - mean) ** 2) / (2 * std ** 2) - log_std - 0.9189385332046727
+                    - torch.log(1 - action.pow(2) + 1e-6)).sum(-1, keepdim=True)
+        return action * self.max_action, log_prob
+
+
+class DeviceReplayBuffer:
+    """The reference's uniform ReplayBuffer (sac_pytorch.py:12-49) as device tensors.
+    add_batch appends B transitions at once (ring, oldest overwritten)."""
+
+    def __init__(self, capacity, state_dim, action_dim, device):
+        self.capacity, self.state_dim, self.action_dim = int(capacity), state_dim, action_dim
+        self.width = 2 * state_dim + action_dim + 2
+        self.data = torch.zeros(self.capacity, self.width, dtype=torch.float32, device=device)
+        self.position = 0
+        self.size = 0
+
+    def add_batch(self, slab):
+        """slab [B, 2S + A + 2] = state | action | reward | next_state | done (float32)."""
+        b = slab.shape[0]
+        if b > self.capacity:
+            slab, b = slab[-self.capacity:], self.capacity
+        end = self.position + b
+        if end <= self.capacity:
+            self.data[self.position:end] = slab
+        else:
+            k = self.capacity - self.position
+            self.data[self.position:] = slab[:k]
+            self.data[:b - k] = slab[k:]
+        self.position = end % self.capacity
+        self.size = min(self.size + b, self.capacity)
+
+    def add(self, state, action, reward, next_state, done):
+        """The reference's one-transition add (sac_pytorch.py:27-35)."""
+        row = torch.cat([torch.as_tensor(state, dtype=torch.float32).reshape(-1),
+                         torch.as_tensor(action, dtype=torch.float32).reshape(-1),
+                         torch.tensor([float(reward)]),
+                         torch.as_tensor(next_state, dtype=torch.float32).reshape(-1),
+                         torch.tensor([float(done)])]).to(self.data.device)
+        self.add_batch(row[None])
+
+    def sample(self, batch_size, generator=None):
+        """Uniform indices in [0, size) (np.random.randint, sac_pytorch.py:37-46)."""
+        idx = torch.randint(0, self.size, (batch_size,), device=self.data.device, generator=generator)
+        d = self.data[idx]
+        S, A = self.state_dim, self.action_dim
+        return (d[:, :S], d[:, S:S + A], d[:, S + A:S + A + 1], d[:, S + A + 1:2 * S + A + 1],
+                d[:, 2 * S + A + 1:])
+
+    def __len__(self):
+        return self.size
+
+
+def transition_slab(obs, action, reward, next_obs, done):
+    """[N, 2S + A + 2] float32: state | action | reward | next_state | done (done, not truncated,
+    as the driver stores it: sac_pytorch_powered_descent.py:170-176)."""
+    return torch.cat([obs.float(), action.float(), reward.float()[:, None], next_obs.float(),
+                      done.float()[:, None]], dim=1).contiguous()
+
+
+def gather_slabs(slab, dist=None):
+    """All ranks' slabs concatenated in rank order (all_gather_into_tensor; RCCL on GPU ranks)."""
+    if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
+        return slab
+    out = torch.empty((dist.get_world_size() * slab.shape[0], slab.shape[1]), dtype=slab.dtype,
+                      device=slab.device)
+    dist.all_gather_into_tensor(out, slab)
+    return out
+
+
+class SACCollector:
+    """One collection step of N envs on this rank: actor sample -> env step -> slab -> gather ->
+    learner-rank buffer append.  `obs` always holds the observation the actor sees next (the
+    post-auto-reset observation of envs whose episode ended)."""
+
+    def __init__(self, env, actor, buffer=None, dist=None, learner_rank=0, generator=None):
+        self.env, self.actor, self.buffer, self.dist = env, actor, buffer, dist
+        self.learner_rank, self.generator = learner_rank, generator
+        self.rank = dist.get_rank() if dist is not None and dist.is_initialized() else 0
+        self.obs = env.reset().float()
+
+    @torch.no_grad()
+    def step(self):
+        act, _ = self.actor.sample(self.obs, generator=self.generator)
+        next_obs, rew, done, trunc, _ = self.env.step(act)
+        slab = transition_slab(self.obs, act, rew, next_obs, done)
+        full = gather_slabs(slab, self.dist)
+        if self.rank == self.learner_rank and self.buffer is not None:
+            self.buffer.add_batch(full)
+        self.obs = self.env.observe().float()
+        return full

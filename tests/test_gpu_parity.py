@@ -368,3 +368,34 @@ def test_pso_facade_fused_vs_torch_actor(pd):
     b = m.objective_function_batch_torch(X).cpu().numpy()
     rel = np.abs(a - b) / np.abs(b)
     assert np.median(rel) < 1e-9 and (rel < 1e-3).mean() >= 0.95, rel
+
+
+def test_sac_collector_single_rank(pd):
+    """c5 data path on one rank: actor -> pd_step -> transition slab -> device replay buffer.
+    Every stored transition is (obs the actor saw, its action, reward, post-step obs, done), and
+    the next step's input is the post-auto-reset observation."""
+    import torch
+    from pdenv.sac import Actor, DeviceReplayBuffer, SACCollector
+    torch.manual_seed(0)
+    N = 2048
+    env = make(pd, N, mode="rl", auto_reset=True, seed=4)
+    actor = Actor(2, 1).cuda()
+    buf = DeviceReplayBuffer(4 * N, 2, 1, "cuda")
+    col = SACCollector(env, actor, buf, generator=torch.Generator(device="cuda").manual_seed(1))
+    obs0 = col.obs.clone()
+    full = col.step()
+    assert full.shape == (N, 7) and len(buf) == N
+    assert torch.equal(buf.data[:N, :2], obs0)
+    assert (buf.data[:N, 2].abs() <= 1).all()
+    # replay the same actions on a twin env: identical rewards / next obs / done
+    twin = make(pd, N, mode="rl", auto_reset=True, seed=4)
+    twin.reset()
+    o, r, d, tr, _ = twin.step(buf.data[:N, 2:3])
+    assert torch.equal(buf.data[:N, 3], r.float()) and torch.equal(buf.data[:N, 4:6], o.float())
+    assert torch.equal(buf.data[:N, 6], d.float())
+    for _ in range(300):
+        col.step()
+    assert len(buf) == 4 * N
+    t = env.state[:, 10]
+    assert (t < t.max() - 1.0).any()        # some episodes ended (truncated) and were auto-reset
+    assert torch.isfinite(buf.data).all()

@@ -91,3 +91,47 @@ def test_sharded_envs_equal_single_batch(oracle_mod):
         got = out["all"]
     ref = np.stack([_episode(g, n_steps) for g in range(world * n_per_rank)])
     assert np.array_equal(got, ref)
+
+
+def _sac_gather_worker(rank, world, port, out):
+    sys.path.insert(0, os.path.join(REPO, "psso-sac-for-powered-descent_amd"))
+    from pdenv.sac import DeviceReplayBuffer, gather_slabs, transition_slab
+    _init(rank, world, port)
+    n = 5
+    obs = torch.full((n, 2), float(rank)) + torch.arange(n)[:, None] * 0.1
+    act = torch.full((n, 1), -float(rank))
+    rew = torch.arange(n, dtype=torch.float64) + 100 * rank
+    nxt = obs + 1
+    done = torch.tensor([0, 1, 0, 0, 1], dtype=torch.uint8)
+    buf = DeviceReplayBuffer(12, 2, 1, "cpu")
+    for k in range(3):                              # 3 steps x 2 ranks x 5 = 30 > capacity 12
+        full = gather_slabs(transition_slab(obs + k, act, rew, nxt + k, done), dist)
+        if rank == 0:
+            buf.add_batch(full)
+    if rank == 0:
+        out["data"] = buf.data.clone().numpy()
+        out["pos"], out["size"] = buf.position, buf.size
+        out["sample"] = [t.shape for t in buf.sample(7, generator=torch.Generator().manual_seed(0))]
+    dist.destroy_process_group()
+
+
+def test_sac_transition_gather_into_replay_buffer():
+    """c5 data path on two gloo ranks: per-rank transition slabs all-gathered in rank order and
+    appended to the learner rank's ring buffer (oldest entries overwritten)."""
+    world, port = 2, _free_port()
+    with mp.Manager() as m:
+        out = m.dict()
+        mp.spawn(_sac_gather_worker, args=(world, port, out), nprocs=world, join=True)
+        data, pos, size, shapes = out["data"], out["pos"], out["size"], out["sample"]
+    # expected stream: for k in 0..2, rank 0 rows then rank 1 rows
+    rows = []
+    for k in range(3):
+        for r in range(2):
+            for i in range(5):
+                s = np.array([r + 0.1 * i + k, r + 0.1 * i + k], dtype=np.float32)
+                rows.append(np.concatenate([s, [-r], [i + 100 * r], s + 1, [[0, 1, 0, 0, 1][i]]]).astype(np.float32))
+    rows = np.array(rows)
+    assert size == 12 and pos == 30 % 12
+    ring = np.roll(rows[-12:], 30 % 12, axis=0)     # row t lands at t % 12
+    assert np.array_equal(data, ring)
+    assert [tuple(s) for s in shapes] == [(7, 2), (7, 1), (7, 1), (7, 2), (7, 1)]
