@@ -149,6 +149,20 @@ pd_status pd_rollout(pd_env* env, const void* actions, int32_t n_steps, void* re
  *            envs are done (one host sync per check); 0 = always run max_steps launches. */
 pd_status pd_rollout_policy(pd_env* env, const float* weights, int32_t n_params, int32_t max_steps,
                             void* fitness, int32_t* steps, int32_t check_every, void* stream);
+/* One PSO generation's particle update on the device (particle_swarm_optimisation.py:437-441
+ * personal best, :515-519 update_velocity_with_local_best, :112-118 update_position), binary64:
+ *   if fitness < best_fitness: best_position = position;  best_fitness = min(best_fitness, fitness)
+ *   v = w v + c1 r1 (best_position - x) + c2 r2 (swarm_best[swarm] - x);  x = clip(x + v, lower, upper)
+ * r1, r2: one uniform per particle and generation (Philox4x32-10 keyed by seed, counter
+ * (particle_offset + p, generation)).  Arrays are parameter-major [dim][n_particles]; swarm_best
+ * [n_swarms][dim]; swarm [n_particles] int32 subswarm ids; lower/upper [dim].  position_f32
+ * (optional, [dim][n_particles]) receives the new positions as the float32 actor weights
+ * pd_rollout_policy reads.  Device pointers; runs on the current HIP device. */
+pd_status pd_pso_step(int64_t n_particles, int32_t dim, const double* fitness, double* best_fitness,
+                      double* position, double* velocity, double* best_position, const double* swarm_best,
+                      const int32_t* swarm, const double* lower, const double* upper, double w, double c1,
+                      double c2, uint64_t seed, uint32_t generation, uint64_t particle_offset,
+                      float* position_f32, void* stream);
 /* Insert the aero neighbourhoods solved on device since the last flush into the handle's
  * tables (one tiny kernel; a no-op when nothing missed).  Call every few steps: a missed
  * neighbourhood is solved exactly on every lookup until it is flushed. */

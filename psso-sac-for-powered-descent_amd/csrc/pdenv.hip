@@ -20,9 +20,14 @@
 
 using namespace pd;
 
+namespace pd {
+// the thread-local message behind pd_last_error(), shared by every source of the library
+thread_local std::string g_err;
+pd_status set_error(pd_status s, const char* m) { g_err = m; return s; }
+}  // namespace pd
+
 namespace {
 
-thread_local std::string g_err;
 pd_status fail(pd_status s, const std::string& m) { g_err = m; return s; }
 
 #define PD_HIP(expr)                                                                   \

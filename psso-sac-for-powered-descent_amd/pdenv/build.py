@@ -5,7 +5,7 @@ import sys
 
 PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
-SRC = os.path.join(ROOT, "csrc", "pdenv.hip")
+SRCS = [os.path.join(ROOT, "csrc", f) for f in ("pdenv.hip", "pdpso.hip")]
 OUT = os.path.join(PKG, "libpdenv.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 # -ffp-contract=off: no FMA contraction, so binary64 arithmetic follows the reference's
@@ -31,7 +31,7 @@ def up_to_date():
 def build(force=False, verbose=True):
     if not force and up_to_date():
         return OUT
-    cmd = [HIPCC] + FLAGS + ["-o", OUT, SRC]
+    cmd = [HIPCC] + FLAGS + ["-o", OUT] + SRCS
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)

@@ -1,0 +1,233 @@
+"""Device-resident particle subswarm optimisation.
+
+ParticleSubswarmOptimisation.run (src/particle_swarm_optimisation/particle_swarm_optimisation.py
+:285-520) with the swarm kept on the GPU between generations: particles are evaluated by
+pd_rollout_policy (the actor fused into the step kernel), the personal-best / velocity /
+position update is pd_pso_step (binary64, parameter-major [D][P]), and only per-subswarm
+minima cross ranks.  The reference's parameters (configs/evolutionary_algorithms_config.py)
+are the defaults; the population can be scaled to config c4's 262 144 particles.
+
+Randomness: positions U(bounds) at init, r1/r2 per particle and generation (Philox, in the
+kernel), and a seeded Python `random.Random` for the share/migrate decisions that the reference
+draws from `random` -- the same on every rank, so all ranks take identical decisions.
+"""
+import math
+import random
+
+import numpy as np
+import torch
+
+from . import _lib as L
+from .env import PoweredDescentEnv, _ptr, _stream
+
+# configs/evolutionary_algorithms_config.py:69-101
+PSO_PARAMS = {
+    "landing_burn_pure_throttle": dict(pop_size=150, generations=400, c1=1, c2=1, w_start=0.9, w_end=0.4,
+                                       num_sub_swarms=2, communication_freq=10, migration_freq=5,
+                                       number_of_migrants=1, re_initialise_number_of_particles=600,
+                                       re_initialise_generation=90),
+    "landing_burn": dict(pop_size=200, generations=400, c1=1, c2=1, w_start=0.9, w_end=0.7,
+                         num_sub_swarms=2, communication_freq=10, migration_freq=5, number_of_migrants=1,
+                         re_initialise_number_of_particles=600, re_initialise_generation=90),
+}
+ACTOR_DIM = {"landing_burn_pure_throttle": 249, "landing_burn": 372}
+
+
+class ParticleSubswarmOptimisationGPU:
+    """One rank's shard of the swarm.  Global particle g belongs to subswarm g // (pop / S)
+    (initialize_swarms, :372-389); rank r holds particles [r*P_local, (r+1)*P_local)."""
+
+    def __init__(self, flight_phase="landing_burn", pso_params=None, pop_size=None, enable_wind=False,
+                 stochastic_wind=False, horiontal_wind_percentile=50, device=0, precision="f64", seed=0,
+                 dist=None, max_steps=2200):
+        self.flight_phase = flight_phase
+        self.p = dict(PSO_PARAMS[flight_phase])
+        if pso_params:
+            self.p.update(pso_params)
+        if pop_size:
+            self.p["pop_size"] = int(pop_size)
+        self.dist = dist if dist is not None and dist.is_initialized() else None
+        self.world = self.dist.get_world_size() if self.dist else 1
+        self.rank = self.dist.get_rank() if self.dist else 0
+        self.device = torch.device("cuda", device)
+        self.D = ACTOR_DIM[flight_phase]
+        self.S = self.p["num_sub_swarms"]
+        pop = self.p["pop_size"]
+        self.sub_size = pop // self.S
+        pop = self.sub_size * self.S                      # the reference builds S * (pop // S)
+        if pop % self.world:
+            raise ValueError("pop_size must split evenly over the ranks")
+        self.P = pop // self.world
+        self.offset = self.rank * self.P
+        self.seed = int(seed)
+        self.max_steps = max_steps
+        self.env_kw = dict(mode="pso", precision=precision, device=device, enable_wind=enable_wind,
+                           stochastic_wind=stochastic_wind, wind_percentile=horiontal_wind_percentile, seed=seed)
+        self.rng = random.Random(seed)                    # share/migrate decisions, same on all ranks
+        self.lib = L.load()
+        b = torch.tensor([[-1.5, 1.5]] * self.D, dtype=torch.float64)   # simple_actor.return_setup_vals bounds
+        self.lower = b[:, 0].contiguous().to(self.device)
+        self.upper = b[:, 1].contiguous().to(self.device)
+        self.initialize_swarms()
+
+    # ------------------------------------------------------------------ state
+    def initialize_swarms(self):
+        g = torch.Generator(device=self.device).manual_seed(self.seed * 1000003 + self.rank)
+        u = torch.rand(self.D, self.P, generator=g, device=self.device, dtype=torch.float64)
+        self.x = (self.lower[:, None] + (self.upper - self.lower)[:, None] * u).contiguous()
+        self.v = torch.zeros_like(self.x)
+        self.pb = torch.zeros_like(self.x)
+        self.pbf = torch.full((self.P,), math.inf, dtype=torch.float64, device=self.device)
+        self.x32 = self.x.float().contiguous()
+        gid = torch.arange(self.offset, self.offset + self.P, device=self.device)
+        self.swarm = (gid // self.sub_size).to(torch.int32).contiguous()
+        self.sb = torch.zeros(self.S, self.D, dtype=torch.float64, device=self.device)
+        self.sbf = [math.inf] * self.S
+        self.gbf, self.gb = math.inf, None
+        self.w = self.p["w_start"]
+        self.env = PoweredDescentEnv(self.P, self.flight_phase, **self.env_kw) if self.P > 0 else None
+        self._aux = {}
+        self.last_fitness = None
+
+    def _env_for(self, n):
+        if self.env is not None and self.env.n == n:
+            return self.env
+        if n not in self._aux:                                  # share_information's candidates
+            self._aux[n] = PoweredDescentEnv(n, self.flight_phase, **self.env_kw)
+        return self._aux[n]
+
+    def evaluate(self, x32):
+        """pso_wrapped_env.objective_function for every column of x32 [D][n] (fused actor)."""
+        n = x32.shape[1]
+        if n == 0:
+            return torch.empty(0, dtype=torch.float64, device=self.device), torch.empty(0, dtype=torch.int32)
+        env = self._env_for(n)
+        fit = torch.empty(n, dtype=env.dtype, device=self.device)
+        steps = torch.empty(n, dtype=torch.int32, device=self.device)
+        L.check(self.lib.pd_rollout_policy(env.h, _ptr(x32), self.D, self.max_steps, _ptr(fit), _ptr(steps), 64,
+                                           _stream(self.device)))
+        return fit.double(), steps
+
+    # ------------------------------------------------------------------ one generation
+    def _swarm_minima(self, fit):
+        """Per subswarm: (min fitness, its position) over all ranks, first particle on ties."""
+        f = torch.full((self.S,), math.inf, dtype=torch.float64, device=self.device)
+        pos = torch.zeros(self.S, self.D, dtype=torch.float64, device=self.device)
+        for s in range(self.S):
+            m = self.swarm == s
+            if bool(m.any()):
+                fs = torch.where(m, fit, torch.full_like(fit, math.inf))
+                i = int(torch.argmin(fs))
+                f[s] = fs[i]
+                pos[s] = self.x[:, i]
+        if self.dist:
+            fa = [torch.empty_like(f) for _ in range(self.world)]
+            pa = [torch.empty_like(pos) for _ in range(self.world)]
+            self.dist.all_gather(fa, f)
+            self.dist.all_gather(pa, pos)
+            F, Pz = torch.stack(fa), torch.stack(pa)            # [world, S], [world, S, D]
+            r = torch.argmin(F, dim=0)                          # lowest rank on ties
+            cols = torch.arange(self.S, device=self.device)
+            f = F[r, cols]
+            pos = Pz[r, cols]
+        return f, pos
+
+    def generation(self, gen):
+        fit, _ = self.evaluate(self.x32)
+        self.last_fitness = fit
+        f, pos = self._swarm_minima(fit)
+        for s in range(self.S):                                 # :442-444
+            if float(f[s]) < self.sbf[s]:
+                self.sbf[s] = float(f[s])
+                self.sb[s] = pos[s]
+        for s in range(self.S):                                 # :474-477
+            if self.sbf[s] < self.gbf:
+                self.gbf = self.sbf[s]
+                self.gb = self.sb[s].clone()
+        self.w = self.p["w_start"] - (self.p["w_start"] - self.p["w_end"]) * gen / self.p["generations"]
+        if self.P > 0:
+            L.check(self.lib.pd_pso_step(self.P, self.D, _ptr(fit), _ptr(self.pbf), _ptr(self.x), _ptr(self.v),
+                                         _ptr(self.pb), _ptr(self.sb), _ptr(self.swarm), _ptr(self.lower),
+                                         _ptr(self.upper), float(self.w), float(self.p["c1"]), float(self.p["c2"]),
+                                         self.seed, gen, self.offset, _ptr(self.x32), _stream(self.device)))
+        if gen % self.p["communication_freq"] == 0 and gen > 0:
+            self.share_information()
+        if gen % self.p["migration_freq"] == 0 and gen > 0:
+            self.migrate_particles()
+        if gen == self.p["re_initialise_generation"]:
+            self.re_initialise_swarms()
+        return fit
+
+    def run(self, generations=None):
+        for gen in range(generations if generations is not None else self.p["generations"]):
+            self.generation(gen)
+        return self.gb, self.gbf
+
+    # ------------------------------------------------------------------ share / migrate / re-init
+    def share_information(self):
+        """:521-543: for every subswarm but the best, with probability 1/2 its best position moves
+        30 % toward the best subswarm's; the moved position is re-evaluated and its fitness kept
+        only if better (the position is kept either way, as in the reference)."""
+        best = int(np.argmin(self.sbf))
+        moved = [i for i in range(self.S) if i != best and self.rng.random() < 0.5]
+        if not moved:
+            return
+        for i in moved:
+            self.sb[i] = (1 - 0.3) * self.sb[i] + 0.3 * self.sb[best]
+        cand = self.sb[moved].t().float().contiguous()          # [D][k]
+        fit, _ = self.evaluate(cand)
+        self.share_log = (moved, fit.clone())
+        for k, i in enumerate(moved):
+            if float(fit[k]) < self.sbf[i]:
+                self.sbf[i] = float(fit[k])
+
+    def migrate_particles(self):
+        """:545-553: number_of_migrants random particles of every subswarm (with > 1 member) move
+        to a random other subswarm.  Decisions are taken on the global membership (all ranks
+        draw the same choices); each rank applies those that hit its own particles."""
+        sw = self.swarm
+        if self.dist:
+            parts = [torch.empty_like(sw) for _ in range(self.world)]
+            self.dist.all_gather(parts, sw)
+            sw = torch.cat(parts)
+        members = [list(torch.nonzero(sw == s).flatten().cpu().numpy()) for s in range(self.S)]
+        moves = []
+        for i in range(self.S):
+            if len(members[i]) > 1:
+                for _ in range(self.p["number_of_migrants"]):
+                    k = self.rng.randrange(len(members[i]))
+                    g = members[i].pop(k)
+                    t = self.rng.choice([j for j in range(self.S) if j != i])
+                    members[t].append(g)
+                    moves.append((g, t))
+        for g, t in moves:
+            if self.offset <= g < self.offset + self.P:
+                self.swarm[g - self.offset] = t
+
+    def re_initialise_swarms(self):
+        """:360-370: every subswarm keeps its re_initialise_number_of_particles // S best
+        particles (by personal best fitness); the rest are dropped."""
+        keep_n = self.p["re_initialise_number_of_particles"] // self.S
+        pbf, sw = self.pbf, self.swarm
+        if self.dist:
+            a = [torch.empty_like(pbf) for _ in range(self.world)]
+            b = [torch.empty_like(sw) for _ in range(self.world)]
+            self.dist.all_gather(a, pbf)
+            self.dist.all_gather(b, sw)
+            pbf, sw = torch.cat(a), torch.cat(b)
+        keep = torch.zeros_like(pbf, dtype=torch.bool)
+        for s in range(self.S):
+            idx = torch.nonzero(sw == s).flatten()
+            order = torch.argsort(pbf[idx], stable=True)[:keep_n]
+            keep[idx[order]] = True
+        mine = keep[self.offset:self.offset + self.P]
+        sel = torch.nonzero(mine).flatten()
+        self.x, self.v, self.pb = (t[:, sel].contiguous() for t in (self.x, self.v, self.pb))
+        self.pbf, self.swarm = self.pbf[sel].contiguous(), self.swarm[sel].contiguous()
+        self.x32 = self.x.float().contiguous()
+        gids = torch.nonzero(keep).flatten()
+        self.offset = int((gids < self.offset).sum()) if self.P else 0
+        self.P = int(sel.numel())
+        if self.env is not None:
+            self.env.close()
+        self.env = PoweredDescentEnv(self.P, self.flight_phase, **self.env_kw) if self.P > 0 else None

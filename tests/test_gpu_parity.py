@@ -399,3 +399,102 @@ def test_sac_collector_single_rank(pd):
     t = env.state[:, 10]
     assert (t < t.max() - 1.0).any()        # some episodes ended (truncated) and were auto-reset
     assert torch.isfinite(buf.data).all()
+
+
+def _np_pso_step(x, v, pb, pbf, fit, sb, swarm, lo, hi, w, c1, c2, seed, gen, offset):
+    """particle_swarm_optimisation.py:437-441, 515-519, 112-118 in NumPy, parameter-major."""
+    from philox_np import philox, u01
+    P = x.shape[1]
+    g = np.arange(offset, offset + P, dtype=np.uint64)
+    r = philox(g & np.uint64(0xFFFFFFFF), g >> np.uint64(32), np.full(P, gen), np.full(P, 32),
+               seed & 0xFFFFFFFF, seed >> 32)
+    r1, r2 = u01(r[0], r[1]), u01(r[2], r[3])
+    better = fit < pbf
+    pb = np.where(better[None, :], x, pb)
+    inertia = w * v
+    cognitive = c1 * r1[None, :] * (pb - x)
+    social = c2 * r2[None, :] * (sb[swarm].T - x)
+    v = inertia + cognitive + social
+    xn = x + v
+    xn = np.where(xn < lo[:, None], lo[:, None], np.where(xn > hi[:, None], hi[:, None], xn))
+    return xn, v, pb, np.where(better, fit, pbf)
+
+
+def test_pso_step_matches_numpy(pd):
+    """pd_pso_step (binary64, one r1/r2 per particle from Philox) is bit-identical to the
+    reference's update written in NumPy with the same uniforms."""
+    import torch
+    from pdenv import _lib as L
+    from pdenv.env import _ptr
+    rng = np.random.default_rng(3)
+    P, D, S = 300, 372, 3
+    x = rng.uniform(-1.5, 1.5, (D, P)); v = rng.normal(0, 0.2, (D, P)); pb = rng.uniform(-1.5, 1.5, (D, P))
+    pbf = rng.uniform(0, 10, P); pbf[::7] = np.inf
+    fit = rng.uniform(0, 10, P); sb = rng.uniform(-1.5, 1.5, (S, D))
+    swarm = rng.integers(0, S, P).astype(np.int32)
+    lo, hi = np.full(D, -1.5), np.full(D, 1.5)
+    w, c1, c2, seed, gen, off = 0.83, 1.0, 1.0, 0x123456789A, 7, 1000
+    T = {k: torch.tensor(a).cuda() for k, a in dict(x=x, v=v, pb=pb, pbf=pbf, fit=fit, sb=sb, swarm=swarm,
+                                                      lo=lo, hi=hi).items()}
+    x32 = torch.empty(D, P, dtype=torch.float32, device="cuda")
+    lib = L.load()
+    L.check(lib.pd_pso_step(P, D, _ptr(T["fit"]), _ptr(T["pbf"]), _ptr(T["x"]), _ptr(T["v"]), _ptr(T["pb"]),
+                            _ptr(T["sb"]), _ptr(T["swarm"]), _ptr(T["lo"]), _ptr(T["hi"]), w, c1, c2, seed, gen,
+                            off, _ptr(x32), None))
+    torch.cuda.synchronize()
+    xn, vn, pbn, pbfn = _np_pso_step(x, v, pb, pbf, fit, sb, swarm, lo, hi, w, c1, c2, seed, gen, off)
+    assert np.array_equal(T["x"].cpu().numpy(), xn) and np.array_equal(T["v"].cpu().numpy(), vn)
+    assert np.array_equal(T["pb"].cpu().numpy(), pbn) and np.array_equal(T["pbf"].cpu().numpy(), pbfn)
+    assert np.array_equal(x32.cpu().numpy(), xn.astype(np.float32))
+
+
+def test_pso_driver_generations_vs_numpy(pd):
+    """Three generations of the device subswarm PSO (evaluation, subswarm/global bests, inertia
+    schedule, update, share_information and migrate_particles at generation 2) against a NumPy
+    restatement of ParticleSubswarmOptimisation.run fed the same fitness values."""
+    import random
+    import torch
+    from pdenv.pso import ParticleSubswarmOptimisationGPU
+    prm = dict(generations=3, communication_freq=2, migration_freq=2, re_initialise_generation=99)
+    opt = ParticleSubswarmOptimisationGPU("landing_burn_pure_throttle", pso_params=prm, pop_size=64, seed=5,
+                                          max_steps=400)
+    x = opt.x.cpu().numpy().copy(); v = np.zeros_like(x); pb = np.zeros_like(x)
+    pbf = np.full(opt.P, np.inf); swarm = opt.swarm.cpu().numpy().copy()
+    S, D = opt.S, opt.D
+    sb = np.zeros((S, D)); sbf = [np.inf] * S; gbf = np.inf
+    lo, hi = np.full(D, -1.5), np.full(D, 1.5)
+    rng = random.Random(5)
+    for gen in range(3):
+        opt.generation(gen)
+        fit = opt.last_fitness.cpu().numpy()
+        for s in range(S):
+            idx = np.nonzero(swarm == s)[0]
+            i = idx[np.argmin(fit[idx])]
+            if fit[i] < sbf[s]:
+                sbf[s], sb[s] = fit[i], x[:, i].copy()
+        for s in range(S):
+            gbf = min(gbf, sbf[s])
+        w = 0.9 - (0.9 - 0.4) * gen / 3
+        x, v, pb, pbf = _np_pso_step(x, v, pb, pbf, fit, sb, swarm, lo, hi, w, 1, 1, 5, gen, 0)
+        if gen == 2:
+            best = int(np.argmin(sbf))
+            moved = [i for i in range(S) if i != best and rng.random() < 0.5]
+            if moved:
+                assert opt.share_log[0] == moved
+                for k, i in enumerate(moved):
+                    sb[i] = (1 - 0.3) * sb[i] + 0.3 * sb[best]
+                    f = float(opt.share_log[1][k])
+                    if f < sbf[i]:
+                        sbf[i] = f
+            members = [list(np.nonzero(swarm == s)[0]) for s in range(S)]
+            for i in range(S):
+                if len(members[i]) > 1:
+                    k = rng.randrange(len(members[i]))
+                    g = members[i].pop(k)
+                    t = rng.choice([j for j in range(S) if j != i])
+                    members[t].append(g)
+                    swarm[g] = t
+    assert np.array_equal(opt.x.cpu().numpy(), x) and np.array_equal(opt.v.cpu().numpy(), v)
+    assert np.array_equal(opt.pb.cpu().numpy(), pb) and np.array_equal(opt.pbf.cpu().numpy(), pbf)
+    assert np.array_equal(opt.sb.cpu().numpy(), sb) and opt.sbf == sbf and opt.gbf == gbf
+    assert np.array_equal(opt.swarm.cpu().numpy(), swarm)
