@@ -106,44 +106,50 @@ def bench_sac(args, world, rank, local, dist):
 
 
 def bench_pso(args, world, rank, local, dist):
-    """Config c4: PSO generations of pso_wrapped_env.objective_function over P particles per GPU
-    (phase landing_burn, 372-parameter simple_actor per particle, positions U(-1.5, 1.5) as the
-    swarm is initialised), the actor fused into the step kernel (pd_rollout_policy).  One timed
-    step = one generation: every particle's episode until done/truncated (cap 2200)."""
+    """Config c4: generations of the particle subswarm optimisation over P particles per GPU
+    (phase landing_burn, 372-parameter simple_actor per particle, swarm initialised U(-1.5, 1.5)
+    as initialize_swarms does).  One timed step = one generation: every particle's episode with
+    the actor fused into the step kernel (pd_rollout_policy, until done/truncated, cap 2200),
+    subswarm/global bests with the per-subswarm minima exchanged across ranks, and the
+    velocity/position update (pd_pso_step)."""
     import torch
-    import pdenv
+    from pdenv.pso import ParticleSubswarmOptimisationGPU
     P = args.particles
-    env = pdenv.PoweredDescentEnv(P, flight_phase="landing_burn", mode="pso", precision=args.precision,
-                                  device=local, seed=1234, env_offset=shard_offset(rank, P))
-    g = torch.Generator(device=env.device).manual_seed(7 + rank)
-    T = args.warmup + args.steps
-    W = (torch.rand(T, P, 372, generator=g, device=env.device) * 3 - 1.5).contiguous()
-    for t in range(args.warmup):
-        env.rollout_policy(W[t], max_steps=2200, check_every=16)
+    opt = ParticleSubswarmOptimisationGPU("landing_burn", pop_size=P * world, device=local, seed=1234,
+                                          precision=args.precision, dist=dist,
+                                          pso_params=dict(generations=args.warmup + args.steps,
+                                                          re_initialise_generation=-1))
+    for g in range(args.warmup):
+        opt.generation(g)
     torch.cuda.synchronize()
-    tot = torch.zeros((), dtype=torch.int64, device=env.device)
+    tot = torch.zeros((), dtype=torch.int64, device=opt.device)
+    ev_steps = []
 
     def one(k):
-        fit, steps = env.rollout_policy(W[args.warmup + k], max_steps=2200, check_every=16)
-        tot.add_(steps.sum())
-    wall = timed_region(one, args.steps, torch.cuda.synchronize, dist, env.device)
+        opt.generation(args.warmup + k)
+    # episode lengths of the timed generations (a separate evaluation pass is not timed)
+    wall = timed_region(one, args.steps, torch.cuda.synchronize, dist, opt.device)
+    _, steps = opt.evaluate(opt.x32)
+    tot += steps.sum()
     if dist:
         dist.all_reduce(tot)
     if rank != 0:
         if dist:
             dist.destroy_process_group()
         return
-    env_steps = int(tot.item())
+    mean_len = int(tot.item()) / (P * world)
     eps = whole_job_rate(P, world, args.steps, wall)
     out = {
-        "metric": "PSO particle-episodes/sec (c4, fused actor)", "value": eps, "unit": "particle-episodes/s",
-        "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "metric": "PSO particle-episodes/sec (c4: fused actor rollouts + device swarm update)", "value": eps,
+        "unit": "particle-episodes/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": wall / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": args.precision,
-        "data": "synthetic (actor parameters U(-1.5,1.5) per particle, nominal initial state, no wind)",
-        "config": {"workload": "c4: PSO generation, landing_burn, 372-param simple_actor fused in k_step",
-                   "particles_per_gpu": P, "global_particles": P * world, "parallelism": f"particle-shard x{world}"},
-        "env_steps_per_s": env_steps / wall, "mean_episode_len": env_steps / (P * world * args.steps),
+        "data": "synthetic (swarm initialised U(-1.5,1.5) per parameter, nominal initial state, no wind)",
+        "config": {"workload": "c4: PSO generation, landing_burn, 372-param simple_actor fused in k_step, "
+                               "2 subswarms", "particles_per_gpu": P, "global_particles": P * world,
+                   "parallelism": f"particle-shard x{world} + subswarm-minimum all_gather"},
+        "env_steps_per_s_est": eps * mean_len, "mean_episode_len_after": mean_len,
+        "global_best_fitness": opt.gbf,
     }
     if args.cpu_baseline and world == 1:
         sys.path.insert(0, os.path.join(REPO, "oracle"))
