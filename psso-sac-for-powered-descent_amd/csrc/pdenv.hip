@@ -428,11 +428,20 @@ __device__ __forceinline__ R rbf(const StepArgs<R>& a, SolveLds* sl, int table, 
     unsigned long long ckey = cache.key;
     int cslot = cache.slot;
     int li = aq == ln.a[t.line0] ? t.line0 : (aq == ln.a[t.line0 + 1] ? t.line0 + 1 : -1);
+    bool trusted = false;
     if (li >= 0 && ln.nbp[li] >= 0) {
-        int l = 0, h = ln.nbp[li];
+        const int nb = ln.nbp[li];
+        int l = 0, h = nb;
         while (l < h) { int mid = (l + h) >> 1; if (ln.bp[li][mid] < M) l = mid + 1; else h = mid; }
         ckey = ln.key[li][l];
         cslot = ln.slot[li][l];
+        // The host split the line at EVERY pairwise bisector, so the 50-NN set is constant
+        // strictly between breakpoints: the interval's key is exact unless M lies within
+        // rounding distance of a breakpoint (then the search below verifies it).
+        const R eps = sizeof(R) == 8 ? R(1e-9) : R(1e-4);
+        const R blo = l > 0 ? ln.bp[li][l - 1] : R(-1);
+        const R bhi = l < nb ? ln.bp[li][l] : R(1e30);
+        trusted = cslot >= 0 && (M - blo > eps) && (bhi - M > eps);
     } else if (t.grid_key) {
         R fm = M * t.grid_inv_dm, fa = (aq - t.grid_a0) * t.grid_inv_da;
         int im = fm < R(0) ? 0 : (fm >= R(t.grid_nm) ? t.grid_nm - 1 : (int)fm);
@@ -442,24 +451,33 @@ __device__ __forceinline__ R rbf(const StepArgs<R>& a, SolveLds* sl, int table, 
         ckey = t.grid_key[cell];
         cslot = t.grid_slot[cell];
     }
-    int lo[kCols], len[kCols];
-    key_unpack(ckey, lo, len);
-    // keys store lo=0 for empty columns; knn_windows uses insertion points for those
+    unsigned long long key = ckey;
+    int slot = cslot;
+#ifdef PD_EXP_TRUSTCHECK
+    const bool check_trusted = trusted;
+    trusted = false;
+#endif
+    if (!trusted) {
+        int lo[kCols], len[kCols];
+        key_unpack(ckey, lo, len);
+        // keys store lo=0 for empty columns; knn_windows uses insertion points for those
 #ifndef PD_EXP_NOKNN
 #ifdef PD_EXP_COUNT
-    int iters = knn_windows<R>(t.smach, t.start, t.n, t.aoa, M, aq, lo, len);
-    atomicAdd(&a.pend.stats[4], 1ull);
-    atomicAdd(&a.pend.stats[5], (unsigned long long)(li >= 0));
-    atomicAdd(&a.pend.stats[6], (unsigned long long)iters);
+        int iters = knn_windows<R>(t.smach, t.start, t.n, t.aoa, M, aq, lo, len);
+        atomicAdd(&a.pend.stats[4], 1ull);
+        atomicAdd(&a.pend.stats[5], (unsigned long long)(li >= 0));
+        atomicAdd(&a.pend.stats[6], (unsigned long long)iters);
 #else
-    knn_windows<R>(t.smach, t.start, t.n, t.aoa, M, aq, lo, len);
+        knn_windows<R>(t.smach, t.start, t.n, t.aoa, M, aq, lo, len);
 #endif
 #endif
-    unsigned long long key = key_pack(lo, len);
-    int slot = key == ckey ? cslot : -1;
-#ifdef PD_EXP_COUNT
-    atomicAdd(&a.pend.stats[7], (unsigned long long)(slot < 0));
+        key = key_pack(lo, len);
+        slot = key == ckey ? cslot : -1;
+#ifdef PD_EXP_TRUSTCHECK
+        atomicAdd(&a.pend.stats[4], (unsigned long long)check_trusted);
+        atomicAdd(&a.pend.stats[7], (unsigned long long)(check_trusted && key != ckey));
 #endif
+    }
     if (slot < 0) {
         uint32_t mask = (1u << t.logcap) - 1u;
         uint32_t h = key_hash(key, t.logcap);
@@ -474,9 +492,6 @@ __device__ __forceinline__ R rbf(const StepArgs<R>& a, SolveLds* sl, int table, 
     cache.slot = slot;
     R val = R(0);
     if (slot >= 0) val = rbf_eval<R>(t.pay + (int64_t)slot * pay_stride<R>(), t.smach, t.saoa, M, aq, part, nparts);
-    // Misses (a neighbourhood outside the pre-enumerated tables): the converged wave solves
-    // each distinct (table, key) cooperatively in the workgroup's LDS scratch, evaluates the
-    // lanes that need it, and queues the payload for insertion (pd_flush_misses).
     // Misses (a neighbourhood outside the pre-enumerated tables) take the wave-cooperative
     // exact solve; the loop in rbf_miss_wave runs only when some lane of the wave missed
     if (__ballot(slot < 0)) {
@@ -563,7 +578,10 @@ template <bool WIND> struct Lds {
 template <typename R, int PHASE, int RTD, bool WIND, int LPE, int POL = 0>
 // waves_per_eu(2): caps VGPR+AGPR at 256 so the f64 kernel keeps two waves per SIMD (without it
 // the allocator spilled into AGPRs and ran one wave per SIMD, 20% slower on the c3 workload).
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) void k_step(StepArgs<R> a) {
+#ifndef PD_WPE
+#define PD_WPE 2
+#endif
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PD_WPE))) void k_step(StepArgs<R> a) {
     using L = Lds<WIND>;
     __shared__ R lds[L::kTotal];
     __shared__ LineLds<R> lines;
