@@ -40,6 +40,7 @@ pd_status fail(pd_status s, const std::string& m) { g_err = m; return s; }
 constexpr int kBlock = 256;
 constexpr int kScratch = kSys * kSys + kSys + 3 * kNbr + kPay;   // doubles per wave
 constexpr int kPendingCap = 1024;
+constexpr int kGridExact = 1 << 30;   // grid_slot flag: every point of the cell has its key
 
 // ---------------------------------------------------------------- per-env device buffers
 template <typename R> struct EnvBufs {
@@ -449,7 +450,13 @@ __device__ __forceinline__ R rbf(const StepArgs<R>& a, SolveLds* sl, int table, 
         if (!(fm == fm) || !(fa == fa)) { im = 0; ia = 0; }   // NaN queries
         int cell = im * t.grid_na + ia;
         ckey = t.grid_key[cell];
-        cslot = t.grid_slot[cell];
+        const int gsl = t.grid_slot[cell];
+        cslot = gsl < 0 ? -1 : (gsl & (kGridExact - 1));
+        // every point of an exact cell has the cell's key (convexity of 50-NN regions); the
+        // rounding margin keeps queries on a cell edge on the verified path
+        const R eps = sizeof(R) == 8 ? R(1e-9) : R(1e-4);
+        trusted = gsl >= 0 && (gsl & kGridExact) && fm - (R)im > eps && (R)(im + 1) - fm > eps &&
+                  fa - (R)ia > eps && (R)(ia + 1) - fa > eps;
     }
     unsigned long long key = ckey;
     int slot = cslot;
@@ -1204,18 +1211,29 @@ pd_status build_line(const pd_aero_table& t, double a, Table<R>& T, int li, DevP
 }
 
 // Candidate grid over the interior query domain [0, 10] Mach x [a0, a1]: the 50-NN key at
-// every cell centre (brute force), inserted into the table.  Device lookups verify it.
+// every cell centre (brute force), inserted into the table.  A 50-NN region is an intersection
+// of half-planes (order-k Voronoi cell), hence convex: when all four corners of a cell carry
+// the centre's key, the whole cell does, and the slot is flagged kGridExact so that device
+// lookups skip the verification.  Other cells' keys are candidates the device verifies.
 template <typename R>
 pd_status build_grid(const pd_aero_table& t, double a0, double a1, int nm, int na, Table<R>& T,
                      std::vector<unsigned long long>& gk, std::vector<int>& gs) {
     gk.assign((size_t)nm * na, 0); gs.assign((size_t)nm * na, -1);
     std::vector<double> work(kScratch), pay(kPay);
     double dm = 10.0 / nm, da = (a1 - a0) / na;
+    std::vector<uint64_t> corner((size_t)(nm + 1) * (na + 1));
+    for (int im = 0; im <= nm; ++im)
+        for (int ia = 0; ia <= na; ++ia)
+            corner[(size_t)im * (na + 1) + ia] = host_knn_key(t, im * dm, a0 + ia * da);
     for (int im = 0; im < nm; ++im)
         for (int ia = 0; ia < na; ++ia) {
             uint64_t key = host_knn_key(t, (im + 0.5) * dm, a0 + (ia + 0.5) * da);
             gk[(size_t)im * na + ia] = key;
-            gs[(size_t)im * na + ia] = table_insert<R>(t, T, key, work, pay);
+            int slot = table_insert<R>(t, T, key, work, pay);
+            bool exact = slot >= 0;
+            for (int c = 0; c < 4 && exact; ++c)
+                exact = corner[(size_t)(im + (c >> 1)) * (na + 1) + ia + (c & 1)] == key;
+            gs[(size_t)im * na + ia] = slot < 0 ? -1 : (slot | (exact ? kGridExact : 0));
         }
     return PD_OK;
 }
