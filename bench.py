@@ -81,7 +81,7 @@ def bench_sac(args, world, rank, local, dist):
     torch.manual_seed(0)
     actor = Actor(2, 1).to(env.device)
     buf = DeviceReplayBuffer(1_000_000, 2, 1, env.device) if rank == 0 else None
-    col = SACCollector(env, actor, buf, dist, generator=torch.Generator(device=env.device).manual_seed(rank))
+    col = SACCollector(env, actor, buf, dist, use_graph=args.graph == 1)
     for _ in range(args.warmup):
         col.step()
     wall = timed_region(lambda k: col.step(), args.steps, torch.cuda.synchronize, dist, env.device)
@@ -98,7 +98,7 @@ def bench_sac(args, world, rank, local, dist):
         "data": "synthetic (random-init SAC actor 2-256-256-1, reference initial state, no wind)",
         "config": {"workload": "c5: SAC collection, landing_burn_pure_throttle, rtd_rl, auto-reset",
                    "envs_per_gpu": n, "global_envs": n * world, "parallelism": f"env-shard x{world} + all_gather"},
-        "replay_buffer_size": len(buf),
+        "replay_buffer_size": len(buf), "hip_graph": args.graph == 1,
     }
     print(json.dumps(out))
     if dist:
@@ -123,7 +123,6 @@ def bench_pso(args, world, rank, local, dist):
         opt.generation(g)
     torch.cuda.synchronize()
     tot = torch.zeros((), dtype=torch.int64, device=opt.device)
-    ev_steps = []
 
     def one(k):
         opt.generation(args.warmup + k)
@@ -182,6 +181,7 @@ def main():
                     help="c3: env-steps/s headline; c4: PSO generations with the fused actor; "
                          "c5: SAC collection (actor + env + RCCL transition gather + replay buffer)")
     ap.add_argument("--particles", type=int, default=32768, help="c4: particles per GPU")
+    ap.add_argument("--graph", type=int, default=1, help="c5: replay the collection step as a HIP graph")
     args = ap.parse_args()
 
     import torch
@@ -214,13 +214,18 @@ def main():
         for t in range(args.warmup):
             env.step_raw(acts[t])
         torch.cuda.synchronize()
-        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-
-        def one(k):
+        # timed region: exactly K launches, nothing else on the stream (a per-launch event pair
+        # costs ~10 us of GPU time per step, so the kernel-duration pass is separate, below)
+        wall = timed_region(lambda k: env.step_raw(acts[args.warmup + k]), args.steps, torch.cuda.synchronize,
+                            dist, env.device)
+        # kernel duration: HIP events around every launch, on the stream the kernel runs on
+        kn = min(args.steps, 100)
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(kn)]
+        for k in range(kn):
             ev[k][0].record()
             env.step_raw(acts[args.warmup + k])
             ev[k][1].record()
-        wall = timed_region(one, args.steps, torch.cuda.synchronize, dist, env.device)
+        torch.cuda.synchronize()
         kern_ms = sorted(a.elapsed_time(b) for a, b in ev)
         c = env.counters()
         res = dict(wall=wall, kern_avg_ms=sum(kern_ms) / len(kern_ms), kern_med_ms=kern_ms[len(kern_ms) // 2],

@@ -113,6 +113,17 @@ class PoweredDescentEnv:
         if self._steps % self.flush_every == 0:
             self.flush()
 
+    def step_raw_noflush(self, actions):
+        """step_raw without the periodic aero-miss flush (graph capture: the caller flushes)."""
+        L.check(self.lib.pd_step(self.h, C.c_void_p(actions.data_ptr()), _ptr(self._obs), _ptr(self._rew),
+                                 _ptr(self._done), _ptr(self._trunc), _ptr(self._tid), None, None,
+                                 _stream(self.device)))
+
+    def observe_raw(self):
+        """pd_observe into the preallocated obs buffer (no copy); returns that buffer."""
+        L.check(self.lib.pd_observe(self.h, _ptr(self._obs), _stream(self.device)))
+        return self._obs
+
     @property
     def obs_buf(self):
         return self._obs

@@ -110,21 +110,58 @@ def gather_slabs(slab, dist=None):
 class SACCollector:
     """One collection step of N envs on this rank: actor sample -> env step -> slab -> gather ->
     learner-rank buffer append.  `obs` always holds the observation the actor sees next (the
-    post-auto-reset observation of envs whose episode ended)."""
+    post-auto-reset observation of envs whose episode ended).
 
-    def __init__(self, env, actor, buffer=None, dist=None, learner_rank=0, generator=None):
+    use_graph=True captures actor + env step + slab + observe into one HIP graph (the step is
+    ~20 small launches; replaying a graph removes their launch gaps).  The gather and the
+    buffer append run eagerly after each replay; the aero-miss flush runs every 16 steps."""
+
+    def __init__(self, env, actor, buffer=None, dist=None, learner_rank=0, generator=None,
+                 deterministic=False, use_graph=False, flush_every=16):
         self.env, self.actor, self.buffer, self.dist = env, actor, buffer, dist
-        self.learner_rank, self.generator = learner_rank, generator
+        self.learner_rank, self.generator, self.deterministic = learner_rank, generator, deterministic
         self.rank = dist.get_rank() if dist is not None and dist.is_initialized() else 0
-        self.obs = env.reset().float()
+        self.obs = env.reset().float().contiguous()
+        self.flush_every = flush_every
+        self.steps = 0
+        self.graph = None
+        self.use_graph = use_graph
 
-    @torch.no_grad()
-    def step(self):
-        act, _ = self.actor.sample(self.obs, generator=self.generator)
-        next_obs, rew, done, trunc, _ = self.env.step(act)
-        slab = transition_slab(self.obs, act, rew, next_obs, done)
+    def _body(self):
+        """actor -> pd_step -> slab -> observe into self.obs; returns the slab (no syncs)."""
+        gen = None if self.use_graph else self.generator
+        act, _ = self.actor.sample(self.obs, deterministic=self.deterministic, generator=gen)
+        act = act.float().contiguous()
+        self.env.step_raw_noflush(act)
+        slab = transition_slab(self.obs, act, self.env.reward_buf, self.env.obs_buf, self.env.done_buf)
+        self.obs.copy_(self.env.observe_raw().float())
+        return slab
+
+    def _finish(self, slab):
+        self.steps += 1
+        if self.steps % self.flush_every == 0:
+            self.env.flush()
         full = gather_slabs(slab, self.dist)
         if self.rank == self.learner_rank and self.buffer is not None:
             self.buffer.add_batch(full)
-        self.obs = self.env.observe().float()
         return full
+
+    @torch.no_grad()
+    def step(self):
+        if not self.use_graph:
+            return self._finish(self._body())
+        if self.graph is None:
+            # one eager step on a side stream warms the allocator and the kernels; it is a real
+            # step (its transitions are kept), then the next step is captured and replayed
+            s = torch.cuda.Stream(device=self.obs.device)
+            s.wait_stream(torch.cuda.current_stream(self.obs.device))
+            with torch.cuda.stream(s):
+                slab = self._body()
+            torch.cuda.current_stream(self.obs.device).wait_stream(s)
+            full = self._finish(slab)
+            self.graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.graph):
+                self._slab = self._body()
+            return full
+        self.graph.replay()
+        return self._finish(self._slab)

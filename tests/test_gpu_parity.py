@@ -498,3 +498,24 @@ def test_pso_driver_generations_vs_numpy(pd):
     assert np.array_equal(opt.pb.cpu().numpy(), pb) and np.array_equal(opt.pbf.cpu().numpy(), pbf)
     assert np.array_equal(opt.sb.cpu().numpy(), sb) and opt.sbf == sbf and opt.gbf == gbf
     assert np.array_equal(opt.swarm.cpu().numpy(), swarm)
+
+
+def test_sac_collector_graph_equals_eager(pd):
+    """The HIP-graph collection step stores exactly the transitions of the eager step
+    (deterministic actor, twin envs, 40 steps including auto-resets and miss flushes)."""
+    import torch
+    from pdenv.sac import Actor, DeviceReplayBuffer, SACCollector
+    torch.manual_seed(0)
+    N = 1024
+    actor = Actor(2, 1).cuda()
+    bufs = []
+    for g in (False, True):
+        env = make(pd, N, mode="rl", auto_reset=True, seed=6, tilt_sigma_rad=0.05)
+        buf = DeviceReplayBuffer(64 * N, 2, 1, "cuda")
+        col = SACCollector(env, actor, buf, deterministic=True, use_graph=g)
+        for _ in range(40):
+            col.step()
+        torch.cuda.synchronize()
+        bufs.append(buf)
+    assert len(bufs[0]) == len(bufs[1]) == 40 * N
+    assert torch.equal(bufs[0].data, bufs[1].data)
