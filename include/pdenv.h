@@ -102,7 +102,8 @@ typedef struct {
     int32_t auto_reset;        /* reset envs in-kernel when done|truncated */
     double tilt_sigma_rad;     /* initial pitch perturbation N(0, s) (0 = reference) */
     int32_t action_f64;        /* actions are double (f64 path, no float32 islands) */
-    int32_t lanes_per_env;     /* step-kernel lanes per env: 1, 2, 4 or 8 (0 = default 2) */
+    int32_t lanes_per_env;     /* step-kernel lanes per env: 1, 2, 4 or 8 (0 = by n_envs: 8 up to
+                                  8 192 envs, 4 up to 32 768, else 2) */
 } pd_config;
 
 typedef enum {
