@@ -72,7 +72,7 @@ def bench_sac(args, world, rank, local, dist):
     to the learner rank's device replay buffer."""
     import torch
     import pdenv
-    from pdenv.sac import Actor, DeviceReplayBuffer, SACCollector
+    from pdenv.sac import Actor, DevicePrioritizedReplayBuffer, SACCollector
     n = args.envs if args.envs != 65536 else 4096
     env = pdenv.PoweredDescentEnv(n, flight_phase="landing_burn_pure_throttle", mode="rl",
                                   precision=args.precision, device=local, auto_reset=True, seed=1234,
@@ -80,7 +80,8 @@ def bench_sac(args, world, rank, local, dist):
     env.flush_every = 16
     torch.manual_seed(0)
     actor = Actor(2, 1).to(env.device)
-    buf = DeviceReplayBuffer(1_000_000, 2, 1, env.device) if rank == 0 else None
+    # the driver's buffer: PrioritizedReplayBuffer, 1e6 transitions (sac_pytorch_powered_descent.py:62-70)
+    buf = DevicePrioritizedReplayBuffer(1_000_000, 2, 1, env.device) if rank == 0 else None
     col = SACCollector(env, actor, buf, dist, use_graph=args.graph == 1)
     for _ in range(args.warmup):
         col.step()
@@ -90,7 +91,7 @@ def bench_sac(args, world, rank, local, dist):
             dist.destroy_process_group()
         return
     out = {
-        "metric": "SAC collection env-steps/sec (c5: actor + env + RCCL gather + replay buffer)",
+        "metric": "SAC collection env-steps/sec (c5: actor + env + RCCL gather + prioritized replay buffer)",
         "value": whole_job_rate(n, world, args.steps, wall), "unit": "env-steps/s",
         "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": wall / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",

@@ -90,6 +90,54 @@ class DeviceReplayBuffer:
         return self.size
 
 
+class DevicePrioritizedReplayBuffer(DeviceReplayBuffer):
+    """The reference's PrioritizedReplayBuffer (sac_pytorch.py:51-127; the SAC driver's buffer,
+    use_per=True) as device tensors.
+
+    New transitions get the current max priority.  sample() draws batch_size distinct indices
+    with probability proportional to priority**alpha without replacement -- the distribution of
+    np.random.choice(size, batch, replace=False, p=probs) -- by the Gumbel-top-k construction
+    (top-k of alpha*log(priority) + Gumbel noise), returns importance weights
+    (size*probs)**(-beta) / max, and anneals beta."""
+
+    def __init__(self, capacity, state_dim, action_dim, device, alpha=0.6, beta=0.4,
+                 beta_annealing_steps=100000, epsilon=1e-6):
+        super().__init__(capacity, state_dim, action_dim, device)
+        self.alpha, self.beta, self.epsilon = alpha, beta, epsilon
+        self.beta_increment = (1.0 - beta) / beta_annealing_steps
+        self.priorities = torch.zeros(self.capacity, dtype=torch.float32, device=device)
+        self.max_priority = 1.0
+
+    def add_batch(self, slab):
+        b = min(slab.shape[0], self.capacity)
+        idx = (self.position + torch.arange(b, device=self.data.device)) % self.capacity
+        self.priorities[idx] = self.max_priority
+        super().add_batch(slab)
+
+    def sample(self, batch_size, generator=None):
+        if self.size == 0:
+            return None
+        pr = self.priorities[:self.size].double()
+        probs = pr ** self.alpha
+        probs = probs / probs.sum()
+        u = torch.rand(self.size, dtype=torch.float64, device=self.data.device, generator=generator)
+        gumbel = -torch.log(-torch.log(u.clamp_min(1e-300)))
+        idx = torch.topk(torch.log(probs) + gumbel, batch_size).indices
+        w = (self.size * probs[idx]) ** (-self.beta)
+        w = (w / w.max()).float().reshape(-1, 1)
+        self.beta = min(1.0, self.beta + self.beta_increment)
+        d = self.data[idx]
+        S, A = self.state_dim, self.action_dim
+        return (d[:, :S], d[:, S:S + A], d[:, S + A:S + A + 1], d[:, S + A + 1:2 * S + A + 1],
+                d[:, 2 * S + A + 1:], w, idx)
+
+    def update_priorities(self, indices, td_errors):
+        """sac_pytorch.py:120-124: priority = |td| + epsilon; max_priority tracks the largest."""
+        p = td_errors.detach().reshape(-1).abs().float() + self.epsilon
+        self.priorities[indices] = p
+        self.max_priority = max(self.max_priority, float(p.max()))
+
+
 def transition_slab(obs, action, reward, next_obs, done):
     """[N, 2S + A + 2] float32: state | action | reward | next_state | done (done, not truncated,
     as the driver stores it: sac_pytorch_powered_descent.py:170-176)."""

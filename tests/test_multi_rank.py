@@ -135,3 +135,35 @@ def test_sac_transition_gather_into_replay_buffer():
     ring = np.roll(rows[-12:], 30 % 12, axis=0)     # row t lands at t % 12
     assert np.array_equal(data, ring)
     assert [tuple(s) for s in shapes] == [(7, 2), (7, 1), (7, 1), (7, 2), (7, 1)]
+
+
+def test_prioritized_buffer_sampling_distribution():
+    """Device PER (Gumbel-top-k) draws pairs with the probabilities of
+    np.random.choice(size, 2, replace=False, p) and reproduces the reference's weights and
+    priority bookkeeping (sac_pytorch.py:77-124)."""
+    import itertools
+    sys.path.insert(0, os.path.join(REPO, "psso-sac-for-powered-descent_amd"))
+    from pdenv.sac import DevicePrioritizedReplayBuffer
+    buf = DevicePrioritizedReplayBuffer(8, 1, 1, "cpu", alpha=0.6, beta=0.4, beta_annealing_steps=10)
+    buf.add_batch(torch.arange(5 * 5, dtype=torch.float32).reshape(5, 5))
+    assert torch.equal(buf.priorities[:5], torch.ones(5))
+    buf.update_priorities(torch.arange(5), torch.tensor([0.5, 1.0, 2.0, 4.0, 8.0]))
+    assert buf.max_priority == pytest.approx(8.0 + 1e-6)
+    p = (np.array([0.5, 1.0, 2.0, 4.0, 8.0]) + 1e-6) ** 0.6
+    p /= p.sum()
+    exact = {}
+    for i, j in itertools.permutations(range(5), 2):
+        exact[(i, j)] = p[i] * p[j] / (1 - p[i])
+    g = torch.Generator().manual_seed(0)
+    counts = {k: 0 for k in exact}
+    T = 40000
+    beta0 = buf.beta
+    for _ in range(T):
+        s, a, r, s2, d, w, idx = buf.sample(2, generator=g)
+        counts[tuple(int(v) for v in idx)] += 1
+    assert buf.beta == pytest.approx(min(1.0, beta0 + T * (1 - 0.4) / 10))
+    for k, e in exact.items():
+        assert abs(counts[k] / T - e) < 5 * np.sqrt(e * (1 - e) / T) + 1e-3, (k, counts[k] / T, e)
+    # weights of the last draw: (size * p)^-beta / max, beta as it was before the last anneal
+    wr = (5 * p[idx.numpy()]) ** (-1.0)
+    assert np.allclose(w.numpy().ravel(), wr / wr.max(), rtol=1e-6)
