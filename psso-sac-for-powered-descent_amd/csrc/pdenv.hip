@@ -1482,9 +1482,14 @@ template <typename R> void dispatch_step(const pd_env* e, const StepArgs<R>& a, 
     else { if (w) launch_lpe<R, 1, 1, true>(l, a, s); else launch_lpe<R, 1, 1, false>(l, a, s); }
 }
 
-template <typename R, int PH, bool W> void launch_policy(const StepArgs<R>& a, hipStream_t s) {
-    unsigned grid = (unsigned)((a.n * 2 + kBlock - 1) / kBlock);
-    hipLaunchKernelGGL((k_step<R, PH, 1, W, 2, 1>), dim3(grid), dim3(kBlock), 0, s, a);
+template <typename R, int PH, bool W, int LPE> void launch_policy_lpe(const StepArgs<R>& a, hipStream_t s) {
+    unsigned grid = (unsigned)((a.n * LPE + kBlock - 1) / kBlock);
+    hipLaunchKernelGGL((k_step<R, PH, 1, W, LPE, 1>), dim3(grid), dim3(kBlock), 0, s, a);
+}
+template <typename R, int PH, bool W> void launch_policy(const StepArgs<R>& a, int lpe, hipStream_t s) {
+    if (lpe >= 8) launch_policy_lpe<R, PH, W, 8>(a, s);
+    else if (lpe == 4) launch_policy_lpe<R, PH, W, 4>(a, s);
+    else launch_policy_lpe<R, PH, W, 2>(a, s);
 }
 
 template <typename R> void launch_insert(pd_env* e, hipStream_t s) {
@@ -1515,8 +1520,8 @@ pd_status rollout_policy_impl(pd_env* e, const float* w, int32_t max_steps, void
     a.policy_w = w; a.reward_sum = (R*)fitness; a.auto_reset = 0;
     const bool wind = e->cfg.enable_wind != 0;
     for (int32_t t = 0; t < max_steps; ++t) {
-        if (e->cfg.phase == PD_PHASE_PURE_THROTTLE) { if (wind) launch_policy<R, 0, true>(a, s); else launch_policy<R, 0, false>(a, s); }
-        else { if (wind) launch_policy<R, 1, true>(a, s); else launch_policy<R, 1, false>(a, s); }
+        if (e->cfg.phase == PD_PHASE_PURE_THROTTLE) { if (wind) launch_policy<R, 0, true>(a, e->lpe, s); else launch_policy<R, 0, false>(a, e->lpe, s); }
+        else { if (wind) launch_policy<R, 1, true>(a, e->lpe, s); else launch_policy<R, 1, false>(a, e->lpe, s); }
         PD_HIP(hipGetLastError());
         if ((t & 15) == 15) launch_insert<R>(e, s);
         if (check_every > 0 && (t + 1) % check_every == 0 && t + 1 < max_steps) {
