@@ -35,8 +35,11 @@ def kernel_avg_ns(stats_csv, kernel="k_step"):
 
 def main(tag="r01"):
     os.makedirs(PROF, exist_ok=True)
-    summary = {"source": "tools/gpu_session.sh stages prof/prof32/pmc/pmc32/pmcv on one MI355X; "
-                         "workload = bench.py defaults (c3, 65536 envs)"}
+    # merge into the existing summary: a session that ran only some stages keeps the others
+    prev = os.path.join(PROF, "pmc_traffic.json")
+    summary = json.load(open(prev)) if os.path.exists(prev) else {}
+    summary["source"] = ("tools/gpu_session.sh stages prof/prof32/pmc/pmc32/pmcv on one MI355X; "
+                         "workload = bench.py defaults (c3, 65536 envs)")
     for prec, d in (("f64", "prof"), ("f32", "prof32")):
         src = os.path.join(OUT, d, "run_kernel_stats.csv")
         if os.path.exists(src):
