@@ -16,12 +16,16 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB = os.path.join(HERE, "build", "liborc.so")
 PACK = os.path.join(HERE, "..", "psso-sac-for-powered-descent_amd", "data", "param_pack.json")
 
-MAXP, MAXT, MAXW = 256, 64, 16
+MAXP, MAXT, MAXW, MAXREF, NPH = 256, 64, 16, 1024, 7
 D = C.c_double
 I32 = C.c_int32
 
-PURE_THROTTLE, LANDING_BURN = 0, 1
-RTD_RL, RTD_PSO = 0, 1
+PURE_THROTTLE, LANDING_BURN, PCONTROL, BALLISTIC, FLIP, SUBSONIC, SUPERSONIC = range(7)
+RTD_RL, RTD_PSO, RTD_NONE = 0, 1, 2
+PHASE_NAMES = ["landing_burn_pure_throttle", "landing_burn", "landing_burn_pure_throttle_Pcontrol",
+               "ballistic_arc_descent", "flip_over_boostbackburn", "subsonic", "supersonic"]
+ACTION_DIM = [1, 4, 1, 1, 1, 2, 2]
+OBS_DIM_RL = [2, 5, 1, 4, 2, 8, 8]
 
 INFO_NAMES = ["air_density", "atmospheric_pressure", "speed_of_sound", "mach_number",
               "dynamic_pressure", "CL", "CD", "mass_flow", "x_cog", "inertia", "d_thrust_cg",
@@ -53,6 +57,12 @@ class OrcParams(C.Structure):
         ("vk_Ad_u", D * 4), ("vk_Bd_u", D * 2), ("vk_Ad_v", D * 4), ("vk_Bd_v", D * 2),
         ("vk_y_threshold", D),
         ("state0", D * 11), ("norm_y", D), ("norm_vy", D), ("norm_x", D), ("norm_vx", D),
+        ("fr", D * 13), ("cop_ascent", D), ("n_eng_stage1", I32), ("n_ref", I32),
+        ("rcs_force", D), ("rcs_d_bottom", D), ("rcs_d_top", D),
+        ("state0_ph", (D * 11) * NPH), ("norm_ph", (D * 8) * NPH),
+        ("ref_y", D * MAXREF), ("ref_x", D * MAXREF), ("ref_vx", D * MAXREF), ("ref_vy", D * MAXREF),
+        ("hyper", ((D * 9) * 12) * 2), ("terminal_mach", D * 2), ("speed0_pc", D),
+        ("rl_discount", D), ("rl_traj_len", I32), ("pad2", I32),
     ]
 
 
@@ -60,12 +70,12 @@ class OrcEnv(C.Structure):
     _fields_ = [("s", D * 11), ("prev_s", D * 11), ("gwin", D * 10), ("gwin_len", I32),
                 ("trunc_id", I32), ("gimbal_prev", D), ("dl_prev", D), ("dr_prev", D),
                 ("wind_on", I32), ("wind_stoch", I32), ("sigma_u", D), ("sigma_v", D),
-                ("fu", D * 2), ("fv", D * 2), ("noise_slotted", I32), ("noise_used", I32)]
+                ("fu", D * 2), ("fv", D * 2), ("noise_slotted", I32), ("noise_used", I32), ("dt", D)]
 
 
 class OrcOut(C.Structure):
     _fields_ = [("reward", D), ("done", I32), ("trunc", I32), ("trunc_id", I32), ("pad", I32),
-                ("obs", D * 5), ("info", D * len(INFO_NAMES))]
+                ("obs", D * 8), ("info", D * len(INFO_NAMES))]
 
 
 def build():
@@ -164,6 +174,25 @@ def make_params(pack=None, wind_percentile=50):
     _fill(p.state0, pk["state0"])
     nm = pk["norm"]
     p.norm_y, p.norm_vy, p.norm_x, p.norm_vx = nm["y"], nm["vy"], nm["x"], nm["vx"]
+    ph = pk["phases"]
+    fr = ph["ascent_inertia"]
+    _fill(p.fr, [fr[k] for k in ("x_wet_2_initial", "x_dry_1", "m_s_1", "m_pay", "m_2", "m_1_ox", "m_1_f",
+                                 "h_lower_1", "h_1_ox", "h_1_f", "h_1", "I_wet_2_initial", "I_dry_1")])
+    p.cop_ascent = ph["cop_ascent"]
+    p.n_eng_stage1 = ph["n_engines_stage1"]
+    p.rcs_force, p.rcs_d_bottom, p.rcs_d_top = ph["rcs"]["max_force"], ph["rcs"]["d_bottom"], ph["rcs"]["d_top"]
+    for k, name in enumerate(PHASE_NAMES):
+        _fill(p.state0_ph[k], ph["state0"].get(name, pk["state0"]))
+        _fill(p.norm_ph[k], ph["norm"].get(name, [nm["y"], nm["vy"]]))
+    ref = ph["ascent_ref"]
+    p.n_ref = len(ref["y"])
+    _fill(p.ref_y, ref["y"]); _fill(p.ref_x, ref["x"]); _fill(p.ref_vx, ref["vx"]); _fill(p.ref_vy, ref["vy"])
+    for w, name in enumerate(("subsonic", "supersonic")):
+        for r, row in enumerate(ph["ascent_hyper"][name]):
+            _fill(p.hyper[w][r], [float(v) for v in row])
+        p.terminal_mach[w] = ph["terminal_mach"][name]
+    p.speed0_pc = ph["speed0_pcontrol"]
+    p.rl_discount, p.rl_traj_len = 0.99, 100
     return p
 
 
@@ -171,19 +200,25 @@ class Oracle:
     """Scalar single-env oracle with the reference's reset/step surface."""
 
     def __init__(self, phase=PURE_THROTTLE, rtd=RTD_RL, wind=False, stochastic=False,
-                 sigma_u=0.0, sigma_v=0.0, wind_percentile=50, pack=None):
+                 sigma_u=0.0, sigma_v=0.0, wind_percentile=50, pack=None, discount_factor=0.99,
+                 trajectory_length=100, dt=0.0):
         self.L = lib()
         self.P = make_params(pack, wind_percentile)
+        self.P.rl_discount, self.P.rl_traj_len = float(discount_factor), int(trajectory_length)
+        self.dt = float(dt)
         self.E = OrcEnv()
         self.phase, self.rtd = phase, rtd
         self.wind, self.stoch, self.su, self.sv = wind, stochastic, sigma_u, sigma_v
         self.reset()
 
     def reset(self, state=None):
-        s0 = None if state is None else (D * 11)(*[float(v) for v in state])
+        if state is None:
+            state = list(self.P.state0_ph[self.phase])
+        s0 = (D * 11)(*[float(v) for v in state])
         self.L.orc_reset(C.byref(self.P), C.byref(self.E), s0, int(self.wind), int(self.stoch),
                          float(self.su), float(self.sv))
         self.E.noise_slotted = int(getattr(self, "slotted", 0))
+        self.E.dt = self.dt
         return np.array(self.E.s[:])
 
     @property
@@ -203,14 +238,17 @@ class Oracle:
         o = OrcOut()
         self.L.orc_step(C.byref(self.P), C.byref(self.E), self.phase, self.rtd, ua, int(f32), nz, C.byref(o))
         info = dict(zip(INFO_NAMES, o.info[:]))
+        nobs = OBS_DIM_RL[self.phase] if self.rtd != RTD_PSO else (2 if self.phase == PURE_THROTTLE else 5)
         return (np.array(self.E.s[:]), o.reward, bool(o.done), bool(o.trunc), int(o.trunc_id),
-                np.array(o.obs[:]), info)
+                np.array(o.obs[:nobs]), info)
 
     def physics(self, state, actions, f32=True, prevs=(0.0, 0.0, 0.0)):
         """Teacher-forced physics only (compile_physics lambda) from an arbitrary state."""
         self.reset(state)
         self.E.gimbal_prev, self.E.dl_prev, self.E.dr_prev = prevs
         a = np.asarray(actions, dtype=np.float64).ravel()
+        if f32:
+            a = a.astype(np.float32).astype(np.float64)
         ua = (D * 4)(*list(a) + [0.0] * (4 - len(a)))
         info = (D * len(INFO_NAMES))()
         self.L.orc_physics(C.byref(self.P), C.byref(self.E), self.phase, ua, int(f32), None, info)

@@ -212,6 +212,37 @@ void orc_inertia(const orc_params* P, double fill, double* x_cog, double* inerti
     *inertia = I_dry_hat + I_prop_hat;
 }
 
+/* full_rocket_inertia closure (rocket_dimensions.py:198-241), the ascent phases'
+ * x_cog_inertia_subrocket_0_lambda; restated with its own expression order (x_prop_1 uses the
+ * untilded m_1_f and h_ox_1_tilde as written). */
+static void orc_inertia_full(const orc_params* P, double fill, double* x_cog, double* inertia) {
+    const double* c = P->fr;
+    double x_wet2 = c[0], x_dry1 = c[1], m_s1 = c[2], m_pay = c[3], m_2 = c[4], m1_ox = c[5], m1_f = c[6];
+    double h_lower1 = c[7], h1_ox = c[8], h1_f = c[9], h1 = c[10], I_wet2 = c[11], I_dry1 = c[12];
+    double h_ox_t = h1_ox * fill, h_f_t = h1_f * fill, m_ox_t = m1_ox * fill, m_f_t = m1_f * fill;
+    double m_prop_t = m_ox_t + m_f_t;
+    double x_prop = (m_ox_t * (h_lower1 + h_ox_t / 2) + m1_f * (h_lower1 + h_ox_t + h_f_t / 2)) / (m_ox_t + m_f_t);
+    double t1 = h_lower1 + h_ox_t / 2 - x_prop;
+    double I_ox = 1.0 / 12 * m_ox_t * (h_ox_t * h_ox_t) + m_ox_t * (t1 * t1);
+    double t2 = h_lower1 + h_ox_t + h_f_t / 2 - x_prop;
+    double I_f = 1.0 / 12 * m_f_t * (h_f_t * h_f_t) + m_f_t * (t2 * t2);
+    double I_prop = I_ox + I_f;
+    double xr = (m_s1 * x_dry1 + (m_2 + m_pay) * (x_wet2 + h1) + m_prop_t * x_prop) / (m_s1 + m_2 + m_pay + m_prop_t);
+    double a = x_dry1 - xr, b = x_wet2 - xr, d = x_prop - xr;
+    *x_cog = xr;
+    *inertia = I_dry1 + m_s1 * (a * a) + I_wet2 + m_2 * (b * b) + I_prop + m_prop_t * (d * d);
+}
+
+/* scipy interp1d(kind='linear', fill_value='extrapolate') -> _call_linear: lo/hi from
+ * searchsorted(x, v) (side='left') clipped to [1, n-1] */
+static double interp1d_ext(const double* x, const double* y, int n, double v) {
+    int lo = 0, hi = n;
+    while (lo < hi) { int mid = (lo + hi) / 2; if (x[mid] < v) lo = mid + 1; else hi = mid; }
+    int i = lo < 1 ? 1 : (lo > n - 1 ? n - 1 : lo);
+    double slope = (y[i] - y[i - 1]) / (x[i] - x[i - 1]);
+    return slope * (v - x[i - 1]) + y[i - 1];
+}
+
 /* ---------------------------------------------------------------- ACS (acs_model.py:13-87) */
 typedef struct { double f_perp, f_par, m_z, dcmd_l, dcmd_r, ca, cn_l; } acs_res;
 static acs_res acs(const orc_params* P, double alpha_eff, double q, double mach, double x_cog,
@@ -267,10 +298,13 @@ static void substep(const orc_params* P, orc_env* E, int phase, const double* u,
     double fpc = (P->m_prop0 - mp) / P->m_prop0;
     if (fpc == 0.0) fpc = 1e-6;
     double x_cog, inertia;
-    orc_inertia(P, 1 - fpc, &x_cog, &inertia);
+    const int ascent = phase == ORC_PHASE_SUBSONIC || phase == ORC_PHASE_SUPERSONIC;
+    /* subrocket_0 closures for the ascent, subrocket_2 for everything after (:748-750, :772-774) */
+    if (ascent) orc_inertia_full(P, 1 - fpc, &x_cog, &inertia);
+    else orc_inertia(P, 1 - fpc, &x_cog, &inertia);
     double d_thrust = x_cog + P->engine_height;
     double ae = (vy < 0) ? ga - th - PI : al;
-    double d_cp_cg = x_cog - P->cop;
+    double d_cp_cg = x_cog - (ascent ? P->cop_ascent : P->cop);
     double ug = 0.0, vg = 0.0;
     if (E->wind_on) {
         ug = wind_profile(P, y);
@@ -304,8 +338,94 @@ static void substep(const orc_params* P, orc_env* E, int phase, const double* u,
 
     double T_full = P->T_e + (P->p_e - patm) * P->A_e;
     double cfp, cfperp, cm, mdot_dt, mdot_info, throttle_info, gimbal_deg_out = 0.0;
+    /* binary32 control forces (ascent with float32 actions): the force sums below then run in
+     * binary32 too, because the aerodynamic terms are Python floats (weak under NEP 50) */
+    int f32_forces = 0;
+    float cfp_f = 0.0f, cfperp_f = 0.0f;
     acs_res ac;
-    if (phase == ORC_PHASE_PURE_THROTTLE) {
+    memset(&ac, 0, sizeof(ac));
+    if (phase == ORC_PHASE_FLIP) {
+        /* flip-over aero is zeroed after the coefficients are computed (:548-551) */
+        aero_x = 0.0; aero_y = 0.0; aero_m = 0.0;
+    }
+    if (phase == ORC_PHASE_PCONTROL) {
+        /* force_moment_decomposer_landing_burn_throttle_PID (:402-451): Kp -0.08 on v_ref - speed,
+         * clip to [0, 1], handed to throttle_only as a list -> u0 = float(...) (binary64 onward) */
+        double u0;
+        if (f32) {
+            float err = (float)u[0] - (float)speed;
+            float nt = err * (float)(-0.08);
+            nt = nt < 0.0f ? 0.0f : (nt > 1.0f ? 1.0f : nt);
+            u0 = (double)(2.0f * (nt - 0.5f));
+        } else {
+            double nt = (u[0] - speed) * -0.08;
+            nt = nt < 0.0 ? 0.0 : (nt > 1.0 ? 1.0 : nt);
+            u0 = 2 * (nt - 0.5);
+        }
+        const double nominal = (0 * 0.4) / (double)P->n_eng;
+        double thr = (u0 + 1) / 2 * (1 - nominal) + nominal;
+        double tg = T_full * P->n_eng * thr;
+        double md = (P->T_e / P->v_ex) * (tg / T_full);
+        ac = acs(P, ae, q, mach, x_cog, 0.0, 0.0, 0.0, 0.0, dt_act);
+        cfp = tg + ac.f_par; cfperp = ac.f_perp; cm = ac.m_z;
+        mdot_dt = md * dt; mdot_info = md; throttle_info = thr;
+    } else if (phase == ORC_PHASE_BALLISTIC) {
+        /* RCS (:149-166): thruster force = max * action (array), moment promoted to binary64 by
+         * the float64 x_cog; no forces, no mass flow */
+        double tf = f32 ? (double)((float)P->rcs_force * (float)u[0]) : P->rcs_force * u[0];
+        cfp = 0.0; cfperp = 0.0;
+        cm = -tf * (x_cog - P->rcs_d_bottom) + tf * (P->rcs_d_top - x_cog);
+        mdot_dt = 0.0; mdot_info = 0.0; throttle_info = 0.0;
+    } else if (phase == ORC_PHASE_FLIP) {
+        /* force_moment_decomposer_flipoverboostbackburn (:63-92): low-pass of the gimbal command
+         * (tau 1, dt = physics dt), all 16 gimballed engines at full throttle.  The filtered
+         * angle is the action's dtype (float32 array with float32 actions). */
+        double gd;
+        if (f32) {
+            float cmd = (float)u[0] * 10.0f, x0 = (float)E->gimbal_prev;
+            gd = (double)(x0 + (float)dt * ((-x0 + cmd) / 1.0f));
+        } else {
+            double cmd = u[0] * 10;
+            gd = E->gimbal_prev + dt * ((-E->gimbal_prev + cmd) / 1.0);
+        }
+        double grad = radians(gd);
+        double tg = T_full * P->n_eng * 1;
+        double tpar = tg * cos(grad), tperp = -tg * sin(grad);
+        cfp = tpar; cfperp = tperp; cm = -tg * sin(grad) * d_thrust;
+        double md = (P->T_e / P->v_ex) * (sqrt(tpar * tpar + tperp * tperp) / T_full);
+        mdot_dt = md * dt; mdot_info = md; throttle_info = 1.0;
+        gimbal_deg_out = gd;
+        E->gimbal_prev = gd;   /* base_environment.py:110 */
+    } else if (ascent) {
+        /* force_moment_decomposer_ascent (:17-56): 16 gimballed + 26 fixed engines, nominal 0.5,
+         * gimbal radians(7) */
+        const int ng = P->n_eng, nng = P->n_eng_stage1 - P->n_eng;
+        const double mg = radians(7.0);
+        if (f32) {
+            float grad = (float)u[0] * (float)mg;
+            float nnt = ((float)u[1] + 1.0f) / 2.0f;
+            float thr = nnt * (float)(1 - 0.5) + (float)0.5;
+            float tg = (float)(T_full * ng) * thr, tng = (float)(T_full * nng) * thr;
+            float cg = (float)cos((double)grad), sg = (float)sin((double)grad);
+            float tpar = tng + tg * cg;
+            float tperp = (-tg) * sg;
+            float tot = sqrtf(tpar * tpar + tperp * tperp);
+            float md = (float)(P->T_e / P->v_ex) * (tot / (float)T_full);
+            cfp_f = tpar; cfperp_f = tperp; f32_forces = 1;
+            cfp = tpar; cfperp = tperp; cm = (double)((-tg) * sg) * d_thrust;
+            mdot_dt = (double)(md * (float)dt); mdot_info = md; throttle_info = thr;
+            gimbal_deg_out = degrees((double)grad);
+        } else {
+            double grad = u[0] * mg;
+            double thr = (u[1] + 1) / 2 * (1 - 0.5) + 0.5;
+            double tg = T_full * ng * thr, tng = T_full * nng * thr;
+            double tpar = tng + tg * cos(grad), tperp = -tg * sin(grad);
+            cfp = tpar; cfperp = tperp; cm = -tg * sin(grad) * d_thrust;
+            double md = (P->T_e / P->v_ex) * (sqrt(tpar * tpar + tperp * tperp) / T_full);
+            mdot_dt = md * dt; mdot_info = md; throttle_info = thr;
+            gimbal_deg_out = degrees(grad);
+        }
+    } else if (phase == ORC_PHASE_PURE_THROTTLE) {
         const double nominal = (0 * 0.4) / (double)P->n_eng;
         if (f32) {
             float u0 = (float)u[0];
@@ -389,10 +509,26 @@ static void substep(const orc_params* P, orc_env* E, int phase, const double* u,
     if (isnan(cfp)) cfp = 0.0;
     else if (isnan(cfperp)) cfperp = 0.0;
     else if (isnan(cm)) cm = 0.0;
-    double cfx = cfp * cos(th) + cfperp * sin(th);
-    double cfy = cfp * sin(th) - cfperp * cos(th);
+    double cfx, cfy, fx, fy;
     double g = orc_gravity(P, y);
-    double fx = aero_x + cfx + Fwx, fy = aero_y + cfy + Fwy;
+    if (f32_forces) {
+        /* rockets_physics.py:608-616 with float32 control forces: cfx, cfy in binary32; the
+         * Python-float aero terms and F_wind_y join in binary32; with wind on F_wind_x is a numpy
+         * float64 (interp1d output) and promotes the last sum */
+        if (isnan(cfp_f)) cfp_f = 0.0f;
+        else if (isnan(cfperp_f)) cfperp_f = 0.0f;
+        float c = (float)cos(th), sn = (float)sin(th);
+        float cx = cfp_f * c + cfperp_f * sn;
+        float cy = cfp_f * sn - cfperp_f * c;
+        float sx = (float)aero_x + cx, sy = (float)aero_y + cy;
+        fx = E->wind_on ? (double)sx + Fwx : (double)(sx + (float)Fwx);
+        fy = (double)(sy + (float)Fwy);
+        cfx = cx; cfy = cy;
+    } else {
+        cfx = cfp * cos(th) + cfperp * sin(th);
+        cfy = cfp * sin(th) - cfperp * cos(th);
+        fx = aero_x + cfx + Fwx; fy = aero_y + cfy + Fwy;
+    }
     double vxd = fx / m, vyd = fy / m - g;
     vx += vxd * dt; vy += vyd * dt; x += vx * dt; y += vy * dt;
     double mz_tot = cm + aero_m + Mw;
@@ -423,6 +559,13 @@ int orc_physics(const orc_params* P, orc_env* E, int phase, const double* u, int
      * landing_burn physics dt = 0.1 x4 with actuator dt 0.025 (:803-861) */
     double dt = phase == ORC_PHASE_PURE_THROTTLE ? 0.025 : 0.1;
     E->noise_used = 0;
+    if (phase >= ORC_PHASE_PCONTROL) {
+        /* the other phases: one call of rocket_physics_fcn at the env dt (:728-802, :959-997);
+         * actuator filters at the same dt */
+        double d = E->dt > 0 ? E->dt : 0.1;
+        substep(P, E, phase, u, f32, d, d, noise, info);
+        return 0;
+    }
     for (int k = 0; k < 4; ++k)
         substep(P, E, phase, u, f32, dt, 0.025, noise ? (E->noise_slotted ? noise + 2 * k : noise) : NULL, info);
     if (phase == ORC_PHASE_LANDING_BURN && info) {
@@ -521,6 +664,193 @@ static void rtd_pso(const orc_params* P, const orc_env* E, int phase, double gl,
     o->reward = r; o->done = done; o->trunc = tr; o->trunc_id = id;
 }
 
+
+/* rtd_rl.py:190-240 (truncated/done shared by both landing-burn RL flavours) + :243-269 (the
+ * reward of landing_burn / landing_burn_ACS).  u0 = actions[0] as the env receives it. */
+static void rtd_rl_landing_burn(const orc_params* P, const orc_env* E, double gl, const double* u, int f32,
+                                orc_out* o) {
+    const double* s = E->s;
+    double y = s[1], vx = s[2], vy = s[3], th = s[4], ga = s[6], mp = s[9];
+    double rho, pa, a;
+    orc_atmosphere(P, y, &rho, &pa, &a);
+    double speed = sqrt(vx * vx + vy * vy);
+    double q = 0.5 * rho * (speed * speed);
+    int tr = 0, id = 0;
+    if (y < -10) { tr = 1; id = 1; }
+    else if (mp <= 0) { tr = 1; id = 2; }
+    else if (th > PI + radians(2)) { tr = 1; id = 3; }
+    else if (q > 65000) { tr = 1; id = 4; }
+    else if (gl > 6.0) { tr = 1; id = 5; }
+    else if (vy > 0.0) { tr = 1; id = 6; }
+    else if (vx > 0.01) { tr = 1; id = 7; }
+    int done = (y > 0 && y < 1 && speed < 5.0);
+    double y0 = P->state0[1];
+    double ae = fabs(ga - th - PI);
+    double lead = 1.5 - log(1 + ae) / log(1 + radians(20));
+    double X;
+    if (f32) {   /* tau = (u0 + 1)/2 in binary32; Python float - float32 -> float32 */
+        float tau = ((float)u[0] + 1.0f) / 2.0f;
+        X = (double)((float)lead - tau * 0.5f);
+    } else {
+        double tau = (u[0] + 1) / 2;
+        X = lead - tau * 0.5;
+    }
+    double r = 0.0;
+    r += X * (1 - y / y0) * 2 / 3;
+    if (y < 100) r += 1 - tanh((speed - 15) / 15);
+    if (tr && y < 5) r += 1 - tanh((speed - 5) / 5);
+    if (done) r += 5;
+    r *= (1 - P->rl_discount) / (1 - pow(P->rl_discount, (double)P->rl_traj_len));
+    o->reward = r; o->done = done; o->trunc = tr; o->trunc_id = id;
+}
+
+/* compile_rtd_rl_landing_burn_PDcontrol (rtd_rl.py:353-534); the reward is the SECOND
+ * reward_func_lambda (:479-531), which rebinds the first.  v_ref = actions[0]. */
+static void rtd_rl_pcontrol(const orc_params* P, const orc_env* E, double gl, const double* u, int f32,
+                            orc_out* o) {
+    const double* s = E->s;
+    double y = s[1], vx = s[2], vy = s[3], th = s[4], m = s[8], mp = s[9];
+    double rho, pa, a;
+    orc_atmosphere(P, y, &rho, &pa, &a);
+    double speed = sqrt(vx * vx + vy * vy);
+    double q = 0.5 * rho * (speed * speed);
+    int tr = 0, id = 0;
+    if (y < -10) { tr = 1; id = 1; }
+    else if (mp <= 0) { tr = 1; id = 2; }
+    else if (th > PI + radians(2)) { tr = 1; id = 3; }
+    else if (q > 65000) { tr = 1; id = 4; }
+    else if (gl > 6.0) { tr = 1; id = 5; }
+    else if (vy > 0.0) { tr = 1; id = 6; }
+    int done = (y > 0 && y < 5 && speed < 1);
+    double y0 = P->state0[1], m0 = P->state0[8];
+    double sp = hypot(vx, vy);
+    double qr = 0.5 * rho * (sp * sp);
+    double r = 0.0;
+    if (qr > 60000.0) { double e = (qr - 60000.0) / (65000.0 - 60000.0); r -= 1.0 * fmin(e * e, 1.0); }
+    if (gl > 5.5) { double e = (gl - 5.5) / (6.0 - 5.5); r -= 1.0 * fmin(e * e, 1.0); }
+    double prog = (y0 - y) / y0;
+    double vt;
+    if (f32) {   /* speed - v_ref: Python float - float32 -> float32 */
+        float d = fabsf((float)sp - (float)u[0]) / 10.0f;
+        float t = 1.0f - d;
+        vt = t > 0.0f ? (double)t : 0.0;
+    } else {
+        double t = 1.0 - fabs(sp - u[0]) / 10.0;
+        vt = t > 0.0 ? t : 0.0;
+    }
+    double wp = (qr <= 60000.0 && gl <= 5.5) ? 0.5 : 0.5 * 0.1;
+    r += wp * prog * vt;
+    if (y < 100.0) { double t = 1.0 - fabs(vy - 0.0) / 50.0; r += 0.5 * (t > 0.0 ? t : 0.0); }
+    r += 0.01 * (1 - P->rl_discount);
+    if (done && !tr) { r += 5.0; double used = y0 * 0.0 + (m0 - m); r -= fmin(0.1 * used, 1.0); }
+    else if (tr) { double imp = fabs(vy), af = y / y0; r -= fmin(4.0 * af * (imp / 100.0), 5.0); }
+    if (r < -10.0) r = -10.0;
+    if (r > 10.0) r = 10.0;
+    o->reward = r; o->done = done; o->trunc = tr; o->trunc_id = id;
+}
+
+/* compile_rtd_rl_ballistic_arc_descent (rtd_rl.py:153-188) */
+static void rtd_rl_ballistic(const orc_params* P, const orc_env* E, orc_out* o) {
+    const double* s = E->s;
+    double y = s[1], vx = s[2], vy = s[3], th = s[4], ga = s[6];
+    double rho, pa, a;
+    orc_atmosphere(P, y, &rho, &pa, &a);
+    double speed = sqrt(vx * vx + vy * vy);
+    double q = 0.5 * rho * (speed * speed);
+    double ae = fabs(ga - th - PI);
+    int done = (q > 10000 && ae < radians(3));
+    int tr = 0, id = 0;
+    if (q > 10000 - 2000 && ae > radians(5)) { tr = 1; id = 1; }
+    double r = (PI - ae) / PI;
+    if (done) r += 3.5;
+    r /= 100;
+    o->reward = r; o->done = done; o->trunc = tr; o->trunc_id = id;
+}
+
+/* compile_rtd_rl_ascent (rtd_rl.py:11-114) with the subsonic / supersonic hyper-parameter
+ * tables (:543-574) and the ascent reference trajectory (reference_trajectory_interpolation.py) */
+static void rtd_rl_ascent(const orc_params* P, const orc_env* E, int which, orc_out* o) {
+    const double* s = E->s;
+    double x = s[0], y = s[1], vx = s[2], vy = s[3], al = s[7], mp = s[9];
+    int nan = 0;
+    for (int k = 0; k < 11; ++k) nan |= isnan(s[k]);
+    if (nan) { o->reward = 0; o->done = 0; o->trunc = 1; o->trunc_id = 0; return; }
+    double rho, pa, a;
+    orc_atmosphere(P, y, &rho, &pa, &a);
+    double speed = sqrt(vx * vx + vy * vy);
+    double mach = (speed != 0 && a != 0) ? speed / a : 0;
+    double tm = P->terminal_mach[which];
+    double h[9][12];
+    for (int k = 0; k < 12; ++k) for (int f = 0; f < 9; ++f) h[f][k] = P->hyper[which][k][f];
+    double mx = interp1d_ext(h[0], h[1], 12, mach), mvy = interp1d_ext(h[0], h[2], 12, mach);
+    double mvx = interp1d_ext(h[0], h[3], 12, mach), mal = interp1d_ext(h[0], h[4], 12, mach);
+    double wal = interp1d_ext(h[0], h[5], 12, mach), wx = interp1d_ext(h[0], h[6], 12, mach);
+    double wvy = interp1d_ext(h[0], h[7], 12, mach), wvx = interp1d_ext(h[0], h[8], 12, mach);
+    int n = P->n_ref;
+    double xr = interp1d_ext(P->ref_y, P->ref_x, n, y), vxr = interp1d_ext(P->ref_y, P->ref_vx, n, y);
+    double vyr = interp1d_ext(P->ref_y, P->ref_vy, n, y);
+    int done = (mp >= 0 && mach > tm);
+    int tr = 0, id = 0;
+    if (mp <= 0) { tr = 1; id = 1; }
+    else if (mach > tm + 0.09) { tr = 1; id = 2; }
+    else if (fabs(x - xr) > mx) { tr = 1; id = 3; }
+    else if (y < 0) { tr = 1; id = 4; }
+    else if (fabs(al) > radians(mal)) { tr = 1; id = 5; }
+    else if (fabs(vx - vxr) > mvx) { tr = 1; id = 6; }
+    else if (fabs(vy - vyr) > mvy) { tr = 1; id = 7; }
+    double r = 0.0;
+    if (!(y < 0)) {
+        double d;
+        d = vx - vxr; r += exp(-4 * (d * d) / (mvx * mvx)) * wvx;
+        d = vy - vyr; r += exp(-4 * (d * d) / (mvy * mvy)) * wvy;
+        d = x - xr; r += exp(-4 * (d * d) / (mx * mx)) * wx;
+        d = degrees(al); r += exp(-4 * (d * d) / (mal * mal)) * wal;
+        if (done) r += 2.5;
+        r /= 10000;
+    }
+    o->reward = r; o->done = done; o->trunc = tr; o->trunc_id = id;
+}
+
+/* RL wrapper observation (env_wrapped_rl_pytorch.py:41-47 float32 cast, then augment_state
+ * :167-202) for every phase */
+static void obs_rl(const orc_params* P, int phase, const double* s, double* ob) {
+    float f[11];
+    for (int k = 0; k < 11; ++k) f[k] = (float)s[k];
+    const double* nm = P->norm_ph[phase];
+    switch (phase) {
+        case ORC_PHASE_PURE_THROTTLE:
+            ob[0] = (1 - (double)f[1] / P->norm_y) * 2 - 1;
+            ob[1] = (1 - (double)f[3] / P->norm_vy) * 2 - 1;
+            break;
+        case ORC_PHASE_PCONTROL:
+            ob[0] = (1 - (double)f[1] / P->norm_y) * 2 - 1;
+            break;
+        case ORC_PHASE_LANDING_BURN: {
+            /* y, vy / norms (binary64); theta, theta_dot, gamma through float32 islands */
+            double kt = atanh(0.75) / radians(5), ktd = atanh(0.75) / 0.01, kg = atanh(0.75) / radians(5);
+            ob[0] = (double)f[1] / P->norm_y;
+            ob[1] = (double)f[3] / P->norm_vy;
+            ob[2] = tanh((double)((float)kt * (f[4] - (float)(PI / 2))));
+            ob[3] = tanh((double)((float)ktd * f[5]));
+            ob[4] = tanh((double)((float)kg * (f[6] - (float)(3.0 / 2 * PI))));
+            break;
+        }
+        case ORC_PHASE_BALLISTIC: {   /* [theta, theta_dot, gamma, alpha] /= norms, in float32 */
+            const int idx[4] = {4, 5, 6, 7};
+            for (int k = 0; k < 4; ++k) ob[k] = (double)(float)((double)f[idx[k]] / nm[k]);
+            break;
+        }
+        case ORC_PHASE_FLIP:
+            ob[0] = (double)(float)((double)f[4] / nm[0]);
+            ob[1] = (double)(float)((double)f[5] / nm[1]);
+            break;
+        default: {   /* ascent: [x, y, vx, vy, theta, theta_dot, alpha, mass] */
+            const int idx[8] = {0, 1, 2, 3, 4, 5, 7, 8};
+            for (int k = 0; k < 8; ++k) ob[k] = (double)(float)((double)f[idx[k]] / nm[k]);
+        }
+    }
+}
+
 /* ---------------------------------------------------------------- env step
  * rocket_environment_pre_wrap.step (base_environment.py:99-154) */
 int orc_step(const orc_params* P, orc_env* E, int phase, int rtd, const double* u, int f32,
@@ -537,14 +867,19 @@ int orc_step(const orc_params* P, orc_env* E, int phase, int rtd, const double* 
     for (int i = 0; i < E->gwin_len; ++i) sum += E->gwin[i];
     double gl = sum / 10;
     o->info[ORC_I_GLOAD] = gl;
-    if (rtd == ORC_RTD_RL) rtd_rl_pure_throttle(P, E, gl, o);
-    else rtd_pso(P, E, phase, gl, o);
+    if (rtd == ORC_RTD_NONE) { o->reward = 0; o->done = 0; o->trunc = 0; o->trunc_id = 0; }
+    else if (rtd == ORC_RTD_PSO) rtd_pso(P, E, phase, gl, o);
+    else if (phase == ORC_PHASE_PURE_THROTTLE) rtd_rl_pure_throttle(P, E, gl, o);
+    else if (phase == ORC_PHASE_LANDING_BURN) rtd_rl_landing_burn(P, E, gl, u, f32, o);
+    else if (phase == ORC_PHASE_PCONTROL) rtd_rl_pcontrol(P, E, gl, u, f32, o);
+    else if (phase == ORC_PHASE_BALLISTIC) rtd_rl_ballistic(P, E, o);
+    else if (phase == ORC_PHASE_SUBSONIC || phase == ORC_PHASE_SUPERSONIC)
+        rtd_rl_ascent(P, E, phase == ORC_PHASE_SUPERSONIC, o);
     E->trunc_id = o->trunc_id;
     memcpy(E->prev_s, E->s, sizeof(E->s));
     /* observations: RL pure throttle (env_wrapped_rl_pytorch.py:195-198), PSO (env_wrapped_ea.py:108-122) */
-    if (rtd == ORC_RTD_RL) {   /* the SAC wrapper casts the state to float32 first */
-        o->obs[0] = (1 - (double)(float)s[1] / P->norm_y) * 2 - 1;
-        o->obs[1] = (1 - (double)(float)s[3] / P->norm_vy) * 2 - 1;
+    if (rtd != ORC_RTD_PSO) {   /* the RL wrapper casts the state to float32 first */
+        obs_rl(P, phase, s, o->obs);
     } else if (phase == ORC_PHASE_PURE_THROTTLE) {
         o->obs[0] = s[1] / P->norm_y; o->obs[1] = s[3] / P->norm_vy;
     } else {

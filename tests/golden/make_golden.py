@@ -84,16 +84,28 @@ def import_reference():
     import dill
 
     def _no_unpickle(_f, *a, **k):
-        from src.RocketSizing.functions.rocket_dimensions import stage_inertia, d_cg_thrusters
+        from src.RocketSizing.functions.rocket_dimensions import stage_inertia, d_cg_thrusters, full_rocket_inertia
         from src.RocketSizing.functions.cop_estimation import cop_func
         c = pack["inertia"]
         inert = stage_inertia(h_ox=c["h_ox"], h_f=c["h_f"], m_ox=c["m_ox"], m_f=c["m_f"],
                               h_lower=c["h_lower"], m_dry=c["m_dry"], x_dry=c["x_dry"], I_dry=c["I_dry"])
         L = pack["sizing"]["stage_1_height"]
+        fr = pack["phases"]["ascent_inertia"]
+        full = full_rocket_inertia(m_s_1=np.float64(fr["m_s_1"]), x_dry_1=np.float64(fr["x_dry_1"]),
+                                   I_dry_1=np.float64(fr["I_dry_1"]), m_2=np.float64(fr["m_2"]), m_pay=fr["m_pay"],
+                                   x_wet_2_initial=np.float64(fr["x_wet_2_initial"]),
+                                   I_wet_2_initial=np.float64(fr["I_wet_2_initial"]), h_1=np.float64(fr["h_1"]),
+                                   h_1_ox=np.float64(fr["h_1_ox"]), h_1_f=np.float64(fr["h_1_f"]),
+                                   m_1_ox=np.float64(fr["m_1_ox"]), m_1_f=np.float64(fr["m_1_f"]),
+                                   h_lower_1=np.float64(fr["h_lower_1"]))
+        L0 = pack["phases"]["cop_ascent"] / 0.25
         return {"x_cog_inertia_subrocket_2_lambda": inert,
                 "d_cg_thrusters_subrocket_2_lambda": lambda x: d_cg_thrusters(x, c["engine_height"]),
                 "cop_subrocket_2_lambda": lambda alpha, M: cop_func(L, alpha, M, d_0=0.75),
-                "cop_subrocket_0_lambda": None, "cop_subrocket_1_lambda": None}
+                "x_cog_inertia_subrocket_0_lambda": full,
+                "d_cg_thrusters_subrocket_0_lambda": lambda x: d_cg_thrusters(x, c["engine_height"]),
+                "cop_subrocket_0_lambda": lambda alpha, M: cop_func(L0, alpha, M, d_0=0.25),
+                "cop_subrocket_1_lambda": None}
 
     dill.load = _no_unpickle
     with contextlib.redirect_stdout(io.StringIO()):
@@ -312,6 +324,114 @@ def pso_objective(pso_wrapped_env_cls):
     save("ref_pso_objective.npz", **out)
 
 
+PHASE_CSV = {   # recorded classical-controller runs of each phase (column names differ per file)
+    "subsonic": "ascent_controls/subsonic_state_action_ascent_control.csv",
+    "supersonic": "ascent_controls/supersonic_state_action_ascent_control.csv",
+    "flip_over_boostbackburn": "flip_over_and_boostbackburn_controls/state_action_flip_over_and_boostbackburn_control.csv",
+    "ballistic_arc_descent": "ballistic_arc_descent_controls/state_action_ballistic_arc_descent_control.csv",
+    "landing_burn_pure_throttle_Pcontrol": "landing_burn_v_ref_control/state_action_landing_burn_pure_throttle_control.csv",
+}
+CSV_STATE = ["x[m]", "y[m]", "vx[m/s]", "vy[m/s]", "theta[rad]", "theta_dot[rad/s]", "gamma[rad]", "alpha[rad]",
+             "mass[kg]", "mass_propellant[kg]", "time[s]"]
+
+
+def phase_states(phase):
+    import pandas as pd
+    d = pd.read_csv(os.path.join(REF, "data/reference_trajectory", PHASE_CSV[phase]))
+    d = d.rename(columns={"masspropellant[kg]": "mass_propellant[kg]"})
+    return d[CSV_STATE].values, d
+
+
+def recorded_phases():
+    """The reference's recorded classical-controller runs of the flip-over and both ascent
+    phases (data/reference_trajectory/*), replayed open-loop by the oracle test."""
+    out = {}
+    for tag, phase, ucols in (("fl", "flip_over_boostbackburn", ["u0"]), ("sub", "subsonic", ["u0", "u1"]),
+                              ("sup", "supersonic", ["u0", "u1"])):
+        S, d = phase_states(phase)
+        out[f"{tag}_state"] = S
+        out[f"{tag}_u"] = d[ucols].values
+    save("recorded_phases.npz", **out)
+
+
+def phases(rp, rl_env_cls):
+    """The flight phases besides the two landing burns:
+    teacher-forced compile_physics steps with float32 and float64 actions from states of the
+    reference's recorded runs of each phase, RL-wrapper episodes, and the phase/type pairs the
+    reference itself cannot step (recorded as the exception they raise)."""
+    rng = np.random.default_rng(2024)
+    out = {}
+    for tag, phase, A in (("pc", "landing_burn_pure_throttle_Pcontrol", 1), ("ba", "ballistic_arc_descent", 1),
+                          ("fl", "flip_over_boostbackburn", 1), ("sub", "subsonic", 2), ("sup", "supersonic", 2)):
+        fn = rp.compile_physics(0.1, phase)
+        pool, _ = phase_states(phase)
+        S = pool[rng.choice(len(pool), 300, replace=len(pool) < 300)]
+        if phase == "landing_burn_pure_throttle_Pcontrol":
+            acts = rng.uniform(0, 1100, (len(S), A))
+        else:
+            acts = rng.uniform(-1, 1, (len(S), A))
+        f32 = np.arange(len(S)) % 2 == 0            # even rows: float32 actions, odd: float64
+        prev = rng.uniform(-10, 10, len(S))
+        res, inf = [], []
+        for i in range(len(S)):
+            st = [np.float64(v) for v in S[i]]
+            a = acts[i].astype(np.float32) if f32[i] else acts[i].astype(np.float64)
+            with contextlib.redirect_stdout(io.StringIO()):
+                if phase == "flip_over_boostbackburn":
+                    g = np.array([prev[i]], dtype=np.float32 if f32[i] else np.float64)
+                    s2, info = fn(st, a, g, wind_generator=None)
+                else:
+                    s2, info = fn(st, a, wind_generator=None)
+            res.append([float(v) for v in s2])
+            ai = info["action_info"]
+            inf.append([info["air_density"], info["mach_number"], info["CL"], info["CD"], float(info["mass_flow"]),
+                        info["dynamic_pressure"], info["x_cog"], info["inertia"],
+                        float(np.asarray(ai.get("gimbal_angle_deg", 0.0)).ravel()[0])])
+        out[f"{tag}_state_in"] = S
+        out[f"{tag}_action"] = acts
+        out[f"{tag}_f32"] = f32
+        out[f"{tag}_prev"] = prev
+        out[f"{tag}_state_out"] = np.array(res)
+        out[f"{tag}_info"] = np.array(inf)
+    out["info_names"] = np.array(["air_density", "mach_number", "CL", "CD", "mass_flow", "dynamic_pressure",
+                                  "x_cog", "inertia", "gimbal_angle_deg"])
+    # RL-wrapper episodes (float32 policy actions, env_wrapped_rl_pytorch.step)
+    specs = [("lb", "landing_burn", 4, [(31, 0.3), (32, 0.05)]),
+             ("pc", "landing_burn_pure_throttle_Pcontrol", 1, [(33, 1.0), (34, 0.2)]),
+             ("ba", "ballistic_arc_descent", 1, [(35, 1.0), (36, 0.1)]),
+             ("sub", "subsonic", 2, [(37, 1.0), (38, 0.05)]),
+             ("sup", "supersonic", 2, [(39, 1.0), (40, 0.05)])]
+    for tag, phase, A, seeds in specs:
+        with contextlib.redirect_stdout(io.StringIO()):
+            env = rl_env_cls(flight_phase=phase, enable_wind=False, stochastic_wind=False,
+                             trajectory_length=100, discount_factor=0.99)
+        for k, (seed, scale) in enumerate(seeds):
+            r = np.random.default_rng(seed)
+            acts = (r.uniform(-1, 1, (2500, A)) * scale).astype(np.float32)
+            if phase == "landing_burn_pure_throttle_Pcontrol":
+                acts = r.uniform(-1, 1, (2500, A)).astype(np.float32) * np.float32(scale)
+            if phase == "subsonic":      # the ascent needs throttle to leave the pad
+                acts[:, 1] = np.clip(acts[:, 1] + np.float32(0.9), -1, 1)
+            ep = run_episode(env, acts, 2500, lambda e, a: e.step(a))
+            for key, v in ep.items():
+                out[f"ep_{tag}{k}_{key}"] = v
+            out[f"ep_{tag}{k}_actions"] = acts[:len(ep["reward"])]
+    # pairs the reference cannot step: record the exception type
+    raised = []
+    for phase, typ in (("landing_burn_ACS", "rl"), ("flip_over_boostbackburn", "rl")):
+        try:
+            with contextlib.redirect_stdout(io.StringIO()):
+                env = rl_env_cls(flight_phase=phase, enable_wind=False, stochastic_wind=False,
+                                 trajectory_length=100, discount_factor=0.99)
+                env.reset()
+                env.step(np.zeros(env.action_dim, dtype=np.float32))
+            raised.append(f"{phase}/{typ}: none")
+        except Exception as e:   # noqa: BLE001 (recording what the reference does)
+            raised.append(f"{phase}/{typ}: {type(e).__name__}")
+    out["raises"] = np.array(raised)
+    save("ref_phases.npz", **out)
+
+
 def main():
     print("recorded fixtures", file=sys.stderr)
     recorded()
@@ -322,11 +442,16 @@ def main():
     print("episodes", file=sys.stderr); episodes(rl_env_cls, pso_wrapper_cls)
     print("wind episodes", file=sys.stderr); wind_episodes(rl_env_cls)
     print("PSO objective", file=sys.stderr); pso_objective(import_reference.pso_wrapped_env)
+    print("other phases", file=sys.stderr); recorded_phases(); phases(rp, rl_env_cls)
 
 
 if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "pso":     # only the PSO-objective fixture
         _, _, _, _, _ = import_reference()
         pso_objective(import_reference.pso_wrapped_env)
+    elif len(sys.argv) > 1 and sys.argv[1] == "phases":     # only the other-phases fixture
+        recorded_phases()
+        rp, _, _, rl_env_cls, _ = import_reference()
+        phases(rp, rl_env_cls)
     else:
         main()

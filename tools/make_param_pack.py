@@ -306,6 +306,131 @@ def von_karman(dt=0.1, V=100.0):
     return out
 
 
+def read_full_rocket_constants():
+    """Static scan of the dill pickle for the 13 float64 cells of
+    `x_cog_inertia_subrocket_0_lambda` = full_rocket_inertia(...).func
+    (rocket_dimensions.py:198-241, unpacked at main_sizing.py:209-212).  dill writes the
+    cells in reverse alphabetical order of the closure's free variables; m_pay is a
+    pickled Python float (BINFLOAT), the others numpy float64 scalars."""
+    data = open(ref_path("data/rocket_parameters/rocket_functions.pkl"), "rb").read()
+    ops = list(pickletools.genops(data))
+    start = end = None
+    for i, (op, arg, pos) in enumerate(ops):
+        if op.name.endswith("UNICODE") and arg == "x_cog_inertia_subrocket_0_lambda":
+            start = i
+        if start is not None and op.name.endswith("UNICODE") and arg == "x_cog_inertia_subrocket_1_lambda":
+            end = i
+            break
+    vals = []
+    first_cell = next(i for i in range(start, end) if ops[i][0].name.endswith("UNICODE") and ops[i][1] == "cell_contents")
+    for op, arg, pos in ops[first_cell:end]:   # the code object's own constants come before
+        if op.name in ("SHORT_BINBYTES", "BINBYTES") and len(arg) == 8:
+            vals.append(struct.unpack("<d", arg)[0])
+        elif op.name == "BINFLOAT":
+            vals.append(float(arg))
+    names = ["x_wet_2_initial", "x_dry_1", "m_s_1", "m_pay", "m_2", "m_1_ox", "m_1_f", "h_lower_1",
+             "h_1_ox", "h_1_f", "h_1", "I_wet_2_initial", "I_dry_1"]
+    assert len(vals) == len(names), vals
+    return dict(zip(names, vals))
+
+
+STATE_NAMES = ["x[m]", "y[m]", "vx[m/s]", "vy[m/s]", "theta[rad]", "theta_dot[rad/s]",
+               "gamma[rad]", "alpha[rad]", "mass[kg]", "mass_propellant[kg]", "time[s]"]
+
+
+def phases_section(sz):
+    """Constants of the flight phases other than the two landing-burn ones
+    (rockets_physics.py:17-166,402-451,728-802,959-997; rtd_rl.py:11-188,353-534;
+    load_initial_states.py:5-53; input_normalisation.py:5-71;
+    reference_trajectory_interpolation.py:5-37)."""
+    import pandas as pd
+    tr = "data/reference_trajectory/"
+    sub = pd.read_csv(ref_path(tr + "ascent_controls/subsonic_state_action_ascent_control.csv"))
+    sup = pd.read_csv(ref_path(tr + "ascent_controls/supersonic_state_action_ascent_control.csv"))
+    flip = pd.read_csv(ref_path(tr + "flip_over_and_boostbackburn_controls/state_action_flip_over_and_boostbackburn_control.csv"))
+    ball = pd.read_csv(ref_path(tr + "ballistic_arc_descent_controls/state_action_ballistic_arc_descent_control.csv"))
+    # load_initial_states.py:13-31 (np.array -> float64), :5-11, :33-45, :47-53
+    state0 = {
+        "subsonic": [0.0, 1.5, 0.0, 0.0, np.pi / 2, 0.0, 0.0, 0.0,
+                     float(sz["Initial mass (subrocket 0)"]) * 1000,
+                     float(sz["Actual propellant mass stage 1"]) * 1000, 0.0],
+        "supersonic": [float(sub.iloc[-1][n]) for n in STATE_NAMES],
+        "flip_over_boostbackburn": [float(sup.iloc[-1][n]) for n in STATE_NAMES],
+        "ballistic_arc_descent": [float(flip.iloc[-1][n]) for n in STATE_NAMES],
+    }
+    state0["flip_over_boostbackburn"][8] = (float(sup.iloc[-1]["mass_propellant[kg]"])
+                                            + float(sz["Actual structural mass stage 1"]) * 1000)
+
+    def mx(df, cols):
+        return np.max(np.abs(df[cols].values), axis=0)
+
+    cols8 = ["x[m]", "y[m]", "vx[m/s]", "vy[m/s]", "theta[rad]", "theta_dot[rad/s]", "alpha[rad]", "mass[kg]"]
+    m = mx(sub, cols8)
+    r = math.radians
+    norm = {
+        "subsonic": [m[0] + 100, m[1] + 500, m[2] + 5, m[3] + 50, m[4] + r(2), m[5] * 2.5, m[6] + r(3), m[7]],
+    }
+    m = mx(sup, cols8)
+    norm["supersonic"] = [m[0] + 2500, m[1] + 5000, m[2] + 100, m[3] + 150, m[4] + r(5), m[5] * 2.5, m[6] + r(3), m[7]]
+    m = mx(flip, ["theta[rad]", "theta_dot[rad/s]"])
+    norm["flip_over_boostbackburn"] = [m[0] + r(5), m[1] * 2.5]
+    m = mx(ball, ["theta[rad]", "theta_dot[rad/s]", "alpha[rad]", "gamma[rad]"])
+    norm["ballistic_arc_descent"] = [m[0] + r(5), m[1] * 2.5, m[3] + r(5), m[2] + r(5)]
+    norm = {k: [float(v) for v in vs] for k, vs in norm.items()}
+    # reference trajectory of the ascent rtd: interp1d(y, .) with extrapolation; scipy sorts
+    # x with a stable argsort before building the interpolant
+    ref = pd.read_csv(ref_path(tr + "ascent_controls/reference_trajectory_ascent_control.csv"))
+    yv = ref["y[m]"].values
+    order = np.argsort(yv, kind="mergesort")
+    ascent_ref = {"y": yv[order].tolist()}
+    for k, c in (("x", "x[m]"), ("vx", "vx[m/s]"), ("vy", "vy[m/s]"), ("m", "mass[kg]")):
+        ascent_ref[k] = ref[c].values[order].tolist()
+    # terminal Mach of the supersonic rtd (rtd_rl.py:580-589): the last reference row at the
+    # restated ISA speed of sound (math.sqrt / Python float arithmetic)
+    xt, yt, vxt, vyt = (float(ref[c].values[-1]) for c in ("x[m]", "y[m]", "vx[m/s]", "vy[m/s]"))
+    _, _, a_t = isa(yt)
+    mach_t = math.sqrt(vxt ** 2 + vyt ** 2) / a_t
+    h1, h2 = float(sz["Stage 1 height "]), float(sz["Stage 2 height "])
+    lb = [float(v) for v in ball.iloc[-1][STATE_NAMES]]
+    return {
+        "ascent_inertia": read_full_rocket_constants(),
+        "cop_ascent": 0.25 * (h1 + h2),     # cop_func(lengths[0] = h_1 + h_2, d_0 = 0.25)
+        "n_engines_stage1": int(sz["Number of engines stage 1"]),
+        "rcs": {"max_force": float(sz["max_RCS_force_per_thruster"]),
+                "d_bottom": float(sz["d_base_rcs_bottom"]), "d_top": float(sz["d_base_rcs_top"])},
+        "state0": state0,
+        "norm": norm,
+        "ascent_ref": ascent_ref,
+        "terminal_mach": {"subsonic": 1.0, "supersonic": mach_t},
+        # rl_wrapped_env_pytorch (env_wrapped_rl_pytorch.py:107-110): speed of the landing
+        # initial state, the v_ref scale of the Pcontrol phase
+        "speed0_pcontrol": math.sqrt(lb[2] ** 2 + lb[3] ** 2),
+        # rtd_rl.py:543-574 [mach, max_x, max_vy, max_vx, max_alpha_deg, w_alpha, w_x, w_vy, w_vx]
+        "ascent_hyper": {
+            "subsonic": [[0.0, 50, 10, 10, 0.5, 100, 100, 100, 100], [0.1, 50, 15, 10, 10, 100, 100, 100, 100]]
+                        + [[m_, 50, 20, 5, 2, 100, 100, 100, 100] for m_ in (0.2, 0.3, 0.4, 0.5)]
+                        + [[m_, 50, 20, 5, 1.75, 100, 100, 100, 100] for m_ in (0.6, 0.7, 0.8, 0.9, 1.0, 1.1)],
+            "supersonic": [[1.0, 100, 50, 9, 8, 100, 100, 100, 100]]
+                          + [[m_, 100, 60, vx_, 8, 100, 100, 100, 100] for m_, vx_ in
+                             ((1.1, 20), (1.5, 20), (1.75, 30), (2.0, 40), (2.25, 50), (2.5, 60), (2.75, 70),
+                              (3.0, 80), (3.25, 90), (3.5, 100), (3.75, 100))],
+        },
+    }
+
+
+def isa(h):
+    """The pack's ISA layer model (same constants as the "isa" section)."""
+    g0, R, kappa, re = 9.80665, 287.05287, 1.4, 6356766.0
+    L = [(-5.0e3, 320.65, -6.5e-3, 1.77687e5), (0.0, 288.15, -6.5e-3, 1.01325e5), (11.0e3, 216.65, 0.0, 2.26320e4),
+         (20.0e3, 216.65, 1.0e-3, 5.47487e3), (32.0e3, 228.65, 2.8e-3, 8.68014e2), (47.0e3, 270.65, 0.0, 1.10906e2),
+         (51.0e3, 270.65, -2.8e-3, 6.69384e1), (71.0e3, 214.65, -2.0e-3, 3.95639e0), (80.0e3, 196.65, -2.0e-3, 8.86272e-1)]
+    H = re * h / (re + h)
+    Hb, Tb, b, pb = [l for l in L if l[0] <= H][-1]
+    T = Tb + b * (H - Hb)
+    p = pb * (1 + b / Tb * (H - Hb)) ** (-g0 / (b * R)) if b != 0 else pb * math.exp(-g0 / (R * T) * (H - Hb))
+    return p / (R * T), p, math.sqrt(kappa * R * T)
+
+
 def main():
     import pandas as pd
     sz = read_sizing()
@@ -378,6 +503,7 @@ def main():
                            y_threshold=15000.0, sigma_u=[0.5, 2.25], sigma_v=[1.25, 2.0]),
         "state0": state0,
         "norm": norm,
+        "phases": phases_section(sz),
     }
     os.makedirs(os.path.dirname(OUT), exist_ok=True)
     with open(OUT, "w") as f:
@@ -385,5 +511,18 @@ def main():
     print("wrote", os.path.normpath(OUT), file=sys.stderr)
 
 
+def phases_only():
+    """Refresh only the "phases" section of an existing pack (no key re-enumeration)."""
+    with open(OUT) as f:
+        pack = json.load(f)
+    pack["phases"] = phases_section(read_sizing())
+    with open(OUT, "w") as f:
+        json.dump(pack, f, indent=1)
+    print("updated phases in", os.path.normpath(OUT), file=sys.stderr)
+
+
 if __name__ == "__main__":
-    main()
+    if "--phases-only" in sys.argv:
+        phases_only()
+    else:
+        main()
