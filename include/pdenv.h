@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define PD_ABI_VERSION 1
+#define PD_ABI_VERSION 2
 #define PD_MAX_PTS 256      /* aero scatter points per table */
 #define PD_MAX_COLS 5       /* AoA columns per aero table */
 #define PD_MAX_TAB 64       /* grid-fin table length */
@@ -46,8 +46,23 @@ extern "C" {
 #define PD_ACTOR_PARAMS_LANDING_BURN 372
 
 typedef enum { PD_OK = 0, PD_ERR_INVALID = 1, PD_ERR_HIP = 2, PD_ERR_NOMEM = 3, PD_ERR_UNSUPPORTED = 4 } pd_status;
-typedef enum { PD_PHASE_PURE_THROTTLE = 0, PD_PHASE_LANDING_BURN = 1 } pd_phase;   /* 1 resp. 4 actions */
-typedef enum { PD_RTD_RL = 0, PD_RTD_PSO = 1 } pd_rtd;                             /* rtd_rl.py / rtd_pso.py */
+/* compile_physics flight phases (rockets_physics.py:707-998; base_environment.py:21).  Actions:
+ * 1 (pure throttle: throttle; Pcontrol: v_ref; ballistic: RCS; flip-over: gimbal), 4 (landing_burn),
+ * 2 (subsonic/supersonic: gimbal, throttle).  PD_PHASE_LANDING_BURN_ACS is accepted by the
+ * enum but pd_create refuses it: the reference raises TypeError at its first step
+ * (rockets_physics.py:867-891 calls the gimballed decomposer with ACS arguments;
+ * base_environment.py:126-130 passes two prevs to a three-prev lambda). */
+typedef enum {
+    PD_PHASE_PURE_THROTTLE = 0, PD_PHASE_LANDING_BURN = 1, PD_PHASE_PCONTROL = 2,
+    PD_PHASE_BALLISTIC_ARC = 3, PD_PHASE_FLIP_OVER = 4, PD_PHASE_SUBSONIC = 5, PD_PHASE_SUPERSONIC = 6,
+    PD_PHASE_LANDING_BURN_ACS = 7
+} pd_phase;
+/* reward/truncated/done family: rtd_rl.py, rtd_pso.py, or none (compile_physics stepping only:
+ * reward 0, never done/truncated).  Pairs the reference cannot step are refused by pd_create
+ * with PD_ERR_UNSUPPORTED: RL + flip-over (rtd_rl.py:134 truncated_func takes one argument,
+ * base_environment.py:150 passes three), PSO + any phase but the two landing burns (the same
+ * arity mismatch in rtd_pso.py:38,107,141). */
+typedef enum { PD_RTD_RL = 0, PD_RTD_PSO = 1, PD_RTD_NONE = 2 } pd_rtd;
 typedef enum { PD_F64 = 0, PD_F32 = 1 } pd_precision;
 
 /* One neighbourhood-aero table: scatter points grouped by AoA column, Mach-sorted inside. */
@@ -87,6 +102,21 @@ typedef struct {
     /* pre-enumerated neighbourhood keys of the two aero tables (host arrays, may be NULL) */
     const uint64_t* keys_cd; int64_t n_keys_cd;
     const uint64_t* keys_cl; int64_t n_keys_cl;
+    /* ---- ABI 2: the other flight phases (rockets_physics.py:17-166,402-451,728-802,959-997) */
+    /* full_rocket_inertia cells of x_cog_inertia_subrocket_0_lambda (rocket_dimensions.py:198-241):
+     * x_wet_2_initial, x_dry_1, m_s_1, m_pay, m_2, m_1_ox, m_1_f, h_lower_1, h_1_ox, h_1_f, h_1,
+     * I_wet_2_initial, I_dry_1 */
+    double full_rocket[13];
+    double cop_ascent;                  /* cop_func(h_1 + h_2, d_0 = 0.25) (main_sizing.py:215) */
+    int32_t n_engines_stage1, pad1;     /* 42: 16 gimballed + 26 fixed in the ascent */
+    double rcs_force, rcs_d_bottom, rcs_d_top;   /* RCS (rockets_physics.py:149-166, 784-786) */
+    double state0_phase[8][PD_N_STATE]; /* initial state per pd_phase (load_initial_states.py) */
+    double norm_phase[8][8];            /* RL observation normalisers (input_normalisation.py) */
+    /* ascent reference trajectory sorted by y (reference_trajectory_interpolation.py:5-37) */
+    const double* ref_y; const double* ref_x; const double* ref_vx; const double* ref_vy;
+    int32_t n_ref, pad2;
+    double hyper[2][12][9];             /* rtd_rl.py:543-574, subsonic / supersonic */
+    double terminal_mach[2];            /* rtd_rl.py:576-589 */
 } pd_params;
 
 typedef struct {
@@ -104,6 +134,11 @@ typedef struct {
     int32_t action_f64;        /* actions are double (f64 path, no float32 islands) */
     int32_t lanes_per_env;     /* step-kernel lanes per env: 1, 2, 4 or 8 (0 = by n_envs: 8 up to
                                   8 192 envs, 4 up to 32 768, else 2) */
+    /* ---- ABI 2 */
+    double dt;                 /* physics dt of phases 2..6, compile_physics(dt, phase) (0 = the env's 0.1) */
+    double discount_factor;    /* rtd_rl landing_burn reward scale (1-g)/(1-g^L) and the Pcontrol
+                                  alive bonus 0.01 (1-g) (rtd_rl.py:267, 472); rl_wrapped_env_pytorch kwargs */
+    int32_t trajectory_length, pad3;
 } pd_config;
 
 typedef enum {
@@ -176,6 +211,11 @@ pd_status pd_set_state(pd_env* env, const void* state, void* stream);
 /* Landing-burn actuator memory [3][N] (gimbal deg, left/right fin command rad). */
 pd_status pd_get_actuators(pd_env* env, void* act, void* stream);
 pd_status pd_set_actuators(pd_env* env, const void* act, void* stream);
+/* g-load history of every env (base_environment.py:137-149: |v| of previous_state and the
+ * g_loads_window list, oldest first): vprev [N], window [10][N] (handle precision), len [N]
+ * (0..10 valid entries).  Teacher forcing and checkpoint/restore. */
+pd_status pd_set_gload_window(pd_env* env, const void* vprev, const void* window, const uint8_t* len,
+                              void* stream);
 /* Per-env wind state: sigma_u, sigma_v [2][N] (double). */
 pd_status pd_set_wind_sigmas(pd_env* env, const double* sig, void* stream);
 /* Counters since create: aero-table misses solved on device, NaN guard hits. Host sync. */

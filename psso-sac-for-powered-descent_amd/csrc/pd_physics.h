@@ -79,6 +79,20 @@ template <typename R> struct DevParams {
     R line_bp[4][kLineMax];
     int line_slot[4][kLineMax + 1];
     unsigned long long line_key[4][kLineMax + 1];
+    // ---- the other flight phases (rockets_physics.py:17-166,402-451,728-802,959-997)
+    int phase, obs_kind;           // pd_phase of the handle; observation layout (obs_write)
+    R fr[13];                      // full_rocket_inertia cells (ascent), see inertia_full
+    R cop_ascent, mg_ascent, kp_pc, rcs_force, rcs_d_bottom, rcs_d_top;
+    int n_eng_stage1, n_ref;
+    float f_mg_ascent, f_kp_pc, f_rcs_force, f_k_theta_rl, f_k_thetad_rl, f_k_gamma_rl, f_pi_2, f_pi_3_2;
+    R norm_ph[8];                  // RL observation normalisers of the phase
+    const R* ref_y;                // ascent reference trajectory, sorted by y (n_ref rows)
+    const R* ref_x;
+    const R* ref_vx;
+    const R* ref_vy;
+    R hyper[12][9];                // ascent rtd hyper-parameters by Mach (rtd_rl.py:543-574)
+    R terminal_mach;
+    R rl_scale, alive_bonus, log_1p_max_ae;   // (1-g)/(1-g^L), 0.01 (1-g), log(1 + radians(20))
 };
 
 // ---------------------------------------------------------------- logarithms
@@ -140,6 +154,86 @@ __device__ __forceinline__ void inertia(const DevParams<R>& P, R fill, R& x_cog,
     R t3 = P.x_dry - x_wet, t4 = x_prop - x_wet;
     x_cog = x_wet;
     I = (P.I_dry + P.m_dry * (t3 * t3)) + ((I_ox + I_f) + mp_t * (t4 * t4));
+}
+
+// full_rocket_inertia closure (rocket_dimensions.py:198-241), x_cog_inertia_subrocket_0_lambda of
+// the ascent phases, with its own expression order (x_prop_1 uses the untilded m_1_f and
+// h_ox_1_tilde as written)
+template <typename R>
+__device__ __forceinline__ void inertia_full(const DevParams<R>& P, R fill, R& x_cog, R& I) {
+    const R* c = P.fr;
+    const R x_wet2 = c[0], x_dry1 = c[1], m_s1 = c[2], m_pay = c[3], m_2 = c[4], m1_ox = c[5], m1_f = c[6];
+    const R h_lower1 = c[7], h1_ox = c[8], h1_f = c[9], h1 = c[10], I_wet2 = c[11], I_dry1 = c[12];
+    R h_ox_t = h1_ox * fill, h_f_t = h1_f * fill, m_ox_t = m1_ox * fill, m_f_t = m1_f * fill;
+    R m_prop_t = m_ox_t + m_f_t;
+    R x_prop = (m_ox_t * (h_lower1 + h_ox_t / R(2)) + m1_f * (h_lower1 + h_ox_t + h_f_t / R(2))) / (m_ox_t + m_f_t);
+    R t1 = h_lower1 + h_ox_t / R(2) - x_prop;
+    R I_ox = R(1.0 / 12) * m_ox_t * (h_ox_t * h_ox_t) + m_ox_t * (t1 * t1);
+    R t2 = h_lower1 + h_ox_t + h_f_t / R(2) - x_prop;
+    R I_f = R(1.0 / 12) * m_f_t * (h_f_t * h_f_t) + m_f_t * (t2 * t2);
+    R xr = (m_s1 * x_dry1 + (m_2 + m_pay) * (x_wet2 + h1) + m_prop_t * x_prop) / (m_s1 + m_2 + m_pay + m_prop_t);
+    R d1 = x_dry1 - xr, d2 = x_wet2 - xr, d3 = x_prop - xr;
+    x_cog = xr;
+    I = I_dry1 + m_s1 * (d1 * d1) + I_wet2 + m_2 * (d2 * d2) + (I_ox + I_f) + m_prop_t * (d3 * d3);
+}
+
+// scipy interp1d(kind='linear', fill_value='extrapolate') on a sorted table in global memory:
+// _call_linear (searchsorted side='left', index clipped to [1, n-1])
+template <typename R>
+__device__ __forceinline__ R interp1d_ext(const R* x, const R* y, int n, R v) {
+    int lo = 0, hi = n;
+    while (lo < hi) { int mid = (lo + hi) >> 1; if (x[mid] < v) lo = mid + 1; else hi = mid; }
+    int i = lo < 1 ? 1 : (lo > n - 1 ? n - 1 : lo);
+    R slope = (y[i] - y[i - 1]) / (x[i] - x[i - 1]);
+    return slope * (v - x[i - 1]) + y[i - 1];
+}
+
+// The same on one column of the ascent hyper-parameter table (Mach in column 0, 12 rows).
+template <typename R>
+__device__ __forceinline__ R hyper_interp(const DevParams<R>& P, int col, R mach) {
+    int lo = 0, hi = 12;
+    while (lo < hi) { int mid = (lo + hi) >> 1; if (P.hyper[mid][0] < mach) lo = mid + 1; else hi = mid; }
+    int i = lo < 1 ? 1 : (lo > 11 ? 11 : lo);
+    R slope = (P.hyper[i][col] - P.hyper[i - 1][col]) / (P.hyper[i][0] - P.hyper[i - 1][0]);
+    return slope * (mach - P.hyper[i - 1][0]) + P.hyper[i - 1][col];
+}
+
+// Observation of state s, written to out[0..dim) (dim = obs_dim(kind)):
+//  0 RL pure throttle  (env_wrapped_rl_pytorch.py:195-198)   1 PSO pure throttle (env_wrapped_ea.py:108-111)
+//  2 PSO landing_burn  (env_wrapped_ea.py:112-122)           3 RL landing_burn / ACS (env_wrapped_rl_pytorch.py:178-194)
+//  4 RL Pcontrol (:199-201)  5 RL ballistic arc (:175-177)  6 RL flip-over (:172-174)  7 RL ascent (:169-171)
+// The RL wrapper casts the state to float32 before augment_state (:41-47); the divisions by the
+// float64 normalisers of kinds 5-7 happen in place on a float32 array (so round back to float32).
+__host__ __device__ constexpr int obs_dim(int kind) {
+    return kind == 2 || kind == 3 ? 5 : (kind == 4 ? 1 : (kind == 5 ? 4 : (kind == 7 ? 8 : 2)));
+}
+template <typename R>
+__device__ __forceinline__ void obs_write(const DevParams<R>& P, int kind, const R* s, R* out, uint32_t idx) {
+    const int d = obs_dim(kind);
+    R* o = out;
+    auto put = [&](int k, R v) { *(R*)((char*)(o + k) + (uint32_t)(idx * (uint32_t)(d * sizeof(R)))) = v; };
+    if (kind == 0) {
+        put(0, (R(1) - (R)(float)s[1] / P.norm_y) * R(2) - R(1));
+        put(1, (R(1) - (R)(float)s[3] / P.norm_vy) * R(2) - R(1));
+    } else if (kind == 1) {
+        put(0, s[1] / P.norm_y); put(1, s[3] / P.norm_vy);
+    } else if (kind == 2) {
+        put(0, s[0] / P.norm_x); put(1, s[1] / P.norm_y); put(2, s[2] / P.norm_vx); put(3, s[3] / P.norm_vy);
+        put(4, tanh(P.k_theta_pso * (s[4] - Cst<R>::pi / R(2))));
+    } else if (kind == 3) {
+        put(0, (R)(float)s[1] / P.norm_y); put(1, (R)(float)s[3] / P.norm_vy);
+        put(2, tanh((R)(P.f_k_theta_rl * ((float)s[4] - P.f_pi_2))));
+        put(3, tanh((R)(P.f_k_thetad_rl * (float)s[5])));
+        put(4, tanh((R)(P.f_k_gamma_rl * ((float)s[6] - P.f_pi_3_2))));
+    } else if (kind == 4) {
+        put(0, (R(1) - (R)(float)s[1] / P.norm_y) * R(2) - R(1));
+    } else {
+        const int n = kind == 5 ? 4 : (kind == 6 ? 2 : 8);
+        for (int k = 0; k < n; ++k) {
+            int j = kind == 5 ? 4 + k : (kind == 6 ? 4 + k : (k < 6 ? k : k + 1));   // ascent skips gamma
+            put(k, (R)(float)((R)(float)s[j] / P.norm_ph[k]));
+        }
+    }
 }
 
 // ---------------------------------------------------------------- tables in LDS

@@ -83,6 +83,8 @@ template <typename R> struct StepArgs {
     R* reward_sum;
     const float* policy_w;           // policy rollouts: actor parameters [P][N] float32
     unsigned long long* n_done;      // policy rollouts: envs whose episode has ended
+    double dt_aux;                   // physics dt of phases 2..6 (compile_physics(dt, phase))
+    int rtd_none;                    // PD_RTD_NONE: physics stepping only (reward/done/trunc 0)
 };
 
 // Per-env element `i` of a wave-uniform base pointer, addressed as base + zero-extended 32-bit
@@ -652,6 +654,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PD_WPE))
     else { cB.key = 0; cB.slot = -1; }
     R gprev = R(0), dlprev = R(0), drprev = R(0);
     if constexpr (PHASE == 1) { gprev = ev(a.b.act, ui); dlprev = ev(a.b.act + N, ui); drprev = ev(a.b.act + (2) * N, ui); }
+    // PHASE 2 = the other compile_physics phases, chosen at run time by P.phase (wave-uniform)
+    const int aux = PHASE == 2 ? a.P->phase : PHASE;
+    const bool ascent = PHASE == 2 && (aux == PD_PHASE_SUBSONIC || aux == PD_PHASE_SUPERSONIC);
+    if constexpr (PHASE == 2) gprev = ev(a.b.act, ui);   // flip-over gimbal memory
     R fu0 = R(0), fu1 = R(0), fv0 = R(0), fv1 = R(0), sgu = R(0), sgv = R(0);
     int prof = 0;
     if constexpr (WIND) {
@@ -663,7 +669,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PD_WPE))
     const uint64_t g = a.env_offset + (uint64_t)i;
 
     // actions (float32 unless act_f64)
-    constexpr int A = PHASE == 0 ? 1 : 4;
+    constexpr int A = PHASE == 0 ? 1 : (PHASE == 1 ? 4 : 2);
+    const int AD = PHASE == 2 ? (ascent ? 2 : 1) : A;   // row stride of the action array
     float uf[A];
     double ud[A];
 #pragma unroll
@@ -682,19 +689,22 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PD_WPE))
         }
     } else if (a.act_f64) {
 #pragma unroll
-        for (int k = 0; k < A; ++k) ud[k] = ev((const double*)a.actions + k, ui * A);
+        for (int k = 0; k < A; ++k) if (k < AD) ud[k] = ev((const double*)a.actions + k, ui * AD);
     } else {
 #pragma unroll
-        for (int k = 0; k < A; ++k) uf[k] = ev((const float*)a.actions + k, ui * A);
+        for (int k = 0; k < A; ++k) if (k < AD) uf[k] = ev((const float*)a.actions + k, ui * AD);
     }
 
-    const R dt = PHASE == 0 ? R(0.025) : R(0.1);
-    const R dt_act = R(0.025);
+    // pure throttle 4 x 0.025 s, landing_burn 4 x 0.1 s (actuators 0.025 s); the other phases
+    // one call of rocket_physics_fcn at dt, actuators at the same dt (rockets_physics.py:728-997)
+    constexpr int NSUB = PHASE == 2 ? 1 : 4;
+    const R dt = PHASE == 0 ? R(0.025) : (PHASE == 1 ? R(0.1) : (R)a.dt_aux);
+    const R dt_act = PHASE == 2 ? dt : R(0.025);
     R gdeg_out = gprev, dcmdl_out = dlprev, dcmdr_out = drprev;
     bool nan_hit = false;
 
 #pragma unroll 1
-    for (int sub = 0; sub < 4; ++sub) {
+    for (int sub = 0; sub < NSUB; ++sub) {
         const DevParams<R>& P = *launder(a.P);
         R x = s[0], y = s[1], vx = s[2], vy = s[3], th = s[4], thd = s[5], ga = s[6], al = s[7];
         R m = s[8], mp = s[9];
@@ -708,10 +718,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PD_WPE))
         R fpc = (P.m_prop0 - mp) / P.m_prop0;
         if (fpc == R(0)) fpc = R(1e-6);
         R x_cog, I;
-        inertia<R>(P, R(1) - fpc, x_cog, I);
+        // subrocket_0 (full rocket) closures for the ascent, subrocket_2 after (:748-750, :772-774)
+        if (ascent) inertia_full<R>(P, R(1) - fpc, x_cog, I);
+        else inertia<R>(P, R(1) - fpc, x_cog, I);
         R d_thrust = x_cog + P.engine_height;
         R ae = (vy < R(0)) ? ga - th - Cst<R>::pi : al;
-        R d_cp_cg = x_cog - P.cop;
+        R d_cp_cg = x_cog - (ascent ? P.cop_ascent : P.cop);
         R ug = R(0), vg = R(0);
         if constexpr (WIND) {
             // WindModel.__call__ (full_wind_model.py:35-43)
@@ -782,12 +794,85 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PD_WPE))
         R aero_x = apar * cth + aperp * sth;
         R aero_y = apar * sth - aperp * cth;
         R aero_m = aperp * d_cp_cg;
+        if (PHASE == 2 && aux == PD_PHASE_FLIP_OVER) { aero_x = R(0); aero_y = R(0); aero_m = R(0); }   // :548-551
 
         R T_full = P.T_e + (P.p_e - patm) * P.A_e;
         R qS = q * P.S_gf;
         R Ca = grid_fin_ca<R>(P, lds + L::kCaX, lds + L::kCaY, mach);
         R cfp, cfperp, cm, mdot_dt, md_info, thr_info;
-        if constexpr (PHASE == 0) {
+        // binary32 control forces (ascent, float32 actions): the force sums then stay binary32,
+        // the aero terms being Python floats (weak under NEP 50, rockets_physics.py:608-616)
+        bool f32_forces = false;
+        float cfp_f = 0.f, cfperp_f = 0.f;
+        if constexpr (PHASE == 2) {
+            if (aux == PD_PHASE_PCONTROL) {
+                // force_moment_decomposer_landing_burn_throttle_PID (:402-451): throttle from
+                // v_ref - speed (Kp -0.08, clip [0, 1]) into throttle_only as a list (binary64)
+                R u0;
+                if (a.act_f64) {
+                    R nt = ((R)ud[0] - speed) * P.kp_pc;
+                    nt = nt < R(0) ? R(0) : (nt > R(1) ? R(1) : nt);
+                    u0 = R(2) * (nt - R(0.5));
+                } else {
+                    float nt = (uf[0] - (float)speed) * P.f_kp_pc;
+                    nt = nt < 0.f ? 0.f : (nt > 1.f ? 1.f : nt);
+                    u0 = (R)(2.0f * (nt - 0.5f));
+                }
+                R thr = (u0 + R(1)) / R(2) * P.one_minus_nom_pt + P.nom_pt;
+                R tg = T_full * (R)P.n_eng * thr;
+                R md = P.Te_over_vex * (tg / T_full);
+                cfp = tg + qS * (Ca * R(4)); cfperp = R(0); cm = R(0);   // ACS, zero deflection
+                mdot_dt = md * dt; md_info = md; thr_info = thr;
+            } else if (aux == PD_PHASE_BALLISTIC_ARC) {
+                // RCS (:149-166): moment only, promoted to binary64 by x_cog; no mass flow
+                R tf = a.act_f64 ? P.rcs_force * (R)ud[0] : (R)(P.f_rcs_force * uf[0]);
+                cfp = R(0); cfperp = R(0);
+                cm = -tf * (x_cog - P.rcs_d_bottom) + tf * (P.rcs_d_top - x_cog);
+                mdot_dt = R(0); md_info = R(0); thr_info = R(0);
+            } else if (aux == PD_PHASE_FLIP_OVER) {
+                // force_moment_decomposer_flipoverboostbackburn (:63-92): gimbal low-pass (tau 1,
+                // dt), full throttle; the filtered angle keeps the action's dtype
+                R gd;
+                if (a.act_f64) gd = gprev + dt * ((-gprev + (R)ud[0] * R(10)) / R(1));
+                else { float x0 = (float)gprev; gd = (R)(x0 + (float)dt * ((-x0 + uf[0] * 10.0f) / 1.0f)); }
+                R grad = gd * Cst<R>::deg2rad;
+                R tg = T_full * (R)P.n_eng;
+                R cg = cos(grad), sg = sin(grad);
+                R tpar = tg * cg, tperp = -tg * sg;
+                cfp = tpar; cfperp = tperp; cm = -tg * sg * d_thrust;
+                R md = P.Te_over_vex * (sqrt(tpar * tpar + tperp * tperp) / T_full);
+                mdot_dt = md * dt; md_info = md; thr_info = R(1);
+                gdeg_out = gd; gprev = gd;
+            } else {
+                // force_moment_decomposer_ascent (:17-56): 16 gimballed + 26 fixed, nominal 0.5,
+                // gimbal radians(7)
+                const R ng = (R)P.n_eng, nng = (R)(P.n_eng_stage1 - P.n_eng);
+                if (a.act_f64) {
+                    R grad = (R)ud[0] * P.mg_ascent;
+                    R thr = ((R)ud[1] + R(1)) / R(2) * R(0.5) + R(0.5);
+                    R tg = T_full * ng * thr, tng = T_full * nng * thr;
+                    R cg = cos(grad), sg = sin(grad);
+                    R tpar = tng + tg * cg, tperp = -tg * sg;
+                    cfp = tpar; cfperp = tperp; cm = -tg * sg * d_thrust;
+                    R md = P.Te_over_vex * (sqrt(tpar * tpar + tperp * tperp) / T_full);
+                    mdot_dt = md * dt; md_info = md; thr_info = thr;
+                    gdeg_out = grad * Cst<R>::rad2deg;
+                } else {
+                    float grad = uf[0] * P.f_mg_ascent;
+                    float nnt = (uf[1] + 1.0f) / 2.0f;
+                    float thr = nnt * 0.5f + 0.5f;
+                    float tg = (float)(T_full * ng) * thr, tng = (float)(T_full * nng) * thr;
+                    float cg = (float)cos((R)grad), sg = (float)sin((R)grad);
+                    float tpar = tng + tg * cg, tperp = (-tg) * sg;
+                    float tot = sqrtf(tpar * tpar + tperp * tperp);
+                    float mdf = P.f_Te_over_vex * (tot / (float)T_full);
+                    cfp_f = tpar; cfperp_f = tperp; f32_forces = true;
+                    cfp = (R)tpar; cfperp = (R)tperp; cm = (R)((-tg) * sg) * d_thrust;
+                    mdot_dt = (R)(mdf * (float)dt); md_info = (R)mdf; thr_info = (R)thr;
+                    gdeg_out = (R)grad * Cst<R>::rad2deg;
+                }
+            }
+        } else if constexpr (PHASE == 0) {
             // force_moment_decomposer_landing_burn_throttle_only (:340-400); ACS with zero
             // deflection: F_perp = M = 0 exactly, F_par = qS * (Ca * (2 + 1 + 1))
             R acs_par = qS * (Ca * R(4));
@@ -867,10 +952,23 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PD_WPE))
         if (isnan(cfp)) { cfp = R(0); nan_hit = true; }
         else if (isnan(cfperp)) { cfperp = R(0); nan_hit = true; }
         else if (isnan(cm)) { cm = R(0); nan_hit = true; }
-        R cfx = cfp * cth + cfperp * sth;
-        R cfy = cfp * sth - cfperp * cth;
         R gr = gravity<R>(P, y);
-        R fx = aero_x + cfx + Fwx, fy = aero_y + cfy + Fwy;
+        R fx, fy;
+        if (PHASE == 2 && f32_forces) {
+            // float32 control forces join the Python-float aero terms in binary32; with wind on
+            // F_wind_x is a numpy float64 (interp1d output) and promotes the last sum
+            if (isnan(cfp_f)) cfp_f = 0.f;
+            else if (isnan(cfperp_f)) cfperp_f = 0.f;
+            float c = (float)cth, sn = (float)sth;
+            float cx = cfp_f * c + cfperp_f * sn, cy = cfp_f * sn - cfperp_f * c;
+            float sx = (float)aero_x + cx, sy = (float)aero_y + cy;
+            fx = WIND ? (R)sx + Fwx : (R)(sx + (float)Fwx);
+            fy = (R)(sy + (float)Fwy);
+        } else {
+            R cfx = cfp * cth + cfperp * sth;
+            R cfy = cfp * sth - cfperp * cth;
+            fx = aero_x + cfx + Fwx; fy = aero_y + cfy + Fwy;
+        }
         R vxd = fx / m, vyd = fy / m - gr;
         vx += vxd * dt; vy += vyd * dt; x += vx * dt; y += vy * dt;
         R thdd = (cm + aero_m + Mw) / I;
@@ -882,7 +980,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PD_WPE))
         mp -= mdot_dt; m -= mdot_dt;
         s[0] = x; s[1] = y; s[2] = vx; s[3] = vy; s[4] = th; s[5] = thd; s[6] = ga; s[7] = al;
         s[8] = m; s[9] = mp; s[10] = s[10] + dt;
-        if (sub == 3 && a.info && role == 0 && live) {   // info of the last sub-step (rockets_physics.py:649-702)
+        if (sub == NSUB - 1 && a.info && role == 0 && live) {   // info of the last sub-step (rockets_physics.py:649-702)
             R vals[PD_N_INFO - 1] = {rho, patm, asnd, mach, q, CL, CD, md_info, x_cog, I, ae, thr_info, ug, vg, gdeg_out};
 #pragma unroll
             for (int k = 0; k < PD_N_INFO - 1; ++k) ev(a.info + ((k < PD_INFO_GLOAD ? k : k + 1)) * N, ui) = vals[k];
@@ -916,7 +1014,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PD_WPE))
     int tr = 0, id = 0, dn = 0;
     R rew = R(0);
     const R r2 = (R)(2.0 * kDeg2Rad);
-    if constexpr (RTD == 0) {
+    if constexpr (RTD == 0 && PHASE != 2) {
+        // landing burns: truncated/done shared by both RL flavours (rtd_rl.py:194-240)
         if (y < R(-10)) { tr = 1; id = 1; }
         else if (mp <= R(0)) { tr = 1; id = 2; }
         else if (th > Cst<R>::pi + r2) { tr = 1; id = 3; }
@@ -925,18 +1024,100 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PD_WPE))
         else if (vy > R(0)) { tr = 1; id = 6; }
         else if (vx > R(0.01)) { tr = 1; id = 7; }
         dn = (y > R(0) && y < R(1) && speed < R(5));
-        R sp = hypot(vx, vy);
-        R qr = R(0.5) * rho * (sp * sp);
-        if (qr > R(60000)) { R e = (qr - R(60000)) / (R(65000) - R(60000)); R e2 = e * e; rew -= R(1) * (e2 > R(1) ? R(1) : e2); }
-        if (gl > R(5.5)) { R e = (gl - R(5.5)) / (R(6) - R(5.5)); R e2 = e * e; rew -= R(1) * (e2 > R(1) ? R(1) : e2); }
-        R prog = (P2.y0_rl - y) / P2.y0_rl;
-        R wp = (qr <= R(60000) && gl <= R(5.5)) ? R(0.5) : R(0.5) * R(0.1);
-        rew += wp * prog;
-        if (y < R(100)) rew += R(5.5) * (R(1) - fabs(vy) / R(50));
-        if (dn && !tr) rew += R(400) * mp / P2.m0_rl;
-        else if (tr && y > R(0)) rew -= R(50) * (fabs(y) / P2.y0_rl);
-        else if (tr && y < R(0)) rew -= R(50) * (fabs(vy) / R(10));
-        if (!dn || !(tr && y < R(0))) rew = rew < R(-10) ? R(-10) : (rew > R(10) ? R(10) : rew);
+        if constexpr (PHASE == 0) {   // pure-throttle reward (rtd_rl.py:272-336)
+            R sp = hypot(vx, vy);
+            R qr = R(0.5) * rho * (sp * sp);
+            if (qr > R(60000)) { R e = (qr - R(60000)) / (R(65000) - R(60000)); R e2 = e * e; rew -= R(1) * (e2 > R(1) ? R(1) : e2); }
+            if (gl > R(5.5)) { R e = (gl - R(5.5)) / (R(6) - R(5.5)); R e2 = e * e; rew -= R(1) * (e2 > R(1) ? R(1) : e2); }
+            R prog = (P2.y0_rl - y) / P2.y0_rl;
+            R wp = (qr <= R(60000) && gl <= R(5.5)) ? R(0.5) : R(0.5) * R(0.1);
+            rew += wp * prog;
+            if (y < R(100)) rew += R(5.5) * (R(1) - fabs(vy) / R(50));
+            if (dn && !tr) rew += R(400) * mp / P2.m0_rl;
+            else if (tr && y > R(0)) rew -= R(50) * (fabs(y) / P2.y0_rl);
+            else if (tr && y < R(0)) rew -= R(50) * (fabs(vy) / R(10));
+            if (!dn || !(tr && y < R(0))) rew = rew < R(-10) ? R(-10) : (rew > R(10) ? R(10) : rew);
+        } else {                      // landing_burn / ACS reward (rtd_rl.py:243-269), u0 = actions[0]
+            R ae = fabs(ga - th - Cst<R>::pi);
+            R lead = R(1.5) - log(R(1) + ae) / P2.log_1p_max_ae;
+            R X;
+            if (a.act_f64) X = lead - ((R)ud[0] + R(1)) / R(2) * R(0.5);
+            else X = (R)((float)lead - ((uf[0] + 1.0f) / 2.0f) * 0.5f);
+            rew = X * (R(1) - y / P2.y0_rl) * R(2) / R(3);
+            if (y < R(100)) rew += R(1) - tanh((speed - R(15)) / R(15));
+            if (tr && y < R(5)) rew += R(1) - tanh((speed - R(5)) / R(5));
+            if (dn) rew += R(5);
+            rew *= P2.rl_scale;
+        }
+        if (a.rtd_none) { tr = 0; id = 0; dn = 0; rew = R(0); }
+    } else if constexpr (RTD == 0) {
+        const int ph = P2.phase;
+        if (ph == PD_PHASE_PCONTROL) {
+            // compile_rtd_rl_landing_burn_PDcontrol (rtd_rl.py:353-401) + the reward that rebinds
+            // the first (:479-531); v_ref = actions[0]
+            if (y < R(-10)) { tr = 1; id = 1; }
+            else if (mp <= R(0)) { tr = 1; id = 2; }
+            else if (th > Cst<R>::pi + r2) { tr = 1; id = 3; }
+            else if (q > R(65000)) { tr = 1; id = 4; }
+            else if (gl > R(6)) { tr = 1; id = 5; }
+            else if (vy > R(0)) { tr = 1; id = 6; }
+            dn = (y > R(0) && y < R(5) && speed < R(1));
+            R sp = hypot(vx, vy);
+            R qr = R(0.5) * rho * (sp * sp);
+            if (qr > R(60000)) { R e = (qr - R(60000)) / (R(65000) - R(60000)); R e2 = e * e; rew -= R(1) * (e2 > R(1) ? R(1) : e2); }
+            if (gl > R(5.5)) { R e = (gl - R(5.5)) / (R(6) - R(5.5)); R e2 = e * e; rew -= R(1) * (e2 > R(1) ? R(1) : e2); }
+            R prog = (P2.y0_rl - y) / P2.y0_rl;
+            R vt;
+            if (a.act_f64) { R t = R(1) - fabs(sp - (R)ud[0]) / R(10); vt = t > R(0) ? t : R(0); }
+            else { float t = 1.0f - fabsf((float)sp - uf[0]) / 10.0f; vt = t > 0.f ? (R)t : R(0); }
+            R wp = (qr <= R(60000) && gl <= R(5.5)) ? R(0.5) : R(0.5) * R(0.1);
+            rew += wp * prog * vt;
+            if (y < R(100)) { R t = R(1) - fabs(vy - R(0)) / R(50); rew += R(0.5) * (t > R(0) ? t : R(0)); }
+            rew += P2.alive_bonus;
+            if (dn && !tr) { rew += R(5); R used = P2.y0_rl * R(0) + (P2.m0_rl - s[8]); R u = R(0.1) * used; rew -= u < R(1) ? u : R(1); }
+            else if (tr) { R u = R(4) * (y / P2.y0_rl) * (fabs(vy) / R(100)); rew -= u < R(5) ? u : R(5); }
+            rew = rew < R(-10) ? R(-10) : (rew > R(10) ? R(10) : rew);
+        } else if (ph == PD_PHASE_BALLISTIC_ARC) {
+            // compile_rtd_rl_ballistic_arc_descent (rtd_rl.py:153-188)
+            R ae = fabs(ga - th - Cst<R>::pi);
+            dn = (q > R(10000) && ae < (R)(3.0 * kDeg2Rad));
+            if (q > R(10000 - 2000) && ae > (R)(5.0 * kDeg2Rad)) { tr = 1; id = 1; }
+            rew = (Cst<R>::pi - ae) / Cst<R>::pi;
+            if (dn) rew += R(3.5);
+            rew /= R(100);
+        } else if (ph == PD_PHASE_SUBSONIC || ph == PD_PHASE_SUPERSONIC) {
+            // compile_rtd_rl_ascent (rtd_rl.py:11-114) over the ascent reference trajectory
+            bool nan_ = false;
+#pragma unroll
+            for (int k = 0; k < 11; ++k) nan_ |= isnan(s[k]);
+            if (nan_) { tr = 1; id = 0; }
+            else {
+                R mach = (speed != R(0) && as_ != R(0)) ? speed / as_ : R(0);
+                R mx = hyper_interp<R>(P2, 1, mach), mvy = hyper_interp<R>(P2, 2, mach);
+                R mvx = hyper_interp<R>(P2, 3, mach), mal = hyper_interp<R>(P2, 4, mach);
+                int n = P2.n_ref;
+                R xr = interp1d_ext<R>(P2.ref_y, P2.ref_x, n, y), vxr = interp1d_ext<R>(P2.ref_y, P2.ref_vx, n, y);
+                R vyr = interp1d_ext<R>(P2.ref_y, P2.ref_vy, n, y);
+                R al = s[7];
+                dn = (mp >= R(0) && mach > P2.terminal_mach);
+                if (mp <= R(0)) { tr = 1; id = 1; }
+                else if (mach > P2.terminal_mach + R(0.09)) { tr = 1; id = 2; }
+                else if (fabs(x - xr) > mx) { tr = 1; id = 3; }
+                else if (y < R(0)) { tr = 1; id = 4; }
+                else if (fabs(al) > mal * Cst<R>::deg2rad) { tr = 1; id = 5; }
+                else if (fabs(vx - vxr) > mvx) { tr = 1; id = 6; }
+                else if (fabs(vy - vyr) > mvy) { tr = 1; id = 7; }
+                if (!(y < R(0))) {
+                    R d = vx - vxr; rew += exp(R(-4) * (d * d) / (mvx * mvx)) * hyper_interp<R>(P2, 8, mach);
+                    d = vy - vyr; rew += exp(R(-4) * (d * d) / (mvy * mvy)) * hyper_interp<R>(P2, 7, mach);
+                    d = x - xr; rew += exp(R(-4) * (d * d) / (mx * mx)) * hyper_interp<R>(P2, 6, mach);
+                    d = al * Cst<R>::rad2deg; rew += exp(R(-4) * (d * d) / (mal * mal)) * hyper_interp<R>(P2, 5, mach);
+                    if (dn) rew += R(2.5);
+                    rew /= R(10000);
+                }
+            }
+        }
+        if (a.rtd_none || ph == PD_PHASE_FLIP_OVER) { tr = 0; id = 0; dn = 0; rew = R(0); }
     } else {
         if constexpr (PHASE == 0) {
             if (y < R(0)) { tr = 1; id = 1; }
@@ -979,18 +1160,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PD_WPE))
     const bool ended = !POL && a.auto_reset && (dn || tr);
     if (role == 0 && live) {
         if (a.obs) {
-            if constexpr (RTD == 0) {
-                // GymnasiumWrapperPyTorch._process_state casts the raw state to float32 BEFORE
-                // augment_state (env_wrapped_rl_pytorch.py:42-47, 195-198)
-                ev(a.obs + 0, ui_out * 2) = (R(1) - (R)(float)y / P2.norm_y) * R(2) - R(1);
-                ev(a.obs + 1, ui_out * 2) = (R(1) - (R)(float)vy / P2.norm_vy) * R(2) - R(1);
-            } else if constexpr (PHASE == 0) {
-                ev(a.obs + 0, ui_out * 2) = y / P2.norm_y; ev(a.obs + 1, ui_out * 2) = vy / P2.norm_vy;
-            } else {
-                ev(a.obs + 0, ui_out * 5) = x / P2.norm_x; ev(a.obs + 1, ui_out * 5) = y / P2.norm_y;
-                ev(a.obs + 2, ui_out * 5) = vx / P2.norm_vx; ev(a.obs + 3, ui_out * 5) = vy / P2.norm_vy;
-                ev(a.obs + 4, ui_out * 5) = tanh(P2.k_theta_pso * (th - Cst<R>::pi / R(2)));
-            }
+            // the wrappers' observation (obs_write kinds); compile-time for the landing burns
+            constexpr int kind = RTD == 1 ? (PHASE == 0 ? 1 : 2) : (PHASE == 0 ? 0 : (PHASE == 1 ? 3 : -1));
+            obs_write<R>(P2, kind >= 0 ? kind : P2.obs_kind, s, a.obs, ui_out);
         }
         if (a.reward) ev(a.reward, ui_out) = rew;
         if constexpr (POL) {
@@ -1013,6 +1185,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PD_WPE))
             ev(a.b.tid, ui_out) = (int8_t)id;
             ev(a.b.tstep, ui_out) = ts + 1;
             if constexpr (PHASE == 1) { ev(a.b.act, ui_out) = gdeg_out; ev(a.b.act + N, ui_out) = dcmdl_out; ev(a.b.act + (2) * N, ui_out) = dcmdr_out; }
+            if constexpr (PHASE == 2) { if (aux == PD_PHASE_FLIP_OVER) ev(a.b.act, ui_out) = gdeg_out; }
             if constexpr (WIND) {
                 ev(a.b.wind, ui_out) = fu0; ev(a.b.wind + N, ui_out) = fu1; ev(a.b.wind + (2) * N, ui_out) = fv0; ev(a.b.wind + (3) * N, ui_out) = fv1;
             }
@@ -1079,17 +1252,10 @@ __global__ __launch_bounds__(kBlock) void k_observe(StepArgs<R> a, int obs_kind)
     int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     const int64_t N = a.n;
     if (i >= N) return;
-    R x = a.b.st[i], y = a.b.st[N + i], vx = a.b.st[2 * N + i], vy = a.b.st[3 * N + i], th = a.b.st[4 * N + i];
-    if (obs_kind == 0) {
-        a.obs[i * 2] = (R(1) - (R)(float)y / P.norm_y) * R(2) - R(1);
-        a.obs[i * 2 + 1] = (R(1) - (R)(float)vy / P.norm_vy) * R(2) - R(1);
-    } else if (obs_kind == 1) {
-        a.obs[i * 2] = y / P.norm_y; a.obs[i * 2 + 1] = vy / P.norm_vy;
-    } else {
-        a.obs[i * 5] = x / P.norm_x; a.obs[i * 5 + 1] = y / P.norm_y;
-        a.obs[i * 5 + 2] = vx / P.norm_vx; a.obs[i * 5 + 3] = vy / P.norm_vy;
-        a.obs[i * 5 + 4] = tanh(P.k_theta_pso * (th - Cst<R>::pi / R(2)));
-    }
+    R s[11];
+#pragma unroll
+    for (int k = 0; k < 11; ++k) s[k] = a.b.st[k * N + i];
+    obs_write<R>(P, obs_kind, s, a.obs, (uint32_t)i);
 }
 
 template <typename R>
@@ -1260,7 +1426,26 @@ struct pd_env {
     int logcap_cd = 0, logcap_cl = 0;
     int64_t entries_cd = 0, entries_cl = 0;
     int lpe = 2;   // lanes per env of the step kernel
+    int obs_kind = 0;   // obs_write layout of the handle's observation
 };
+
+namespace {
+// observation layout (obs_write) and widths of a (phase, rtd) pair
+int obs_kind_of(int phase, int rtd) {
+    if (rtd == PD_RTD_PSO) return phase == PD_PHASE_PURE_THROTTLE ? 1 : 2;
+    switch (phase) {
+        case PD_PHASE_PURE_THROTTLE: return 0;
+        case PD_PHASE_LANDING_BURN: return 3;
+        case PD_PHASE_PCONTROL: return 4;
+        case PD_PHASE_BALLISTIC_ARC: return 5;
+        case PD_PHASE_FLIP_OVER: return 6;
+        default: return 7;
+    }
+}
+int act_dim_of(int phase) {
+    return phase == PD_PHASE_LANDING_BURN ? 4 : ((phase == PD_PHASE_SUBSONIC || phase == PD_PHASE_SUPERSONIC) ? 2 : 1);
+}
+}  // namespace
 
 namespace {
 
@@ -1288,6 +1473,8 @@ template <typename R> StepArgs<R> make_args(pd_env* e) {
     a.fixed_prof = e->cfg.wind_percentile >= 50 ? e->cfg.wind_percentile - 50 : -1;
     a.use_tilt = e->cfg.tilt_sigma_rad > 0.0;
     a.tilt_sigma = e->cfg.tilt_sigma_rad;
+    a.dt_aux = e->cfg.dt > 0.0 ? e->cfg.dt : 0.1;
+    a.rtd_none = e->cfg.rtd == PD_RTD_NONE;
     return a;
 }
 
@@ -1355,17 +1542,62 @@ template <typename R> void fill_params(const pd_params* p, const pd_config* c, D
     D.k_theta_pso = (R)(std::atanh(0.75) / (25.0 * kDeg2Rad));
     log_table_fill(D.logtab);
     D.y0_rl = (R)p->state0[1]; D.m0_rl = (R)p->state0[8];
-    (void)c;
+    // ---- phase of the handle: its initial state, observation, and the constants of the
+    // other compile_physics phases (rockets_physics.py:17-166,402-451,728-802,959-997)
+    D.phase = c->phase;
+    D.obs_kind = obs_kind_of(c->phase, c->rtd);
+    if (c->phase >= PD_PHASE_PCONTROL)
+        for (int k = 0; k < 11; ++k) { D.state0[k] = (R)p->state0_phase[c->phase][k]; D.state0_d[k] = p->state0_phase[c->phase][k]; }
+    for (int k = 0; k < 13; ++k) D.fr[k] = (R)p->full_rocket[k];
+    D.cop_ascent = (R)p->cop_ascent; D.n_eng_stage1 = p->n_engines_stage1;
+    double mg_ascent = 7.0 * kDeg2Rad;
+    D.mg_ascent = (R)mg_ascent; D.f_mg_ascent = (float)mg_ascent;
+    D.kp_pc = (R)-0.08; D.f_kp_pc = (float)-0.08;
+    D.rcs_force = (R)p->rcs_force; D.f_rcs_force = (float)p->rcs_force;
+    D.rcs_d_bottom = (R)p->rcs_d_bottom; D.rcs_d_top = (R)p->rcs_d_top;
+    // rl_wrapped_env_pytorch.augment_state (env_wrapped_rl_pytorch.py:178-194) constants
+    D.f_k_theta_rl = (float)(std::atanh(0.75) / (5.0 * kDeg2Rad));
+    D.f_k_thetad_rl = (float)(std::atanh(0.75) / 0.01);
+    D.f_k_gamma_rl = (float)(std::atanh(0.75) / (5.0 * kDeg2Rad));
+    D.f_pi_2 = (float)(kPi / 2); D.f_pi_3_2 = (float)(3.0 / 2 * kPi);
+    for (int k = 0; k < 8; ++k) D.norm_ph[k] = (R)p->norm_phase[c->phase][k];
+    int which = c->phase == PD_PHASE_SUPERSONIC ? 1 : 0;
+    for (int r = 0; r < 12; ++r) for (int f = 0; f < 9; ++f) D.hyper[r][f] = (R)p->hyper[which][r][f];
+    D.terminal_mach = (R)p->terminal_mach[which];
+    D.n_ref = p->n_ref;
+    // rtd_rl.py:267 (n-step scale, Python float ** int -> C pow), :472 (alive bonus), :250
+    double g = c->discount_factor;
+    D.rl_scale = (R)((1 - g) / (1 - std::pow(g, (double)c->trajectory_length)));
+    D.alive_bonus = (R)(0.01 * (1 - g));
+    D.log_1p_max_ae = (R)std::log(1 + 20.0 * kDeg2Rad);
 }
 
 pd_status validate(const pd_params* p, const pd_config* c) {
     if (!p || !c) return fail(PD_ERR_INVALID, "null params/config");
     // per-lane byte offsets in k_step are 32-bit (largest per-env row: noise, 64 B)
     if (c->n_envs <= 0 || c->n_envs > (int64_t)1 << 25) return fail(PD_ERR_INVALID, "n_envs out of range (1 .. 2^25 per handle)");
-    if (c->phase != PD_PHASE_PURE_THROTTLE && c->phase != PD_PHASE_LANDING_BURN) return fail(PD_ERR_INVALID, "bad phase");
-    if (c->rtd != PD_RTD_RL && c->rtd != PD_RTD_PSO) return fail(PD_ERR_INVALID, "bad rtd");
-    if (c->rtd == PD_RTD_RL && c->phase != PD_PHASE_PURE_THROTTLE)
-        return fail(PD_ERR_UNSUPPORTED, "RL reward is implemented for landing_burn_pure_throttle (the SAC driver's phase)");
+    if (c->phase < 0 || c->phase > PD_PHASE_LANDING_BURN_ACS) return fail(PD_ERR_INVALID, "bad phase");
+    if (c->rtd != PD_RTD_RL && c->rtd != PD_RTD_PSO && c->rtd != PD_RTD_NONE) return fail(PD_ERR_INVALID, "bad rtd");
+    if (c->phase == PD_PHASE_LANDING_BURN_ACS)
+        return fail(PD_ERR_UNSUPPORTED, "landing_burn_ACS: the reference raises TypeError at its first step "
+                                        "(rockets_physics.py:867-891 passes ACS arguments to the gimballed decomposer; "
+                                        "base_environment.py:126-130 passes two prevs to a three-prev lambda)");
+    if (c->rtd == PD_RTD_RL && c->phase == PD_PHASE_FLIP_OVER)
+        return fail(PD_ERR_UNSUPPORTED, "flip_over_boostbackburn with rtd RL: the reference raises TypeError at its first "
+                                        "step (rtd_rl.py:134 truncated_func(state) called with three arguments, "
+                                        "base_environment.py:150); use PD_RTD_NONE for physics stepping");
+    if (c->rtd == PD_RTD_PSO && c->phase > PD_PHASE_LANDING_BURN)
+        return fail(PD_ERR_UNSUPPORTED, "rtd PSO exists for the two landing burns only: the other rtd_pso functions take "
+                                        "(state) / (state, done, truncated) and raise TypeError when the env calls them "
+                                        "(rtd_pso.py:38,63,107,120,141,157 vs base_environment.py:150-152)");
+    if (c->dt < 0.0) return fail(PD_ERR_INVALID, "dt must be >= 0");
+    if (c->rtd == PD_RTD_RL && (c->phase == PD_PHASE_LANDING_BURN || c->phase == PD_PHASE_PCONTROL) &&
+        (c->trajectory_length < 1 || !(c->discount_factor > 0.0 && c->discount_factor < 1.0)))
+        return fail(PD_ERR_INVALID, "this RL reward needs discount_factor in (0, 1) and trajectory_length >= 1");
+    if (c->phase == PD_PHASE_SUBSONIC || c->phase == PD_PHASE_SUPERSONIC) {
+        if (!p->ref_y || !p->ref_x || !p->ref_vx || !p->ref_vy || p->n_ref < 2)
+            return fail(PD_ERR_INVALID, "ascent phases need the reference trajectory (ref_y/x/vx/vy, n_ref >= 2)");
+    }
     if (c->precision != PD_F64 && c->precision != PD_F32) return fail(PD_ERR_INVALID, "bad precision");
     if (c->action_f64 && c->precision != PD_F64) return fail(PD_ERR_INVALID, "f64 actions need PD_F64");
     if (c->enable_wind && !(c->wind_percentile == -1 || (c->wind_percentile >= 50 && c->wind_percentile <= 99)))
@@ -1432,6 +1664,19 @@ template <typename R> pd_status create_impl(const pd_params* p, const pd_config*
     // (any valid 50-set works; the in-kernel swap search repairs it)
     D.init_key_cd = host_knn_key(p->cd, 3.0, 0.0);
     D.init_key_cl = host_knn_key(p->cl, 3.0, 10.0);
+    if (c->phase == PD_PHASE_SUBSONIC || c->phase == PD_PHASE_SUPERSONIC) {
+        // ascent reference trajectory, in the handle's precision (binary-searched per env-step)
+        const double* src[4] = {p->ref_y, p->ref_x, p->ref_vx, p->ref_vy};
+        const R** dst[4] = {&D.ref_y, &D.ref_x, &D.ref_vx, &D.ref_vy};
+        std::vector<R> buf((size_t)p->n_ref);
+        for (int k = 0; k < 4; ++k) {
+            void* d;
+            if ((st = dalloc(e, &d, buf.size() * sizeof(R)))) return st;
+            for (int32_t r = 0; r < p->n_ref; ++r) buf[r] = (R)src[k][r];
+            PD_HIP(hipMemcpy(d, buf.data(), buf.size() * sizeof(R), hipMemcpyHostToDevice));
+            *dst[k] = (const R*)d;
+        }
+    }
     if ((st = dalloc(e, &e->dparams, sizeof(D)))) return st;
     PD_HIP(hipMemcpy(e->dparams, &D, sizeof(D), hipMemcpyHostToDevice));
     size_t R_ = sizeof(R);
@@ -1475,11 +1720,14 @@ template <typename R, int PH, int RT, bool W> void launch_lpe(int lpe, const Ste
 }
 
 template <typename R> void dispatch_step(const pd_env* e, const StepArgs<R>& a, hipStream_t s) {
-    int ph = e->cfg.phase, rt = e->cfg.rtd, l = e->lpe;
+    int ph = e->cfg.phase, l = e->lpe;
+    bool pso = e->cfg.rtd == PD_RTD_PSO;   // RL and NONE share the RL instantiation (NONE zeroes the rtd)
     bool w = e->cfg.enable_wind != 0;
-    if (ph == 0 && rt == 0) { if (w) launch_lpe<R, 0, 0, true>(l, a, s); else launch_lpe<R, 0, 0, false>(l, a, s); }
-    else if (ph == 0 && rt == 1) { if (w) launch_lpe<R, 0, 1, true>(l, a, s); else launch_lpe<R, 0, 1, false>(l, a, s); }
-    else { if (w) launch_lpe<R, 1, 1, true>(l, a, s); else launch_lpe<R, 1, 1, false>(l, a, s); }
+    if (ph == 0 && !pso) { if (w) launch_lpe<R, 0, 0, true>(l, a, s); else launch_lpe<R, 0, 0, false>(l, a, s); }
+    else if (ph == 0) { if (w) launch_lpe<R, 0, 1, true>(l, a, s); else launch_lpe<R, 0, 1, false>(l, a, s); }
+    else if (ph == 1 && pso) { if (w) launch_lpe<R, 1, 1, true>(l, a, s); else launch_lpe<R, 1, 1, false>(l, a, s); }
+    else if (ph == 1) { if (w) launch_lpe<R, 1, 0, true>(l, a, s); else launch_lpe<R, 1, 0, false>(l, a, s); }
+    else { if (w) launch_lpe<R, 2, 0, true>(l, a, s); else launch_lpe<R, 2, 0, false>(l, a, s); }
 }
 
 template <typename R, int PH, bool W, int LPE> void launch_policy_lpe(const StepArgs<R>& a, hipStream_t s) {
@@ -1565,8 +1813,9 @@ pd_status pd_create(const pd_params* params, const pd_config* cfg, pd_env** out)
     pd_env* e = new pd_env();
     e->cfg = *cfg;
     e->device = cfg->device;
-    e->act_dim = cfg->phase == PD_PHASE_PURE_THROTTLE ? 1 : 4;
-    e->obs_dim = (cfg->phase == PD_PHASE_LANDING_BURN) ? 5 : 2;
+    e->act_dim = act_dim_of(cfg->phase);
+    e->obs_kind = obs_kind_of(cfg->phase, cfg->rtd);
+    e->obs_dim = obs_dim(e->obs_kind);
     e->rsize = cfg->precision == PD_F64 ? 8 : 4;
     // default lanes per env: enough waves to fill the chip.  Below ~32k envs the step is bound by
     // one wave's latency, and splitting each RBF over more lanes shortens it (measured, f64:
@@ -1647,7 +1896,7 @@ pd_status pd_flush_misses(pd_env* e, void* stream) {
 pd_status pd_observe(pd_env* e, void* obs, void* stream) {
     if (!e || !obs) return fail(PD_ERR_INVALID, "null env/obs");
     PD_HIP(hipSetDevice(e->device));
-    int kind = e->cfg.rtd == PD_RTD_RL ? 0 : (e->cfg.phase == PD_PHASE_PURE_THROTTLE ? 1 : 2);
+    int kind = e->obs_kind;
     unsigned grid = (unsigned)((e->cfg.n_envs + kBlock - 1) / kBlock);
     hipStream_t s = (hipStream_t)stream;
     if (e->rsize == 8) { auto a = make_args<double>(e); a.obs = (double*)obs; hipLaunchKernelGGL(k_observe<double>, dim3(grid), dim3(kBlock), 0, s, a, kind); }
@@ -1681,6 +1930,18 @@ pd_status pd_set_actuators(pd_env* e, const void* act, void* stream) {
     if (!e || !act) return fail(PD_ERR_INVALID, "null env/act");
     PD_HIP(hipSetDevice(e->device));
     PD_HIP(hipMemcpyAsync(e->act, act, 3 * e->cfg.n_envs * e->rsize, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+    return PD_OK;
+}
+
+pd_status pd_set_gload_window(pd_env* e, const void* vprev, const void* window, const uint8_t* len, void* stream) {
+    if (!e || !vprev || !window || !len) return fail(PD_ERR_INVALID, "null env/vprev/window/len");
+    PD_HIP(hipSetDevice(e->device));
+    hipStream_t s = (hipStream_t)stream;
+    const size_t N = (size_t)e->cfg.n_envs;
+    PD_HIP(hipMemcpyAsync(e->vprev, vprev, N * e->rsize, hipMemcpyDeviceToDevice, s));
+    PD_HIP(hipMemcpyAsync(e->gwin, window, 10 * N * e->rsize, hipMemcpyDeviceToDevice, s));
+    PD_HIP(hipMemcpyAsync(e->glen, len, N, hipMemcpyDeviceToDevice, s));
+    PD_HIP(hipMemsetAsync(e->ghead, 0, N, s));   // oldest entry in slot 0
     return PD_OK;
 }
 

@@ -14,8 +14,9 @@ MAX_PTS, MAX_COLS, MAX_TAB, MAX_WIND, N_PROF = 256, 5, 64, 16, 50
 N_STATE, N_INFO = 11, 16
 
 PD_OK, PD_ERR_INVALID, PD_ERR_HIP, PD_ERR_NOMEM, PD_ERR_UNSUPPORTED = range(5)
-PURE_THROTTLE, LANDING_BURN = 0, 1
-RTD_RL, RTD_PSO = 0, 1
+(PURE_THROTTLE, LANDING_BURN, PCONTROL, BALLISTIC_ARC, FLIP_OVER, SUBSONIC, SUPERSONIC,
+ LANDING_BURN_ACS) = range(8)
+RTD_RL, RTD_PSO, RTD_NONE = 0, 1, 2
 F64, F32 = 0, 1
 ACTOR_PARAMS = {0: 249, 1: 372}   # PD_ACTOR_PARAMS_PURE_THROTTLE / _LANDING_BURN
 
@@ -53,6 +54,13 @@ class PdParams(C.Structure):
         ("state0", D * N_STATE), ("norm_y", D), ("norm_vy", D), ("norm_x", D), ("norm_vx", D),
         ("keys_cd", C.POINTER(U64)), ("n_keys_cd", I64),
         ("keys_cl", C.POINTER(U64)), ("n_keys_cl", I64),
+        # ABI 2: the other flight phases
+        ("full_rocket", D * 13), ("cop_ascent", D), ("n_engines_stage1", I32), ("pad1", I32),
+        ("rcs_force", D), ("rcs_d_bottom", D), ("rcs_d_top", D),
+        ("state0_phase", (D * N_STATE) * 8), ("norm_phase", (D * 8) * 8),
+        ("ref_y", C.POINTER(D)), ("ref_x", C.POINTER(D)), ("ref_vx", C.POINTER(D)), ("ref_vy", C.POINTER(D)),
+        ("n_ref", I32), ("pad2", I32),
+        ("hyper", ((D * 9) * 12) * 2), ("terminal_mach", D * 2),
     ]
 
 
@@ -60,12 +68,13 @@ class PdConfig(C.Structure):
     _fields_ = [("n_envs", I64), ("device", I32), ("phase", I32), ("rtd", I32), ("precision", I32),
                 ("seed", U64), ("env_offset", U64), ("enable_wind", I32), ("stochastic_wind", I32),
                 ("wind_percentile", I32), ("auto_reset", I32), ("tilt_sigma_rad", D),
-                ("action_f64", I32), ("lanes_per_env", I32)]
+                ("action_f64", I32), ("lanes_per_env", I32),
+                ("dt", D), ("discount_factor", D), ("trajectory_length", I32), ("pad3", I32)]
 
 
 EXPORTS = ["pd_abi_version", "pd_sizeof_params", "pd_sizeof_config", "pd_last_error", "pd_device_count", "pd_create", "pd_destroy", "pd_reset",
            "pd_step", "pd_rollout", "pd_rollout_policy", "pd_pso_step", "pd_flush_misses", "pd_observe", "pd_get_state", "pd_set_state", "pd_get_actuators",
-           "pd_set_actuators", "pd_set_wind_sigmas", "pd_counters", "pd_obs_dim", "pd_action_dim"]
+           "pd_set_actuators", "pd_set_gload_window", "pd_set_wind_sigmas", "pd_counters", "pd_obs_dim", "pd_action_dim"]
 
 _lib = None
 
@@ -103,16 +112,17 @@ def load(path=None):
     L.pd_get_actuators.argtypes = [vp, vp, vp]
     L.pd_set_actuators.argtypes = [vp, vp, vp]
     L.pd_set_wind_sigmas.argtypes = [vp, vp, vp]
+    L.pd_set_gload_window.argtypes = [vp, vp, vp, vp, vp]
     L.pd_counters.argtypes = [vp, P(I64), P(I64), P(I64), P(I64)]
     L.pd_obs_dim.argtypes = [vp]; L.pd_obs_dim.restype = C.c_int
     L.pd_action_dim.argtypes = [vp]; L.pd_action_dim.restype = C.c_int
     for name in ("pd_create", "pd_destroy", "pd_reset", "pd_step", "pd_rollout", "pd_rollout_policy", "pd_pso_step", "pd_flush_misses", "pd_observe",
                  "pd_get_state", "pd_set_state", "pd_get_actuators", "pd_set_actuators",
-                 "pd_set_wind_sigmas", "pd_counters"):
+                 "pd_set_wind_sigmas", "pd_set_gload_window", "pd_counters"):
         getattr(L, name).restype = C.c_int
     L.pd_sizeof_params.restype = C.c_size_t
     L.pd_sizeof_config.restype = C.c_size_t
-    if L.pd_abi_version() != 1:
+    if L.pd_abi_version() != 2:
         raise PdError("libpdenv ABI version mismatch")
     if L.pd_sizeof_params() != C.sizeof(PdParams) or L.pd_sizeof_config() != C.sizeof(PdConfig):
         raise PdError("pd_params/pd_config layout mismatch between ctypes and libpdenv.so")

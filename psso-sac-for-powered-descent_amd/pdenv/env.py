@@ -1,10 +1,13 @@
 """Batched powered-descent environment over HBM-resident torch tensors.
 
 `PoweredDescentEnv(n_envs, ...)` is the vectorised counterpart of the reference's
-`rocket_environment_pre_wrap` (src/envs/base_environment.py:12-154) for the two phases the
-north-star drivers use: 'landing_burn_pure_throttle' (SAC driver) and 'landing_burn' (PSO
-driver).  All compute runs in libpdenv.so (HIP kernels); torch only provides device memory
-and the current stream.
+`rocket_environment_pre_wrap` (src/envs/base_environment.py:12-154) for every flight phase of
+compile_physics: the two the north-star drivers use, 'landing_burn_pure_throttle' (SAC driver)
+and 'landing_burn' (PSO driver), and 'landing_burn_pure_throttle_Pcontrol',
+'ballistic_arc_descent', 'flip_over_boostbackburn', 'subsonic', 'supersonic'.
+'landing_burn_ACS' is accepted by the constructor (as the reference's is) and raises TypeError
+at the first step, as the reference does.  All compute runs in libpdenv.so (HIP kernels); torch
+only provides device memory and the current stream.
 """
 import ctypes as C
 
@@ -13,8 +16,15 @@ import torch
 from . import _lib as L
 from .params import Params
 
-PHASES = {"landing_burn_pure_throttle": L.PURE_THROTTLE, "landing_burn": L.LANDING_BURN}
-MODES = {"rl": L.RTD_RL, "pso": L.RTD_PSO}
+PHASES = {"landing_burn_pure_throttle": L.PURE_THROTTLE, "landing_burn": L.LANDING_BURN,
+          "landing_burn_pure_throttle_Pcontrol": L.PCONTROL, "ballistic_arc_descent": L.BALLISTIC_ARC,
+          "flip_over_boostbackburn": L.FLIP_OVER, "subsonic": L.SUBSONIC, "supersonic": L.SUPERSONIC,
+          "landing_burn_ACS": L.LANDING_BURN_ACS}
+# 'physics': compile_physics stepping only (reward 0, never done/truncated)
+MODES = {"rl": L.RTD_RL, "pso": L.RTD_PSO, "physics": L.RTD_NONE}
+# (phase, mode) pairs whose reference env raises TypeError at the first step (include/pdenv.h)
+UNSTEPPABLE = {("landing_burn_ACS", m) for m in MODES} | {("flip_over_boostbackburn", "rl")} | \
+    {(p, "pso") for p in PHASES if p not in ("landing_burn_pure_throttle", "landing_burn")}
 
 
 def _stream(device):
@@ -29,17 +39,26 @@ class PoweredDescentEnv:
     def __init__(self, n_envs, flight_phase="landing_burn_pure_throttle", mode="rl", precision="f64",
                  device=0, enable_wind=False, stochastic_wind=False, wind_percentile=50,
                  auto_reset=False, tilt_sigma_rad=0.0, seed=0, env_offset=0, action_f64=False,
-                 params=None, lanes_per_env=0):
+                 params=None, lanes_per_env=0, dt=0.0, discount_factor=0.99, trajectory_length=100):
         if flight_phase not in PHASES:
             raise ValueError(f"flight_phase must be one of {list(PHASES)} (got {flight_phase!r})")
         if mode not in MODES:
-            raise ValueError(f"mode must be 'rl' or 'pso' (got {mode!r})")
+            raise ValueError(f"mode must be one of {list(MODES)} (got {mode!r})")
+        if mode == "pso" and flight_phase in ("landing_burn_ACS", "landing_burn_pure_throttle_Pcontrol"):
+            # compile_rtd_pso asserts its phase list (rtd_pso.py:321) at construction
+            raise AssertionError(f"compile_rtd_pso has no {flight_phase!r}")
+        self.flight_phase, self.mode = flight_phase, mode
+        self.n = int(n_envs)
+        self.unsteppable = (flight_phase, mode) in UNSTEPPABLE
+        if self.unsteppable:
+            # the reference constructs these envs and raises TypeError at their first step
+            self.h = None
+            self.obs_dim, self.action_dim = 0, 0
+            return
         self.lib = L.load()
         if self.lib.pd_device_count() <= 0 or not torch.cuda.is_available():
             raise L.PdError("no HIP device visible: the powered-descent env runs on MI355X only")
         self.device = torch.device("cuda", device) if isinstance(device, int) else torch.device(device)
-        self.n = int(n_envs)
-        self.flight_phase, self.mode = flight_phase, mode
         self.dtype = torch.float64 if precision == "f64" else torch.float32
         self.params = params or Params()
         cfg = L.PdConfig()
@@ -57,6 +76,9 @@ class PoweredDescentEnv:
         cfg.tilt_sigma_rad = float(tilt_sigma_rad)
         cfg.action_f64 = int(bool(action_f64))
         cfg.lanes_per_env = int(lanes_per_env)
+        cfg.dt = float(dt)
+        cfg.discount_factor = float(discount_factor) if discount_factor is not None else 0.0
+        cfg.trajectory_length = int(trajectory_length) if trajectory_length is not None else 0
         self.cfg = cfg
         handle = C.c_void_p()
         with torch.cuda.device(self.device):
@@ -77,6 +99,8 @@ class PoweredDescentEnv:
     # ------------------------------------------------------------------ reference surface
     def reset(self, mask=None):
         """base_environment.py:80-97 for all envs (or a bool/uint8 mask [N]); returns obs [N, O]."""
+        if self.unsteppable:
+            return None
         m = None
         if mask is not None:
             m = mask.to(device=self.device, dtype=torch.uint8).contiguous()
@@ -87,6 +111,7 @@ class PoweredDescentEnv:
         """base_environment.py:99-154 for every env.  actions: [N, A] float32 (float64 with
         action_f64).  Returns (obs, reward, done, truncated, extras) as device tensors; with
         auto_reset the obs is the post-step (terminal) observation."""
+        self._check_steppable()
         a = actions.to(device=self.device, dtype=self.action_dtype).reshape(self.n, self.action_dim).contiguous()
         nz = None
         if noise is not None:
@@ -101,6 +126,11 @@ class PoweredDescentEnv:
         if info:
             extras.update({k: inf[j] for j, k in enumerate(L.INFO_FIELDS)})
         return self._obs.clone(), self._rew.clone(), self._done.bool(), self._trunc.bool(), extras
+
+    def _check_steppable(self):
+        if self.unsteppable:
+            raise TypeError(f"{self.flight_phase!r} with mode {self.mode!r} cannot be stepped: the reference "
+                            "raises TypeError here (argument-count mismatch, see include/pdenv.h pd_phase/pd_rtd)")
 
     def step_raw(self, actions):
         """Hot-loop step: launches pd_step into the handle's preallocated output buffers
@@ -181,6 +211,15 @@ class PoweredDescentEnv:
     def set_actuators(self, act):
         soa = act.to(device=self.device, dtype=self.dtype).reshape(self.n, 3).t().contiguous()
         L.check(self.lib.pd_set_actuators(self.h, _ptr(soa), _stream(self.device)))
+        torch.cuda.current_stream(self.device).synchronize()
+
+    def set_gload_window(self, vprev, window, length):
+        """g-load history (base_environment.py:137-149): |v| of the previous state [N], the
+        window [N, 10] oldest first, and its valid length [N] (0..10)."""
+        vp = torch.as_tensor(vprev, dtype=self.dtype).to(self.device).reshape(self.n).contiguous()
+        w = torch.as_tensor(window, dtype=self.dtype).to(self.device).reshape(self.n, 10).t().contiguous()
+        ln = torch.as_tensor(length, dtype=torch.uint8).to(self.device).reshape(self.n).contiguous()
+        L.check(self.lib.pd_set_gload_window(self.h, _ptr(vp), _ptr(w), _ptr(ln), _stream(self.device)))
         torch.cuda.current_stream(self.device).synchronize()
 
     def set_wind_sigmas(self, sigma_u, sigma_v):

@@ -12,6 +12,10 @@ import numpy as np
 
 from ._lib import MAX_COLS, PdParams, U64
 
+# pd_phase order (include/pdenv.h)
+PHASE_NAMES = ["landing_burn_pure_throttle", "landing_burn", "landing_burn_pure_throttle_Pcontrol",
+               "ballistic_arc_descent", "flip_over_boostbackburn", "subsonic", "supersonic", "landing_burn_ACS"]
+
 PACK_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "data", "param_pack.json")
 
 _pack_cache = {}
@@ -81,6 +85,27 @@ class Params:
         self.keys_cl = np.array([int(k) for k in pk["rbf_keys_cl"]], dtype=np.uint64)
         p.keys_cd = self.keys_cd.ctypes.data_as(C.POINTER(U64)); p.n_keys_cd = len(self.keys_cd)
         p.keys_cl = self.keys_cl.ctypes.data_as(C.POINTER(U64)); p.n_keys_cl = len(self.keys_cl)
+        # the other flight phases (data/param_pack.json "phases", tools/make_param_pack.py)
+        ph = pk["phases"]
+        fr = ph["ascent_inertia"]
+        _fill(p.full_rocket, [fr[k] for k in ("x_wet_2_initial", "x_dry_1", "m_s_1", "m_pay", "m_2", "m_1_ox",
+                                              "m_1_f", "h_lower_1", "h_1_ox", "h_1_f", "h_1", "I_wet_2_initial",
+                                              "I_dry_1")])
+        p.cop_ascent = ph["cop_ascent"]
+        p.n_engines_stage1 = ph["n_engines_stage1"]
+        p.rcs_force, p.rcs_d_bottom, p.rcs_d_top = ph["rcs"]["max_force"], ph["rcs"]["d_bottom"], ph["rcs"]["d_top"]
+        for k, name in enumerate(PHASE_NAMES):
+            _fill(p.state0_phase[k], ph["state0"].get(name, pk["state0"]))
+            _fill(p.norm_phase[k], ph["norm"].get(name, [nm["y"], nm["vy"]]))
+        ref = ph["ascent_ref"]
+        self.ref = [np.ascontiguousarray(ref[k], dtype=np.float64) for k in ("y", "x", "vx", "vy")]
+        p.ref_y, p.ref_x, p.ref_vx, p.ref_vy = (a.ctypes.data_as(C.POINTER(C.c_double)) for a in self.ref)
+        p.n_ref = len(ref["y"])
+        for w, name in enumerate(("subsonic", "supersonic")):
+            for r, row in enumerate(ph["ascent_hyper"][name]):
+                _fill(p.hyper[w][r], [float(v) for v in row])
+            p.terminal_mach[w] = ph["terminal_mach"][name]
+        self.speed0_pcontrol = ph["speed0_pcontrol"]
         self.struct = p
         self.pack = pk
 
@@ -97,3 +122,8 @@ class Params:
     @property
     def state0(self):
         return np.array(self.pack["state0"])
+
+    def state0_of(self, phase):
+        """Initial state of a phase (load_initial_states.py), by pd_phase index or name."""
+        k = PHASE_NAMES.index(phase) if isinstance(phase, str) else int(phase)
+        return np.array(self.struct.state0_phase[k][:])

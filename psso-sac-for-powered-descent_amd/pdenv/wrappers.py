@@ -8,6 +8,8 @@ float/bool, an info dict); all physics runs in libpdenv.so on the GPU.  The batc
 points (`PoweredDescentEnv`, `pso_wrapped_env.objective_function_batch`) keep everything on
 the device for thousands of envs / particles.
 """
+import math
+
 import numpy as np
 import torch
 import torch.nn as nn
@@ -27,37 +29,77 @@ def _info_dict(env, ex, state, action):
     return info
 
 
+# state_dim / action_dim per phase (env_wrapped_rl_pytorch.py:87-104)
+RL_DIMS = {"subsonic": (8, 2), "supersonic": (8, 2), "flip_over_boostbackburn": (2, 1),
+           "ballistic_arc_descent": (4, 1), "landing_burn": (5, 4), "landing_burn_ACS": (5, 3),
+           "landing_burn_pure_throttle": (2, 1), "landing_burn_pure_throttle_Pcontrol": (1, 1)}
+
+
+def augment_action(flight_phase, actions, speed0=None):
+    """rl_wrapped_env_pytorch.augment_action (env_wrapped_rl_pytorch.py:120-165) on a batch of
+    float32 policy actions [N, A] (device tensor) -> the actions the env receives.
+
+    landing_burn: u' = sign(u) log(1 + c|u|)/log(1 + c), c = 10 (gimbal) / 5 (fins), u1 as is.
+        NumPy keeps c*|u| and 1 + c|u| in float32 (NEP 50); math.log and the division are
+        binary64, and np.array([...]) of the mix is float64 -> float64 actions.
+    landing_burn_pure_throttle_Pcontrol: v_ref = (u + 1)/2 * speed0, all float32.
+    other phases: unchanged (float32)."""
+    a = actions.to(torch.float32)
+    if flight_phase == "landing_burn":
+        def comp(u, c):
+            t = 1.0 + c * u.abs()                                   # float32 (NEP 50)
+            return torch.copysign(torch.log(t.double()) / math.log(1 + c), u.double())
+        return torch.stack([comp(a[:, 0], 10.0), a[:, 1].double(), comp(a[:, 2], 5.0), comp(a[:, 3], 5.0)], 1)
+    if flight_phase == "landing_burn_pure_throttle_Pcontrol":
+        return (a + 1.0) / 2.0 * torch.tensor(speed0, dtype=torch.float32, device=a.device)
+    return a
+
+
 class rl_wrapped_env_pytorch:
-    """env_wrapped_rl_pytorch.py:68-205 for the SAC driver's phase, landing_burn_pure_throttle.
+    """env_wrapped_rl_pytorch.py:68-205 for every flight phase (the SAC driver's is
+    landing_burn_pure_throttle).
 
-    step(action) -> (obs float64[2], float reward, bool done, bool truncated, info dict).
+    step(action) -> (obs float64[state_dim], float reward, bool done, bool truncated, info dict).
     Actions are taken as float32, the dtype SACPyTorch.select_action returns
-    (sac_pytorch.py:404-409); pass action_f64=True to reproduce float64 callers."""
+    (sac_pytorch.py:404-409), and augmented as the reference's wrapper does (augment_action);
+    pass action_f64=True to reproduce float64 callers of the pure-throttle phase.
+    flip_over_boostbackburn and landing_burn_ACS construct, and raise TypeError at step() as the
+    reference's do."""
 
-    def __init__(self, flight_phase="landing_burn_pure_throttle", enable_wind=False, stochastic_wind=True,
+    def __init__(self, flight_phase="subsonic", enable_wind=False, stochastic_wind=True,
                  horiontal_wind_percentile=50, trajectory_length=None, discount_factor=None,
                  precision="f64", device=0, seed=0, action_f64=False):
-        if flight_phase != "landing_burn_pure_throttle":
-            raise NotImplementedError("the RL facade covers the SAC driver's phase 'landing_burn_pure_throttle'")
+        if flight_phase not in RL_DIMS:
+            raise AssertionError(f"unknown flight_phase {flight_phase!r}")
         self.flight_phase = flight_phase
         self.enable_wind = enable_wind
+        self.state_dim, self.action_dim = RL_DIMS[flight_phase]
+        # landing_burn's augmented actions are float64 arrays (np.array of Python floats)
+        f64 = action_f64 or flight_phase == "landing_burn"
         self.env = PoweredDescentEnv(1, flight_phase, mode="rl", precision=precision, device=device,
                                      enable_wind=enable_wind, stochastic_wind=stochastic_wind,
                                      wind_percentile=horiontal_wind_percentile, seed=seed,
-                                     action_f64=action_f64)
-        self.state_dim, self.action_dim = 2, 1
+                                     action_f64=f64, discount_factor=discount_factor,
+                                     trajectory_length=trajectory_length)
+        self.speed0 = self.env.params.speed0_pcontrol if not self.env.unsteppable else None
         self._state = None
 
     def reset(self):
         obs = self.env.reset()
-        return obs[0].double().cpu().numpy()
+        return None if obs is None else obs[0].double().cpu().numpy()
+
+    def augment_action(self, actions):
+        return augment_action(self.flight_phase, actions, self.speed0)
 
     def step(self, action):
+        self.env._check_steppable()
         if isinstance(action, torch.Tensor):
             a = action.detach()
         else:
             a = torch.as_tensor(np.asarray(action))
-        a = a.reshape(-1)[:1].reshape(1, 1)
+        a = a.reshape(-1)[:self.action_dim].reshape(1, self.action_dim).to(self.env.device)
+        if self.flight_phase in ("landing_burn", "landing_burn_pure_throttle_Pcontrol"):
+            a = self.augment_action(a)
         obs, r, d, tr, ex = self.env.step(a, info=True)
         state = self.env.state[0].cpu().numpy()
         self._tid = int(ex["trunc_id"][0])

@@ -29,7 +29,7 @@ def test_struct_layout_and_abi():
     import pdenv
     from pdenv import _lib
     L = pdenv.load()
-    assert L.pd_abi_version() == 1
+    assert L.pd_abi_version() == 2
     assert L.pd_sizeof_params() == C.sizeof(_lib.PdParams)
     assert L.pd_sizeof_config() == C.sizeof(_lib.PdConfig)
 
@@ -60,3 +60,37 @@ def test_params_pack_consistency():
         k = int(k)
         tot = sum((k >> (12 * c + 6)) & 63 for c in range(5))
         assert tot == 50
+
+
+def test_phase_pairs_the_reference_cannot_step():
+    """landing_burn_ACS, RL flip-over and PSO outside the landing burns construct (no GPU needed)
+    and raise TypeError at step(), as the reference's envs do; PSO + Pcontrol/ACS fails the
+    reference's compile_rtd_pso assertion at construction."""
+    import pdenv
+    for phase, mode in (("landing_burn_ACS", "rl"), ("flip_over_boostbackburn", "rl"), ("subsonic", "pso"),
+                        ("ballistic_arc_descent", "pso")):
+        env = pdenv.PoweredDescentEnv(4, phase, mode=mode)
+        assert env.reset() is None
+        with pytest.raises(TypeError):
+            env.step(None)
+    with pytest.raises(AssertionError):
+        pdenv.PoweredDescentEnv(4, "landing_burn_pure_throttle_Pcontrol", mode="pso")
+    from pdenv.wrappers import rl_wrapped_env_pytorch
+    w = rl_wrapped_env_pytorch("landing_burn_ACS", trajectory_length=100, discount_factor=0.99)
+    assert (w.state_dim, w.action_dim) == (5, 3)
+    with pytest.raises(TypeError):
+        w.step([0.0, 0.0, 0.0])
+
+
+def test_params_phases():
+    """The other phases' constants from the pack (tools/make_param_pack.py "phases")."""
+    import numpy as np
+    import pdenv
+    p = pdenv.Params()
+    s = p.struct
+    assert s.n_engines_stage1 == 42 and s.n_ref == 864
+    assert np.allclose(p.state0_of("subsonic")[:5], [0, 1.5, 0, 0, np.pi / 2])
+    assert np.allclose(p.state0_of("landing_burn_pure_throttle_Pcontrol"), p.state0)
+    ys = np.array(s.ref_y[:s.n_ref])
+    assert np.all(np.diff(ys) > 0)
+    assert abs(s.terminal_mach[1] - 4.11865) < 1e-4

@@ -1,0 +1,216 @@
+"""GPU parity for the flight phases besides the two landing burns and the RL
+reward of landing_burn, through the C ABI, against the fixtures made by importing the reference
+(tests/golden/ref_phases.npz), the reference's own recorded runs (recorded_phases.npz) and the
+CPU oracle.
+
+Tolerances (fp64 handle): teacher-forced step <= 1e-10 relative per channel, theta_dot 1e-9
+(1e-3 rad/s floor); rewards <= 1e-10 relative (1.0 floor); done/truncated/id exact;
+observations <= 1e-12 absolute; recorded open-loop runs <= 1e-10 of per-channel range.
+"""
+import math
+
+import numpy as np
+import pytest
+
+from conftest import golden
+
+pytestmark = pytest.mark.gpu
+
+ST = ["x", "y", "vx", "vy", "theta", "theta_dot", "gamma", "alpha", "mass", "mass_propellant", "time"]
+TAGS = {"pc": "landing_burn_pure_throttle_Pcontrol", "ba": "ballistic_arc_descent", "fl": "flip_over_boostbackburn",
+        "sub": "subsonic", "sup": "supersonic"}
+EP_TAGS = {"lb": "landing_burn", **{k: v for k, v in TAGS.items() if k != "fl"}}
+
+
+@pytest.fixture(scope="module")
+def pd():
+    import torch
+    import pdenv
+    assert torch.cuda.is_available(), "GPU tests need a HIP device"
+    return pdenv
+
+
+def rel_err(got, ref, floor=1e-3):
+    return np.abs(got - ref) / np.maximum(np.abs(ref), floor)
+
+
+@pytest.mark.parametrize("lpe", [2, 8])
+@pytest.mark.parametrize("tag", list(TAGS))
+def test_teacher_forced_physics(pd, tag, lpe):
+    """compile_physics(0.1, phase) from recorded states, float32 rows and float64 rows on two
+    handles (physics mode)."""
+    import torch
+    d = golden("ref_phases.npz")
+    S0, A, F, PV, SO = (d[f"{tag}_{k}"] for k in ("state_in", "action", "f32", "prev", "state_out"))
+    names = list(d["info_names"])
+    for f32 in (True, False):
+        rows = np.nonzero(F == f32)[0]
+        env = pd.PoweredDescentEnv(len(rows), TAGS[tag], mode="physics", action_f64=not f32, lanes_per_env=lpe)
+        env.set_state(torch.tensor(S0[rows]))
+        prev = PV[rows].astype(np.float32).astype(np.float64) if f32 else PV[rows]
+        env.set_actuators(torch.tensor(np.stack([prev, 0 * prev, 0 * prev], 1)))
+        a = torch.tensor(A[rows], dtype=torch.float32 if f32 else torch.float64)
+        obs, r, dn, tr, ex = env.step(a, info=True)
+        S = env.state.cpu().numpy()
+        err = rel_err(S, SO[rows]).max(0)
+        tol = np.full(11, 1e-10); tol[5] = 1e-9
+        assert (err < tol).all(), (tag, f32, dict(zip(ST, err)))
+        md = ex["mass_flow"].cpu().numpy()
+        ref_md = d[f"{tag}_info"][rows, names.index("mass_flow")]
+        assert np.abs(md - ref_md).max() <= 1e-15 * np.abs(ref_md).max(), (tag, f32, "mass flow")
+        if tag == "fl":
+            g = env.actuators.cpu().numpy()[:, 0]
+            ref_g = d[f"{tag}_info"][rows, names.index("gimbal_angle_deg")]
+            assert np.array_equal(g, ref_g), "flip-over gimbal low-pass (float32 array with float32 actions)"
+        assert not dn.any() and not tr.any() and float(r.abs().max()) == 0.0   # physics mode
+
+
+def _augment(tag, a, speed0):
+    a = np.asarray(a, np.float32)
+    if tag == "lb":
+        f = lambda u, c: math.copysign(math.log(1 + c * abs(u)) / math.log(1 + c), u)
+        return np.array([f(a[0], 10), a[1], f(a[2], 5), f(a[3], 5)]), False
+    if tag == "pc":
+        return ((a + np.float32(1)) / np.float32(2) * np.float32(speed0)).astype(np.float64), True
+    return a.astype(np.float64), True
+
+
+@pytest.mark.parametrize("k", [0, 1])
+@pytest.mark.parametrize("tag", list(EP_TAGS))
+def test_teacher_forced_rl_episode(pd, tag, k):
+    """rl_wrapped_env_pytorch episodes of the reference: one env per time step, each started
+    from the reference's previous state, g-load history and actuator memory; checks the next
+    state, the reward, done/truncated/id and the wrapper's observation."""
+    import torch
+    d = golden("ref_phases.npz")
+    p = f"ep_{tag}{k}_"
+    S, R, Dn, T, TI, OB, A = (d[p + n] for n in ("state", "reward", "done", "trunc", "trunc_id", "obs", "actions"))
+    n = len(R)
+    speed0 = pd.Params().speed0_pcontrol
+    aug = [_augment(tag, A[t], speed0) for t in range(n)]
+    f32 = aug[0][1]
+    env = pd.PoweredDescentEnv(n, EP_TAGS[tag], mode="rl", action_f64=not f32, discount_factor=0.99,
+                               trajectory_length=100)
+    s0 = pd.Params().state0_of(EP_TAGS[tag])
+    allS = np.vstack([s0[None], S])
+    v = np.hypot(allS[:, 2], allS[:, 3])
+    g = np.abs(np.diff(v)) / 0.1 / 9.81
+    win = np.zeros((n, 10)); ln = np.zeros(n, np.uint8)
+    for t in range(n):
+        w = g[max(0, t - 9):t]
+        win[t, :len(w)] = w; ln[t] = len(w)
+    env.set_state(torch.tensor(allS[:n]))
+    env.set_gload_window(v[:n], win, ln)
+    if tag == "lb":   # actuator memory: the previous step's filtered gimbal and fin commands (oracle replay)
+        import oracle as O
+        o = O.Oracle(phase=O.LANDING_BURN, rtd=O.RTD_NONE)
+        prevs = [(0.0, 0.0, 0.0)]
+        for t in range(n - 1):
+            _, info = o.physics(allS[t], aug[t][0], f32=False, prevs=prevs[-1])
+            prevs.append((info["gimbal_angle_deg"], info["delta_command_left_rad"], info["delta_command_right_rad"]))
+        env.set_actuators(torch.tensor(np.array(prevs)))
+    acts = torch.tensor(np.array([a for a, _ in aug]), dtype=torch.float32 if f32 else torch.float64)
+    obs, r, dn, tr, ex = env.step(acts)
+    Sg = env.state.cpu().numpy()
+    err = rel_err(Sg, S).max(0)
+    tol = np.full(11, 1e-10); tol[5] = 1e-9
+    assert (err < tol).all(), dict(zip(ST, err))
+    r = r.cpu().numpy()
+    assert (np.abs(r - R) <= 1e-10 * np.maximum(1.0, np.abs(R))).all(), np.abs(r - R).max()
+    assert np.array_equal(dn.cpu().numpy(), Dn) and np.array_equal(tr.cpu().numpy(), T)
+    assert np.array_equal(ex["trunc_id"].cpu().numpy(), TI)
+    assert np.abs(obs.cpu().numpy() - OB).max() < 1e-12
+
+
+@pytest.mark.parametrize("tag,phase,skip", [("fl", "flip_over_boostbackburn", []), ("sub", "subsonic", [6]),
+                                            ("sup", "supersonic", [])])
+def test_recorded_runs_open_loop(pd, tag, phase, skip):
+    """The reference's recorded classical-controller run of the phase, replayed open loop on
+    the GPU with its float64 controls (the subsonic CSV's gamma column holds degrees)."""
+    import torch
+    d = golden("recorded_phases.npz")
+    S, U = d[f"{tag}_state"], d[f"{tag}_u"]
+    env = pd.PoweredDescentEnv(1, phase, mode="physics", action_f64=True)
+    got = []
+    for t in range(len(S)):
+        env.step(torch.tensor(U[t][None], dtype=torch.float64))
+        got.append(env.state.cpu().numpy()[0])
+    got = np.array(got)
+    err = np.abs(got - S).max(0) / (S.max(0) - S.min(0) + 1e-300)
+    err[skip] = 0
+    assert err.max() < 1e-10, dict(zip(ST, err))
+
+
+@pytest.mark.parametrize("phase", ["landing_burn_pure_throttle_Pcontrol", "ballistic_arc_descent", "subsonic",
+                                   "supersonic", "landing_burn"])
+def test_batch_vs_oracle_rl(pd, phase, oracle_mod):
+    """256 envs x 40 steps of random float32 (float64 for landing_burn) actions with auto-reset,
+    against the oracle env by env: state, reward and flags each step (free-running: attitude
+    tolerances grow with the chaos, see inside)."""
+    import torch
+    O = oracle_mod
+    ph = {"landing_burn_pure_throttle_Pcontrol": O.PCONTROL, "ballistic_arc_descent": O.BALLISTIC,
+          "subsonic": O.SUBSONIC, "supersonic": O.SUPERSONIC, "landing_burn": O.LANDING_BURN}[phase]
+    n, T = 256, 40
+    f64 = phase == "landing_burn"
+    env = pd.PoweredDescentEnv(n, phase, mode="rl", action_f64=f64, discount_factor=0.99, trajectory_length=100,
+                               auto_reset=True)
+    A_dim = env.action_dim
+    rng = np.random.default_rng(5)
+    acts = rng.uniform(-1, 1, (T, n, A_dim))
+    if phase == "landing_burn_pure_throttle_Pcontrol":
+        acts = rng.uniform(0, 1100, (T, n, A_dim))
+    if phase == "subsonic":
+        acts[..., 1] = rng.uniform(0.5, 1, (T, n))
+    acts = acts if f64 else acts.astype(np.float32)
+    orcs = [O.Oracle(phase=ph, rtd=O.RTD_RL, discount_factor=0.99, trajectory_length=100) for _ in range(8)]
+    idx = np.linspace(0, n - 1, 8).astype(int)
+    for t in range(T):
+        obs, r, dn, tr, ex = env.step(torch.tensor(acts[t]))
+        S = env.state.cpu().numpy()
+        r = r.cpu().numpy()
+        for o, i in zip(orcs, idx):
+            s, rr, d_, tr_, tid, ob, info = o.step(acts[t, i].astype(np.float64), f32=not f64)
+            assert (bool(dn[i]), bool(tr[i])) == (d_, tr_), (phase, t, i)
+            assert abs(r[i] - rr) <= 1e-9 * max(1.0, abs(rr)), (phase, t, i, r[i], rr)
+            assert np.abs(obs.cpu().numpy()[i] - ob).max() < 1e-9
+            if d_ or tr_:
+                o.reset()
+            else:
+                e = rel_err(S[i], s)
+                # free-running 40 steps: the attitude channels are chaotic, last-ulp
+                # differences of the device transcendentals grow; the per-step bar is above
+                tol = np.full(11, 1e-8); tol[[4, 6, 7]] = 1e-6; tol[5] = 1e-4
+                assert (e < tol).all(), (phase, t, i, dict(zip(ST, e)))
+
+
+def test_flip_over_physics_rollout_vs_oracle(pd, oracle_mod):
+    """Flip-over stepping (physics mode, the only one the reference can run) with float32
+    actions: gimbal memory carried between steps as base_environment.py:110 does."""
+    import torch
+    O = oracle_mod
+    n, T = 128, 60
+    env = pd.PoweredDescentEnv(n, "flip_over_boostbackburn", mode="physics")
+    rng = np.random.default_rng(9)
+    acts = rng.uniform(-1, 1, (T, n, 1)).astype(np.float32)
+    o = O.Oracle(phase=O.FLIP, rtd=O.RTD_NONE)
+    i = 77
+    for t in range(T):
+        env.step(torch.tensor(acts[t]))
+        s, *_ = o.step(acts[t, i].astype(np.float64), f32=True)
+    e = rel_err(env.state.cpu().numpy()[i], s)
+    assert e.max() < 1e-9, dict(zip(ST, e))
+    assert env.actuators.cpu().numpy()[i, 0] == pytest.approx(o.E.gimbal_prev, abs=0)
+
+
+def test_rl_wrapper_facades(pd):
+    """rl_wrapped_env_pytorch for the new phases returns the reference's types and dims."""
+    from pdenv.wrappers import rl_wrapped_env_pytorch
+    for phase, (sd, ad) in (("landing_burn", (5, 4)), ("landing_burn_pure_throttle_Pcontrol", (1, 1)),
+                            ("ballistic_arc_descent", (4, 1)), ("subsonic", (8, 2)), ("supersonic", (8, 2))):
+        w = rl_wrapped_env_pytorch(phase, trajectory_length=100, discount_factor=0.99)
+        o = w.reset()
+        assert (w.state_dim, w.action_dim) == (sd, ad) and o.shape == (sd,)
+        obs, r, d, tr, info = w.step(np.zeros(ad, np.float32))
+        assert obs.shape == (sd,) and isinstance(r, float) and isinstance(d, bool) and isinstance(tr, bool)
+        assert isinstance(w.truncation_id(), int)
