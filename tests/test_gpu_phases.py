@@ -172,7 +172,10 @@ def test_batch_vs_oracle_rl(pd, phase, oracle_mod):
         for o, i in zip(orcs, idx):
             s, rr, d_, tr_, tid, ob, info = o.step(acts[t, i].astype(np.float64), f32=not f64)
             assert (bool(dn[i]), bool(tr[i])) == (d_, tr_), (phase, t, i)
-            assert abs(r[i] - rr) <= 1e-9 * max(1.0, abs(rr)), (phase, t, i, r[i], rr)
+            # landing_burn's reward reads x, vx and theta (rtd_rl.py:243-269), the free-running
+            # chaotic channels held to 1e-6 below; the other phases' rewards read y/v/mass only
+            rtol = 1e-6 if phase == "landing_burn" else 1e-9
+            assert abs(r[i] - rr) <= rtol * max(1.0, abs(rr)), (phase, t, i, r[i], rr)
             assert np.abs(obs.cpu().numpy()[i] - ob).max() < 1e-4    # steep tanh of the chaotic attitude (obs 2-4 of landing_burn)
             if d_ or tr_:
                 o.reset()

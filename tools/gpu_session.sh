@@ -16,8 +16,8 @@ stage() {  # name, seconds, command...
 STAGES=${STAGES:-"tests smoke bench prof"}
 for s in $STAGES; do
   case $s in
-    tests) stage gpu_tests 900 python -m pytest tests/ -m gpu -x -q ;;
-    testsall) stage gpu_tests 900 python -m pytest tests/ -m gpu -q ;;
+    tests) stage gpu_tests 900 python -u -m pytest tests/ -m gpu -x -q --timeout 120 --timeout-method thread ;;
+    testsall) stage gpu_tests 900 python -u -m pytest tests/ -m gpu -q --timeout 120 --timeout-method thread ;;
     smoke) stage smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) stage bench 600 python bench.py ;;
     bench32) stage bench32 600 python bench.py --precision f32 ;;
