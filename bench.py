@@ -35,6 +35,25 @@ def algorithmic_bytes(precision, phase, wind, obs_dim, act_dim):
     return rd + wr
 
 
+def valu_roofline(mix, kern_avg_ms, simds=1024, clock_hz=2.4e9, fp64_peak_tflops=78.6):
+    """The bound that actually limits k_step: vector-ALU issue.  `mix` is the
+    per-launch instruction mix of the same workload from rocprofv3 PMC passes
+    (profiles/pmc_traffic.json); the launch time is the one measured live.  Issue model of a
+    SIMD-32 (MI355X guide): a wave64 VALU instruction occupies 2 cycles, a binary64 one 4."""
+    f64 = sum(mix.get(f"SQ_INSTS_VALU_{k}_F64", 0.0) for k in ("ADD", "MUL", "FMA", "TRANS"))
+    valu = mix["SQ_INSTS_VALU"]
+    issue_cycles = 4.0 * f64 + 2.0 * (valu - f64)
+    sec = kern_avg_ms * 1e-3
+    flop = 64.0 * (mix.get("SQ_INSTS_VALU_ADD_F64", 0.0) + mix.get("SQ_INSTS_VALU_MUL_F64", 0.0)
+                   + mix.get("SQ_INSTS_VALU_TRANS_F64", 0.0) + 2.0 * mix.get("SQ_INSTS_VALU_FMA_F64", 0.0))
+    return {"bound": "valu", "achieved": issue_cycles / sec / 1e12, "peak": simds * clock_hz / 1e12,
+            "unit": "T SIMD-issue-cycles/s", "frac": issue_cycles / (simds * clock_hz * sec),
+            "valu_insts_per_launch": valu, "f64_insts_per_launch": f64,
+            "fp64_tflops": flop / sec / 1e12, "fp64_peak_tflops": fp64_peak_tflops,
+            "waves_per_launch": mix.get("SQ_WAVES"),
+            "source": "profiles/pmc_traffic.json f64_valu_mix_per_launch (rocprofv3 --pmc, 2 passes)"}
+
+
 def shard_offset(rank, n_per_rank):
     """Global index of a rank's first env: contiguous shards, disjoint Philox streams."""
     return rank * n_per_rank
@@ -248,10 +267,13 @@ def main():
     bpe = algorithmic_bytes(args.precision, args.phase, wind, main_res["obs_dim"], main_res["act_dim"])
     achieved = bpe * main_res["n"] / (main_res["kern_avg_ms"] * 1e-3) / 1e9
     traffic = None
+    mix = None
     pmc = os.path.join(REPO, "profiles", "pmc_traffic.json")
     if os.path.exists(pmc):
         try:
-            traffic = json.load(open(pmc)).get(f"{args.precision}_bytes_per_launch")
+            summ = json.load(open(pmc))
+            traffic = summ.get(f"{args.precision}_bytes_per_launch")
+            mix = summ.get("f64_valu_mix_per_launch") if args.precision == "f64" else None
         except Exception:
             traffic = None
     out = {
@@ -276,6 +298,8 @@ def main():
                      "note": "VALU/transcendental-bound elementwise ODE (no MFMA); see DESIGN.md"},
         "rbf_table_misses": main_res["counters"]["rbf_misses"],
     }
+    if mix and args.envs == 65536 and args.phase == "landing_burn_pure_throttle" and not args.no_wind:
+        out["valu_roofline"] = valu_roofline(mix, main_res["kern_avg_ms"])
     if other is not None:
         op = "f32" if args.precision == "f64" else "f64"
         out["secondary"] = {"dtype": op, "value": whole_job_rate(other["n"], world, args.steps, other["wall"]),

@@ -38,6 +38,12 @@ pd_status fail(pd_status s, const std::string& m) { g_err = m; return s; }
     } while (0)
 
 constexpr int kBlock = 256;
+// k_step workgroup: its LDS tables (~63 KB) are shared by all its waves, so the size sets how
+// many waves per SIMD the LDS admits (two workgroups per CU)
+#ifndef PD_STEP_BLOCK
+#define PD_STEP_BLOCK 256
+#endif
+constexpr int kStepBlock = PD_STEP_BLOCK;
 constexpr int kScratch = kSys * kSys + kSys + 3 * kNbr + kPay;   // doubles per wave
 constexpr int kPendingCap = 1024;
 constexpr int kGridExact = 1 << 30;   // grid_slot flag: every point of the cell has its key
@@ -225,7 +231,10 @@ __device__ __forceinline__ R rbf_eval(const R* __restrict__ pay, const R* smach,
                                       int part, int nparts) {
     const uint8_t* ib = (const uint8_t*)(pay + kPayIdx);
     R s0 = R(0), s1 = R(0);
-    constexpr int kChunk = 10;
+#ifndef PD_CHUNK
+#define PD_CHUNK 10
+#endif
+    constexpr int kChunk = PD_CHUNK;
 #pragma unroll 1
     for (int j0 = part; j0 < kNbr; j0 += kChunk * nparts) {
         R mm[kChunk], aa[kChunk], pp[kChunk];
@@ -590,13 +599,13 @@ template <typename R, int PHASE, int RTD, bool WIND, int LPE, int POL = 0>
 #ifndef PD_WPE
 #define PD_WPE 2
 #endif
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PD_WPE))) void k_step(StepArgs<R> a) {
+__global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_WPE))) void k_step(StepArgs<R> a) {
     using L = Lds<WIND>;
     __shared__ R lds[L::kTotal];
     __shared__ LineLds<R> lines;
     __shared__ SolveLds solve;
     const DevParams<R>& P = *a.P;
-    for (int t = threadIdx.x; t < 256; t += kBlock) {
+    for (int t = threadIdx.x; t < 256; t += kStepBlock) {
         lds[L::kCd + t] = P.cd_mach[t]; lds[L::kCl + t] = P.cl_mach[t];
         lds[L::kCdA + t] = P.cd_pt_aoa[t]; lds[L::kClA + t] = P.cl_pt_aoa[t];
     }
@@ -605,24 +614,24 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PD_WPE))
         lds[L::kCnX + threadIdx.x] = P.cn_x[threadIdx.x]; lds[L::kCnY + threadIdx.x] = P.cn_y[threadIdx.x];
     }
     if constexpr (WIND) {
-        for (int t = threadIdx.x; t < 800; t += kBlock) {
+        for (int t = threadIdx.x; t < 800; t += kStepBlock) {
             lds[L::kWAlt + t] = (&P.wind_alt_km[0][0])[t];
             lds[L::kWSp + t] = (&P.wind_speed[0][0])[t];
         }
     }
-    for (int t = threadIdx.x; t < 4 * kLineMax; t += kBlock) (&lines.bp[0][0])[t] = (&P.line_bp[0][0])[t];
-    for (int t = threadIdx.x; t < 4 * (kLineMax + 1); t += kBlock) {
+    for (int t = threadIdx.x; t < 4 * kLineMax; t += kStepBlock) (&lines.bp[0][0])[t] = (&P.line_bp[0][0])[t];
+    for (int t = threadIdx.x; t < 4 * (kLineMax + 1); t += kStepBlock) {
         (&lines.slot[0][0])[t] = (&P.line_slot[0][0])[t];
         (&lines.key[0][0])[t] = (&P.line_key[0][0])[t];
     }
     if (threadIdx.x < 4) { lines.a[threadIdx.x] = P.line_a[threadIdx.x]; lines.nbp[threadIdx.x] = P.line_nbp[threadIdx.x]; }
     if (threadIdx.x == 0) solve.lock = 0;
-    for (int t = threadIdx.x; t < kLogCells; t += kBlock) {
+    for (int t = threadIdx.x; t < kLogCells; t += kStepBlock) {
         s_logtab[t] = P.logtab.invc[t]; s_logtab[kLogCells + t] = P.logtab.logc[t];
     }
     __syncthreads();
     const int64_t N = a.n;
-    const int64_t gt = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const int64_t gt = (int64_t)blockIdx.x * kStepBlock + threadIdx.x;
     // every lane stays active (the cooperative miss solve needs converged waves): lanes past
     // the end recompute the last env and write nothing
     const bool valid = gt / LPE < N;
@@ -1706,8 +1715,8 @@ template <typename R> pd_status create_impl(const pd_params* p, const pd_config*
 }
 
 template <typename R, int PH, int RT, bool W, int LPE> void launch_step(const StepArgs<R>& a, hipStream_t s) {
-    unsigned grid = (unsigned)((a.n * LPE + kBlock - 1) / kBlock);
-    hipLaunchKernelGGL((k_step<R, PH, RT, W, LPE>), dim3(grid), dim3(kBlock), 0, s, a);
+    unsigned grid = (unsigned)((a.n * LPE + kStepBlock - 1) / kStepBlock);
+    hipLaunchKernelGGL((k_step<R, PH, RT, W, LPE>), dim3(grid), dim3(kStepBlock), 0, s, a);
 }
 
 template <typename R, int PH, int RT, bool W> void launch_lpe(int lpe, const StepArgs<R>& a, hipStream_t s) {
@@ -1731,8 +1740,8 @@ template <typename R> void dispatch_step(const pd_env* e, const StepArgs<R>& a, 
 }
 
 template <typename R, int PH, bool W, int LPE> void launch_policy_lpe(const StepArgs<R>& a, hipStream_t s) {
-    unsigned grid = (unsigned)((a.n * LPE + kBlock - 1) / kBlock);
-    hipLaunchKernelGGL((k_step<R, PH, 1, W, LPE, 1>), dim3(grid), dim3(kBlock), 0, s, a);
+    unsigned grid = (unsigned)((a.n * LPE + kStepBlock - 1) / kStepBlock);
+    hipLaunchKernelGGL((k_step<R, PH, 1, W, LPE, 1>), dim3(grid), dim3(kStepBlock), 0, s, a);
 }
 template <typename R, int PH, bool W> void launch_policy(const StepArgs<R>& a, int lpe, hipStream_t s) {
     if (lpe >= 8) launch_policy_lpe<R, PH, W, 8>(a, s);

@@ -69,6 +69,14 @@ def main(tag="r01"):
     if os.path.exists(vp):
         v, n = per_launch(vp)
         summary["f64_pmc_per_launch"] = v
+    # instruction mix of k_step (stage pmcmix: two passes, <= 8 SQ counters each)
+    mix = {}
+    for d in ("pmc_mix", "pmc_mix2"):
+        p = os.path.join(OUT, d, "run_counter_collection.csv")
+        if os.path.exists(p):
+            mix.update(per_launch(p)[0])
+    if mix:
+        summary["f64_valu_mix_per_launch"] = mix
     for extra in ("pmc_f64ops",):
         p = os.path.join(OUT, extra, "run_counter_collection.csv")
         if os.path.exists(p):
