@@ -181,8 +181,11 @@ pd_status pd_rollout(pd_env* env, const void* actions, int32_t n_steps, void* re
  *  weights : [n_params][N] float32, parameter-major (named_parameters() order per particle)
  *  n_params: PD_ACTOR_PARAMS_* for the handle's phase; the handle must have rtd = PD_RTD_PSO
  *  fitness : [N] (handle precision); steps: [N] int32 episode lengths (may be NULL)
- *  check_every: >0 = read the finished-env count every that many steps and stop early when all
- *            envs are done (one host sync per check); 0 = always run max_steps launches. */
+ *  check_every: >0 = read the live-env count every that many steps, stop early when all envs
+ *            are done, and size later launches to the live count (one host sync per check);
+ *            0 = always max_steps launches over the full grid.
+ * Each launch steps only the live envs: a compacted index list, rebuilt inside the step kernel
+ * (wave ballot + prefix count, one atomic per wave), so finished particles cost nothing. */
 pd_status pd_rollout_policy(pd_env* env, const float* weights, int32_t n_params, int32_t max_steps,
                             void* fitness, int32_t* steps, int32_t check_every, void* stream);
 /* One PSO generation's particle update on the device (particle_swarm_optimisation.py:437-441

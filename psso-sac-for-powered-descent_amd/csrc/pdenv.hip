@@ -88,7 +88,13 @@ template <typename R> struct StepArgs {
     R* info;
     R* reward_sum;
     const float* policy_w;           // policy rollouts: actor parameters [P][N] float32
-    unsigned long long* n_done;      // policy rollouts: envs whose episode has ended
+    // policy rollouts: the live envs as a compacted index list; a launch steps list_in[0, *cnt_in)
+    // and appends the envs whose episode goes on to list_out (wave ballot + prefix count, one
+    // atomic per wave), then the next launch steps those only (triple-buffered counts: this
+    // launch also zeroes the count the launch after next appends to)
+    const int32_t* list_in; int32_t* list_out;
+    const uint32_t* cnt_in; uint32_t* cnt_out; uint32_t* cnt_zero;
+    int use_list;   // step list_in (else all N envs, finished ones skipped by their fin flag)
     double dt_aux;                   // physics dt of phases 2..6 (compile_physics(dt, phase))
     int rtd_none;                    // PD_RTD_NONE: physics stepping only (reward/done/trunc 0)
 };
@@ -605,6 +611,16 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
     __shared__ LineLds<R> lines;
     __shared__ SolveLds solve;
     const DevParams<R>& P = *a.P;
+    // envs this launch steps: all N, or (POL) the compacted live list; a workgroup past its end
+    // leaves before staging the tables (workgroup-uniform)
+    int64_t n_act = a.n;
+    if constexpr (POL) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) *a.cnt_zero = 0u;
+        if (a.use_list) {
+            n_act = (int64_t)*a.cnt_in;
+            if ((int64_t)blockIdx.x * (kStepBlock / LPE) >= n_act) return;
+        }
+    }
     for (int t = threadIdx.x; t < 256; t += kStepBlock) {
         lds[L::kCd + t] = P.cd_mach[t]; lds[L::kCl + t] = P.cl_mach[t];
         lds[L::kCdA + t] = P.cd_pt_aoa[t]; lds[L::kClA + t] = P.cl_pt_aoa[t];
@@ -634,16 +650,19 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
     const int64_t gt = (int64_t)blockIdx.x * kStepBlock + threadIdx.x;
     // every lane stays active (the cooperative miss solve needs converged waves): lanes past
     // the end recompute the last env and write nothing
-    const bool valid = gt / LPE < N;
-    const int64_t i = valid ? gt / LPE : N - 1;
+    const bool valid = gt / LPE < n_act;
+    const int64_t e_act = valid ? gt / LPE : n_act - 1;
+    const int64_t i = (POL && a.use_list) ? (int64_t)a.list_in[e_act] : e_act;
     const int role = (int)(gt % LPE);
     const uint32_t ui = (uint32_t)i;   // N <= 2^25 (validated): 32-bit per-lane byte offsets
-    // POL (policy rollout): envs whose episode ended stay frozen; a wave with none left exits
-    // (wave-uniform, after the only workgroup barrier)
+    // POL (policy rollout): with the list, only live envs are stepped; without it, finished
+    // envs stay frozen and a wave with none left exits (wave-uniform, after the only barrier)
     bool live_ = valid;
     if constexpr (POL) {
-        live_ = live_ && ev(a.b.fin, ui) == 0;
-        if (__ballot(live_) == 0) return;
+        if (!a.use_list) {
+            live_ = live_ && ev(a.b.fin, ui) == 0;
+            if (__ballot(live_) == 0) return;
+        }
     }
     const bool live = live_;
     // role -> (table, part): LPE 1: both tables on one lane; else table = role / (LPE/2)
@@ -1177,7 +1196,7 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
         if constexpr (POL) {
             // objective_function: episode_reward -= reward until done or truncated (env_wrapped_ea.py:200-222)
             ev(a.reward_sum, ui_out) -= rew;
-            if (dn || tr) { ev(a.b.fin, ui_out) = 1; atomicAdd(a.n_done, 1ull); }
+            if (dn || tr) ev(a.b.fin, ui_out) = 1;
         } else if (a.reward_sum) {
             ev(a.reward_sum, ui_out) += rew;
         }
@@ -1198,6 +1217,21 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
             if constexpr (WIND) {
                 ev(a.b.wind, ui_out) = fu0; ev(a.b.wind + N, ui_out) = fu1; ev(a.b.wind + (2) * N, ui_out) = fv0; ev(a.b.wind + (3) * N, ui_out) = fv1;
             }
+        }
+    }
+    if constexpr (POL) {
+        // done-mask compaction: the envs whose episode goes on, in lane order, appended to the
+        // next launch's list at a base taken by one atomic per wave (the count also tells the
+        // host when every episode has ended)
+        const bool cont = role == 0 && live && !(dn || tr);
+        const unsigned long long m = __ballot(cont);
+        if (m) {
+            const int lane = (int)__lane_id();
+            const int leader = __ffsll((long long)m) - 1;
+            uint32_t base = 0;
+            if (lane == leader) base = atomicAdd(a.cnt_out, (uint32_t)__popcll(m));
+            base = (uint32_t)__shfl((int)base, leader);
+            if (cont) a.list_out[base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = (int32_t)i;
         }
     }
     // neighbourhood caches survive resets (any valid 50-set is a correct start)
@@ -1428,7 +1462,11 @@ struct pd_env {
     uint8_t *ghead = nullptr, *glen = nullptr, *wprof = nullptr;
     unsigned long long* key = nullptr; int* slot = nullptr;
     int8_t* tid = nullptr; uint32_t *epi = nullptr, *tstep = nullptr;
-    uint8_t* fin = nullptr; unsigned long long* n_done = nullptr;
+    uint8_t* fin = nullptr;
+    int32_t* live[2] = {nullptr, nullptr};   // policy rollouts: compacted live-env lists
+    uint32_t* live_cnt = nullptr;            // [3] their lengths (triple-buffered)
+    uint32_t* host_cnt = nullptr;            // [2] pinned host copies of checked lengths
+    hipEvent_t cnt_ev[2] = {nullptr, nullptr};
     Pending pend{};
     unsigned long long *keys_cd = nullptr, *keys_cl = nullptr;
     void *pay_cd = nullptr, *pay_cl = nullptr;
@@ -1471,7 +1509,6 @@ template <typename R> StepArgs<R> make_args(pd_env* e) {
     a.b.st = (R*)e->st; a.b.vprev = (R*)e->vprev; a.b.gwin = (R*)e->gwin; a.b.ghead = e->ghead; a.b.glen = e->glen;
     a.b.act = (R*)e->act; a.b.wind = (R*)e->wind; a.b.wprof = e->wprof; a.b.key = e->key; a.b.slot = e->slot;
     a.b.tid = e->tid; a.b.epi = e->epi; a.b.tstep = e->tstep; a.b.fin = e->fin;
-    a.n_done = e->n_done;
     a.pend = e->pend;
     a.n = e->cfg.n_envs;
     a.env_offset = e->cfg.env_offset;
@@ -1696,7 +1733,8 @@ template <typename R> pd_status create_impl(const pd_params* p, const pd_config*
         (st = dalloc(e, (void**)&e->key, 2 * N * 8)) || (st = dalloc(e, (void**)&e->slot, 2 * N * 4)) ||
         (st = dalloc(e, (void**)&e->tid, N)) || (st = dalloc(e, (void**)&e->epi, N * 4)) ||
         (st = dalloc(e, (void**)&e->tstep, N * 4)) || (st = dalloc(e, (void**)&e->fin, N)) ||
-        (st = dalloc(e, (void**)&e->n_done, 8)))
+        (st = dalloc(e, (void**)&e->live[0], N * 4)) ||
+        (st = dalloc(e, (void**)&e->live[1], N * 4)) || (st = dalloc(e, (void**)&e->live_cnt, 3 * 4)))
         return st;
     PD_HIP(hipMemset(e->gwin, 0, 10 * N * R_));
     PD_HIP(hipMemset(e->epi, 0xff, N * 4));   // first reset -> episode 0
@@ -1739,14 +1777,15 @@ template <typename R> void dispatch_step(const pd_env* e, const StepArgs<R>& a, 
     else { if (w) launch_lpe<R, 2, 0, true>(l, a, s); else launch_lpe<R, 2, 0, false>(l, a, s); }
 }
 
-template <typename R, int PH, bool W, int LPE> void launch_policy_lpe(const StepArgs<R>& a, hipStream_t s) {
-    unsigned grid = (unsigned)((a.n * LPE + kStepBlock - 1) / kStepBlock);
+template <typename R, int PH, bool W, int LPE> void launch_policy_lpe(const StepArgs<R>& a, int64_t n_launch,
+                                                                      hipStream_t s) {
+    unsigned grid = (unsigned)((n_launch * LPE + kStepBlock - 1) / kStepBlock);
     hipLaunchKernelGGL((k_step<R, PH, 1, W, LPE, 1>), dim3(grid), dim3(kStepBlock), 0, s, a);
 }
-template <typename R, int PH, bool W> void launch_policy(const StepArgs<R>& a, int lpe, hipStream_t s) {
-    if (lpe >= 8) launch_policy_lpe<R, PH, W, 8>(a, s);
-    else if (lpe == 4) launch_policy_lpe<R, PH, W, 4>(a, s);
-    else launch_policy_lpe<R, PH, W, 2>(a, s);
+template <typename R, int PH, bool W> void launch_policy(const StepArgs<R>& a, int lpe, int64_t n_launch, hipStream_t s) {
+    if (lpe >= 8) launch_policy_lpe<R, PH, W, 8>(a, n_launch, s);
+    else if (lpe == 4) launch_policy_lpe<R, PH, W, 4>(a, n_launch, s);
+    else launch_policy_lpe<R, PH, W, 2>(a, n_launch, s);
 }
 
 template <typename R> void launch_insert(pd_env* e, hipStream_t s) {
@@ -1765,6 +1804,13 @@ pd_status step_impl(pd_env* e, const void* actions, void* obs, void* reward, uin
     return PD_OK;
 }
 
+// policy rollouts: every env live, in index order
+__global__ __launch_bounds__(kBlock) void k_live_init(int32_t* list, uint32_t* cnt, int64_t n) {
+    int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i < n) list[i] = (int32_t)i;
+    if (i < 3) cnt[i] = i == 0 ? (uint32_t)n : 0u;
+}
+
 template <typename R>
 pd_status rollout_policy_impl(pd_env* e, const float* w, int32_t max_steps, void* fitness, int32_t* steps,
                               int32_t check_every, hipStream_t s) {
@@ -1772,20 +1818,47 @@ pd_status rollout_policy_impl(pd_env* e, const float* w, int32_t max_steps, void
     unsigned grid = (unsigned)((N + kBlock - 1) / kBlock);
     hipLaunchKernelGGL(k_reset<R>, dim3(grid), dim3(kBlock), 0, s, make_args<R>(e), (const uint8_t*)nullptr);
     PD_HIP(hipMemsetAsync(fitness, 0, (size_t)N * sizeof(R), s));
-    PD_HIP(hipMemsetAsync(e->n_done, 0, 8, s));
+    hipLaunchKernelGGL(k_live_init, dim3(grid), dim3(kBlock), 0, s, e->live[0], e->live_cnt, N);
     StepArgs<R> a = make_args<R>(e);
     a.policy_w = w; a.reward_sum = (R*)fitness; a.auto_reset = 0;
     const bool wind = e->cfg.enable_wind != 0;
+    // launch t steps live[t & 1][0, live_cnt[t % 3]) and appends the survivors to the other list;
+    // the grid covers the live count last read back (a workgroup past the device count leaves
+    // at once), so the launches shrink with the swarm's live envs.  Checks are one interval
+    // behind: at a check the count is copied to pinned memory under an event, and the host
+    // waits for the PREVIOUS check's event, with check_every launches still queued behind it
+    // (no bubble); at most 2 * check_every nearly empty launches run after the last episode.
+    if (check_every > 0 && !e->host_cnt) {
+        PD_HIP(hipHostMalloc((void**)&e->host_cnt, 2 * sizeof(uint32_t), hipHostMallocDefault));
+        for (hipEvent_t& ev : e->cnt_ev) PD_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    }
+    // The list pays off once the grid no longer fits the chip in one round (a launch then costs
+    // the rounds its waves need); below that the launch time is one wave's, and reading the
+    // state and actor weights through the list (gathers) only costs.  PDENV_COMPACT=0/1 forces.
+    int dev_cus = 256;
+    (void)hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, e->device);
+    const char* force = getenv("PDENV_COMPACT");
+    a.use_list = force && *force ? (atoi(force) != 0) : (N * e->lpe > (int64_t)dev_cus * 512);
+    int64_t n_launch = N;
+    int checks = 0;
     for (int32_t t = 0; t < max_steps; ++t) {
-        if (e->cfg.phase == PD_PHASE_PURE_THROTTLE) { if (wind) launch_policy<R, 0, true>(a, e->lpe, s); else launch_policy<R, 0, false>(a, e->lpe, s); }
-        else { if (wind) launch_policy<R, 1, true>(a, e->lpe, s); else launch_policy<R, 1, false>(a, e->lpe, s); }
+        a.list_in = e->live[t & 1]; a.list_out = e->live[(t + 1) & 1];
+        a.cnt_in = e->live_cnt + t % 3; a.cnt_out = e->live_cnt + (t + 1) % 3; a.cnt_zero = e->live_cnt + (t + 2) % 3;
+        if (e->cfg.phase == PD_PHASE_PURE_THROTTLE) { if (wind) launch_policy<R, 0, true>(a, e->lpe, n_launch, s); else launch_policy<R, 0, false>(a, e->lpe, n_launch, s); }
+        else { if (wind) launch_policy<R, 1, true>(a, e->lpe, n_launch, s); else launch_policy<R, 1, false>(a, e->lpe, n_launch, s); }
         PD_HIP(hipGetLastError());
         if ((t & 15) == 15) launch_insert<R>(e, s);
         if (check_every > 0 && (t + 1) % check_every == 0 && t + 1 < max_steps) {
-            unsigned long long done = 0;
-            PD_HIP(hipMemcpyAsync(&done, e->n_done, 8, hipMemcpyDeviceToHost, s));
-            PD_HIP(hipStreamSynchronize(s));
-            if ((int64_t)done >= N) break;
+            const int k = checks & 1;
+            PD_HIP(hipMemcpyAsync(e->host_cnt + k, e->live_cnt + (t + 1) % 3, 4, hipMemcpyDeviceToHost, s));
+            PD_HIP(hipEventRecord(e->cnt_ev[k], s));
+            if (checks > 0) {
+                PD_HIP(hipEventSynchronize(e->cnt_ev[k ^ 1]));
+                const uint32_t live = ((volatile uint32_t*)e->host_cnt)[k ^ 1];
+                if (live == 0) break;
+                if (a.use_list) n_launch = live;
+            }
+            ++checks;
         }
     }
     launch_insert<R>(e, s);
@@ -1842,6 +1915,8 @@ pd_status pd_destroy(pd_env* e) {
     if (!e) return PD_OK;
     (void)hipSetDevice(e->device);
     for (void* p : e->allocs) (void)hipFree(p);
+    if (e->host_cnt) (void)hipHostFree(e->host_cnt);
+    for (hipEvent_t ev : e->cnt_ev) if (ev) (void)hipEventDestroy(ev);
     delete e;
     return PD_OK;
 }

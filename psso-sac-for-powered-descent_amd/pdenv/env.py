@@ -228,7 +228,7 @@ class PoweredDescentEnv:
         L.check(self.lib.pd_set_wind_sigmas(self.h, _ptr(sig), _stream(self.device)))
         torch.cuda.current_stream(self.device).synchronize()
 
-    def rollout_policy(self, weights, max_steps=2200, check_every=64):
+    def rollout_policy(self, weights, max_steps=2200, check_every=8):
         """PSO objective of N particles on the device (pd_rollout_policy): every env is reset and
         driven by its own simple_actor until done/truncated or max_steps.
         weights: [N, P] per-particle parameter vectors (named_parameters() order).

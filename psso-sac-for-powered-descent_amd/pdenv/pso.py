@@ -104,7 +104,7 @@ class ParticleSubswarmOptimisationGPU:
         env = self._env_for(n)
         fit = torch.empty(n, dtype=env.dtype, device=self.device)
         steps = torch.empty(n, dtype=torch.int32, device=self.device)
-        L.check(self.lib.pd_rollout_policy(env.h, _ptr(x32), self.D, self.max_steps, _ptr(fit), _ptr(steps), 64,
+        L.check(self.lib.pd_rollout_policy(env.h, _ptr(x32), self.D, self.max_steps, _ptr(fit), _ptr(steps), 8,
                                            _stream(self.device)))
         return fit.double(), steps
 

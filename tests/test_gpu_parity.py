@@ -519,3 +519,29 @@ def test_sac_collector_graph_equals_eager(pd):
         bufs.append(buf)
     assert len(bufs[0]) == len(bufs[1]) == 40 * N
     assert torch.equal(bufs[0].data, bufs[1].data)
+
+
+def test_policy_rollout_compaction_invariant(pd, monkeypatch):
+    """Done-mask compaction: the live-env list is rebuilt inside every launch and, with the list
+    in use (PDENV_COMPACT=1; by default only for grids larger than one chip round), later
+    launches are sized to the live count read back every check_every steps.  Fitness, episode
+    lengths and final states must be bit-identical with and without the list and whatever the
+    check interval (0 = never), and equal to those of envs stepped in their own handle (the
+    order of the list is irrelevant)."""
+    import torch
+    rng = np.random.default_rng(77)
+    W = np.concatenate([rng.uniform(-1.5, 1.5, (700, 372)), rng.uniform(-0.3, 0.3, (324, 372))]).astype(np.float32)
+    env = make(pd, len(W), phase="landing_burn", mode="pso")
+    res = []
+    for force, ce in (("0", 8), ("1", 0), ("1", 1), ("1", 3), ("1", 8), ("1", 64), ("", 8)):
+        monkeypatch.setenv("PDENV_COMPACT", force)
+        fit, steps = env.rollout_policy(torch.tensor(W), max_steps=300, check_every=ce)
+        res.append((fit.cpu().numpy(), steps.cpu().numpy(), env.state.cpu().numpy()))
+    for f, s, S in res[1:]:
+        assert np.array_equal(f, res[0][0]) and np.array_equal(s, res[0][1]) and np.array_equal(S, res[0][2])
+    assert len(set(res[0][1].tolist())) > 5            # ragged episode lengths: compaction exercised
+    sub = np.arange(0, len(W), 97)
+    env2 = make(pd, len(sub), phase="landing_burn", mode="pso")
+    f2, s2 = env2.rollout_policy(torch.tensor(W[sub]), max_steps=300)
+    assert np.array_equal(s2.cpu().numpy(), res[0][1][sub])
+    np.testing.assert_allclose(f2.cpu().numpy(), res[0][0][sub], rtol=1e-12)
