@@ -107,6 +107,27 @@ template <typename T> __device__ __forceinline__ T& ev(T* base, uint32_t i) {
     return *(T*)((B*)base + (uint32_t)(i * (uint32_t)sizeof(T)));
 }
 
+// Streamed per-env fields of the step kernel: read once and written once per launch, so with
+// PD_NT they bypass the caches' retention (nontemporal) and leave L2 to the aero tables.
+template <typename T> __device__ __forceinline__ T ldv(const T* base, uint32_t i) {
+#ifdef PD_NT
+    return __builtin_nontemporal_load(&ev(base, i));
+#else
+    return ev(base, i);
+#endif
+}
+template <typename T> struct StRef {
+    T* p;
+    __device__ __forceinline__ void operator=(T v) const {
+#ifdef PD_NT
+        __builtin_nontemporal_store(v, p);
+#else
+        *p = v;
+#endif
+    }
+};
+template <typename T> __device__ __forceinline__ StRef<T> stv(T* base, uint32_t i) { return {&ev(base, i)}; }
+
 // ---------------------------------------------------------------- reset of one env
 template <typename R>
 __device__ void reset_env(const StepArgs<R>& a, int64_t i, uint32_t episode, bool reset_cache) {
@@ -241,7 +262,13 @@ __device__ __forceinline__ R rbf_eval(const R* __restrict__ pay, const R* smach,
 #define PD_CHUNK 10
 #endif
     constexpr int kChunk = PD_CHUNK;
+    // fully unrolled: the scheduler issues a later chunk's loads under an earlier chunk's
+    // arithmetic (c3 f64 0.089 -> 0.085 ms; tools/sweep.py, profiles/r01_experiments.json)
+#ifdef PD_RBF_NO_UNROLL
 #pragma unroll 1
+#else
+#pragma unroll
+#endif
     for (int j0 = part; j0 < kNbr; j0 += kChunk * nparts) {
         R mm[kChunk], aa[kChunk], pp[kChunk];
 #pragma unroll
@@ -675,25 +702,25 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
 
     R s[11];
 #pragma unroll
-    for (int k = 0; k < 11; ++k) s[k] = ev(a.b.st + (k) * N, ui);
+    for (int k = 0; k < 11; ++k) s[k] = ldv(a.b.st + (k) * N, ui);
     RbfCache<R> cA, cB;   // LPE 1: A = C_D, B = C_L; LPE >= 2: A = own table
-    cA.key = ev(a.b.key + (my_table) * N, ui); cA.slot = ev(a.b.slot + (my_table) * N, ui);
-    if constexpr (LPE == 1) { cB.key = ev(a.b.key + N, ui); cB.slot = ev(a.b.slot + N, ui); }
+    cA.key = ldv(a.b.key + (my_table) * N, ui); cA.slot = ldv(a.b.slot + (my_table) * N, ui);
+    if constexpr (LPE == 1) { cB.key = ldv(a.b.key + N, ui); cB.slot = ldv(a.b.slot + N, ui); }
     else { cB.key = 0; cB.slot = -1; }
     R gprev = R(0), dlprev = R(0), drprev = R(0);
-    if constexpr (PHASE == 1) { gprev = ev(a.b.act, ui); dlprev = ev(a.b.act + N, ui); drprev = ev(a.b.act + (2) * N, ui); }
+    if constexpr (PHASE == 1) { gprev = ldv(a.b.act, ui); dlprev = ldv(a.b.act + N, ui); drprev = ldv(a.b.act + (2) * N, ui); }
     // PHASE 2 = the other compile_physics phases, chosen at run time by P.phase (wave-uniform)
     const int aux = PHASE == 2 ? a.P->phase : PHASE;
     const bool ascent = PHASE == 2 && (aux == PD_PHASE_SUBSONIC || aux == PD_PHASE_SUPERSONIC);
-    if constexpr (PHASE == 2) gprev = ev(a.b.act, ui);   // flip-over gimbal memory
+    if constexpr (PHASE == 2) gprev = ldv(a.b.act, ui);   // flip-over gimbal memory
     R fu0 = R(0), fu1 = R(0), fv0 = R(0), fv1 = R(0), sgu = R(0), sgv = R(0);
     int prof = 0;
     if constexpr (WIND) {
-        fu0 = ev(a.b.wind, ui); fu1 = ev(a.b.wind + N, ui); fv0 = ev(a.b.wind + (2) * N, ui); fv1 = ev(a.b.wind + (3) * N, ui);
-        sgu = ev(a.b.wind + (4) * N, ui); sgv = ev(a.b.wind + (5) * N, ui);
-        prof = ev(a.b.wprof, ui);
+        fu0 = ldv(a.b.wind, ui); fu1 = ldv(a.b.wind + N, ui); fv0 = ldv(a.b.wind + (2) * N, ui); fv1 = ldv(a.b.wind + (3) * N, ui);
+        sgu = ldv(a.b.wind + (4) * N, ui); sgv = ldv(a.b.wind + (5) * N, ui);
+        prof = ldv(a.b.wprof, ui);
     }
-    const uint32_t ep = ev(a.b.epi, ui), ts = ev(a.b.tstep, ui);
+    const uint32_t ep = ldv(a.b.epi, ui), ts = ldv(a.b.tstep, ui);
     const uint64_t g = a.env_offset + (uint64_t)i;
 
     // actions (float32 unless act_f64)
@@ -717,10 +744,10 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
         }
     } else if (a.act_f64) {
 #pragma unroll
-        for (int k = 0; k < A; ++k) if (k < AD) ud[k] = ev((const double*)a.actions + k, ui * AD);
+        for (int k = 0; k < A; ++k) if (k < AD) ud[k] = ldv((const double*)a.actions + k, ui * AD);
     } else {
 #pragma unroll
-        for (int k = 0; k < A; ++k) if (k < AD) uf[k] = ev((const float*)a.actions + k, ui * AD);
+        for (int k = 0; k < A; ++k) if (k < AD) uf[k] = ldv((const float*)a.actions + k, ui * AD);
     }
 
     // pure throttle 4 x 0.025 s, landing_burn 4 x 0.1 s (actuators 0.025 s); the other phases
@@ -1019,16 +1046,16 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
     // ---- g-load window (base_environment.py:136-149): ring of 10, Python sum() from the oldest
     const DevParams<R>& P2 = *launder(a.P);
     R v = sqrt(s[2] * s[2] + s[3] * s[3]);
-    R vp = ev(a.b.vprev, ui);
+    R vp = ldv(a.b.vprev, ui);
     R gl_new = fabs(v - vp) / R(0.1) * R(1) / R(9.81);
-    int glen = ev(a.b.glen, ui), ghead = ev(a.b.ghead, ui);
+    int glen = ldv(a.b.glen, ui), ghead = ldv(a.b.ghead, ui);
     int wslot;
     if (glen < 10) { wslot = glen; glen += 1; }
     else { wslot = ghead; ghead = ghead == 9 ? 0 : ghead + 1; }
     R gsum = R(0);
     int idx = glen < 10 ? 0 : ghead;
     for (int k = 0; k < glen; ++k) {
-        gsum += idx == wslot ? gl_new : ev(a.b.gwin + (idx) * N, ui);
+        gsum += idx == wslot ? gl_new : ldv(a.b.gwin + (idx) * N, ui);
         idx = idx == 9 ? 0 : idx + 1;
     }
     R gl = gsum / R(10);
@@ -1192,30 +1219,30 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
             constexpr int kind = RTD == 1 ? (PHASE == 0 ? 1 : 2) : (PHASE == 0 ? 0 : (PHASE == 1 ? 3 : -1));
             obs_write<R>(P2, kind >= 0 ? kind : P2.obs_kind, s, a.obs, ui_out);
         }
-        if (a.reward) ev(a.reward, ui_out) = rew;
+        if (a.reward) stv(a.reward, ui_out) = rew;
         if constexpr (POL) {
             // objective_function: episode_reward -= reward until done or truncated (env_wrapped_ea.py:200-222)
             ev(a.reward_sum, ui_out) -= rew;
-            if (dn || tr) ev(a.b.fin, ui_out) = 1;
+            if (dn || tr) stv(a.b.fin, ui_out) = 1;
         } else if (a.reward_sum) {
             ev(a.reward_sum, ui_out) += rew;
         }
-        if (a.done) ev(a.done, ui_out) = (uint8_t)dn;
-        if (a.trunc) ev(a.trunc, ui_out) = (uint8_t)tr;
-        if (a.trunc_id) ev(a.trunc_id, ui_out) = (int8_t)id;
-        if (a.info) ev(a.info + (PD_INFO_GLOAD) * N, ui_out) = gl;
+        if (a.done) stv(a.done, ui_out) = (uint8_t)dn;
+        if (a.trunc) stv(a.trunc, ui_out) = (uint8_t)tr;
+        if (a.trunc_id) stv(a.trunc_id, ui_out) = (int8_t)id;
+        if (a.info) stv(a.info + (PD_INFO_GLOAD) * N, ui_out) = gl;
         if (ended) {
             reset_env(a, i, ep + 1, false);
         } else {
-            ev(a.b.vprev, ui_out) = v;
-            ev(a.b.gwin + (wslot) * N, ui_out) = gl_new;
-            ev(a.b.glen, ui_out) = (uint8_t)glen; ev(a.b.ghead, ui_out) = (uint8_t)ghead;
-            ev(a.b.tid, ui_out) = (int8_t)id;
-            ev(a.b.tstep, ui_out) = ts + 1;
-            if constexpr (PHASE == 1) { ev(a.b.act, ui_out) = gdeg_out; ev(a.b.act + N, ui_out) = dcmdl_out; ev(a.b.act + (2) * N, ui_out) = dcmdr_out; }
-            if constexpr (PHASE == 2) { if (aux == PD_PHASE_FLIP_OVER) ev(a.b.act, ui_out) = gdeg_out; }
+            stv(a.b.vprev, ui_out) = v;
+            stv(a.b.gwin + (wslot) * N, ui_out) = gl_new;
+            stv(a.b.glen, ui_out) = (uint8_t)glen; stv(a.b.ghead, ui_out) = (uint8_t)ghead;
+            stv(a.b.tid, ui_out) = (int8_t)id;
+            stv(a.b.tstep, ui_out) = ts + 1;
+            if constexpr (PHASE == 1) { stv(a.b.act, ui_out) = gdeg_out; stv(a.b.act + N, ui_out) = dcmdl_out; stv(a.b.act + (2) * N, ui_out) = dcmdr_out; }
+            if constexpr (PHASE == 2) { if (aux == PD_PHASE_FLIP_OVER) stv(a.b.act, ui_out) = gdeg_out; }
             if constexpr (WIND) {
-                ev(a.b.wind, ui_out) = fu0; ev(a.b.wind + N, ui_out) = fu1; ev(a.b.wind + (2) * N, ui_out) = fv0; ev(a.b.wind + (3) * N, ui_out) = fv1;
+                stv(a.b.wind, ui_out) = fu0; stv(a.b.wind + N, ui_out) = fu1; stv(a.b.wind + (2) * N, ui_out) = fv0; stv(a.b.wind + (3) * N, ui_out) = fv1;
             }
         }
     }
@@ -1236,13 +1263,13 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
     }
     // neighbourhood caches survive resets (any valid 50-set is a correct start)
     if (part == 0 && live) {
-        ev(a.b.key + (my_table) * N, ui_out) = cA.key; ev(a.b.slot + (my_table) * N, ui_out) = cA.slot;
-        if constexpr (LPE == 1) { ev(a.b.key + N, ui_out) = cB.key; ev(a.b.slot + N, ui_out) = cB.slot; }
+        stv(a.b.key + (my_table) * N, ui_out) = cA.key; stv(a.b.slot + (my_table) * N, ui_out) = cA.slot;
+        if constexpr (LPE == 1) { stv(a.b.key + N, ui_out) = cB.key; stv(a.b.slot + N, ui_out) = cB.slot; }
     }
     if (!ended && live) {
 #pragma unroll
         for (int k = 0; k < 11; ++k)
-            if (k % LPE == role) ev(a.b.st + (k) * N, ui_out) = s[k];
+            if (k % LPE == role) stv(a.b.st + (k) * N, ui_out) = s[k];
     }
 }
 
