@@ -620,6 +620,16 @@ __device__ __forceinline__ void actor_forward(const float* __restrict__ W, int64
     }
 }
 
+// PD_STAMP (diagnostic builds only): per-wave shader-clock sections of k_step, summed into
+// pend.stats[8..15] (staging, loads, pre-aero, aero tables, post-aero, rtd, outputs, waves)
+#ifdef PD_STAMP
+#define PD_T(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
+#define PD_ACC(k, d) acc_[k] += (d)
+#else
+#define PD_T(v)
+#define PD_ACC(k, d)
+#endif
+
 template <bool WIND> struct Lds {
     // table Mach values and, 512 further on, each point's AoA (tab_view relies on that offset)
     static constexpr int kCd = 0, kCl = 256, kCdA = 512, kClA = 768, kCaX = 1024, kCaY = 1088, kCnX = 1152,
@@ -634,6 +644,10 @@ template <typename R, int PHASE, int RTD, bool WIND, int LPE, int POL = 0>
 #endif
 __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_WPE))) void k_step(StepArgs<R> a) {
     using L = Lds<WIND>;
+#ifdef PD_STAMP
+    unsigned long long acc_[7] = {0, 0, 0, 0, 0, 0, 0};
+#endif
+    PD_T(t_start);
     __shared__ R lds[L::kTotal];
     __shared__ LineLds<R> lines;
     __shared__ SolveLds solve;
@@ -673,6 +687,8 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
         s_logtab[t] = P.logtab.invc[t]; s_logtab[kLogCells + t] = P.logtab.logc[t];
     }
     __syncthreads();
+    PD_T(t_staged);
+    PD_ACC(0, t_staged - t_start);
     const int64_t N = a.n;
     const int64_t gt = (int64_t)blockIdx.x * kStepBlock + threadIdx.x;
     // every lane stays active (the cooperative miss solve needs converged waves): lanes past
@@ -758,8 +774,11 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
     R gdeg_out = gprev, dcmdl_out = dlprev, dcmdr_out = drprev;
     bool nan_hit = false;
 
+    PD_T(t_loaded);
+    PD_ACC(1, t_loaded - t_staged);
 #pragma unroll 1
     for (int sub = 0; sub < NSUB; ++sub) {
+        PD_T(t_sub);
         const DevParams<R>& P = *launder(a.P);
         R x = s[0], y = s[1], vx = s[2], vy = s[3], th = s[4], thd = s[5], ga = s[6], al = s[7];
         R m = s[8], mp = s[9];
@@ -814,6 +833,8 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
         R Fwy = R(0.5) * rho * (vg * vg) * P.A_front * P.C_gust_y;
         R Mw = -d_cp_cg * Fwy;
         R CL = R(0), CD = R(0);
+        PD_T(t_aero0);
+        PD_ACC(2, t_aero0 - t_sub);
 #ifndef PD_EXP_NORBF
         {
             // evaluated convergently by every lane; results of lanes that need none (speed of
@@ -839,6 +860,8 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
             }
         }
 #endif
+        PD_T(t_aero1);
+        PD_ACC(3, t_aero1 - t_aero0);
         R drag = R(0.5) * rho * (speed * speed) * CD * P.A_front;
         R lift = R(0.5) * rho * (speed * speed) * CL * P.A_front;
         R sae = sin(ae), cae = cos(ae);
@@ -1035,6 +1058,8 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
         mp -= mdot_dt; m -= mdot_dt;
         s[0] = x; s[1] = y; s[2] = vx; s[3] = vy; s[4] = th; s[5] = thd; s[6] = ga; s[7] = al;
         s[8] = m; s[9] = mp; s[10] = s[10] + dt;
+        PD_T(t_subend);
+        PD_ACC(4, t_subend - t_aero1);
         if (sub == NSUB - 1 && a.info && role == 0 && live) {   // info of the last sub-step (rockets_physics.py:649-702)
             R vals[PD_N_INFO - 1] = {rho, patm, asnd, mach, q, CL, CD, md_info, x_cog, I, ae, thr_info, ug, vg, gdeg_out};
 #pragma unroll
@@ -1042,6 +1067,7 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
         }
     }
     if (nan_hit && role == 0 && live) atomicAdd(&a.pend.stats[1], 1ull);
+    PD_T(t_loop);
 
     // ---- g-load window (base_environment.py:136-149): ring of 10, Python sum() from the oldest
     const DevParams<R>& P2 = *launder(a.P);
@@ -1052,12 +1078,20 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
     int wslot;
     if (glen < 10) { wslot = glen; glen += 1; }
     else { wslot = ghead; ghead = ghead == 9 ? 0 : ghead + 1; }
-    R gsum = R(0);
-    int idx = glen < 10 ? 0 : ghead;
-    for (int k = 0; k < glen; ++k) {
-        gsum += idx == wslot ? gl_new : ldv(a.b.gwin + (idx) * N, ui);
-        idx = idx == 9 ? 0 : idx + 1;
+    // the window's slots in summation order (oldest first); their addresses are known up front,
+    // so the (at most 9) loads are issued together instead of one round trip per term
+    const int gstart = glen < 10 ? 0 : ghead;
+    R gv[10];
+#pragma unroll
+    for (int k = 0; k < 10; ++k) {
+        int p = gstart + k;
+        p = p >= 10 ? p - 10 : p;
+        gv[k] = (k < glen && p != wslot) ? ldv(a.b.gwin + (p) * N, ui) : gl_new;
     }
+    R gsum = R(0);
+#pragma unroll
+    for (int k = 0; k < 10; ++k)
+        if (k < glen) gsum += gv[k];
     R gl = gsum / R(10);
 
     // ---- truncated -> done -> reward (rtd_rl.py:190-336 / rtd_pso.py:172-317)
@@ -1207,6 +1241,8 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
         }
     }
 
+    PD_T(t_rtd);
+    PD_ACC(5, t_rtd - t_loop);
     // ---- outputs (role 0 of the env's lane group)
     // fresh copy of the offset: the store addresses are recomputed here from the SGPR bases
     // instead of keeping the load addresses live (spilled) across the sub-step loop
@@ -1271,6 +1307,15 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
         for (int k = 0; k < 11; ++k)
             if (k % LPE == role) stv(a.b.st + (k) * N, ui_out) = s[k];
     }
+#ifdef PD_STAMP
+    PD_T(t_end);
+    PD_ACC(6, t_end - t_rtd);
+    if (__lane_id() == 0) {
+#pragma unroll
+        for (int k = 0; k < 7; ++k) atomicAdd(&a.pend.stats[8 + k], acc_[k]);
+        atomicAdd(&a.pend.stats[15], 1ull);
+    }
+#endif
 }
 
 // Insert the neighbourhoods solved on device during the last launch (single block; the only
@@ -1766,10 +1811,10 @@ template <typename R> pd_status create_impl(const pd_params* p, const pd_config*
     PD_HIP(hipMemset(e->gwin, 0, 10 * N * R_));
     PD_HIP(hipMemset(e->epi, 0xff, N * 4));   // first reset -> episode 0
     if ((st = dalloc(e, (void**)&e->pend.count, 8)) || (st = dalloc(e, (void**)&e->pend.keys, kPendingCap * 8)) ||
-        (st = dalloc(e, (void**)&e->pend.pay, (size_t)kPendingCap * kPay * 8)) || (st = dalloc(e, (void**)&e->pend.stats, 8 * 8)))
+        (st = dalloc(e, (void**)&e->pend.pay, (size_t)kPendingCap * kPay * 8)) || (st = dalloc(e, (void**)&e->pend.stats, 16 * 8)))
         return st;
     PD_HIP(hipMemset(e->pend.count, 0, 8));
-    unsigned long long stats0[8] = {0, 0, (unsigned long long)tcd.entries, (unsigned long long)tcl.entries, 0, 0, 0, 0};
+    unsigned long long stats0[16] = {0, 0, (unsigned long long)tcd.entries, (unsigned long long)tcl.entries};
     PD_HIP(hipMemcpy(e->pend.stats, stats0, sizeof(stats0), hipMemcpyHostToDevice));
     StepArgs<R> a = make_args<R>(e);
     unsigned grid = (unsigned)((N + kBlock - 1) / kBlock);
@@ -2070,10 +2115,16 @@ pd_status pd_set_wind_sigmas(pd_env* e, const double* sig, void* stream) {
 pd_status pd_counters(pd_env* e, int64_t* misses, int64_t* ecd, int64_t* ecl, int64_t* nans) {
     if (!e) return fail(PD_ERR_INVALID, "null env");
     PD_HIP(hipSetDevice(e->device));
-    unsigned long long st[8];
+    unsigned long long st[16];
     PD_HIP(hipMemcpy(st, e->pend.stats, sizeof(st), hipMemcpyDeviceToHost));
-    if (getenv("PDENV_DEBUG_COUNTERS"))
+    if (getenv("PDENV_DEBUG_COUNTERS")) {
         fprintf(stderr, "[pdenv] knn calls %llu line-candidates %llu iterations %llu probes %llu\n", st[4], st[5], st[6], st[7]);
+        if (st[15])
+            fprintf(stderr, "[pdenv] k_step wave clocks (mean per wave): staging %.0f loads %.0f pre-aero %.0f aero %.0f "
+                    "post-aero %.0f rtd %.0f outputs %.0f (waves %llu)\n", (double)st[8] / st[15], (double)st[9] / st[15],
+                    (double)st[10] / st[15], (double)st[11] / st[15], (double)st[12] / st[15], (double)st[13] / st[15],
+                    (double)st[14] / st[15], st[15]);
+    }
     if (misses) *misses = (int64_t)st[0];
     if (nans) *nans = (int64_t)st[1];
     if (ecd) *ecd = (int64_t)st[2];
