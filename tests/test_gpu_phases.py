@@ -165,17 +165,23 @@ def test_batch_vs_oracle_rl(pd, phase, oracle_mod):
     acts = acts if f64 else acts.astype(np.float32)
     orcs = [O.Oracle(phase=ph, rtd=O.RTD_RL, discount_factor=0.99, trajectory_length=100) for _ in range(8)]
     idx = np.linspace(0, n - 1, 8).astype(int)
+    # landing_burn: random gimbal and fin commands tumble the vehicle, which amplifies ulp
+    # differences ~3x per step (chaos, not error), so each oracle env is teacher-forced with
+    # the device's pre-step state and actuator memory (its g-load window is its own)
+    forced = phase == "landing_burn"
     for t in range(T):
+        if forced:
+            S_pre, A_pre = env.state.cpu().numpy(), env.actuators.cpu().numpy()
         obs, r, dn, tr, ex = env.step(torch.tensor(acts[t]))
         S = env.state.cpu().numpy()
         r = r.cpu().numpy()
         for o, i in zip(orcs, idx):
+            if forced:
+                o.E.s[:] = list(S_pre[i]); o.E.prev_s[:] = list(S_pre[i])
+                o.E.gimbal_prev, o.E.dl_prev, o.E.dr_prev = (float(v) for v in A_pre[i])
             s, rr, d_, tr_, tid, ob, info = o.step(acts[t, i].astype(np.float64), f32=not f64)
             assert (bool(dn[i]), bool(tr[i])) == (d_, tr_), (phase, t, i)
-            # landing_burn's reward reads x, vx and theta (rtd_rl.py:243-269), the free-running
-            # chaotic channels held to 1e-6 below; the other phases' rewards read y/v/mass only
-            rtol = 1e-6 if phase == "landing_burn" else 1e-9
-            assert abs(r[i] - rr) <= rtol * max(1.0, abs(rr)), (phase, t, i, r[i], rr)
+            assert abs(r[i] - rr) <= 1e-9 * max(1.0, abs(rr)), (phase, t, i, r[i], rr)
             assert np.abs(obs.cpu().numpy()[i] - ob).max() < 1e-4    # steep tanh of the chaotic attitude (obs 2-4 of landing_burn)
             if d_ or tr_:
                 o.reset()
@@ -184,6 +190,8 @@ def test_batch_vs_oracle_rl(pd, phase, oracle_mod):
                 # free-running 40 steps: the attitude channels are chaotic, last-ulp
                 # differences of the device transcendentals grow; the per-step bar is above
                 tol = np.full(11, 1e-8); tol[[0, 2, 4, 6, 7]] = 1e-6; tol[5] = 1e-4
+                if forced:
+                    tol = np.full(11, 1e-10); tol[5] = 1e-8
                 assert (e < tol).all(), (phase, t, i, dict(zip(ST, e)))
 
 
