@@ -132,8 +132,9 @@ typedef struct {
     int32_t auto_reset;        /* reset envs in-kernel when done|truncated */
     double tilt_sigma_rad;     /* initial pitch perturbation N(0, s) (0 = reference) */
     int32_t action_f64;        /* actions are double (f64 path, no float32 islands) */
-    int32_t lanes_per_env;     /* step-kernel lanes per env: 1, 2, 4 or 8 (0 = by n_envs: 8 up to
-                                  8 192 envs, 4 up to 32 768, else 2) */
+    int32_t lanes_per_env;     /* step-kernel lanes per env: 1, 2, 4, 8 or 16 (0 = by n_envs: 16 up
+                                  to 4 096 envs, 8 up to 8 192, 4 up to 16 384, else 2; policy
+                                  rollouts use at most 8) */
     /* ---- ABI 2 */
     double dt;                 /* physics dt of phases 2..6, compile_physics(dt, phase) (0 = the env's 0.1) */
     double discount_factor;    /* rtd_rl landing_burn reward scale (1-g)/(1-g^L) and the Pcontrol

@@ -853,6 +853,7 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
                              my_table ? aq_cl : aq_cd, part, nparts);
                 if constexpr (nparts >= 2) v += __shfl_xor(v, 1);
                 if constexpr (nparts >= 4) v += __shfl_xor(v, 2);
+                if constexpr (nparts >= 8) v += __shfl_xor(v, 4);
                 R vcd = __shfl(v, gbase);
                 R vcl = __shfl(v, gbase + nparts);
                 CD = have ? vcd : R(0);
@@ -1834,6 +1835,7 @@ template <typename R, int PH, int RT, bool W> void launch_lpe(int lpe, const Ste
         case 1: launch_step<R, PH, RT, W, 1>(a, s); break;
         case 2: launch_step<R, PH, RT, W, 2>(a, s); break;
         case 8: launch_step<R, PH, RT, W, 8>(a, s); break;
+        case 16: launch_step<R, PH, RT, W, 16>(a, s); break;
         default: launch_step<R, PH, RT, W, 4>(a, s); break;
     }
 }
@@ -1971,12 +1973,13 @@ pd_status pd_create(const pd_params* params, const pd_config* cfg, pd_env** out)
     e->obs_kind = obs_kind_of(cfg->phase, cfg->rtd);
     e->obs_dim = obs_dim(e->obs_kind);
     e->rsize = cfg->precision == PD_F64 ? 8 : 4;
-    // default lanes per env: enough waves to fill the chip.  Below ~32k envs the step is bound by
-    // one wave's latency, and splitting each RBF over more lanes shortens it (measured, f64:
-    // 4 096 envs LPE 8 0.061 vs LPE 2 0.076 ms; 16 384 LPE 4 0.069 vs 0.076; 65 536 LPE 2 best)
+    // default lanes per env: about one wave per SIMD (n_envs x LPE ~ 65 536 lanes), at least 2.
+    // Below ~64k envs the step is bound by one wave's latency, and splitting each RBF over more
+    // lanes shortens it (measured, f64 ms/step: 4 096 envs LPE 16 0.049, 8 0.054, 2 0.071;
+    // 16 384 LPE 4 0.066, 8 0.067, 16 0.105; 32 768 LPE 2 0.072, 4 0.075; 65 536 LPE 2 best)
     e->lpe = cfg->lanes_per_env != 0 ? cfg->lanes_per_env
-                                     : (cfg->n_envs <= 8192 ? 8 : (cfg->n_envs <= 32768 ? 4 : 2));
-    if (e->lpe != 1 && e->lpe != 2 && e->lpe != 4 && e->lpe != 8) { delete e; return fail(PD_ERR_INVALID, "lanes_per_env must be 0, 1, 2, 4 or 8"); }
+                                     : (cfg->n_envs <= 4096 ? 16 : (cfg->n_envs <= 8192 ? 8 : (cfg->n_envs <= 16384 ? 4 : 2)));
+    if (e->lpe != 1 && e->lpe != 2 && e->lpe != 4 && e->lpe != 8 && e->lpe != 16) { delete e; return fail(PD_ERR_INVALID, "lanes_per_env must be 0, 1, 2, 4, 8 or 16"); }
     st = cfg->precision == PD_F64 ? create_impl<double>(params, cfg, e) : create_impl<float>(params, cfg, e);
     if (st != PD_OK) { pd_destroy(e); return st; }
     *out = e;

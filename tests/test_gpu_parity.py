@@ -29,7 +29,7 @@ def make(pd, n, phase="landing_burn_pure_throttle", mode="rl", **kw):
     return pd.PoweredDescentEnv(n, flight_phase=phase, mode=mode, **kw)
 
 
-@pytest.mark.parametrize("lpe", [1, 2, 4, 8])
+@pytest.mark.parametrize("lpe", [1, 2, 4, 8, 16])
 @pytest.mark.parametrize("tag,phase", [("pt", "landing_burn_pure_throttle"), ("lb", "landing_burn")])
 def test_teacher_forced_step_vs_reference(pd, tag, phase, lpe):
     import torch
@@ -103,7 +103,7 @@ def test_episode_vs_reference(pd, name, phase, mode):
     assert np.abs(OBS - ref_obs).max() < 1e-6   # bounded by the (chaotic) state drift
 
 
-@pytest.mark.parametrize("lpe", [1, 4, 8])
+@pytest.mark.parametrize("lpe", [1, 4, 8, 16])
 def test_batched_random_vs_oracle(pd, oracle_mod, lpe):
     """4096 envs (config c2 size), random float32 actions, 40 steps: every env against the
     scalar oracle on a sampled subset, and batch-invariance (env i does not depend on N)."""
@@ -547,7 +547,7 @@ def test_policy_rollout_compaction_invariant(pd, monkeypatch):
     np.testing.assert_allclose(f2.cpu().numpy(), res[0][0][sub], rtol=1e-12)
 
 
-@pytest.mark.parametrize("lpe", [1, 2, 4, 8])
+@pytest.mark.parametrize("lpe", [1, 2, 4, 8, 16])
 def test_ragged_batch_sizes_bit_identical(pd, lpe):
     """Batch sizes that are not multiples of a wave or a workgroup (1, 3, 63, 65, 257, 1000):
     lanes past the end recompute the last env and write nothing, so env i's trajectory is
