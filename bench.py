@@ -207,12 +207,20 @@ def main():
     import torch
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    # one process per GPU; PD_BENCH_BACKEND=gloo rehearses the multi-rank path with several ranks
+    # sharing fewer GPUs (ranks map onto the visible devices round-robin)
+    backend = os.environ.get("PD_BENCH_BACKEND", "nccl")
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if backend != "nccl":
+        local %= max(1, torch.cuda.device_count())
     dist = None
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     torch.cuda.set_device(local)
     import pdenv
     if args.workload == "c4":
