@@ -30,7 +30,9 @@ class Actor(nn.Module):
         f = self.shared_net(state)
         return self.mean(f), torch.clamp(self.log_std(f), self.log_std_min, self.log_std_max)
 
-    def sample(self, state, deterministic=False, generator=None):
+    def sample(self, state, deterministic=False, generator=None, with_log_prob=True):
+        """with_log_prob=False skips the log-probability (select_action discards it,
+        sac_pytorch_powered_descent.py / sac_pytorch.py:404-409): same action, fewer kernels."""
         mean, log_std = self(state)
         if deterministic:
             return torch.tanh(mean) * self.max_action, None
@@ -38,6 +40,8 @@ class Actor(nn.Module):
         eps = torch.randn(mean.shape, device=mean.device, dtype=mean.dtype, generator=generator)
         x = mean + std * eps                                   # Normal(mean, std).rsample()
         action = torch.tanh(x)
+        if not with_log_prob:
+            return action * self.max_action, None
         log_prob = (-((x - mean) ** 2) / (2 * std ** 2) - log_std - 0.9189385332046727
                     - torch.log(1 - action.pow(2) + 1e-6)).sum(-1, keepdim=True)
         return action * self.max_action, log_prob
@@ -110,8 +114,11 @@ class DevicePrioritizedReplayBuffer(DeviceReplayBuffer):
 
     def add_batch(self, slab):
         b = min(slab.shape[0], self.capacity)
-        idx = (self.position + torch.arange(b, device=self.data.device)) % self.capacity
-        self.priorities[idx] = self.max_priority
+        if self.position + b <= self.capacity:                 # no wrap: one fill
+            self.priorities[self.position:self.position + b] = self.max_priority
+        else:
+            idx = (self.position + torch.arange(b, device=self.data.device)) % self.capacity
+            self.priorities[idx] = self.max_priority
         super().add_batch(slab)
 
     def sample(self, batch_size, generator=None):
@@ -178,11 +185,11 @@ class SACCollector:
     def _body(self):
         """actor -> pd_step -> slab -> observe into self.obs; returns the slab (no syncs)."""
         gen = None if self.use_graph else self.generator
-        act, _ = self.actor.sample(self.obs, deterministic=self.deterministic, generator=gen)
+        act, _ = self.actor.sample(self.obs, deterministic=self.deterministic, generator=gen, with_log_prob=False)
         act = act.float().contiguous()
         self.env.step_raw_noflush(act)
         slab = transition_slab(self.obs, act, self.env.reward_buf, self.env.obs_buf, self.env.done_buf)
-        self.obs.copy_(self.env.observe_raw().float())
+        self.obs.copy_(self.env.observe_raw())                 # copy_ casts: one kernel
         return slab
 
     def _finish(self, slab):
