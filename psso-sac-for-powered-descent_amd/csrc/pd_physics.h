@@ -107,6 +107,40 @@ template <> __device__ __forceinline__ float eval_log<float>(float x) {
     return __builtin_amdgcn_logf(x) * 0.693147180559945309f;
 }
 
+// ---------------------------------------------------------------- sine and cosine together
+// Binary64 sin and cos of one angle in one pass (the step kernel needs both of alpha_eff, of
+// theta, ...): reduction by pi/2 to a double-double r + y (the first fma term is exact for
+// |k| < 2^20; beyond 1e6 rad, the device library), then the public-domain fdlibm kernels
+// k_sin.c / k_cos.c with their tail argument, and a quadrant swap.  Error <= 1 ulp against
+// long double over 2e7 arguments, like the device library's (neither is glibc's bit for bit).
+template <typename R> __device__ __forceinline__ void pd_sincos(R x, R& s, R& c) {
+    s = sin(x); c = cos(x);
+}
+template <> __device__ __forceinline__ void pd_sincos<double>(double x, double& s, double& c) {
+#ifdef PD_LIB_TRIG
+    s = sin(x); c = cos(x);
+#else
+    if (!(fabs(x) < 1.0e6)) { s = sin(x); c = cos(x); return; }   // huge or NaN
+    const double k = rint(x * 6.36619772367581382433e-01);
+    const double r1 = fma(-k, 1.57079632679489655800e+00, x);      // exact for |k| < 2^20
+    const double ph = k * 6.12323399573676603587e-17;               // k (pi/2 - high), two terms
+    const double pl = fma(k, 6.12323399573676603587e-17, -ph) + k * -1.4973849048591698e-33;
+    const double r = r1 - ph;                                       // reduced angle r + y
+    const double y = ((r1 - r) - ph) - pl;
+    const double z = r * r, v = z * r, w = z * z;
+    const double ps = 8.33333333332248946124e-03 + z * (-1.98412698298579493134e-04 + z * (2.75573137070700676789e-06 +
+                      z * (-2.50507602534068634195e-08 + z * 1.58969099521155010221e-10)));
+    const double sn = r - ((z * (0.5 * y - v * ps) - y) - v * -1.66666666666666324348e-01);
+    const double pc = z * (4.16666666666666019037e-02 + z * (-1.38888888888741095749e-03 + z * 2.48015872894767294178e-05)) +
+                      w * w * (-2.75573143513906633035e-07 + z * (2.08757232129817482790e-09 + z * -1.13596475577881948265e-11));
+    const double hz = 0.5 * z, ww = 1.0 - hz;
+    const double cs = ww + (((1.0 - ww) - hz) + (z * pc - r * y));
+    const int q = (int)(long long)k & 3;
+    s = q == 0 ? sn : (q == 1 ? cs : (q == 2 ? -sn : -cs));
+    c = q == 0 ? cs : (q == 1 ? -sn : (q == 2 ? -cs : sn));
+#endif
+}
+
 // ---------------------------------------------------------------- atmosphere
 // atmosphere_dynamics.py:5-27 (ambiance ISA restated)
 template <typename R>

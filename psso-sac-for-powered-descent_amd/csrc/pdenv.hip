@@ -865,11 +865,13 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
         PD_ACC(3, t_aero1 - t_aero0);
         R drag = R(0.5) * rho * (speed * speed) * CD * P.A_front;
         R lift = R(0.5) * rho * (speed * speed) * CL * P.A_front;
-        R sae = sin(ae), cae = cos(ae);
+        R sae, cae;
+        pd_sincos<R>(ae, sae, cae);
         R apar, aperp;
         if (vy >= R(0)) { apar = lift * sae - drag * cae; aperp = -lift * cae - drag * sae; }
         else { apar = drag * cae - lift * sae; aperp = -drag * sae - lift * cae; }
-        R sth = sin(th), cth = cos(th);
+        R sth, cth;
+        pd_sincos<R>(th, sth, cth);
         R aero_x = apar * cth + aperp * sth;
         R aero_y = apar * sth - aperp * cth;
         R aero_m = aperp * d_cp_cg;
@@ -984,7 +986,8 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
                 R nnt = ((R)ud[1] + R(1)) / R(2);
                 thr = nnt * P.one_minus_nom_lb + P.nom_lb;
                 R tg = T_full * (R)(P.n_eng + 2) * thr;
-                R cg = cos(grad2), sg = sin(grad2);
+                R cg, sg;
+                pd_sincos<R>(grad2, sg, cg);
                 tpar = tg * cg; tperp = -tg * sg; tmz = -tg * sg * d_thrust;
                 R tot = sqrt(tpar * tpar + tperp * tperp);
                 md = P.Te_over_vex * (tot / T_full);
@@ -1019,7 +1022,9 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
             R cna = grid_fin_cn_alpha<R>(P, lds + L::kCnX, lds + L::kCnY, mach);
             R CnL = cna * ((ae - dl) * Cst<R>::rad2deg);
             R CnR = cna * ((ae - dr) * Cst<R>::rad2deg);
-            R cl_ = cos(dl), cr_ = cos(dr), sl_ = sin(dl), sr_ = sin(dr);
+            R cl_, cr_, sl_, sr_;
+            pd_sincos<R>(dl, sl_, cl_);
+            pd_sincos<R>(dr, sr_, cr_);
             R f_perp = qS * (CnR * cr_ - CnL * cl_ - Ca * (sl_ - sr_));
             R f_par = qS * (Ca * (R(2) + cl_ + cr_) - CnL * sl_ + CnR * sr_);
             R m_z = -(P.d_base_gf - x_cog) * f_perp + P.R_rocket * qS * (Ca * (sr_ - sl_) - CnL * cl_ + CnR * cr_);
