@@ -1760,7 +1760,13 @@ template <typename R> pd_status create_impl(const pd_params* p, const pd_config*
     // interior candidate grids: C_D abscissa in [-radians(10), radians(10)], C_L in [0, 10]
     std::vector<unsigned long long> gk[2];
     std::vector<int> gs[2];
-    const int gnm[2] = {400, 400}, gna[2] = {16, 200};
+    int gnm[2] = {400, 400}, gna[2] = {16, 200};
+    if (const char* g = getenv("PDENV_GRID")) {   // experiments: "nm_cd,na_cd,nm_cl,na_cl"
+        int v[4];
+        if (sscanf(g, "%d,%d,%d,%d", &v[0], &v[1], &v[2], &v[3]) == 4 && v[0] > 0 && v[1] > 0 && v[2] > 0 && v[3] > 0) {
+            gnm[0] = v[0]; gna[0] = v[1]; gnm[1] = v[2]; gna[1] = v[3];
+        }
+    }
     const double ga0[2] = {-10.0 * kDeg2Rad, 0.0}, ga1[2] = {10.0 * kDeg2Rad, 10.0};
     if ((st = build_grid<R>(p->cd, ga0[0], ga1[0], gnm[0], gna[0], tcd, gk[0], gs[0])) != PD_OK) return st;
     if ((st = build_grid<R>(p->cl, ga0[1], ga1[1], gnm[1], gna[1], tcl, gk[1], gs[1])) != PD_OK) return st;
