@@ -171,8 +171,18 @@ pd_status pd_reset(pd_env* env, const uint8_t* mask, void* obs, void* stream);
  *  info    : optional [PD_N_INFO][N] (last sub-step values), NULL = not written */
 pd_status pd_step(pd_env* env, const void* actions, void* obs, void* reward, uint8_t* done,
                   uint8_t* truncated, int8_t* trunc_id, const double* noise, void* info, void* stream);
-/* Multi-step rollout with device-resident actions [T][N][A]: T launches of the step kernel,
- * rewards accumulated into reward_sum [N] (may be NULL).  No host synchronisation. */
+/* n_steps consecutive pd_step calls over device-resident actions [n_steps][N][A], landing-burn
+ * phases: obs [n_steps][N][O], reward [n_steps][N], done/truncated/trunc_id [n_steps][N] receive
+ * every step's outputs (any may be NULL).  Replaces a Python loop over
+ * rocket_environment_pre_wrap.step (base_environment.py:99-154) with fused launches: each launch
+ * runs up to 16 steps (PDENV_FUSE) of every env in one kernel, so the LDS table staging and the
+ * launch tail are paid once per launch, followed by the miss flush.  Results are bit-identical
+ * to n_steps pd_step calls.  No host synchronisation. */
+pd_status pd_step_n(pd_env* env, const void* actions, int32_t n_steps, void* obs, void* reward, uint8_t* done,
+                    uint8_t* truncated, int8_t* trunc_id, void* stream);
+/* Multi-step rollout with device-resident actions [T][N][A]: the fused launches of pd_step_n
+ * (per-step launches for the other phases), rewards accumulated into reward_sum [N] (may be
+ * NULL), no per-step outputs.  No host synchronisation. */
 pd_status pd_rollout(pd_env* env, const void* actions, int32_t n_steps, void* reward_sum,
                      void* stream);
 /* PSO objective for a batch of particles, one env per particle, on the device:

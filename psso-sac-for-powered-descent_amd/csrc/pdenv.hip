@@ -97,6 +97,7 @@ template <typename R> struct StepArgs {
     int use_list;   // step list_in (else all N envs, finished ones skipped by their fin flag)
     double dt_aux;                   // physics dt of phases 2..6 (compile_physics(dt, phase))
     int rtd_none;                    // PD_RTD_NONE: physics stepping only (reward/done/trunc 0)
+    int n_fused;                     // env-steps per launch (actions/outputs: [n_fused][N] rows)
 };
 
 // Per-env element `i` of a wave-uniform base pointer, addressed as base + zero-extended 32-bit
@@ -716,6 +717,18 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
     const R* s_cd = lds + L::kCd;
     const R* s_cl = lds + L::kCl;
 
+    // Fused launches (pd_step_n, pd_rollout): n_fused consecutive env-steps of the same envs,
+    // each the body below with its own action row and output rows.  The per-env state goes
+    // through memory between them exactly as between launches; the lanes that store a field
+    // and the lanes that load it next are in the same wave, so a workgroup-scope fence (a
+    // wait on the outstanding stores) orders them.  Saves the table staging and the launch
+    // tail per step, and lets each wave run ahead of the slowest (e.g. a miss-solving) one.
+    const int nf = POL ? 1 : a.n_fused;
+#pragma unroll 1
+    for (int f = 0; f < nf; ++f) {
+    if (f > 0) __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    const size_t fo = (size_t)f * (size_t)N;
+
     R s[11];
 #pragma unroll
     for (int k = 0; k < 11; ++k) s[k] = ldv(a.b.st + (k) * N, ui);
@@ -760,10 +773,10 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
         }
     } else if (a.act_f64) {
 #pragma unroll
-        for (int k = 0; k < A; ++k) if (k < AD) ud[k] = ldv((const double*)a.actions + k, ui * AD);
+        for (int k = 0; k < A; ++k) if (k < AD) ud[k] = ldv((const double*)a.actions + fo * AD + k, ui * AD);
     } else {
 #pragma unroll
-        for (int k = 0; k < A; ++k) if (k < AD) uf[k] = ldv((const float*)a.actions + k, ui * AD);
+        for (int k = 0; k < A; ++k) if (k < AD) uf[k] = ldv((const float*)a.actions + fo * AD + k, ui * AD);
     }
 
     // pure throttle 4 x 0.025 s, landing_burn 4 x 0.1 s (actuators 0.025 s); the other phases
@@ -1259,9 +1272,10 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
         if (a.obs) {
             // the wrappers' observation (obs_write kinds); compile-time for the landing burns
             constexpr int kind = RTD == 1 ? (PHASE == 0 ? 1 : 2) : (PHASE == 0 ? 0 : (PHASE == 1 ? 3 : -1));
-            obs_write<R>(P2, kind >= 0 ? kind : P2.obs_kind, s, a.obs, ui_out);
+            const int ok = kind >= 0 ? kind : P2.obs_kind;
+            obs_write<R>(P2, ok, s, a.obs + fo * obs_dim(ok), ui_out);
         }
-        if (a.reward) stv(a.reward, ui_out) = rew;
+        if (a.reward) stv(a.reward + fo, ui_out) = rew;
         if constexpr (POL) {
             // objective_function: episode_reward -= reward until done or truncated (env_wrapped_ea.py:200-222)
             ev(a.reward_sum, ui_out) -= rew;
@@ -1269,9 +1283,9 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
         } else if (a.reward_sum) {
             ev(a.reward_sum, ui_out) += rew;
         }
-        if (a.done) stv(a.done, ui_out) = (uint8_t)dn;
-        if (a.trunc) stv(a.trunc, ui_out) = (uint8_t)tr;
-        if (a.trunc_id) stv(a.trunc_id, ui_out) = (int8_t)id;
+        if (a.done) stv(a.done + fo, ui_out) = (uint8_t)dn;
+        if (a.trunc) stv(a.trunc + fo, ui_out) = (uint8_t)tr;
+        if (a.trunc_id) stv(a.trunc_id + fo, ui_out) = (int8_t)id;
         if (a.info) stv(a.info + (PD_INFO_GLOAD) * N, ui_out) = gl;
         if (ended) {
             reset_env(a, i, ep + 1, false);
@@ -1313,6 +1327,7 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
         for (int k = 0; k < 11; ++k)
             if (k % LPE == role) stv(a.b.st + (k) * N, ui_out) = s[k];
     }
+    }   // fused steps
 #ifdef PD_STAMP
     PD_T(t_end);
     PD_ACC(6, t_end - t_rtd);
@@ -1599,6 +1614,7 @@ template <typename R> StepArgs<R> make_args(pd_env* e) {
     a.tilt_sigma = e->cfg.tilt_sigma_rad;
     a.dt_aux = e->cfg.dt > 0.0 ? e->cfg.dt : 0.1;
     a.rtd_none = e->cfg.rtd == PD_RTD_NONE;
+    a.n_fused = 1;
     return a;
 }
 
@@ -1880,10 +1896,12 @@ template <typename R> void launch_insert(pd_env* e, hipStream_t s) {
 
 template <typename R>
 pd_status step_impl(pd_env* e, const void* actions, void* obs, void* reward, uint8_t* done, uint8_t* trunc,
-                    int8_t* tid, const double* noise, void* info, void* reward_sum, hipStream_t s) {
+                    int8_t* tid, const double* noise, void* info, void* reward_sum, hipStream_t s,
+                    int n_fused = 1) {
     StepArgs<R> a = make_args<R>(e);
     a.actions = actions; a.obs = (R*)obs; a.reward = (R*)reward; a.done = done; a.trunc = trunc; a.trunc_id = tid;
     a.noise = noise; a.info = (R*)info; a.reward_sum = (R*)reward_sum;
+    a.n_fused = n_fused;
     dispatch_step<R>(e, a, s);
     PD_HIP(hipGetLastError());
     return PD_OK;
@@ -1949,6 +1967,37 @@ pd_status rollout_policy_impl(pd_env* e, const float* w, int32_t max_steps, void
     launch_insert<R>(e, s);
     if (steps) PD_HIP(hipMemcpyAsync(steps, e->tstep, (size_t)N * 4, hipMemcpyDeviceToDevice, s));
     PD_HIP(hipGetLastError());
+    return PD_OK;
+}
+
+// Steps per fused launch: the miss flush runs between launches, so a neighbourhood solved on
+// device is re-solved at most this many steps before it is in the tables (PDENV_FUSE overrides).
+int fuse_chunk() {
+    const char* s = getenv("PDENV_FUSE");
+    int k = s && *s ? atoi(s) : 16;
+    return k < 1 ? 1 : (k > 256 ? 256 : k);
+}
+
+// n_steps env-steps in launches of fuse_chunk() fused steps, each followed by the miss flush.
+// Row t of every [n_steps][N...] array belongs to step t; NULL outputs are not written.
+pd_status step_n_impl(pd_env* e, const void* actions, int32_t n_steps, void* obs, void* reward, uint8_t* done,
+                      uint8_t* trunc, int8_t* tid, void* reward_sum, hipStream_t s) {
+    const size_t N = (size_t)e->cfg.n_envs;
+    const size_t sa = N * e->act_dim * (e->cfg.action_f64 ? 8 : 4), so = N * e->obs_dim * e->rsize;
+    const size_t sr = N * e->rsize;
+    const int K = fuse_chunk();
+    for (int32_t t = 0; t < n_steps; t += K) {
+        const int k = n_steps - t < K ? n_steps - t : K;
+        auto at = [&](void* p, size_t stride) { return p ? (void*)((char*)p + stride * t) : nullptr; };
+        const void* act = (const char*)actions + sa * t;
+        pd_status st = e->rsize == 8
+            ? step_impl<double>(e, act, at(obs, so), at(reward, sr), (uint8_t*)at(done, N), (uint8_t*)at(trunc, N),
+                                (int8_t*)at(tid, N), nullptr, nullptr, reward_sum, s, k)
+            : step_impl<float>(e, act, at(obs, so), at(reward, sr), (uint8_t*)at(done, N), (uint8_t*)at(trunc, N),
+                               (int8_t*)at(tid, N), nullptr, nullptr, reward_sum, s, k);
+        if (st != PD_OK) return st;
+        if ((st = pd_flush_misses(e, s)) != PD_OK) return st;
+    }
     return PD_OK;
 }
 
@@ -2028,9 +2077,21 @@ pd_status pd_step(pd_env* e, const void* actions, void* obs, void* reward, uint8
     return step_impl<float>(e, actions, obs, reward, done, truncated, trunc_id, noise, info, nullptr, (hipStream_t)stream);
 }
 
+pd_status pd_step_n(pd_env* e, const void* actions, int32_t n_steps, void* obs, void* reward, uint8_t* done,
+                    uint8_t* truncated, int8_t* trunc_id, void* stream) {
+    if (!e || !actions || n_steps < 0) return fail(PD_ERR_INVALID, "bad step_n args");
+    if (e->cfg.phase != PD_PHASE_PURE_THROTTLE && e->cfg.phase != PD_PHASE_LANDING_BURN)
+        return fail(PD_ERR_UNSUPPORTED, "pd_step_n: landing-burn phases only (use pd_step)");
+    PD_HIP(hipSetDevice(e->device));
+    return step_n_impl(e, actions, n_steps, obs, reward, done, truncated, trunc_id, nullptr, (hipStream_t)stream);
+}
+
 pd_status pd_rollout(pd_env* e, const void* actions, int32_t n_steps, void* reward_sum, void* stream) {
     if (!e || !actions || n_steps < 0) return fail(PD_ERR_INVALID, "bad rollout args");
     PD_HIP(hipSetDevice(e->device));
+    if (e->cfg.phase == PD_PHASE_PURE_THROTTLE || e->cfg.phase == PD_PHASE_LANDING_BURN)
+        return step_n_impl(e, actions, n_steps, nullptr, nullptr, nullptr, nullptr, nullptr, reward_sum,
+                           (hipStream_t)stream);
     size_t stride = (size_t)e->cfg.n_envs * e->act_dim * (e->cfg.action_f64 ? 8 : 4);
     for (int32_t t = 0; t < n_steps; ++t) {
         const void* at = (const char*)actions + stride * t;

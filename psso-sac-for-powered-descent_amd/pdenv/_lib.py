@@ -73,7 +73,7 @@ class PdConfig(C.Structure):
 
 
 EXPORTS = ["pd_abi_version", "pd_sizeof_params", "pd_sizeof_config", "pd_last_error", "pd_device_count", "pd_create", "pd_destroy", "pd_reset",
-           "pd_step", "pd_rollout", "pd_rollout_policy", "pd_pso_step", "pd_flush_misses", "pd_observe", "pd_get_state", "pd_set_state", "pd_get_actuators",
+           "pd_step", "pd_step_n", "pd_rollout", "pd_rollout_policy", "pd_pso_step", "pd_flush_misses", "pd_observe", "pd_get_state", "pd_set_state", "pd_get_actuators",
            "pd_set_actuators", "pd_set_gload_window", "pd_set_wind_sigmas", "pd_counters", "pd_obs_dim", "pd_action_dim"]
 
 _lib = None
@@ -101,6 +101,7 @@ def load(path=None):
     L.pd_destroy.argtypes = [vp]
     L.pd_reset.argtypes = [vp, vp, vp, vp]
     L.pd_step.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
+    L.pd_step_n.argtypes = [vp, vp, I32, vp, vp, vp, vp, vp, vp]
     L.pd_rollout.argtypes = [vp, vp, I32, vp, vp]
     L.pd_rollout_policy.argtypes = [vp, vp, I32, I32, vp, vp, I32, vp]
     L.pd_pso_step.argtypes = [I64, I32, vp, vp, vp, vp, vp, vp, vp, vp, vp, C.c_double, C.c_double, C.c_double,
@@ -116,7 +117,7 @@ def load(path=None):
     L.pd_counters.argtypes = [vp, P(I64), P(I64), P(I64), P(I64)]
     L.pd_obs_dim.argtypes = [vp]; L.pd_obs_dim.restype = C.c_int
     L.pd_action_dim.argtypes = [vp]; L.pd_action_dim.restype = C.c_int
-    for name in ("pd_create", "pd_destroy", "pd_reset", "pd_step", "pd_rollout", "pd_rollout_policy", "pd_pso_step", "pd_flush_misses", "pd_observe",
+    for name in ("pd_create", "pd_destroy", "pd_reset", "pd_step", "pd_step_n", "pd_rollout", "pd_rollout_policy", "pd_pso_step", "pd_flush_misses", "pd_observe",
                  "pd_get_state", "pd_set_state", "pd_get_actuators", "pd_set_actuators",
                  "pd_set_wind_sigmas", "pd_set_gload_window", "pd_counters"):
         getattr(L, name).restype = C.c_int

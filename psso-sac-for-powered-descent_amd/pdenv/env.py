@@ -182,6 +182,32 @@ class PoweredDescentEnv:
         L.check(self.lib.pd_rollout(self.h, _ptr(a), int(T), _ptr(rs), _stream(self.device)))
         return rs
 
+    def step_n(self, actions, outputs=True):
+        """T consecutive env-steps over device-resident actions [T, N, A] (pd_step_n: fused
+        launches of up to 16 steps each, then the miss flush), the same results as T step()
+        calls.  Landing-burn phases only.  outputs=True returns per-step
+        (obs [T, N, O], reward [T, N], done [T, N], truncated [T, N], trunc_id [T, N]);
+        outputs=False writes nothing per step and returns None."""
+        self._check_steppable()
+        a = actions.to(device=self.device, dtype=self.action_dtype).contiguous()
+        T = int(a.shape[0])
+        if a.dim() != 3 or a.shape[1] != self.n:
+            raise ValueError(f"actions must be [T, {self.n}, A]")
+        if outputs:
+            kw = dict(device=self.device)
+            obs = torch.empty(T, self.n, self._obs.shape[-1], dtype=self.dtype, **kw)
+            rew = torch.empty(T, self.n, dtype=self.dtype, **kw)
+            dn = torch.empty(T, self.n, dtype=torch.uint8, **kw)
+            tr = torch.empty(T, self.n, dtype=torch.uint8, **kw)
+            tid = torch.empty(T, self.n, dtype=torch.int8, **kw)
+            ptrs = [_ptr(x) for x in (obs, rew, dn, tr, tid)]
+        else:
+            ptrs = [None] * 5
+        L.check(self.lib.pd_step_n(self.h, _ptr(a), T, *ptrs, _stream(self.device)))
+        self._steps += T
+        if outputs:
+            return obs, rew, dn.bool(), tr.bool(), tid
+
     def flush(self):
         """Insert device-solved aero neighbourhoods into the tables (pd_flush_misses)."""
         L.check(self.lib.pd_flush_misses(self.h, _stream(self.device)))

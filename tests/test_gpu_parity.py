@@ -604,3 +604,33 @@ def test_maximum_handle_size(pd):
         small.step(A[t, idx].contiguous())
     assert torch.equal(small.state, S)
     assert abs(float(S[0, 10]) - (float(small.state[0, 10]))) == 0.0
+
+
+@pytest.mark.parametrize("phase,precision,lpe", [("landing_burn_pure_throttle", "f64", 2),
+                                                 ("landing_burn_pure_throttle", "f64", 1),
+                                                 ("landing_burn_pure_throttle", "f32", 4),
+                                                 ("landing_burn", "f64", 2)])
+def test_step_n_fused_equals_step_loop(pd, phase, precision, lpe):
+    """pd_step_n runs up to 16 env-steps per launch (state through memory between the fused
+    steps, miss flush after each launch).  Every per-step output row and the final state must
+    equal T separate pd_step calls bit for bit: wind + tilt + auto-reset + device-solved
+    misses (tables cut to 4 entries) + a ragged batch, T not a multiple of the chunk."""
+    import torch
+    N, T = 1000, 37
+    A_dim = 1 if phase == "landing_burn_pure_throttle" else 4
+    g = torch.Generator(device="cuda").manual_seed(5)
+    A = (torch.rand(T, N, A_dim, device="cuda", generator=g) * 2 - 1).contiguous()
+    kw = dict(precision=precision, lanes_per_env=lpe, enable_wind=True, stochastic_wind=True,
+              wind_percentile=None, auto_reset=True, tilt_sigma_rad=0.02, seed=21,
+              params=pd.Params().restrict_keys(4, 4))
+    loop = make(pd, N, phase=phase, **kw)
+    fused = make(pd, N, phase=phase, **kw)
+    rows = [loop.step(A[t]) for t in range(T)]
+    obs, rew, dn, tr, tid = fused.step_n(A)
+    for t, (o, r, d, tt, ex) in enumerate(rows):
+        assert torch.equal(o, obs[t]) and torch.equal(r, rew[t]), t
+        assert torch.equal(d, dn[t]) and torch.equal(tt, tr[t]) and torch.equal(ex["trunc_id"], tid[t]), t
+    assert torch.equal(loop.state, fused.state)
+    # the reward-only fused rollout matches the per-step rewards' sum
+    r2 = make(pd, N, phase=phase, **kw).rollout(A)
+    torch.testing.assert_close(r2, rew.sum(0), rtol=1e-12 if precision == "f64" else 1e-5, atol=1e-9)
