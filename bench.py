@@ -5,8 +5,9 @@ Workload (BASELINE config c3, one GPU): 65 536 parallel envs per GPU, phase
 landing_burn_pure_throttle with the SAC driver's reward (rtd_rl), the horizontal wind
 profile + von Karman gusts (percentile drawn per reset, as WindModel(given_percentile=None)),
 initial pitch perturbation N(0, 1 deg), synthetic uniform float32 random actions resident in
-HBM, auto-reset on done/truncated.  One timed "step" = one env.step() of all envs (one
-k_step launch; 4 physics sub-steps + g-load window + truncated/done/reward + obs each).
+HBM, auto-reset on done/truncated.  One timed "step" = one env.step() of all envs (4 physics
+sub-steps + g-load window + truncated/done/reward + obs written per step); by default 16
+consecutive steps run in one k_step launch (pd_step_n, --fuse 16), --fuse 1 launches per step.
 
 Multi-GPU: one process per GPU (torchrun), each rank steps its own contiguous env shard
 (env_offset = rank * N); the env batch shards with no data-path collective, so scaling is
@@ -189,8 +190,8 @@ def bench_pso(args, world, rank, local, dist):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=192)
+    ap.add_argument("--warmup", type=int, default=32)
     ap.add_argument("--envs", type=int, default=65536, help="envs per GPU")
     ap.add_argument("--precision", choices=["f64", "f32"], default="f64")
     ap.add_argument("--phase", default="landing_burn_pure_throttle")
@@ -201,6 +202,8 @@ def main():
                     help="c3: env-steps/s headline; c4: PSO generations with the fused actor; "
                          "c5: SAC collection (actor + env + RCCL transition gather + replay buffer)")
     ap.add_argument("--particles", type=int, default=32768, help="c4: particles per GPU")
+    ap.add_argument("--fuse", type=int, default=16,
+                    help="c3: env-steps per k_step launch (pd_step_n; 1 = one pd_step launch per step)")
     ap.add_argument("--graph", type=int, default=1, help="c5: replay the collection step as a HIP graph")
     args = ap.parse_args()
 
@@ -239,24 +242,42 @@ def main():
         T = args.warmup + args.steps
         g = torch.Generator(device=env.device).manual_seed(42 + rank)
         acts = (torch.rand(T, n, env.action_dim, generator=g, device=env.device) * 2 - 1).contiguous()
-        for t in range(args.warmup):
-            env.step_raw(acts[t])
+        F = max(1, args.fuse)
+        if F > 1:
+            # pd_step_n: F env-steps per launch, every step's outputs written (rows of [F, N, ...]
+            # buffers reused chunk to chunk, as the per-step loop reuses one [N, ...] buffer)
+            kw = dict(device=env.device)
+            outs = (torch.empty(F, n, env.obs_dim, dtype=env.dtype, **kw), torch.empty(F, n, dtype=env.dtype, **kw),
+                    torch.empty(F, n, dtype=torch.uint8, **kw), torch.empty(F, n, dtype=torch.uint8, **kw),
+                    torch.empty(F, n, dtype=torch.int8, **kw))
+            os.environ["PDENV_FUSE"] = str(F)
+
+            def chunk(t0, t1):
+                k = t1 - t0
+                env.step_n_raw(acts[t0:t1], tuple(o[:k] for o in outs))
+        else:
+            def chunk(t0, t1):
+                env.step_raw(acts[t0])
+        bounds = lambda a, b: [(t, min(t + F, b)) for t in range(a, b, F)]
+        for t0, t1 in bounds(0, args.warmup):
+            chunk(t0, t1)
         torch.cuda.synchronize()
-        # timed region: exactly K launches, nothing else on the stream (a per-launch event pair
-        # costs ~10 us of GPU time per step, so the kernel-duration pass is separate, below)
-        wall = timed_region(lambda k: env.step_raw(acts[args.warmup + k]), args.steps, torch.cuda.synchronize,
-                            dist, env.device)
-        # kernel duration: HIP events around every launch, on the stream the kernel runs on
-        kn = min(args.steps, 100)
-        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(kn)]
-        for k in range(kn):
+        # timed region: exactly K env-steps (ceil(K / F) launches), nothing else on the stream (a
+        # per-launch event pair costs ~10 us of GPU time, so the kernel-duration pass is separate)
+        tb = bounds(args.warmup, T)
+        wall = timed_region(lambda k: chunk(*tb[k]), len(tb), torch.cuda.synchronize, dist, env.device)
+        # kernel duration: HIP events around every launch (with F > 1 the launch and its miss
+        # flush), on the stream the kernel runs on; full F-step launches only
+        full = [b for b in tb if b[1] - b[0] == F][:100]
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in full]
+        for k, b in enumerate(full):
             ev[k][0].record()
-            env.step_raw(acts[args.warmup + k])
+            chunk(*b)
             ev[k][1].record()
         torch.cuda.synchronize()
         kern_ms = sorted(a.elapsed_time(b) for a, b in ev)
         c = env.counters()
-        res = dict(wall=wall, kern_avg_ms=sum(kern_ms) / len(kern_ms), kern_med_ms=kern_ms[len(kern_ms) // 2],
+        res = dict(wall=wall, kern_avg_ms=sum(kern_ms) / len(kern_ms), kern_med_ms=kern_ms[len(kern_ms) // 2], fuse=F,
                    n=n, obs_dim=env.obs_dim, act_dim=env.action_dim, counters=c)
         env.close()
         return res
@@ -273,15 +294,21 @@ def main():
     value = whole_job_rate(main_res["n"], world, args.steps, main_res["wall"])
     wind = not args.no_wind
     bpe = algorithmic_bytes(args.precision, args.phase, wind, main_res["obs_dim"], main_res["act_dim"])
-    achieved = bpe * main_res["n"] / (main_res["kern_avg_ms"] * 1e-3) / 1e9
+    F = main_res["fuse"]
+    achieved = bpe * main_res["n"] * F / (main_res["kern_avg_ms"] * 1e-3) / 1e9
     traffic = None
     mix = None
     pmc = os.path.join(REPO, "profiles", "pmc_traffic.json")
     if os.path.exists(pmc):
         try:
             summ = json.load(open(pmc))
+            # PMC figures are per launch of the profiled run's env-steps-per-launch: rescale to F
+            scale = F / float(summ.get("env_steps_per_launch", 1))
             traffic = summ.get(f"{args.precision}_bytes_per_launch")
+            traffic = traffic * scale if traffic is not None else None
             mix = summ.get("f64_valu_mix_per_launch") if args.precision == "f64" else None
+            if mix:
+                mix = {k: v * scale for k, v in mix.items()}
         except Exception:
             traffic = None
     out = {
@@ -303,6 +330,7 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": 8000.0, "unit": "GB/s",
                      "frac": achieved / 8000.0, "traffic": traffic,
                      "bytes_per_env_step": bpe, "kernel": "k_step", "kernel_avg_ms": main_res["kern_avg_ms"],
+                     "env_steps_per_launch": F, "envs_per_launch": main_res["n"],
                      "note": "VALU/transcendental-bound elementwise ODE (no MFMA); see DESIGN.md"},
         "rbf_table_misses": main_res["counters"]["rbf_misses"],
     }

@@ -208,6 +208,15 @@ class PoweredDescentEnv:
         if outputs:
             return obs, rew, dn.bool(), tr.bool(), tid
 
+    def step_n_raw(self, actions, outputs=None):
+        """Hot-loop pd_step_n: actions a contiguous [T, N, A] device tensor of action_dtype;
+        outputs None or preallocated (obs [T,N,O], reward [T,N], done, truncated uint8 [T,N],
+        trunc_id int8 [T,N]).  No copies, allocations or syncs."""
+        ptrs = [None] * 5 if outputs is None else [_ptr(x) for x in outputs]
+        L.check(self.lib.pd_step_n(self.h, C.c_void_p(actions.data_ptr()), int(actions.shape[0]), *ptrs,
+                                   _stream(self.device)))
+        self._steps += int(actions.shape[0])
+
     def flush(self):
         """Insert device-solved aero neighbourhoods into the tables (pd_flush_misses)."""
         L.check(self.lib.pd_flush_misses(self.h, _stream(self.device)))
