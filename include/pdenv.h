@@ -32,14 +32,14 @@
 extern "C" {
 #endif
 
-#define PD_ABI_VERSION 2
+#define PD_ABI_VERSION 3
 #define PD_MAX_PTS 256      /* aero scatter points per table */
 #define PD_MAX_COLS 5       /* AoA columns per aero table */
 #define PD_MAX_TAB 64       /* grid-fin table length */
 #define PD_MAX_WIND 16      /* nodes per wind profile */
 #define PD_N_WIND_PROFILES 50   /* integer percentiles 50..99 */
 #define PD_N_STATE 11       /* x y vx vy theta theta_dot gamma alpha mass mass_propellant time */
-#define PD_N_INFO 16        /* see pd_info_field */
+#define PD_N_INFO 49        /* see pd_info_field */
 /* simple_actor sizes of the PSO drivers (env_wrapped_ea.py:18-36, 174-185):
  * pure throttle 2-8-(8-8)x3-1, landing_burn 5-8-(8-8)x4-4 */
 #define PD_ACTOR_PARAMS_PURE_THROTTLE 249
@@ -142,10 +142,27 @@ typedef struct {
     int32_t trajectory_length, pad3;
 } pd_config;
 
+/* Info tap of pd_step: the quantities of the LAST physics sub-step that rocket_physics_fcn puts in
+ * its info dict (rockets_physics.py:649-702, incl. acceleration_dict / moments_dict), the
+ * action_info of the phase's control law and the ACS's acs_info (acs_model.py:62-86), and the
+ * env's g_load_1_sec_window (base_environment.py:149).  Layout [PD_N_INFO][N].  Entries that are
+ * arithmetic of these and the post-step state (accelerations, gravity_force_y, F_n_L = C_n_L qS,
+ * ...) are formed by the caller (pdenv/wrappers.py builds the reference's dict). */
 typedef enum {
     PD_INFO_AIR_DENSITY = 0, PD_INFO_PRESSURE, PD_INFO_SPEED_OF_SOUND, PD_INFO_MACH, PD_INFO_Q,
     PD_INFO_CL, PD_INFO_CD, PD_INFO_MASS_FLOW, PD_INFO_X_COG, PD_INFO_INERTIA, PD_INFO_ALPHA_EFF,
-    PD_INFO_THROTTLE, PD_INFO_GLOAD, PD_INFO_UG, PD_INFO_VG, PD_INFO_GIMBAL_DEG
+    PD_INFO_THROTTLE, PD_INFO_GLOAD, PD_INFO_UG, PD_INFO_VG, PD_INFO_GIMBAL_DEG,
+    PD_INFO_MACH_MAX,                  /* sqrt(2 Qmax / rho) / a, Qmax 30000 (200 above the ISA) */
+    PD_INFO_DRAG, PD_INFO_LIFT, PD_INFO_D_CP_CG, PD_INFO_D_THRUST_CG, PD_INFO_FUEL_CONSUMED,
+    PD_INFO_CF_PAR, PD_INFO_CF_PERP, PD_INFO_CF_X, PD_INFO_CF_Y, PD_INFO_AERO_X, PD_INFO_AERO_Y,
+    PD_INFO_GRAVITY,                   /* g at the sub-step's altitude */
+    PD_INFO_F_WIND_X, PD_INFO_F_WIND_Y, PD_INFO_VX_DOT, PD_INFO_VY_DOT,
+    PD_INFO_CONTROL_MOMENT, PD_INFO_AERO_MOMENT, PD_INFO_M_WIND, PD_INFO_MOMENTS, PD_INFO_THETA_DDOT,
+    PD_INFO_DCMD_L, PD_INFO_DCMD_R,    /* fin deflection commands (rad) */
+    PD_INFO_DELTA_L, PD_INFO_DELTA_R,  /* filtered fin deflections (rad) */
+    PD_INFO_GF_CA, PD_INFO_GF_CN_L, PD_INFO_GF_CN_R,   /* grid-fin C_a, C_n of the left/right fin */
+    PD_INFO_GF_F_PERP, PD_INFO_GF_F_PAR, PD_INFO_GF_MZ, /* grid-fin force perpendicular/parallel, moment */
+    PD_INFO_THETA_IN                   /* pitch at the start of the sub-step (the ACS's pitch_angle) */
 } pd_info_field;
 
 typedef struct pd_env pd_env;
@@ -230,11 +247,38 @@ pd_status pd_set_actuators(pd_env* env, const void* act, void* stream);
  * (0..10 valid entries).  Teacher forcing and checkpoint/restore. */
 pd_status pd_set_gload_window(pd_env* env, const void* vprev, const void* window, const uint8_t* len,
                               void* stream);
+/* g-load history read back: vprev [N], window [10][N] (ring slots), len and head [N] (the oldest
+ * entry is slot head when len == 10, slot 0 otherwise). */
+pd_status pd_get_gload_window(pd_env* env, void* vprev, void* window, uint8_t* len, uint8_t* head, void* stream);
 /* Per-env wind state: sigma_u, sigma_v [2][N] (double). */
 pd_status pd_set_wind_sigmas(pd_env* env, const double* sig, void* stream);
+/* Wind state (vonkarman.py:33-36 filter states, full_wind_model.py percentile): filters [4][N]
+ * (u0 u1 v0 v1, handle precision), sigmas [2][N] (handle precision), profile [N] uint8
+ * (percentile - 50).  Any pointer may be NULL. */
+pd_status pd_get_wind_state(pd_env* env, void* filters, void* sigmas, uint8_t* profile, void* stream);
+pd_status pd_set_wind_state(pd_env* env, const void* filters, const void* sigmas, const uint8_t* profile, void* stream);
+/* Episode bookkeeping: episode counter and step-within-episode [N] uint32 (the Philox counter
+ * words of the wind and reset draws), truncation id [N] int8.  Any pointer may be NULL. */
+pd_status pd_get_counters(pd_env* env, uint32_t* episode, uint32_t* step, int8_t* trunc_id, void* stream);
+pd_status pd_set_counters(pd_env* env, const uint32_t* episode, const uint32_t* step, const int8_t* trunc_id,
+                          void* stream);
+/* Checkpoint of every per-env buffer (state, g-load window, actuator memory, wind, counters,
+ * aero caches, episode flags) as one opaque device blob of pd_checkpoint_size() bytes: save
+ * into, load from a device buffer.  Restoring into a handle of the same configuration continues
+ * bit-identically (the Philox draws depend only on (seed, env, episode, step)). */
+size_t pd_checkpoint_size(const pd_env* env);
+pd_status pd_checkpoint_save(pd_env* env, void* blob, void* stream);
+pd_status pd_checkpoint_load(pd_env* env, const void* blob, void* stream);
 /* Counters since create: aero-table misses solved on device, NaN guard hits. Host sync. */
 pd_status pd_counters(pd_env* env, int64_t* rbf_misses, int64_t* table_entries_cd,
                       int64_t* table_entries_cl, int64_t* nan_events);
+/* The handle's ISA atmosphere (endo_atmospheric_model, atmosphere_dynamics.py:5-27) at n device
+ * altitudes [n] (handle precision): out [3][n] = density, pressure, speed of sound.  Used by the
+ * facade's maximum_velocity (env_wrapped_rl_pytorch.py:60-66). */
+pd_status pd_atmosphere(pd_env* env, const void* altitude, void* out, int64_t n, void* stream);
+/* All device statistics words (up to n): 0 misses, 1 NaN events, 2/3 table entries C_D/C_L,
+ * 16 solved neighbourhoods not queued (queue full; solved again until a later flush). */
+pd_status pd_stats(pd_env* env, int64_t* out, int32_t n);
 /* Observation / action widths of the handle. */
 int pd_obs_dim(const pd_env* env);
 int pd_action_dim(const pd_env* env);

@@ -63,6 +63,7 @@ class OrcParams(C.Structure):
         ("ref_y", D * MAXREF), ("ref_x", D * MAXREF), ("ref_vx", D * MAXREF), ("ref_vy", D * MAXREF),
         ("hyper", ((D * 9) * 12) * 2), ("terminal_mach", D * 2), ("speed0_pc", D),
         ("rl_discount", D), ("rl_traj_len", I32), ("pad2", I32),
+        ("wind_n_all", I32 * 50), ("wind_alt_all", (D * MAXW) * 50), ("wind_sp_all", (D * MAXW) * 50),
     ]
 
 
@@ -70,12 +71,19 @@ class OrcEnv(C.Structure):
     _fields_ = [("s", D * 11), ("prev_s", D * 11), ("gwin", D * 10), ("gwin_len", I32),
                 ("trunc_id", I32), ("gimbal_prev", D), ("dl_prev", D), ("dr_prev", D),
                 ("wind_on", I32), ("wind_stoch", I32), ("sigma_u", D), ("sigma_v", D),
-                ("fu", D * 2), ("fv", D * 2), ("noise_slotted", I32), ("noise_used", I32), ("dt", D)]
+                ("fu", D * 2), ("fv", D * 2), ("noise_slotted", I32), ("noise_used", I32), ("dt", D),
+                ("rng_philox", I32), ("wind_prof", I32), ("rng_g", C.c_uint64), ("rng_ep", C.c_uint32),
+                ("rng_ts", C.c_uint32), ("seed_lo", C.c_uint32), ("seed_hi", C.c_uint32),
+                ("cur_sub", I32), ("pad3", I32)]
 
 
 class OrcOut(C.Structure):
     _fields_ = [("reward", D), ("done", I32), ("trunc", I32), ("trunc_id", I32), ("pad", I32),
                 ("obs", D * 8), ("info", D * len(INFO_NAMES))]
+
+
+class OrcU32x4(C.Structure):
+    _fields_ = [("x", C.c_uint32), ("y", C.c_uint32), ("z", C.c_uint32), ("w", C.c_uint32)]
 
 
 def build():
@@ -119,6 +127,18 @@ def lib():
         L.orc_actor.argtypes = [P(OrcParams), C.c_int, P(C.c_float), P(D), P(C.c_float)]
         L.orc_rollout_policy.argtypes = [P(OrcParams), C.c_int, C.c_int, P(C.c_float), C.c_int, P(D),
                                          P(C.c_int32)]
+        L.orc_reset_philox.restype = None
+        L.orc_reset_philox.argtypes = [P(OrcParams), P(OrcEnv), C.c_int, C.c_uint64, C.c_uint64, C.c_uint32,
+                                       C.c_int, C.c_int, C.c_int, D]
+        L.orc_rollout_philox.restype = D
+        L.orc_rollout_philox.argtypes = [P(OrcParams), C.c_int, C.c_int, C.c_int, P(C.c_uint64), P(C.c_uint32),
+                                         C.c_int, P(C.c_float), C.c_int, C.c_int, C.c_int, C.c_int, D, C.c_uint64,
+                                         P(D), P(C.c_uint8), P(C.c_uint8), P(C.c_int8), P(D), C.c_int, P(D),
+                                         C.c_int, P(C.c_int64)]
+        L.orc_gauss_pair.restype = None
+        L.orc_gauss_pair.argtypes = [OrcU32x4, P(D), P(D)]
+        L.orc_philox.restype = OrcU32x4
+        L.orc_philox.argtypes = [OrcU32x4, C.c_uint32, C.c_uint32]
         L.orc_rollout.restype = D
         L.orc_rollout.argtypes = [P(OrcParams), C.c_int, C.c_int, C.c_int, C.c_int, P(C.c_float),
                                   C.c_int, P(C.c_int64)]
@@ -168,6 +188,9 @@ def make_params(pack=None, wind_percentile=50):
         cn["min_mach"], cn["max_mach"], cn["min_val"], cn["max_val"], cn["slope"])
     prof = [w for w in pk["wind_profiles"] if w["percentile"] == int(wind_percentile)][0]
     p.wind_n = len(prof["alt_km"]); _fill(p.wind_alt_km, prof["alt_km"]); _fill(p.wind_speed, prof["speed"])
+    for w in pk["wind_profiles"]:
+        k = int(w["percentile"]) - 50
+        p.wind_n_all[k] = len(w["alt_km"]); _fill(p.wind_alt_all[k], w["alt_km"]); _fill(p.wind_sp_all[k], w["speed"])
     vk = pk["von_karman"]
     _fill(p.vk_Ad_u, vk["Ad_u"]); _fill(p.vk_Bd_u, vk["Bd_u"]); _fill(p.vk_Ad_v, vk["Ad_v"]); _fill(p.vk_Bd_v, vk["Bd_v"])
     p.vk_y_threshold = vk["y_threshold"]
@@ -292,6 +315,40 @@ def rollout(phase, rtd, n_env, n_steps, actions_f32, auto_reset=True, wind=False
                                acts.ctypes.data_as(C.POINTER(C.c_float)), int(auto_reset), int(wind),
                                float(tilt), int(seed), int(threads), C.byref(steps))
     return acc, steps.value
+
+
+def rollout_philox(phase, rtd, g, ep0, actions_f32, auto_reset=True, wind=True, stochastic=True, fixed_prof=-1,
+                   tilt=0.0, seed=0, obs_dim=2, threads=8, outputs=True):
+    """The envs with global indices g (first episode ep0) under the device's Philox draw scheme,
+    T steps of actions [T, n, A] float32: per-step reward/done/trunc/trunc_id [T, n], obs
+    [T, n, obs_dim] and the final state [n, 11] (outputs=False: only (sum, env-steps))."""
+    acts = np.ascontiguousarray(actions_f32, dtype=np.float32)
+    T, n = acts.shape[0], acts.shape[1]
+    g = np.ascontiguousarray(g, dtype=np.uint64)
+    ep0 = np.ascontiguousarray(ep0, dtype=np.uint32)
+    P = C.POINTER
+    out = dict(reward=np.zeros((T, n)), done=np.zeros((T, n), np.uint8), trunc=np.zeros((T, n), np.uint8),
+               trunc_id=np.zeros((T, n), np.int8), obs=np.zeros((T, n, max(obs_dim, 1))), state=np.zeros((n, 11)))
+    ptr = lambda a, t: a.ctypes.data_as(P(t)) if outputs else None
+    steps = C.c_int64()
+    acc = lib().orc_rollout_philox(C.byref(params()), phase, rtd, n, g.ctypes.data_as(P(C.c_uint64)),
+                                   ep0.ctypes.data_as(P(C.c_uint32)), T, acts.ctypes.data_as(P(C.c_float)),
+                                   int(auto_reset), int(wind), int(stochastic), int(fixed_prof), float(tilt), int(seed),
+                                   ptr(out["reward"], D), ptr(out["done"], C.c_uint8), ptr(out["trunc"], C.c_uint8),
+                                   ptr(out["trunc_id"], C.c_int8), ptr(out["obs"], D), int(obs_dim),
+                                   ptr(out["state"], D), int(threads), C.byref(steps))
+    if not outputs:
+        return acc, steps.value
+    return out
+
+
+def gauss_pair(seed, counter):
+    """Two normals of the device scheme for Philox counter (c0, c1, c2, c3) under key `seed`."""
+    c = OrcU32x4(*[int(v) & 0xFFFFFFFF for v in counter])
+    r = lib().orc_philox(c, int(seed) & 0xFFFFFFFF, (int(seed) >> 32) & 0xFFFFFFFF)
+    z0, z1 = D(), D()
+    lib().orc_gauss_pair(r, C.byref(z0), C.byref(z1))
+    return z0.value, z1.value
 
 
 def actor(phase, w, state):

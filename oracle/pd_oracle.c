@@ -264,14 +264,99 @@ static acs_res acs(const orc_params* P, double alpha_eff, double q, double mach,
 }
 
 /* ---------------------------------------------------------------- wind (full_wind_model.py:35-43) */
-static double wind_profile(const orc_params* P, double y) {
-    /* HorizontalWindSpeed.py:58-68: interp1d(alt_km, speed, fill_value=(first,last)) */
+static double wind_profile(const orc_params* P, const orc_env* E, double y) {
+    /* HorizontalWindSpeed.py:58-68: interp1d(alt_km, speed, fill_value=(first,last)) of the
+     * env's percentile (E->wind_prof) or of P's single profile */
     double km = y / 1000.0;
-    int n = P->wind_n;
-    if (km < P->wind_alt_km[0]) return P->wind_speed[0];
-    if (km > P->wind_alt_km[n - 1]) return P->wind_speed[n - 1];
-    return np_interp(P->wind_alt_km, P->wind_speed, n, km);
+    const int w = E->wind_prof;
+    const int n = w >= 0 ? P->wind_n_all[w] : P->wind_n;
+    const double* xa = w >= 0 ? P->wind_alt_all[w] : P->wind_alt_km;
+    const double* ya = w >= 0 ? P->wind_sp_all[w] : P->wind_speed;
+    if (km < xa[0]) return ya[0];
+    if (km > xa[n - 1]) return ya[n - 1];
+    return np_interp(xa, ya, n, km);
 }
+
+/* ---------------------------------------------------------------- the device's random draws
+ * Restatement of libpdenv's scheme (test infrastructure, so that a stochastic env can be
+ * followed env for env): Philox4x32-10 (Salmon et al., SC'11; constants of the Random123
+ * reference), 53-bit uniforms, Box-Muller with a cell-table log (512 cells, degree-5 log1p)
+ * and fdlibm's sin/cos kernels -- IEEE +, *, fma, sqrt and rint only, so the draws are the
+ * device's bit for bit. */
+orc_u32x4 orc_philox(orc_u32x4 c, uint32_t k0, uint32_t k1) {
+    for (int r = 0; r < 10; ++r) {
+        uint64_t p0 = (uint64_t)0xD2511F53u * c.x;
+        uint64_t p1 = (uint64_t)0xCD9E8D57u * c.z;
+        orc_u32x4 n;
+        n.x = (uint32_t)(p1 >> 32) ^ c.y ^ k0;
+        n.y = (uint32_t)p1;
+        n.z = (uint32_t)(p0 >> 32) ^ c.w ^ k1;
+        n.w = (uint32_t)p0;
+        c = n;
+        k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+    }
+    return c;
+}
+double orc_u01(uint32_t hi, uint32_t lo) {
+    return ((double)(hi >> 5) * 67108864.0 + (double)(lo >> 6)) * (1.0 / 9007199254740992.0);
+}
+#define ORC_LOG_CELLS 512
+static double g_invc[ORC_LOG_CELLS], g_logc[ORC_LOG_CELLS];
+static pthread_once_t g_log_once = PTHREAD_ONCE_INIT;
+static void log_cells_fill(void) {
+    for (int i = 0; i < ORC_LOG_CELLS; ++i) {
+        long double c = 1.0L + (i + 0.5L) / ORC_LOG_CELLS;
+        double invc = (double)(1.0L / c);
+        g_invc[i] = invc;
+        g_logc[i] = (double)(-logl((long double)invc));
+    }
+}
+static double log_cells(double x) {
+    uint64_t b;
+    memcpy(&b, &x, 8);
+    uint32_t hi = (uint32_t)(b >> 32);
+    double e = (double)((int)(hi >> 20) - 1023);
+    uint32_t i = (hi >> (20 - 9)) & (ORC_LOG_CELLS - 1);
+    uint64_t mb = (b & 0x000fffffffffffffull) | 0x3ff0000000000000ull;
+    double m;
+    memcpy(&m, &mb, 8);
+    double r = fma(m, g_invc[i], -1.0);
+    double t = fma(r, 0.2, -0.25);
+    t = fma(r, t, 1.0 / 3.0);
+    t = fma(r, t, -0.5);
+    double p = fma(r * r, t, r);
+    return fma(e, 6.93147180559945286227e-01, g_logc[i] + p);
+}
+static void sincos_fd(double x, double* s, double* c) {
+    if (!(fabs(x) < 1.0e6)) { *s = sin(x); *c = cos(x); return; }
+    const double k = rint(x * 6.36619772367581382433e-01);
+    const double r1 = fma(-k, 1.57079632679489655800e+00, x);
+    const double ph = k * 6.12323399573676603587e-17;
+    const double pl = fma(k, 6.12323399573676603587e-17, -ph) + k * -1.4973849048591698e-33;
+    const double r = r1 - ph;
+    const double y = ((r1 - r) - ph) - pl;
+    const double z = r * r, v = z * r, w = z * z;
+    const double ps = 8.33333333332248946124e-03 + z * (-1.98412698298579493134e-04 + z * (2.75573137070700676789e-06 +
+                      z * (-2.50507602534068634195e-08 + z * 1.58969099521155010221e-10)));
+    const double sn = r - ((z * (0.5 * y - v * ps) - y) - v * -1.66666666666666324348e-01);
+    const double pc = z * (4.16666666666666019037e-02 + z * (-1.38888888888741095749e-03 + z * 2.48015872894767294178e-05)) +
+                      w * w * (-2.75573143513906633035e-07 + z * (2.08757232129817482790e-09 + z * -1.13596475577881948265e-11));
+    const double hz = 0.5 * z, ww = 1.0 - hz;
+    const double cs = ww + (((1.0 - ww) - hz) + (z * pc - r * y));
+    const int q = (int)(long long)k & 3;
+    *s = q == 0 ? sn : (q == 1 ? cs : (q == 2 ? -sn : -cs));
+    *c = q == 0 ? cs : (q == 1 ? -sn : (q == 2 ? -cs : sn));
+}
+void orc_gauss_pair(orc_u32x4 r, double* z0, double* z1) {
+    pthread_once(&g_log_once, log_cells_fill);
+    const double u1 = 1.0 - orc_u01(r.x, r.y), u2 = orc_u01(r.z, r.w);
+    const double rho = sqrt(-2.0 * log_cells(u1));
+    double s, c;
+    sincos_fd(6.283185307179586 * u2, &s, &c);
+    *z0 = rho * c;
+    *z1 = rho * s;
+}
+enum { ORC_TAG_WIND_SUB = 0, ORC_TAG_RESET = 16, ORC_TAG_TILT = 17 };
 
 static void vk_step(const double* Ad, const double* Bd, double sigma, double* s, double w) {
     /* vonkarman.py:33-36: state = Ad @ state + Bd * w, Bd = sigma * Bd(sigma=1) */
@@ -307,13 +392,17 @@ static void substep(const orc_params* P, orc_env* E, int phase, const double* u,
     double d_cp_cg = x_cog - (ascent ? P->cop_ascent : P->cop);
     double ug = 0.0, vg = 0.0;
     if (E->wind_on) {
-        ug = wind_profile(P, y);
+        ug = wind_profile(P, E, y);
         if (y < P->vk_y_threshold && E->wind_stoch) {
             /* vonkarman.py:34: one np.random.randn() per filter step, u first then v */
             double w0 = 0.0, w1 = 0.0;
             if (noise2) {
                 int off = E->noise_slotted ? 0 : E->noise_used;
                 w0 = noise2[off]; w1 = noise2[off + 1];
+            } else if (E->rng_philox) {
+                orc_u32x4 c = {(uint32_t)E->rng_g, (uint32_t)(E->rng_g >> 32) ^ E->rng_ep, E->rng_ts,
+                               ORC_TAG_WIND_SUB + (uint32_t)E->cur_sub};
+                orc_gauss_pair(orc_philox(c, E->seed_lo, E->seed_hi), &w0, &w1);
             }
             E->noise_used += 2;
             vk_step(P->vk_Ad_u, P->vk_Bd_u, E->sigma_u, E->fu, w0);
@@ -563,11 +652,14 @@ int orc_physics(const orc_params* P, orc_env* E, int phase, const double* u, int
         /* the other phases: one call of rocket_physics_fcn at the env dt (:728-802, :959-997);
          * actuator filters at the same dt */
         double d = E->dt > 0 ? E->dt : 0.1;
+        E->cur_sub = 0;
         substep(P, E, phase, u, f32, d, d, noise, info);
         return 0;
     }
-    for (int k = 0; k < 4; ++k)
+    for (int k = 0; k < 4; ++k) {
+        E->cur_sub = k;
         substep(P, E, phase, u, f32, dt, 0.025, noise ? (E->noise_slotted ? noise + 2 * k : noise) : NULL, info);
+    }
     if (phase == ORC_PHASE_LANDING_BURN && info) {
         /* base_environment.py:122-124: prevs <- filtered gimbal, fin COMMANDS */
         E->gimbal_prev = info[ORC_I_GIMBAL_DEG];
@@ -583,6 +675,34 @@ void orc_reset(const orc_params* P, orc_env* E, const double* s0, int wind_on, i
     memcpy(E->s, s0 ? s0 : P->state0, sizeof(E->s));
     memcpy(E->prev_s, E->s, sizeof(E->s));
     E->wind_on = wind_on; E->wind_stoch = wind_stoch; E->sigma_u = sigma_u; E->sigma_v = sigma_v;
+    E->wind_prof = -1;
+}
+
+/* base_environment.py:80-97 with the device's draws (libpdenv reset_values): the phase's initial
+ * state, pitch tilt N(0, tilt) (theta += tilt z, alpha = theta - gamma), sigma_u ~ U(0.5, 2.25),
+ * sigma_v ~ U(1.25, 2.0) (vonkarman.py:60-66) and the percentile randint(50, 99)
+ * (full_wind_model.py:27-33) unless fixed. */
+void orc_reset_philox(const orc_params* P, orc_env* E, int phase, uint64_t seed, uint64_t g,
+                      uint32_t episode, int wind_on, int wind_stoch, int fixed_prof, double tilt) {
+    double s0[11];
+    memcpy(s0, P->state0_ph[phase], sizeof(s0));
+    const uint32_t klo = (uint32_t)seed, khi = (uint32_t)(seed >> 32);
+    if (tilt > 0) {
+        orc_u32x4 c = {(uint32_t)g, (uint32_t)(g >> 32) ^ episode, 0u, ORC_TAG_TILT};
+        double z0, z1;
+        orc_gauss_pair(orc_philox(c, klo, khi), &z0, &z1);
+        s0[4] = s0[4] + tilt * z0;
+        s0[7] = s0[4] - s0[6];
+    }
+    orc_u32x4 c = {(uint32_t)g, (uint32_t)(g >> 32) ^ episode, 0u, ORC_TAG_RESET};
+    orc_u32x4 r = orc_philox(c, klo, khi);
+    const double su = 0.5 + (2.25 - 0.5) * orc_u01(r.x, r.y);
+    const double sv = 1.25 + (2.0 - 1.25) * orc_u01(r.z, r.w);
+    orc_reset(P, E, s0, wind_on, wind_stoch, su, sv);
+    E->wind_prof = wind_on ? (fixed_prof >= 0 ? fixed_prof : (int)((r.x ^ r.w) % 49u)) : -1;
+    E->rng_philox = 1;
+    E->rng_g = g; E->rng_ep = episode; E->rng_ts = 0;
+    E->seed_lo = klo; E->seed_hi = khi;
 }
 
 /* ---------------------------------------------------------------- rtd */
@@ -876,6 +996,7 @@ int orc_step(const orc_params* P, orc_env* E, int phase, int rtd, const double* 
     else if (phase == ORC_PHASE_SUBSONIC || phase == ORC_PHASE_SUPERSONIC)
         rtd_rl_ascent(P, E, phase == ORC_PHASE_SUPERSONIC, o);
     E->trunc_id = o->trunc_id;
+    E->rng_ts += 1;   /* the device's step-within-episode counter (Philox counter word) */
     memcpy(E->prev_s, E->s, sizeof(E->s));
     /* observations: RL pure throttle (env_wrapped_rl_pytorch.py:195-198), PSO (env_wrapped_ea.py:108-122) */
     if (rtd != ORC_RTD_PSO) {   /* the RL wrapper casts the state to float32 first */
@@ -891,97 +1012,96 @@ int orc_step(const orc_params* P, orc_env* E, int phase, int rtd, const double* 
     return 0;
 }
 
-/* CPU baseline driver: n_env independent envs stepped in a static loop (the reference runs
- * one env per process; this is its scalar port).  Optional stochastic wind (sigmas and
- * normals from a xorshift64* + Box-Muller stream) and initial tilt N(0, tilt_sigma). */
-static uint64_t xs_next(uint64_t* s) { uint64_t x = *s; x ^= x >> 12; x ^= x << 25; x ^= x >> 27; *s = x; return x * 2685821657736338717ull; }
-static double xs_u01(uint64_t* s) { return (double)(xs_next(s) >> 11) * (1.0 / 9007199254740992.0); }
-static double xs_normal(uint64_t* s) {
-    double u1 = 1.0 - xs_u01(s), u2 = xs_u01(s);
-    return sqrt(-2.0 * log(u1)) * cos(2.0 * PI * u2);
-}
-static void rollout_reset(const orc_params* P, orc_env* E, int wind, double tilt, uint64_t* rng) {
-    double s0[11];
-    memcpy(s0, P->state0, sizeof(s0));
-    if (tilt > 0) { s0[4] += tilt * xs_normal(rng); s0[7] = s0[4] - s0[6]; }
-    orc_reset(P, E, s0, wind, wind, 0.5 + 1.75 * xs_u01(rng), 1.25 + 0.75 * xs_u01(rng));
-    E->noise_slotted = 1;
-}
-double orc_rollout(const orc_params* P, int phase, int rtd, int n_env, int n_steps,
-                   const float* actions, int auto_reset, int64_t* env_steps_out) {
-    return orc_rollout_ex(P, phase, rtd, n_env, n_steps, actions, auto_reset, 0, 0.0, 1, env_steps_out);
-}
-/* Envs [i0, i1) of a rollout over n_env envs (actions [T][n_env][A]); own RNG stream. */
-static double rollout_range(const orc_params* P, int phase, int rtd, int i0, int i1, int n_env, int n_steps,
-                            const float* actions, int auto_reset, int wind, double tilt, uint64_t seed,
-                            int64_t* env_steps_out) {
-    int A = phase == ORC_PHASE_PURE_THROTTLE ? 1 : 4;
-    int n = i1 - i0;
-    uint64_t rng = seed ? seed : 1;
-    orc_env* envs = (orc_env*)malloc(sizeof(orc_env) * (size_t)(n > 0 ? n : 1));
-    for (int i = 0; i < n; ++i) rollout_reset(P, &envs[i], wind, tilt, &rng);
-    double acc = 0.0; int64_t steps = 0;
-    orc_out o;
-    double nz[8];
-    for (int t = 0; t < n_steps; ++t) {
-        for (int i = 0; i < n; ++i) {
-            double u[4];
-            for (int k = 0; k < A; ++k) u[k] = actions[((size_t)t * n_env + i0 + i) * A + k];
-            if (wind) for (int k = 0; k < 8; ++k) nz[k] = xs_normal(&rng);
-            orc_step(P, &envs[i], phase, rtd, u, 1, wind ? nz : NULL, &o);
-            acc += o.reward; ++steps;
-            if (auto_reset && (o.done || o.trunc)) rollout_reset(P, &envs[i], wind, tilt, &rng);
-        }
-    }
-    free(envs);
-    if (env_steps_out) *env_steps_out = steps;
-    return acc;
-}
-
-double orc_rollout_ex(const orc_params* P, int phase, int rtd, int n_env, int n_steps,
-                      const float* actions, int auto_reset, int wind, double tilt, uint64_t seed,
-                      int64_t* env_steps_out) {
-    return rollout_range(P, phase, rtd, 0, n_env, n_env, n_steps, actions, auto_reset, wind, tilt, seed,
-                         env_steps_out);
-}
-
+/* Batched rollout with the device's draws: envs [i0, i1) of n (global indices g[i], first
+ * episode ep0[i]), actions [T][n][A] float32, auto-reset into episode + 1. */
 typedef struct {
-    const orc_params* P; int phase, rtd, i0, i1, n_env, n_steps; const float* actions;
-    int auto_reset, wind; double tilt; uint64_t seed; double acc; int64_t steps;
-} rollout_job;
+    const orc_params* P; int phase, rtd, n, i0, i1, n_steps; const uint64_t* g; const uint32_t* ep0;
+    const float* actions; int auto_reset, wind, stoch, fixed_prof; double tilt; uint64_t seed;
+    double* reward; uint8_t* done; uint8_t* trunc; int8_t* tid; double* obs; int obs_dim; double* state_final;
+    double acc; int64_t steps;
+} philox_job;
 
-static void* rollout_worker(void* p) {
-    rollout_job* j = (rollout_job*)p;
-    j->acc = rollout_range(j->P, j->phase, j->rtd, j->i0, j->i1, j->n_env, j->n_steps, j->actions,
-                           j->auto_reset, j->wind, j->tilt, j->seed, &j->steps);
-    return NULL;
+static void philox_range(philox_job* j) {
+    const orc_params* P = j->P;
+    const int A = j->phase == ORC_PHASE_LANDING_BURN ? 4 : ((j->phase == ORC_PHASE_SUBSONIC || j->phase == ORC_PHASE_SUPERSONIC) ? 2 : 1);
+    double acc = 0.0; int64_t steps = 0;
+    orc_env E;
+    orc_out o;
+    for (int i = j->i0; i < j->i1; ++i) {
+        uint32_t ep = j->ep0 ? j->ep0[i] : 0u;
+        const uint64_t g = j->g ? j->g[i] : (uint64_t)i;
+        orc_reset_philox(P, &E, j->phase, j->seed, g, ep, j->wind, j->stoch, j->fixed_prof, j->tilt);
+        for (int t = 0; t < j->n_steps; ++t) {
+            double u[4] = {0, 0, 0, 0};
+            for (int k = 0; k < A; ++k) u[k] = j->actions[((size_t)t * j->n + i) * A + k];
+            orc_step(P, &E, j->phase, j->rtd, u, 1, NULL, &o);
+            acc += o.reward; ++steps;
+            const size_t at = (size_t)t * j->n + i;
+            if (j->reward) j->reward[at] = o.reward;
+            if (j->done) j->done[at] = (uint8_t)o.done;
+            if (j->trunc) j->trunc[at] = (uint8_t)o.trunc;
+            if (j->tid) j->tid[at] = (int8_t)o.trunc_id;
+            if (j->obs) for (int k = 0; k < j->obs_dim; ++k) j->obs[at * j->obs_dim + k] = o.obs[k];
+            if (j->auto_reset && (o.done || o.trunc)) {
+                ++ep;
+                orc_reset_philox(P, &E, j->phase, j->seed, g, ep, j->wind, j->stoch, j->fixed_prof, j->tilt);
+            }
+        }
+        if (j->state_final) memcpy(j->state_final + (size_t)i * 11, E.s, sizeof(E.s));
+    }
+    j->acc = acc; j->steps = steps;
 }
+static void* philox_worker(void* p) { philox_range((philox_job*)p); return NULL; }
 
-/* The same rollout on n_threads host threads over a static contiguous env partition (the
- * multi-core CPU baseline); thread k draws its wind noise from seed + k. */
-double orc_rollout_mt(const orc_params* P, int phase, int rtd, int n_env, int n_steps,
-                      const float* actions, int auto_reset, int wind, double tilt, uint64_t seed,
-                      int n_threads, int64_t* env_steps_out) {
+double orc_rollout_philox(const orc_params* P, int phase, int rtd, int n, const uint64_t* g, const uint32_t* ep0,
+                          int n_steps, const float* actions, int auto_reset, int wind, int stoch, int fixed_prof,
+                          double tilt, uint64_t seed, double* reward, uint8_t* done, uint8_t* trunc, int8_t* tid,
+                          double* obs, int obs_dim, double* state_final, int n_threads, int64_t* env_steps_out) {
+    pthread_once(&g_log_once, log_cells_fill);
     if (n_threads < 1) n_threads = 1;
-    if (n_threads > n_env) n_threads = n_env;
-    rollout_job* jobs = (rollout_job*)calloc((size_t)n_threads, sizeof(rollout_job));
+    if (n_threads > n) n_threads = n > 0 ? n : 1;
+    philox_job* jobs = (philox_job*)calloc((size_t)n_threads, sizeof(philox_job));
     pthread_t* th = (pthread_t*)calloc((size_t)n_threads, sizeof(pthread_t));
     for (int k = 0; k < n_threads; ++k) {
-        rollout_job* j = &jobs[k];
-        j->P = P; j->phase = phase; j->rtd = rtd; j->n_env = n_env; j->n_steps = n_steps;
-        j->i0 = (int)((int64_t)n_env * k / n_threads); j->i1 = (int)((int64_t)n_env * (k + 1) / n_threads);
-        j->actions = actions; j->auto_reset = auto_reset; j->wind = wind; j->tilt = tilt;
-        j->seed = seed + (uint64_t)k;
-        pthread_create(&th[k], NULL, rollout_worker, j);
+        philox_job* j = &jobs[k];
+        j->P = P; j->phase = phase; j->rtd = rtd; j->n = n; j->n_steps = n_steps; j->g = g; j->ep0 = ep0;
+        j->i0 = (int)((int64_t)n * k / n_threads); j->i1 = (int)((int64_t)n * (k + 1) / n_threads);
+        j->actions = actions; j->auto_reset = auto_reset; j->wind = wind; j->stoch = stoch;
+        j->fixed_prof = fixed_prof; j->tilt = tilt; j->seed = seed;
+        j->reward = reward; j->done = done; j->trunc = trunc; j->tid = tid; j->obs = obs; j->obs_dim = obs_dim;
+        j->state_final = state_final;
+        if (n_threads > 1) pthread_create(&th[k], NULL, philox_worker, j);
+        else philox_range(j);
     }
     double acc = 0.0; int64_t steps = 0;
     for (int k = 0; k < n_threads; ++k) {
-        pthread_join(th[k], NULL);
+        if (n_threads > 1) pthread_join(th[k], NULL);
         acc += jobs[k].acc; steps += jobs[k].steps;
     }
     free(jobs); free(th);
     if (env_steps_out) *env_steps_out = steps;
     return acc;
+}
+
+/* CPU baseline driver: n_env independent envs (the reference runs one env per process; this is
+ * its scalar port), the device's draws for wind and tilt (seed, env i, episodes from 0). */
+double orc_rollout(const orc_params* P, int phase, int rtd, int n_env, int n_steps,
+                   const float* actions, int auto_reset, int64_t* env_steps_out) {
+    return orc_rollout_ex(P, phase, rtd, n_env, n_steps, actions, auto_reset, 0, 0.0, 1, env_steps_out);
+}
+double orc_rollout_ex(const orc_params* P, int phase, int rtd, int n_env, int n_steps,
+                      const float* actions, int auto_reset, int wind, double tilt, uint64_t seed,
+                      int64_t* env_steps_out) {
+    return orc_rollout_philox(P, phase, rtd, n_env, NULL, NULL, n_steps, actions, auto_reset, wind, wind, -1, tilt,
+                              seed, NULL, NULL, NULL, NULL, NULL, 0, NULL, 1, env_steps_out);
+}
+/* The same on n_threads host threads over a static contiguous env partition (the multi-core
+ * CPU baseline). */
+double orc_rollout_mt(const orc_params* P, int phase, int rtd, int n_env, int n_steps,
+                      const float* actions, int auto_reset, int wind, double tilt, uint64_t seed,
+                      int n_threads, int64_t* env_steps_out) {
+    return orc_rollout_philox(P, phase, rtd, n_env, NULL, NULL, n_steps, actions, auto_reset, wind, wind, -1, tilt,
+                              seed, NULL, NULL, NULL, NULL, NULL, 0, NULL, n_threads, env_steps_out);
 }
 
 /* ---------------------------------------------------------------- PSO actor (test oracle)

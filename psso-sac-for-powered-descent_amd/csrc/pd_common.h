@@ -242,4 +242,45 @@ constexpr uint32_t kTagWindSub = 0;   // +substep 0..3
 constexpr uint32_t kTagReset = 16;
 constexpr uint32_t kTagTilt = 17;
 
+// ---------------------------------------------------------------- sine and cosine together
+// Binary64 sin and cos of one angle in one pass: reduction by pi/2 to a double-double r + y
+// (the first fma term is exact for |k| < 2^20; beyond 1e6 rad, the library), then the
+// public-domain fdlibm kernels k_sin.c / k_cos.c with their tail argument, and a quadrant swap.
+// <= 1 ulp against long double over 2e7 arguments.  Only IEEE +, *, fma and rint: the host and
+// the device give the same bits (the wind normals below rely on that).
+PD_HD void sincos_fd(double x, double& s, double& c) {
+    if (!(fabs(x) < 1.0e6)) { s = sin(x); c = cos(x); return; }   // huge or NaN
+    const double k = rint(x * 6.36619772367581382433e-01);
+    const double r1 = fma(-k, 1.57079632679489655800e+00, x);      // exact for |k| < 2^20
+    const double ph = k * 6.12323399573676603587e-17;               // k (pi/2 - high), two terms
+    const double pl = fma(k, 6.12323399573676603587e-17, -ph) + k * -1.4973849048591698e-33;
+    const double r = r1 - ph;                                       // reduced angle r + y
+    const double y = ((r1 - r) - ph) - pl;
+    const double z = r * r, v = z * r, w = z * z;
+    const double ps = 8.33333333332248946124e-03 + z * (-1.98412698298579493134e-04 + z * (2.75573137070700676789e-06 +
+                      z * (-2.50507602534068634195e-08 + z * 1.58969099521155010221e-10)));
+    const double sn = r - ((z * (0.5 * y - v * ps) - y) - v * -1.66666666666666324348e-01);
+    const double pc = z * (4.16666666666666019037e-02 + z * (-1.38888888888741095749e-03 + z * 2.48015872894767294178e-05)) +
+                      w * w * (-2.75573143513906633035e-07 + z * (2.08757232129817482790e-09 + z * -1.13596475577881948265e-11));
+    const double hz = 0.5 * z, ww = 1.0 - hz;
+    const double cs = ww + (((1.0 - ww) - hz) + (z * pc - r * y));
+    const int q = (int)(long long)k & 3;
+    s = q == 0 ? sn : (q == 1 ? cs : (q == 2 ? -sn : -cs));
+    c = q == 0 ? cs : (q == 1 ? -sn : (q == 2 ? -cs : sn));
+}
+
+// Two standard normals from one Philox4x32-10 block by Box-Muller in binary64:
+// u1 = 1 - u01(x, y) in (0, 1], u2 = u01(z, w); rho = sqrt(-2 log u1); (rho cos 2 pi u2,
+// rho sin 2 pi u2).  The log is log_tab (cell table from log_table_fill), sqrt is correctly
+// rounded, sincos_fd is IEEE-only: the oracle restates this and draws the same bits.  The
+// wind gusts (vonkarman.py:34, one np.random.randn() per filter step) and the tilt use it.
+PD_HD void gauss_pair(u32x4 r, const double* invc, const double* logc, double& z0, double& z1) {
+    const double u1 = 1.0 - u01(r.x, r.y), u2 = u01(r.z, r.w);
+    const double rho = sqrt(-2.0 * log_tab(u1, invc, logc));
+    double s, c;
+    sincos_fd(6.283185307179586 * u2, s, c);
+    z0 = rho * c;
+    z1 = rho * s;
+}
+
 }  // namespace pd

@@ -21,6 +21,13 @@ template <> struct Cst<float> {
 
 constexpr int kLineMax = 96;   // breakpoints per clamped query line
 
+// Address spaces of the step kernel's memory: the per-handle parameter block is read through a
+// constant-address-space view (uniform fields become scalar loads into SGPRs), the tables behind
+// its pointers through global-address-space pointers (global_load, not flat: a flat load waits
+// on both the LDS and the vector-memory counters).
+#define PD_AS1 __attribute__((address_space(1)))
+#define PD_AS4 __attribute__((address_space(4)))
+
 // Device parameter block (one per handle, in HBM, read with uniform scalar loads).
 template <typename R> struct DevParams {
     // sizing
@@ -94,6 +101,13 @@ template <typename R> struct DevParams {
     R terminal_mach;
     R rl_scale, alive_bonus, log_1p_max_ae;   // (1-g)/(1-g^L), 0.01 (1-g), log(1 + radians(20))
 };
+template <typename R> using DP = const PD_AS4 DevParams<R>;
+template <typename T> __device__ __forceinline__ const PD_AS1 T* gbl(const T* p) { return (const PD_AS1 T*)(uint64_t)p; }
+template <typename T> __device__ __forceinline__ PD_AS1 T* gblw(T* p) { return (PD_AS1 T*)(uint64_t)p; }
+
+// ISA layer constants staged in LDS per workgroup (the layer is a per-lane index):
+// Hb, Tb, beta, pb, beta/Tb, exponent -g0/(beta R), isothermal -g0/(R Tb), pad
+constexpr int kIsaCols = 8;
 
 // ---------------------------------------------------------------- logarithms
 // Hot-path log(): binary64 through the LDS-staged cell table (log_tab, pd_common.h; the step
@@ -108,11 +122,7 @@ template <> __device__ __forceinline__ float eval_log<float>(float x) {
 }
 
 // ---------------------------------------------------------------- sine and cosine together
-// Binary64 sin and cos of one angle in one pass (the step kernel needs both of alpha_eff, of
-// theta, ...): reduction by pi/2 to a double-double r + y (the first fma term is exact for
-// |k| < 2^20; beyond 1e6 rad, the device library), then the public-domain fdlibm kernels
-// k_sin.c / k_cos.c with their tail argument, and a quadrant swap.  Error <= 1 ulp against
-// long double over 2e7 arguments, like the device library's (neither is glibc's bit for bit).
+// Binary64: sincos_fd (pd_common.h, fdlibm kernels, <= 1 ulp); binary32: the device library.
 template <typename R> __device__ __forceinline__ void pd_sincos(R x, R& s, R& c) {
     s = sin(x); c = cos(x);
 }
@@ -120,47 +130,31 @@ template <> __device__ __forceinline__ void pd_sincos<double>(double x, double& 
 #ifdef PD_LIB_TRIG
     s = sin(x); c = cos(x);
 #else
-    if (!(fabs(x) < 1.0e6)) { s = sin(x); c = cos(x); return; }   // huge or NaN
-    const double k = rint(x * 6.36619772367581382433e-01);
-    const double r1 = fma(-k, 1.57079632679489655800e+00, x);      // exact for |k| < 2^20
-    const double ph = k * 6.12323399573676603587e-17;               // k (pi/2 - high), two terms
-    const double pl = fma(k, 6.12323399573676603587e-17, -ph) + k * -1.4973849048591698e-33;
-    const double r = r1 - ph;                                       // reduced angle r + y
-    const double y = ((r1 - r) - ph) - pl;
-    const double z = r * r, v = z * r, w = z * z;
-    const double ps = 8.33333333332248946124e-03 + z * (-1.98412698298579493134e-04 + z * (2.75573137070700676789e-06 +
-                      z * (-2.50507602534068634195e-08 + z * 1.58969099521155010221e-10)));
-    const double sn = r - ((z * (0.5 * y - v * ps) - y) - v * -1.66666666666666324348e-01);
-    const double pc = z * (4.16666666666666019037e-02 + z * (-1.38888888888741095749e-03 + z * 2.48015872894767294178e-05)) +
-                      w * w * (-2.75573143513906633035e-07 + z * (2.08757232129817482790e-09 + z * -1.13596475577881948265e-11));
-    const double hz = 0.5 * z, ww = 1.0 - hz;
-    const double cs = ww + (((1.0 - ww) - hz) + (z * pc - r * y));
-    const int q = (int)(long long)k & 3;
-    s = q == 0 ? sn : (q == 1 ? cs : (q == 2 ? -sn : -cs));
-    c = q == 0 ? cs : (q == 1 ? -sn : (q == 2 ? -cs : sn));
+    sincos_fd(x, s, c);
 #endif
 }
 
 // ---------------------------------------------------------------- atmosphere
 // atmosphere_dynamics.py:5-27 (ambiance ISA restated)
 template <typename R>
-__device__ __forceinline__ void atmosphere(const DevParams<R>& P, R y, R& rho, R& p, R& a) {
+__device__ __forceinline__ void atmosphere(DP<R>& P, const R* isa, R y, R& rho, R& p, R& a) {
     R alt = y < R(0) ? R(0) : y;
     if (alt < P.isa_alt_max) {
         R H = P.isa_r * alt / (P.isa_r + alt);
         int i = 0;
 #pragma unroll
-        for (int k = 1; k < 9; ++k) i = (P.isa_Hb[k] <= H) ? k : i;
-        R Hb = P.isa_Hb[i], Tb = P.isa_Tb[i], b = P.isa_beta[i], pb = P.isa_pb[i];
+        for (int k = 1; k < 9; ++k) i = (P.isa_Hb[k] <= H) ? k : i;   // uniform bases (SGPRs)
+        const R* L = isa + i * kIsaCols;                                  // the lane's layer (LDS)
+        R Hb = L[0], Tb = L[1], b = L[2], pb = L[3];
         R dH = H - Hb;
         R T = Tb + b * dH;
         R pp;
         // (1 + beta/Tb dH)^ex; binary64 as exp(ex log(.)) with the table log (|err| < 1e-15 rel)
         if (b != R(0)) {
-            if constexpr (sizeof(R) == 8) pp = pb * exp(P.isa_ex[i] * eval_log<R>(R(1) + P.isa_bt[i] * dH));
-            else pp = pb * pow(R(1) + P.isa_bt[i] * dH, P.isa_ex[i]);
+            if constexpr (sizeof(R) == 8) pp = pb * exp(L[5] * eval_log<R>(R(1) + L[4] * dH));
+            else pp = pb * pow(R(1) + L[4] * dH, L[5]);
         }
-        else pp = pb * exp(P.isa_iso[i] * dH);
+        else pp = pb * exp(L[6] * dH);
         p = pp;
         rho = pp / (P.isa_R * T);
         a = sqrt(P.isa_kappaR * T);
@@ -169,14 +163,14 @@ __device__ __forceinline__ void atmosphere(const DevParams<R>& P, R y, R& rho, R
     }
 }
 
-template <typename R> __device__ __forceinline__ R gravity(const DevParams<R>& P, R y) {
+template <typename R> __device__ __forceinline__ R gravity(DP<R>& P, R y) {
     R q = P.grav_R / (P.grav_R + y);      // atmosphere_dynamics.py:29-33
     return P.grav_g0 * (q * q);
 }
 
 // stage_inertia closure (rocket_dimensions.py:167-196)
 template <typename R>
-__device__ __forceinline__ void inertia(const DevParams<R>& P, R fill, R& x_cog, R& I) {
+__device__ __forceinline__ void inertia(DP<R>& P, R fill, R& x_cog, R& I) {
     R h_ox_t = P.h_ox * fill, h_f_t = P.h_f * fill, m_ox_t = P.m_ox * fill, m_f_t = P.m_f * fill;
     R x_prop = (m_ox_t * (P.h_lower + h_ox_t / R(2)) + m_f_t * (P.h_lower + P.h_ox + h_f_t / R(2))) / (m_ox_t + m_f_t);
     R t1 = P.h_lower + h_ox_t / R(2) - x_prop;
@@ -194,8 +188,8 @@ __device__ __forceinline__ void inertia(const DevParams<R>& P, R fill, R& x_cog,
 // the ascent phases, with its own expression order (x_prop_1 uses the untilded m_1_f and
 // h_ox_1_tilde as written)
 template <typename R>
-__device__ __forceinline__ void inertia_full(const DevParams<R>& P, R fill, R& x_cog, R& I) {
-    const R* c = P.fr;
+__device__ __forceinline__ void inertia_full(DP<R>& P, R fill, R& x_cog, R& I) {
+    const PD_AS4 R* c = P.fr;
     const R x_wet2 = c[0], x_dry1 = c[1], m_s1 = c[2], m_pay = c[3], m_2 = c[4], m1_ox = c[5], m1_f = c[6];
     const R h_lower1 = c[7], h1_ox = c[8], h1_f = c[9], h1 = c[10], I_wet2 = c[11], I_dry1 = c[12];
     R h_ox_t = h1_ox * fill, h_f_t = h1_f * fill, m_ox_t = m1_ox * fill, m_f_t = m1_f * fill;
@@ -214,7 +208,7 @@ __device__ __forceinline__ void inertia_full(const DevParams<R>& P, R fill, R& x
 // scipy interp1d(kind='linear', fill_value='extrapolate') on a sorted table in global memory:
 // _call_linear (searchsorted side='left', index clipped to [1, n-1])
 template <typename R>
-__device__ __forceinline__ R interp1d_ext(const R* x, const R* y, int n, R v) {
+__device__ __forceinline__ R interp1d_ext(const PD_AS1 R* x, const PD_AS1 R* y, int n, R v) {
     int lo = 0, hi = n;
     while (lo < hi) { int mid = (lo + hi) >> 1; if (x[mid] < v) lo = mid + 1; else hi = mid; }
     int i = lo < 1 ? 1 : (lo > n - 1 ? n - 1 : lo);
@@ -224,7 +218,7 @@ __device__ __forceinline__ R interp1d_ext(const R* x, const R* y, int n, R v) {
 
 // The same on one column of the ascent hyper-parameter table (Mach in column 0, 12 rows).
 template <typename R>
-__device__ __forceinline__ R hyper_interp(const DevParams<R>& P, int col, R mach) {
+__device__ __forceinline__ R hyper_interp(DP<R>& P, int col, R mach) {
     int lo = 0, hi = 12;
     while (lo < hi) { int mid = (lo + hi) >> 1; if (P.hyper[mid][0] < mach) lo = mid + 1; else hi = mid; }
     int i = lo < 1 ? 1 : (lo > 11 ? 11 : lo);
@@ -242,10 +236,10 @@ __host__ __device__ constexpr int obs_dim(int kind) {
     return kind == 2 || kind == 3 ? 5 : (kind == 4 ? 1 : (kind == 5 ? 4 : (kind == 7 ? 8 : 2)));
 }
 template <typename R>
-__device__ __forceinline__ void obs_write(const DevParams<R>& P, int kind, const R* s, R* out, uint32_t idx) {
+__device__ __forceinline__ void obs_write(DP<R>& P, int kind, const R* s, R* out, uint32_t idx) {
     const int d = obs_dim(kind);
-    R* o = out;
-    auto put = [&](int k, R v) { *(R*)((char*)(o + k) + (uint32_t)(idx * (uint32_t)(d * sizeof(R)))) = v; };
+    PD_AS1 char* o = (PD_AS1 char*)(uint64_t)out;
+    auto put = [&](int k, R v) { *(PD_AS1 R*)(o + (uint32_t)(idx * (uint32_t)(d * sizeof(R)) + k * (uint32_t)sizeof(R))) = v; };
     if (kind == 0) {
         put(0, (R(1) - (R)(float)s[1] / P.norm_y) * R(2) - R(1));
         put(1, (R(1) - (R)(float)s[3] / P.norm_vy) * R(2) - R(1));
@@ -273,7 +267,7 @@ __device__ __forceinline__ void obs_write(const DevParams<R>& P, int kind, const
 // ---------------------------------------------------------------- tables in LDS
 // scipy interp1d._call_linear with fill_value='extrapolate' (grid_fin_aerodynamics.py:7-18)
 template <typename R>
-__device__ __forceinline__ R grid_fin_ca(const DevParams<R>& P, const R* sx, const R* sy, R mach) {
+__device__ __forceinline__ R grid_fin_ca(DP<R>& P, const R* sx, const R* sy, R mach) {
     if (mach < P.ca_min_mach) return P.ca_min_val;
     int n = P.ca_n;
     int lo = 0, hi = n;                       // lower_bound: first x >= mach
@@ -299,7 +293,7 @@ __device__ __forceinline__ R np_interp(const R* x, const R* y, int n, R v) {
 
 // grid_fin_aerodynamics.py:21-46: cn_alpha(M) * degrees(alpha)
 template <typename R>
-__device__ __forceinline__ R grid_fin_cn_alpha(const DevParams<R>& P, const R* sx, const R* sy, R mach) {
+__device__ __forceinline__ R grid_fin_cn_alpha(DP<R>& P, const R* sx, const R* sy, R mach) {
     if (mach < P.cn_min_mach) return P.cn_min_val;
     if (mach <= P.cn_max_mach) return np_interp(sx, sy, P.cn_n, mach);
     return P.cn_max_val + P.cn_slope * (mach - P.cn_max_mach);
@@ -324,8 +318,8 @@ __device__ __forceinline__ R d2_at(const R* mach, int start, int i, R M, R dz) {
 }
 
 template <typename R>
-__device__ __forceinline__ int knn_windows(const R* smach, const int* start, const int* n,
-                                           const R* aoa, R M, R a, int lo[kCols], int len[kCols]) {
+__device__ __forceinline__ int knn_windows(const R* smach, const PD_AS4 int* start, const PD_AS4 int* n,
+                                           const PD_AS4 R* aoa, R M, R a, int lo[kCols], int len[kCols]) {
     R dz[kCols];
 #pragma unroll
     for (int c = 0; c < kCols; ++c) { R da = a - aoa[c]; dz[c] = da * da; }

@@ -1,0 +1,92 @@
+// pd_step.h -- the step kernel of libpdenv: declarations shared by the host translation unit
+// (pdenv.hip) and the kernel translation units (kstep_*.hip, which include pd_step_impl.h).
+//
+// Layout in HBM: struct-of-arrays, one env per group of LPE lanes.  A launch loads each env's
+// state once into registers (its g-load ring into LDS), runs F consecutive env-steps of
+// rocket_environment_pre_wrap.step (4 physics sub-steps, g-load window, truncated -> done ->
+// reward, observation, in-register auto-reset), writes each step's outputs, and stores the
+// state once at the end.  See DESIGN.md for the roofline of each kernel.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "../../include/pdenv.h"
+#include "pd_physics.h"
+
+namespace pd {
+
+constexpr int kBlock = 256;
+constexpr int kStepBlock = 256;
+constexpr int kScratch = kSys * kSys + kSys + 3 * kNbr + kPay;   // doubles per solve slot
+constexpr int kPendingCap = 4096;     // device-solved neighbourhoods queued per launch
+constexpr int kSolveSlots = 1024;     // global-memory LU scratch slots (one per workgroup, modulo)
+constexpr int kGridExact = 1 << 30;   // grid_slot flag: every point of the cell has its key
+constexpr int kStats = 32;            // pend.stats words (see Stat)
+
+// pend.stats[] words
+enum Stat {
+    kStMisses = 0, kStNan = 1, kStInsCd = 2, kStInsCl = 3,       // 4..7 PD_EXP_* counters
+    kStStamp = 8,                                                 // 8..15 PD_STAMP sections
+    kStDropped = 16, kStSolves = 17, kStSlotHits = 18
+};
+
+// ---------------------------------------------------------------- per-env device buffers
+template <typename R> struct EnvBufs {
+    R* st;            // [11][N]
+    R* vprev;         // [N]   |v| of the previous state (base_environment.py:137-139)
+    R* gwin;          // [10][N] g-load ring
+    uint8_t* ghead;   // [N]
+    uint8_t* glen;    // [N]
+    R* act;           // [3][N] landing_burn actuator memory
+    R* wind;          // [6][N] fu0 fu1 fv0 fv1 sigma_u sigma_v
+    uint8_t* wprof;   // [N] wind profile (percentile-50)
+    unsigned long long* key;   // [2][N] cached neighbourhood keys (cd, cl)
+    int* slot;                 // [2][N] cached table slots
+    int8_t* tid;      // [N] truncation id
+    uint32_t* epi;    // [N] episode counter
+    uint32_t* tstep;  // [N] step within episode
+    uint8_t* fin;     // [N] episode finished (policy rollouts: the env is frozen until reset)
+};
+
+struct Pending {
+    unsigned long long* count;   // [1] entries appended this launch
+    unsigned long long* keys;    // [cap] (table id in bit 63)
+    double* pay;                 // [cap][kPay]
+    unsigned long long* stats;   // [kStats]
+    double* solve_ws;            // [kSolveSlots][kScratch] exact-solve scratch (global memory)
+    unsigned long long* solve_tag;   // [kSolveSlots] (table << 63 | key) whose payload the slot holds
+    int* solve_lock;             // [kSolveSlots]
+};
+
+template <typename R> struct StepArgs {
+    uint64_t P;                      // const DevParams<R>* (read through a constant-AS view)
+    EnvBufs<R> b;
+    Pending pend;
+    int64_t n;
+    uint64_t env_offset;
+    uint32_t seed_lo, seed_hi;
+    int act_f64, auto_reset, stochastic, fixed_prof, use_tilt;
+    double tilt_sigma;
+    const void* actions;
+    R* obs; R* reward; uint8_t* done; uint8_t* trunc; int8_t* trunc_id;
+    const double* noise;
+    R* info;                         // [PD_N_INFO][N] (single-step launches)
+    R* reward_sum;
+    const float* policy_w;           // policy rollouts: actor parameters [P][N] float32
+    // policy rollouts: the live envs as a compacted index list; a launch steps list_in[0, *cnt_in)
+    // and appends the envs whose episode goes on to list_out (wave ballot + prefix count, one
+    // atomic per wave), then the next launch steps those only (triple-buffered counts: this
+    // launch also zeroes the count the launch after next appends to)
+    const int32_t* list_in; int32_t* list_out;
+    const uint32_t* cnt_in; uint32_t* cnt_out; uint32_t* cnt_zero;
+    int use_list;   // step list_in (else all N envs, finished ones skipped by their fin flag)
+    double dt_aux;                   // physics dt of phases 2..6 (compile_physics(dt, phase))
+    int rtd_none;                    // PD_RTD_NONE: physics stepping only (reward/done/trunc 0)
+    int n_fused;                     // env-steps per launch (actions/outputs: [n_fused][N] rows)
+};
+
+// Kernel launchers, explicitly instantiated in the kstep_*.hip translation units.
+template <typename R, int PH, int RT, bool W, int LPE> void launch_step(const StepArgs<R>& a, hipStream_t s);
+template <typename R, int PH, bool W, int LPE> void launch_policy_lpe(const StepArgs<R>& a, int64_t n_launch,
+                                                                      hipStream_t s);
+
+}  // namespace pd

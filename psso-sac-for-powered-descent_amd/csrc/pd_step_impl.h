@@ -1,0 +1,1293 @@
+// pd_step_impl.h -- the step kernel k_step and its launchers (included by the kstep_*.hip
+// translation units, each of which instantiates a subset; pdenv.hip sees pd_step.h only).
+#pragma once
+#include "pd_envdev.h"
+
+namespace pd {
+
+// ---------------------------------------------------------------- lane pairs
+// Value of the partner lane (2k <-> 2k+1) by a DPP quad permutation [1,0,3,2] (no LDS
+// crossbar).  Only at converged points of the wave.
+__device__ __forceinline__ int dpp_swap1(int v) { return __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false); }
+__device__ __forceinline__ float pair_swap(float v) { return __int_as_float(dpp_swap1(__float_as_int(v))); }
+__device__ __forceinline__ double pair_swap(double v) {
+    const uint64_t b = (uint64_t)__double_as_longlong(v);
+    const uint32_t lo = (uint32_t)dpp_swap1((int)(uint32_t)b), hi = (uint32_t)dpp_swap1((int)(uint32_t)(b >> 32));
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+
+// sin/cos of two angles of one env; with LPE >= 2 the env's even lane evaluates x0 and its odd
+// lane x1 (one pass of the instruction stream for both), then they swap.
+template <int LPE, typename R>
+__device__ __forceinline__ void sincos_pair(R x0, R x1, int role, R& s0, R& c0, R& s1, R& c1) {
+    if constexpr (LPE >= 2) {
+        const bool odd = role & 1;
+        R s, c;
+        pd_sincos<R>(odd ? x1 : x0, s, c);
+        const R so = pair_swap(s), co = pair_swap(c);
+        s0 = odd ? so : s; c0 = odd ? co : c;
+        s1 = odd ? s : so; c1 = odd ? c : co;
+    } else {
+        pd_sincos<R>(x0, s0, c0);
+        pd_sincos<R>(x1, s1, c1);
+    }
+}
+// a0 / b0 and a1 / b1 as one division per lane pair (LPE >= 2)
+template <int LPE, typename R>
+__device__ __forceinline__ void div_pair(R a0, R b0, R a1, R b1, int role, R& q0, R& q1) {
+    if constexpr (LPE >= 2) {
+        const bool odd = role & 1;
+        const R q = (odd ? a1 : a0) / (odd ? b1 : b0);
+        const R qo = pair_swap(q);
+        q0 = odd ? qo : q; q1 = odd ? q : qo;
+    } else {
+        q0 = a0 / b0; q1 = a1 / b1;
+    }
+}
+
+// ---------------------------------------------------------------- RBF lookup + evaluation
+// Lanes-per-env (LPE) decomposition: with LPE = 1 one lane evaluates both tables; with
+// LPE = 2 lane role 0 owns C_D and role 1 owns C_L; with LPE = 4/8/16 each table is owned by
+// LPE/2 lanes that split its 50-term thin-plate sum (terms k = part, part + nparts, ..).
+template <typename R> struct TabView {
+    const R* smach;            // LDS: the table's Mach values, 512 further on each point's AoA
+    const R* saoa;
+    const PD_AS4 int* start;   // column geometry (uniform: scalar loads)
+    const PD_AS4 int* n;
+    const PD_AS4 R* aoa;
+    const PD_AS1 unsigned long long* keys;
+    const PD_AS1 R* pay;
+    int logcap;
+    int line0;                 // index of this table's first clamped line (0: C_D, 2: C_L)
+    const PD_AS1 unsigned long long* grid_key;
+    const PD_AS1 int* grid_slot;
+    int grid_nm, grid_na;
+    R grid_a0, grid_inv_da, grid_inv_dm;
+};
+
+// LDS copy of the clamped-line interval tables
+template <typename R> struct LineLds {
+    R bp[4][kLineMax];
+    int slot[4][kLineMax + 1];
+    unsigned long long key[4][kLineMax + 1];
+    R a[4];
+    int nbp[4];
+};
+
+// This lane's share of sum_j c_j phi(|x - y_j|) + poly of one neighbourhood payload.
+// phi(r) = r^2 log r = d2 log(d2) / 2 with d2 = |x - y|^2 (thin_plate_spline, phi(0) = 0).
+// The payload names each term's table point by a byte index, whose (Mach, AoA) sit in LDS; the
+// terms are evaluated in chunks of 10 independent terms so that the loads of a chunk are in
+// flight together and the 10 log chains interleave.
+template <typename R>
+__device__ __forceinline__ R rbf_eval(const PD_AS1 R* __restrict__ pay, const R* smach, const R* saoa, R M, R a,
+                                      int part, int nparts) {
+    const PD_AS1 uint32_t* iw = (const PD_AS1 uint32_t*)(pay + kPayIdx);
+    R s0 = R(0), s1 = R(0);
+#ifndef PD_CHUNK
+#define PD_CHUNK 10
+#endif
+    constexpr int kChunk = PD_CHUNK;
+    // Chunks as a loop: fully unrolled, the scheduler hoists every chunk's loads ahead and the
+    // kernel spills (256 VGPRs + 260 spilled); rolled it needs 235 VGPRs and no scratch.
+    // PD_RBF_UNROLL restores the full unroll (experiments).
+#ifdef PD_RBF_UNROLL
+#pragma unroll
+#else
+#pragma unroll 1
+#endif
+    for (int j0 = part; j0 < kNbr; j0 += kChunk * nparts) {
+        R mm[kChunk], aa[kChunk], pp[kChunk];
+#pragma unroll
+        for (int u = 0; u < kChunk; ++u) {
+            int j = j0 + u * nparts;
+            bool ok = j < kNbr;
+            int jj = ok ? j : 0;
+            const int ix = (int)((iw[jj >> 2] >> ((jj & 3) * 8)) & 0xffu);
+            mm[u] = smach[ix];
+            aa[u] = saoa[ix];
+            pp[u] = ok ? pay[jj] : R(0);
+        }
+#pragma unroll
+        for (int u = 0; u < kChunk; ++u) {
+            R dm = M - mm[u], da = a - aa[u];
+            R d2 = dm * dm + da * da;
+            // c_j d2 log(d2) accumulated (the 1/2 of phi is applied once below); d2 = 0 (query
+            // on a table point) contributes c_j * 0 * finite = 0
+            R w = d2 * pp[u];
+#ifdef PD_EXP_NOLOG
+            R l = d2;
+#elif defined(PD_EXP_LIBLOG)
+            R l = log(d2 > R(0) ? d2 : R(1));
+#else
+            R l = eval_log<R>(sizeof(R) == 8 ? d2 : (d2 > R(1e-30) ? d2 : R(1e-30)));
+#endif
+            if (u & 1) s1 = fma(w, l, s1); else s0 = fma(w, l, s0);
+        }
+    }
+    R s = R(0.5) * (s0 + s1);
+    if (part == 0) {
+        s += R(1) * pay[kNbr];
+        s += (M - pay[kSys + 0]) / pay[kSys + 2] * pay[kNbr + 1];
+        s += (a - pay[kSys + 1]) / pay[kSys + 3] * pay[kNbr + 2];
+    }
+    return s;
+}
+
+// Orders this wave's global-memory accesses (the solve scratch is written and read back by the
+// same wave: same CU, so an s_waitcnt on its stores is all the ordering it needs).
+__device__ __forceinline__ void wave_mem_sync() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup"); }
+
+// Wave-cooperative exact solve of one neighbourhood into a global-memory scratch slot: lane r
+// owns row r of the 53x53 system; LU with partial pivoting (pivot by a wave max-reduction,
+// smallest row index on ties) and column-oriented back substitution -- the operations and
+// their order per element are those of solve_neighbourhood(), so the payload is bit-identical
+// to the host-built one.  Must be called by a converged wave (all 64 lanes active).  Leaves the
+// binary64 payload at work + kScratch - kPay and the handle-precision payload at work.
+template <typename R>
+__device__ __forceinline__ void solve_wave(DP<R>& P, int table, unsigned long long key, PD_AS1 double* work) {
+    const int lane = (int)__lane_id();
+    PD_AS1 double* A = work;
+    PD_AS1 double* b = A + kSys * kSys;
+    PD_AS1 double* ym = b + kSys;
+    PD_AS1 double* ya = ym + kNbr;
+    PD_AS1 double* yd = ya + kNbr;
+    PD_AS1 double* pay = work + (kScratch - kPay);
+    const PD_AS4 double* mach = table ? P.cl_mach_d : P.cd_mach_d;
+    const PD_AS4 double* coef = table ? P.cl_coef_d : P.cd_coef_d;
+    const PD_AS4 int* start = table ? P.cl_start : P.cd_start;
+    const PD_AS4 double* aoa = table ? P.cl_aoa_d : P.cd_aoa_d;
+    int lo[kCols], len[kCols];
+    key_unpack(key, lo, len);
+    int my_idx = 0;
+    if (lane < kNbr) {
+        int c = 0, off = lane, acc = 0;
+#pragma unroll
+        for (int q = 0; q < kCols; ++q) {
+            if (lane >= acc && lane < acc + len[q]) { c = q; off = lane - acc; }
+            acc += len[q];
+        }
+        int idx = start[c] + lo[c] + off;
+        my_idx = idx;
+        ym[lane] = mach[idx]; ya[lane] = aoa[c]; yd[lane] = coef[idx];
+    }
+    wave_mem_sync();
+    double mn0 = ym[0], mx0 = ym[0], mn1 = ya[0], mx1 = ya[0];
+    for (int j = 1; j < kNbr; ++j) {
+        double u = ym[j], w = ya[j];
+        mn0 = u < mn0 ? u : mn0; mx0 = u > mx0 ? u : mx0;
+        mn1 = w < mn1 ? w : mn1; mx1 = w > mx1 ? w : mx1;
+    }
+    double sh0 = (mx0 + mn0) / 2, sc0 = (mx0 - mn0) / 2, sh1 = (mx1 + mn1) / 2, sc1 = (mx1 - mn1) / 2;
+    if (sc0 == 0.0) sc0 = 1.0;
+    if (sc1 == 0.0) sc1 = 1.0;
+    if (lane < kNbr) {
+        double yi = ym[lane], ai = ya[lane];
+        for (int j = 0; j < kNbr; ++j) {
+            double d0 = yi - ym[j], d1 = ai - ya[j];
+            A[lane * kSys + j] = tps(sqrt(d0 * d0 + d1 * d1));
+        }
+        A[lane * kSys + kNbr] = 1.0;
+        A[lane * kSys + kNbr + 1] = (yi - sh0) / sc0;
+        A[lane * kSys + kNbr + 2] = (ai - sh1) / sc1;
+        b[lane] = yd[lane];
+    } else if (lane < kSys) {
+        for (int j = 0; j < kNbr; ++j)
+            A[lane * kSys + j] = lane == kNbr ? 1.0 : (lane == kNbr + 1 ? (ym[j] - sh0) / sc0 : (ya[j] - sh1) / sc1);
+        for (int j = kNbr; j < kSys; ++j) A[lane * kSys + j] = 0.0;
+        b[lane] = 0.0;
+    }
+    wave_mem_sync();
+    bool singular = false;
+    for (int k = 0; k < kSys; ++k) {
+        double v = (lane >= k && lane < kSys) ? fabs(A[lane * kSys + k]) : -1.0;
+        int p = lane;
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {
+            double ov = __shfl_xor(v, o);
+            int op = __shfl_xor(p, o);
+            if (ov > v || (ov == v && op < p)) { v = ov; p = op; }
+        }
+        if (v == 0.0) { singular = true; break; }
+        if (p != k) {
+            if (lane < kSys) { double t = A[k * kSys + lane]; A[k * kSys + lane] = A[p * kSys + lane]; A[p * kSys + lane] = t; }
+            if (lane == 0) { double t = b[k]; b[k] = b[p]; b[p] = t; }
+            wave_mem_sync();
+        }
+        double r = 1.0 / A[k * kSys + k];
+        if (lane > k && lane < kSys) {
+            double l = A[lane * kSys + k] * r;
+            if (l != 0.0)
+                for (int j = k + 1; j < kSys; ++j) A[lane * kSys + j] -= l * A[k * kSys + j];
+            b[lane] -= l * b[k];
+        }
+        wave_mem_sync();
+    }
+    if (!singular) {
+        for (int i = kSys - 1; i >= 0; --i) {
+            double xi = b[i] / A[i * kSys + i];
+            wave_mem_sync();
+            if (lane == i) b[i] = xi;
+            if (lane < i) b[lane] -= A[lane * kSys + i] * xi;
+            wave_mem_sync();
+        }
+    }
+    if (lane < kSys) pay[lane] = singular ? (double)NAN : b[lane];
+    else if (lane == kSys) pay[kSys] = sh0;
+    else if (lane == kSys + 1) pay[kSys + 1] = sh1;
+    else if (lane == kSys + 2) pay[kSys + 2] = sc0;
+    else if (lane == kSys + 3) pay[kSys + 3] = sc1;
+    else if (lane < kPay) pay[lane] = 0.0;
+    wave_mem_sync();
+    if (lane < kNbr) ((PD_AS1 uint8_t*)(pay + kPayIdx))[lane] = (uint8_t)my_idx;
+    wave_mem_sync();
+    // payload in the kernel's precision, in the (now free) matrix area (pay_store, by lanes)
+    PD_AS1 R* pr = (PD_AS1 R*)work;
+    if (lane < kPayIdx) pr[lane] = (R)pay[lane];
+    else if (lane < pay_stride<R>()) pr[lane] = R(0);
+    wave_mem_sync();
+    if (lane < kNbr) ((PD_AS1 uint8_t*)(pr + kPayIdx))[lane] = (uint8_t)my_idx;
+    wave_mem_sync();
+}
+
+// Each distinct (table, key) missed by the wave is solved cooperatively into the workgroup's
+// global scratch slot (under the slot's lock), evaluated by the lanes that need it, and queued
+// for insertion into the device table (pd_flush_misses).  Called by the converged wave.
+template <typename R>
+__device__ __forceinline__ R rbf_miss_wave(const StepArgs<R>& a, DP<R>& P, int table, const R* smach,
+                                           const R* saoa, unsigned long long key, R M, R aq,
+                                           int part, int nparts, bool need) {
+    R val = R(0);
+    unsigned long long mm = __ballot(need);
+    const unsigned slot = blockIdx.x % kSolveSlots;
+    PD_AS1 double* work = gblw(a.pend.solve_ws) + (size_t)slot * kScratch;
+    while (mm) {
+        int leader = __ffsll((long long)mm) - 1;
+        unsigned long long lk = ((unsigned long long)(unsigned int)__shfl((int)(key >> 32), leader) << 32) |
+                                (unsigned int)__shfl((int)key, leader);
+        int lt = __shfl(table, leader);
+        if (__lane_id() == 0) {
+            while (atomicCAS(&a.pend.solve_lock[slot], 0, 1) != 0) __builtin_amdgcn_s_sleep(2);
+        }
+        wave_mem_sync();
+        solve_wave<R>(P, lt, lk, work);
+        if (need && key == lk && table == lt) {
+            val = rbf_eval<R>((const PD_AS1 R*)work, smach, saoa, M, aq, part, nparts);
+            need = false;
+        }
+        if ((int)__lane_id() == leader) {
+            atomicAdd(&a.pend.stats[kStMisses], 1ull);
+            unsigned long long idx = atomicAdd(a.pend.count, 1ull);
+            const PD_AS1 double* pay = work + (kScratch - kPay);
+            if (idx < (unsigned long long)kPendingCap) {
+                for (int j = 0; j < kPay; ++j) a.pend.pay[idx * kPay + j] = pay[j];
+                a.pend.keys[idx] = lk | ((unsigned long long)lt << 63);
+            } else {
+                atomicAdd(&a.pend.stats[kStDropped], 1ull);   // solved again until a later flush
+            }
+        }
+        wave_mem_sync();
+        if (__lane_id() == 0) atomicExch(&a.pend.solve_lock[slot], 0);
+        mm = __ballot(need);
+    }
+    return val;
+}
+
+// This lane's share of the RBF value of `table` at (M, aq).
+// Candidate neighbourhood: on a clamped query line (the common case: |alpha_eff| > 0.003 rad
+// clamps both tables) the interval table of that line (binary search over <= 96 Mach
+// breakpoints in LDS); elsewhere the interior grid cell's, or the env's cached set.  Unless the
+// candidate is trusted (strictly inside its interval/exact cell) it is VERIFIED (and repaired by
+// the swap search) against the exact distances before it is used.
+template <typename R>
+__device__ __forceinline__ R rbf(const StepArgs<R>& a, DP<R>& P, int table, const TabView<R>& t, const LineLds<R>& ln,
+                                 RbfCache<R>& cache, R M, R aq, int part, int nparts) {
+    unsigned long long ckey = cache.key;
+    int cslot = cache.slot;
+    int li = aq == ln.a[t.line0] ? t.line0 : (aq == ln.a[t.line0 + 1] ? t.line0 + 1 : -1);
+    bool trusted = false;
+    if (li >= 0 && ln.nbp[li] >= 0) {
+        const int nb = ln.nbp[li];
+        int l = 0, h = nb;
+        while (l < h) { int mid = (l + h) >> 1; if (ln.bp[li][mid] < M) l = mid + 1; else h = mid; }
+        ckey = ln.key[li][l];
+        cslot = ln.slot[li][l];
+        // The host split the line at EVERY pairwise bisector, so the 50-NN set is constant
+        // strictly between breakpoints: the interval's key is exact unless M lies within
+        // rounding distance of a breakpoint (then the search below verifies it).
+        const R eps = sizeof(R) == 8 ? R(1e-9) : R(1e-4);
+        const R blo = l > 0 ? ln.bp[li][l - 1] : R(-1);
+        const R bhi = l < nb ? ln.bp[li][l] : R(1e30);
+        trusted = cslot >= 0 && (M - blo > eps) && (bhi - M > eps);
+    } else if (t.grid_key) {
+        R fm = M * t.grid_inv_dm, fa = (aq - t.grid_a0) * t.grid_inv_da;
+        int im = fm < R(0) ? 0 : (fm >= R(t.grid_nm) ? t.grid_nm - 1 : (int)fm);
+        int ia = fa < R(0) ? 0 : (fa >= R(t.grid_na) ? t.grid_na - 1 : (int)fa);
+        if (!(fm == fm) || !(fa == fa)) { im = 0; ia = 0; }   // NaN queries
+        int cell = im * t.grid_na + ia;
+        ckey = t.grid_key[cell];
+        const int gsl = t.grid_slot[cell];
+        cslot = gsl < 0 ? -1 : (gsl & (kGridExact - 1));
+        // every point of an exact cell has the cell's key (convexity of 50-NN regions); the
+        // rounding margin keeps queries on a cell edge on the verified path
+        const R eps = sizeof(R) == 8 ? R(1e-9) : R(1e-4);
+        trusted = gsl >= 0 && (gsl & kGridExact) && fm - (R)im > eps && (R)(im + 1) - fm > eps &&
+                  fa - (R)ia > eps && (R)(ia + 1) - fa > eps;
+    }
+    unsigned long long key = ckey;
+    int slot = cslot;
+#ifdef PD_EXP_TRUSTCHECK
+    const bool check_trusted = trusted;
+    trusted = false;
+#endif
+    if (!trusted) {
+        int lo[kCols], len[kCols];
+        key_unpack(ckey, lo, len);
+        // keys store lo=0 for empty columns; knn_windows uses insertion points for those
+#ifndef PD_EXP_NOKNN
+#ifdef PD_EXP_COUNT
+        int iters = knn_windows<R>(t.smach, t.start, t.n, t.aoa, M, aq, lo, len);
+        atomicAdd(&a.pend.stats[4], 1ull);
+        atomicAdd(&a.pend.stats[5], (unsigned long long)(li >= 0));
+        atomicAdd(&a.pend.stats[6], (unsigned long long)iters);
+#else
+        knn_windows<R>(t.smach, t.start, t.n, t.aoa, M, aq, lo, len);
+#endif
+#endif
+        key = key_pack(lo, len);
+        slot = key == ckey ? cslot : -1;
+#ifdef PD_EXP_TRUSTCHECK
+        atomicAdd(&a.pend.stats[4], (unsigned long long)check_trusted);
+        atomicAdd(&a.pend.stats[7], (unsigned long long)(check_trusted && key != ckey));
+#endif
+    }
+    if (slot < 0) {
+        uint32_t mask = (1u << t.logcap) - 1u;
+        uint32_t h = key_hash(key, t.logcap);
+        for (uint32_t probe = 0; probe <= mask; ++probe) {
+            unsigned long long k = t.keys[h];
+            if (k == key) { slot = (int)h; break; }
+            if (k == kEmptyKey) break;
+            h = (h + 1) & mask;
+        }
+    }
+    cache.key = key;
+    cache.slot = slot;
+    R val = R(0);
+    if (slot >= 0) val = rbf_eval<R>(t.pay + (int64_t)slot * pay_stride<R>(), t.smach, t.saoa, M, aq, part, nparts);
+    // Misses (a neighbourhood outside the pre-enumerated tables) take the wave-cooperative
+    // exact solve; the loop in rbf_miss_wave runs only when some lane of the wave missed
+    if (__ballot(slot < 0)) {
+        R mv = rbf_miss_wave<R>(a, P, table, t.smach, t.saoa, key, M, aq, part, nparts, slot < 0);
+        if (slot < 0) val = mv;
+    }
+    return val;
+}
+
+// rocket_CD query: CD_func = rocket_CD(M, degrees(alpha)); clamp of the DEGREE value at
+// +-radians(10) (rockets_physics.py:712, aerodynamic_coefficients.py:105-115)
+template <typename R> __device__ __forceinline__ R cd_query(R ae) {
+    R aoa = ae * Cst<R>::rad2deg;
+    const R r10 = (R)(10.0 * kDeg2Rad);
+    if (aoa > r10) aoa = r10;
+    else if (aoa < (R)(-10.0 * kDeg2Rad)) aoa = (R)(-10.0 * kDeg2Rad);
+    return aoa;
+}
+// rocket_CL query: degrees applied twice (rockets_physics.py:711 + aerodynamic_coefficients.py:117-132)
+// returns the RBF abscissa, the sign to apply, and whether C_L is exactly 0
+template <typename R> __device__ __forceinline__ R cl_query(R ae, R& sgn, bool& zero) {
+    R aq = (ae * Cst<R>::rad2deg) * Cst<R>::rad2deg;
+    sgn = R(1);
+    zero = false;
+    if (aq > R(10)) aq = R(10);
+    else if (aq < R(-10)) aq = R(-10);
+    else if (fabs(aq) < R(1e-6)) zero = true;
+    else if (aq < R(0)) { aq = fabs(aq); sgn = R(-1); }
+    return aq;
+}
+
+// ---------------------------------------------------------------- the fused actor
+// simple_actor.forward (env_wrapped_ea.py:18-44): Linear(IN,8)-ReLU-[Linear(8,8)-ReLU]xNL-
+// Linear(8,OUT)-Tanh in binary32 on the float32-cast observation.  Parameters are in
+// named_parameters() order (weight [out][in] row-major, then bias, layer by layer), stored
+// parameter-major [P][N] so that every load is coalesced across the envs of a wave.
+// Each output is the sequential sum over inputs (no FMA) plus the bias; tanh is evaluated in
+// binary64 and rounded (the oracle restates the same order: oracle/pd_oracle.c orc_actor).
+template <int IN, int NL, int OUT>
+__device__ __forceinline__ void actor_forward(const float* __restrict__ W, int64_t N, uint32_t ui,
+                                              const float* x, float* y) {
+    constexpr int H = 8;
+    float h[H], g[H];
+    int64_t p = 0;
+#pragma unroll
+    for (int j = 0; j < H; ++j) {
+        float acc = 0.f;
+#pragma unroll
+        for (int k = 0; k < IN; ++k) acc = acc + ev(W + (p + j * IN + k) * N, ui) * x[k];
+        acc = acc + ev(W + (p + H * IN + j) * N, ui);
+        h[j] = acc < 0.f ? 0.f : acc;
+    }
+    p += H * IN + H;
+#pragma unroll
+    for (int l = 0; l < NL; ++l) {
+#pragma unroll
+        for (int j = 0; j < H; ++j) {
+            float acc = 0.f;
+#pragma unroll
+            for (int k = 0; k < H; ++k) acc = acc + ev(W + (p + j * H + k) * N, ui) * h[k];
+            acc = acc + ev(W + (p + H * H + j) * N, ui);
+            g[j] = acc < 0.f ? 0.f : acc;
+        }
+#pragma unroll
+        for (int j = 0; j < H; ++j) h[j] = g[j];
+        p += H * H + H;
+    }
+#pragma unroll
+    for (int j = 0; j < OUT; ++j) {
+        float acc = 0.f;
+#pragma unroll
+        for (int k = 0; k < H; ++k) acc = acc + ev(W + (p + j * H + k) * N, ui) * h[k];
+        acc = acc + ev(W + (p + H * OUT + j) * N, ui);
+        y[j] = (float)tanh((double)acc);
+    }
+}
+
+// PD_STAMP (diagnostic builds only): per-wave shader-clock sections of k_step, summed into
+// pend.stats[8..15] (staging, loads, pre-aero, aero tables, post-aero, rtd, outputs, waves)
+#ifdef PD_STAMP
+#define PD_T(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
+#define PD_ACC(k, d) acc_[k] += (d)
+#else
+#define PD_T(v)
+#define PD_ACC(k, d)
+#endif
+
+// ---------------------------------------------------------------- LDS of one step workgroup
+template <typename R, bool WIND, int EPB> struct StepLds {
+    // table Mach values [0, 512) (C_D, C_L), each point's AoA 512 further on (tab_view relies on it)
+    R tab[1024];
+    R gf[256];                    // grid fins: ca_x, ca_y, cn_x, cn_y (64 each)
+    R isa[9 * kIsaCols];          // ISA layers
+    R walt[WIND ? 800 : 1];       // wind profiles [50][16]: altitude km, speed
+    R wsp[WIND ? 800 : 1];
+    LineLds<R> lines;
+    R gwin[10][EPB];              // the g-load ring of each env of the workgroup (register-resident launches)
+};
+
+template <typename R>
+__device__ __forceinline__ TabView<R> tab_view(DP<R>& P, const R* tab, int table) {
+    TabView<R> t;
+    t.smach = tab + (table ? 256 : 0);
+    t.saoa = t.smach + 512;
+    t.start = table ? &P.cl_start[0] : &P.cd_start[0];
+    t.n = table ? &P.cl_len[0] : &P.cd_len[0];
+    t.aoa = table ? &P.cl_aoa[0] : &P.cd_aoa[0];
+    t.keys = gbl(table ? P.keys_cl : P.keys_cd);
+    t.pay = gbl(table ? P.pay_cl : P.pay_cd);
+    t.logcap = table ? P.logcap_cl : P.logcap_cd;
+    t.line0 = table ? 2 : 0;
+    t.grid_key = gbl(P.grid_key[table]);
+    t.grid_slot = gbl(P.grid_slot[table]);
+    t.grid_nm = P.grid_nm[table];
+    t.grid_na = P.grid_na[table];
+    t.grid_a0 = P.grid_a0[table];
+    t.grid_inv_da = P.grid_inv_da[table];
+    t.grid_inv_dm = P.grid_inv_dm[table];
+    return t;
+}
+
+// ---------------------------------------------------------------- the step kernel
+// One launch = n_fused consecutive env-steps of every env (or, POL, one policy step of the live
+// envs).  The env's state is loaded once into registers (its g-load ring into LDS), the steps
+// run in registers with their per-step outputs written as they go (row f of every [F][N]
+// output), auto-reset happens in registers, and the state is stored once at the end.
+template <typename R, int PHASE, int RTD, bool WIND, int LPE, int POL = 0>
+// waves_per_eu(2): caps VGPR+AGPR at 256 so the f64 kernel keeps two waves per SIMD
+#ifndef PD_WPE
+#define PD_WPE 2
+#endif
+__global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_WPE))) void k_step(StepArgs<R> a) {
+    constexpr int EPB = kStepBlock / LPE;   // envs per workgroup
+    __shared__ StepLds<R, WIND, EPB> L;
+#ifdef PD_STAMP
+    unsigned long long acc_[7] = {0, 0, 0, 0, 0, 0, 0};
+#endif
+    PD_T(t_start);
+    // envs this launch steps: all N, or (POL) the compacted live list; a workgroup past its end
+    // leaves before staging the tables (workgroup-uniform)
+    int64_t n_act = a.n;
+    if constexpr (POL) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) *a.cnt_zero = 0u;
+        if (a.use_list) {
+            n_act = (int64_t)*a.cnt_in;
+            if ((int64_t)blockIdx.x * EPB >= n_act) return;
+        }
+    }
+    {
+        DP<R>& P = *params<R>(a.P);
+        for (int t = threadIdx.x; t < 256; t += kStepBlock) {
+            L.tab[t] = P.cd_mach[t]; L.tab[256 + t] = P.cl_mach[t];
+            L.tab[512 + t] = P.cd_pt_aoa[t]; L.tab[768 + t] = P.cl_pt_aoa[t];
+        }
+        if (threadIdx.x < 64) {
+            L.gf[threadIdx.x] = P.ca_x[threadIdx.x]; L.gf[64 + threadIdx.x] = P.ca_y[threadIdx.x];
+            L.gf[128 + threadIdx.x] = P.cn_x[threadIdx.x]; L.gf[192 + threadIdx.x] = P.cn_y[threadIdx.x];
+        }
+        if (threadIdx.x < 9) {
+            const int k = threadIdx.x;
+            R* r = L.isa + k * kIsaCols;
+            r[0] = P.isa_Hb[k]; r[1] = P.isa_Tb[k]; r[2] = P.isa_beta[k]; r[3] = P.isa_pb[k];
+            r[4] = P.isa_bt[k]; r[5] = P.isa_ex[k]; r[6] = P.isa_iso[k]; r[7] = R(0);
+        }
+        if constexpr (WIND) {
+            for (int t = threadIdx.x; t < 800; t += kStepBlock) {
+                L.walt[t] = (&P.wind_alt_km[0][0])[t];
+                L.wsp[t] = (&P.wind_speed[0][0])[t];
+            }
+        }
+        for (int t = threadIdx.x; t < 4 * kLineMax; t += kStepBlock) (&L.lines.bp[0][0])[t] = (&P.line_bp[0][0])[t];
+        for (int t = threadIdx.x; t < 4 * (kLineMax + 1); t += kStepBlock) {
+            (&L.lines.slot[0][0])[t] = (&P.line_slot[0][0])[t];
+            (&L.lines.key[0][0])[t] = (&P.line_key[0][0])[t];
+        }
+        if (threadIdx.x < 4) { L.lines.a[threadIdx.x] = P.line_a[threadIdx.x]; L.lines.nbp[threadIdx.x] = P.line_nbp[threadIdx.x]; }
+        for (int t = threadIdx.x; t < kLogCells; t += kStepBlock) {
+            s_logtab[t] = P.logtab.invc[t]; s_logtab[kLogCells + t] = P.logtab.logc[t];
+        }
+    }
+    __syncthreads();
+    PD_T(t_staged);
+    PD_ACC(0, t_staged - t_start);
+    const int64_t N = a.n;
+    const int64_t gt = (int64_t)blockIdx.x * kStepBlock + threadIdx.x;
+    // Every lane stays active (the cooperative miss solve needs converged waves).  Lanes past the
+    // end run a private copy of the initial state (no loads of another env's state, no stores).
+    const bool valid = gt / LPE < n_act;
+    const int64_t e_act = valid ? gt / LPE : n_act - 1;
+    const int64_t i = (POL && a.use_list) ? (int64_t)a.list_in[e_act] : e_act;
+    const int role = (int)(gt % LPE);
+    const int le = (int)threadIdx.x / LPE;   // the env's column of the workgroup's LDS g-load ring
+    const uint32_t ui = (uint32_t)i;   // N <= 2^25 (validated): 32-bit per-lane byte offsets
+    // POL (policy rollout): with the list, only live envs are stepped; without it, finished
+    // envs stay frozen and a wave with none left exits (wave-uniform, after the only barrier)
+    bool live = valid;
+    if constexpr (POL) {
+        if (!a.use_list) {
+            live = live && ev(a.b.fin, ui) == 0;
+            if (__ballot(live) == 0) return;
+        }
+    }
+    // role -> (table, part): LPE 1: both tables on one lane; else table = role / (LPE/2)
+    constexpr int nparts = LPE >= 2 ? LPE / 2 : 1;
+    const int my_table = LPE >= 2 ? role / nparts : 0;   // 0 = C_D, 1 = C_L
+    const int part = LPE >= 2 ? role % nparts : 0;
+    const int gbase = (int)__lane_id() & ~(LPE - 1);
+    const uint64_t g = a.env_offset + (uint64_t)i;
+
+    // ---- the env's state into registers (its g-load ring into LDS)
+    EnvRegs<R> e;
+    RbfCache<R> cA, cB;   // LPE 1: A = C_D, B = C_L; LPE >= 2: A = own table
+    {
+        DP<R>& P = *params<R>(a.P);
+#pragma unroll
+        for (int k = 0; k < 11; ++k) e.s[k] = valid ? ldv(a.b.st + (k) * N, ui) : P.state0[k];
+        e.vprev = valid ? ldv(a.b.vprev, ui) : sqrt(e.s[2] * e.s[2] + e.s[3] * e.s[3]);
+        e.glen = valid ? (int)ldv(a.b.glen, ui) : 0;
+        e.ghead = valid ? (int)ldv(a.b.ghead, ui) : 0;
+#pragma unroll
+        for (int k = 0; k < 10; ++k) L.gwin[k][le] = valid ? ldv(a.b.gwin + (k) * N, ui) : R(0);
+        e.act0 = R(0); e.act1 = R(0); e.act2 = R(0);
+        if constexpr (PHASE == 1 || PHASE == 2) e.act0 = valid ? ldv(a.b.act, ui) : R(0);
+        if constexpr (PHASE == 1) {
+            e.act1 = valid ? ldv(a.b.act + N, ui) : R(0);
+            e.act2 = valid ? ldv(a.b.act + (2) * N, ui) : R(0);
+        }
+        e.fu0 = R(0); e.fu1 = R(0); e.fv0 = R(0); e.fv1 = R(0); e.sgu = R(0); e.sgv = R(0); e.prof = 0;
+        if constexpr (WIND) {
+            if (valid) {
+                e.fu0 = ldv(a.b.wind, ui); e.fu1 = ldv(a.b.wind + N, ui);
+                e.fv0 = ldv(a.b.wind + (2) * N, ui); e.fv1 = ldv(a.b.wind + (3) * N, ui);
+                e.sgu = ldv(a.b.wind + (4) * N, ui); e.sgv = ldv(a.b.wind + (5) * N, ui);
+                e.prof = ldv(a.b.wprof, ui);
+            }
+        }
+        e.ep = valid ? ldv(a.b.epi, ui) : 0u;
+        e.ts = valid ? ldv(a.b.tstep, ui) : 0u;
+        e.tid = valid ? (int)ldv(a.b.tid, ui) : 0;
+        cA.key = valid ? ldv(a.b.key + (my_table) * N, ui) : (my_table ? P.init_key_cl : P.init_key_cd);
+        cA.slot = valid ? ldv(a.b.slot + (my_table) * N, ui) : -1;
+        if constexpr (LPE == 1) { cB.key = valid ? ldv(a.b.key + N, ui) : P.init_key_cl; cB.slot = valid ? ldv(a.b.slot + N, ui) : -1; }
+        else { cB.key = 0; cB.slot = -1; }
+    }
+    // PHASE 2 = the other compile_physics phases, chosen at run time by P.phase (wave-uniform)
+    const int aux = PHASE == 2 ? params<R>(a.P)->phase : PHASE;
+    const bool ascent = PHASE == 2 && (aux == PD_PHASE_SUBSONIC || aux == PD_PHASE_SUPERSONIC);
+    constexpr int A = PHASE == 0 ? 1 : (PHASE == 1 ? 4 : 2);
+    const int AD = PHASE == 2 ? (ascent ? 2 : 1) : A;   // row stride of the action array
+    // pure throttle 4 x 0.025 s, landing_burn 4 x 0.1 s (actuators 0.025 s); the other phases
+    // one call of rocket_physics_fcn at dt, actuators at the same dt (rockets_physics.py:728-997)
+    constexpr int NSUB = PHASE == 2 ? 1 : 4;
+    const R dt = PHASE == 0 ? R(0.025) : (PHASE == 1 ? R(0.1) : (R)a.dt_aux);
+    const R dt_act = PHASE == 2 ? dt : R(0.025);
+    PD_T(t_loaded);
+    PD_ACC(1, t_loaded - t_staged);
+
+    const int nf = POL ? 1 : a.n_fused;
+#pragma unroll 1
+    for (int f = 0; f < nf; ++f) {
+    const size_t fo = (size_t)f * (size_t)N;
+    float uf[A];
+    double ud[A];
+#pragma unroll
+    for (int k = 0; k < A; ++k) { uf[k] = 0.f; ud[k] = 0.0; }
+    if constexpr (POL) {
+        // pso_wrapper.augment_state (env_wrapped_ea.py:97-123) of the current state in the
+        // handle's precision, cast to float32 (simple_actor.forward), then the actor
+        DP<R>& Q = *params<R>(a.P);
+        if constexpr (PHASE == 0) {
+            float x[2] = {(float)(e.s[1] / Q.norm_y), (float)(e.s[3] / Q.norm_vy)};
+            actor_forward<2, 3, 1>(a.policy_w, N, ui, x, uf);
+        } else {
+            float x[5] = {(float)(e.s[0] / Q.norm_x), (float)(e.s[1] / Q.norm_y), (float)(e.s[2] / Q.norm_vx),
+                          (float)(e.s[3] / Q.norm_vy), (float)tanh(Q.k_theta_pso * (e.s[4] - Cst<R>::pi / R(2)))};
+            actor_forward<5, 4, 4>(a.policy_w, N, ui, x, uf);
+        }
+    } else if (a.act_f64) {
+#pragma unroll
+        for (int k = 0; k < A; ++k) if (k < AD) ud[k] = ldv((const double*)a.actions + fo * AD + k, ui * AD);
+    } else {
+#pragma unroll
+        for (int k = 0; k < A; ++k) if (k < AD) uf[k] = ldv((const float*)a.actions + fo * AD + k, ui * AD);
+    }
+    R gdeg_out = e.act0, dcmdl_out = e.act1, dcmdr_out = e.act2;
+    const R gprev = e.act0, dlprev = e.act1, drprev = e.act2;
+    bool nan_hit = false;
+    // info tap (single-step launches): the last sub-step's quantities (rockets_physics.py:649-702)
+#ifdef PD_EXP_NOTAP
+    const bool tap = false;
+#else
+    const bool tap = a.info != nullptr && role == 0 && live;
+#endif
+    // (the lane offset is laundered per use so that the 49 loop-invariant store addresses are
+    // formed inside the taken branch, not hoisted out of the loops and kept live: 92 VGPRs)
+    auto info = [&](int k, R v) {
+        uint32_t u = ui;
+        asm volatile("" : "+v"(u));
+        ev(a.info + (size_t)k * (size_t)N, u) = v;
+    };
+
+#pragma unroll 1
+    for (int sub = 0; sub < NSUB; ++sub) {
+        PD_T(t_sub);
+        DP<R>& P = *params<R>(a.P);
+        const bool tap_sub = tap && sub == NSUB - 1;
+        R x = e.s[0], y = e.s[1], vx = e.s[2], vy = e.s[3], th = e.s[4], thd = e.s[5], ga = e.s[6], al = e.s[7];
+        R m = e.s[8], mp = e.s[9];
+        // rocket_physics_fcn (rockets_physics.py:455-704)
+        R rho, patm, asnd;
+        atmosphere<R>(P, L.isa, y, rho, patm, asnd);
+        R speed = sqrt(vx * vx + vy * vy);
+        R mach = R(0);
+        if (asnd != R(0)) { R mr = speed / asnd; mach = (R(10) < mr) ? R(10) : mr; }
+        R q = R(0.5) * rho * (speed * speed);
+        R fpc = (P.m_prop0 - mp) / P.m_prop0;
+        if (fpc == R(0)) fpc = R(1e-6);
+        R x_cog, I;
+        // subrocket_0 (full rocket) closures for the ascent, subrocket_2 after (:748-750, :772-774)
+        if (ascent) inertia_full<R>(P, R(1) - fpc, x_cog, I);
+        else inertia<R>(P, R(1) - fpc, x_cog, I);
+        R d_thrust = x_cog + P.engine_height;
+        R ae = (vy < R(0)) ? ga - th - Cst<R>::pi : al;
+        R d_cp_cg = x_cog - (ascent ? P.cop_ascent : P.cop);
+        R ug = R(0), vg = R(0);
+        if constexpr (WIND) {
+            // WindModel.__call__ (full_wind_model.py:35-43)
+            const R* walt = L.walt + e.prof * 16;
+            const R* wsp = L.wsp + e.prof * 16;
+            R km = y / R(1000);
+            int wn = P.wind_n[e.prof];
+            ug = np_interp<R>(walt, wsp, wn, km);
+            if (y < P.vk_y_threshold && a.stochastic) {
+                double w0, w1;
+                if (a.noise) { w0 = ev(a.noise + 2 * sub, ui * 8); w1 = ev(a.noise + 2 * sub + 1, ui * 8); }
+                else {
+                    // vonkarman.py:34: one np.random.randn() per filter step, u then v (gauss_pair:
+                    // Philox counter (env, episode, step, sub-step), reproducible by the oracle)
+                    u32x4 r = philox({(uint32_t)g, (uint32_t)(g >> 32) ^ e.ep, e.ts, kTagWindSub + (uint32_t)sub},
+                                     a.seed_lo, a.seed_hi);
+                    gauss_pair(r, s_logtab, s_logtab + kLogCells, w0, w1);
+                }
+                // vonkarman.py:33-36: state = Ad @ state + Bd * w  (Bd = sigma * Bd(sigma=1))
+                R n0 = (P.vk_Ad_u[0] * e.fu0 + P.vk_Ad_u[1] * e.fu1) + (e.sgu * P.vk_Bd_u[0]) * (R)w0;
+                R n1 = (P.vk_Ad_u[2] * e.fu0 + P.vk_Ad_u[3] * e.fu1) + (e.sgu * P.vk_Bd_u[1]) * (R)w0;
+                e.fu0 = n0; e.fu1 = n1;
+                n0 = (P.vk_Ad_v[0] * e.fv0 + P.vk_Ad_v[1] * e.fv1) + (e.sgv * P.vk_Bd_v[0]) * (R)w1;
+                n1 = (P.vk_Ad_v[2] * e.fv0 + P.vk_Ad_v[3] * e.fv1) + (e.sgv * P.vk_Bd_v[1]) * (R)w1;
+                e.fv0 = n0; e.fv1 = n1;
+                ug = ug + e.fu1;
+                vg = e.fv1;
+            }
+        }
+        R Fwx = R(0.5) * rho * (ug * ug) * P.A_front * P.C_gust_x;
+        R Fwy = R(0.5) * rho * (vg * vg) * P.A_front * P.C_gust_y;
+        R Mw = -d_cp_cg * Fwy;
+        R CL = R(0), CD = R(0);
+        if (tap_sub) {   // info of the last sub-step (rockets_physics.py:649-702), stored where computed
+            const R mmax = asnd != R(0) ? sqrt(R(2) * R(30000) / rho) * R(1) / asnd : R(200);
+            info(PD_INFO_AIR_DENSITY, rho); info(PD_INFO_PRESSURE, patm); info(PD_INFO_SPEED_OF_SOUND, asnd);
+            info(PD_INFO_MACH, mach); info(PD_INFO_Q, q); info(PD_INFO_X_COG, x_cog); info(PD_INFO_INERTIA, I);
+            info(PD_INFO_ALPHA_EFF, ae); info(PD_INFO_UG, ug); info(PD_INFO_VG, vg); info(PD_INFO_MACH_MAX, mmax);
+            info(PD_INFO_D_CP_CG, d_cp_cg); info(PD_INFO_D_THRUST_CG, d_thrust); info(PD_INFO_FUEL_CONSUMED, fpc);
+            info(PD_INFO_F_WIND_X, Fwx); info(PD_INFO_F_WIND_Y, Fwy); info(PD_INFO_M_WIND, Mw); info(PD_INFO_THETA_IN, th);
+        }
+        PD_T(t_aero0);
+        PD_ACC(2, t_aero0 - t_sub);
+#ifndef PD_EXP_NORBF
+        {
+            // evaluated convergently by every lane; results of lanes that need none (speed of
+            // sound 0 above 81 km, |deg(deg(alpha))| < 1e-6 for C_L) are discarded
+            R cl_sgn; bool cl_zero;
+            R aq_cl = cl_query<R>(ae, cl_sgn, cl_zero);
+            R aq_cd = cd_query<R>(ae);
+            const bool have = asnd != R(0);
+            if constexpr (LPE == 1) {
+                R v = rbf<R>(a, P, 1, tab_view<R>(P, L.tab, 1), L.lines, cB, mach, aq_cl, 0, 1);
+                CL = (!have || cl_zero) ? R(0) : (cl_sgn < R(0) ? -v : v);
+                R w = rbf<R>(a, P, 0, tab_view<R>(P, L.tab, 0), L.lines, cA, mach, aq_cd, 0, 1);
+                CD = have ? w : R(0);
+            } else {
+                R v = rbf<R>(a, P, my_table, tab_view<R>(P, L.tab, my_table), L.lines, cA, mach,
+                             my_table ? aq_cl : aq_cd, part, nparts);
+                if constexpr (nparts >= 2) v += __shfl_xor(v, 1);
+                if constexpr (nparts >= 4) v += __shfl_xor(v, 2);
+                if constexpr (nparts >= 8) v += __shfl_xor(v, 4);
+                R vcd, vcl;
+                if constexpr (LPE == 2) {   // role 0 holds C_D, role 1 C_L: one DPP swap
+                    const R vo = pair_swap(v);
+                    vcd = role ? vo : v; vcl = role ? v : vo;
+                } else {
+                    vcd = __shfl(v, gbase);
+                    vcl = __shfl(v, gbase + nparts);
+                }
+                CD = have ? vcd : R(0);
+                CL = (!have || cl_zero) ? R(0) : (cl_sgn < R(0) ? -vcl : vcl);
+            }
+        }
+#endif
+        PD_T(t_aero1);
+        PD_ACC(3, t_aero1 - t_aero0);
+        R drag = R(0.5) * rho * (speed * speed) * CD * P.A_front;
+        R lift = R(0.5) * rho * (speed * speed) * CL * P.A_front;
+        R sae, cae, sth, cth;
+        sincos_pair<LPE, R>(ae, th, role, sae, cae, sth, cth);
+        R apar, aperp;
+        if (vy >= R(0)) { apar = lift * sae - drag * cae; aperp = -lift * cae - drag * sae; }
+        else { apar = drag * cae - lift * sae; aperp = -drag * sae - lift * cae; }
+        R aero_x = apar * cth + aperp * sth;
+        R aero_y = apar * sth - aperp * cth;
+        R aero_m = aperp * d_cp_cg;
+        if (PHASE == 2 && aux == PD_PHASE_FLIP_OVER) { aero_x = R(0); aero_y = R(0); aero_m = R(0); }   // :548-551
+
+        R T_full = P.T_e + (P.p_e - patm) * P.A_e;
+        R qS = q * P.S_gf;
+        R Ca = grid_fin_ca<R>(P, L.gf, L.gf + 64, mach);
+        R cfp, cfperp, cm, mdot_dt, md_info, thr_info;
+        // info of the grid-fin ACS (acs_model.py:62-86): deflections, C_n of both fins, forces
+        R i_dl = R(0), i_dr = R(0), i_cnl = R(0), i_cnr = R(0), i_gfperp = R(0), i_gfpar = R(0), i_gfm = R(0);
+        // binary32 control forces (ascent, float32 actions): the force sums then stay binary32,
+        // the aero terms being Python floats (weak under NEP 50, rockets_physics.py:608-616)
+        bool f32_forces = false;
+        float cfp_f = 0.f, cfperp_f = 0.f;
+        if constexpr (PHASE == 2) {
+            if (aux == PD_PHASE_PCONTROL) {
+                // force_moment_decomposer_landing_burn_throttle_PID (:402-451): throttle from
+                // v_ref - speed (Kp -0.08, clip [0, 1]) into throttle_only as a list (binary64)
+                R u0;
+                if (a.act_f64) {
+                    R nt = ((R)ud[0] - speed) * P.kp_pc;
+                    nt = nt < R(0) ? R(0) : (nt > R(1) ? R(1) : nt);
+                    u0 = R(2) * (nt - R(0.5));
+                } else {
+                    float nt = (uf[0] - (float)speed) * P.f_kp_pc;
+                    nt = nt < 0.f ? 0.f : (nt > 1.f ? 1.f : nt);
+                    u0 = (R)(2.0f * (nt - 0.5f));
+                }
+                R thr = (u0 + R(1)) / R(2) * P.one_minus_nom_pt + P.nom_pt;
+                R tg = T_full * (R)P.n_eng * thr;
+                R md = P.Te_over_vex * (tg / T_full);
+                cfp = tg + qS * (Ca * R(4)); cfperp = R(0); cm = R(0);   // ACS, zero deflection
+                mdot_dt = md * dt; md_info = md; thr_info = thr;
+                i_gfpar = qS * (Ca * R(4));
+                if (tap_sub) {   // C_n of the undeflected fins (acs_info only)
+                    const R cna = grid_fin_cn_alpha<R>(P, L.gf + 128, L.gf + 192, mach);
+                    i_cnl = cna * (ae * Cst<R>::rad2deg); i_cnr = i_cnl;
+                }
+            } else if (aux == PD_PHASE_BALLISTIC_ARC) {
+                // RCS (:149-166): moment only, promoted to binary64 by x_cog; no mass flow
+                R tf = a.act_f64 ? P.rcs_force * (R)ud[0] : (R)(P.f_rcs_force * uf[0]);
+                cfp = R(0); cfperp = R(0);
+                cm = -tf * (x_cog - P.rcs_d_bottom) + tf * (P.rcs_d_top - x_cog);
+                mdot_dt = R(0); md_info = R(0); thr_info = R(0);
+            } else if (aux == PD_PHASE_FLIP_OVER) {
+                // force_moment_decomposer_flipoverboostbackburn (:63-92): gimbal low-pass (tau 1,
+                // dt), full throttle; the filtered angle keeps the action's dtype
+                R gd;
+                if (a.act_f64) gd = gprev + dt * ((-gprev + (R)ud[0] * R(10)) / R(1));
+                else { float x0 = (float)gprev; gd = (R)(x0 + (float)dt * ((-x0 + uf[0] * 10.0f) / 1.0f)); }
+                R grad = gd * Cst<R>::deg2rad;
+                R tg = T_full * (R)P.n_eng;
+                R cg = cos(grad), sg = sin(grad);
+                R tpar = tg * cg, tperp = -tg * sg;
+                cfp = tpar; cfperp = tperp; cm = -tg * sg * d_thrust;
+                R md = P.Te_over_vex * (sqrt(tpar * tpar + tperp * tperp) / T_full);
+                mdot_dt = md * dt; md_info = md; thr_info = R(1);
+                gdeg_out = gd;
+            } else {
+                // force_moment_decomposer_ascent (:17-56): 16 gimballed + 26 fixed, nominal 0.5,
+                // gimbal radians(7)
+                const R ng = (R)P.n_eng, nng = (R)(P.n_eng_stage1 - P.n_eng);
+                if (a.act_f64) {
+                    R grad = (R)ud[0] * P.mg_ascent;
+                    R thr = ((R)ud[1] + R(1)) / R(2) * R(0.5) + R(0.5);
+                    R tg = T_full * ng * thr, tng = T_full * nng * thr;
+                    R cg = cos(grad), sg = sin(grad);
+                    R tpar = tng + tg * cg, tperp = -tg * sg;
+                    cfp = tpar; cfperp = tperp; cm = -tg * sg * d_thrust;
+                    R md = P.Te_over_vex * (sqrt(tpar * tpar + tperp * tperp) / T_full);
+                    mdot_dt = md * dt; md_info = md; thr_info = thr;
+                    gdeg_out = grad * Cst<R>::rad2deg;
+                } else {
+                    float grad = uf[0] * P.f_mg_ascent;
+                    float nnt = (uf[1] + 1.0f) / 2.0f;
+                    float thr = nnt * 0.5f + 0.5f;
+                    float tg = (float)(T_full * ng) * thr, tng = (float)(T_full * nng) * thr;
+                    float cg = (float)cos((R)grad), sg = (float)sin((R)grad);
+                    float tpar = tng + tg * cg, tperp = (-tg) * sg;
+                    float tot = sqrtf(tpar * tpar + tperp * tperp);
+                    float mdf = P.f_Te_over_vex * (tot / (float)T_full);
+                    cfp_f = tpar; cfperp_f = tperp; f32_forces = true;
+                    cfp = (R)tpar; cfperp = (R)tperp; cm = (R)((-tg) * sg) * d_thrust;
+                    mdot_dt = (R)(mdf * (float)dt); md_info = (R)mdf; thr_info = (R)thr;
+                    gdeg_out = (R)grad * Cst<R>::rad2deg;
+                }
+            }
+        } else if constexpr (PHASE == 0) {
+            // force_moment_decomposer_landing_burn_throttle_only (:340-400); ACS with zero
+            // deflection: F_perp = M = 0 exactly, F_par = qS * (Ca * (2 + 1 + 1))
+            R acs_par = qS * (Ca * R(4));
+            if (a.act_f64) {
+                R u0 = (R)ud[0];
+                R nnt = (u0 + R(1)) / R(2);
+                R thr = nnt * P.one_minus_nom_pt + P.nom_pt;
+                R tg = T_full * (R)P.n_eng * thr;
+                R md = P.Te_over_vex * (tg / T_full);
+                cfp = tg + acs_par; mdot_dt = md * dt; md_info = md; thr_info = thr;
+            } else {
+                float nnt = (uf[0] + 1.0f) / 2.0f;
+                float thr = nnt * P.f_one_minus_nom_pt + P.f_nom_pt;
+                float tg = (float)(T_full * (R)P.n_eng) * thr;
+                float md = P.f_Te_over_vex * (tg / (float)T_full);
+                cfp = (R)tg + acs_par; mdot_dt = (R)(md * P.f_dt_pt); md_info = (R)md; thr_info = (R)thr;
+            }
+            cfperp = R(0); cm = R(0);
+            i_gfpar = acs_par;
+            if (tap_sub) {   // C_n of the undeflected fins (acs_info only)
+                const R cna = grid_fin_cn_alpha<R>(P, L.gf + 128, L.gf + 192, mach);
+                i_cnl = cna * (ae * Cst<R>::rad2deg); i_cnr = i_cnl;
+            }
+        } else {
+            // force_moment_decomposer_landing_burn_gimballed (:168-269)
+            R gdeg_cmd, tpar, tperp, tmz, cmd_l, cmd_r, md, thr;
+            R gd;
+            if (a.act_f64) {
+                R grad = (R)ud[0] * P.max_gimbal_rad;
+                gdeg_cmd = grad * Cst<R>::rad2deg;
+                gd = gprev + dt_act * ((-gprev + gdeg_cmd) / R(1));
+                gd = gd < -P.max_gimbal_deg ? -P.max_gimbal_deg : gd;
+                gd = gd > P.max_gimbal_deg ? P.max_gimbal_deg : gd;
+                R grad2 = gd * Cst<R>::deg2rad;
+                R nnt = ((R)ud[1] + R(1)) / R(2);
+                thr = nnt * P.one_minus_nom_lb + P.nom_lb;
+                R tg = T_full * (R)(P.n_eng + 2) * thr;
+                R cg, sg;
+                pd_sincos<R>(grad2, sg, cg);
+                tpar = tg * cg; tperp = -tg * sg; tmz = -tg * sg * d_thrust;
+                R tot = sqrt(tpar * tpar + tperp * tperp);
+                md = P.Te_over_vex * (tot / T_full);
+                gdeg_out = grad2 * Cst<R>::rad2deg;
+                cmd_l = (R)ud[2] * P.max_defl_rad * R(60); cmd_r = (R)ud[3] * P.max_defl_rad * R(60);
+                mdot_dt = md * dt;
+            } else {
+                float grad = uf[0] * P.f_max_gimbal_rad;
+                gdeg_cmd = (R)grad * Cst<R>::rad2deg;
+                gd = gprev + dt_act * ((-gprev + gdeg_cmd) / R(1));
+                gd = gd < -P.max_gimbal_deg ? -P.max_gimbal_deg : gd;
+                gd = gd > P.max_gimbal_deg ? P.max_gimbal_deg : gd;
+                R grad2 = gd * Cst<R>::deg2rad;
+                float nnt = (uf[1] + 1.0f) / 2.0f;
+                float thrf = nnt * P.f_one_minus_nom_lb + P.f_nom_lb;
+                float tg = (float)(T_full * (R)(P.n_eng + 2)) * thrf;
+                float cg = (float)cos(grad2), sg = (float)sin(grad2);
+                float fpar = tg * cg, fperp = (-tg) * sg, fm = (-tg) * sg;
+                float tot = sqrtf(fpar * fpar + fperp * fperp);
+                float mdf = P.f_Te_over_vex * (tot / (float)T_full);
+                tpar = (R)fpar; tperp = (R)fperp; tmz = (R)fm * d_thrust;   // d_thrust_cg is float64
+                md = (R)mdf; thr = (R)thrf;
+                gdeg_out = grad2 * Cst<R>::rad2deg;
+                float dlf = uf[2] * P.f_max_defl_rad, drf = uf[3] * P.f_max_defl_rad;
+                cmd_l = (R)(dlf * 60.0f); cmd_r = (R)(drf * 60.0f);
+                mdot_dt = (R)(mdf * P.f_dt_lb);
+            }
+            // ACS (acs_model.py:13-87)
+            R dcl = cmd_l * Cst<R>::deg2rad, dcr = cmd_r * Cst<R>::deg2rad;
+            R dl = dlprev + dt_act * ((-dlprev + dcl) / R(0.5));
+            R dr = drprev + dt_act * ((-drprev + dcr) / R(0.5));
+            R cna = grid_fin_cn_alpha<R>(P, L.gf + 128, L.gf + 192, mach);
+            R CnL = cna * ((ae - dl) * Cst<R>::rad2deg);
+            R CnR = cna * ((ae - dr) * Cst<R>::rad2deg);
+            R cl_, cr_, sl_, sr_;
+            sincos_pair<LPE, R>(dl, dr, role, sl_, cl_, sr_, cr_);
+            R f_perp = qS * (CnR * cr_ - CnL * cl_ - Ca * (sl_ - sr_));
+            R f_par = qS * (Ca * (R(2) + cl_ + cr_) - CnL * sl_ + CnR * sr_);
+            R m_z = -(P.d_base_gf - x_cog) * f_perp + P.R_rocket * qS * (Ca * (sr_ - sl_) - CnL * cl_ + CnR * cr_);
+            cfp = tpar + f_par; cfperp = tperp + f_perp; cm = tmz + m_z;
+            dcmdl_out = dcl; dcmdr_out = dcr;
+            md_info = md; thr_info = thr;
+            i_dl = dl; i_dr = dr; i_cnl = CnL; i_cnr = CnR; i_gfperp = f_perp; i_gfpar = f_par; i_gfm = m_z;
+        }
+        // NaN guard (rockets_physics.py:599-607), an elif chain
+        if (isnan(cfp)) { cfp = R(0); nan_hit = true; }
+        else if (isnan(cfperp)) { cfperp = R(0); nan_hit = true; }
+        else if (isnan(cm)) { cm = R(0); nan_hit = true; }
+        if (tap_sub) {
+            info(PD_INFO_CL, CL); info(PD_INFO_CD, CD); info(PD_INFO_DRAG, drag); info(PD_INFO_LIFT, lift);
+            info(PD_INFO_AERO_X, aero_x); info(PD_INFO_AERO_Y, aero_y); info(PD_INFO_AERO_MOMENT, aero_m);
+            info(PD_INFO_MASS_FLOW, md_info); info(PD_INFO_THROTTLE, thr_info); info(PD_INFO_GIMBAL_DEG, gdeg_out);
+            info(PD_INFO_CF_PAR, cfp); info(PD_INFO_CF_PERP, cfperp); info(PD_INFO_CONTROL_MOMENT, cm);
+            info(PD_INFO_DCMD_L, dcmdl_out); info(PD_INFO_DCMD_R, dcmdr_out); info(PD_INFO_DELTA_L, i_dl);
+            info(PD_INFO_DELTA_R, i_dr); info(PD_INFO_GF_CA, Ca); info(PD_INFO_GF_CN_L, i_cnl); info(PD_INFO_GF_CN_R, i_cnr);
+            info(PD_INFO_GF_F_PERP, i_gfperp); info(PD_INFO_GF_F_PAR, i_gfpar); info(PD_INFO_GF_MZ, i_gfm);
+        }
+        R cfx, cfy;
+        R fx, fy;
+        if (PHASE == 2 && f32_forces) {
+            // float32 control forces join the Python-float aero terms in binary32; with wind on
+            // F_wind_x is a numpy float64 (interp1d output) and promotes the last sum
+            if (isnan(cfp_f)) cfp_f = 0.f;
+            else if (isnan(cfperp_f)) cfperp_f = 0.f;
+            float c = (float)cth, sn = (float)sth;
+            float cx = cfp_f * c + cfperp_f * sn, cy = cfp_f * sn - cfperp_f * c;
+            float sx = (float)aero_x + cx, sy = (float)aero_y + cy;
+            fx = WIND ? (R)sx + Fwx : (R)(sx + (float)Fwx);
+            fy = (R)(sy + (float)Fwy);
+            cfx = (R)cx; cfy = (R)cy;
+        } else {
+            cfx = cfp * cth + cfperp * sth;
+            cfy = cfp * sth - cfperp * cth;
+            fx = aero_x + cfx + Fwx; fy = aero_y + cfy + Fwy;
+        }
+        // vx_dot = F_x / m, vy_dot = F_y / m - g, theta_dot_dot = M_z / I, g = g0 (R/(R+y))^2:
+        // three divisions as two lane-paired ones
+        const R mz = cm + aero_m + Mw;
+        R vxd, vyq, thdd, grq;
+        div_pair<LPE, R>(fx, m, fy, m, role, vxd, vyq);
+        div_pair<LPE, R>(mz, I, P.grav_R, P.grav_R + y, role, thdd, grq);
+        const R gr = P.grav_g0 * (grq * grq);
+        const R vyd = vyq - gr;
+        vx += vxd * dt; vy += vyd * dt; x += vx * dt; y += vy * dt;
+        thd += thdd * dt; th += thd * dt;
+        ga = atan2(vy, vx);
+        if (th > Cst<R>::two_pi) th -= Cst<R>::two_pi;
+        if (ga < R(0)) ga = Cst<R>::two_pi + ga;
+        al = th - ga;
+        mp -= mdot_dt; m -= mdot_dt;
+        if (tap_sub) {
+            info(PD_INFO_CF_X, cfx); info(PD_INFO_CF_Y, cfy); info(PD_INFO_GRAVITY, gr); info(PD_INFO_VX_DOT, vxd);
+            info(PD_INFO_VY_DOT, vyd); info(PD_INFO_MOMENTS, mz); info(PD_INFO_THETA_DDOT, thdd);
+        }
+        e.s[0] = x; e.s[1] = y; e.s[2] = vx; e.s[3] = vy; e.s[4] = th; e.s[5] = thd; e.s[6] = ga; e.s[7] = al;
+        e.s[8] = m; e.s[9] = mp; e.s[10] = e.s[10] + dt;
+        PD_T(t_subend);
+        PD_ACC(4, t_subend - t_aero1);
+    }
+    if (nan_hit && role == 0 && live) atomicAdd(&a.pend.stats[kStNan], 1ull);
+    PD_T(t_loop);
+
+    // ---- g-load window (base_environment.py:136-149): ring of 10 in LDS, Python sum() from the
+    // oldest; the new entry is written first, then the window is read back in summation order
+    DP<R>& P2 = *params<R>(a.P);
+    const R* s = e.s;
+    R v = sqrt(s[2] * s[2] + s[3] * s[3]);
+    R gl_new = fabs(v - e.vprev) / R(0.1) * R(1) / R(9.81);
+    int glen = e.glen, ghead = e.ghead;
+    int wslot;
+    if (glen < 10) { wslot = glen; glen += 1; }
+    else { wslot = ghead; ghead = ghead == 9 ? 0 : ghead + 1; }
+    L.gwin[wslot][le] = gl_new;
+    const int gstart = glen < 10 ? 0 : ghead;
+    R gv[10];
+#pragma unroll
+    for (int k = 0; k < 10; ++k) {
+        int p = gstart + k;
+        p = p >= 10 ? p - 10 : p;
+        gv[k] = L.gwin[p][le];
+    }
+    R gsum = R(0);
+#pragma unroll
+    for (int k = 0; k < 10; ++k)
+        if (k < glen) gsum += gv[k];
+    R gl = gsum / R(10);
+
+    // ---- truncated -> done -> reward (rtd_rl.py:190-336 / rtd_pso.py:172-317)
+    R x = s[0], y = s[1], vx = s[2], vy = s[3], th = s[4], ga = s[6], mp = s[9];
+    R rho, pa_, as_;
+    atmosphere<R>(P2, L.isa, y, rho, pa_, as_);
+    R speed = v;
+    R q = R(0.5) * rho * (speed * speed);
+    int tr = 0, id = 0, dn = 0;
+    R rew = R(0);
+    const R r2 = (R)(2.0 * kDeg2Rad);
+    if constexpr (RTD == 0 && PHASE != 2) {
+        // landing burns: truncated/done shared by both RL flavours (rtd_rl.py:194-240)
+        if (y < R(-10)) { tr = 1; id = 1; }
+        else if (mp <= R(0)) { tr = 1; id = 2; }
+        else if (th > Cst<R>::pi + r2) { tr = 1; id = 3; }
+        else if (q > R(65000)) { tr = 1; id = 4; }
+        else if (gl > R(6)) { tr = 1; id = 5; }
+        else if (vy > R(0)) { tr = 1; id = 6; }
+        else if (vx > R(0.01)) { tr = 1; id = 7; }
+        dn = (y > R(0) && y < R(1) && speed < R(5));
+        if constexpr (PHASE == 0) {   // pure-throttle reward (rtd_rl.py:272-336)
+            R sp = hypot(vx, vy);
+            R qr = R(0.5) * rho * (sp * sp);
+            if (qr > R(60000)) { R e_ = (qr - R(60000)) / (R(65000) - R(60000)); R e2 = e_ * e_; rew -= R(1) * (e2 > R(1) ? R(1) : e2); }
+            if (gl > R(5.5)) { R e_ = (gl - R(5.5)) / (R(6) - R(5.5)); R e2 = e_ * e_; rew -= R(1) * (e2 > R(1) ? R(1) : e2); }
+            R prog = (P2.y0_rl - y) / P2.y0_rl;
+            R wp = (qr <= R(60000) && gl <= R(5.5)) ? R(0.5) : R(0.5) * R(0.1);
+            rew += wp * prog;
+            if (y < R(100)) rew += R(5.5) * (R(1) - fabs(vy) / R(50));
+            if (dn && !tr) rew += R(400) * mp / P2.m0_rl;
+            else if (tr && y > R(0)) rew -= R(50) * (fabs(y) / P2.y0_rl);
+            else if (tr && y < R(0)) rew -= R(50) * (fabs(vy) / R(10));
+            if (!dn || !(tr && y < R(0))) rew = rew < R(-10) ? R(-10) : (rew > R(10) ? R(10) : rew);
+        } else {                      // landing_burn / ACS reward (rtd_rl.py:243-269), u0 = actions[0]
+            R aef = fabs(ga - th - Cst<R>::pi);
+            R lead = R(1.5) - log(R(1) + aef) / P2.log_1p_max_ae;
+            R X;
+            if (a.act_f64) X = lead - ((R)ud[0] + R(1)) / R(2) * R(0.5);
+            else X = (R)((float)lead - ((uf[0] + 1.0f) / 2.0f) * 0.5f);
+            rew = X * (R(1) - y / P2.y0_rl) * R(2) / R(3);
+            if (y < R(100)) rew += R(1) - tanh((speed - R(15)) / R(15));
+            if (tr && y < R(5)) rew += R(1) - tanh((speed - R(5)) / R(5));
+            if (dn) rew += R(5);
+            rew *= P2.rl_scale;
+        }
+        if (a.rtd_none) { tr = 0; id = 0; dn = 0; rew = R(0); }
+    } else if constexpr (RTD == 0) {
+        const int ph = P2.phase;
+        if (ph == PD_PHASE_PCONTROL) {
+            // compile_rtd_rl_landing_burn_PDcontrol (rtd_rl.py:353-401) + the reward that rebinds
+            // the first (:479-531); v_ref = actions[0]
+            if (y < R(-10)) { tr = 1; id = 1; }
+            else if (mp <= R(0)) { tr = 1; id = 2; }
+            else if (th > Cst<R>::pi + r2) { tr = 1; id = 3; }
+            else if (q > R(65000)) { tr = 1; id = 4; }
+            else if (gl > R(6)) { tr = 1; id = 5; }
+            else if (vy > R(0)) { tr = 1; id = 6; }
+            dn = (y > R(0) && y < R(5) && speed < R(1));
+            R sp = hypot(vx, vy);
+            R qr = R(0.5) * rho * (sp * sp);
+            if (qr > R(60000)) { R e_ = (qr - R(60000)) / (R(65000) - R(60000)); R e2 = e_ * e_; rew -= R(1) * (e2 > R(1) ? R(1) : e2); }
+            if (gl > R(5.5)) { R e_ = (gl - R(5.5)) / (R(6) - R(5.5)); R e2 = e_ * e_; rew -= R(1) * (e2 > R(1) ? R(1) : e2); }
+            R prog = (P2.y0_rl - y) / P2.y0_rl;
+            R vt;
+            if (a.act_f64) { R t = R(1) - fabs(sp - (R)ud[0]) / R(10); vt = t > R(0) ? t : R(0); }
+            else { float t = 1.0f - fabsf((float)sp - uf[0]) / 10.0f; vt = t > 0.f ? (R)t : R(0); }
+            R wp = (qr <= R(60000) && gl <= R(5.5)) ? R(0.5) : R(0.5) * R(0.1);
+            rew += wp * prog * vt;
+            if (y < R(100)) { R t = R(1) - fabs(vy - R(0)) / R(50); rew += R(0.5) * (t > R(0) ? t : R(0)); }
+            rew += P2.alive_bonus;
+            if (dn && !tr) { rew += R(5); R used = P2.y0_rl * R(0) + (P2.m0_rl - s[8]); R u = R(0.1) * used; rew -= u < R(1) ? u : R(1); }
+            else if (tr) { R u = R(4) * (y / P2.y0_rl) * (fabs(vy) / R(100)); rew -= u < R(5) ? u : R(5); }
+            rew = rew < R(-10) ? R(-10) : (rew > R(10) ? R(10) : rew);
+        } else if (ph == PD_PHASE_BALLISTIC_ARC) {
+            // compile_rtd_rl_ballistic_arc_descent (rtd_rl.py:153-188)
+            R aef = fabs(ga - th - Cst<R>::pi);
+            dn = (q > R(10000) && aef < (R)(3.0 * kDeg2Rad));
+            if (q > R(10000 - 2000) && aef > (R)(5.0 * kDeg2Rad)) { tr = 1; id = 1; }
+            rew = (Cst<R>::pi - aef) / Cst<R>::pi;
+            if (dn) rew += R(3.5);
+            rew /= R(100);
+        } else if (ph == PD_PHASE_SUBSONIC || ph == PD_PHASE_SUPERSONIC) {
+            // compile_rtd_rl_ascent (rtd_rl.py:11-114) over the ascent reference trajectory
+            bool nan_ = false;
+#pragma unroll
+            for (int k = 0; k < 11; ++k) nan_ |= isnan(s[k]);
+            if (nan_) { tr = 1; id = 0; }
+            else {
+                R mach = (speed != R(0) && as_ != R(0)) ? speed / as_ : R(0);
+                R mx = hyper_interp<R>(P2, 1, mach), mvy = hyper_interp<R>(P2, 2, mach);
+                R mvx = hyper_interp<R>(P2, 3, mach), mal = hyper_interp<R>(P2, 4, mach);
+                int n = P2.n_ref;
+                const PD_AS1 R* ry = gbl(P2.ref_y);
+                R xr = interp1d_ext<R>(ry, gbl(P2.ref_x), n, y), vxr = interp1d_ext<R>(ry, gbl(P2.ref_vx), n, y);
+                R vyr = interp1d_ext<R>(ry, gbl(P2.ref_vy), n, y);
+                R al = s[7];
+                dn = (mp >= R(0) && mach > P2.terminal_mach);
+                if (mp <= R(0)) { tr = 1; id = 1; }
+                else if (mach > P2.terminal_mach + R(0.09)) { tr = 1; id = 2; }
+                else if (fabs(x - xr) > mx) { tr = 1; id = 3; }
+                else if (y < R(0)) { tr = 1; id = 4; }
+                else if (fabs(al) > mal * Cst<R>::deg2rad) { tr = 1; id = 5; }
+                else if (fabs(vx - vxr) > mvx) { tr = 1; id = 6; }
+                else if (fabs(vy - vyr) > mvy) { tr = 1; id = 7; }
+                if (!(y < R(0))) {
+                    R d = vx - vxr; rew += exp(R(-4) * (d * d) / (mvx * mvx)) * hyper_interp<R>(P2, 8, mach);
+                    d = vy - vyr; rew += exp(R(-4) * (d * d) / (mvy * mvy)) * hyper_interp<R>(P2, 7, mach);
+                    d = x - xr; rew += exp(R(-4) * (d * d) / (mx * mx)) * hyper_interp<R>(P2, 6, mach);
+                    d = al * Cst<R>::rad2deg; rew += exp(R(-4) * (d * d) / (mal * mal)) * hyper_interp<R>(P2, 5, mach);
+                    if (dn) rew += R(2.5);
+                    rew /= R(10000);
+                }
+            }
+        }
+        if (a.rtd_none || ph == PD_PHASE_FLIP_OVER) { tr = 0; id = 0; dn = 0; rew = R(0); }
+    } else {
+        if constexpr (PHASE == 0) {
+            if (y < R(0)) { tr = 1; id = 1; }
+            else if (mp <= R(0)) { tr = 1; id = 2; }
+            else if (th > Cst<R>::pi + r2) { tr = 1; id = 3; }
+            else if (q > R(65000)) { tr = 1; id = 4; }
+            else if (vy > R(0)) { tr = 1; id = 6; }
+            else if (gl > R(6)) { tr = 1; id = 7; }
+            dn = (y > R(0) && y < R(1) && speed < R(5.5));
+            if (tr && y > R(0)) rew = -fabs(y);
+            else if (tr && y < R(0)) rew = R(200) - fabs(speed);
+            else if (dn) rew = mp;
+        } else {
+            R dist = sqrt(x * x + y * y);
+            R over;
+            if (x < R(0) && y < R(0)) over = sqrt(x * x + y * y);
+            else if (x < R(0)) over = -x;
+            else if (y < R(0)) over = -y;
+            else over = R(0);
+            R aeff = (vy < R(0)) ? fabs(ga - th - Cst<R>::pi) : fabs(th - ga);
+            if (over > R(0.5)) { tr = 1; id = 1; }
+            else if (mp <= R(0)) { tr = 1; id = 2; }
+            else if (aeff > (R)(10.0 * kDeg2Rad)) { tr = 1; id = 3; }
+            else if (q > R(65000)) { tr = 1; id = 4; }
+            else if (vy > R(0)) { tr = 1; id = 6; }
+            else if (gl > R(6)) { tr = 1; id = 7; }
+            else if (y > R(1000) && vx > R(0)) { tr = 1; id = 8; }
+            dn = (dist > R(0) && dist < R(1) && speed < R(2.5));
+            if (tr && over < R(0.5)) rew = -fabs(dist);
+            else if (tr) rew = R(200) - fabs(speed);
+            else if (dn) rew = mp;
+        }
+    }
+
+    PD_T(t_rtd);
+    PD_ACC(5, t_rtd - t_loop);
+    // ---- outputs of step f (role 0 of the env's lane group)
+    const bool ended = !POL && a.auto_reset && (dn || tr);
+    if (role == 0 && live) {
+        if (a.obs) {
+            // the wrappers' observation (obs_write kinds); compile-time for the landing burns
+            constexpr int kind = RTD == 1 ? (PHASE == 0 ? 1 : 2) : (PHASE == 0 ? 0 : (PHASE == 1 ? 3 : -1));
+            const int ok = kind >= 0 ? kind : P2.obs_kind;
+            obs_write<R>(P2, ok, s, a.obs + fo * obs_dim(ok), ui);
+        }
+        if (a.reward) ev(a.reward + fo, ui) = rew;
+        if constexpr (POL) {
+            // objective_function: episode_reward -= reward until done or truncated (env_wrapped_ea.py:200-222)
+            ev(a.reward_sum, ui) -= rew;
+            if (dn || tr) ev(a.b.fin, ui) = 1;
+        } else if (a.reward_sum) {
+            ev(a.reward_sum, ui) += rew;
+        }
+        if (a.done) ev(a.done + fo, ui) = (uint8_t)dn;
+        if (a.trunc) ev(a.trunc + fo, ui) = (uint8_t)tr;
+        if (a.trunc_id) ev(a.trunc_id + fo, ui) = (int8_t)id;
+        if (a.info) ev(a.info + (PD_INFO_GLOAD) * N, ui) = gl;
+    }
+    if constexpr (POL) {
+        // done-mask compaction: the envs whose episode goes on, in lane order, appended to the
+        // next launch's list at a base taken by one atomic per wave (the count also tells the
+        // host when every episode has ended)
+        const bool cont = role == 0 && live && !(dn || tr);
+        const unsigned long long mk = __ballot(cont);
+        if (mk) {
+            const int lane = (int)__lane_id();
+            const int leader = __ffsll((long long)mk) - 1;
+            uint32_t base = 0;
+            if (lane == leader) base = atomicAdd(a.cnt_out, (uint32_t)__popcll(mk));
+            base = (uint32_t)__shfl((int)base, leader);
+            if (cont) a.list_out[base + (uint32_t)__popcll(mk & ((1ull << lane) - 1ull))] = (int32_t)i;
+        }
+    }
+    // ---- the env's bookkeeping for the next step: auto-reset in registers, or carry on
+    if (ended) {
+        reset_values<R>(P2, a, g, e.ep + 1, s_logtab, s_logtab + kLogCells, e);   // keeps the aero caches
+    } else {
+        e.vprev = v;
+        e.glen = glen; e.ghead = ghead;
+        e.tid = id;
+        e.ts = e.ts + 1;
+        e.act0 = gdeg_out; e.act1 = dcmdl_out; e.act2 = dcmdr_out;
+    }
+    }   // fused steps
+
+    // ---- the env's state back to HBM, once.  A fresh copy of the offset: the store addresses are
+    // recomputed here from the SGPR bases instead of being kept live (spilled) from the loads
+    uint32_t uo = ui;
+    asm volatile("" : "+v"(uo));
+    if (live) {
+        const uint32_t ui = uo;
+#pragma unroll
+        for (int k = 0; k < 11; ++k)
+            if (k % LPE == role) ev(a.b.st + (k) * N, ui) = e.s[k];
+        if (role == 0) {
+            ev(a.b.vprev, ui) = e.vprev;
+            ev(a.b.glen, ui) = (uint8_t)e.glen; ev(a.b.ghead, ui) = (uint8_t)e.ghead;
+#pragma unroll
+            for (int k = 0; k < 10; ++k) ev(a.b.gwin + (k) * N, ui) = L.gwin[k][le];
+            ev(a.b.tid, ui) = (int8_t)e.tid;
+            ev(a.b.epi, ui) = e.ep; ev(a.b.tstep, ui) = e.ts;
+            if constexpr (PHASE == 1) { ev(a.b.act, ui) = e.act0; ev(a.b.act + N, ui) = e.act1; ev(a.b.act + (2) * N, ui) = e.act2; }
+            if constexpr (PHASE == 2) { if (aux == PD_PHASE_FLIP_OVER) ev(a.b.act, ui) = e.act0; }
+            if constexpr (WIND) {
+                ev(a.b.wind, ui) = e.fu0; ev(a.b.wind + N, ui) = e.fu1; ev(a.b.wind + (2) * N, ui) = e.fv0; ev(a.b.wind + (3) * N, ui) = e.fv1;
+                ev(a.b.wind + (4) * N, ui) = e.sgu; ev(a.b.wind + (5) * N, ui) = e.sgv;
+                ev(a.b.wprof, ui) = (uint8_t)e.prof;
+            }
+        }
+        // neighbourhood caches survive resets (any valid 50-set is a correct start)
+        if (part == 0) {
+            ev(a.b.key + (my_table) * N, ui) = cA.key; ev(a.b.slot + (my_table) * N, ui) = cA.slot;
+            if constexpr (LPE == 1) { ev(a.b.key + N, ui) = cB.key; ev(a.b.slot + N, ui) = cB.slot; }
+        }
+    }
+#ifdef PD_STAMP
+    PD_T(t_end);
+    PD_ACC(6, t_end - t_rtd);
+    if (__lane_id() == 0) {
+#pragma unroll
+        for (int k = 0; k < 7; ++k) atomicAdd(&a.pend.stats[kStStamp + k], acc_[k]);
+        atomicAdd(&a.pend.stats[kStStamp + 7], 1ull);
+    }
+#endif
+}
+
+// ---------------------------------------------------------------- launchers
+template <typename R, int PH, int RT, bool W, int LPE> void launch_step(const StepArgs<R>& a, hipStream_t s) {
+    unsigned grid = (unsigned)((a.n * LPE + kStepBlock - 1) / kStepBlock);
+    hipLaunchKernelGGL((k_step<R, PH, RT, W, LPE>), dim3(grid), dim3(kStepBlock), 0, s, a);
+}
+
+template <typename R, int PH, bool W, int LPE> void launch_policy_lpe(const StepArgs<R>& a, int64_t n_launch,
+                                                                      hipStream_t s) {
+    unsigned grid = (unsigned)((n_launch * LPE + kStepBlock - 1) / kStepBlock);
+    hipLaunchKernelGGL((k_step<R, PH, 1, W, LPE, 1>), dim3(grid), dim3(kStepBlock), 0, s, a);
+}
+
+}  // namespace pd

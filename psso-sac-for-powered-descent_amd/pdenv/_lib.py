@@ -11,7 +11,7 @@ LIB_PATH = os.path.join(HERE, "libpdenv.so")
 
 D, I32, I64, U64 = C.c_double, C.c_int32, C.c_int64, C.c_uint64
 MAX_PTS, MAX_COLS, MAX_TAB, MAX_WIND, N_PROF = 256, 5, 64, 16, 50
-N_STATE, N_INFO = 11, 16
+N_STATE, N_INFO = 11, 49
 
 PD_OK, PD_ERR_INVALID, PD_ERR_HIP, PD_ERR_NOMEM, PD_ERR_UNSUPPORTED = range(5)
 (PURE_THROTTLE, LANDING_BURN, PCONTROL, BALLISTIC_ARC, FLIP_OVER, SUBSONIC, SUPERSONIC,
@@ -20,9 +20,17 @@ RTD_RL, RTD_PSO, RTD_NONE = 0, 1, 2
 F64, F32 = 0, 1
 ACTOR_PARAMS = {0: 249, 1: 372}   # PD_ACTOR_PARAMS_PURE_THROTTLE / _LANDING_BURN
 
+# pd_info_field order (include/pdenv.h): the last physics sub-step's quantities
 INFO_FIELDS = ["air_density", "atmospheric_pressure", "speed_of_sound", "mach_number",
                "dynamic_pressure", "CL", "CD", "mass_flow", "x_cog", "inertia",
-               "alpha_effective", "throttle", "g_load_1_sec_window", "ug", "vg", "gimbal_angle_deg"]
+               "alpha_effective", "throttle", "g_load_1_sec_window", "ug", "vg", "gimbal_angle_deg",
+               "mach_number_max", "drag", "lift", "d_cp_cg", "d_thrust_cg", "fuel_percentage_consumed",
+               "control_force_parallel", "control_force_perpendicular", "control_force_x", "control_force_y",
+               "aero_force_x", "aero_force_y", "gravity", "F_wind_x", "F_wind_y", "vx_dot", "vy_dot",
+               "control_moment_z", "aero_moment_z", "M_wind_z", "moments_z", "theta_dot_dot",
+               "delta_command_left_rad", "delta_command_right_rad", "delta_left_rad", "delta_right_rad",
+               "C_a", "C_n_L", "C_n_R", "gf_F_perpendicular", "gf_F_parallel", "gf_Mz", "theta_in"]
+assert len(INFO_FIELDS) == N_INFO
 
 
 class PdAeroTable(C.Structure):
@@ -72,9 +80,13 @@ class PdConfig(C.Structure):
                 ("dt", D), ("discount_factor", D), ("trajectory_length", I32), ("pad3", I32)]
 
 
-EXPORTS = ["pd_abi_version", "pd_sizeof_params", "pd_sizeof_config", "pd_last_error", "pd_device_count", "pd_create", "pd_destroy", "pd_reset",
-           "pd_step", "pd_step_n", "pd_rollout", "pd_rollout_policy", "pd_pso_step", "pd_flush_misses", "pd_observe", "pd_get_state", "pd_set_state", "pd_get_actuators",
-           "pd_set_actuators", "pd_set_gload_window", "pd_set_wind_sigmas", "pd_counters", "pd_obs_dim", "pd_action_dim"]
+EXPORTS = ["pd_abi_version", "pd_sizeof_params", "pd_sizeof_config", "pd_last_error", "pd_device_count", "pd_create",
+           "pd_destroy", "pd_reset", "pd_step", "pd_step_n", "pd_rollout", "pd_rollout_policy", "pd_pso_step",
+           "pd_flush_misses", "pd_observe", "pd_get_state", "pd_set_state", "pd_get_actuators", "pd_set_actuators",
+           "pd_set_gload_window", "pd_get_gload_window", "pd_set_wind_sigmas", "pd_get_wind_state",
+           "pd_set_wind_state", "pd_get_counters", "pd_set_counters", "pd_checkpoint_size", "pd_checkpoint_save",
+           "pd_checkpoint_load", "pd_counters", "pd_stats", "pd_atmosphere", "pd_obs_dim", "pd_action_dim"]
+ABI_VERSION = 3
 
 _lib = None
 
@@ -115,15 +127,27 @@ def load(path=None):
     L.pd_set_wind_sigmas.argtypes = [vp, vp, vp]
     L.pd_set_gload_window.argtypes = [vp, vp, vp, vp, vp]
     L.pd_counters.argtypes = [vp, P(I64), P(I64), P(I64), P(I64)]
+    L.pd_stats.argtypes = [vp, P(I64), I32]
+    L.pd_atmosphere.argtypes = [vp, vp, vp, I64, vp]
+    L.pd_get_gload_window.argtypes = [vp, vp, vp, vp, vp, vp]
+    L.pd_get_wind_state.argtypes = [vp, vp, vp, vp, vp]
+    L.pd_set_wind_state.argtypes = [vp, vp, vp, vp, vp]
+    L.pd_get_counters.argtypes = [vp, vp, vp, vp, vp]
+    L.pd_set_counters.argtypes = [vp, vp, vp, vp, vp]
+    L.pd_checkpoint_size.argtypes = [vp]; L.pd_checkpoint_size.restype = C.c_size_t
+    L.pd_checkpoint_save.argtypes = [vp, vp, vp]
+    L.pd_checkpoint_load.argtypes = [vp, vp, vp]
     L.pd_obs_dim.argtypes = [vp]; L.pd_obs_dim.restype = C.c_int
     L.pd_action_dim.argtypes = [vp]; L.pd_action_dim.restype = C.c_int
     for name in ("pd_create", "pd_destroy", "pd_reset", "pd_step", "pd_step_n", "pd_rollout", "pd_rollout_policy", "pd_pso_step", "pd_flush_misses", "pd_observe",
                  "pd_get_state", "pd_set_state", "pd_get_actuators", "pd_set_actuators",
-                 "pd_set_wind_sigmas", "pd_set_gload_window", "pd_counters"):
+                 "pd_set_wind_sigmas", "pd_set_gload_window", "pd_counters", "pd_stats", "pd_get_gload_window",
+                 "pd_get_wind_state", "pd_set_wind_state", "pd_get_counters", "pd_set_counters",
+                 "pd_checkpoint_save", "pd_checkpoint_load", "pd_atmosphere"):
         getattr(L, name).restype = C.c_int
     L.pd_sizeof_params.restype = C.c_size_t
     L.pd_sizeof_config.restype = C.c_size_t
-    if L.pd_abi_version() != 2:
+    if L.pd_abi_version() != ABI_VERSION:
         raise PdError("libpdenv ABI version mismatch")
     if L.pd_sizeof_params() != C.sizeof(PdParams) or L.pd_sizeof_config() != C.sizeof(PdConfig):
         raise PdError("pd_params/pd_config layout mismatch between ctypes and libpdenv.so")

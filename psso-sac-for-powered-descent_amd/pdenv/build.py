@@ -1,37 +1,75 @@
-"""Compile libpdenv.so for gfx950 in-tree (hipcc cross-compiles without a GPU)."""
+"""Compile libpdenv.so for gfx950 in-tree (hipcc cross-compiles without a GPU).
+
+The step kernel is instantiated per (precision, phase family, wind) in 12 objects from
+csrc/kstep.hip, compiled in parallel with the host unit (pdenv.hip) and the PSO kernels
+(pdpso.hip), then linked into one shared library.  Objects are rebuilt when any source is
+newer than them."""
+import concurrent.futures as cf
 import os
 import subprocess
 import sys
 
 PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
-SRCS = [os.path.join(ROOT, "csrc", f) for f in ("pdenv.hip", "pdpso.hip")]
+CSRC = os.path.join(ROOT, "csrc")
+OBJ = os.path.join(ROOT, "build", "obj")
 OUT = os.path.join(PKG, "libpdenv.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 # -ffp-contract=off: no FMA contraction, so binary64 arithmetic follows the reference's
 # (CPython/NumPy) operation-by-operation rounding.
 # -disable-machine-licm: machine LICM hoists the literal constants of the inlined libm
 # polynomials out of the sub-step loop into VGPRs (>60 VGPRs, a 2x occupancy loss).
-FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared",
+FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC",
          "-Wno-unused-result", "-mllvm", "-disable-machine-licm"]
+KSTEP = [(r, ph, w) for r in (0, 1) for ph in (0, 1, 2) for w in (0, 1)]
+
+
+def units(extra=()):
+    """(object path, source, defines) of every translation unit."""
+    u = [(os.path.join(OBJ, "pdenv.o"), "pdenv.hip", []), (os.path.join(OBJ, "pdpso.o"), "pdpso.hip", [])]
+    for r, ph, w in KSTEP:
+        u.append((os.path.join(OBJ, f"kstep_r{r}_p{ph}_w{w}.o"), "kstep.hip",
+                  [f"-DPD_KR={r}", f"-DPD_KPH={ph}", f"-DPD_KW={w}"]))
+    return [(o, os.path.join(CSRC, s), list(d) + list(extra)) for o, s, d in u]
 
 
 def sources():
-    d = os.path.join(ROOT, "csrc")
-    return [os.path.join(d, f) for f in os.listdir(d)] + [os.path.join(os.path.dirname(ROOT), "include", "pdenv.h")]
+    return [os.path.join(CSRC, f) for f in os.listdir(CSRC)] + [os.path.join(os.path.dirname(ROOT), "include", "pdenv.h")]
+
+
+def _newest_source():
+    return max(os.path.getmtime(s) for s in sources())
 
 
 def up_to_date():
     if not os.path.exists(OUT):
         return False
-    t = os.path.getmtime(OUT)
-    return all(os.path.getmtime(s) <= t for s in sources())
+    return _newest_source() <= os.path.getmtime(OUT)
 
 
-def build(force=False, verbose=True):
-    if not force and up_to_date():
+def _compile(job, verbose):
+    obj, src, defs = job
+    cmd = [HIPCC] + FLAGS + defs + ["-c", "-o", obj, src]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc failed for {os.path.basename(obj)}:\n{r.stderr}")
+    return obj
+
+
+def build(force=False, verbose=True, jobs=None, extra=()):
+    """Compile stale objects in parallel (at most `jobs`, default the CPU count capped at 16) and
+    link libpdenv.so.  `extra`: additional hipcc flags (experiments; forces a rebuild)."""
+    if not force and not extra and up_to_date():
         return OUT
-    cmd = [HIPCC] + FLAGS + ["-o", OUT] + SRCS
+    os.makedirs(OBJ, exist_ok=True)
+    newest = _newest_source()
+    todo = [u for u in units(extra) if force or extra or not os.path.exists(u[0]) or os.path.getmtime(u[0]) < newest]
+    jobs = jobs or min(16, os.cpu_count() or 4)
+    with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
+        list(ex.map(lambda j: _compile(j, verbose), todo))
+    cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", OUT] + [u[0] for u in units()]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)

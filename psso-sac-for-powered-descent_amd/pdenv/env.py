@@ -174,9 +174,17 @@ class PoweredDescentEnv:
     def trunc_id_buf(self):
         return self._tid
 
+    def _check_actions(self, a):
+        """[T, N, A] with A the handle's action width: the kernel reads row t of env i at
+        (t N + i) A + k, so anything narrower would be read past its end."""
+        if a.dim() != 3 or a.shape[1] != self.n or a.shape[2] != self.action_dim:
+            raise ValueError(f"actions must be [T, {self.n}, {self.action_dim}] (got {list(a.shape)})")
+
     def rollout(self, actions, reward_sum=None):
         """T step launches over device-resident actions [T, N, A]; returns summed rewards [N]."""
+        self._check_steppable()
         a = actions.to(device=self.device, dtype=self.action_dtype).contiguous()
+        self._check_actions(a)
         T = a.shape[0]
         rs = reward_sum if reward_sum is not None else torch.zeros(self.n, dtype=self.dtype, device=self.device)
         L.check(self.lib.pd_rollout(self.h, _ptr(a), int(T), _ptr(rs), _stream(self.device)))
@@ -190,9 +198,8 @@ class PoweredDescentEnv:
         outputs=False writes nothing per step and returns None."""
         self._check_steppable()
         a = actions.to(device=self.device, dtype=self.action_dtype).contiguous()
+        self._check_actions(a)
         T = int(a.shape[0])
-        if a.dim() != 3 or a.shape[1] != self.n:
-            raise ValueError(f"actions must be [T, {self.n}, A]")
         if outputs:
             kw = dict(device=self.device)
             obs = torch.empty(T, self.n, self._obs.shape[-1], dtype=self.dtype, **kw)
@@ -206,12 +213,16 @@ class PoweredDescentEnv:
         L.check(self.lib.pd_step_n(self.h, _ptr(a), T, *ptrs, _stream(self.device)))
         self._steps += T
         if outputs:
+            if T > 0:   # the handle's step buffers (obs_buf, ...) hold the last step, as after step()
+                for dst, src in zip((self._obs, self._rew, self._done, self._trunc, self._tid), (obs, rew, dn, tr, tid)):
+                    dst.copy_(src[-1])
             return obs, rew, dn.bool(), tr.bool(), tid
 
     def step_n_raw(self, actions, outputs=None):
-        """Hot-loop pd_step_n: actions a contiguous [T, N, A] device tensor of action_dtype;
-        outputs None or preallocated (obs [T,N,O], reward [T,N], done, truncated uint8 [T,N],
-        trunc_id int8 [T,N]).  No copies, allocations or syncs."""
+        """Hot-loop pd_step_n: actions a contiguous [T, N, A] device tensor of action_dtype (the
+        caller guarantees the shape: nothing is checked here); outputs None or preallocated
+        (obs [T,N,O], reward [T,N], done, truncated uint8 [T,N], trunc_id int8 [T,N]).  No copies,
+        allocations or syncs; the handle's obs_buf/... are not updated."""
         ptrs = [None] * 5 if outputs is None else [_ptr(x) for x in outputs]
         L.check(self.lib.pd_step_n(self.h, C.c_void_p(actions.data_ptr()), int(actions.shape[0]), *ptrs,
                                    _stream(self.device)))
@@ -278,6 +289,73 @@ class PoweredDescentEnv:
                                            _ptr(steps), int(check_every), _stream(self.device)))
         self._keep = wt                               # alive until the stream has consumed it
         return fit, steps
+
+    # ------------------------------------------------------------------ checkpoint / restore
+    def checkpoint(self):
+        """Every per-env buffer (state, g-load window, actuators, wind, counters, aero caches)
+        as one device uint8 tensor (pd_checkpoint_save)."""
+        blob = torch.empty(int(self.lib.pd_checkpoint_size(self.h)), dtype=torch.uint8, device=self.device)
+        L.check(self.lib.pd_checkpoint_save(self.h, _ptr(blob), _stream(self.device)))
+        return blob
+
+    def restore(self, blob):
+        """Load a checkpoint() of a handle with the same configuration; stepping then continues
+        bit-identically to the saved handle."""
+        b = blob.to(device=self.device, dtype=torch.uint8).contiguous()
+        if b.numel() != int(self.lib.pd_checkpoint_size(self.h)):
+            raise ValueError("checkpoint size does not match this handle's configuration")
+        L.check(self.lib.pd_checkpoint_load(self.h, _ptr(b), _stream(self.device)))
+        torch.cuda.current_stream(self.device).synchronize()
+
+    def gload_window(self):
+        """(vprev [N], ring [N, 10], len [N], head [N]) of the g-load window (base_environment.py:136-149)."""
+        kw = dict(device=self.device)
+        vp = torch.empty(self.n, dtype=self.dtype, **kw)
+        w = torch.empty(10, self.n, dtype=self.dtype, **kw)
+        ln = torch.empty(self.n, dtype=torch.uint8, **kw)
+        hd = torch.empty(self.n, dtype=torch.uint8, **kw)
+        L.check(self.lib.pd_get_gload_window(self.h, _ptr(vp), _ptr(w), _ptr(ln), _ptr(hd), _stream(self.device)))
+        return vp, w.t().contiguous(), ln, hd
+
+    def wind_state(self):
+        """(filters [N, 4] = u0 u1 v0 v1, sigmas [N, 2], percentile [N] int) of the wind model."""
+        kw = dict(device=self.device)
+        f = torch.empty(4, self.n, dtype=self.dtype, **kw)
+        s = torch.empty(2, self.n, dtype=self.dtype, **kw)
+        pr = torch.empty(self.n, dtype=torch.uint8, **kw)
+        L.check(self.lib.pd_get_wind_state(self.h, _ptr(f), _ptr(s), _ptr(pr), _stream(self.device)))
+        return f.t().contiguous(), s.t().contiguous(), pr.to(torch.int32) + 50
+
+    def set_wind_state(self, filters=None, sigmas=None, percentile=None):
+        kw = dict(device=self.device)
+        f = None if filters is None else torch.as_tensor(filters, dtype=self.dtype).to(**kw).reshape(self.n, 4).t().contiguous()
+        s = None if sigmas is None else torch.as_tensor(sigmas, dtype=self.dtype).to(**kw).reshape(self.n, 2).t().contiguous()
+        pr = None if percentile is None else (torch.as_tensor(percentile).to(**kw).reshape(self.n) - 50).to(torch.uint8).contiguous()
+        L.check(self.lib.pd_set_wind_state(self.h, _ptr(f), _ptr(s), _ptr(pr), _stream(self.device)))
+        torch.cuda.current_stream(self.device).synchronize()
+
+    def episode_counters(self):
+        """(episode [N], step within episode [N], truncation id [N]) -- the Philox counter words."""
+        kw = dict(device=self.device)
+        ep = torch.empty(self.n, dtype=torch.int32, **kw)
+        st = torch.empty(self.n, dtype=torch.int32, **kw)
+        tid = torch.empty(self.n, dtype=torch.int8, **kw)
+        L.check(self.lib.pd_get_counters(self.h, _ptr(ep), _ptr(st), _ptr(tid), _stream(self.device)))
+        return ep, st, tid
+
+    def atmosphere(self, altitude):
+        """The handle's ISA (pd_atmosphere) at altitudes [n]: (density, pressure, speed_of_sound)."""
+        alt = torch.as_tensor(altitude, dtype=self.dtype).to(self.device).reshape(-1).contiguous()
+        out = torch.empty(3, alt.numel(), dtype=self.dtype, device=self.device)
+        L.check(self.lib.pd_atmosphere(self.h, _ptr(alt), _ptr(out), int(alt.numel()), _stream(self.device)))
+        return out[0], out[1], out[2]
+
+    def stats(self):
+        """Device statistics words (pd_stats): misses, NaN events, table entries, dropped queue entries."""
+        v = (L.I64 * 32)()
+        L.check(self.lib.pd_stats(self.h, v, 32))
+        return {"rbf_misses": v[0], "nan_events": v[1], "table_entries_cd": v[2], "table_entries_cl": v[3],
+                "miss_queue_dropped": v[16]}
 
     def counters(self):
         v = [L.I64() for _ in range(4)]

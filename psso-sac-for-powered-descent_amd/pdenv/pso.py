@@ -33,6 +33,53 @@ PSO_PARAMS = {
 ACTOR_DIM = {"landing_burn_pure_throttle": 249, "landing_burn": 372}
 
 
+def all_gather_var(t, dist):
+    """Every rank's 1-D tensor `t` concatenated in rank order, for shards of DIFFERENT lengths
+    (after re_initialise_swarms the ranks keep different numbers of particles, possibly none):
+    the lengths are gathered first, each shard padded to the longest, gathered, and trimmed."""
+    if dist is None:
+        return t
+    world = dist.get_world_size()
+    n = torch.tensor([t.numel()], dtype=torch.int64, device=t.device)
+    ns = [torch.empty_like(n) for _ in range(world)]
+    dist.all_gather(ns, n)
+    ns = [int(x) for x in ns]
+    m = max(ns)
+    pad = torch.zeros(m, dtype=t.dtype, device=t.device)
+    pad[:t.numel()] = t
+    parts = [torch.empty_like(pad) for _ in range(world)]
+    dist.all_gather(parts, pad)
+    return torch.cat([parts[r][:ns[r]] for r in range(world)])
+
+
+def reinit_keep(pbf, swarm, n_swarms, keep_n):
+    """re_initialise_swarms' selection (particle_swarm_optimisation.py:360-370) on the global
+    population: per subswarm the keep_n particles with the best personal-best fitness (stable,
+    the lowest index first on ties).  Returns the boolean keep mask."""
+    keep = torch.zeros_like(pbf, dtype=torch.bool)
+    for s in range(n_swarms):
+        idx = torch.nonzero(swarm == s).flatten()
+        order = torch.argsort(pbf[idx], stable=True)[:keep_n]
+        keep[idx[order]] = True
+    return keep
+
+
+def migration_moves(swarm, n_swarms, n_migrants, rng):
+    """migrate_particles' decisions (particle_swarm_optimisation.py:545-553) on the global
+    membership `swarm` (subswarm id per global particle): [(particle, new subswarm)]."""
+    members = [list(torch.nonzero(swarm == s).flatten().cpu().numpy()) for s in range(n_swarms)]
+    moves = []
+    for i in range(n_swarms):
+        if len(members[i]) > 1:
+            for _ in range(n_migrants):
+                k = rng.randrange(len(members[i]))
+                g = members[i].pop(k)
+                t = rng.choice([j for j in range(n_swarms) if j != i])
+                members[t].append(g)
+                moves.append((int(g), t))
+    return moves
+
+
 class ParticleSubswarmOptimisationGPU:
     """One rank's shard of the swarm.  Global particle g belongs to subswarm g // (pop / S)
     (initialize_swarms, :372-389); rank r holds particles [r*P_local, (r+1)*P_local)."""
@@ -185,21 +232,8 @@ class ParticleSubswarmOptimisationGPU:
         """:545-553: number_of_migrants random particles of every subswarm (with > 1 member) move
         to a random other subswarm.  Decisions are taken on the global membership (all ranks
         draw the same choices); each rank applies those that hit its own particles."""
-        sw = self.swarm
-        if self.dist:
-            parts = [torch.empty_like(sw) for _ in range(self.world)]
-            self.dist.all_gather(parts, sw)
-            sw = torch.cat(parts)
-        members = [list(torch.nonzero(sw == s).flatten().cpu().numpy()) for s in range(self.S)]
-        moves = []
-        for i in range(self.S):
-            if len(members[i]) > 1:
-                for _ in range(self.p["number_of_migrants"]):
-                    k = self.rng.randrange(len(members[i]))
-                    g = members[i].pop(k)
-                    t = self.rng.choice([j for j in range(self.S) if j != i])
-                    members[t].append(g)
-                    moves.append((g, t))
+        sw = all_gather_var(self.swarm, self.dist)
+        moves = migration_moves(sw, self.S, self.p["number_of_migrants"], self.rng)
         for g, t in moves:
             if self.offset <= g < self.offset + self.P:
                 self.swarm[g - self.offset] = t
@@ -208,18 +242,9 @@ class ParticleSubswarmOptimisationGPU:
         """:360-370: every subswarm keeps its re_initialise_number_of_particles // S best
         particles (by personal best fitness); the rest are dropped."""
         keep_n = self.p["re_initialise_number_of_particles"] // self.S
-        pbf, sw = self.pbf, self.swarm
-        if self.dist:
-            a = [torch.empty_like(pbf) for _ in range(self.world)]
-            b = [torch.empty_like(sw) for _ in range(self.world)]
-            self.dist.all_gather(a, pbf)
-            self.dist.all_gather(b, sw)
-            pbf, sw = torch.cat(a), torch.cat(b)
-        keep = torch.zeros_like(pbf, dtype=torch.bool)
-        for s in range(self.S):
-            idx = torch.nonzero(sw == s).flatten()
-            order = torch.argsort(pbf[idx], stable=True)[:keep_n]
-            keep[idx[order]] = True
+        pbf = all_gather_var(self.pbf, self.dist)
+        sw = all_gather_var(self.swarm, self.dist)
+        keep = reinit_keep(pbf, sw, self.S, keep_n)
         mine = keep[self.offset:self.offset + self.P]
         sel = torch.nonzero(mine).flatten()
         self.x, self.v, self.pb = (t[:, sel].contiguous() for t in (self.x, self.v, self.pb))

@@ -18,15 +18,100 @@ from . import _lib as L
 from .env import PoweredDescentEnv
 
 
-def _info_dict(env, ex, state, action):
-    """The info keys the drivers read (sac_pytorch_powered_descent.py:253-374), last sub-step."""
-    info = {k: float(ex[k][0]) for k in L.INFO_FIELDS if k in ex}
-    info["state"] = [float(v) for v in state]
-    info["actions"] = action
-    info["action_info"] = {"throttle": info.get("throttle", float("nan"))}
-    if env.flight_phase == "landing_burn":
-        info["action_info"]["gimbal_angle_deg"] = info.get("gimbal_angle_deg", float("nan"))
+def _acs_info(v, q_s):
+    """acs_model.py:62-86 from the kernel's ACS quantities (qS = dynamic_pressure * grid_fin_area)."""
+    dl, dr, ca, cnl, cnr = v["delta_left_rad"], v["delta_right_rad"], v["C_a"], v["C_n_L"], v["C_n_R"]
+    th, ae = v["theta_in"], v["alpha_effective"]
+    fpar, fperp = v["gf_F_parallel"], v["gf_F_perpendicular"]
+    return {
+        "alpha_local_left_rad": ae - dl, "alpha_local_right_rad": ae - dr,
+        "C_n_L": cnl, "C_a_L": ca, "C_n_R": cnr, "C_a_R": ca,
+        "F_n_L": cnl * q_s, "F_a_L": ca * q_s, "F_n_R": cnr * q_s, "F_a_R": ca * q_s,
+        "F_perpendicular_L": q_s * (cnl * math.cos(dl) - ca * math.sin(dl)),
+        "F_perpendicular_R": q_s * (cnr * math.cos(dr) - ca * math.sin(dr)),
+        "F_perpendicular": fperp,
+        "F_parallel_L": q_s * (ca * math.cos(dl) + cnl * math.sin(dl)),
+        "F_parallel_R": q_s * (ca * math.cos(dr) + cnr * math.sin(dr)),
+        "F_parallel": fpar,
+        "Fx": fpar * math.cos(th) + fperp * math.sin(th),
+        "Fy": fpar * math.sin(th) - fperp * math.cos(th),
+        "Mz": v["gf_Mz"], "d_fin_cg": v["_d_base_gf"] - v["x_cog"],
+        "delta_left_rad": dl, "delta_right_rad": dr,
+    }
+
+
+def info_dict(flight_phase, ex, state, actions, params, i=0):
+    """The info dict of rocket_physics_fcn (rockets_physics.py:649-702) + the env's keys
+    (base_environment.py:134-149) for env i, built from pd_step's info tap (the last sub-step's
+    quantities, include/pdenv.h pd_info_field) and the post-step state.  Entries that are
+    arithmetic of those (accelerations, F_n = C_n qS, ...) are formed here as the reference forms
+    them; trigonometric ones may differ from the reference's in the last ulp."""
+    v = {k: float(ex[k][i]) for k in L.INFO_FIELDS if k in ex}
+    v["_d_base_gf"] = float(params.struct.d_base_grid_fin)
+    s = [float(x) for x in state]
+    mass, gamma = s[8], s[6]
+    g, drag, lift = v["gravity"], v["drag"], v["lift"]
+    acc = {
+        "acceleration_x_component_control": v["control_force_x"] / mass,
+        "acceleration_y_component_control": v["control_force_y"] / mass,
+        "acceleration_x_component_drag": -drag * math.cos(gamma) / mass,
+        "acceleration_y_component_drag": -drag / mass * math.sin(gamma) / mass,
+        "acceleration_x_component_lift": -lift * math.cos(math.pi - gamma) / mass,
+        "acceleration_y_component_lift": lift * math.sin(math.pi - gamma) / mass,
+        "acceleration_x_component_gravity": 0,
+        "acceleration_y_component_gravity": -g,
+        "acceleration_x_component": v["vx_dot"],
+        "acceleration_y_component": v["vy_dot"],
+        "acceleration_x_component_wind": v["F_wind_x"] / mass,
+        "acceleration_y_component_wind": v["F_wind_y"] / mass,
+    }
+    mom = {"control_moment_z": v["control_moment_z"], "aero_moment_z": v["aero_moment_z"],
+           "moments_z": v["moments_z"], "theta_dot_dot": v["theta_dot_dot"], "M_wind_z": v["M_wind_z"]}
+    q_s = v["dynamic_pressure"] * float(params.struct.grid_fin_area)
+    if flight_phase in ("landing_burn_pure_throttle", "landing_burn_pure_throttle_Pcontrol"):
+        ai = {"throttle": v["throttle"], "acs_info": _acs_info(v, q_s)}
+    elif flight_phase == "landing_burn":
+        ai = {"throttle": v["throttle"], "delta_command_left_rad": v["delta_command_left_rad"],
+              "delta_command_right_rad": v["delta_command_right_rad"], "gimbal_angle_deg": v["gimbal_angle_deg"],
+              "acs_info": _acs_info(v, q_s)}
+    elif flight_phase in ("subsonic", "supersonic"):
+        ai = {"gimbal_angle_deg": v["gimbal_angle_deg"], "throttle": v["throttle"]}
+    elif flight_phase == "flip_over_boostbackburn":
+        ai = {"gimbal_angle_deg": v["gimbal_angle_deg"]}
+    else:
+        ai = {"RCS_throttle": actions}
+    info = {
+        "inertia": v["inertia"], "acceleration_dict": acc, "mach_number": v["mach_number"],
+        "mach_number_max": v["mach_number_max"], "CL": v["CL"], "CD": v["CD"], "drag": drag, "lift": lift,
+        "moment_dict": mom, "d_cp_cg": v["d_cp_cg"], "d_thrust_cg": v["d_thrust_cg"], "x_cog": v["x_cog"],
+        "dynamic_pressure": v["dynamic_pressure"], "mass_flow": v["mass_flow"],
+        "fuel_percentage_consumed": v["fuel_percentage_consumed"],
+        "control_force_parallel": v["control_force_parallel"],
+        "control_force_perpendicular": v["control_force_perpendicular"],
+        "control_force_x": v["control_force_x"], "control_force_y": v["control_force_y"],
+        "aero_force_x": v["aero_force_x"], "aero_force_y": v["aero_force_y"], "gravity_force_y": -g * mass,
+        "atmospheric_pressure": v["atmospheric_pressure"], "air_density": v["air_density"],
+        "speed_of_sound": v["speed_of_sound"], "action_info": ai, "ug": v["ug"], "vg": v["vg"],
+        "alpha_effective": v["alpha_effective"],
+        "state": s, "actions": actions, "g_load_1_sec_window": v["g_load_1_sec_window"],
+    }
     return info
+
+
+_ATM = {}
+
+
+def maximum_velocity(y, vy):
+    """env_wrapped_rl_pytorch.py:60-66: sqrt(2 p / rho) of the ISA at altitude y (the handle's
+    device atmosphere, pd_atmosphere), or vy above the ISA's top.  The SAC driver imports it as
+    maximum_velocity_lambda (sac_pytorch_powered_descent.py:11, used at :370)."""
+    if "env" not in _ATM:
+        _ATM["env"] = PoweredDescentEnv(1, "landing_burn_pure_throttle", mode="rl")
+    rho, p, a = _ATM["env"].atmosphere(torch.tensor([float(y)], dtype=torch.float64))
+    rho, p, a = float(rho[0]), float(p[0]), float(a[0])
+    if a != 0:
+        return math.sqrt(2 * p / rho)
+    return vy
 
 
 # state_dim / action_dim per phase (env_wrapped_rl_pytorch.py:87-104)
@@ -103,7 +188,8 @@ class rl_wrapped_env_pytorch:
         obs, r, d, tr, ex = self.env.step(a, info=True)
         state = self.env.state[0].cpu().numpy()
         self._tid = int(ex["trunc_id"][0])
-        info = _info_dict(self.env, {k: v.cpu() for k, v in ex.items() if k != "trunc_id"}, state, a.cpu().numpy())
+        info = info_dict(self.flight_phase, {k: v.cpu() for k, v in ex.items() if k != "trunc_id"}, state,
+                         a.cpu().numpy(), self.env.params)
         return obs[0].double().cpu().numpy(), float(r[0]), bool(d[0]), bool(tr[0]), info
 
     def truncation_id(self):
@@ -174,10 +260,16 @@ class pso_wrapper:
         return getattr(self, "_tid", 0)
 
     def step(self, action):
+        """env_wrapped_ea.py:125-129: (augmented state, reward, done, truncated, info) with the full
+        info dict of rocket_physics_fcn (the PSO driver's collect_trajectory_data /
+        save_trajectory_data flatten it, particle_swarm_optimisation.py:759-833)."""
         a = action.detach().reshape(1, -1).float()
-        obs, r, d, tr, ex = self.env.step(a)
+        obs, r, d, tr, ex = self.env.step(a, info=True)
         self._tid = int(ex["trunc_id"][0])
-        return obs[0].double().cpu().numpy(), float(r[0]), bool(d[0]), bool(tr[0]), {"state": self.env.state[0].tolist()}
+        state = self.env.state[0].cpu().numpy()
+        info = info_dict(self.flight_phase, {k: v.cpu() for k, v in ex.items() if k != "trunc_id"}, state,
+                         action.detach().cpu().numpy(), self.env.params)
+        return obs[0].double().cpu().numpy(), float(r[0]), bool(d[0]), bool(tr[0]), info
 
     def reset(self):
         return self.env.reset()[0].double().cpu().numpy()
@@ -270,3 +362,58 @@ class pso_wrapped_env:
     @property
     def bounds_array(self):
         return np.array(self.bounds)
+
+    def plot_results(self, individual, save_path):
+        """env_wrapped_ea.py:224-229 (called by the PSO driver every save_interval generations,
+        particle_swarm_optimisation.py:503): one episode of the particle's actor, as
+        universal_physics_plotter runs it (universal_physics_plotter.py:94-103), saved as
+        save_path + 'trajectory.csv' (state, action, reward and the flattened info per step)
+        and, when matplotlib is importable, save_path + 'Simulation.png'.  The reference's other
+        figures are out of scope (plotting)."""
+        import csv
+        import os
+        self.individual_update_model(individual)
+        state = self.env.reset()
+        rows, done_or_truncated, total = [], False, 0.0
+        while not done_or_truncated:
+            action = self.actor.forward(state)
+            state, reward, done, truncated, info = self.env.step(action)
+            total += reward
+            done_or_truncated = done or truncated
+            row = {"reward": reward}
+            row.update({k: v for k, v in zip(["x", "y", "vx", "vy", "theta", "theta_dot", "gamma", "alpha", "mass",
+                                               "mass_propellant", "time"], info["state"])})
+            for j, u in enumerate(np.asarray(action.detach()).ravel()):
+                row[f"u{j}"] = float(u)
+
+            def flat(d, prefix=""):
+                for k, v in d.items():
+                    if isinstance(v, dict):
+                        flat(v, f"{prefix}{k}_")
+                    elif k not in ("state", "actions") and np.isscalar(v):
+                        row[f"{prefix}{k}"] = v
+            flat(info)
+            rows.append(row)
+        os.makedirs(os.path.dirname(save_path) or ".", exist_ok=True)
+        with open(save_path + "trajectory.csv", "w", newline="") as f:
+            w = csv.DictWriter(f, fieldnames=list(rows[0].keys()))
+            w.writeheader()
+            w.writerows(rows)
+        try:
+            import matplotlib
+            matplotlib.use("Agg")
+            import matplotlib.pyplot as plt
+        except ImportError:
+            return rows
+        t = [r["time"] for r in rows]
+        fig, ax = plt.subplots(2, 2, figsize=(12, 8))
+        for a_, key in zip(ax.ravel(), ("y", "vy", "mass_propellant", "dynamic_pressure")):
+            a_.plot(t, [r[key] for r in rows])
+            a_.set_xlabel("time [s]")
+            a_.set_ylabel(key)
+            a_.grid(True)
+        fig.suptitle(f"{self.flight_phase}: episode reward {total:.4g}")
+        fig.tight_layout()
+        fig.savefig(save_path + "Simulation.png")
+        plt.close(fig)
+        return rows

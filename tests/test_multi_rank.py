@@ -167,3 +167,37 @@ def test_prioritized_buffer_sampling_distribution():
     # weights of the last draw: (size * p)^-beta / max, beta as it was before the last anneal
     wr = (5 * p[idx.numpy()]) ** (-1.0)
     assert np.allclose(w.numpy().ravel(), wr / wr.max(), rtol=1e-6)
+
+
+def _pso_uneven_worker(rank, world, port, out):
+    """After re_initialise_swarms the ranks hold different numbers of particles (rank 1 none):
+    the variable-size gathers and the migration decisions must still agree on every rank."""
+    import random
+    sys.path.insert(0, os.path.join(REPO, "psso-sac-for-powered-descent_amd"))
+    from pdenv.pso import all_gather_var, migration_moves, reinit_keep
+    _init(rank, world, port)
+    # global population of 12 in 2 subswarms; rank 0 holds 0..5, rank 1 holds 6..11
+    g = torch.Generator().manual_seed(4)
+    pbf_all = torch.rand(12, generator=g, dtype=torch.float64)
+    sw_all = torch.tensor([0] * 6 + [1] * 6, dtype=torch.int32)
+    mine = slice(0, 6) if rank == 0 else slice(6, 12)
+    keep = reinit_keep(all_gather_var(pbf_all[mine].contiguous(), dist),
+                       all_gather_var(sw_all[mine].contiguous(), dist), 2, 3)
+    assert torch.equal(keep, reinit_keep(pbf_all, sw_all, 2, 3))
+    # uneven shards: rank 0 keeps 5 particles of both subswarms, rank 1 none (an empty shard)
+    local = torch.tensor([0, 1, 0, 1, 1], dtype=torch.int32) if rank == 0 else torch.empty(0, dtype=torch.int32)
+    sw = all_gather_var(local, dist)
+    moves = migration_moves(sw, 2, 1, random.Random(9))
+    out[rank] = (sw.tolist(), moves)
+    dist.destroy_process_group()
+
+
+def test_pso_uneven_shards_gather_and_migrate():
+    """after re-initialisation shards differ in size; migrate_particles and a second
+    re-initialisation gather with all_gather_var (sizes first, padded, trimmed) on two gloo ranks."""
+    port = _free_port()
+    out = mp.Manager().dict()
+    mp.spawn(_pso_uneven_worker, args=(2, port, out), nprocs=2, join=True)
+    assert out[0] == out[1]
+    assert out[0][0] == [0, 1, 0, 1, 1]
+    assert len(out[0][1]) == 2
