@@ -5,13 +5,16 @@ profile of a percentile drawn per reset (WindModel(given_percentile=None),
 full_wind_model.py:27-33) plus von Karman gusts (vonkarman.py:33-36), a pitch tilt N(0, 1 deg)
 at every reset, and auto-reset.  The reference draws its randomness from np.random with
 seed(None) (vonkarman.py:88), so no run of it can be replayed; the oracle instead restates the
-device's Philox4x32-10 draw scheme (oracle/pd_oracle.c orc_reset_philox / orc_gauss_pair), and
-sampled envs of the full-size GPU run are followed env for env.  The oracle's wind model itself
-is pinned to the reference by tests/test_oracle_golden.py (recorded normals, every percentile).
+device's Philox4x32-10 draw scheme (oracle/pd_oracle.c orc_reset_philox / orc_gauss_pair).  The
+env is chaotic (a 1-ulp pitch change moves the oracle's own rewards by 4e-3 within an episode,
+tests/test_oracle_golden.py::test_oracle_episode_chaos_bound), so sampled envs of the full-size
+run are teacher-forced against the oracle at every step (tests/shadow.py) instead of being
+compared after hundreds of free-running steps.  The oracle's wind model itself is pinned to the
+reference by tests/test_oracle_golden.py (recorded normals, every percentile).
 
-Tolerances (f64 handle): per-step reward <= 1e-9 absolute, done/truncated/trunc_id exact, obs
-<= 1e-6 (float32-cast state), final state <= 1e-8 relative on y, vy, masses, time, <= 1e-6 on the
-attitude channels (chaotic).
+Tolerances (f64 handle, per env-step): state <= 1e-10 relative (theta_dot 1e-8), reward <= 1e-9
+absolute, done/truncated/trunc_id exact, obs <= 1e-6 (float32-cast state), gust filters <= 1e-12,
+auto-resets bit-identical.
 """
 import math
 
@@ -21,7 +24,6 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 ST = ["x", "y", "vx", "vy", "theta", "theta_dot", "gamma", "alpha", "mass", "mass_propellant", "time"]
-TOL_STATE = np.array([1e-6, 1e-8, 1e-6, 1e-8, 1e-6, 1e-6, 1e-6, 1e-6, 1e-10, 1e-10, 1e-12])
 
 
 @pytest.fixture(scope="module")
@@ -39,37 +41,51 @@ def c3_env(pd, n, seed=1234, **kw):
     return pd.PoweredDescentEnv(n, **args)
 
 
-def test_c3_full_size_vs_oracle(pd, oracle_mod):
-    """65 536 envs x 200 steps of the c3 workload through pd_step_n (16 steps per launch, state in
-    registers across the fused steps); 96 sampled envs (both ends of the batch, and spread
-    through it) followed by the oracle under the same draws: every step's reward, done,
-    truncated, trunc_id and observation, and the final state."""
+def c3_actions(T, N, seed):
+    """Random actions U(-1, 1) on every 4th env (episodes end by truncation after ~130 steps and
+    auto-reset), U(0.5, 1) elsewhere (high throttle: the vehicles get below the 15 km gust
+    ceiling, vonkarman.py / full_wind_model.py:39-41, where the Philox gust draws act)."""
     import torch
-    N, T = 65536, 200
-    g = torch.Generator().manual_seed(7)
-    A = (torch.rand(T, N, 1, generator=g) * 2 - 1).contiguous()
-    env = c3_env(pd, N)
-    _, _, prof0 = env.wind_state()
-    obs, rew, dn, tr, tid = env.step_n(A.cuda())
-    idx = np.unique(np.concatenate([np.arange(16), np.arange(N - 16, N), np.linspace(16, N - 17, 64).astype(int)]))
-    it = torch.tensor(idx, device=obs.device)
-    got = dict(reward=rew[:, it].cpu().numpy(), done=dn[:, it].cpu().numpy(), trunc=tr[:, it].cpu().numpy(),
-               trunc_id=tid[:, it].cpu().numpy(), obs=obs[:, it].cpu().numpy())
-    S = env.state[it].cpu().numpy()
-    prof = prof0[it].cpu().numpy()
-    o = oracle_mod.rollout_philox(0, 0, idx, np.zeros(len(idx)), A[:, idx].numpy(), auto_reset=True, wind=True,
-                                  stochastic=True, fixed_prof=-1, tilt=math.radians(1.0), seed=1234, obs_dim=2)
-    # coverage: resets happened, the sample spans many percentiles
-    assert (got["done"] | got["trunc"]).sum() >= len(idx), "every sampled env should end an episode"
-    assert len(set(prof.tolist())) >= 20, sorted(set(prof.tolist()))
-    assert np.array_equal(got["done"].astype(bool), o["done"].astype(bool))
-    assert np.array_equal(got["trunc"].astype(bool), o["trunc"].astype(bool))
-    assert np.array_equal(got["trunc_id"], o["trunc_id"])
-    assert np.abs(got["reward"] - o["reward"]).max() <= 1e-9
-    assert np.abs(got["obs"] - o["obs"]).max() <= 1e-6
-    err = np.abs(S - o["state"]) / np.maximum(np.abs(o["state"]), 1e-3)
-    assert (err.max(0) <= TOL_STATE).all(), dict(zip(ST, err.max(0)))
+    g = torch.Generator().manual_seed(seed)
+    u = torch.rand(T, N, 1, generator=g)
+    hi = torch.arange(N) % 4 != 0
+    a = torch.where(hi.view(1, N, 1), 0.5 + 0.5 * u, 2 * u - 1)
+    return a.contiguous()
+
+
+def c3_sample(N):
+    return np.unique(np.concatenate([np.arange(16), np.arange(N - 16, N), np.linspace(16, N - 17, 64).astype(int)]))
+
+
+def test_c3_full_size_shadowed(pd, oracle_mod):
+    """65 536 envs x 400 steps of the c3 workload (wind with a percentile drawn per reset, gusts,
+    tilt, auto-reset), stepped by pd_step; 96 sampled envs (both ends of the batch and spread
+    through it) teacher-forced against the oracle at every step (tests/shadow.py): state <= 1e-10
+    rel (theta_dot 1e-8), reward <= 1e-9, done/truncated/trunc_id exact, obs <= 1e-6, gust filters
+    <= 1e-12, every auto-reset bit-identical.  Then the same 400 steps through pd_step_n (16 fused
+    steps per launch, state in registers) from a fresh handle: every output and the final state
+    bit-identical to the per-step run."""
+    import torch
+    from shadow import shadow_run, check_stats
+    N, T, seed = 65536, 400, 1234
+    A = c3_actions(T, N, 7).cuda()
+    idx = c3_sample(N)
+    env = c3_env(pd, N, seed=seed)
+    st = shadow_run(oracle_mod, env, A, idx, 0, 0, seed, math.radians(1.0))
+    check_stats(st)
+    # coverage: resets, gusts, many percentiles, the truncations random actions reach
+    assert st["resets"] >= len(idx), st["resets"]
+    assert st["gust_steps"] >= 20 * len(idx), st["gust_steps"]
+    assert len(st["profiles"]) >= 20, sorted(st["profiles"])
     assert env.counters()["nan_events"] == 0
+    S_loop = env.state
+    ref = st["outs"]
+    env2 = c3_env(pd, N, seed=seed)
+    obs, rew, dn, tr, tid = env2.step_n(A)
+    assert torch.equal(obs, ref["obs"]) and torch.equal(rew, ref["rew"])
+    assert torch.equal(dn, ref["done"]) and torch.equal(tr, ref["trunc"]) and torch.equal(tid, ref["tid"])
+    assert torch.equal(env2.state, S_loop)
+    assert torch.equal(env2.checkpoint(), env.checkpoint())
 
 
 def test_c3_full_size_properties(pd):
@@ -77,7 +93,7 @@ def test_c3_full_size_properties(pd):
     propellant never grows, and every env that ended is back at the initial state with its own
     tilt (theta perturbed, alpha = theta - gamma, all other channels the nominal ones)."""
     import torch
-    N, T = 65536, 200
+    N, T = 65536, 300
     env = c3_env(pd, N, seed=99)
     g = torch.Generator(device="cuda").manual_seed(0)
     s_nom = torch.tensor(env.params.state0, dtype=torch.float64, device="cuda")
@@ -103,42 +119,33 @@ def test_c3_full_size_properties(pd):
 
 
 @pytest.mark.parametrize("percentile", [50, 57, 63, 75, 88, 98, 99])
-def test_fixed_percentile_profiles_vs_oracle(pd, oracle_mod, percentile):
+def test_fixed_percentile_profiles_shadowed(pd, oracle_mod, percentile):
     """Each percentile's horizontal profile (HorizontalWindSpeed.py:44-114) with gusts, 64 envs x
-    150 steps, against the oracle on the same draws (the profiles are pinned to the reference by
-    tests/test_oracle_golden.py::test_wind_profiles_every_percentile)."""
-    import torch
-    N, T = 64, 150
-    A = (torch.rand(T, N, 1, generator=torch.Generator().manual_seed(percentile)) * 2 - 1).contiguous()
+    300 steps (mostly high throttle, so the vehicles descend through the gust band), every step
+    teacher-forced against the oracle (tests/shadow.py; the profiles are pinned to the reference
+    by tests/test_oracle_golden.py::test_wind_profiles_every_percentile)."""
+    from shadow import shadow_run, check_stats
+    N, T = 64, 300
+    A = c3_actions(T, N, percentile).cuda()
     env = c3_env(pd, N, seed=5, wind_percentile=percentile)
-    obs, rew, dn, tr, tid = env.step_n(A.cuda())
-    o = oracle_mod.rollout_philox(0, 0, np.arange(N), np.zeros(N), A.numpy(), wind=True, stochastic=True,
-                                  fixed_prof=percentile - 50, tilt=math.radians(1.0), seed=5, obs_dim=2)
-    assert np.array_equal(dn.cpu().numpy().astype(bool), o["done"].astype(bool))
-    assert np.array_equal(tid.cpu().numpy(), o["trunc_id"])
-    assert np.abs(rew.cpu().numpy() - o["reward"]).max() <= 1e-9
-    S = env.state.cpu().numpy()
-    err = np.abs(S - o["state"]) / np.maximum(np.abs(o["state"]), 1e-3)
-    assert (err.max(0) <= TOL_STATE).all(), dict(zip(ST, err.max(0)))
+    st = shadow_run(oracle_mod, env, A, np.arange(N), 0, 0, 5, math.radians(1.0), fixed_prof=percentile - 50)
+    check_stats(st)
+    assert st["gust_steps"] >= 20 * N and st["resets"] >= N // 4
+    assert st["profiles"] == {percentile - 50}
     assert (env.wind_state()[2].cpu().numpy() == percentile).all()
 
 
-def test_landing_burn_wind_vs_oracle(pd, oracle_mod):
+def test_landing_burn_wind_shadowed(pd, oracle_mod):
     """The PSO driver's phase (landing_burn, 4 actions, actuator memory) with the c3 wind and
-    tilt: 256 envs x 60 steps against the oracle under the same draws."""
+    tilt: 128 envs x 120 steps, every step teacher-forced against the oracle (PSO reward)."""
     import torch
-    N, T = 256, 60
-    A = (torch.rand(T, N, 4, generator=torch.Generator().manual_seed(3)) * 2 - 1).contiguous()
+    from shadow import shadow_run, check_stats
+    N, T = 128, 120
+    A = (torch.rand(T, N, 4, generator=torch.Generator().manual_seed(3)) * 2 - 1).contiguous().cuda()
     env = c3_env(pd, N, seed=11, flight_phase="landing_burn", mode="pso")
-    obs, rew, dn, tr, tid = env.step_n(A.cuda())
-    o = oracle_mod.rollout_philox(1, 1, np.arange(N), np.zeros(N), A.numpy(), wind=True, stochastic=True,
-                                  fixed_prof=-1, tilt=math.radians(1.0), seed=11, obs_dim=5)
-    d_ok = (dn.cpu().numpy().astype(bool) == o["done"].astype(bool)).all(0) & \
-        (tid.cpu().numpy() == o["trunc_id"]).all(0)
-    # tumbling landing_burn vehicles amplify last-ulp differences (SURVEY 0.6): bounds on the ensemble
-    assert d_ok.mean() >= 0.95, d_ok.mean()
-    r_ok = (np.abs(rew.cpu().numpy() - o["reward"]) <= 1e-6 * np.maximum(1, np.abs(o["reward"]))).all(0)
-    assert r_ok.mean() >= 0.95, r_ok.mean()
+    st = shadow_run(oracle_mod, env, A, np.arange(N), 1, 1, 11, math.radians(1.0))
+    check_stats(st)
+    assert st["resets"] >= N // 2
 
 
 def test_checkpoint_restore_continues_bit_identically(pd):
@@ -146,7 +153,7 @@ def test_checkpoint_restore_continues_bit_identically(pd):
     (state, g-load window, actuators, wind filters/sigmas/percentile, episode and step counters,
     aero caches), restore into a fresh handle, and continue: outputs and state bit-identical."""
     import torch
-    N, T1, T2 = 4096, 37, 45
+    N, T1, T2 = 4096, 150, 45
     A = (torch.rand(T1 + T2, N, 4, device="cuda", generator=torch.Generator(device="cuda").manual_seed(2)) * 2 - 1)
     for phase, adim in (("landing_burn_pure_throttle", 1), ("landing_burn", 4)):
         a = A[..., :adim].contiguous()
@@ -168,6 +175,10 @@ def test_checkpoint_restore_continues_bit_identically(pd):
             assert torch.equal(x, y)
         for x, y in zip(src.gload_window(), dst.gload_window()):
             assert torch.equal(x, y)
+
+
+FORCE_KEYS = ("drag", "lift", "aero_force_x", "aero_force_y")
+A_FRONT = 107.5131545874767   # sizing_results.csv frontal area (param_pack.json)
 
 
 def test_info_tap_vs_oracle(pd, oracle_mod):
@@ -195,4 +206,8 @@ def test_info_tap_vs_oracle(pd, oracle_mod):
                 if k not in ex:
                     continue
                 gv, ov = float(ex[k][i]), info[k]
-                assert abs(gv - ov) <= 1e-9 * max(1.0, abs(ov)), (tag, i, k, gv, ov)
+                # forces built from C_L/C_D carry their absolute 1e-9 tolerance times q A_front
+                scale = max(1.0, abs(ov))
+                if k in FORCE_KEYS:
+                    scale = max(scale, info["dynamic_pressure"] * A_FRONT)
+                assert abs(gv - ov) <= 1e-9 * scale, (tag, i, k, gv, ov)

@@ -196,7 +196,7 @@ def test_prioritized_buffer_on_device(pd):
 
 def test_c5_collector_4096_envs_prioritized(pd):
     """c5's per-GPU share: 4 096 envs, the reference Actor (2-256-256-1), HIP-graph collection into
-    the device prioritized buffer (1e6, the driver's size): 120 steps with auto-resets, then the
+    the device prioritized buffer (1e6, the driver's size): 220 steps with auto-resets, then the
     learner's sample -> update_priorities round trip."""
     import torch
     from pdenv.sac import Actor, DevicePrioritizedReplayBuffer, SACCollector
@@ -206,10 +206,10 @@ def test_c5_collector_4096_envs_prioritized(pd):
     actor = Actor(2, 1).cuda()
     buf = DevicePrioritizedReplayBuffer(1_000_000, 2, 1, "cuda")
     col = SACCollector(env, actor, buf, use_graph=True)
-    for _ in range(120):
+    for _ in range(220):
         col.step()
     torch.cuda.synchronize()
-    assert len(buf) == 120 * N
+    assert len(buf) == 220 * N
     assert torch.isfinite(buf.data[:len(buf)]).all()
     assert (buf.data[:len(buf), 2].abs() <= 1).all()                 # tanh-squashed actions
     assert float(buf.data[:len(buf), 6].sum()) >= 0                   # done flags are 0/1
