@@ -12,6 +12,10 @@ constexpr int kSys = kNbr + 3;      // + degree-1 polynomial tail (TPS default d
 constexpr int kCols = 5;            // AoA columns of each V2 table
 constexpr int kPay = 64;            // payload (binary64): 50 kernel coefs, 3 poly, shift0/1, scale0/1,
 constexpr int kPayIdx = kNbr + 3 + 4;   // then from slot 57 the 50 points' table indices as bytes
+// Byte position of term j's point index in the index area.  Terms 0..39 are chunk-interleaved:
+// term 10c + u (c < 4) is byte c of word u, so one load of words 0..9 serves the step kernel's
+// four 10-term chunks (byte c extracted by a shift); terms 40..49 follow at bytes 40..49.
+PD_HD constexpr int idx_pos(int j) { return j < 40 ? 4 * (j % 10) + j / 10 : j; }
 constexpr int kKeyLoBits = 6, kKeyLenBits = 6, kKeyField = kKeyLoBits + kKeyLenBits;
 constexpr uint64_t kEmptyKey = ~0ull;
 
@@ -203,7 +207,7 @@ PD_HD int solve_neighbourhood(const double* mach, const double* coef, const int*
     payload[kSys + 0] = sh0; payload[kSys + 1] = sh1;
     payload[kSys + 2] = sc0; payload[kSys + 3] = sc1;
     for (int j = kSys + 4; j < kPay; ++j) payload[j] = 0.0;
-    __builtin_memcpy((uint8_t*)(payload + kPayIdx), idx, kNbr);
+    for (int j = 0; j < kNbr; ++j) ((uint8_t*)(payload + kPayIdx))[idx_pos(j)] = idx[j];
     return 0;
 }
 

@@ -84,6 +84,64 @@ __device__ __forceinline__ R rbf_eval(const PD_AS1 R* __restrict__ pay, const R*
                                       int part, int nparts) {
     const PD_AS1 uint32_t* iw = (const PD_AS1 uint32_t*)(pay + kPayIdx);
     R s0 = R(0), s1 = R(0);
+    // one term: c_j d2 log(d2) accumulated (the 1/2 of phi is applied once at the end); d2 = 0
+    // (query on a table point) contributes c_j * 0 * finite = 0
+    auto term = [&](R mj, R aj, R cj, bool odd) {
+        R dm = M - mj, da = a - aj;
+        R d2 = dm * dm + da * da;
+        R w = d2 * cj;
+#ifdef PD_EXP_NOLOG
+        R l = d2;
+#elif defined(PD_EXP_LIBLOG)
+        R l = log(d2 > R(0) ? d2 : R(1));
+#else
+        R l = eval_log<R>(sizeof(R) == 8 ? d2 : (d2 > R(1e-30) ? d2 : R(1e-30)));
+#endif
+        if (odd) s1 = fma(w, l, s1); else s0 = fma(w, l, s0);
+    };
+#ifndef PD_RBF_STRIDED
+    if (nparts == 1) {
+        // The lane owns all 50 terms.  The index bytes of terms 0..39 are chunk-interleaved
+        // (idx_pos): words 0..9, loaded once, hold chunk c's ten indices in byte c, so a chunk's
+        // table points come from LDS without waiting on a global load; its ten coefficients are
+        // one contiguous 80-byte load.  Terms 40..49 (words 10..12, in order) end the sum.
+        uint32_t wd[10];
+#pragma unroll
+        for (int u = 0; u < 10; ++u) wd[u] = iw[u];
+#pragma unroll 1
+        for (int c = 0; c < 4; ++c) {
+            R mm[10], aa[10], pp[10];
+#pragma unroll
+            for (int u = 0; u < 10; ++u) {
+                const int ix = (int)((wd[u] >> (8 * c)) & 0xffu);
+                mm[u] = smach[ix];
+                aa[u] = saoa[ix];
+                pp[u] = pay[10 * c + u];
+            }
+#pragma unroll
+            for (int u = 0; u < 10; ++u) term(mm[u], aa[u], pp[u], u & 1);
+        }
+        {
+            const uint32_t x0 = iw[10], x1 = iw[11], x2 = iw[12];
+            R mm[10], aa[10], pp[10];
+#pragma unroll
+            for (int u = 0; u < 10; ++u) {
+                const uint32_t wv = u < 4 ? x0 : (u < 8 ? x1 : x2);
+                const int ix = (int)((wv >> (8 * (u & 3))) & 0xffu);
+                mm[u] = smach[ix];
+                aa[u] = saoa[ix];
+                pp[u] = pay[40 + u];
+            }
+#pragma unroll
+            for (int u = 0; u < 10; ++u) term(mm[u], aa[u], pp[u], u & 1);
+        }
+        R s = R(0.5) * (s0 + s1);
+        s += R(1) * pay[kNbr];
+        s += (M - pay[kSys + 0]) / pay[kSys + 2] * pay[kNbr + 1];
+        s += (a - pay[kSys + 1]) / pay[kSys + 3] * pay[kNbr + 2];
+        return s;
+    }
+#endif
 #ifndef PD_CHUNK
 #define PD_CHUNK 10
 #endif
@@ -91,39 +149,29 @@ __device__ __forceinline__ R rbf_eval(const PD_AS1 R* __restrict__ pay, const R*
     // Chunks as a loop: fully unrolled, the scheduler hoists every chunk's loads ahead and the
     // kernel spills (256 VGPRs + 260 spilled); rolled it needs 235 VGPRs and no scratch.
     // PD_RBF_UNROLL restores the full unroll (experiments).
-#ifdef PD_RBF_UNROLL
+#if defined(PD_RBF_UNROLL) || defined(PD_RBF_SB)
 #pragma unroll
 #else
 #pragma unroll 1
 #endif
     for (int j0 = part; j0 < kNbr; j0 += kChunk * nparts) {
+#ifdef PD_RBF_SB
+        __builtin_amdgcn_sched_barrier(0);
+#endif
         R mm[kChunk], aa[kChunk], pp[kChunk];
 #pragma unroll
         for (int u = 0; u < kChunk; ++u) {
             int j = j0 + u * nparts;
             bool ok = j < kNbr;
             int jj = ok ? j : 0;
-            const int ix = (int)((iw[jj >> 2] >> ((jj & 3) * 8)) & 0xffu);
+            const int bp = idx_pos(jj);
+            const int ix = (int)((iw[bp >> 2] >> ((bp & 3) * 8)) & 0xffu);
             mm[u] = smach[ix];
             aa[u] = saoa[ix];
             pp[u] = ok ? pay[jj] : R(0);
         }
 #pragma unroll
-        for (int u = 0; u < kChunk; ++u) {
-            R dm = M - mm[u], da = a - aa[u];
-            R d2 = dm * dm + da * da;
-            // c_j d2 log(d2) accumulated (the 1/2 of phi is applied once below); d2 = 0 (query
-            // on a table point) contributes c_j * 0 * finite = 0
-            R w = d2 * pp[u];
-#ifdef PD_EXP_NOLOG
-            R l = d2;
-#elif defined(PD_EXP_LIBLOG)
-            R l = log(d2 > R(0) ? d2 : R(1));
-#else
-            R l = eval_log<R>(sizeof(R) == 8 ? d2 : (d2 > R(1e-30) ? d2 : R(1e-30)));
-#endif
-            if (u & 1) s1 = fma(w, l, s1); else s0 = fma(w, l, s0);
-        }
+        for (int u = 0; u < kChunk; ++u) term(mm[u], aa[u], pp[u], u & 1);
     }
     R s = R(0.5) * (s0 + s1);
     if (part == 0) {
@@ -239,14 +287,14 @@ __device__ __forceinline__ void solve_wave(DP<R>& P, int table, unsigned long lo
     else if (lane == kSys + 3) pay[kSys + 3] = sc1;
     else if (lane < kPay) pay[lane] = 0.0;
     wave_mem_sync();
-    if (lane < kNbr) ((PD_AS1 uint8_t*)(pay + kPayIdx))[lane] = (uint8_t)my_idx;
+    if (lane < kNbr) ((PD_AS1 uint8_t*)(pay + kPayIdx))[idx_pos(lane)] = (uint8_t)my_idx;
     wave_mem_sync();
     // payload in the kernel's precision, in the (now free) matrix area (pay_store, by lanes)
     PD_AS1 R* pr = (PD_AS1 R*)work;
     if (lane < kPayIdx) pr[lane] = (R)pay[lane];
     else if (lane < pay_stride<R>()) pr[lane] = R(0);
     wave_mem_sync();
-    if (lane < kNbr) ((PD_AS1 uint8_t*)(pr + kPayIdx))[lane] = (uint8_t)my_idx;
+    if (lane < kNbr) ((PD_AS1 uint8_t*)(pr + kPayIdx))[idx_pos(lane)] = (uint8_t)my_idx;
     wave_mem_sync();
 }
 

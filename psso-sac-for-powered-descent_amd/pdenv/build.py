@@ -78,3 +78,20 @@ def build(force=False, verbose=True, jobs=None, extra=()):
 
 if __name__ == "__main__":
     build(force="--force" in sys.argv)
+
+
+def build_variant(name, defines, unit=(0, 0, 1)):
+    """Experiments: libpdenv_<name>.so with the step-kernel object of `unit` (precision, phase
+    family, wind; default the c3 one) compiled with extra `defines`, the other objects shared
+    with the main build (which must be current).  Returns the library path."""
+    build(verbose=False)
+    r, ph, w = unit
+    odir = os.path.join(ROOT, "build", "obj_" + name)
+    os.makedirs(odir, exist_ok=True)
+    obj = os.path.join(odir, f"kstep_r{r}_p{ph}_w{w}.o")
+    _compile((obj, os.path.join(CSRC, "kstep.hip"), [f"-DPD_KR={r}", f"-DPD_KPH={ph}", f"-DPD_KW={w}"] + list(defines)),
+             False)
+    out = os.path.join(PKG, f"libpdenv_{name}.so")
+    objs = [obj if os.path.basename(u[0]) == os.path.basename(obj) else u[0] for u in units()]
+    subprocess.run([HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", out] + objs, check=True)
+    return out

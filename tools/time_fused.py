@@ -1,0 +1,45 @@
+#!/usr/bin/env python3
+"""Time the c3 workload through pd_step_n (16 fused env-steps per launch) with the library named by
+PDENV_LIB (default the in-tree one): one JSON line with the event-timed k_step launch average and
+the wall ms per env-step.  N, LAUNCHES, PREC, LPE, PHASE from the environment."""
+import json
+import math
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "psso-sac-for-powered-descent_amd"))
+import torch  # noqa: E402
+import pdenv  # noqa: E402
+
+n = int(os.environ.get("N", "65536"))
+launches = int(os.environ.get("LAUNCHES", "24"))
+F = 16
+phase = os.environ.get("PHASE", "landing_burn_pure_throttle")
+env = pdenv.PoweredDescentEnv(n, flight_phase=phase, mode="rl" if phase == "landing_burn_pure_throttle" else "pso",
+                              precision=os.environ.get("PREC", "f64"), enable_wind=True, stochastic_wind=True,
+                              wind_percentile=None, auto_reset=True, tilt_sigma_rad=math.radians(1.0), seed=1234,
+                              lanes_per_env=int(os.environ.get("LPE", "0")))
+g = torch.Generator(device="cuda").manual_seed(42)
+acts = (torch.rand((launches + 8) * F, n, env.action_dim, generator=g, device="cuda") * 2 - 1).contiguous()
+kw = dict(device="cuda")
+outs = (torch.empty(F, n, env.obs_dim, dtype=env.dtype, **kw), torch.empty(F, n, dtype=env.dtype, **kw),
+        torch.empty(F, n, dtype=torch.uint8, **kw), torch.empty(F, n, dtype=torch.uint8, **kw),
+        torch.empty(F, n, dtype=torch.int8, **kw))
+for k in range(8):
+    env.step_n_raw(acts[k * F:(k + 1) * F], outs)
+torch.cuda.synchronize()
+ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(launches)]
+t0 = time.perf_counter()
+for k in range(launches):
+    ev[k][0].record()
+    env.step_n_raw(acts[(8 + k) * F:(9 + k) * F], outs)
+    ev[k][1].record()
+torch.cuda.synchronize()
+wall = time.perf_counter() - t0
+ms = sorted(a.elapsed_time(b) for a, b in ev)
+print(json.dumps({"lib": os.path.basename(os.environ.get("PDENV_LIB", "libpdenv.so")), "n": n,
+                  "launch_ms_avg": sum(ms) / len(ms), "launch_ms_med": ms[len(ms) // 2],
+                  "ms_per_step": sum(ms) / len(ms) / F, "wall_ms_per_step": wall * 1e3 / (launches * F),
+                  "misses": env.counters()["rbf_misses"]}), flush=True)

@@ -1,0 +1,17 @@
+#!/usr/bin/env python3
+"""Build experiment variants of libpdenv (c3 step-kernel object only) in parallel:
+python tools/variants.py name=-DFOO,-DBAR name2=-DBAZ ..."""
+import concurrent.futures as cf
+import os
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                "psso-sac-for-powered-descent_amd"))
+from pdenv import build as b  # noqa: E402
+
+if __name__ == "__main__":
+    b.build(verbose=False)
+    specs = [a.split("=", 1) for a in sys.argv[1:]]
+    with cf.ThreadPoolExecutor(max_workers=8) as ex:
+        for p in ex.map(lambda s: b.build_variant(s[0], [d for d in s[1].split(",") if d]), specs):
+            print(p)
