@@ -106,8 +106,19 @@ inline void log_table_fill(LogTable& t) {
         t.logc[i] = (double)(-logl((long double)invc));
     }
 }
-PD_HD double log_tab(double x, const double* invc, const double* logc) {
+// S: element stride of the cell arrays (the device keeps (invc, logc) interleaved, S = 2)
+// log x from x = 2^e m and the cell's (invc, logc)
+PD_HD double log_tab_finish(double m, double e, double invc, double logc) {
     const double ln2 = 6.93147180559945286227e-01;
+    double r = fma(m, invc, -1.0);
+    double t = fma(r, 0.2, -0.25);
+    t = fma(r, t, 1.0 / 3.0);
+    t = fma(r, t, -0.5);
+    double p = fma(r * r, t, r);
+    return fma(e, ln2, logc + p);
+}
+template <int S = 1>
+PD_HD double log_tab(double x, const double* invc, const double* logc) {
     uint64_t b;
     __builtin_memcpy(&b, &x, 8);
     uint32_t hi = (uint32_t)(b >> 32);
@@ -116,12 +127,7 @@ PD_HD double log_tab(double x, const double* invc, const double* logc) {
     uint64_t mb = (b & 0x000fffffffffffffull) | 0x3ff0000000000000ull;
     double m;
     __builtin_memcpy(&m, &mb, 8);
-    double r = fma(m, invc[i], -1.0);
-    double t = fma(r, 0.2, -0.25);
-    t = fma(r, t, 1.0 / 3.0);
-    t = fma(r, t, -0.5);
-    double p = fma(r * r, t, r);
-    return fma(e, ln2, logc[i] + p);
+    return log_tab_finish(m, e, invc[S * i], logc[S * i]);
 }
 
 // Build and solve the thin-plate-spline system of ONE 50-point neighbourhood, exactly the
@@ -278,9 +284,10 @@ PD_HD void sincos_fd(double x, double& s, double& c) {
 // rho sin 2 pi u2).  The log is log_tab (cell table from log_table_fill), sqrt is correctly
 // rounded, sincos_fd is IEEE-only: the oracle restates this and draws the same bits.  The
 // wind gusts (vonkarman.py:34, one np.random.randn() per filter step) and the tilt use it.
+template <int S = 1>
 PD_HD void gauss_pair(u32x4 r, const double* invc, const double* logc, double& z0, double& z1) {
     const double u1 = 1.0 - u01(r.x, r.y), u2 = u01(r.z, r.w);
-    const double rho = sqrt(-2.0 * log_tab(u1, invc, logc));
+    const double rho = sqrt(-2.0 * log_tab<S>(u1, invc, logc));
     double s, c;
     sincos_fd(6.283185307179586 * u2, s, c);
     z0 = rho * c;

@@ -42,8 +42,9 @@ template <typename R> struct EnvRegs {
 // (Philox tag kTagTilt, alpha = theta - gamma); actuator memory, g-load window and wind filters
 // zeroed; sigma_u, sigma_v ~ U (VKDisturbanceGenerator._new_filters, vonkarman.py:60-66) and
 // the percentile randint(50, 99) (WindModel.compile_horizontal_fixed_wind,
-// full_wind_model.py:27-33) from Philox tag kTagReset.  invc/logc: the log_tab cells.
-template <typename R>
+// full_wind_model.py:27-33) from Philox tag kTagReset.  invc/logc: the log_tab cells (element
+// stride S: 2 for the step kernel's interleaved LDS copy).
+template <typename R, int S = 1>
 __device__ __forceinline__ void reset_values(DP<R>& P, const StepArgs<R>& a, uint64_t g, uint32_t episode,
                                              const double* invc, const double* logc, EnvRegs<R>& e) {
 #pragma unroll
@@ -51,7 +52,7 @@ __device__ __forceinline__ void reset_values(DP<R>& P, const StepArgs<R>& a, uin
     if (a.use_tilt) {
         u32x4 r = philox({(uint32_t)g, (uint32_t)(g >> 32) ^ episode, 0u, kTagTilt}, a.seed_lo, a.seed_hi);
         double z0, z1;
-        gauss_pair(r, invc, logc, z0, z1);
+        gauss_pair<S>(r, invc, logc, z0, z1);
         e.s[4] = e.s[4] + (R)(a.tilt_sigma * z0);
         e.s[7] = e.s[4] - e.s[6];
     }

@@ -112,10 +112,20 @@ constexpr int kIsaCols = 8;
 // ---------------------------------------------------------------- logarithms
 // Hot-path log(): binary64 through the LDS-staged cell table (log_tab, pd_common.h; the step
 // kernel stages it before its barrier), binary32 through the hardware log2.
-__shared__ double s_logtab[2 * kLogCells];
+// (invc, logc) of cell i at [2i], [2i + 1]: one 16-byte ds_read_b128 per log
+__shared__ __attribute__((aligned(16))) double s_logtab[2 * kLogCells];
 template <typename R> __device__ __forceinline__ R eval_log(R x);
 template <> __device__ __forceinline__ double eval_log<double>(double x) {
-    return log_tab(x, s_logtab, s_logtab + kLogCells);
+    uint64_t b;
+    __builtin_memcpy(&b, &x, 8);
+    const uint32_t hi = (uint32_t)(b >> 32);
+    const double e = (double)((int)(hi >> 20) - 1023);
+    const uint32_t i = (hi >> (20 - kLogBits)) & (kLogCells - 1);
+    const uint64_t mb = (b & 0x000fffffffffffffull) | 0x3ff0000000000000ull;
+    double m;
+    __builtin_memcpy(&m, &mb, 8);
+    const double2 c = ((const double2*)s_logtab)[i];
+    return log_tab_finish(m, e, c.x, c.y);
 }
 template <> __device__ __forceinline__ float eval_log<float>(float x) {
     return __builtin_amdgcn_logf(x) * 0.693147180559945309f;
@@ -313,7 +323,7 @@ template <typename R> struct RbfCache {
 
 template <typename R>
 __device__ __forceinline__ R d2_at(const R* mach, int start, int i, R M, R dz) {
-    R dm = M - mach[start + i];
+    R dm = M - mach[2 * (start + i)];   // (Mach, AoA) pairs in LDS
     return dm * dm + dz;
 }
 
@@ -345,7 +355,7 @@ __device__ __forceinline__ int knn_windows(const R* smach, const PD_AS4 int* sta
         for (int c = 0; c < kCols; ++c) {
             if (len[c] == 0 && dz[c] < maxin) {
                 int l = 0, h = n[c];
-                while (l < h) { int mid = (l + h) >> 1; if (smach[start[c] + mid] < M) l = mid + 1; else h = mid; }
+                while (l < h) { int mid = (l + h) >> 1; if (smach[2 * (start[c] + mid)] < M) l = mid + 1; else h = mid; }
                 if (l > 0) { R d = d2_at(smach, start[c], l - 1, M, dz[c]); if (d < minex) { minex = d; minc = c; mini = l - 1; } }
                 if (l < n[c]) { R d = d2_at(smach, start[c], l, M, dz[c]); if (d < minex) { minex = d; minc = c; mini = l; } }
             }

@@ -50,8 +50,7 @@ __device__ __forceinline__ void div_pair(R a0, R b0, R a1, R b1, int role, R& q0
 // LPE = 2 lane role 0 owns C_D and role 1 owns C_L; with LPE = 4/8/16 each table is owned by
 // LPE/2 lanes that split its 50-term thin-plate sum (terms k = part, part + nparts, ..).
 template <typename R> struct TabView {
-    const R* smach;            // LDS: the table's Mach values, 512 further on each point's AoA
-    const R* saoa;
+    const R* smach;            // LDS: the table's points as (Mach, AoA) pairs (smach[2i], smach[2i + 1])
     const PD_AS4 int* start;   // column geometry (uniform: scalar loads)
     const PD_AS4 int* n;
     const PD_AS4 R* aoa;
@@ -79,9 +78,29 @@ template <typename R> struct LineLds {
 // The payload names each term's table point by a byte index, whose (Mach, AoA) sit in LDS; the
 // terms are evaluated in chunks of 10 independent terms so that the loads of a chunk are in
 // flight together and the 10 log chains interleave.
+// The index words and the first coefficient chunk of one payload.  (Requesting them for the
+// env's cached neighbourhood at the start of each sub-step, to overlap the atmosphere and the
+// lookup, measured 17 % slower: the registers held across the sub-step spill.)
+template <typename R> struct PayPre {
+    uint32_t wd[10], x0, x1, x2;
+    R pn[10];
+    int slot;
+};
 template <typename R>
-__device__ __forceinline__ R rbf_eval(const PD_AS1 R* __restrict__ pay, const R* smach, const R* saoa, R M, R a,
+__device__ __forceinline__ void pay_prefetch(const PD_AS1 R* __restrict__ pay, PayPre<R>& p) {
+    const PD_AS1 uint32_t* iw = (const PD_AS1 uint32_t*)(pay + kPayIdx);
+#pragma unroll
+    for (int u = 0; u < 10; ++u) p.wd[u] = iw[u];
+    p.x0 = iw[10]; p.x1 = iw[11]; p.x2 = iw[12];
+#pragma unroll
+    for (int u = 0; u < 10; ++u) p.pn[u] = pay[u];
+}
+
+template <typename R>
+__device__ __forceinline__ R rbf_eval(const PD_AS1 R* __restrict__ pay, const R* spt, R M, R a,
                                       int part, int nparts) {
+    using R2 = typename std::conditional<sizeof(R) == 8, double2, float2>::type;
+    const R2* pt = (const R2*)spt;
     const PD_AS1 uint32_t* iw = (const PD_AS1 uint32_t*)(pay + kPayIdx);
     R s0 = R(0), s1 = R(0);
     // one term: c_j d2 log(d2) accumulated (the 1/2 of phi is applied once at the end); d2 = 0
@@ -105,32 +124,37 @@ __device__ __forceinline__ R rbf_eval(const PD_AS1 R* __restrict__ pay, const R*
         // (idx_pos): words 0..9, loaded once, hold chunk c's ten indices in byte c, so a chunk's
         // table points come from LDS without waiting on a global load; its ten coefficients are
         // one contiguous 80-byte load.  Terms 40..49 (words 10..12, in order) end the sum.
-        uint32_t wd[10];
-#pragma unroll
-        for (int u = 0; u < 10; ++u) wd[u] = iw[u];
+        PayPre<R> q;
+        pay_prefetch<R>(pay, q);
+        const uint32_t* wd = q.wd;
+        const uint32_t x0 = q.x0, x1 = q.x1, x2 = q.x2;
+        R* pn = q.pn;
+        constexpr bool kPf = true;   // chunk c + 1's coefficients requested before chunk c computes
 #pragma unroll 1
         for (int c = 0; c < 4; ++c) {
             R mm[10], aa[10], pp[10];
 #pragma unroll
             for (int u = 0; u < 10; ++u) {
                 const int ix = (int)((wd[u] >> (8 * c)) & 0xffu);
-                mm[u] = smach[ix];
-                aa[u] = saoa[ix];
-                pp[u] = pay[10 * c + u];
+                const R2 v = pt[ix];
+                mm[u] = v.x;
+                aa[u] = v.y;
+                if constexpr (kPf) { pp[u] = pn[u]; pn[u] = pay[10 * c + 10 + u]; }
+                else pp[u] = pay[10 * c + u];
             }
 #pragma unroll
             for (int u = 0; u < 10; ++u) term(mm[u], aa[u], pp[u], u & 1);
         }
         {
-            const uint32_t x0 = iw[10], x1 = iw[11], x2 = iw[12];
             R mm[10], aa[10], pp[10];
 #pragma unroll
             for (int u = 0; u < 10; ++u) {
                 const uint32_t wv = u < 4 ? x0 : (u < 8 ? x1 : x2);
                 const int ix = (int)((wv >> (8 * (u & 3))) & 0xffu);
-                mm[u] = smach[ix];
-                aa[u] = saoa[ix];
-                pp[u] = pay[40 + u];
+                const R2 v = pt[ix];
+                mm[u] = v.x;
+                aa[u] = v.y;
+                pp[u] = kPf ? pn[u] : pay[40 + u];
             }
 #pragma unroll
             for (int u = 0; u < 10; ++u) term(mm[u], aa[u], pp[u], u & 1);
@@ -166,8 +190,9 @@ __device__ __forceinline__ R rbf_eval(const PD_AS1 R* __restrict__ pay, const R*
             int jj = ok ? j : 0;
             const int bp = idx_pos(jj);
             const int ix = (int)((iw[bp >> 2] >> ((bp & 3) * 8)) & 0xffu);
-            mm[u] = smach[ix];
-            aa[u] = saoa[ix];
+            const R2 v = pt[ix];
+            mm[u] = v.x;
+            aa[u] = v.y;
             pp[u] = ok ? pay[jj] : R(0);
         }
 #pragma unroll
@@ -302,8 +327,8 @@ __device__ __forceinline__ void solve_wave(DP<R>& P, int table, unsigned long lo
 // global scratch slot (under the slot's lock), evaluated by the lanes that need it, and queued
 // for insertion into the device table (pd_flush_misses).  Called by the converged wave.
 template <typename R>
-__device__ __forceinline__ R rbf_miss_wave(const StepArgs<R>& a, DP<R>& P, int table, const R* smach,
-                                           const R* saoa, unsigned long long key, R M, R aq,
+__device__ __forceinline__ R rbf_miss_wave(const StepArgs<R>& a, DP<R>& P, int table, const R* spt,
+                                           unsigned long long key, R M, R aq,
                                            int part, int nparts, bool need) {
     R val = R(0);
     unsigned long long mm = __ballot(need);
@@ -320,7 +345,7 @@ __device__ __forceinline__ R rbf_miss_wave(const StepArgs<R>& a, DP<R>& P, int t
         wave_mem_sync();
         solve_wave<R>(P, lt, lk, work);
         if (need && key == lk && table == lt) {
-            val = rbf_eval<R>((const PD_AS1 R*)work, smach, saoa, M, aq, part, nparts);
+            val = rbf_eval<R>((const PD_AS1 R*)work, spt, M, aq, part, nparts);
             need = false;
         }
         if ((int)__lane_id() == leader) {
@@ -422,11 +447,11 @@ __device__ __forceinline__ R rbf(const StepArgs<R>& a, DP<R>& P, int table, cons
     cache.key = key;
     cache.slot = slot;
     R val = R(0);
-    if (slot >= 0) val = rbf_eval<R>(t.pay + (int64_t)slot * pay_stride<R>(), t.smach, t.saoa, M, aq, part, nparts);
+    if (slot >= 0) val = rbf_eval<R>(t.pay + (int64_t)slot * pay_stride<R>(), t.smach, M, aq, part, nparts);
     // Misses (a neighbourhood outside the pre-enumerated tables) take the wave-cooperative
     // exact solve; the loop in rbf_miss_wave runs only when some lane of the wave missed
     if (__ballot(slot < 0)) {
-        R mv = rbf_miss_wave<R>(a, P, table, t.smach, t.saoa, key, M, aq, part, nparts, slot < 0);
+        R mv = rbf_miss_wave<R>(a, P, table, t.smach, key, M, aq, part, nparts, slot < 0);
         if (slot < 0) val = mv;
     }
     return val;
@@ -512,8 +537,8 @@ __device__ __forceinline__ void actor_forward(const float* __restrict__ W, int64
 
 // ---------------------------------------------------------------- LDS of one step workgroup
 template <typename R, bool WIND, int EPB> struct StepLds {
-    // table Mach values [0, 512) (C_D, C_L), each point's AoA 512 further on (tab_view relies on it)
-    R tab[1024];
+    // table points as (Mach, AoA) pairs, C_D's 256 then C_L's: one 16-byte LDS read per point
+    alignas(16) R tab[1024];
     R gf[256];                    // grid fins: ca_x, ca_y, cn_x, cn_y (64 each)
     R isa[9 * kIsaCols];          // ISA layers
     R walt[WIND ? 800 : 1];       // wind profiles [50][16]: altitude km, speed
@@ -525,8 +550,7 @@ template <typename R, bool WIND, int EPB> struct StepLds {
 template <typename R>
 __device__ __forceinline__ TabView<R> tab_view(DP<R>& P, const R* tab, int table) {
     TabView<R> t;
-    t.smach = tab + (table ? 256 : 0);
-    t.saoa = t.smach + 512;
+    t.smach = tab + (table ? 512 : 0);
     t.start = table ? &P.cl_start[0] : &P.cd_start[0];
     t.n = table ? &P.cl_len[0] : &P.cd_len[0];
     t.aoa = table ? &P.cl_aoa[0] : &P.cd_aoa[0];
@@ -574,8 +598,8 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
     {
         DP<R>& P = *params<R>(a.P);
         for (int t = threadIdx.x; t < 256; t += kStepBlock) {
-            L.tab[t] = P.cd_mach[t]; L.tab[256 + t] = P.cl_mach[t];
-            L.tab[512 + t] = P.cd_pt_aoa[t]; L.tab[768 + t] = P.cl_pt_aoa[t];
+            L.tab[2 * t] = P.cd_mach[t]; L.tab[2 * t + 1] = P.cd_pt_aoa[t];
+            L.tab[512 + 2 * t] = P.cl_mach[t]; L.tab[513 + 2 * t] = P.cl_pt_aoa[t];
         }
         if (threadIdx.x < 64) {
             L.gf[threadIdx.x] = P.ca_x[threadIdx.x]; L.gf[64 + threadIdx.x] = P.ca_y[threadIdx.x];
@@ -600,7 +624,7 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
         }
         if (threadIdx.x < 4) { L.lines.a[threadIdx.x] = P.line_a[threadIdx.x]; L.lines.nbp[threadIdx.x] = P.line_nbp[threadIdx.x]; }
         for (int t = threadIdx.x; t < kLogCells; t += kStepBlock) {
-            s_logtab[t] = P.logtab.invc[t]; s_logtab[kLogCells + t] = P.logtab.logc[t];
+            s_logtab[2 * t] = P.logtab.invc[t]; s_logtab[2 * t + 1] = P.logtab.logc[t];
         }
     }
     __syncthreads();
@@ -737,57 +761,10 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
         R speed = sqrt(vx * vx + vy * vy);
         R mach = R(0);
         if (asnd != R(0)) { R mr = speed / asnd; mach = (R(10) < mr) ? R(10) : mr; }
-        R q = R(0.5) * rho * (speed * speed);
-        R fpc = (P.m_prop0 - mp) / P.m_prop0;
-        if (fpc == R(0)) fpc = R(1e-6);
-        R x_cog, I;
-        // subrocket_0 (full rocket) closures for the ascent, subrocket_2 after (:748-750, :772-774)
-        if (ascent) inertia_full<R>(P, R(1) - fpc, x_cog, I);
-        else inertia<R>(P, R(1) - fpc, x_cog, I);
-        R d_thrust = x_cog + P.engine_height;
+        // alpha_effective (rockets_physics.py:498-501) and Mach feed the aero tables; what the
+        // tables do not need is computed after them (fewer values live across the RBF)
         R ae = (vy < R(0)) ? ga - th - Cst<R>::pi : al;
-        R d_cp_cg = x_cog - (ascent ? P.cop_ascent : P.cop);
-        R ug = R(0), vg = R(0);
-        if constexpr (WIND) {
-            // WindModel.__call__ (full_wind_model.py:35-43)
-            const R* walt = L.walt + e.prof * 16;
-            const R* wsp = L.wsp + e.prof * 16;
-            R km = y / R(1000);
-            int wn = P.wind_n[e.prof];
-            ug = np_interp<R>(walt, wsp, wn, km);
-            if (y < P.vk_y_threshold && a.stochastic) {
-                double w0, w1;
-                if (a.noise) { w0 = ev(a.noise + 2 * sub, ui * 8); w1 = ev(a.noise + 2 * sub + 1, ui * 8); }
-                else {
-                    // vonkarman.py:34: one np.random.randn() per filter step, u then v (gauss_pair:
-                    // Philox counter (env, episode, step, sub-step), reproducible by the oracle)
-                    u32x4 r = philox({(uint32_t)g, (uint32_t)(g >> 32) ^ e.ep, e.ts, kTagWindSub + (uint32_t)sub},
-                                     a.seed_lo, a.seed_hi);
-                    gauss_pair(r, s_logtab, s_logtab + kLogCells, w0, w1);
-                }
-                // vonkarman.py:33-36: state = Ad @ state + Bd * w  (Bd = sigma * Bd(sigma=1))
-                R n0 = (P.vk_Ad_u[0] * e.fu0 + P.vk_Ad_u[1] * e.fu1) + (e.sgu * P.vk_Bd_u[0]) * (R)w0;
-                R n1 = (P.vk_Ad_u[2] * e.fu0 + P.vk_Ad_u[3] * e.fu1) + (e.sgu * P.vk_Bd_u[1]) * (R)w0;
-                e.fu0 = n0; e.fu1 = n1;
-                n0 = (P.vk_Ad_v[0] * e.fv0 + P.vk_Ad_v[1] * e.fv1) + (e.sgv * P.vk_Bd_v[0]) * (R)w1;
-                n1 = (P.vk_Ad_v[2] * e.fv0 + P.vk_Ad_v[3] * e.fv1) + (e.sgv * P.vk_Bd_v[1]) * (R)w1;
-                e.fv0 = n0; e.fv1 = n1;
-                ug = ug + e.fu1;
-                vg = e.fv1;
-            }
-        }
-        R Fwx = R(0.5) * rho * (ug * ug) * P.A_front * P.C_gust_x;
-        R Fwy = R(0.5) * rho * (vg * vg) * P.A_front * P.C_gust_y;
-        R Mw = -d_cp_cg * Fwy;
         R CL = R(0), CD = R(0);
-        if (tap_sub) {   // info of the last sub-step (rockets_physics.py:649-702), stored where computed
-            const R mmax = asnd != R(0) ? sqrt(R(2) * R(30000) / rho) * R(1) / asnd : R(200);
-            info(PD_INFO_AIR_DENSITY, rho); info(PD_INFO_PRESSURE, patm); info(PD_INFO_SPEED_OF_SOUND, asnd);
-            info(PD_INFO_MACH, mach); info(PD_INFO_Q, q); info(PD_INFO_X_COG, x_cog); info(PD_INFO_INERTIA, I);
-            info(PD_INFO_ALPHA_EFF, ae); info(PD_INFO_UG, ug); info(PD_INFO_VG, vg); info(PD_INFO_MACH_MAX, mmax);
-            info(PD_INFO_D_CP_CG, d_cp_cg); info(PD_INFO_D_THRUST_CG, d_thrust); info(PD_INFO_FUEL_CONSUMED, fpc);
-            info(PD_INFO_F_WIND_X, Fwx); info(PD_INFO_F_WIND_Y, Fwy); info(PD_INFO_M_WIND, Mw); info(PD_INFO_THETA_IN, th);
-        }
         PD_T(t_aero0);
         PD_ACC(2, t_aero0 - t_sub);
 #ifndef PD_EXP_NORBF
@@ -824,6 +801,55 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
 #endif
         PD_T(t_aero1);
         PD_ACC(3, t_aero1 - t_aero0);
+        R q = R(0.5) * rho * (speed * speed);
+        R fpc = (P.m_prop0 - mp) / P.m_prop0;
+        if (fpc == R(0)) fpc = R(1e-6);
+        R x_cog, I;
+        // subrocket_0 (full rocket) closures for the ascent, subrocket_2 after (:748-750, :772-774)
+        if (ascent) inertia_full<R>(P, R(1) - fpc, x_cog, I);
+        else inertia<R>(P, R(1) - fpc, x_cog, I);
+        R d_thrust = x_cog + P.engine_height;
+        R d_cp_cg = x_cog - (ascent ? P.cop_ascent : P.cop);
+        R ug = R(0), vg = R(0);
+        if constexpr (WIND) {
+            // WindModel.__call__ (full_wind_model.py:35-43)
+            const R* walt = L.walt + e.prof * 16;
+            const R* wsp = L.wsp + e.prof * 16;
+            R km = y / R(1000);
+            int wn = P.wind_n[e.prof];
+            ug = np_interp<R>(walt, wsp, wn, km);
+            if (y < P.vk_y_threshold && a.stochastic) {
+                double w0, w1;
+                if (a.noise) { w0 = ev(a.noise + 2 * sub, ui * 8); w1 = ev(a.noise + 2 * sub + 1, ui * 8); }
+                else {
+                    // vonkarman.py:34: one np.random.randn() per filter step, u then v (gauss_pair:
+                    // Philox counter (env, episode, step, sub-step), reproducible by the oracle)
+                    u32x4 r = philox({(uint32_t)g, (uint32_t)(g >> 32) ^ e.ep, e.ts, kTagWindSub + (uint32_t)sub},
+                                     a.seed_lo, a.seed_hi);
+                    gauss_pair<2>(r, s_logtab, s_logtab + 1, w0, w1);
+                }
+                // vonkarman.py:33-36: state = Ad @ state + Bd * w  (Bd = sigma * Bd(sigma=1))
+                R n0 = (P.vk_Ad_u[0] * e.fu0 + P.vk_Ad_u[1] * e.fu1) + (e.sgu * P.vk_Bd_u[0]) * (R)w0;
+                R n1 = (P.vk_Ad_u[2] * e.fu0 + P.vk_Ad_u[3] * e.fu1) + (e.sgu * P.vk_Bd_u[1]) * (R)w0;
+                e.fu0 = n0; e.fu1 = n1;
+                n0 = (P.vk_Ad_v[0] * e.fv0 + P.vk_Ad_v[1] * e.fv1) + (e.sgv * P.vk_Bd_v[0]) * (R)w1;
+                n1 = (P.vk_Ad_v[2] * e.fv0 + P.vk_Ad_v[3] * e.fv1) + (e.sgv * P.vk_Bd_v[1]) * (R)w1;
+                e.fv0 = n0; e.fv1 = n1;
+                ug = ug + e.fu1;
+                vg = e.fv1;
+            }
+        }
+        R Fwx = R(0.5) * rho * (ug * ug) * P.A_front * P.C_gust_x;
+        R Fwy = R(0.5) * rho * (vg * vg) * P.A_front * P.C_gust_y;
+        R Mw = -d_cp_cg * Fwy;
+        if (tap_sub) {   // info of the last sub-step (rockets_physics.py:649-702), stored where computed
+            const R mmax = asnd != R(0) ? sqrt(R(2) * R(30000) / rho) * R(1) / asnd : R(200);
+            info(PD_INFO_AIR_DENSITY, rho); info(PD_INFO_PRESSURE, patm); info(PD_INFO_SPEED_OF_SOUND, asnd);
+            info(PD_INFO_MACH, mach); info(PD_INFO_Q, q); info(PD_INFO_X_COG, x_cog); info(PD_INFO_INERTIA, I);
+            info(PD_INFO_ALPHA_EFF, ae); info(PD_INFO_UG, ug); info(PD_INFO_VG, vg); info(PD_INFO_MACH_MAX, mmax);
+            info(PD_INFO_D_CP_CG, d_cp_cg); info(PD_INFO_D_THRUST_CG, d_thrust); info(PD_INFO_FUEL_CONSUMED, fpc);
+            info(PD_INFO_F_WIND_X, Fwx); info(PD_INFO_F_WIND_Y, Fwy); info(PD_INFO_M_WIND, Mw); info(PD_INFO_THETA_IN, th);
+        }
         R drag = R(0.5) * rho * (speed * speed) * CD * P.A_front;
         R lift = R(0.5) * rho * (speed * speed) * CL * P.A_front;
         R sae, cae, sth, cth;
@@ -1275,7 +1301,7 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
     }
     // ---- the env's bookkeeping for the next step: auto-reset in registers, or carry on
     if (ended) {
-        reset_values<R>(P2, a, g, e.ep + 1, s_logtab, s_logtab + kLogCells, e);   // keeps the aero caches
+        reset_values<R, 2>(P2, a, g, e.ep + 1, s_logtab, s_logtab + 1, e);   // keeps the aero caches
     } else {
         e.vprev = v;
         e.glen = glen; e.ghead = ghead;

@@ -138,7 +138,7 @@ __global__ __launch_bounds__(kBlock) void k_atmosphere(StepArgs<R> a, const R* a
         r[4] = P.isa_bt[k]; r[5] = P.isa_ex[k]; r[6] = P.isa_iso[k]; r[7] = R(0);
     }
     for (int t = threadIdx.x; t < kLogCells; t += kBlock) {
-        s_logtab[t] = P.logtab.invc[t]; s_logtab[kLogCells + t] = P.logtab.logc[t];
+        s_logtab[2 * t] = P.logtab.invc[t]; s_logtab[2 * t + 1] = P.logtab.logc[t];
     }
     __syncthreads();
     int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
