@@ -24,16 +24,32 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "psso-sac-for-powered-descent_amd"))
 
 
-def algorithmic_bytes(precision, phase, wind, obs_dim, act_dim):
-    """HBM bytes one env-step must move (SoA state in/out + caches + I/O), DESIGN.md s3."""
-    r = 8 if precision == "f64" else 4
-    rd = 11 * r + r + 10 * r + 2 + 16 + 8 + 4 + 4 + 4 * act_dim
-    wr = 11 * r + r + r + 2 + 1 + 4 + 16 + 8 + obs_dim * r + r + 3
-    if phase == "landing_burn":
-        rd += 3 * r; wr += 3 * r
+def algorithmic_bytes(precision, phase, wind):
+    """SURVEY.md 8(d) ALGORITHMIC bytes per env-step (the roofline's per-unit figure): step-mode
+    SoA, binary32 base 163 B (reads: 11 state + prev speed + 10 g-window + 1 action = 92 B;
+    writes: 11 state + prev speed + window slot + head + 2 obs + reward = 68 B, + done, trunc,
+    trunc_id 3 B); binary64 state +88 B; wind +56 B (4 filter values r/w, 2 sigmas, RNG counter);
+    landing_burn +48 B.  c3 (f64, wind, pure throttle) = 307 B."""
+    b = 163 + (88 if precision == "f64" else 0)
     if wind:
-        rd += 6 * r + 1; wr += 4 * r
-    return rd + wr
+        b += 56
+    if phase == "landing_burn":
+        b += 48
+    return b
+
+
+def implementation_bytes(precision, phase, wind, obs_dim, act_dim, fuse):
+    """Bytes k_step actually moves per env-step in a launch of `fuse` fused steps: the per-env
+    state is read and written once per launch (registers in between), the per-step I/O every
+    step (action in; obs, reward, done/trunc/trunc_id out)."""
+    r = 8 if precision == "f64" else 4
+    state = 11 * r + r + 10 * r + 2 + 16 + 8 + 8 + 1          # state, |v_prev|, g-window, head/len, keys, slots, counters, tid
+    if phase == "landing_burn":
+        state += 3 * r
+    if wind:
+        state += 6 * r + 1                                      # filters, sigmas, percentile
+    per_step = 4 * act_dim + obs_dim * r + r + 3
+    return 2 * state / fuse + per_step
 
 
 def valu_roofline(mix, kern_avg_ms, simds=1024, clock_hz=2.4e9, fp64_peak_tflops=78.6):
@@ -240,9 +256,10 @@ def main():
             auto_reset=True, tilt_sigma_rad=math.radians(1.0), seed=1234, env_offset=shard_offset(rank, n))
         env.flush_every = 16
         T = args.warmup + args.steps
-        g = torch.Generator(device=env.device).manual_seed(42 + rank)
-        acts = (torch.rand(T, n, env.action_dim, generator=g, device=env.device) * 2 - 1).contiguous()
         F = max(1, args.fuse)
+        KT = 8                  # full launches of the separate kernel-duration pass
+        g = torch.Generator(device=env.device).manual_seed(42 + rank)
+        acts = (torch.rand(max(T, args.warmup + KT * F), n, env.action_dim, generator=g, device=env.device) * 2 - 1).contiguous()
         if F > 1:
             # pd_step_n: F env-steps per launch, every step's outputs written (rows of [F, N, ...]
             # buffers reused chunk to chunk, as the per-step loop reuses one [N, ...] buffer)
@@ -265,10 +282,14 @@ def main():
         # timed region: exactly K env-steps (ceil(K / F) launches), nothing else on the stream (a
         # per-launch event pair costs ~10 us of GPU time, so the kernel-duration pass is separate)
         tb = bounds(args.warmup, T)
+        blob = env.checkpoint()          # every per-env buffer at the start of the timed region
         wall = timed_region(lambda k: chunk(*tb[k]), len(tb), torch.cuda.synchronize, dist, env.device)
-        # kernel duration: HIP events around every launch (with F > 1 the launch and its miss
-        # flush), on the stream the kernel runs on; full F-step launches only
-        full = [b for b in tb if b[1] - b[0] == F][:100]
+        # kernel duration: the timed region's launches replayed from the checkpoint (the same
+        # work, bit for bit), extended by the following actions to at least KT full launches,
+        # with HIP events around each launch (and its miss flush) on the stream the kernel runs on
+        env.restore(blob)
+        nfull = max(KT, args.steps // F)
+        full = [(args.warmup + k * F, args.warmup + (k + 1) * F) for k in range(nfull)]
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in full]
         for k, b in enumerate(full):
             ev[k][0].record()
@@ -278,6 +299,7 @@ def main():
         kern_ms = sorted(a.elapsed_time(b) for a, b in ev)
         c = env.counters()
         res = dict(wall=wall, kern_avg_ms=sum(kern_ms) / len(kern_ms), kern_med_ms=kern_ms[len(kern_ms) // 2], fuse=F,
+                   kern_launches=len(kern_ms),
                    n=n, obs_dim=env.obs_dim, act_dim=env.action_dim, counters=c)
         env.close()
         return res
@@ -293,8 +315,9 @@ def main():
     n_total = main_res["n"] * world
     value = whole_job_rate(main_res["n"], world, args.steps, main_res["wall"])
     wind = not args.no_wind
-    bpe = algorithmic_bytes(args.precision, args.phase, wind, main_res["obs_dim"], main_res["act_dim"])
+    bpe = algorithmic_bytes(args.precision, args.phase, wind)
     F = main_res["fuse"]
+    ibpe = implementation_bytes(args.precision, args.phase, wind, main_res["obs_dim"], main_res["act_dim"], F)
     achieved = bpe * main_res["n"] * F / (main_res["kern_avg_ms"] * 1e-3) / 1e9
     traffic = None
     mix = None
@@ -329,7 +352,10 @@ def main():
                    "envs_per_gpu": main_res["n"], "global_envs": n_total, "parallelism": f"env-shard x{world}"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": 8000.0, "unit": "GB/s",
                      "frac": achieved / 8000.0, "traffic": traffic,
-                     "bytes_per_env_step": bpe, "kernel": "k_step", "kernel_avg_ms": main_res["kern_avg_ms"],
+                     "bytes_per_env_step": bpe, "bytes_source": "SURVEY.md 8(d) algorithmic count",
+                     "implementation_bytes_per_env_step": round(ibpe, 1),
+                     "kernel": "k_step", "kernel_avg_ms": main_res["kern_avg_ms"],
+                     "kernel_launches_timed": main_res["kern_launches"],
                      "env_steps_per_launch": F, "envs_per_launch": main_res["n"],
                      "note": "VALU/transcendental-bound elementwise ODE (no MFMA); see DESIGN.md"},
         "rbf_table_misses": main_res["counters"]["rbf_misses"],

@@ -10,12 +10,27 @@ namespace pd {
 constexpr int kNbr = 50;            // RBFInterpolator(neighbors=50), aerodynamic_coefficients.py:59
 constexpr int kSys = kNbr + 3;      // + degree-1 polynomial tail (TPS default degree)
 constexpr int kCols = 5;            // AoA columns of each V2 table
-constexpr int kPay = 64;            // payload (binary64): 50 kernel coefs, 3 poly, shift0/1, scale0/1,
-constexpr int kPayIdx = kNbr + 3 + 4;   // then from slot 57 the 50 points' table indices as bytes
-// Byte position of term j's point index in the index area.  Terms 0..39 are chunk-interleaved:
-// term 10c + u (c < 4) is byte c of word u, so one load of words 0..9 serves the step kernel's
-// four 10-term chunks (byte c extracted by a shift); terms 40..49 follow at bytes 40..49.
-PD_HD constexpr int idx_pos(int j) { return j < 40 ? 4 * (j % 10) + j / 10 : j; }
+// Payload of one neighbourhood (binary64 words).  The 50 terms are stored as pair slots: a
+// window of consecutive table points (one column's Mach run) is cut into pairs (p, p + 1), an
+// odd window's last point padded with a zero-coefficient partner, so that one 16-byte LDS read
+// (the point table holds (Mach_p, Mach_p+1) per entry) serves two terms that share the
+// column's AoA.  50 points in <= 5 windows (an even number of them odd) fill <= 27 slots.
+//   [0, 54)   coefficients, slot k at 2k, 2k + 1 (zero for padding)
+//   [54, 57)  degree-1 polynomial coefficients
+//   [57, 61)  shift0, shift1, scale0, scale1
+//   [61, 70)  72 index bytes: per slot its entry (first point) and the column's integer AoA,
+//             see pair_entry_pos / pair_aoa_pos
+constexpr int kPairs = 27;
+constexpr int kPayPoly = 2 * kPairs;
+constexpr int kPaySS = kPayPoly + 3;
+constexpr int kPayIdx = kPaySS + 4;
+constexpr int kPayIdxBytes = 72;
+constexpr int kPay = kPayIdx + kPayIdxBytes / 8;
+// Byte positions in the index area: slot 5c + u (chunk c of five) at 12c + 2u (entry) and
+// 12c + 2u + 1 (AoA), so that a chunk's ten bytes are one 12-byte (3-dword) load issued with its
+// ten coefficients; the last chunk (slots 25, 26) is padded to 12 bytes.
+PD_HD constexpr int pair_entry_pos(int k) { return 12 * (k / 5) + 2 * (k % 5); }
+PD_HD constexpr int pair_aoa_pos(int k) { return pair_entry_pos(k) + 1; }
 constexpr int kKeyLoBits = 6, kKeyLenBits = 6, kKeyField = kKeyLoBits + kKeyLenBits;
 constexpr uint64_t kEmptyKey = ~0ull;
 
@@ -98,6 +113,20 @@ PD_HD double tps(double r) { return r == 0.0 ? 0.0 : r * r * pd_log(r); }
 // the device library's double log.  Positive normal finite x; x = 0 gives a finite value.
 constexpr int kLogBits = 9, kLogCells = 1 << kLogBits;
 struct LogTable { double invc[kLogCells], logc[kLogCells]; };
+// The step kernel's hot-path log (eval_log, pd_physics.h): 1024 cells of (2 invc, -log(invc) -
+// ln 2), interleaved for one 16-byte LDS read, used with frexp's mantissa in [0.5, 1) and a
+// degree-4 log1p (|r| < 2^-11, truncation < 6e-18); same accuracy as log_tab (max 1.4e-15
+// absolute over [1e-6, 300] against long double, 2e7 arguments), fewer instructions.
+constexpr int kLogBitsD = 10, kLogCellsD = 1 << kLogBitsD;
+struct LogTableD { double cell[2 * kLogCellsD]; };
+inline void log_table_fill(LogTableD& t) {
+    for (int i = 0; i < kLogCellsD; ++i) {
+        long double c = 1.0L + (i + 0.5L) / kLogCellsD;
+        double invc = (double)(1.0L / c);
+        t.cell[2 * i] = 2.0 * invc;
+        t.cell[2 * i + 1] = (double)(-logl((long double)invc) - logl(2.0L));
+    }
+}
 inline void log_table_fill(LogTable& t) {
     for (int i = 0; i < kLogCells; ++i) {
         long double c = 1.0L + (i + 0.5L) / kLogCells;
@@ -136,8 +165,8 @@ PD_HD double log_tab(double x, const double* invc, const double* logc) {
 // [[K, P], [P^T, 0]] c = [d, 0]) and solve it by LU with partial pivoting (LAPACK dgesv's
 // algorithm).  Points are taken in window order (column by column, Mach-ascending).
 //   mach/coef: table arrays (column-grouped); col_start/col_aoa: column geometry
-//   work: >= kSys*kSys + kSys + 3*kNbr doubles of scratch;  payload: kPay doubles out (the
-//   last 7 hold the points' table indices as bytes, see pay_store).
+//   work: >= kSys*kSys + kSys + 3*kNbr doubles of scratch;  payload: kPay doubles out in the
+//   pair-slot layout above (column AoAs must be integers in [0, 255], checked by pd_create).
 // Returns 0 on success, -1 on a singular system.
 PD_HD int solve_neighbourhood(const double* mach, const double* coef, const int* col_start,
                               const double* col_aoa, uint64_t key, double* work, double* payload) {
@@ -209,21 +238,31 @@ PD_HD int solve_neighbourhood(const double* mach, const double* coef, const int*
         b[i] = xi;
         for (int r = 0; r < i; ++r) b[r] -= A[r * kSys + i] * xi;
     }
-    for (int j = 0; j < kSys; ++j) payload[j] = b[j];
-    payload[kSys + 0] = sh0; payload[kSys + 1] = sh1;
-    payload[kSys + 2] = sc0; payload[kSys + 3] = sc1;
-    for (int j = kSys + 4; j < kPay; ++j) payload[j] = 0.0;
-    for (int j = 0; j < kNbr; ++j) ((uint8_t*)(payload + kPayIdx))[idx_pos(j)] = idx[j];
+    for (int j = 0; j < kPay; ++j) payload[j] = 0.0;
+    uint8_t* ib = (uint8_t*)(payload + kPayIdx);
+    int t = 0, slot0 = 0;
+    for (int c = 0; c < kCols; ++c) {
+        for (int i = 0; i < len[c]; ++i, ++t) {
+            const int k = slot0 + i / 2;
+            payload[2 * k + (i & 1)] = b[t];
+            if ((i & 1) == 0) { ib[pair_entry_pos(k)] = idx[t]; ib[pair_aoa_pos(k)] = (uint8_t)col_aoa[c]; }
+        }
+        slot0 += (len[c] + 1) / 2;
+    }
+    if (slot0 > kPairs) return -1;
+    for (int j = 0; j < 3; ++j) payload[kPayPoly + j] = b[kNbr + j];
+    payload[kPaySS + 0] = sh0; payload[kPaySS + 1] = sh1;
+    payload[kPaySS + 2] = sc0; payload[kPaySS + 3] = sc1;
     return 0;
 }
 
 // Payload in a handle's precision: coefficients converted, index bytes copied.  Stride in R
-// units: 64 (binary64) or 72 (binary32: 57 coefficients + 50 bytes = 13 floats + padding).
-template <typename R> constexpr int pay_stride() { return sizeof(R) == 8 ? kPay : 72; }
+// units: kPay = 70 (binary64) or 80 (binary32: 61 values + 72 bytes = 18 floats + padding).
+template <typename R> constexpr int pay_stride() { return sizeof(R) == 8 ? kPay : 80; }
 template <typename R> PD_HD void pay_store(const double* src, R* dst) {
     for (int j = 0; j < kPayIdx; ++j) dst[j] = (R)src[j];
     for (int j = kPayIdx; j < pay_stride<R>(); ++j) dst[j] = R(0);
-    __builtin_memcpy((uint8_t*)(dst + kPayIdx), (const uint8_t*)(src + kPayIdx), kNbr);
+    __builtin_memcpy((uint8_t*)(dst + kPayIdx), (const uint8_t*)(src + kPayIdx), kPayIdxBytes);
 }
 
 // ---------------------------------------------------------------- Philox4x32-10

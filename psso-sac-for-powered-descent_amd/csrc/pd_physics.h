@@ -64,7 +64,8 @@ template <typename R> struct DevParams {
     R state0[11];
     double state0_d[11];
     R norm_y, norm_vy, norm_x, norm_vx, k_theta_pso;
-    LogTable logtab;   // log_tab cells (pd_common.h), staged into LDS by the step kernel
+    LogTable logtab;   // log_tab cells (pd_common.h): the Box-Muller draws (oracle-restated)
+    LogTableD logtab_d;   // eval_log cells, staged into LDS by the step kernel
     R y0_rl, m0_rl;
     // neighbourhood hash tables
     const unsigned long long* keys_cd;
@@ -112,20 +113,34 @@ constexpr int kIsaCols = 8;
 // ---------------------------------------------------------------- logarithms
 // Hot-path log(): binary64 through the LDS-staged cell table (log_tab, pd_common.h; the step
 // kernel stages it before its barrier), binary32 through the hardware log2.
-// (invc, logc) of cell i at [2i], [2i + 1]: one 16-byte ds_read_b128 per log
-__shared__ __attribute__((aligned(16))) double s_logtab[2 * kLogCells];
+// eval_log's cells (LogTableD): (2 invc, logc - ln 2) of cell i at [2i], [2i + 1], one 16-byte
+// ds_read_b128 per log
+__shared__ __attribute__((aligned(16))) double s_logtab[2 * kLogCellsD];
 template <typename R> __device__ __forceinline__ R eval_log(R x);
 template <> __device__ __forceinline__ double eval_log<double>(double x) {
-    uint64_t b;
-    __builtin_memcpy(&b, &x, 8);
+    // x = 2^e1 m1, m1 in [0.5, 1) (v_frexp_*); cell from the top 10 mantissa bits;
+    // r = m1 (2 invc) - 1 = m invc - 1; log x = e1 ln2 + (logc - ln2) + log1p(r)
+#ifndef PD_LOG_BITS   // (bit-operation extraction: measured 2.6 % slower)
+    const int e1 = __builtin_amdgcn_frexp_exp(x);
+    const double m1 = __builtin_amdgcn_frexp_mant(x);
+    const uint32_t hi = (uint32_t)(__double_as_longlong(x) >> 32);
+#else
+    const uint64_t b = (uint64_t)__double_as_longlong(x);
     const uint32_t hi = (uint32_t)(b >> 32);
-    const double e = (double)((int)(hi >> 20) - 1023);
-    const uint32_t i = (hi >> (20 - kLogBits)) & (kLogCells - 1);
-    const uint64_t mb = (b & 0x000fffffffffffffull) | 0x3ff0000000000000ull;
-    double m;
-    __builtin_memcpy(&m, &mb, 8);
+    const int e1 = (int)(hi >> 20) - 1022;
+    const double m1 = __longlong_as_double((long long)((b & 0x000fffffffffffffull) | 0x3fe0000000000000ull));
+#endif
+    const uint32_t i = __builtin_amdgcn_ubfe(hi, 20 - kLogBitsD, kLogBitsD);
+#ifdef PD_EXP_LOGCELL0   // experiment: every lane reads cell 0 (no bank conflicts; wrong values)
+    const double2 c = ((const double2*)s_logtab)[i & 0u];
+#else
     const double2 c = ((const double2*)s_logtab)[i];
-    return log_tab_finish(m, e, c.x, c.y);
+#endif
+    const double r = fma(m1, c.x, -1.0);
+    double t = fma(r, -0.25, 1.0 / 3.0);
+    t = fma(r, t, -0.5);
+    const double p = fma(r * r, t, r);
+    return fma((double)e1, 6.93147180559945286227e-01, c.y + p);
 }
 template <> __device__ __forceinline__ float eval_log<float>(float x) {
     return __builtin_amdgcn_logf(x) * 0.693147180559945309f;

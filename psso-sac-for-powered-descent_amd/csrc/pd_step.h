@@ -26,7 +26,8 @@ constexpr int kStats = 32;            // pend.stats words (see Stat)
 enum Stat {
     kStMisses = 0, kStNan = 1, kStInsCd = 2, kStInsCl = 3,       // 4..7 PD_EXP_* counters
     kStStamp = 8,                                                 // 8..15 PD_STAMP sections
-    kStDropped = 16, kStSolves = 17, kStSlotHits = 18
+    kStDropped = 16,
+    kStCount = 24   // 24..29 PD_EXP_COUNT: queries, interior, interior trusted, key changed, untrusted C_D / C_L
 };
 
 // ---------------------------------------------------------------- per-env device buffers

@@ -50,7 +50,7 @@ __device__ __forceinline__ void div_pair(R a0, R b0, R a1, R b1, int role, R& q0
 // LPE = 2 lane role 0 owns C_D and role 1 owns C_L; with LPE = 4/8/16 each table is owned by
 // LPE/2 lanes that split its 50-term thin-plate sum (terms k = part, part + nparts, ..).
 template <typename R> struct TabView {
-    const R* smach;            // LDS: the table's points as (Mach, AoA) pairs (smach[2i], smach[2i + 1])
+    const R* smach;            // LDS: entry p = (Mach_p, Mach_p+1); smach[2p] = point p's Mach
     const PD_AS4 int* start;   // column geometry (uniform: scalar loads)
     const PD_AS4 int* n;
     const PD_AS4 R* aoa;
@@ -75,27 +75,11 @@ template <typename R> struct LineLds {
 
 // This lane's share of sum_j c_j phi(|x - y_j|) + poly of one neighbourhood payload.
 // phi(r) = r^2 log r = d2 log(d2) / 2 with d2 = |x - y|^2 (thin_plate_spline, phi(0) = 0).
-// The payload names each term's table point by a byte index, whose (Mach, AoA) sit in LDS; the
-// terms are evaluated in chunks of 10 independent terms so that the loads of a chunk are in
-// flight together and the 10 log chains interleave.
-// The index words and the first coefficient chunk of one payload.  (Requesting them for the
-// env's cached neighbourhood at the start of each sub-step, to overlap the atmosphere and the
-// lookup, measured 17 % slower: the registers held across the sub-step spill.)
-template <typename R> struct PayPre {
-    uint32_t wd[10], x0, x1, x2;
-    R pn[10];
-    int slot;
-};
-template <typename R>
-__device__ __forceinline__ void pay_prefetch(const PD_AS1 R* __restrict__ pay, PayPre<R>& p) {
-    const PD_AS1 uint32_t* iw = (const PD_AS1 uint32_t*)(pay + kPayIdx);
-#pragma unroll
-    for (int u = 0; u < 10; ++u) p.wd[u] = iw[u];
-    p.x0 = iw[10]; p.x1 = iw[11]; p.x2 = iw[12];
-#pragma unroll
-    for (int u = 0; u < 10; ++u) p.pn[u] = pay[u];
-}
-
+// Terms come in pair slots (pd_common.h): one 16-byte LDS read gives the Mach values of a slot's
+// two consecutive table points, whose column AoA (an integer, in the slot's AoA byte) gives one
+// d_a^2 for both.  Slots are evaluated in chunks of five (ten terms) so that a chunk's LDS reads
+// are in flight together and its ten log chains interleave; the next chunk's coefficients and
+// index bytes are requested one chunk ahead.
 template <typename R>
 __device__ __forceinline__ R rbf_eval(const PD_AS1 R* __restrict__ pay, const R* spt, R M, R a,
                                       int part, int nparts) {
@@ -104,10 +88,10 @@ __device__ __forceinline__ R rbf_eval(const PD_AS1 R* __restrict__ pay, const R*
     const PD_AS1 uint32_t* iw = (const PD_AS1 uint32_t*)(pay + kPayIdx);
     R s0 = R(0), s1 = R(0);
     // one term: c_j d2 log(d2) accumulated (the 1/2 of phi is applied once at the end); d2 = 0
-    // (query on a table point) contributes c_j * 0 * finite = 0
-    auto term = [&](R mj, R aj, R cj, bool odd) {
-        R dm = M - mj, da = a - aj;
-        R d2 = dm * dm + da * da;
+    // (query on a table point) contributes c_j * 0 * finite = 0, as do padding terms (c_j = 0)
+    auto term = [&](R mj, R da2, R cj, bool second) {
+        R dm = M - mj;
+        R d2 = fma(dm, dm, da2);
         R w = d2 * cj;
 #ifdef PD_EXP_NOLOG
         R l = d2;
@@ -116,93 +100,75 @@ __device__ __forceinline__ R rbf_eval(const PD_AS1 R* __restrict__ pay, const R*
 #else
         R l = eval_log<R>(sizeof(R) == 8 ? d2 : (d2 > R(1e-30) ? d2 : R(1e-30)));
 #endif
-        if (odd) s1 = fma(w, l, s1); else s0 = fma(w, l, s0);
+        if (second) s1 = fma(w, l, s1); else s0 = fma(w, l, s0);
     };
-#ifndef PD_RBF_STRIDED
+    // one slot: entry byte e (its two Mach values), AoA byte ao, coefficients c0, c1
+    auto slot = [&](uint32_t e, uint32_t ao, R c0, R c1) {
+        const R2 v = pt[e];
+        const R da = a - (R)ao;
+        const R da2 = da * da;
+        term(v.x, da2, c0, false);
+        term(v.y, da2, c1, true);
+    };
     if (nparts == 1) {
-        // The lane owns all 50 terms.  The index bytes of terms 0..39 are chunk-interleaved
-        // (idx_pos): words 0..9, loaded once, hold chunk c's ten indices in byte c, so a chunk's
-        // table points come from LDS without waiting on a global load; its ten coefficients are
-        // one contiguous 80-byte load.  Terms 40..49 (words 10..12, in order) end the sum.
-        PayPre<R> q;
-        pay_prefetch<R>(pay, q);
-        const uint32_t* wd = q.wd;
-        const uint32_t x0 = q.x0, x1 = q.x1, x2 = q.x2;
-        R* pn = q.pn;
-        constexpr bool kPf = true;   // chunk c + 1's coefficients requested before chunk c computes
-#pragma unroll 1
-        for (int c = 0; c < 4; ++c) {
-            R mm[10], aa[10], pp[10];
+        // The lane owns all 27 slots: five rolled chunks of five slots, chunk c + 1's ten
+        // coefficients and 12 index bytes requested before chunk c computes; slots 25, 26 end it.
+        auto bytes = [&](int c, uint32_t w[3]) {
+            const PD_AS1 uint32_t* q = iw + 3 * c;
+            w[0] = q[0]; w[1] = q[1]; w[2] = q[2];
+        };
+        R pn[10];
+        uint32_t wn[3];
 #pragma unroll
-            for (int u = 0; u < 10; ++u) {
-                const int ix = (int)((wd[u] >> (8 * c)) & 0xffu);
-                const R2 v = pt[ix];
-                mm[u] = v.x;
-                aa[u] = v.y;
-                if constexpr (kPf) { pp[u] = pn[u]; pn[u] = pay[10 * c + 10 + u]; }
-                else pp[u] = pay[10 * c + u];
+        for (int u = 0; u < 10; ++u) pn[u] = pay[u];
+        bytes(0, wn);
+#ifndef PD_CHUNK_UNROLL
+#define PD_CHUNK_UNROLL 1
+#endif
+#pragma unroll PD_CHUNK_UNROLL
+        for (int c = 0; c < 5; ++c) {
+            R pp[10];
+            uint32_t w[3] = {wn[0], wn[1], wn[2]};
+#pragma unroll
+            for (int u = 0; u < 10; ++u) { pp[u] = pn[u]; pn[u] = pay[10 * c + 10 + u]; }
+            bytes(c + 1, wn);
+#pragma unroll
+            for (int u = 0; u < 5; ++u) {
+                const uint32_t h = w[u >> 1] >> (16 * (u & 1));
+                slot(h & 0xffu, (h >> 8) & 0xffu, pp[2 * u], pp[2 * u + 1]);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const uint32_t h = wn[0] >> (16 * u);
+            slot(h & 0xffu, (h >> 8) & 0xffu, pn[2 * u], pn[2 * u + 1]);
+        }
+    } else {
+        // LPE >= 4: the lane's slots are part, part + nparts, ...
+        const PD_AS1 uint8_t* ib = (const PD_AS1 uint8_t*)iw;
+#pragma unroll 1
+        for (int k0 = part; k0 < kPairs; k0 += 5 * nparts) {
+            uint32_t e[5], ao[5];
+            R c0[5], c1[5];
+#pragma unroll
+            for (int u = 0; u < 5; ++u) {
+                const int k = k0 + u * nparts;
+                const bool ok = k < kPairs;
+                const int kk = ok ? k : 0;
+                e[u] = ib[pair_entry_pos(kk)];
+                ao[u] = ib[pair_aoa_pos(kk)];
+                c0[u] = ok ? pay[2 * kk] : R(0);
+                c1[u] = ok ? pay[2 * kk + 1] : R(0);
             }
 #pragma unroll
-            for (int u = 0; u < 10; ++u) term(mm[u], aa[u], pp[u], u & 1);
+            for (int u = 0; u < 5; ++u) slot(e[u], ao[u], c0[u], c1[u]);
         }
-        {
-            R mm[10], aa[10], pp[10];
-#pragma unroll
-            for (int u = 0; u < 10; ++u) {
-                const uint32_t wv = u < 4 ? x0 : (u < 8 ? x1 : x2);
-                const int ix = (int)((wv >> (8 * (u & 3))) & 0xffu);
-                const R2 v = pt[ix];
-                mm[u] = v.x;
-                aa[u] = v.y;
-                pp[u] = kPf ? pn[u] : pay[40 + u];
-            }
-#pragma unroll
-            for (int u = 0; u < 10; ++u) term(mm[u], aa[u], pp[u], u & 1);
-        }
-        R s = R(0.5) * (s0 + s1);
-        s += R(1) * pay[kNbr];
-        s += (M - pay[kSys + 0]) / pay[kSys + 2] * pay[kNbr + 1];
-        s += (a - pay[kSys + 1]) / pay[kSys + 3] * pay[kNbr + 2];
-        return s;
-    }
-#endif
-#ifndef PD_CHUNK
-#define PD_CHUNK 10
-#endif
-    constexpr int kChunk = PD_CHUNK;
-    // Chunks as a loop: fully unrolled, the scheduler hoists every chunk's loads ahead and the
-    // kernel spills (256 VGPRs + 260 spilled); rolled it needs 235 VGPRs and no scratch.
-    // PD_RBF_UNROLL restores the full unroll (experiments).
-#if defined(PD_RBF_UNROLL) || defined(PD_RBF_SB)
-#pragma unroll
-#else
-#pragma unroll 1
-#endif
-    for (int j0 = part; j0 < kNbr; j0 += kChunk * nparts) {
-#ifdef PD_RBF_SB
-        __builtin_amdgcn_sched_barrier(0);
-#endif
-        R mm[kChunk], aa[kChunk], pp[kChunk];
-#pragma unroll
-        for (int u = 0; u < kChunk; ++u) {
-            int j = j0 + u * nparts;
-            bool ok = j < kNbr;
-            int jj = ok ? j : 0;
-            const int bp = idx_pos(jj);
-            const int ix = (int)((iw[bp >> 2] >> ((bp & 3) * 8)) & 0xffu);
-            const R2 v = pt[ix];
-            mm[u] = v.x;
-            aa[u] = v.y;
-            pp[u] = ok ? pay[jj] : R(0);
-        }
-#pragma unroll
-        for (int u = 0; u < kChunk; ++u) term(mm[u], aa[u], pp[u], u & 1);
     }
     R s = R(0.5) * (s0 + s1);
     if (part == 0) {
-        s += R(1) * pay[kNbr];
-        s += (M - pay[kSys + 0]) / pay[kSys + 2] * pay[kNbr + 1];
-        s += (a - pay[kSys + 1]) / pay[kSys + 3] * pay[kNbr + 2];
+        s += R(1) * pay[kPayPoly];
+        s += (M - pay[kPaySS + 0]) / pay[kPaySS + 2] * pay[kPayPoly + 1];
+        s += (a - pay[kPaySS + 1]) / pay[kPaySS + 3] * pay[kPayPoly + 2];
     }
     return s;
 }
@@ -232,16 +198,18 @@ __device__ __forceinline__ void solve_wave(DP<R>& P, int table, unsigned long lo
     const PD_AS4 double* aoa = table ? P.cl_aoa_d : P.cd_aoa_d;
     int lo[kCols], len[kCols];
     key_unpack(key, lo, len);
-    int my_idx = 0;
+    // lane < 50: term `lane` of the window order, column c, window offset off, pair slot my_slot
+    int my_idx = 0, my_c = 0, my_off = 0, my_slot = 0;
     if (lane < kNbr) {
-        int c = 0, off = lane, acc = 0;
+        int c = 0, off = lane, acc = 0, sl0 = 0, sl = 0;
 #pragma unroll
         for (int q = 0; q < kCols; ++q) {
-            if (lane >= acc && lane < acc + len[q]) { c = q; off = lane - acc; }
+            if (lane >= acc && lane < acc + len[q]) { c = q; off = lane - acc; sl = sl0; }
             acc += len[q];
+            sl0 += (len[q] + 1) / 2;
         }
         int idx = start[c] + lo[c] + off;
-        my_idx = idx;
+        my_idx = idx; my_c = c; my_off = off; my_slot = sl + off / 2;
         ym[lane] = mach[idx]; ya[lane] = aoa[c]; yd[lane] = coef[idx];
     }
     wave_mem_sync();
@@ -305,21 +273,25 @@ __device__ __forceinline__ void solve_wave(DP<R>& P, int table, unsigned long lo
             wave_mem_sync();
         }
     }
-    if (lane < kSys) pay[lane] = singular ? (double)NAN : b[lane];
-    else if (lane == kSys) pay[kSys] = sh0;
-    else if (lane == kSys + 1) pay[kSys + 1] = sh1;
-    else if (lane == kSys + 2) pay[kSys + 2] = sc0;
-    else if (lane == kSys + 3) pay[kSys + 3] = sc1;
-    else if (lane < kPay) pay[lane] = 0.0;
+    // binary64 payload in the pair-slot layout of solve_neighbourhood (pd_common.h)
+    for (int j = lane; j < kPay; j += 64) pay[j] = 0.0;
     wave_mem_sync();
-    if (lane < kNbr) ((PD_AS1 uint8_t*)(pay + kPayIdx))[idx_pos(lane)] = (uint8_t)my_idx;
+    PD_AS1 uint8_t* ib = (PD_AS1 uint8_t*)(pay + kPayIdx);
+    if (lane < kNbr) {
+        pay[2 * my_slot + (my_off & 1)] = singular ? (double)NAN : b[lane];
+        if ((my_off & 1) == 0) { ib[pair_entry_pos(my_slot)] = (uint8_t)my_idx; ib[pair_aoa_pos(my_slot)] = (uint8_t)aoa[my_c]; }
+    } else if (lane < kSys) {
+        pay[kPayPoly + lane - kNbr] = singular ? (double)NAN : b[lane];
+    } else if (lane == kSys) pay[kPaySS + 0] = sh0;
+    else if (lane == kSys + 1) pay[kPaySS + 1] = sh1;
+    else if (lane == kSys + 2) pay[kPaySS + 2] = sc0;
+    else if (lane == kSys + 3) pay[kPaySS + 3] = sc1;
     wave_mem_sync();
     // payload in the kernel's precision, in the (now free) matrix area (pay_store, by lanes)
     PD_AS1 R* pr = (PD_AS1 R*)work;
-    if (lane < kPayIdx) pr[lane] = (R)pay[lane];
-    else if (lane < pay_stride<R>()) pr[lane] = R(0);
+    for (int j = lane; j < pay_stride<R>(); j += 64) pr[j] = j < kPayIdx ? (R)pay[j] : R(0);
     wave_mem_sync();
-    if (lane < kNbr) ((PD_AS1 uint8_t*)(pr + kPayIdx))[idx_pos(lane)] = (uint8_t)my_idx;
+    if (lane < kPayIdxBytes) ((PD_AS1 uint8_t*)(pr + kPayIdx))[lane] = ib[lane];
     wave_mem_sync();
 }
 
@@ -409,6 +381,11 @@ __device__ __forceinline__ R rbf(const StepArgs<R>& a, DP<R>& P, int table, cons
     }
     unsigned long long key = ckey;
     int slot = cslot;
+#ifdef PD_EXP_COUNT
+    atomicAdd(&a.pend.stats[24], 1ull);
+    atomicAdd(&a.pend.stats[25], (unsigned long long)(li < 0));
+    atomicAdd(&a.pend.stats[26], (unsigned long long)(li < 0 && trusted));
+#endif
 #ifdef PD_EXP_TRUSTCHECK
     const bool check_trusted = trusted;
     trusted = false;
@@ -423,6 +400,8 @@ __device__ __forceinline__ R rbf(const StepArgs<R>& a, DP<R>& P, int table, cons
         atomicAdd(&a.pend.stats[4], 1ull);
         atomicAdd(&a.pend.stats[5], (unsigned long long)(li >= 0));
         atomicAdd(&a.pend.stats[6], (unsigned long long)iters);
+        atomicAdd(&a.pend.stats[27], (unsigned long long)(key_pack(lo, len) != ckey));
+        atomicAdd(&a.pend.stats[28 + table], 1ull);
 #else
         knn_windows<R>(t.smach, t.start, t.n, t.aoa, M, aq, lo, len);
 #endif
@@ -537,7 +516,8 @@ __device__ __forceinline__ void actor_forward(const float* __restrict__ W, int64
 
 // ---------------------------------------------------------------- LDS of one step workgroup
 template <typename R, bool WIND, int EPB> struct StepLds {
-    // table points as (Mach, AoA) pairs, C_D's 256 then C_L's: one 16-byte LDS read per point
+    // table points as (Mach_p, Mach_p+1) entries, C_D's 256 then C_L's: one 16-byte LDS read per
+    // payload pair slot (smach[2p] is point p's Mach for the neighbourhood search)
     alignas(16) R tab[1024];
     R gf[256];                    // grid fins: ca_x, ca_y, cn_x, cn_y (64 each)
     R isa[9 * kIsaCols];          // ISA layers
@@ -598,8 +578,8 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
     {
         DP<R>& P = *params<R>(a.P);
         for (int t = threadIdx.x; t < 256; t += kStepBlock) {
-            L.tab[2 * t] = P.cd_mach[t]; L.tab[2 * t + 1] = P.cd_pt_aoa[t];
-            L.tab[512 + 2 * t] = P.cl_mach[t]; L.tab[513 + 2 * t] = P.cl_pt_aoa[t];
+            L.tab[2 * t] = P.cd_mach[t]; L.tab[2 * t + 1] = t < 255 ? P.cd_mach[t + 1] : R(0);
+            L.tab[512 + 2 * t] = P.cl_mach[t]; L.tab[513 + 2 * t] = t < 255 ? P.cl_mach[t + 1] : R(0);
         }
         if (threadIdx.x < 64) {
             L.gf[threadIdx.x] = P.ca_x[threadIdx.x]; L.gf[64 + threadIdx.x] = P.ca_y[threadIdx.x];
@@ -623,8 +603,8 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
             (&L.lines.key[0][0])[t] = (&P.line_key[0][0])[t];
         }
         if (threadIdx.x < 4) { L.lines.a[threadIdx.x] = P.line_a[threadIdx.x]; L.lines.nbp[threadIdx.x] = P.line_nbp[threadIdx.x]; }
-        for (int t = threadIdx.x; t < kLogCells; t += kStepBlock) {
-            s_logtab[2 * t] = P.logtab.invc[t]; s_logtab[2 * t + 1] = P.logtab.logc[t];
+        for (int t = threadIdx.x; t < 2 * kLogCellsD; t += kStepBlock) {
+            s_logtab[t] = P.logtab_d.cell[t];
         }
     }
     __syncthreads();
@@ -826,7 +806,7 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
                     // Philox counter (env, episode, step, sub-step), reproducible by the oracle)
                     u32x4 r = philox({(uint32_t)g, (uint32_t)(g >> 32) ^ e.ep, e.ts, kTagWindSub + (uint32_t)sub},
                                      a.seed_lo, a.seed_hi);
-                    gauss_pair<2>(r, s_logtab, s_logtab + 1, w0, w1);
+                    gauss_pair(r, (const double*)(uint64_t)&P.logtab.invc[0], (const double*)(uint64_t)&P.logtab.logc[0], w0, w1);
                 }
                 // vonkarman.py:33-36: state = Ad @ state + Bd * w  (Bd = sigma * Bd(sigma=1))
                 R n0 = (P.vk_Ad_u[0] * e.fu0 + P.vk_Ad_u[1] * e.fu1) + (e.sgu * P.vk_Bd_u[0]) * (R)w0;
@@ -1301,7 +1281,8 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
     }
     // ---- the env's bookkeeping for the next step: auto-reset in registers, or carry on
     if (ended) {
-        reset_values<R, 2>(P2, a, g, e.ep + 1, s_logtab, s_logtab + 1, e);   // keeps the aero caches
+        reset_values<R>(P2, a, g, e.ep + 1, (const double*)(uint64_t)&P2.logtab.invc[0],
+                        (const double*)(uint64_t)&P2.logtab.logc[0], e);   // keeps the aero caches
     } else {
         e.vprev = v;
         e.glen = glen; e.ghead = ghead;

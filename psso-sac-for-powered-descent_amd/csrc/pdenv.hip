@@ -137,8 +137,8 @@ __global__ __launch_bounds__(kBlock) void k_atmosphere(StepArgs<R> a, const R* a
         r[0] = P.isa_Hb[k]; r[1] = P.isa_Tb[k]; r[2] = P.isa_beta[k]; r[3] = P.isa_pb[k];
         r[4] = P.isa_bt[k]; r[5] = P.isa_ex[k]; r[6] = P.isa_iso[k]; r[7] = R(0);
     }
-    for (int t = threadIdx.x; t < kLogCells; t += kBlock) {
-        s_logtab[2 * t] = P.logtab.invc[t]; s_logtab[2 * t + 1] = P.logtab.logc[t];
+    for (int t = threadIdx.x; t < 2 * kLogCellsD; t += kBlock) {
+        s_logtab[t] = P.logtab_d.cell[t];
     }
     __syncthreads();
     int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -435,6 +435,7 @@ template <typename R> void fill_params(const pd_params* p, const pd_config* c, D
     D.norm_y = (R)p->norm_y; D.norm_vy = (R)p->norm_vy; D.norm_x = (R)p->norm_x; D.norm_vx = (R)p->norm_vx;
     D.k_theta_pso = (R)(std::atanh(0.75) / (25.0 * kDeg2Rad));
     log_table_fill(D.logtab);
+    log_table_fill(D.logtab_d);
     D.y0_rl = (R)p->state0[1]; D.m0_rl = (R)p->state0[8];
     // ---- phase of the handle: its initial state, observation, and the constants of the
     // other compile_physics phases (rockets_physics.py:17-166,402-451,728-802,959-997)
@@ -493,6 +494,11 @@ pd_status validate(const pd_params* p, const pd_config* c) {
             return fail(PD_ERR_INVALID, "ascent phases need the reference trajectory (ref_y/x/vx/vy, n_ref >= 2)");
     }
     if (c->precision != PD_F64 && c->precision != PD_F32) return fail(PD_ERR_INVALID, "bad precision");
+    // the neighbourhood payloads carry each pair slot's column AoA as a byte (pd_common.h)
+    for (const pd_aero_table* t : {&p->cd, &p->cl})
+        for (int k = 0; k < t->n_cols; ++k)
+            if (!(t->col_aoa[k] >= 0.0 && t->col_aoa[k] <= 255.0 && t->col_aoa[k] == (double)(int)t->col_aoa[k]))
+                return fail(PD_ERR_INVALID, "aero table column AoAs must be integers in [0, 255]");
     if (c->action_f64 && c->precision != PD_F64) return fail(PD_ERR_INVALID, "f64 actions need PD_F64");
     if (c->enable_wind && !(c->wind_percentile == -1 || (c->wind_percentile >= 50 && c->wind_percentile <= 99)))
         return fail(PD_ERR_INVALID, "wind_percentile must be 50..99 or -1");
