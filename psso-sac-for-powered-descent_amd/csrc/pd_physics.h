@@ -84,6 +84,9 @@ template <typename R> struct DevParams {
     R grid_a0[2], grid_inv_da[2], grid_inv_dm[2];
     const unsigned long long* grid_key[2];
     const int* grid_slot[2];
+    // refined cells (kGridRefine): kGridSub x kGridSub sub-cells each, Mach-major
+    const unsigned long long* sub_key[2];
+    const int* sub_slot[2];
     R line_bp[4][kLineMax];
     int line_slot[4][kLineMax + 1];
     unsigned long long line_key[4][kLineMax + 1];

@@ -60,6 +60,8 @@ template <typename R> struct TabView {
     int line0;                 // index of this table's first clamped line (0: C_D, 2: C_L)
     const PD_AS1 unsigned long long* grid_key;
     const PD_AS1 int* grid_slot;
+    const PD_AS1 unsigned long long* sub_key;
+    const PD_AS1 int* sub_slot;
     int grid_nm, grid_na;
     R grid_a0, grid_inv_da, grid_inv_dm;
 };
@@ -371,13 +373,27 @@ __device__ __forceinline__ R rbf(const StepArgs<R>& a, DP<R>& P, int table, cons
         if (!(fm == fm) || !(fa == fa)) { im = 0; ia = 0; }   // NaN queries
         int cell = im * t.grid_na + ia;
         ckey = t.grid_key[cell];
-        const int gsl = t.grid_slot[cell];
-        cslot = gsl < 0 ? -1 : (gsl & (kGridExact - 1));
+        int gsl = t.grid_slot[cell];
+        R um = fm - (R)im, ua = fa - (R)ia;     // position in the cell, [0, 1)
+        if (sizeof(R) != 8 && gsl >= 0 && (gsl & kGridRefine)) gsl = -1;   // centre key, verified
+        if (sizeof(R) == 8 && gsl >= 0 && (gsl & kGridRefine)) {
+            // a cell that straddles neighbourhood regions: its sub-cell (binary64 handles; the
+            // binary32 handle's rounding is too coarse for sub-cell margins and verifies instead)
+            const int ref = gsl & (kGridRefine - 1);
+            const R sm = um * R(kGridSub), sa = ua * R(kGridSub);
+            int jm = (int)sm, ja = (int)sa;
+            jm = jm < 0 ? 0 : (jm > kGridSub - 1 ? kGridSub - 1 : jm);
+            ja = ja < 0 ? 0 : (ja > kGridSub - 1 ? kGridSub - 1 : ja);
+            const int sc = (ref * kGridSub + jm) * kGridSub + ja;
+            ckey = t.sub_key[sc];
+            gsl = t.sub_slot[sc];
+            um = sm - (R)jm; ua = sa - (R)ja;
+        }
+        cslot = gsl < 0 ? -1 : (gsl & (kGridRefine - 1));
         // every point of an exact cell has the cell's key (convexity of 50-NN regions); the
         // rounding margin keeps queries on a cell edge on the verified path
         const R eps = sizeof(R) == 8 ? R(1e-9) : R(1e-4);
-        trusted = gsl >= 0 && (gsl & kGridExact) && fm - (R)im > eps && (R)(im + 1) - fm > eps &&
-                  fa - (R)ia > eps && (R)(ia + 1) - fa > eps;
+        trusted = gsl >= 0 && (gsl & kGridExact) && um > eps && R(1) - um > eps && ua > eps && R(1) - ua > eps;
     }
     unsigned long long key = ckey;
     int slot = cslot;
@@ -540,6 +556,8 @@ __device__ __forceinline__ TabView<R> tab_view(DP<R>& P, const R* tab, int table
     t.line0 = table ? 2 : 0;
     t.grid_key = gbl(P.grid_key[table]);
     t.grid_slot = gbl(P.grid_slot[table]);
+    t.sub_key = gbl(P.sub_key[table]);
+    t.sub_slot = gbl(P.sub_slot[table]);
     t.grid_nm = P.grid_nm[table];
     t.grid_na = P.grid_na[table];
     t.grid_a0 = P.grid_a0[table];

@@ -10,7 +10,10 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/pdenv.h"
@@ -196,10 +199,10 @@ int table_insert(const pd_aero_table& t, Table<R>& T, uint64_t key, std::vector<
     uint32_t mask = (uint32_t)(cap - 1), h = key_hash(key, T.logcap);
     while (T.keys[h] != kEmptyKey && T.keys[h] != key) h = (h + 1) & mask;
     if (T.keys[h] == key) return (int)h;
+    if ((T.entries + 1) * 2 > cap) return -1;   // full (load factor 1/2): no solve
     double aoa[kCols];
     for (int c = 0; c < kCols; ++c) aoa[c] = t.col_aoa[c];
     if (solve_neighbourhood(t.mach, t.coef, t.col_start, aoa, key, work.data(), pay.data()) != 0) return -1;
-    if ((T.entries + 1) * 2 > cap) return -1;
     T.keys[h] = key;
     pay_store<R>(pay.data(), T.pay.data() + h * pay_stride<R>());
     ++T.entries;
@@ -266,31 +269,143 @@ pd_status build_line(const pd_aero_table& t, double a, Table<R>& T, int li, DevP
     return PD_OK;
 }
 
-// Candidate grid over the interior query domain [0, 10] Mach x [a0, a1]: the 50-NN key at
-// every cell centre (brute force), inserted into the table.  A 50-NN region is an intersection
-// of half-planes (order-k Voronoi cell), hence convex: when all four corners of a cell carry
-// the centre's key, the whole cell does, and the slot is flagged kGridExact so that device
-// lookups skip the verification.  Other cells' keys are candidates the device verifies.
-template <typename R>
-pd_status build_grid(const pd_aero_table& t, double a0, double a1, int nm, int na, Table<R>& T,
-                     std::vector<unsigned long long>& gk, std::vector<int>& gs) {
-    gk.assign((size_t)nm * na, 0); gs.assign((size_t)nm * na, -1);
-    std::vector<double> work(kScratch), pay(kPay);
-    double dm = 10.0 / nm, da = (a1 - a0) / na;
-    std::vector<uint64_t> corner((size_t)(nm + 1) * (na + 1));
-    for (int im = 0; im <= nm; ++im)
-        for (int ia = 0; ia <= na; ++ia)
-            corner[(size_t)im * (na + 1) + ia] = host_knn_key(t, im * dm, a0 + ia * da);
+// The same 50-NN key by selection instead of a full sort: the 50 smallest under the total order
+// (distance, point index) are exactly stable_sort's first 50, so the key is host_knn_key's.
+uint64_t knn_key_select(const pd_aero_table& t, double M, double a) {
+    double d[PD_MAX_PTS];
+    int id[PD_MAX_PTS], col[PD_MAX_PTS];
+    int n = 0;
+    for (int c = 0; c < t.n_cols; ++c)
+        for (int k = 0; k < t.col_len[c]; ++k, ++n) {
+            double dm = M - t.mach[t.col_start[c] + k], da = a - t.col_aoa[c];
+            d[n] = dm * dm + da * da;
+            id[n] = n;
+            col[n] = c;
+        }
+    std::nth_element(id, id + (kNbr - 1), id + n, [&](int x, int y) { return d[x] < d[y] || (d[x] == d[y] && x < y); });
+    int lo[kCols], hi[kCols];
+    for (int c = 0; c < kCols; ++c) { lo[c] = 1 << 20; hi[c] = -1; }
+    int base[kCols] = {0, 0, 0, 0, 0};
+    for (int c = 1; c < t.n_cols; ++c) base[c] = base[c - 1] + t.col_len[c - 1];
+    for (int j = 0; j < kNbr; ++j) {
+        const int p = id[j], c = col[p], k = p - base[c];
+        lo[c] = std::min(lo[c], k); hi[c] = std::max(hi[c], k);
+    }
+    int L[kCols], N[kCols];
+    for (int c = 0; c < kCols; ++c) {
+        if (hi[c] < 0) { L[c] = 0; N[c] = 0; } else { L[c] = lo[c]; N[c] = hi[c] - lo[c] + 1; }
+    }
+    return key_pack(L, N);
+}
+
+// Keys of one interior candidate grid: cell centres and corners, and for every cell whose
+// corners disagree with its centre a kGridSub x kGridSub sub-grid (centres and corners).  Pure
+// functions of the table, so they are computed once per process (threads over cells) and
+// cached; slots are assigned per handle.
+struct GridKeys {
+    int nm = 0, na = 0;
+    std::vector<uint64_t> centre, corner;            // [nm][na], [nm + 1][na + 1]
+    std::vector<int> refined;                        // cell index of each refined cell
+    std::vector<uint64_t> sub_centre, sub_corner;    // [ref][S][S], [ref][S + 1][S + 1]
+};
+
+template <typename F> void parallel_for(int64_t n, F f) {
+    unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    if (n < 64) nt = 1;
+    std::vector<std::thread> th;
+    for (unsigned k = 0; k < nt; ++k)
+        th.emplace_back([=] { for (int64_t i = (int64_t)k; i < n; i += nt) f(i); });
+    for (auto& x : th) x.join();
+}
+
+const GridKeys& grid_keys(const pd_aero_table& t, double a0, double a1, int nm, int na) {
+    static std::mutex mu;
+    static std::map<uint64_t, GridKeys> cache;
+    uint64_t h = 1469598103934665603ull;
+    auto mix = [&](const void* p, size_t n) {
+        for (size_t i = 0; i < n; ++i) { h ^= ((const uint8_t*)p)[i]; h *= 1099511628211ull; }
+    };
+    mix(&t, sizeof(t)); mix(&a0, 8); mix(&a1, 8); mix(&nm, 4); mix(&na, 4);
+    std::lock_guard<std::mutex> lock(mu);
+    auto it = cache.find(h);
+    if (it != cache.end()) return it->second;
+    GridKeys& g = cache[h];
+    g.nm = nm; g.na = na;
+    const double dm = 10.0 / nm, da = (a1 - a0) / na;
+    const int S = kGridSub;
+    g.corner.resize((size_t)(nm + 1) * (na + 1));
+    g.centre.resize((size_t)nm * na);
+    parallel_for(nm + 1, [&](int64_t im) {
+        for (int ia = 0; ia <= na; ++ia) g.corner[(size_t)im * (na + 1) + ia] = knn_key_select(t, im * dm, a0 + ia * da);
+        if (im < nm)
+            for (int ia = 0; ia < na; ++ia)
+                g.centre[(size_t)im * na + ia] = knn_key_select(t, (im + 0.5) * dm, a0 + (ia + 0.5) * da);
+    });
     for (int im = 0; im < nm; ++im)
         for (int ia = 0; ia < na; ++ia) {
-            uint64_t key = host_knn_key(t, (im + 0.5) * dm, a0 + (ia + 0.5) * da);
-            gk[(size_t)im * na + ia] = key;
-            int slot = table_insert<R>(t, T, key, work, pay);
-            bool exact = slot >= 0;
-            for (int c = 0; c < 4 && exact; ++c)
-                exact = corner[(size_t)(im + (c >> 1)) * (na + 1) + ia + (c & 1)] == key;
-            gs[(size_t)im * na + ia] = slot < 0 ? -1 : (slot | (exact ? kGridExact : 0));
+            const uint64_t key = g.centre[(size_t)im * na + ia];
+            bool same = true;
+            for (int c = 0; c < 4 && same; ++c) same = g.corner[(size_t)(im + (c >> 1)) * (na + 1) + ia + (c & 1)] == key;
+            if (!same) g.refined.push_back(im * na + ia);
         }
+    const int64_t nr = (int64_t)g.refined.size();
+    g.sub_corner.resize((size_t)nr * (S + 1) * (S + 1));
+    g.sub_centre.resize((size_t)nr * S * S);
+    parallel_for(nr, [&](int64_t r) {
+        const int im = g.refined[r] / na, ia = g.refined[r] % na;
+        for (int jm = 0; jm <= S; ++jm)
+            for (int ja = 0; ja <= S; ++ja) {
+                g.sub_corner[((size_t)r * (S + 1) + jm) * (S + 1) + ja] =
+                    knn_key_select(t, (im + (double)jm / S) * dm, a0 + (ia + (double)ja / S) * da);
+                if (jm < S && ja < S)
+                    g.sub_centre[((size_t)r * S + jm) * S + ja] =
+                        knn_key_select(t, (im + (jm + 0.5) / S) * dm, a0 + (ia + (ja + 0.5) / S) * da);
+            }
+    });
+    return g;
+}
+
+// Candidate grid over the interior query domain [0, 10] Mach x [a0, a1]: the 50-NN key at
+// every cell centre, inserted into the table.  A 50-NN region is an intersection of
+// half-planes (order-k Voronoi cell), hence convex: when all four corners of a cell carry the
+// centre's key, the whole cell does, and the slot is flagged kGridExact so that device lookups
+// skip the verification.  A cell whose corners disagree is refined into kGridSub x kGridSub
+// sub-cells with the same construction (flagged kGridRefine, its sub-grid index in the low
+// bits), so that only queries near a region boundary are verified on the device.
+template <typename R>
+pd_status build_grid(const pd_aero_table& t, double a0, double a1, int nm, int na, Table<R>& T,
+                     std::vector<unsigned long long>& gk, std::vector<int>& gs,
+                     std::vector<unsigned long long>& sk, std::vector<int>& ss) {
+    const GridKeys& g = grid_keys(t, a0, a1, nm, na);
+    const int S = kGridSub;
+    gk.assign((size_t)nm * na, 0); gs.assign((size_t)nm * na, -1);
+    std::vector<double> work(kScratch), pay(kPay);
+    auto slot_of = [&](uint64_t key, bool exact) {
+        int slot = table_insert<R>(t, T, key, work, pay);
+        return slot < 0 ? -1 : (slot | (exact ? kGridExact : 0));
+    };
+    for (int im = 0; im < nm; ++im)
+        for (int ia = 0; ia < na; ++ia) {
+            const uint64_t key = g.centre[(size_t)im * na + ia];
+            gk[(size_t)im * na + ia] = key;
+            gs[(size_t)im * na + ia] = slot_of(key, true);   // refined cells overwritten below
+        }
+    const int64_t nr = (int64_t)g.refined.size();
+    if (nr >= kGridRefine) return fail(PD_ERR_INVALID, "too many refined grid cells");
+    sk.assign((size_t)nr * S * S, 0); ss.assign((size_t)nr * S * S, -1);
+    for (int64_t r = 0; r < nr; ++r) {
+        gs[g.refined[r]] = kGridRefine | (int)r;
+        for (int jm = 0; jm < S; ++jm)
+            for (int ja = 0; ja < S; ++ja) {
+                const size_t q = ((size_t)r * S + jm) * S + ja;
+                const uint64_t key = g.sub_centre[q];
+                bool exact = true;
+                for (int c = 0; c < 4 && exact; ++c)
+                    exact = g.sub_corner[((size_t)r * (S + 1) + jm + (c >> 1)) * (S + 1) + ja + (c & 1)] == key;
+                sk[q] = key;
+                ss[q] = slot_of(key, exact);
+            }
+    }
     return PD_OK;
 }
 
@@ -534,8 +649,8 @@ template <typename R> pd_status create_impl(const pd_params* p, const pd_config*
     if ((st = build_line<R>(p->cl, 10.0, tcl, 2, D)) != PD_OK) return st;
     if ((st = build_line<R>(p->cl, -10.0, tcl, 3, D)) != PD_OK) return st;
     // interior candidate grids: C_D abscissa in [-radians(10), radians(10)], C_L in [0, 10]
-    std::vector<unsigned long long> gk[2];
-    std::vector<int> gs[2];
+    std::vector<unsigned long long> gk[2], sk[2];
+    std::vector<int> gs[2], ss[2];
     int gnm[2] = {400, 400}, gna[2] = {16, 200};
     if (const char* g = getenv("PDENV_GRID")) {   // experiments: "nm_cd,na_cd,nm_cl,na_cl"
         int v[4];
@@ -544,13 +659,21 @@ template <typename R> pd_status create_impl(const pd_params* p, const pd_config*
         }
     }
     const double ga0[2] = {-10.0 * kDeg2Rad, 0.0}, ga1[2] = {10.0 * kDeg2Rad, 10.0};
-    if ((st = build_grid<R>(p->cd, ga0[0], ga1[0], gnm[0], gna[0], tcd, gk[0], gs[0])) != PD_OK) return st;
-    if ((st = build_grid<R>(p->cl, ga0[1], ga1[1], gnm[1], gna[1], tcl, gk[1], gs[1])) != PD_OK) return st;
+    if ((st = build_grid<R>(p->cd, ga0[0], ga1[0], gnm[0], gna[0], tcd, gk[0], gs[0], sk[0], ss[0])) != PD_OK) return st;
+    if ((st = build_grid<R>(p->cl, ga0[1], ga1[1], gnm[1], gna[1], tcl, gk[1], gs[1], sk[1], ss[1])) != PD_OK) return st;
     for (int tb = 0; tb < 2; ++tb) {
-        void *dk, *ds;
-        if ((st = dalloc(e, &dk, gk[tb].size() * 8)) || (st = dalloc(e, &ds, gs[tb].size() * 4))) return st;
+        void *dk, *ds, *dsk, *dss;
+        const size_t nsub = std::max<size_t>(sk[tb].size(), 1);
+        if ((st = dalloc(e, &dk, gk[tb].size() * 8)) || (st = dalloc(e, &ds, gs[tb].size() * 4)) ||
+            (st = dalloc(e, &dsk, nsub * 8)) || (st = dalloc(e, &dss, nsub * 4)))
+            return st;
         PD_HIP(hipMemcpy(dk, gk[tb].data(), gk[tb].size() * 8, hipMemcpyHostToDevice));
         PD_HIP(hipMemcpy(ds, gs[tb].data(), gs[tb].size() * 4, hipMemcpyHostToDevice));
+        if (!sk[tb].empty()) {
+            PD_HIP(hipMemcpy(dsk, sk[tb].data(), sk[tb].size() * 8, hipMemcpyHostToDevice));
+            PD_HIP(hipMemcpy(dss, ss[tb].data(), ss[tb].size() * 4, hipMemcpyHostToDevice));
+        }
+        D.sub_key[tb] = (const unsigned long long*)dsk; D.sub_slot[tb] = (const int*)dss;
         D.grid_key[tb] = (const unsigned long long*)dk; D.grid_slot[tb] = (const int*)ds;
         D.grid_nm[tb] = gnm[tb]; D.grid_na[tb] = gna[tb]; D.grid_a0[tb] = (R)ga0[tb];
         D.grid_inv_da[tb] = (R)(gna[tb] / (ga1[tb] - ga0[tb])); D.grid_inv_dm[tb] = (R)(gnm[tb] / 10.0);

@@ -17,10 +17,12 @@ n = int(os.environ.get("N", "65536"))
 launches = int(os.environ.get("LAUNCHES", "24"))
 F = 16
 phase = os.environ.get("PHASE", "landing_burn_pure_throttle")
+t_c = time.perf_counter()
 env = pdenv.PoweredDescentEnv(n, flight_phase=phase, mode="rl" if phase == "landing_burn_pure_throttle" else "pso",
                               precision=os.environ.get("PREC", "f64"), enable_wind=True, stochastic_wind=True,
                               wind_percentile=None, auto_reset=True, tilt_sigma_rad=math.radians(1.0), seed=1234,
                               lanes_per_env=int(os.environ.get("LPE", "0")))
+t_create = time.perf_counter() - t_c
 g = torch.Generator(device="cuda").manual_seed(42)
 acts = (torch.rand((launches + 8) * F, n, env.action_dim, generator=g, device="cuda") * 2 - 1).contiguous()
 kw = dict(device="cuda")
@@ -42,4 +44,10 @@ ms = sorted(a.elapsed_time(b) for a, b in ev)
 print(json.dumps({"lib": os.path.basename(os.environ.get("PDENV_LIB", "libpdenv.so")), "n": n,
                   "launch_ms_avg": sum(ms) / len(ms), "launch_ms_med": ms[len(ms) // 2],
                   "ms_per_step": sum(ms) / len(ms) / F, "wall_ms_per_step": wall * 1e3 / (launches * F),
-                  "misses": env.counters()["rbf_misses"]}), flush=True)
+                  "misses": env.counters()["rbf_misses"], "create_s": round(t_create, 2)}), flush=True)
+if os.environ.get("STATS"):
+    import ctypes as C
+    from pdenv import _lib as L
+    v = (L.I64 * 32)()
+    L.check(env.lib.pd_stats(env.h, v, 32))
+    print(json.dumps({"stats": list(v)}), flush=True)
