@@ -133,17 +133,36 @@ template <> __device__ __forceinline__ double eval_log<double>(double x) {
     const int e1 = (int)(hi >> 20) - 1022;
     const double m1 = __longlong_as_double((long long)((b & 0x000fffffffffffffull) | 0x3fe0000000000000ull));
 #endif
-    const uint32_t i = __builtin_amdgcn_ubfe(hi, 20 - kLogBitsD, kLogBitsD);
 #ifdef PD_EXP_LOGCELL0   // experiment: every lane reads cell 0 (no bank conflicts; wrong values)
-    const double2 c = ((const double2*)s_logtab)[i & 0u];
+    const uint32_t off = 0u;
 #else
-    const double2 c = ((const double2*)s_logtab)[i];
+    const uint32_t off = (hi >> (16 - kLogBitsD)) & ((kLogCellsD - 1) << 4);   // cell * 16 bytes
 #endif
+    const double2 c = *(const double2*)((const char*)s_logtab + off);
+    // log1p(r) = r + r^2 (r/3 - 1/2 - r^2/4): constants as SGPR / inline operands (no moves)
     const double r = fma(m1, c.x, -1.0);
-    double t = fma(r, -0.25, 1.0 / 3.0);
-    t = fma(r, t, -0.5);
-    const double p = fma(r * r, t, r);
+    const double r2 = r * r;
+    const double t = fma(r2, -0.25, fma(r, 1.0 / 3.0, -0.5));
+    const double p = fma(r2, t, r);
     return fma((double)e1, 6.93147180559945286227e-01, c.y + p);
+}
+// eval_log<double> in two stages, so that a caller can issue the cell reads of several
+// arguments before finishing any of them (same arithmetic, same bits)
+struct LogPart { double m1; int e1; double2 c; };
+__device__ __forceinline__ LogPart log_start(double x) {
+    LogPart q;
+    q.e1 = __builtin_amdgcn_frexp_exp(x);
+    q.m1 = __builtin_amdgcn_frexp_mant(x);
+    const uint32_t hi = (uint32_t)(__double_as_longlong(x) >> 32);
+    q.c = *(const double2*)((const char*)s_logtab + ((hi >> (16 - kLogBitsD)) & ((kLogCellsD - 1) << 4)));
+    return q;
+}
+__device__ __forceinline__ double log_finish(const LogPart& q) {
+    const double r = fma(q.m1, q.c.x, -1.0);
+    const double r2 = r * r;
+    const double t = fma(r2, -0.25, fma(r, 1.0 / 3.0, -0.5));
+    const double p = fma(r2, t, r);
+    return fma((double)q.e1, 6.93147180559945286227e-01, q.c.y + p);
 }
 template <> __device__ __forceinline__ float eval_log<float>(float x) {
     return __builtin_amdgcn_logf(x) * 0.693147180559945309f;

@@ -134,10 +134,41 @@ __device__ __forceinline__ R rbf_eval(const PD_AS1 R* __restrict__ pay, const R*
 #pragma unroll
             for (int u = 0; u < 10; ++u) { pp[u] = pn[u]; pn[u] = pay[10 * c + 10 + u]; }
             bytes(c + 1, wn);
+#ifndef PD_RBF_UNPHASED
+            if constexpr (sizeof(R) == 8) {
+                // the chunk in phases: five pair reads, ten d2, ten log-cell reads, ten finishes
+                R2 v[5];
+                R da2[5];
+#pragma unroll
+                for (int u = 0; u < 5; ++u) {
+                    const uint32_t h = w[u >> 1] >> (16 * (u & 1));
+                    v[u] = pt[h & 0xffu];
+                    const R da = a - (R)((h >> 8) & 0xffu);
+                    da2[u] = da * da;
+                }
+                R d2[10];
+#pragma unroll
+                for (int u = 0; u < 5; ++u) {
+                    const R dm0 = M - v[u].x, dm1 = M - v[u].y;
+                    d2[2 * u] = fma(dm0, dm0, da2[u]);
+                    d2[2 * u + 1] = fma(dm1, dm1, da2[u]);
+                }
+                LogPart lp[10];
+#pragma unroll
+                for (int k = 0; k < 10; ++k) lp[k] = log_start(d2[k]);
+#pragma unroll
+                for (int k = 0; k < 10; ++k) {
+                    const R wk = d2[k] * pp[k];
+                    if (k & 1) s1 = fma(wk, log_finish(lp[k]), s1); else s0 = fma(wk, log_finish(lp[k]), s0);
+                }
+            } else
+#endif
+            {
 #pragma unroll
             for (int u = 0; u < 5; ++u) {
                 const uint32_t h = w[u >> 1] >> (16 * (u & 1));
                 slot(h & 0xffu, (h >> 8) & 0xffu, pp[2 * u], pp[2 * u + 1]);
+            }
             }
         }
 #pragma unroll
