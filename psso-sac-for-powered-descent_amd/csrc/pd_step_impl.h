@@ -734,6 +734,12 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
     PD_ACC(1, t_loaded - t_staged);
 
     const int nf = POL ? 1 : a.n_fused;
+#ifndef PD_NO_ATM_CARRY
+    // the atmosphere and speed of the state a step ends in, computed by its rtd, are the next
+    // step's first sub-step's (same y, vx, vy; bit-identical): carried unless the env reset
+    R k_rho = R(0), k_patm = R(0), k_asnd = R(0), k_speed = R(0);
+    bool k_have = false;
+#endif
 #pragma unroll 1
     for (int f = 0; f < nf; ++f) {
     const size_t fo = (size_t)f * (size_t)N;
@@ -785,9 +791,15 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
         R x = e.s[0], y = e.s[1], vx = e.s[2], vy = e.s[3], th = e.s[4], thd = e.s[5], ga = e.s[6], al = e.s[7];
         R m = e.s[8], mp = e.s[9];
         // rocket_physics_fcn (rockets_physics.py:455-704)
-        R rho, patm, asnd;
-        atmosphere<R>(P, L.isa, y, rho, patm, asnd);
-        R speed = sqrt(vx * vx + vy * vy);
+        R rho, patm, asnd, speed;
+#ifndef PD_NO_ATM_CARRY
+        if (sub == 0 && k_have) { rho = k_rho; patm = k_patm; asnd = k_asnd; speed = k_speed; }
+        else
+#endif
+        {
+            atmosphere<R>(P, L.isa, y, rho, patm, asnd);
+            speed = sqrt(vx * vx + vy * vy);
+        }
         R mach = R(0);
         if (asnd != R(0)) { R mr = speed / asnd; mach = (R(10) < mr) ? R(10) : mr; }
         // alpha_effective (rockets_physics.py:498-501) and Mach feed the aero tables; what the
@@ -1146,6 +1158,9 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
     R rho, pa_, as_;
     atmosphere<R>(P2, L.isa, y, rho, pa_, as_);
     R speed = v;
+#ifndef PD_NO_ATM_CARRY
+    k_rho = rho; k_patm = pa_; k_asnd = as_; k_speed = v;
+#endif
     R q = R(0.5) * rho * (speed * speed);
     int tr = 0, id = 0, dn = 0;
     R rew = R(0);
@@ -1293,6 +1308,9 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
     PD_ACC(5, t_rtd - t_loop);
     // ---- outputs of step f (role 0 of the env's lane group)
     const bool ended = !POL && a.auto_reset && (dn || tr);
+#ifndef PD_NO_ATM_CARRY
+    k_have = !ended;
+#endif
     if (role == 0 && live) {
         if (a.obs) {
             // the wrappers' observation (obs_write kinds); compile-time for the landing burns
