@@ -371,15 +371,15 @@ __device__ __forceinline__ R rbf_miss_wave(const StepArgs<R>& a, DP<R>& P, int t
     return val;
 }
 
-// This lane's share of the RBF value of `table` at (M, aq).
-// Candidate neighbourhood: on a clamped query line (the common case: |alpha_eff| > 0.003 rad
+// The neighbourhood of `table` at (M, aq): its table slot (-1: not in the tables), the key in
+// cache.key.  Candidate neighbourhood: on a clamped query line (the common case: |alpha_eff| > 0.003 rad
 // clamps both tables) the interval table of that line (binary search over <= 96 Mach
 // breakpoints in LDS); elsewhere the interior grid cell's, or the env's cached set.  Unless the
 // candidate is trusted (strictly inside its interval/exact cell) it is VERIFIED (and repaired by
 // the swap search) against the exact distances before it is used.
 template <typename R>
-__device__ __forceinline__ R rbf(const StepArgs<R>& a, DP<R>& P, int table, const TabView<R>& t, const LineLds<R>& ln,
-                                 RbfCache<R>& cache, R M, R aq, int part, int nparts) {
+__device__ __forceinline__ int rbf_lookup(const StepArgs<R>& a, DP<R>& P, int table, const TabView<R>& t,
+                                          const LineLds<R>& ln, RbfCache<R>& cache, R M, R aq) {
     unsigned long long ckey = cache.key;
     int cslot = cache.slot;
     int li = aq == ln.a[t.line0] ? t.line0 : (aq == ln.a[t.line0 + 1] ? t.line0 + 1 : -1);
@@ -472,6 +472,16 @@ __device__ __forceinline__ R rbf(const StepArgs<R>& a, DP<R>& P, int table, cons
     }
     cache.key = key;
     cache.slot = slot;
+    return slot;
+}
+
+// This lane's share of the RBF value of `table` at (M, aq): lookup, evaluation, and the
+// wave-cooperative solve of missed neighbourhoods.
+template <typename R>
+__device__ __forceinline__ R rbf(const StepArgs<R>& a, DP<R>& P, int table, const TabView<R>& t, const LineLds<R>& ln,
+                                 RbfCache<R>& cache, R M, R aq, int part, int nparts) {
+    const int slot = rbf_lookup<R>(a, P, table, t, ln, cache, M, aq);
+    const unsigned long long key = cache.key;
     R val = R(0);
     if (slot >= 0) val = rbf_eval<R>(t.pay + (int64_t)slot * pay_stride<R>(), t.smach, M, aq, part, nparts);
     // Misses (a neighbourhood outside the pre-enumerated tables) take the wave-cooperative
@@ -817,9 +827,11 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
             R aq_cd = cd_query<R>(ae);
             const bool have = asnd != R(0);
             if constexpr (LPE == 1) {
+                // (both sums interleaved in lockstep on one lane, 1 wave per SIMD with AGPR
+                // spill space, measured 14 % slower than these two calls)
                 R v = rbf<R>(a, P, 1, tab_view<R>(P, L.tab, 1), L.lines, cB, mach, aq_cl, 0, 1);
-                CL = (!have || cl_zero) ? R(0) : (cl_sgn < R(0) ? -v : v);
                 R w = rbf<R>(a, P, 0, tab_view<R>(P, L.tab, 0), L.lines, cA, mach, aq_cd, 0, 1);
+                CL = (!have || cl_zero) ? R(0) : (cl_sgn < R(0) ? -v : v);
                 CD = have ? w : R(0);
             } else {
                 R v = rbf<R>(a, P, my_table, tab_view<R>(P, L.tab, my_table), L.lines, cA, mach,
