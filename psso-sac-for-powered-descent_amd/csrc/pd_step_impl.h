@@ -743,7 +743,39 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
     PD_T(t_loaded);
     PD_ACC(1, t_loaded - t_staged);
 
-    const int nf = POL ? 1 : a.n_fused;
+    // The env's fields back to HBM (live lanes).  A fresh copy of the offset: the store
+    // addresses are recomputed from the SGPR bases instead of being kept live from the loads
+    auto store_all = [&]() {
+    uint32_t uo = ui;
+    asm volatile("" : "+v"(uo));
+    if (live) {
+        const uint32_t ui = uo;
+#pragma unroll
+        for (int k = 0; k < 11; ++k)
+            if (k % LPE == role) ev(a.b.st + (k) * N, ui) = e.s[k];
+        if (role == 0) {
+            ev(a.b.vprev, ui) = e.vprev;
+            ev(a.b.glen, ui) = (uint8_t)e.glen; ev(a.b.ghead, ui) = (uint8_t)e.ghead;
+#pragma unroll
+            for (int k = 0; k < 10; ++k) ev(a.b.gwin + (k) * N, ui) = L.gwin[k][le];
+            ev(a.b.tid, ui) = (int8_t)e.tid;
+            ev(a.b.epi, ui) = e.ep; ev(a.b.tstep, ui) = e.ts;
+            if constexpr (PHASE == 1) { ev(a.b.act, ui) = e.act0; ev(a.b.act + N, ui) = e.act1; ev(a.b.act + (2) * N, ui) = e.act2; }
+            if constexpr (PHASE == 2) { if (aux == PD_PHASE_FLIP_OVER) ev(a.b.act, ui) = e.act0; }
+            if constexpr (WIND) {
+                ev(a.b.wind, ui) = e.fu0; ev(a.b.wind + N, ui) = e.fu1; ev(a.b.wind + (2) * N, ui) = e.fv0; ev(a.b.wind + (3) * N, ui) = e.fv1;
+                ev(a.b.wind + (4) * N, ui) = e.sgu; ev(a.b.wind + (5) * N, ui) = e.sgv;
+                ev(a.b.wprof, ui) = (uint8_t)e.prof;
+            }
+        }
+        // neighbourhood caches survive resets (any valid 50-set is a correct start)
+        if (part == 0) {
+            ev(a.b.key + (my_table) * N, ui) = cA.key; ev(a.b.slot + (my_table) * N, ui) = cA.slot;
+            if constexpr (LPE == 1) { ev(a.b.key + N, ui) = cB.key; ev(a.b.slot + N, ui) = cB.slot; }
+        }
+    }
+    };
+    const int nf = a.n_fused;   // policy rollouts: finished envs freeze, stored at their last step
 #ifndef PD_NO_ATM_CARRY
     // the atmosphere and speed of the state a step ends in, computed by its rtd, are the next
     // step's first sub-step's (same y, vx, vy; bit-identical): carried unless the env reset
@@ -761,13 +793,17 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
         // pso_wrapper.augment_state (env_wrapped_ea.py:97-123) of the current state in the
         // handle's precision, cast to float32 (simple_actor.forward), then the actor
         DP<R>& Q = *params<R>(a.P);
+        // the weights are the same every fused step: a laundered offset per step keeps their
+        // 372 loads inside the loop (hoisted, they would be held in registers and spill)
+        uint32_t uw = ui;
+        asm volatile("" : "+v"(uw));
         if constexpr (PHASE == 0) {
             float x[2] = {(float)(e.s[1] / Q.norm_y), (float)(e.s[3] / Q.norm_vy)};
-            actor_forward<2, 3, 1>(a.policy_w, N, ui, x, uf);
+            actor_forward<2, 3, 1>(a.policy_w, N, uw, x, uf);
         } else {
             float x[5] = {(float)(e.s[0] / Q.norm_x), (float)(e.s[1] / Q.norm_y), (float)(e.s[2] / Q.norm_vx),
                           (float)(e.s[3] / Q.norm_vy), (float)tanh(Q.k_theta_pso * (e.s[4] - Cst<R>::pi / R(2)))};
-            actor_forward<5, 4, 4>(a.policy_w, N, ui, x, uf);
+            actor_forward<5, 4, 4>(a.policy_w, N, uw, x, uf);
         }
     } else if (a.act_f64) {
 #pragma unroll
@@ -1343,21 +1379,6 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
         if (a.trunc_id) ev(a.trunc_id + fo, ui) = (int8_t)id;
         if (a.info) ev(a.info + (PD_INFO_GLOAD) * N, ui) = gl;
     }
-    if constexpr (POL) {
-        // done-mask compaction: the envs whose episode goes on, in lane order, appended to the
-        // next launch's list at a base taken by one atomic per wave (the count also tells the
-        // host when every episode has ended)
-        const bool cont = role == 0 && live && !(dn || tr);
-        const unsigned long long mk = __ballot(cont);
-        if (mk) {
-            const int lane = (int)__lane_id();
-            const int leader = __ffsll((long long)mk) - 1;
-            uint32_t base = 0;
-            if (lane == leader) base = atomicAdd(a.cnt_out, (uint32_t)__popcll(mk));
-            base = (uint32_t)__shfl((int)base, leader);
-            if (cont) a.list_out[base + (uint32_t)__popcll(mk & ((1ull << lane) - 1ull))] = (int32_t)i;
-        }
-    }
     // ---- the env's bookkeeping for the next step: auto-reset in registers, or carry on
     if (ended) {
         reset_values<R>(P2, a, g, e.ep + 1, (const double*)(uint64_t)&P2.logtab.invc[0],
@@ -1369,38 +1390,30 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
         e.ts = e.ts + 1;
         e.act0 = gdeg_out; e.act1 = dcmdl_out; e.act2 = dcmdr_out;
     }
+    if constexpr (POL) {
+        // an episode that ended is stored now and its lanes freeze (they go on computing in step
+        // with the wave, convergent for the cooperative miss solve, but write nothing)
+        if (live && (dn || tr)) { store_all(); live = false; }
+    }
     }   // fused steps
-
-    // ---- the env's state back to HBM, once.  A fresh copy of the offset: the store addresses are
-    // recomputed here from the SGPR bases instead of being kept live (spilled) from the loads
-    uint32_t uo = ui;
-    asm volatile("" : "+v"(uo));
-    if (live) {
-        const uint32_t ui = uo;
-#pragma unroll
-        for (int k = 0; k < 11; ++k)
-            if (k % LPE == role) ev(a.b.st + (k) * N, ui) = e.s[k];
-        if (role == 0) {
-            ev(a.b.vprev, ui) = e.vprev;
-            ev(a.b.glen, ui) = (uint8_t)e.glen; ev(a.b.ghead, ui) = (uint8_t)e.ghead;
-#pragma unroll
-            for (int k = 0; k < 10; ++k) ev(a.b.gwin + (k) * N, ui) = L.gwin[k][le];
-            ev(a.b.tid, ui) = (int8_t)e.tid;
-            ev(a.b.epi, ui) = e.ep; ev(a.b.tstep, ui) = e.ts;
-            if constexpr (PHASE == 1) { ev(a.b.act, ui) = e.act0; ev(a.b.act + N, ui) = e.act1; ev(a.b.act + (2) * N, ui) = e.act2; }
-            if constexpr (PHASE == 2) { if (aux == PD_PHASE_FLIP_OVER) ev(a.b.act, ui) = e.act0; }
-            if constexpr (WIND) {
-                ev(a.b.wind, ui) = e.fu0; ev(a.b.wind + N, ui) = e.fu1; ev(a.b.wind + (2) * N, ui) = e.fv0; ev(a.b.wind + (3) * N, ui) = e.fv1;
-                ev(a.b.wind + (4) * N, ui) = e.sgu; ev(a.b.wind + (5) * N, ui) = e.sgv;
-                ev(a.b.wprof, ui) = (uint8_t)e.prof;
-            }
-        }
-        // neighbourhood caches survive resets (any valid 50-set is a correct start)
-        if (part == 0) {
-            ev(a.b.key + (my_table) * N, ui) = cA.key; ev(a.b.slot + (my_table) * N, ui) = cA.slot;
-            if constexpr (LPE == 1) { ev(a.b.key + N, ui) = cB.key; ev(a.b.slot + N, ui) = cB.slot; }
+    if constexpr (POL) {
+        // done-mask compaction: the envs whose episode goes on, in lane order, appended to the
+        // next launch's list at a base taken by one atomic per wave (the count also tells the
+        // host when every episode has ended)
+        const bool cont = role == 0 && live;
+        const unsigned long long mk = __ballot(cont);
+        if (mk) {
+            const int lane = (int)__lane_id();
+            const int leader = __ffsll((long long)mk) - 1;
+            uint32_t base = 0;
+            if (lane == leader) base = atomicAdd(a.cnt_out, (uint32_t)__popcll(mk));
+            base = (uint32_t)__shfl((int)base, leader);
+            if (cont) a.list_out[base + (uint32_t)__popcll(mk & ((1ull << lane) - 1ull))] = (int32_t)i;
         }
     }
+
+    // ---- the env's state back to HBM, once (policy rollouts: also when its episode ends)
+    store_all();
 #ifdef PD_STAMP
     PD_T(t_end);
     PD_ACC(6, t_end - t_rtd);

@@ -791,6 +791,8 @@ __global__ __launch_bounds__(kBlock) void k_live_init(int32_t* list, uint32_t* c
     if (i < 3) cnt[i] = i == 0 ? (uint32_t)n : 0u;
 }
 
+int policy_fuse();
+
 template <typename R>
 pd_status rollout_policy_impl(pd_env* e, const float* w, int32_t max_steps, void* fitness, int32_t* steps,
                               int32_t check_every, hipStream_t s) {
@@ -821,16 +823,23 @@ pd_status rollout_policy_impl(pd_env* e, const float* w, int32_t max_steps, void
     a.use_list = force && *force ? (atoi(force) != 0) : (N * e->lpe > (int64_t)dev_cus * 512);
     int64_t n_launch = N;
     int checks = 0;
-    for (int32_t t = 0; t < max_steps; ++t) {
-        a.list_in = e->live[t & 1]; a.list_out = e->live[(t + 1) & 1];
-        a.cnt_in = e->live_cnt + t % 3; a.cnt_out = e->live_cnt + (t + 1) % 3; a.cnt_zero = e->live_cnt + (t + 2) % 3;
+    // F policy steps per launch (an episode that ends inside a launch is stored at its last step
+    // and its lanes freeze); the live list is compacted once per launch
+    const int F = policy_fuse();
+    const int check_launches = check_every > 0 ? std::max(1, check_every / F) : 0;
+    int32_t t = 0;
+    for (int l = 0; t < max_steps; ++l) {
+        a.n_fused = std::min<int32_t>(F, max_steps - t);
+        t += a.n_fused;
+        a.list_in = e->live[l & 1]; a.list_out = e->live[(l + 1) & 1];
+        a.cnt_in = e->live_cnt + l % 3; a.cnt_out = e->live_cnt + (l + 1) % 3; a.cnt_zero = e->live_cnt + (l + 2) % 3;
         if (e->cfg.phase == PD_PHASE_PURE_THROTTLE) { if (wind) launch_policy<R, 0, true>(a, e->lpe, n_launch, s); else launch_policy<R, 0, false>(a, e->lpe, n_launch, s); }
         else { if (wind) launch_policy<R, 1, true>(a, e->lpe, n_launch, s); else launch_policy<R, 1, false>(a, e->lpe, n_launch, s); }
         PD_HIP(hipGetLastError());
-        if ((t & 15) == 15) launch_insert<R>(e, s);
-        if (check_every > 0 && (t + 1) % check_every == 0 && t + 1 < max_steps) {
+        if (F >= 16 || (l & (16 / F - 1)) == 16 / F - 1) launch_insert<R>(e, s);
+        if (check_launches > 0 && (l + 1) % check_launches == 0 && t < max_steps) {
             const int k = checks & 1;
-            PD_HIP(hipMemcpyAsync(e->host_cnt + k, e->live_cnt + (t + 1) % 3, 4, hipMemcpyDeviceToHost, s));
+            PD_HIP(hipMemcpyAsync(e->host_cnt + k, e->live_cnt + (l + 1) % 3, 4, hipMemcpyDeviceToHost, s));
             PD_HIP(hipEventRecord(e->cnt_ev[k], s));
             if (checks > 0) {
                 PD_HIP(hipEventSynchronize(e->cnt_ev[k ^ 1]));
@@ -845,6 +854,15 @@ pd_status rollout_policy_impl(pd_env* e, const float* w, int32_t max_steps, void
     if (steps) PD_HIP(hipMemcpyAsync(steps, e->tstep, (size_t)N * 4, hipMemcpyDeviceToDevice, s));
     PD_HIP(hipGetLastError());
     return PD_OK;
+}
+
+// Policy steps per fused policy-rollout launch (PDENV_PFUSE overrides; a power of two <= 16).
+int policy_fuse() {
+    const char* s = getenv("PDENV_PFUSE");
+    int k = s && *s ? atoi(s) : 8;
+    int f = 1;
+    while (f * 2 <= k && f < 16) f *= 2;
+    return f;
 }
 
 // Steps per fused launch: the miss flush runs between launches, so a neighbourhood solved on
