@@ -934,6 +934,7 @@ pd_status pd_create(const pd_params* params, const pd_config* cfg, pd_env** out)
     // 16 384 LPE 4 0.066, 8 0.067, 16 0.105; 32 768 LPE 2 0.072, 4 0.075; 65 536 LPE 2 best)
     e->lpe = cfg->lanes_per_env != 0 ? cfg->lanes_per_env
                                      : (cfg->n_envs <= 4096 ? 16 : (cfg->n_envs <= 8192 ? 8 : (cfg->n_envs <= 16384 ? 4 : 2)));
+    if (const char* lv = getenv("PDENV_LPE"); lv && *lv && cfg->lanes_per_env == 0) e->lpe = atoi(lv);   // experiments
     if (e->lpe != 1 && e->lpe != 2 && e->lpe != 4 && e->lpe != 8 && e->lpe != 16) { delete e; return fail(PD_ERR_INVALID, "lanes_per_env must be 0, 1, 2, 4, 8 or 16"); }
     st = cfg->precision == PD_F64 ? create_impl<double>(params, cfg, e) : create_impl<float>(params, cfg, e);
     if (st != PD_OK) { pd_destroy(e); return st; }
