@@ -113,10 +113,12 @@ PD_HD double tps(double r) { return r == 0.0 ? 0.0 : r * r * pd_log(r); }
 // the device library's double log.  Positive normal finite x; x = 0 gives a finite value.
 constexpr int kLogBits = 9, kLogCells = 1 << kLogBits;
 struct LogTable { double invc[kLogCells], logc[kLogCells]; };
-// The step kernel's hot-path log (eval_log, pd_physics.h): 1024 cells of (2 invc, -log(invc) -
-// ln 2), interleaved for one 16-byte LDS read, used with frexp's mantissa in [0.5, 1) and a
+// The step kernel's hot-path log (eval_log, pd_physics.h): 1024 cells of (2 invc, 4 (-log(invc) -
+// ln 2)), interleaved for one 16-byte LDS read, used with frexp's mantissa in [0.5, 1) and a
 // degree-4 log1p (|r| < 2^-11, truncation < 6e-18); same accuracy as log_tab (max 1.4e-15
-// absolute over [1e-6, 300] against long double, 2e7 arguments), fewer instructions.
+// absolute over [1e-6, 300] against long double, 2e7 arguments), fewer instructions.  The
+// second entry is scaled by 4 (exactly) so that the Horner steps run on 4 log1p and every FMA
+// has at most one non-inline constant (pd_physics.h log_cell_poly4).
 constexpr int kLogBitsD = 10, kLogCellsD = 1 << kLogBitsD;
 struct LogTableD { double cell[2 * kLogCellsD]; };
 inline void log_table_fill(LogTableD& t) {
@@ -124,7 +126,7 @@ inline void log_table_fill(LogTableD& t) {
         long double c = 1.0L + (i + 0.5L) / kLogCellsD;
         double invc = (double)(1.0L / c);
         t.cell[2 * i] = 2.0 * invc;
-        t.cell[2 * i + 1] = (double)(-logl((long double)invc) - logl(2.0L));
+        t.cell[2 * i + 1] = 4.0 * (double)(-logl((long double)invc) - logl(2.0L));
     }
 }
 inline void log_table_fill(LogTable& t) {

@@ -120,6 +120,19 @@ constexpr int kIsaCols = 8;
 // ds_read_b128 per log
 __shared__ __attribute__((aligned(16))) double s_logtab[2 * kLogCellsD];
 template <typename R> __device__ __forceinline__ R eval_log(R x);
+// 4 ((logc - ln2) + log1p(r)), r = m1 (2 invc) - 1, |r| <= 2^-11, c.y = 4 (logc - ln2): the
+// degree-4 series in Horner form scaled by 4 (exact), 4 log1p(r) = r (4 + r (-2 + r (4/3 - r))),
+// so that each step has one SGPR constant at most (4, -2 and -1 are inline operands): five
+// VALU operations, no constant moves
+__device__ __forceinline__ double log_cell_poly4(double m1, double2 c) {
+    const double r = fma(m1, c.x, -1.0);
+    const double t = fma(r, fma(r, 4.0 / 3.0 - r, -2.0), 4.0);
+    return fma(r, t, c.y);
+}
+// 4 log x (the RBF sums accumulate 4 d2 log d2 and scale once at the end)
+__device__ __forceinline__ double log4_from(int e1, double m1, double2 c) {
+    return fma((double)e1, 4.0 * 6.93147180559945286227e-01, log_cell_poly4(m1, c));
+}
 template <> __device__ __forceinline__ double eval_log<double>(double x) {
     // x = 2^e1 m1, m1 in [0.5, 1) (v_frexp_*); cell from the top 10 mantissa bits;
     // r = m1 (2 invc) - 1 = m invc - 1; log x = e1 ln2 + (logc - ln2) + log1p(r)
@@ -139,12 +152,7 @@ template <> __device__ __forceinline__ double eval_log<double>(double x) {
     const uint32_t off = (hi >> (16 - kLogBitsD)) & ((kLogCellsD - 1) << 4);   // cell * 16 bytes
 #endif
     const double2 c = *(const double2*)((const char*)s_logtab + off);
-    // log1p(r) = r + r^2 (r/3 - 1/2 - r^2/4): constants as SGPR / inline operands (no moves)
-    const double r = fma(m1, c.x, -1.0);
-    const double r2 = r * r;
-    const double t = fma(r2, -0.25, fma(r, 1.0 / 3.0, -0.5));
-    const double p = fma(r2, t, r);
-    return fma((double)e1, 6.93147180559945286227e-01, c.y + p);
+    return 0.25 * log4_from(e1, m1, c);
 }
 // eval_log<double> in two stages, so that a caller can issue the cell reads of several
 // arguments before finishing any of them (same arithmetic, same bits)
@@ -157,15 +165,22 @@ __device__ __forceinline__ LogPart log_start(double x) {
     q.c = *(const double2*)((const char*)s_logtab + ((hi >> (16 - kLogBitsD)) & ((kLogCellsD - 1) << 4)));
     return q;
 }
-__device__ __forceinline__ double log_finish(const LogPart& q) {
-    const double r = fma(q.m1, q.c.x, -1.0);
-    const double r2 = r * r;
-    const double t = fma(r2, -0.25, fma(r, 1.0 / 3.0, -0.5));
-    const double p = fma(r2, t, r);
-    return fma((double)q.e1, 6.93147180559945286227e-01, q.c.y + p);
-}
+// 4 log x
+__device__ __forceinline__ double log4_finish(const LogPart& q) { return log4_from(q.e1, q.m1, q.c); }
 template <> __device__ __forceinline__ float eval_log<float>(float x) {
     return __builtin_amdgcn_logf(x) * 0.693147180559945309f;
+}
+// 4 log x (the RBF term sums)
+template <typename R> __device__ __forceinline__ R eval_log4(R x);
+template <> __device__ __forceinline__ double eval_log4<double>(double x) {
+    const int e1 = __builtin_amdgcn_frexp_exp(x);
+    const double m1 = __builtin_amdgcn_frexp_mant(x);
+    const uint32_t hi = (uint32_t)(__double_as_longlong(x) >> 32);
+    const double2 c = *(const double2*)((const char*)s_logtab + ((hi >> (16 - kLogBitsD)) & ((kLogCellsD - 1) << 4)));
+    return log4_from(e1, m1, c);
+}
+template <> __device__ __forceinline__ float eval_log4<float>(float x) {
+    return __builtin_amdgcn_logf(x) * (4.0f * 0.693147180559945309f);
 }
 
 // ---------------------------------------------------------------- sine and cosine together

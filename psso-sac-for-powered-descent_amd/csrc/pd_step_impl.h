@@ -89,8 +89,9 @@ __device__ __forceinline__ R rbf_eval(const PD_AS1 R* __restrict__ pay, const R*
     const R2* pt = (const R2*)spt;
     const PD_AS1 uint32_t* iw = (const PD_AS1 uint32_t*)(pay + kPayIdx);
     R s0 = R(0), s1 = R(0);
-    // one term: c_j d2 log(d2) accumulated (the 1/2 of phi is applied once at the end); d2 = 0
-    // (query on a table point) contributes c_j * 0 * finite = 0, as do padding terms (c_j = 0)
+    // one term: c_j d2 4 log(d2) accumulated (the 1/8 = 1/2 of phi and 1/4 of eval_log4 is
+    // applied once at the end, exactly); d2 = 0 (query on a table point) contributes
+    // c_j * 0 * finite = 0, as do padding terms (c_j = 0)
     auto term = [&](R mj, R da2, R cj, bool second) {
         R dm = M - mj;
         R d2 = fma(dm, dm, da2);
@@ -98,9 +99,9 @@ __device__ __forceinline__ R rbf_eval(const PD_AS1 R* __restrict__ pay, const R*
 #ifdef PD_EXP_NOLOG
         R l = d2;
 #elif defined(PD_EXP_LIBLOG)
-        R l = log(d2 > R(0) ? d2 : R(1));
+        R l = R(4) * log(d2 > R(0) ? d2 : R(1));
 #else
-        R l = eval_log<R>(sizeof(R) == 8 ? d2 : (d2 > R(1e-30) ? d2 : R(1e-30)));
+        R l = eval_log4<R>(sizeof(R) == 8 ? d2 : (d2 > R(1e-30) ? d2 : R(1e-30)));
 #endif
         if (second) s1 = fma(w, l, s1); else s0 = fma(w, l, s0);
     };
@@ -159,7 +160,7 @@ __device__ __forceinline__ R rbf_eval(const PD_AS1 R* __restrict__ pay, const R*
 #pragma unroll
                 for (int k = 0; k < 10; ++k) {
                     const R wk = d2[k] * pp[k];
-                    if (k & 1) s1 = fma(wk, log_finish(lp[k]), s1); else s0 = fma(wk, log_finish(lp[k]), s0);
+                    if (k & 1) s1 = fma(wk, log4_finish(lp[k]), s1); else s0 = fma(wk, log4_finish(lp[k]), s0);
                 }
             } else
 #endif
@@ -197,7 +198,7 @@ __device__ __forceinline__ R rbf_eval(const PD_AS1 R* __restrict__ pay, const R*
             for (int u = 0; u < 5; ++u) slot(e[u], ao[u], c0[u], c1[u]);
         }
     }
-    R s = R(0.5) * (s0 + s1);
+    R s = R(0.125) * (s0 + s1);
     if (part == 0) {
         s += R(1) * pay[kPayPoly];
         s += (M - pay[kPaySS + 0]) / pay[kPaySS + 2] * pay[kPayPoly + 1];
@@ -768,9 +769,12 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
                 ev(a.b.wprof, ui) = (uint8_t)e.prof;
             }
         }
-        // neighbourhood caches survive resets (any valid 50-set is a correct start)
+        // neighbourhood caches survive resets (any valid 50-set is a correct start); the table
+        // row is laundered too (its 64-bit row offset would otherwise stay live from the loads)
+        int mt = my_table;
+        asm volatile("" : "+v"(mt));
         if (part == 0) {
-            ev(a.b.key + (my_table) * N, ui) = cA.key; ev(a.b.slot + (my_table) * N, ui) = cA.slot;
+            ev(a.b.key + (size_t)mt * (size_t)N, ui) = cA.key; ev(a.b.slot + (size_t)mt * (size_t)N, ui) = cA.slot;
             if constexpr (LPE == 1) { ev(a.b.key + N, ui) = cB.key; ev(a.b.slot + N, ui) = cB.slot; }
         }
     }
