@@ -14,21 +14,24 @@ constexpr int kCols = 5;            // AoA columns of each V2 table
 // window of consecutive table points (one column's Mach run) is cut into pairs (p, p + 1), an
 // odd window's last point padded with a zero-coefficient partner, so that one 16-byte LDS read
 // (the point table holds (Mach_p, Mach_p+1) per entry) serves two terms that share the
-// column's AoA.  50 points in <= 5 windows (an even number of them odd) fill <= 27 slots.
-//   [0, 54)   coefficients, slot k at 2k, 2k + 1 (zero for padding)
-//   [54, 57)  degree-1 polynomial coefficients
-//   [57, 61)  shift0, shift1, scale0, scale1
-//   [61, 70)  72 index bytes: per slot its entry (first point) and the column's integer AoA,
-//             see pair_entry_pos / pair_aoa_pos
-constexpr int kPairs = 27;
+// column's AoA.  50 points in <= 5 windows (an even number of them odd) fill <= 27 slots, padded
+// to 30 = six chunks of five slots (the evaluation unit, see rbf_eval / rbf_balanced).
+//   [0, 60)   coefficients, slot k at 2k, 2k + 1 (zero for padding)
+//   [60, 63)  degree-1 polynomial coefficients
+//   [63, 67)  shift0, shift1, scale0, scale1
+//   [67, 76)  72 index bytes: per slot its entry (first point) and the column's integer AoA,
+//             see pair_entry_pos / pair_aoa_pos (padding slots: entry 0, AoA 0)
+constexpr int kPairsUsed = 27;   // slots a neighbourhood can fill
+constexpr int kChunks = 6;       // chunks of five slots (ten terms) per payload
+constexpr int kPairs = 5 * kChunks;
 constexpr int kPayPoly = 2 * kPairs;
 constexpr int kPaySS = kPayPoly + 3;
 constexpr int kPayIdx = kPaySS + 4;
-constexpr int kPayIdxBytes = 72;
+constexpr int kPayIdxBytes = 12 * kChunks;
 constexpr int kPay = kPayIdx + kPayIdxBytes / 8;
 // Byte positions in the index area: slot 5c + u (chunk c of five) at 12c + 2u (entry) and
 // 12c + 2u + 1 (AoA), so that a chunk's ten bytes are one 12-byte (3-dword) load issued with its
-// ten coefficients; the last chunk (slots 25, 26) is padded to 12 bytes.
+// ten coefficients.
 PD_HD constexpr int pair_entry_pos(int k) { return 12 * (k / 5) + 2 * (k % 5); }
 PD_HD constexpr int pair_aoa_pos(int k) { return pair_entry_pos(k) + 1; }
 constexpr int kKeyLoBits = 6, kKeyLenBits = 6, kKeyField = kKeyLoBits + kKeyLenBits;
@@ -251,7 +254,7 @@ PD_HD int solve_neighbourhood(const double* mach, const double* coef, const int*
         }
         slot0 += (len[c] + 1) / 2;
     }
-    if (slot0 > kPairs) return -1;
+    if (slot0 > kPairsUsed) return -1;
     for (int j = 0; j < 3; ++j) payload[kPayPoly + j] = b[kNbr + j];
     payload[kPaySS + 0] = sh0; payload[kPaySS + 1] = sh1;
     payload[kPaySS + 2] = sc0; payload[kPaySS + 3] = sc1;
@@ -259,8 +262,8 @@ PD_HD int solve_neighbourhood(const double* mach, const double* coef, const int*
 }
 
 // Payload in a handle's precision: coefficients converted, index bytes copied.  Stride in R
-// units: kPay = 70 (binary64) or 80 (binary32: 61 values + 72 bytes = 18 floats + padding).
-template <typename R> constexpr int pay_stride() { return sizeof(R) == 8 ? kPay : 80; }
+// units: kPay = 76 (binary64) or 88 (binary32: 67 values + 72 bytes = 18 floats + padding).
+template <typename R> constexpr int pay_stride() { return sizeof(R) == 8 ? kPay : 88; }
 template <typename R> PD_HD void pay_store(const double* src, R* dst) {
     for (int j = 0; j < kPayIdx; ++j) dst[j] = (R)src[j];
     for (int j = kPayIdx; j < pay_stride<R>(); ++j) dst[j] = R(0);

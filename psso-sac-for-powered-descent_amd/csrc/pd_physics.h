@@ -20,6 +20,15 @@ template <> struct Cst<float> {
 };
 
 constexpr int kLineMax = 96;   // breakpoints per clamped query line
+// line search buckets: Mach [0, 10) in kLineBuckets; bucket b's breakpoint index range (lo, hi),
+// lo = #{bp < b w - 1e-4}, hi = #{bp < (b + 1) w + 1e-4}, packed lo | hi << 8
+constexpr int kLineBuckets = 128;
+// Taylor pieces of the clamped query lines (pdenv.hip build_taylor): Mach [0, 10] in kTayCells
+// uniform cells; a cell's piece for neighbourhood interval l is at line offset + cell + l.  A
+// piece: kTayDeg + 1 coefficients of the expansion at the cell centre, then kTayExact exact
+// terms (Mach, coefficient / 8, d_a^2) for the singularities nearest to the cell.
+constexpr int kTayCells = 2048, kTayDeg = 10, kTayExact = 2;
+constexpr int kTayStride = kTayDeg + 1 + 3 * kTayExact + 1;
 
 // Address spaces of the step kernel's memory: the per-handle parameter block is read through a
 // constant-address-space view (uniform fields become scalar loads into SGPRs), the tables behind
@@ -78,6 +87,10 @@ template <typename R> struct DevParams {
     // C_L at +-10): breakpoints in Mach, and the key/slot of each interval
     R line_a[4];
     int line_nbp[4];
+    uint16_t line_lb[4][kLineBuckets];
+    // Taylor pieces of the four lines in one array; tay_off[li]: the line's first piece, -1 none
+    const R* tay;
+    int tay_off[4];
     // 2-D candidate grids over the interior query domain (Mach x AoA-abscissa), one per table:
     // the key/slot of the 50-NN set at each cell centre
     int grid_nm[2], grid_na[2];
@@ -385,6 +398,11 @@ __device__ __forceinline__ int knn_windows(const R* smach, const PD_AS4 int* sta
     R dz[kCols];
 #pragma unroll
     for (int c = 0; c < kCols; ++c) { R da = a - aoa[c]; dz[c] = da * da; }
+    // each column's insertion point of M (lower_bound), searched the first time the column is
+    // needed empty (its nearest candidates are then points ins - 1 and ins); -1: not yet
+    int ins[kCols];
+#pragma unroll
+    for (int c = 0; c < kCols; ++c) ins[c] = -1;
     int it = 0;
     for (; it < 256; ++it) {
         R maxin = R(-1); int maxc = -1, maxi = 0;
@@ -406,8 +424,12 @@ __device__ __forceinline__ int knn_windows(const R* smach, const PD_AS4 int* sta
 #pragma unroll
         for (int c = 0; c < kCols; ++c) {
             if (len[c] == 0 && dz[c] < maxin) {
-                int l = 0, h = n[c];
-                while (l < h) { int mid = (l + h) >> 1; if (smach[2 * (start[c] + mid)] < M) l = mid + 1; else h = mid; }
+                if (ins[c] < 0) {
+                    int l = 0, h = n[c];
+                    while (l < h) { int mid = (l + h) >> 1; if (smach[2 * (start[c] + mid)] < M) l = mid + 1; else h = mid; }
+                    ins[c] = l;
+                }
+                const int l = ins[c];
                 if (l > 0) { R d = d2_at(smach, start[c], l - 1, M, dz[c]); if (d < minex) { minex = d; minc = c; mini = l - 1; } }
                 if (l < n[c]) { R d = d2_at(smach, start[c], l, M, dz[c]); if (d < minex) { minex = d; minc = c; mini = l; } }
             }

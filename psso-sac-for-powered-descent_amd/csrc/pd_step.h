@@ -21,7 +21,10 @@ constexpr int kPendingCap = 4096;     // device-solved neighbourhoods queued per
 constexpr int kSolveSlots = 1024;     // global-memory LU scratch slots (one per workgroup, modulo)
 constexpr int kGridExact = 1 << 30;   // grid_slot flag: every point of the cell has its key
 constexpr int kGridRefine = 1 << 29;  // grid_slot flag: the cell is refined, low bits = its sub-grid
-constexpr int kGridSub = 16;          // sub-cells per refined cell side
+#ifndef PD_GRID_SUB
+#define PD_GRID_SUB 8
+#endif
+constexpr int kGridSub = PD_GRID_SUB;   // sub-cells per refined cell side
 constexpr int kStats = 32;            // pend.stats words (see Stat)
 
 // pend.stats[] words

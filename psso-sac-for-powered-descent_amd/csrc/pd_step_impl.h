@@ -73,138 +73,165 @@ template <typename R> struct LineLds {
     unsigned long long key[4][kLineMax + 1];
     R a[4];
     int nbp[4];
+    int tay_off[4];
+    uint16_t lb[4][kLineBuckets];
 };
 
+// One chunk (five pair slots, ten terms) of sum_j c_j phi(|x - y_j|), phi(r) = r^2 log r =
+// d2 log(d2) / 2 with d2 = |x - y|^2 (thin_plate_spline, phi(0) = 0), times 8: the lane-
+// independent unit of every evaluation order below, so that its bits do not depend on which lane
+// computes it.  pp: the chunk's ten coefficients, w: its three index words.  Terms come in pair
+// slots (pd_common.h): one 16-byte LDS read gives the Mach values of a slot's two consecutive
+// table points, whose column AoA (an integer, in the slot's AoA byte) gives one d_a^2 for both.
+// Binary64 evaluates in phases (five pair reads, ten d2, ten log-cell reads, ten finishes) so
+// that the reads are in flight together and the ten log chains interleave.  d2 = 0 (query on a
+// table point) contributes c_j * 0 * finite = 0, as do padding terms (c_j = 0).
+template <typename R, typename R2>
+__device__ __forceinline__ R chunk_sum(const R pp[10], const uint32_t w[3], const R2* pt, R M, R a) {
+    R s0 = R(0), s1 = R(0);
+#ifndef PD_RBF_UNPHASED
+    if constexpr (sizeof(R) == 8) {
+        R2 v[5];
+        R da2[5];
+#pragma unroll
+        for (int u = 0; u < 5; ++u) {
+            const uint32_t h = w[u >> 1] >> (16 * (u & 1));
+            v[u] = pt[h & 0xffu];
+            const R da = a - (R)((h >> 8) & 0xffu);
+            da2[u] = da * da;
+        }
+        R d2[10];
+#pragma unroll
+        for (int u = 0; u < 5; ++u) {
+            const R dm0 = M - v[u].x, dm1 = M - v[u].y;
+            d2[2 * u] = fma(dm0, dm0, da2[u]);
+            d2[2 * u + 1] = fma(dm1, dm1, da2[u]);
+        }
+#ifdef PD_EXP_NOLOG
+#pragma unroll
+        for (int k = 0; k < 10; ++k) { if (k & 1) s1 = fma(d2[k] * pp[k], d2[k], s1); else s0 = fma(d2[k] * pp[k], d2[k], s0); }
+#else
+        LogPart lp[10];
+#pragma unroll
+        for (int k = 0; k < 10; ++k) lp[k] = log_start(d2[k]);
+#pragma unroll
+        for (int k = 0; k < 10; ++k) {
+            const R wk = d2[k] * pp[k];
+            if (k & 1) s1 = fma(wk, log4_finish(lp[k]), s1); else s0 = fma(wk, log4_finish(lp[k]), s0);
+        }
+#endif
+    } else
+#endif
+    {
+#pragma unroll
+        for (int u = 0; u < 5; ++u) {
+            const uint32_t h = w[u >> 1] >> (16 * (u & 1));
+            const R2 v = pt[h & 0xffu];
+            const R da = a - (R)((h >> 8) & 0xffu);
+            const R da2 = da * da;
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const R dm = M - (i ? v.y : v.x);
+                const R d2 = fma(dm, dm, da2);
+#ifdef PD_EXP_NOLOG
+                const R l = d2;
+#else
+                const R l = eval_log4<R>(sizeof(R) == 8 ? d2 : (d2 > R(1e-30) ? d2 : R(1e-30)));
+#endif
+                if (i) s1 = fma(d2 * pp[2 * u + 1], l, s1); else s0 = fma(d2 * pp[2 * u], l, s0);
+            }
+        }
+    }
+    return s0 + s1;
+}
+
+// The payload's degree-1 polynomial added to the scaled kernel sum (the same order everywhere);
+// f: the payload's fields [kPayPoly, kPayPoly + 7) (poly coefficients, shifts, scales)
+template <typename R>
+__device__ __forceinline__ R rbf_finish_f(const R f[7], R tot, R M, R a) {
+    R s = R(0.125) * tot;
+    s += R(1) * f[0];
+    s += (M - f[3]) / f[5] * f[1];
+    s += (a - f[4]) / f[6] * f[2];
+    return s;
+}
+template <typename R>
+__device__ __forceinline__ R rbf_finish(const PD_AS1 R* __restrict__ pay, R tot, R M, R a) {
+    R f[7];
+#pragma unroll
+    for (int u = 0; u < 7; ++u) f[u] = pay[kPayPoly + u];
+    return rbf_finish_f<R>(f, tot, M, a);
+}
+
 // This lane's share of sum_j c_j phi(|x - y_j|) + poly of one neighbourhood payload.
-// phi(r) = r^2 log r = d2 log(d2) / 2 with d2 = |x - y|^2 (thin_plate_spline, phi(0) = 0).
-// Terms come in pair slots (pd_common.h): one 16-byte LDS read gives the Mach values of a slot's
-// two consecutive table points, whose column AoA (an integer, in the slot's AoA byte) gives one
-// d_a^2 for both.  Slots are evaluated in chunks of five (ten terms) so that a chunk's LDS reads
-// are in flight together and its ten log chains interleave; the next chunk's coefficients and
-// index bytes are requested one chunk ahead.
+// nparts = 1 (the lane owns the query): the six chunks in order, each chunk_sum'd, the next
+// chunk's coefficients and index words requested before the current one computes; the same
+// bits as rbf_balanced's distributed evaluation.  nparts > 1 (LPE >= 4): the lane's slots are
+// part, part + nparts, ... (summed by the caller's shuffles).
 template <typename R>
 __device__ __forceinline__ R rbf_eval(const PD_AS1 R* __restrict__ pay, const R* spt, R M, R a,
                                       int part, int nparts) {
     using R2 = typename std::conditional<sizeof(R) == 8, double2, float2>::type;
     const R2* pt = (const R2*)spt;
     const PD_AS1 uint32_t* iw = (const PD_AS1 uint32_t*)(pay + kPayIdx);
-    R s0 = R(0), s1 = R(0);
-    // one term: c_j d2 4 log(d2) accumulated (the 1/8 = 1/2 of phi and 1/4 of eval_log4 is
-    // applied once at the end, exactly); d2 = 0 (query on a table point) contributes
-    // c_j * 0 * finite = 0, as do padding terms (c_j = 0)
-    auto term = [&](R mj, R da2, R cj, bool second) {
-        R dm = M - mj;
-        R d2 = fma(dm, dm, da2);
-        R w = d2 * cj;
-#ifdef PD_EXP_NOLOG
-        R l = d2;
-#elif defined(PD_EXP_LIBLOG)
-        R l = R(4) * log(d2 > R(0) ? d2 : R(1));
-#else
-        R l = eval_log4<R>(sizeof(R) == 8 ? d2 : (d2 > R(1e-30) ? d2 : R(1e-30)));
-#endif
-        if (second) s1 = fma(w, l, s1); else s0 = fma(w, l, s0);
-    };
-    // one slot: entry byte e (its two Mach values), AoA byte ao, coefficients c0, c1
-    auto slot = [&](uint32_t e, uint32_t ao, R c0, R c1) {
-        const R2 v = pt[e];
-        const R da = a - (R)ao;
-        const R da2 = da * da;
-        term(v.x, da2, c0, false);
-        term(v.y, da2, c1, true);
-    };
     if (nparts == 1) {
-        // The lane owns all 27 slots: five rolled chunks of five slots, chunk c + 1's ten
-        // coefficients and 12 index bytes requested before chunk c computes; slots 25, 26 end it.
-        auto bytes = [&](int c, uint32_t w[3]) {
-            const PD_AS1 uint32_t* q = iw + 3 * c;
-            w[0] = q[0]; w[1] = q[1]; w[2] = q[2];
-        };
         R pn[10];
         uint32_t wn[3];
 #pragma unroll
         for (int u = 0; u < 10; ++u) pn[u] = pay[u];
-        bytes(0, wn);
-#ifndef PD_CHUNK_UNROLL
-#define PD_CHUNK_UNROLL 1
+#pragma unroll
+        for (int u = 0; u < 3; ++u) wn[u] = iw[u];
+        R tot = R(0);
+#ifndef PD_EXP_CHUNKS   // experiment: fewer chunks per query (wrong values; timing bound)
+#define PD_EXP_CHUNKS kChunks
 #endif
-#pragma unroll PD_CHUNK_UNROLL
-        for (int c = 0; c < 5; ++c) {
-            R pp[10];
-            uint32_t w[3] = {wn[0], wn[1], wn[2]};
-#pragma unroll
-            for (int u = 0; u < 10; ++u) { pp[u] = pn[u]; pn[u] = pay[10 * c + 10 + u]; }
-            bytes(c + 1, wn);
-#ifndef PD_RBF_UNPHASED
-            if constexpr (sizeof(R) == 8) {
-                // the chunk in phases: five pair reads, ten d2, ten log-cell reads, ten finishes
-                R2 v[5];
-                R da2[5];
-#pragma unroll
-                for (int u = 0; u < 5; ++u) {
-                    const uint32_t h = w[u >> 1] >> (16 * (u & 1));
-                    v[u] = pt[h & 0xffu];
-                    const R da = a - (R)((h >> 8) & 0xffu);
-                    da2[u] = da * da;
-                }
-                R d2[10];
-#pragma unroll
-                for (int u = 0; u < 5; ++u) {
-                    const R dm0 = M - v[u].x, dm1 = M - v[u].y;
-                    d2[2 * u] = fma(dm0, dm0, da2[u]);
-                    d2[2 * u + 1] = fma(dm1, dm1, da2[u]);
-                }
-                LogPart lp[10];
-#pragma unroll
-                for (int k = 0; k < 10; ++k) lp[k] = log_start(d2[k]);
-#pragma unroll
-                for (int k = 0; k < 10; ++k) {
-                    const R wk = d2[k] * pp[k];
-                    if (k & 1) s1 = fma(wk, log4_finish(lp[k]), s1); else s0 = fma(wk, log4_finish(lp[k]), s0);
-                }
-            } else
-#endif
-            {
-#pragma unroll
-            for (int u = 0; u < 5; ++u) {
-                const uint32_t h = w[u >> 1] >> (16 * (u & 1));
-                slot(h & 0xffu, (h >> 8) & 0xffu, pp[2 * u], pp[2 * u + 1]);
-            }
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            const uint32_t h = wn[0] >> (16 * u);
-            slot(h & 0xffu, (h >> 8) & 0xffu, pn[2 * u], pn[2 * u + 1]);
-        }
-    } else {
-        // LPE >= 4: the lane's slots are part, part + nparts, ...
-        const PD_AS1 uint8_t* ib = (const PD_AS1 uint8_t*)iw;
 #pragma unroll 1
-        for (int k0 = part; k0 < kPairs; k0 += 5 * nparts) {
-            uint32_t e[5], ao[5];
-            R c0[5], c1[5];
+        for (int c = 0; c < PD_EXP_CHUNKS; ++c) {
+            R pp[10];
+            uint32_t w[3];
+            const int cn = c + 1 < kChunks ? c + 1 : c;   // (the last chunk reloads itself)
 #pragma unroll
-            for (int u = 0; u < 5; ++u) {
-                const int k = k0 + u * nparts;
-                const bool ok = k < kPairs;
-                const int kk = ok ? k : 0;
-                e[u] = ib[pair_entry_pos(kk)];
-                ao[u] = ib[pair_aoa_pos(kk)];
-                c0[u] = ok ? pay[2 * kk] : R(0);
-                c1[u] = ok ? pay[2 * kk + 1] : R(0);
+            for (int u = 0; u < 10; ++u) { pp[u] = pn[u]; pn[u] = pay[10 * cn + u]; }
+#pragma unroll
+            for (int u = 0; u < 3; ++u) { w[u] = wn[u]; wn[u] = iw[3 * cn + u]; }
+            const R cs = chunk_sum<R, R2>(pp, w, pt, M, a);
+            tot = c == 0 ? cs : tot + cs;
+        }
+        return rbf_finish<R>(pay, tot, M, a);
+    }
+    // LPE >= 4: this lane's slots (its terms accumulated as in a chunk: even / odd)
+    const PD_AS1 uint8_t* ib = (const PD_AS1 uint8_t*)iw;
+    R s0 = R(0), s1 = R(0);
+#pragma unroll 1
+    for (int k0 = part; k0 < kPairsUsed; k0 += 5 * nparts) {
+        uint32_t e[5], ao[5];
+        R c0[5], c1[5];
+#pragma unroll
+        for (int u = 0; u < 5; ++u) {
+            const int k = k0 + u * nparts;
+            const bool ok = k < kPairsUsed;
+            const int kk = ok ? k : 0;
+            e[u] = ib[pair_entry_pos(kk)];
+            ao[u] = ib[pair_aoa_pos(kk)];
+            c0[u] = ok ? pay[2 * kk] : R(0);
+            c1[u] = ok ? pay[2 * kk + 1] : R(0);
+        }
+#pragma unroll
+        for (int u = 0; u < 5; ++u) {
+            const R2 v = pt[e[u]];
+            const R da = a - (R)ao[u];
+            const R da2 = da * da;
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const R dm = M - (i ? v.y : v.x);
+                const R d2 = fma(dm, dm, da2);
+                const R l = eval_log4<R>(sizeof(R) == 8 ? d2 : (d2 > R(1e-30) ? d2 : R(1e-30)));
+                if (i) s1 = fma(d2 * c1[u], l, s1); else s0 = fma(d2 * c0[u], l, s0);
             }
-#pragma unroll
-            for (int u = 0; u < 5; ++u) slot(e[u], ao[u], c0[u], c1[u]);
         }
     }
-    R s = R(0.125) * (s0 + s1);
-    if (part == 0) {
-        s += R(1) * pay[kPayPoly];
-        s += (M - pay[kPaySS + 0]) / pay[kPaySS + 2] * pay[kPayPoly + 1];
-        s += (a - pay[kPaySS + 1]) / pay[kPaySS + 3] * pay[kPayPoly + 2];
-    }
-    return s;
+    if (part == 0) return rbf_finish<R>(pay, s0 + s1, M, a);
+    return R(0.125) * (s0 + s1);
 }
 
 // Orders this wave's global-memory accesses (the solve scratch is written and read back by the
@@ -325,7 +352,7 @@ __device__ __forceinline__ void solve_wave(DP<R>& P, int table, unsigned long lo
     PD_AS1 R* pr = (PD_AS1 R*)work;
     for (int j = lane; j < pay_stride<R>(); j += 64) pr[j] = j < kPayIdx ? (R)pay[j] : R(0);
     wave_mem_sync();
-    if (lane < kPayIdxBytes) ((PD_AS1 uint8_t*)(pr + kPayIdx))[lane] = ib[lane];
+    for (int j = lane; j < kPayIdxBytes; j += 64) ((PD_AS1 uint8_t*)(pr + kPayIdx))[j] = ib[j];
     wave_mem_sync();
 }
 
@@ -378,16 +405,58 @@ __device__ __forceinline__ R rbf_miss_wave(const StepArgs<R>& a, DP<R>& P, int t
 // breakpoints in LDS); elsewhere the interior grid cell's, or the env's cached set.  Unless the
 // candidate is trusted (strictly inside its interval/exact cell) it is VERIFIED (and repaired by
 // the swap search) against the exact distances before it is used.
-template <typename R>
+// A query's Taylor piece on a clamped line (rbf2): its record index and cell, piece < 0: none
+struct TayRef { int piece, cell; };
+
+struct NoPre { __device__ void operator()() const {} };
+
+// pre(): the caller's work that does not depend on the tables, run while the grid loads are in
+// flight
+template <typename R, typename Pre = NoPre>
 __device__ __forceinline__ int rbf_lookup(const StepArgs<R>& a, DP<R>& P, int table, const TabView<R>& t,
-                                          const LineLds<R>& ln, RbfCache<R>& cache, R M, R aq) {
+                                          const LineLds<R>& ln, RbfCache<R>& cache, R M, R aq,
+                                          TayRef* tay = nullptr, unsigned long long* st = nullptr,
+                                          Pre&& pre = Pre()) {
+#ifdef PD_STAMP
+    unsigned long long ts0 = __builtin_amdgcn_s_memtime();
+#define PD_LST(k) if (st) { const unsigned long long ts1 = __builtin_amdgcn_s_memtime(); st[k] += ts1 - ts0; ts0 = ts1; }
+#else
+#define PD_LST(k)
+#endif
     unsigned long long ckey = cache.key;
     int cslot = cache.slot;
     int li = aq == ln.a[t.line0] ? t.line0 : (aq == ln.a[t.line0 + 1] ? t.line0 + 1 : -1);
     bool trusted = false;
-    if (li >= 0 && ln.nbp[li] >= 0) {
+    const bool on_line = li >= 0 && ln.nbp[li] >= 0;
+    // the interior grid cell's candidate is requested by every lane first (its global loads are
+    // in flight during the line search; lanes on a line discard it)
+    unsigned long long gkey = 0ull;
+    int gsl0 = -1;
+    R um = R(0), ua = R(0);
+#ifdef PD_EXP_NOGRID   // experiment: interior queries verify the cached key (no grid)
+    const bool use_grid = false;
+#else
+    const bool use_grid = t.grid_key != nullptr;
+#endif
+    if (use_grid) {
+        R fm = M * t.grid_inv_dm, fa = (aq - t.grid_a0) * t.grid_inv_da;
+        int im = fm < R(0) ? 0 : (fm >= R(t.grid_nm) ? t.grid_nm - 1 : (int)fm);
+        int ia = fa < R(0) ? 0 : (fa >= R(t.grid_na) ? t.grid_na - 1 : (int)fa);
+        if (!(fm == fm) || !(fa == fa)) { im = 0; ia = 0; }   // NaN queries
+        const int cell = im * t.grid_na + ia;
+        gkey = t.grid_key[cell];
+        gsl0 = t.grid_slot[cell];
+        um = fm - (R)im; ua = fa - (R)ia;     // position in the cell, [0, 1)
+    }
+    pre();
+    if (on_line) {
         const int nb = ln.nbp[li];
-        int l = 0, h = nb;
+        // lower_bound of M over the breakpoints, within the bucket's range
+        int bk = (int)(M * R(kLineBuckets / 10.0));
+        bk = bk < 0 ? 0 : (bk > kLineBuckets - 1 ? kLineBuckets - 1 : bk);
+        const uint32_t rg = ln.lb[li][bk];
+        int l = (int)(rg & 0xffu), h = (int)(rg >> 8);
+        if (!(M >= R(0) && M < R(10))) { l = 0; h = nb; }   // (outside the buckets: whole line)
         while (l < h) { int mid = (l + h) >> 1; if (ln.bp[li][mid] < M) l = mid + 1; else h = mid; }
         ckey = ln.key[li][l];
         cslot = ln.slot[li][l];
@@ -398,15 +467,17 @@ __device__ __forceinline__ int rbf_lookup(const StepArgs<R>& a, DP<R>& P, int ta
         const R blo = l > 0 ? ln.bp[li][l - 1] : R(-1);
         const R bhi = l < nb ? ln.bp[li][l] : R(1e30);
         trusted = cslot >= 0 && (M - blo > eps) && (bhi - M > eps);
-    } else if (t.grid_key) {
-        R fm = M * t.grid_inv_dm, fa = (aq - t.grid_a0) * t.grid_inv_da;
-        int im = fm < R(0) ? 0 : (fm >= R(t.grid_nm) ? t.grid_nm - 1 : (int)fm);
-        int ia = fa < R(0) ? 0 : (fa >= R(t.grid_na) ? t.grid_na - 1 : (int)fa);
-        if (!(fm == fm) || !(fa == fa)) { im = 0; ia = 0; }   // NaN queries
-        int cell = im * t.grid_na + ia;
-        ckey = t.grid_key[cell];
-        int gsl = t.grid_slot[cell];
-        R um = fm - (R)im, ua = fa - (R)ia;     // position in the cell, [0, 1)
+        if (tay != nullptr && trusted && ln.tay_off[li] >= 0) {
+            // strictly inside interval l: the piece of (cell, l), Mach in [0, 10]
+            int cell = (int)(M * R(kTayCells / 10.0));
+            cell = cell < 0 ? 0 : (cell > kTayCells - 1 ? kTayCells - 1 : cell);
+            tay->piece = ln.tay_off[li] + cell + l;
+            tay->cell = cell;
+        }
+        PD_LST(0);
+    } else if (use_grid) {
+        ckey = gkey;
+        int gsl = gsl0;
         if (sizeof(R) != 8 && gsl >= 0 && (gsl & kGridRefine)) gsl = -1;   // centre key, verified
         if (sizeof(R) == 8 && gsl >= 0 && (gsl & kGridRefine)) {
             // a cell that straddles neighbourhood regions: its sub-cell (binary64 handles; the
@@ -427,6 +498,7 @@ __device__ __forceinline__ int rbf_lookup(const StepArgs<R>& a, DP<R>& P, int ta
         const R eps = sizeof(R) == 8 ? R(1e-9) : R(1e-4);
         trusted = gsl >= 0 && (gsl & kGridExact) && um > eps && R(1) - um > eps && ua > eps && R(1) - ua > eps;
     }
+    PD_LST(1);
     unsigned long long key = ckey;
     int slot = cslot;
 #ifdef PD_EXP_COUNT
@@ -461,6 +533,7 @@ __device__ __forceinline__ int rbf_lookup(const StepArgs<R>& a, DP<R>& P, int ta
         atomicAdd(&a.pend.stats[7], (unsigned long long)(check_trusted && key != ckey));
 #endif
     }
+    PD_LST(2);
     if (slot < 0) {
         uint32_t mask = (1u << t.logcap) - 1u;
         uint32_t h = key_hash(key, t.logcap);
@@ -471,6 +544,8 @@ __device__ __forceinline__ int rbf_lookup(const StepArgs<R>& a, DP<R>& P, int ta
             h = (h + 1) & mask;
         }
     }
+    PD_LST(3);
+#undef PD_LST
     cache.key = key;
     cache.slot = slot;
     return slot;
@@ -490,6 +565,165 @@ __device__ __forceinline__ R rbf(const StepArgs<R>& a, DP<R>& P, int table, cons
     if (__ballot(slot < 0)) {
         R mv = rbf_miss_wave<R>(a, P, table, t.smach, key, M, aq, part, nparts, slot < 0);
         if (slot < 0) val = mv;
+    }
+    return val;
+}
+
+// ---------------------------------------------------------------- LPE 2: Taylor lines + balanced sums
+// A clamped-line query's value from its Taylor piece (pdenv.hip build_taylor): the degree-
+// kTayDeg polynomial in M - (cell centre) plus the piece's exact terms.
+template <typename R>
+__device__ __forceinline__ R taylor_eval(const PD_AS1 R* __restrict__ rec, R M, int cell) {
+    const R w = R(10.0 / kTayCells);
+    const R t = M - fma((R)cell, w, R(0.5) * w);
+    R c[kTayStride - 1];
+#pragma unroll
+    for (int n = 0; n < kTayStride - 1; ++n) c[n] = rec[n];
+    R f = c[kTayDeg];
+#pragma unroll
+    for (int n = kTayDeg - 1; n >= 0; --n) f = fma(f, t, c[n]);
+#pragma unroll
+    for (int e = 0; e < kTayExact; ++e) {
+        const R* x = c + kTayDeg + 1 + 3 * e;
+        const R dm = M - x[0];
+        const R d2 = fma(dm, dm, x[2]);
+        f = fma(x[1] * d2, eval_log4<R>(sizeof(R) == 8 ? d2 : (d2 > R(1e-30) ? d2 : R(1e-30))), f);
+    }
+    return f;
+}
+
+// Per-wave LDS of the balanced evaluation: the wave's payload queries by rank (Mach, AoA
+// abscissa, table << 31 | slot) and the chunk sums of each
+template <typename R> struct BalLds {
+    alignas(16) R part[kChunks * 64];
+    R qm[64];
+    R qa[64];
+    unsigned long long qp[64];   // payload address | table (bit 0)
+};
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
+// The payload sums of the wave's lanes with `mine` set, spread over all 64 lanes: the n queries'
+// 6n chunks are numbered g = 6 rank + c and lane L computes chunks L, L + 64, ... (ceil(6n / 64)
+// rounds instead of six per query); each chunk_sum goes to LDS and the query's lane adds its six
+// in order -- the bits of rbf_eval (nparts = 1), whichever lanes computed the chunks.  `mid` runs
+// once the first round's loads are in flight (the caller's own latency-bound work overlaps
+// them).  Called by the converged wave.
+template <typename R, typename Mid>
+__device__ __forceinline__ R rbf_balanced(DP<R>& P, BalLds<R>& B, const R* tab, bool mine, int table, int slot,
+                                          R M, R aq, Mid&& mid) {
+    using R2 = typename std::conditional<sizeof(R) == 8, double2, float2>::type;
+    const unsigned long long mask = __ballot(mine);
+    if (mask == 0ull) { mid(); return R(0); }
+    const int lane = (int)__lane_id();
+    const int n = __popcll(mask);
+    const int rank = __popcll(mask & ((1ull << lane) - 1ull));
+    const PD_AS1 R* pcd = gbl(P.pay_cd);
+    const PD_AS1 R* pcl = gbl(P.pay_cl);
+    const PD_AS1 R* own = (table ? pcl : pcd) + (size_t)(mine ? slot : 0) * pay_stride<R>();
+    if (mine) { B.qm[rank] = M; B.qa[rank] = aq; B.qp[rank] = (unsigned long long)(uint64_t)own | (unsigned long long)table; }
+    wave_lds_sync();
+    const int total = kChunks * n;
+    const int K = (total + 63) >> 6;
+    // chunk g's coefficients / index words / point table / query
+    struct Buf { R pp[10]; uint32_t w[3]; const R2* pt; R M, a; };
+    auto fetch = [&](int g, Buf& b) {
+        const int gc = g < total ? g : total - 1;
+        const int r = gc / kChunks, c = gc - kChunks * r;
+        const unsigned long long q = B.qp[r];
+        b.M = B.qm[r]; b.a = B.qa[r];
+        const PD_AS1 R* pay = (const PD_AS1 R*)(uint64_t)(q & ~1ull) + 10 * c;
+        const PD_AS1 uint32_t* iw = (const PD_AS1 uint32_t*)(pay + (kPayIdx - 10 * c)) + 3 * c;
+#pragma unroll
+        for (int u = 0; u < 10; ++u) b.pp[u] = pay[u];
+#pragma unroll
+        for (int u = 0; u < 3; ++u) b.w[u] = iw[u];
+        b.pt = (const R2*)(tab + ((q & 1ull) ? 512 : 0));
+    };
+    auto run = [&](int g, const Buf& b) {
+        const R cs = chunk_sum<R, R2>(b.pp, b.w, b.pt, b.M, b.a);
+        if (g < total) B.part[g] = cs;
+    };
+    Buf b0, b1;
+    fetch(lane, b0);
+    R pf[7];   // the own query's polynomial fields, requested with the first round
+#pragma unroll
+    for (int u = 0; u < 7; ++u) pf[u] = own[kPayPoly + u];
+    mid();
+    // two rounds per trip, ping-pong buffers: each round's loads are requested one round early
+#pragma unroll 1
+    for (int k = 0; k < K; k += 2) {
+        const int g = (k << 6) + lane;
+        fetch(k + 1 < K ? g + 64 : g, b1);
+        run(g, b0);
+        if (k + 1 < K) {
+            fetch(k + 2 < K ? g + 128 : g + 64, b0);
+            run(g + 64, b1);
+        }
+    }
+    wave_lds_sync();
+    R val = R(0);
+    if (mine) {
+        const R* pr = B.part + kChunks * rank;
+        R tot = pr[0];
+#pragma unroll
+        for (int c = 1; c < kChunks; ++c) tot = tot + pr[c];
+        val = rbf_finish_f<R>(pf, tot, M, aq);
+    }
+    wave_lds_sync();   // (B is reused by the next call)
+    return val;
+}
+
+// rbf() for LPE 2 (one query per lane): trusted clamped-line queries from their Taylor piece,
+// the other table hits by the balanced payload sums, misses by the cooperative solve (whose
+// evaluation, rbf_eval, has the balanced sums' bits).  Lanes with act = false (past the batch,
+// frozen policy envs) only take part.
+template <typename R, typename Pre>
+__device__ __forceinline__ R rbf2(const StepArgs<R>& a, DP<R>& P, int table, const TabView<R>& t, const LineLds<R>& ln,
+                                  RbfCache<R>& cache, R M, R aq, bool act, BalLds<R>& B, const R* tab,
+                                  Pre&& pre, unsigned long long* stamp = nullptr) {
+#ifdef PD_STAMP
+    const unsigned long long s0 = __builtin_amdgcn_s_memtime();
+#endif
+    TayRef tr{-1, 0};
+    const int slot = rbf_lookup<R>(a, P, table, t, ln, cache, M, aq, &tr, stamp ? stamp + 2 : nullptr, pre);
+#ifdef PD_STAMP
+    const unsigned long long s1 = __builtin_amdgcn_s_memtime();
+    stamp[0] += s1 - s0;
+#endif
+#ifndef PD_EXP_NOTAYLOR
+    const bool tay = act && tr.piece >= 0;
+#else
+    const bool tay = false;
+#endif
+    const bool full = act && !tay && slot >= 0;
+    R vt = R(0);
+    const R vb = rbf_balanced<R>(P, B, tab, full, table, slot, M, aq, [&]() {
+        if (tay) vt = taylor_eval<R>(gbl(P.tay) + (size_t)tr.piece * kTayStride, M, tr.cell);
+    });
+    R val = full ? vb : vt;
+#ifdef PD_STAMP
+    const unsigned long long s2 = __builtin_amdgcn_s_memtime();
+    stamp[1] += s2 - s1;
+#endif
+    const bool miss = act && !tay && slot < 0;
+#ifdef PD_EXP_BALCOUNT   // experiment: Taylor / balanced / miss lanes, balanced rounds, calls
+    {
+        const unsigned long long mt = __ballot(tay), mf = __ballot(full), mm = __ballot(miss);
+        if (__lane_id() == 0) {
+            atomicAdd(&a.pend.stats[17], (unsigned long long)__popcll(mt));
+            atomicAdd(&a.pend.stats[18], (unsigned long long)__popcll(mf));
+            atomicAdd(&a.pend.stats[19], (unsigned long long)__popcll(mm));
+            atomicAdd(&a.pend.stats[20], (unsigned long long)((kChunks * __popcll(mf) + 63) >> 6));
+            atomicAdd(&a.pend.stats[21], 1ull);
+        }
+    }
+#endif
+    if (__ballot(miss)) {
+        R mv = rbf_miss_wave<R>(a, P, table, t.smach, cache.key, M, aq, 0, 1, miss);
+        if (miss) val = mv;
     }
     return val;
 }
@@ -573,7 +807,7 @@ __device__ __forceinline__ void actor_forward(const float* __restrict__ W, int64
 #endif
 
 // ---------------------------------------------------------------- LDS of one step workgroup
-template <typename R, bool WIND, int EPB> struct StepLds {
+template <typename R, bool WIND, int EPB, bool BAL = false> struct StepLds {
     // table points as (Mach_p, Mach_p+1) entries, C_D's 256 then C_L's: one 16-byte LDS read per
     // payload pair slot (smach[2p] is point p's Mach for the neighbourhood search)
     alignas(16) R tab[1024];
@@ -583,6 +817,7 @@ template <typename R, bool WIND, int EPB> struct StepLds {
     R wsp[WIND ? 800 : 1];
     LineLds<R> lines;
     R gwin[10][EPB];              // the g-load ring of each env of the workgroup (register-resident launches)
+    BalLds<R> bal[BAL ? kStepBlock / 64 : 1];   // LPE 2: per-wave balanced-sum space
 };
 
 template <typename R>
@@ -620,9 +855,9 @@ template <typename R, int PHASE, int RTD, bool WIND, int LPE, int POL = 0>
 #endif
 __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_WPE))) void k_step(StepArgs<R> a) {
     constexpr int EPB = kStepBlock / LPE;   // envs per workgroup
-    __shared__ StepLds<R, WIND, EPB> L;
+    __shared__ StepLds<R, WIND, EPB, LPE == 2> L;
 #ifdef PD_STAMP
-    unsigned long long acc_[7] = {0, 0, 0, 0, 0, 0, 0};
+    unsigned long long acc_[17] = {};   // [7], [8]: rbf2 lookup, evaluation; [9..12] lookup parts; [13..16] post-aero parts
 #endif
     PD_T(t_start);
     // envs this launch steps: all N, or (POL) the compacted live list; a workgroup past its end
@@ -662,7 +897,11 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
             (&L.lines.slot[0][0])[t] = (&P.line_slot[0][0])[t];
             (&L.lines.key[0][0])[t] = (&P.line_key[0][0])[t];
         }
-        if (threadIdx.x < 4) { L.lines.a[threadIdx.x] = P.line_a[threadIdx.x]; L.lines.nbp[threadIdx.x] = P.line_nbp[threadIdx.x]; }
+        if (threadIdx.x < 4) {
+            L.lines.a[threadIdx.x] = P.line_a[threadIdx.x]; L.lines.nbp[threadIdx.x] = P.line_nbp[threadIdx.x];
+            L.lines.tay_off[threadIdx.x] = P.tay_off[threadIdx.x];
+        }
+        for (int t = threadIdx.x; t < 4 * kLineBuckets; t += kStepBlock) (&L.lines.lb[0][0])[t] = (&P.line_lb[0][0])[t];
         for (int t = threadIdx.x; t < 2 * kLogCellsD; t += kStepBlock) {
             s_logtab[t] = P.logtab_d.cell[t];
         }
@@ -855,6 +1094,39 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
         // alpha_effective (rockets_physics.py:498-501) and Mach feed the aero tables; what the
         // tables do not need is computed after them (fewer values live across the RBF)
         R ae = (vy < R(0)) ? ga - th - Cst<R>::pi : al;
+        // the horizontal wind and the gust filters (no table dependence): with LPE 2 run while
+        // the aero lookup's grid loads are in flight, else after the tables
+        R ug = R(0), vg = R(0);
+        auto wind_block = [&]() {
+            if constexpr (WIND) {
+                // WindModel.__call__ (full_wind_model.py:35-43)
+                const R* walt = L.walt + e.prof * 16;
+                const R* wsp = L.wsp + e.prof * 16;
+                R km = y / R(1000);
+                int wn = P.wind_n[e.prof];
+                ug = np_interp<R>(walt, wsp, wn, km);
+                if (y < P.vk_y_threshold && a.stochastic) {
+                    double w0, w1;
+                    if (a.noise) { w0 = ev(a.noise + 2 * sub, ui * 8); w1 = ev(a.noise + 2 * sub + 1, ui * 8); }
+                    else {
+                        // vonkarman.py:34: one np.random.randn() per filter step, u then v (gauss_pair:
+                        // Philox counter (env, episode, step, sub-step), reproducible by the oracle)
+                        u32x4 r = philox({(uint32_t)g, (uint32_t)(g >> 32) ^ e.ep, e.ts, kTagWindSub + (uint32_t)sub},
+                                         a.seed_lo, a.seed_hi);
+                        gauss_pair(r, (const double*)(uint64_t)&P.logtab.invc[0], (const double*)(uint64_t)&P.logtab.logc[0], w0, w1);
+                    }
+                    // vonkarman.py:33-36: state = Ad @ state + Bd * w  (Bd = sigma * Bd(sigma=1))
+                    R n0 = (P.vk_Ad_u[0] * e.fu0 + P.vk_Ad_u[1] * e.fu1) + (e.sgu * P.vk_Bd_u[0]) * (R)w0;
+                    R n1 = (P.vk_Ad_u[2] * e.fu0 + P.vk_Ad_u[3] * e.fu1) + (e.sgu * P.vk_Bd_u[1]) * (R)w0;
+                    e.fu0 = n0; e.fu1 = n1;
+                    n0 = (P.vk_Ad_v[0] * e.fv0 + P.vk_Ad_v[1] * e.fv1) + (e.sgv * P.vk_Bd_v[0]) * (R)w1;
+                    n1 = (P.vk_Ad_v[2] * e.fv0 + P.vk_Ad_v[3] * e.fv1) + (e.sgv * P.vk_Bd_v[1]) * (R)w1;
+                    e.fv0 = n0; e.fv1 = n1;
+                    ug = ug + e.fu1;
+                    vg = e.fv1;
+                }
+            }
+        };
         R CL = R(0), CD = R(0);
         PD_T(t_aero0);
         PD_ACC(2, t_aero0 - t_sub);
@@ -874,8 +1146,17 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
                 CL = (!have || cl_zero) ? R(0) : (cl_sgn < R(0) ? -v : v);
                 CD = have ? w : R(0);
             } else {
-                R v = rbf<R>(a, P, my_table, tab_view<R>(P, L.tab, my_table), L.lines, cA, mach,
-                             my_table ? aq_cl : aq_cd, part, nparts);
+                R v;
+                if constexpr (LPE == 2)
+                    v = rbf2<R>(a, P, my_table, tab_view<R>(P, L.tab, my_table), L.lines, cA, mach,
+                                my_table ? aq_cl : aq_cd, live, L.bal[threadIdx.x >> 6], L.tab, wind_block
+#ifdef PD_STAMP
+                                , acc_ + 7
+#endif
+                                );
+                else
+                    v = rbf<R>(a, P, my_table, tab_view<R>(P, L.tab, my_table), L.lines, cA, mach,
+                               my_table ? aq_cl : aq_cd, part, nparts);
                 if constexpr (nparts >= 2) v += __shfl_xor(v, 1);
                 if constexpr (nparts >= 4) v += __shfl_xor(v, 2);
                 if constexpr (nparts >= 8) v += __shfl_xor(v, 4);
@@ -903,35 +1184,14 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
         else inertia<R>(P, R(1) - fpc, x_cog, I);
         R d_thrust = x_cog + P.engine_height;
         R d_cp_cg = x_cog - (ascent ? P.cop_ascent : P.cop);
-        R ug = R(0), vg = R(0);
-        if constexpr (WIND) {
-            // WindModel.__call__ (full_wind_model.py:35-43)
-            const R* walt = L.walt + e.prof * 16;
-            const R* wsp = L.wsp + e.prof * 16;
-            R km = y / R(1000);
-            int wn = P.wind_n[e.prof];
-            ug = np_interp<R>(walt, wsp, wn, km);
-            if (y < P.vk_y_threshold && a.stochastic) {
-                double w0, w1;
-                if (a.noise) { w0 = ev(a.noise + 2 * sub, ui * 8); w1 = ev(a.noise + 2 * sub + 1, ui * 8); }
-                else {
-                    // vonkarman.py:34: one np.random.randn() per filter step, u then v (gauss_pair:
-                    // Philox counter (env, episode, step, sub-step), reproducible by the oracle)
-                    u32x4 r = philox({(uint32_t)g, (uint32_t)(g >> 32) ^ e.ep, e.ts, kTagWindSub + (uint32_t)sub},
-                                     a.seed_lo, a.seed_hi);
-                    gauss_pair(r, (const double*)(uint64_t)&P.logtab.invc[0], (const double*)(uint64_t)&P.logtab.logc[0], w0, w1);
-                }
-                // vonkarman.py:33-36: state = Ad @ state + Bd * w  (Bd = sigma * Bd(sigma=1))
-                R n0 = (P.vk_Ad_u[0] * e.fu0 + P.vk_Ad_u[1] * e.fu1) + (e.sgu * P.vk_Bd_u[0]) * (R)w0;
-                R n1 = (P.vk_Ad_u[2] * e.fu0 + P.vk_Ad_u[3] * e.fu1) + (e.sgu * P.vk_Bd_u[1]) * (R)w0;
-                e.fu0 = n0; e.fu1 = n1;
-                n0 = (P.vk_Ad_v[0] * e.fv0 + P.vk_Ad_v[1] * e.fv1) + (e.sgv * P.vk_Bd_v[0]) * (R)w1;
-                n1 = (P.vk_Ad_v[2] * e.fv0 + P.vk_Ad_v[3] * e.fv1) + (e.sgv * P.vk_Bd_v[1]) * (R)w1;
-                e.fv0 = n0; e.fv1 = n1;
-                ug = ug + e.fu1;
-                vg = e.fv1;
-            }
-        }
+#ifndef PD_EXP_NORBF
+        if constexpr (LPE != 2) wind_block();
+#else
+        wind_block();
+#endif
+#ifdef PD_STAMP
+        PD_T(t_p1); acc_[9 + 4] += t_p1 - t_aero1;
+#endif
         R Fwx = R(0.5) * rho * (ug * ug) * P.A_front * P.C_gust_x;
         R Fwy = R(0.5) * rho * (vg * vg) * P.A_front * P.C_gust_y;
         R Mw = -d_cp_cg * Fwy;
@@ -955,6 +1215,9 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
         R aero_m = aperp * d_cp_cg;
         if (PHASE == 2 && aux == PD_PHASE_FLIP_OVER) { aero_x = R(0); aero_y = R(0); aero_m = R(0); }   // :548-551
 
+#ifdef PD_STAMP
+        PD_T(t_p2); acc_[9 + 5] += t_p2 - t_p1;
+#endif
         R T_full = P.T_e + (P.p_e - patm) * P.A_e;
         R qS = q * P.S_gf;
         R Ca = grid_fin_ca<R>(P, L.gf, L.gf + 64, mach);
@@ -1122,6 +1385,9 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
             md_info = md; thr_info = thr;
             i_dl = dl; i_dr = dr; i_cnl = CnL; i_cnr = CnR; i_gfperp = f_perp; i_gfpar = f_par; i_gfm = m_z;
         }
+#ifdef PD_STAMP
+        PD_T(t_p3); acc_[9 + 6] += t_p3 - t_p2;
+#endif
         // NaN guard (rockets_physics.py:599-607), an elif chain
         if (isnan(cfp)) { cfp = R(0); nan_hit = true; }
         else if (isnan(cfperp)) { cfperp = R(0); nan_hit = true; }
@@ -1157,6 +1423,9 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
         // three divisions as two lane-paired ones
         const R mz = cm + aero_m + Mw;
         R vxd, vyq, thdd, grq;
+#ifdef PD_STAMP
+        PD_T(t_p4); acc_[9 + 7] += t_p4 - t_p3;
+#endif
         div_pair<LPE, R>(fx, m, fy, m, role, vxd, vyq);
         div_pair<LPE, R>(mz, I, P.grav_R, P.grav_R + y, role, thdd, grq);
         const R gr = P.grav_g0 * (grq * grq);
@@ -1417,14 +1686,19 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
     }
 
     // ---- the env's state back to HBM, once (policy rollouts: also when its episode ends)
+    PD_T(t_store);
     store_all();
 #ifdef PD_STAMP
     PD_T(t_end);
-    PD_ACC(6, t_end - t_rtd);
+    PD_ACC(6, t_end - t_store);
     if (__lane_id() == 0) {
 #pragma unroll
         for (int k = 0; k < 7; ++k) atomicAdd(&a.pend.stats[kStStamp + k], acc_[k]);
         atomicAdd(&a.pend.stats[kStStamp + 7], 1ull);
+        atomicAdd(&a.pend.stats[22], acc_[7]);
+        atomicAdd(&a.pend.stats[23], acc_[8]);
+        for (int k = 0; k < 4; ++k) atomicAdd(&a.pend.stats[24 + k], acc_[9 + k]);
+        for (int k = 0; k < 4; ++k) atomicAdd(&a.pend.stats[28 + k], acc_[13 + k]);
     }
 #endif
 }

@@ -262,11 +262,153 @@ pd_status build_line(const pd_aero_table& t, double a, Table<R>& T, int li, DevP
     std::vector<double> work(kScratch), pay(kPay);
     D.line_nbp[li] = (int)B.size();
     for (size_t k = 0; k < B.size(); ++k) D.line_bp[li][k] = (R)B[k];
+    // search buckets (pd_physics.h kLineBuckets), on the handle-precision breakpoints
+    for (int b = 0; b < kLineBuckets; ++b) {
+        const double w = 10.0 / kLineBuckets, lo = b * w - 1e-4, hi = (b + 1) * w + 1e-4;
+        int nlo = 0, nhi = 0;
+        for (size_t k = 0; k < B.size(); ++k) {
+            nlo += (double)D.line_bp[li][k] < lo;
+            nhi += (double)D.line_bp[li][k] < hi;
+        }
+        D.line_lb[li][b] = (uint16_t)(nlo | (nhi << 8));
+    }
     for (size_t k = 0; k < K.size(); ++k) {
         D.line_key[li][k] = K[k];
         D.line_slot[li][k] = table_insert<R>(t, T, K[k], work, pay);
     }
     return PD_OK;
+}
+
+// Taylor pieces of clamped query line li (kTayCells cells of Mach [0, 10], one piece per (cell,
+// neighbourhood interval) pair, piece index cell + l with l the interval's index -- the device's
+// binary-search result -- so no piece table is needed).  Along the line a = const the thin-plate
+// sum f(M) = sum_j c_j phi(|(M, a) - y_j|) + poly is analytic except at the points ON the line
+// (d_a = 0, the C_L +10 line lies on the AoA-10 column): each term's singularities are at
+// M = m_j +- i d_a.  A piece keeps the kTayExact terms whose singularity is nearest to its cell
+// centre x0 as exact terms and expands the rest to degree kTayDeg in t = M - x0 (long double):
+//   log((u0 + t)^2 + d^2) = log|z|^2 + sum_k 2 (-1)^(k+1) Re(z^-k) t^k / k,   z = u0 + i d,
+//   times (|z|^2 + 2 u0 t + t^2), halved (phi = d2 log(d2) / 2), plus the degree-1 polynomial.
+// The remaining singularities are >= 10x the cell half-width away (>= 0.17 on the C_D lines,
+// >= 0.024 past the two nearest AoA-10 points), so the truncation is below binary64 rounding;
+// every piece is checked at five points against the long double sum and a line whose worst
+// error exceeds 1e-13 relative to sum |c_j phi_j| is left to the exact path (tay_off = -1).
+struct TayStats { double max_abs = 0, max_rel = 0; int64_t pieces = 0; };
+
+template <typename R>
+void build_taylor(const pd_aero_table& t, int li, DevParams<R>& D, std::vector<R>& out, TayStats& ts) {
+    D.tay_off[li] = -1;
+    const int nb = D.line_nbp[li];
+    if (nb < 0) return;
+    const long double a = (long double)D.line_a[li];
+    const double w = 10.0 / kTayCells;
+    std::vector<double> bp(nb);
+    for (int k = 0; k < nb; ++k) bp[k] = (double)D.line_bp[li][k];
+    auto count_below = [&](double x) { return (int)(std::lower_bound(bp.begin(), bp.end(), x) - bp.begin()); };
+    // the binary64 payload of every interval (the same solve as the tables')
+    std::vector<std::vector<double>> pays(nb + 1, std::vector<double>(kPay));
+    std::vector<double> work(kScratch);
+    std::vector<double> aoa(kCols);
+    for (int c = 0; c < kCols; ++c) aoa[c] = t.col_aoa[c];
+    for (int l = 0; l <= nb; ++l)
+        if (solve_neighbourhood(t.mach, t.coef, t.col_start, aoa.data(), D.line_key[li][l], work.data(), pays[l].data()) != 0)
+            return;
+    const size_t base = out.size();
+    out.resize(base + (size_t)(kTayCells + nb) * kTayStride, R(0));
+    double worst_rel = 0.0;
+    for (int cell = 0; cell < kTayCells; ++cell) {
+        const double lo = cell * w, hi = (cell + 1) * w;
+        const long double x0 = (long double)cell * w + 0.5L * w;
+        for (int l = count_below(lo); l <= count_below(hi) && l <= nb; ++l) {
+            const double* pay = pays[l].data();
+            const uint8_t* ib = (const uint8_t*)(pay + kPayIdx);
+            // the terms: Mach, d_a^2, coefficient
+            long double m[2 * kPairs], dl2[2 * kPairs], cf[2 * kPairs], z2[2 * kPairs];
+            int nt = 0;
+            for (int k = 0; k < kPairs; ++k)
+                for (int i = 0; i < 2; ++i) {
+                    const double c = pay[2 * k + i];
+                    if (c == 0.0) continue;
+                    const int pidx = ib[pair_entry_pos(k)] + i;
+                    const long double da = a - (long double)ib[pair_aoa_pos(k)];
+                    m[nt] = t.mach[pidx]; dl2[nt] = da * da; cf[nt] = c;
+                    const long double u0 = x0 - m[nt];
+                    z2[nt] = u0 * u0 + dl2[nt];
+                    ++nt;
+                }
+            int ex[kTayExact];
+            for (int e = 0; e < kTayExact; ++e) {
+                int best = -1;
+                for (int j = 0; j < nt; ++j) {
+                    bool used = false;
+                    for (int q = 0; q < e; ++q) used |= ex[q] == j;
+                    if (!used && (best < 0 || z2[j] < z2[best])) best = j;
+                }
+                ex[e] = best;
+            }
+            long double B[kTayDeg + 1] = {};
+            for (int j = 0; j < nt; ++j) {
+                bool is_ex = false;
+                for (int e = 0; e < kTayExact; ++e) is_ex |= ex[e] == j;
+                if (is_ex) continue;
+                const long double u0 = x0 - m[j], d = sqrtl(dl2[j]);
+                // z^-k = conj(z)^k / |z|^(2k): real parts by the recurrence on (re, im)
+                long double L[kTayDeg + 1];
+                L[0] = logl(z2[j]);
+                long double zr = 1.0L, zi = 0.0L;   // (conj(z) / |z|^2)^k
+                const long double ir = u0 / z2[j], ii = -d / z2[j];
+                for (int k = 1; k <= kTayDeg; ++k) {
+                    const long double nr = zr * ir - zi * ii, ni = zr * ii + zi * ir;
+                    zr = nr; zi = ni;
+                    L[k] = 2.0L * ((k & 1) ? 1.0L : -1.0L) * zr / k;
+                }
+                const long double Q[3] = {z2[j], 2.0L * u0, 1.0L};
+                for (int n = 0; n <= kTayDeg; ++n) {
+                    long double b = 0.0L;
+                    for (int q = 0; q < 3 && q <= n; ++q) b += Q[q] * L[n - q];
+                    B[n] += 0.5L * cf[j] * b;
+                }
+            }
+            const long double p0 = pay[kPayPoly], p1 = pay[kPayPoly + 1], p2 = pay[kPayPoly + 2];
+            const long double sh0 = pay[kPaySS + 0], sh1 = pay[kPaySS + 1], sc0 = pay[kPaySS + 2], sc1 = pay[kPaySS + 3];
+            B[0] += p0 + (x0 - sh0) / sc0 * p1 + (a - sh1) / sc1 * p2;
+            B[1] += p1 / sc0;
+            R* rec = out.data() + base + (size_t)(cell + l) * kTayStride;
+            for (int n = 0; n <= kTayDeg; ++n) rec[n] = (R)B[n];
+            for (int e = 0; e < kTayExact; ++e) {
+                R* x = rec + kTayDeg + 1 + 3 * e;
+                if (ex[e] < 0) { x[0] = R(0); x[1] = R(0); x[2] = R(1); continue; }
+                x[0] = (R)m[ex[e]]; x[1] = (R)(cf[ex[e]] * 0.125L); x[2] = (R)dl2[ex[e]];
+            }
+            // check: five points of the piece's part of the cell
+            const double plo = std::max(lo, l > 0 ? bp[l - 1] : lo), phi = std::min(hi, l < nb ? bp[l] : hi);
+            for (int q = 0; q < 5; ++q) {
+                const double M = plo + (phi - plo) * (0.02 + 0.24 * q);
+                long double exact = p0 + ((long double)M - sh0) / sc0 * p1 + (a - sh1) / sc1 * p2, mag = 0.0L;
+                for (int j = 0; j < nt; ++j) {
+                    const long double dm = M - m[j], d2 = dm * dm + dl2[j];
+                    const long double ph = d2 > 0 ? 0.5L * cf[j] * d2 * logl(d2) : 0.0L;
+                    exact += ph; mag += fabsl(ph);
+                }
+                const double tt = M - (double)x0;
+                double f = (double)rec[kTayDeg];
+                for (int n = kTayDeg - 1; n >= 0; --n) f = std::fma(f, tt, (double)rec[n]);
+                for (int e = 0; e < kTayExact; ++e) {
+                    const R* x = rec + kTayDeg + 1 + 3 * e;
+                    const double dm = M - (double)x[0], d2 = std::fma(dm, dm, (double)x[2]);
+                    if (d2 > 0) f = std::fma((double)x[1] * d2, 4.0 * std::log(d2), f);
+                }
+                const double err = std::fabs(f - (double)exact);
+                ts.max_abs = std::max(ts.max_abs, err);
+                const double rel = err / (double)(mag + fabsl(exact) + 1e-300L);
+                worst_rel = std::max(worst_rel, rel);
+            }
+            ++ts.pieces;
+        }
+    }
+    ts.max_rel = std::max(ts.max_rel, worst_rel);
+    const double lim = sizeof(R) == 8 ? 1e-13 : 1e-6;
+    if (worst_rel > lim) { out.resize(base); return; }
+    D.tay_off[li] = (int)(base / kTayStride);
 }
 
 // The same 50-NN key by selection instead of a full sort: the 50 smallest under the total order
@@ -648,10 +790,25 @@ template <typename R> pd_status create_impl(const pd_params* p, const pd_config*
     if ((st = build_line<R>(p->cd, -10.0 * kDeg2Rad, tcd, 1, D)) != PD_OK) return st;
     if ((st = build_line<R>(p->cl, 10.0, tcl, 2, D)) != PD_OK) return st;
     if ((st = build_line<R>(p->cl, -10.0, tcl, 3, D)) != PD_OK) return st;
+    // Taylor pieces of the lines (evaluated instead of the payload sums by the LPE-2 kernels)
+    std::vector<R> tay;
+    TayStats tst;
+    for (int li = 0; li < 4; ++li) build_taylor<R>(li < 2 ? p->cd : p->cl, li, D, tay, tst);
+    if (getenv("PDENV_TAY_DEBUG"))
+        fprintf(stderr, "pdenv taylor: %lld pieces, max abs err %.3g, max rel err %.3g, lines %d %d %d %d\n",
+                (long long)tst.pieces, tst.max_abs, tst.max_rel, D.tay_off[0], D.tay_off[1], D.tay_off[2], D.tay_off[3]);
+    {
+        void* dt;
+        if ((st = dalloc(e, &dt, std::max<size_t>(tay.size(), 1) * sizeof(R)))) return st;
+        if (!tay.empty()) PD_HIP(hipMemcpy(dt, tay.data(), tay.size() * sizeof(R), hipMemcpyHostToDevice));
+        D.tay = (const R*)dt;
+    }
     // interior candidate grids: C_D abscissa in [-radians(10), radians(10)], C_L in [0, 10]
     std::vector<unsigned long long> gk[2], sk[2];
     std::vector<int> gs[2], ss[2];
-    int gnm[2] = {400, 400}, gna[2] = {16, 200};
+    // (1600 x 64 / 1600 x 800 cells of 8 x 8 sub-cells where refined: verified queries 0.8 % ->
+    // 0.4 %, measured 3 % faster than 400 x 16 / 400 x 200 of 16 x 16 at the same memory order)
+    int gnm[2] = {1600, 1600}, gna[2] = {64, 800};
     if (const char* g = getenv("PDENV_GRID")) {   // experiments: "nm_cd,na_cd,nm_cl,na_cl"
         int v[4];
         if (sscanf(g, "%d,%d,%d,%d", &v[0], &v[1], &v[2], &v[3]) == 4 && v[0] > 0 && v[1] > 0 && v[2] > 0 && v[3] > 0) {
@@ -661,6 +818,14 @@ template <typename R> pd_status create_impl(const pd_params* p, const pd_config*
     const double ga0[2] = {-10.0 * kDeg2Rad, 0.0}, ga1[2] = {10.0 * kDeg2Rad, 10.0};
     if ((st = build_grid<R>(p->cd, ga0[0], ga1[0], gnm[0], gna[0], tcd, gk[0], gs[0], sk[0], ss[0])) != PD_OK) return st;
     if ((st = build_grid<R>(p->cl, ga0[1], ga1[1], gnm[1], gna[1], tcl, gk[1], gs[1], sk[1], ss[1])) != PD_OK) return st;
+    if (getenv("PDENV_TAY_DEBUG"))
+        for (int tb = 0; tb < 2; ++tb) {
+            int64_t nref = 0, nne = 0, nce = 0;
+            for (int v : gs[tb]) { nref += v >= 0 && (v & kGridRefine); nce += v >= 0 && !(v & kGridRefine) && !(v & kGridExact); }
+            for (int v : ss[tb]) nne += v < 0 || !(v & kGridExact);
+            fprintf(stderr, "pdenv grid %d: %d x %d cells, %lld refined, %lld non-exact cells, %lld of %zu sub-cells non-exact\n", tb,
+                    gnm[tb], gna[tb], (long long)nref, (long long)nce, (long long)nne, ss[tb].size());
+        }
     for (int tb = 0; tb < 2; ++tb) {
         void *dk, *ds, *dsk, *dss;
         const size_t nsub = std::max<size_t>(sk[tb].size(), 1);
