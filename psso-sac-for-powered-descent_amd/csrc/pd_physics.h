@@ -100,6 +100,7 @@ template <typename R> struct DevParams {
     // refined cells (kGridRefine): kGridSub x kGridSub sub-cells each, Mach-major
     const unsigned long long* sub_key[2];
     const int* sub_slot[2];
+    const void* sub_bis[2];          // GridBisect records (pd_step.h) of the kGridBisect sub-cells
     R line_bp[4][kLineMax];
     int line_slot[4][kLineMax + 1];
     unsigned long long line_key[4][kLineMax + 1];

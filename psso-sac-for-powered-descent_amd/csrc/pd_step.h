@@ -21,6 +21,18 @@ constexpr int kPendingCap = 4096;     // device-solved neighbourhoods queued per
 constexpr int kSolveSlots = 1024;     // global-memory LU scratch slots (one per workgroup, modulo)
 constexpr int kGridExact = 1 << 30;   // grid_slot flag: every point of the cell has its key
 constexpr int kGridRefine = 1 << 29;  // grid_slot flag: the cell is refined, low bits = its sub-grid
+constexpr int kGridBisect = 1 << 28;  // sub_slot flag: two regions split by one bisector, low bits = its record
+
+// A sub-cell holding two 50-NN regions A, B whose keys differ by one point swap (p in A, q in B):
+// s(x) = n . x - c < 0 on A's side (p nearer than q).  Each side's slot carries kGridExact only if
+// the host checked that the side's part of the sub-cell, kept tau off the bisector, has that key
+// everywhere (its clipped polygon's vertices carry it; regions are convex); |s| <= 3 tau: verified.
+struct GridBisect {
+    double nx, ny, c, tau;
+    unsigned long long key_a, key_b;
+    int slot_a, slot_b;
+    int pad[2];
+};
 #ifndef PD_GRID_SUB
 #define PD_GRID_SUB 8
 #endif

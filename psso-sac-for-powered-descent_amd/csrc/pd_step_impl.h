@@ -62,6 +62,7 @@ template <typename R> struct TabView {
     const PD_AS1 int* grid_slot;
     const PD_AS1 unsigned long long* sub_key;
     const PD_AS1 int* sub_slot;
+    const PD_AS1 GridBisect* sub_bis;
     int grid_nm, grid_na;
     R grid_a0, grid_inv_da, grid_inv_dm;
 };
@@ -491,6 +492,16 @@ __device__ __forceinline__ int rbf_lookup(const StepArgs<R>& a, DP<R>& P, int ta
             ckey = t.sub_key[sc];
             gsl = t.sub_slot[sc];
             um = sm - (R)jm; ua = sa - (R)ja;
+            if (gsl >= 0 && (gsl & kGridBisect)) {
+                // two regions split by one bisector: the query's side (trusted off the line)
+                const PD_AS1 GridBisect& b = t.sub_bis[gsl & (kGridBisect - 1)];
+                const double sv = fma(b.nx, (double)M, fma(b.ny, (double)aq, -b.c));
+                const bool side_a = sv < 0.0;
+                int sl = side_a ? b.slot_a : b.slot_b;
+                ckey = side_a ? b.key_a : b.key_b;
+                if (!(fabs(sv) > 3.0 * b.tau) && sl >= 0) sl &= ~kGridExact;
+                gsl = sl;
+            }
         }
         cslot = gsl < 0 ? -1 : (gsl & (kGridRefine - 1));
         // every point of an exact cell has the cell's key (convexity of 50-NN regions); the
@@ -835,6 +846,7 @@ __device__ __forceinline__ TabView<R> tab_view(DP<R>& P, const R* tab, int table
     t.grid_slot = gbl(P.grid_slot[table]);
     t.sub_key = gbl(P.sub_key[table]);
     t.sub_slot = gbl(P.sub_slot[table]);
+    t.sub_bis = gbl((const GridBisect*)P.sub_bis[table]);
     t.grid_nm = P.grid_nm[table];
     t.grid_na = P.grid_na[table];
     t.grid_a0 = P.grid_a0[table];

@@ -444,12 +444,80 @@ uint64_t knn_key_select(const pd_aero_table& t, double M, double a) {
 // corners disagree with its centre a kGridSub x kGridSub sub-grid (centres and corners).  Pure
 // functions of the table, so they are computed once per process (threads over cells) and
 // cached; slots are assigned per handle.
+struct BisectHost { double nx, ny, c, tau; uint64_t key_a, key_b; bool ok_a, ok_b; };
 struct GridKeys {
     int nm = 0, na = 0;
     std::vector<uint64_t> centre, corner;            // [nm][na], [nm + 1][na + 1]
     std::vector<int> refined;                        // cell index of each refined cell
     std::vector<uint64_t> sub_centre, sub_corner;    // [ref][S][S], [ref][S + 1][S + 1]
+    std::vector<int> sub_bis;                        // [ref][S][S]: index into bis, -1 none
+    std::vector<BisectHost> bis;
 };
+
+// The one point swap between two keys (A \ B = {p}, B \ A = {q}), as table point indices;
+// false if the keys differ otherwise
+bool single_swap(const pd_aero_table& t, uint64_t ka, uint64_t kb, int& p, int& q) {
+    int la[kCols], na[kCols], lb[kCols], nb[kCols];
+    key_unpack(ka, la, na);
+    key_unpack(kb, lb, nb);
+    int np = 0, nq = 0;
+    p = q = -1;
+    for (int c = 0; c < kCols; ++c) {
+        for (int i = la[c]; i < la[c] + na[c]; ++i)
+            if (!(nb[c] > 0 && i >= lb[c] && i < lb[c] + nb[c])) { ++np; p = t.col_start[c] + i; }
+        for (int i = lb[c]; i < lb[c] + nb[c]; ++i)
+            if (!(na[c] > 0 && i >= la[c] && i < la[c] + na[c])) { ++nq; q = t.col_start[c] + i; }
+    }
+    return np == 1 && nq == 1;
+}
+double point_aoa(const pd_aero_table& t, int idx) {
+    int c = 0;
+    while (c + 1 < t.n_cols && idx >= t.col_start[c + 1]) ++c;
+    return t.col_aoa[c];
+}
+
+// Bisector record of a non-exact sub-cell [m0, m1] x [a0, a1] whose sample keys are {A, B} (see
+// GridBisect): the bisector of the swapped points, and for each side whether its part of the
+// cell, tau off the line, provably has the side's key (every vertex of the clipped polygon does).
+bool make_bisect(const pd_aero_table& t, double m0, double m1, double a0, double a1, uint64_t ka, uint64_t kb,
+                 BisectHost& out) {
+    int p, q;
+    if (!single_swap(t, ka, kb, p, q)) {
+        if (!single_swap(t, kb, ka, p, q)) return false;
+        std::swap(ka, kb);
+    }
+    const double pm = t.mach[p], pa = point_aoa(t, p), qm = t.mach[q], qa = point_aoa(t, q);
+    out.nx = 2.0 * (qm - pm); out.ny = 2.0 * (qa - pa);
+    out.c = (qm * qm + qa * qa) - (pm * pm + pa * pa);
+    out.tau = 1e-9 * (std::fabs(out.nx) * 10.0 + std::fabs(out.ny) * 10.0 + std::fabs(out.c) + 1.0);
+    out.key_a = ka; out.key_b = kb;
+    auto side_ok = [&](double sign) {
+        // the side's part of the cell kept 2 tau off the line (A: s <= -2 tau, B: s >= 2 tau) is
+        // the convex polygon f <= 0; every vertex must carry the side's key (the device trusts
+        // |s| > 3 tau, inside it)
+        const double cx[4] = {m0, m1, m1, m0}, cy[4] = {a0, a0, a1, a1};
+        std::vector<std::pair<double, double>> poly;
+        auto f = [&](double x, double y) { return -sign * (out.nx * x + out.ny * y - out.c) + 2.0 * out.tau; };
+        for (int k = 0; k < 4; ++k) {
+            const int k1 = (k + 1) & 3;
+            const double f0 = f(cx[k], cy[k]), f1 = f(cx[k1], cy[k1]);
+            if (f0 <= 0) poly.push_back({cx[k], cy[k]});
+            if ((f0 < 0) != (f1 < 0) && f0 != f1) {
+                const double u = f0 / (f0 - f1);
+                poly.push_back({cx[k] + u * (cx[k1] - cx[k]), cy[k] + u * (cy[k1] - cy[k])});
+            }
+        }
+        if (poly.empty()) return false;
+        const uint64_t want = sign < 0 ? ka : kb;
+        for (auto& v : poly)
+            if (knn_key_select(t, std::min(std::max(v.first, m0), m1), std::min(std::max(v.second, a0), a1)) != want)
+                return false;
+        return true;
+    };
+    out.ok_a = side_ok(-1.0);
+    out.ok_b = side_ok(+1.0);
+    return out.ok_a || out.ok_b;
+}
 
 template <typename F> void parallel_for(int64_t n, F f) {
     unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
@@ -504,6 +572,36 @@ const GridKeys& grid_keys(const pd_aero_table& t, double a0, double a1, int nm, 
                         knn_key_select(t, (im + (jm + 0.5) / S) * dm, a0 + (ia + (ja + 0.5) / S) * da);
             }
     });
+    // non-exact sub-cells split by one bisector between two keys: records (threads per refined
+    // cell, then gathered in order)
+    g.sub_bis.assign((size_t)nr * S * S, -1);
+    std::vector<std::vector<std::pair<int, BisectHost>>> found((size_t)nr);
+    parallel_for(nr, [&](int64_t r) {
+        const int im = g.refined[r] / na, ia = g.refined[r] % na;
+        for (int jm = 0; jm < S; ++jm)
+            for (int ja = 0; ja < S; ++ja) {
+                const uint64_t kc = g.sub_centre[((size_t)r * S + jm) * S + ja];
+                uint64_t other = kc;
+                bool two = true, exact = true;
+                for (int c = 0; c < 4 && two; ++c) {
+                    const uint64_t k = g.sub_corner[((size_t)r * (S + 1) + jm + (c >> 1)) * (S + 1) + ja + (c & 1)];
+                    if (k == kc) continue;
+                    exact = false;
+                    if (other == kc) other = k;
+                    else if (k != other) two = false;
+                }
+                if (exact || !two) continue;
+                BisectHost b;
+                const double m0 = (im + (double)jm / S) * dm, m1 = (im + (double)(jm + 1) / S) * dm;
+                const double c0 = a0 + (ia + (double)ja / S) * da, c1 = a0 + (ia + (double)(ja + 1) / S) * da;
+                if (make_bisect(t, m0, m1, c0, c1, kc, other, b)) found[r].push_back({jm * S + ja, b});
+            }
+    });
+    for (int64_t r = 0; r < nr; ++r)
+        for (auto& fb : found[r]) {
+            g.sub_bis[(size_t)r * S * S + fb.first] = (int)g.bis.size();
+            g.bis.push_back(fb.second);
+        }
     return g;
 }
 
@@ -517,7 +615,7 @@ const GridKeys& grid_keys(const pd_aero_table& t, double a0, double a1, int nm, 
 template <typename R>
 pd_status build_grid(const pd_aero_table& t, double a0, double a1, int nm, int na, Table<R>& T,
                      std::vector<unsigned long long>& gk, std::vector<int>& gs,
-                     std::vector<unsigned long long>& sk, std::vector<int>& ss) {
+                     std::vector<unsigned long long>& sk, std::vector<int>& ss, std::vector<GridBisect>& bs) {
     const GridKeys& g = grid_keys(t, a0, a1, nm, na);
     const int S = kGridSub;
     gk.assign((size_t)nm * na, 0); gs.assign((size_t)nm * na, -1);
@@ -546,6 +644,17 @@ pd_status build_grid(const pd_aero_table& t, double a0, double a1, int nm, int n
                     exact = g.sub_corner[((size_t)r * (S + 1) + jm + (c >> 1)) * (S + 1) + ja + (c & 1)] == key;
                 sk[q] = key;
                 ss[q] = slot_of(key, exact);
+                const int bi = g.sub_bis[q];
+                if (!exact && bi >= 0 && sizeof(R) == 8 && bs.size() < (size_t)kGridBisect) {
+                    const BisectHost& h = g.bis[bi];
+                    GridBisect b{};
+                    b.nx = h.nx; b.ny = h.ny; b.c = h.c; b.tau = h.tau; b.key_a = h.key_a; b.key_b = h.key_b;
+                    const int sa = table_insert<R>(t, T, h.key_a, work, pay), sb = table_insert<R>(t, T, h.key_b, work, pay);
+                    b.slot_a = sa < 0 ? -1 : (sa | (h.ok_a ? kGridExact : 0));
+                    b.slot_b = sb < 0 ? -1 : (sb | (h.ok_b ? kGridExact : 0));
+                    ss[q] = kGridBisect | (int)bs.size();
+                    bs.push_back(b);
+                }
             }
     }
     return PD_OK;
@@ -806,6 +915,7 @@ template <typename R> pd_status create_impl(const pd_params* p, const pd_config*
     // interior candidate grids: C_D abscissa in [-radians(10), radians(10)], C_L in [0, 10]
     std::vector<unsigned long long> gk[2], sk[2];
     std::vector<int> gs[2], ss[2];
+    std::vector<GridBisect> bs[2];
     // (1600 x 64 / 1600 x 800 cells of 8 x 8 sub-cells where refined: verified queries 0.8 % ->
     // 0.4 %, measured 3 % faster than 400 x 16 / 400 x 200 of 16 x 16 at the same memory order)
     int gnm[2] = {1600, 1600}, gna[2] = {64, 800};
@@ -816,13 +926,16 @@ template <typename R> pd_status create_impl(const pd_params* p, const pd_config*
         }
     }
     const double ga0[2] = {-10.0 * kDeg2Rad, 0.0}, ga1[2] = {10.0 * kDeg2Rad, 10.0};
-    if ((st = build_grid<R>(p->cd, ga0[0], ga1[0], gnm[0], gna[0], tcd, gk[0], gs[0], sk[0], ss[0])) != PD_OK) return st;
-    if ((st = build_grid<R>(p->cl, ga0[1], ga1[1], gnm[1], gna[1], tcl, gk[1], gs[1], sk[1], ss[1])) != PD_OK) return st;
+    if ((st = build_grid<R>(p->cd, ga0[0], ga1[0], gnm[0], gna[0], tcd, gk[0], gs[0], sk[0], ss[0], bs[0])) != PD_OK) return st;
+    if ((st = build_grid<R>(p->cl, ga0[1], ga1[1], gnm[1], gna[1], tcl, gk[1], gs[1], sk[1], ss[1], bs[1])) != PD_OK) return st;
     if (getenv("PDENV_TAY_DEBUG"))
         for (int tb = 0; tb < 2; ++tb) {
             int64_t nref = 0, nne = 0, nce = 0;
             for (int v : gs[tb]) { nref += v >= 0 && (v & kGridRefine); nce += v >= 0 && !(v & kGridRefine) && !(v & kGridExact); }
+            int64_t nbs = 0, nbs2 = 0;
             for (int v : ss[tb]) nne += v < 0 || !(v & kGridExact);
+            for (auto& b : bs[tb]) { nbs += 1; nbs2 += (b.slot_a >= 0 && (b.slot_a & kGridExact)) + (b.slot_b >= 0 && (b.slot_b & kGridExact)); }
+            fprintf(stderr, "pdenv grid %d: %lld bisector sub-cells, %lld trusted sides\n", tb, (long long)nbs, (long long)nbs2);
             fprintf(stderr, "pdenv grid %d: %d x %d cells, %lld refined, %lld non-exact cells, %lld of %zu sub-cells non-exact\n", tb,
                     gnm[tb], gna[tb], (long long)nref, (long long)nce, (long long)nne, ss[tb].size());
         }
@@ -839,6 +952,10 @@ template <typename R> pd_status create_impl(const pd_params* p, const pd_config*
             PD_HIP(hipMemcpy(dss, ss[tb].data(), ss[tb].size() * 4, hipMemcpyHostToDevice));
         }
         D.sub_key[tb] = (const unsigned long long*)dsk; D.sub_slot[tb] = (const int*)dss;
+        void* dbs;
+        if ((st = dalloc(e, &dbs, std::max<size_t>(bs[tb].size(), 1) * sizeof(GridBisect)))) return st;
+        if (!bs[tb].empty()) PD_HIP(hipMemcpy(dbs, bs[tb].data(), bs[tb].size() * sizeof(GridBisect), hipMemcpyHostToDevice));
+        D.sub_bis[tb] = dbs;
         D.grid_key[tb] = (const unsigned long long*)dk; D.grid_slot[tb] = (const int*)ds;
         D.grid_nm[tb] = gnm[tb]; D.grid_na[tb] = gna[tb]; D.grid_a0[tb] = (R)ga0[tb];
         D.grid_inv_da[tb] = (R)(gna[tb] / (ga1[tb] - ga0[tb])); D.grid_inv_dm[tb] = (R)(gnm[tb] / 10.0);
