@@ -63,6 +63,7 @@ template <typename R> struct DevParams {
     // grid fins
     int ca_n, cn_n;
     R ca_x[64], ca_y[64], ca_min_mach, ca_min_val;
+    uint16_t ca_lb[64];              // C_a search buckets over Mach [0, 10) (as line_lb)
     R cn_x[64], cn_y[64], cn_min_mach, cn_max_mach, cn_min_val, cn_max_val, cn_slope;
     // wind
     int wind_n[50];
@@ -343,10 +344,16 @@ __device__ __forceinline__ void obs_write(DP<R>& P, int kind, const R* s, R* out
 // ---------------------------------------------------------------- tables in LDS
 // scipy interp1d._call_linear with fill_value='extrapolate' (grid_fin_aerodynamics.py:7-18)
 template <typename R>
-__device__ __forceinline__ R grid_fin_ca(DP<R>& P, const R* sx, const R* sy, R mach) {
+__device__ __forceinline__ R grid_fin_ca(DP<R>& P, const R* sx, const R* sy, R mach, const uint16_t* lb = nullptr) {
     if (mach < P.ca_min_mach) return P.ca_min_val;
     int n = P.ca_n;
     int lo = 0, hi = n;                       // lower_bound: first x >= mach
+    if (lb != nullptr && mach >= R(0) && mach < R(10)) {   // within the Mach bucket's index range
+        int b = (int)(mach * R(6.4));
+        b = b > 63 ? 63 : b;
+        const uint32_t rg = lb[b];
+        lo = (int)(rg & 0xffu); hi = (int)(rg >> 8);
+    }
     while (lo < hi) { int mid = (lo + hi) >> 1; if (sx[mid] < mach) lo = mid + 1; else hi = mid; }
     int idx = lo < 1 ? 1 : (lo > n - 1 ? n - 1 : lo);
     R xl = sx[idx - 1], xh = sx[idx], yl = sy[idx - 1], yh = sy[idx];

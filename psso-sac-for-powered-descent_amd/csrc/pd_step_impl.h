@@ -823,6 +823,7 @@ template <typename R, bool WIND, int EPB, bool BAL = false> struct StepLds {
     // payload pair slot (smach[2p] is point p's Mach for the neighbourhood search)
     alignas(16) R tab[1024];
     R gf[256];                    // grid fins: ca_x, ca_y, cn_x, cn_y (64 each)
+    uint16_t ca_lb[64];           // C_a search buckets
     R isa[9 * kIsaCols];          // ISA layers
     R walt[WIND ? 800 : 1];       // wind profiles [50][16]: altitude km, speed
     R wsp[WIND ? 800 : 1];
@@ -891,6 +892,7 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
         if (threadIdx.x < 64) {
             L.gf[threadIdx.x] = P.ca_x[threadIdx.x]; L.gf[64 + threadIdx.x] = P.ca_y[threadIdx.x];
             L.gf[128 + threadIdx.x] = P.cn_x[threadIdx.x]; L.gf[192 + threadIdx.x] = P.cn_y[threadIdx.x];
+            L.ca_lb[threadIdx.x] = P.ca_lb[threadIdx.x];
         }
         if (threadIdx.x < 9) {
             const int k = threadIdx.x;
@@ -1232,7 +1234,7 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
 #endif
         R T_full = P.T_e + (P.p_e - patm) * P.A_e;
         R qS = q * P.S_gf;
-        R Ca = grid_fin_ca<R>(P, L.gf, L.gf + 64, mach);
+        R Ca = grid_fin_ca<R>(P, L.gf, L.gf + 64, mach, L.ca_lb);
         R cfp, cfperp, cm, mdot_dt, md_info, thr_info;
         // info of the grid-fin ACS (acs_model.py:62-86): deflections, C_n of both fins, forces
         R i_dl = R(0), i_dr = R(0), i_cnl = R(0), i_cnr = R(0), i_gfperp = R(0), i_gfpar = R(0), i_gfm = R(0);
