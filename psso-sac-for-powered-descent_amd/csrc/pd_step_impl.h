@@ -1647,24 +1647,27 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
     k_have = !ended;
 #endif
     if (role == 0 && live) {
+        // (loop-invariant addresses from a laundered offset: formed here, not held across the loop)
+        uint32_t uo = ui;
+        asm volatile("" : "+v"(uo));
         if (a.obs) {
             // the wrappers' observation (obs_write kinds); compile-time for the landing burns
             constexpr int kind = RTD == 1 ? (PHASE == 0 ? 1 : 2) : (PHASE == 0 ? 0 : (PHASE == 1 ? 3 : -1));
             const int ok = kind >= 0 ? kind : P2.obs_kind;
-            obs_write<R>(P2, ok, s, a.obs + fo * obs_dim(ok), ui);
+            obs_write<R>(P2, ok, s, a.obs + fo * obs_dim(ok), uo);
         }
         if (a.reward) ev(a.reward + fo, ui) = rew;
         if constexpr (POL) {
             // objective_function: episode_reward -= reward until done or truncated (env_wrapped_ea.py:200-222)
-            ev(a.reward_sum, ui) -= rew;
-            if (dn || tr) ev(a.b.fin, ui) = 1;
+            ev(a.reward_sum, uo) -= rew;
+            if (dn || tr) ev(a.b.fin, uo) = 1;
         } else if (a.reward_sum) {
-            ev(a.reward_sum, ui) += rew;
+            ev(a.reward_sum, uo) += rew;
         }
         if (a.done) ev(a.done + fo, ui) = (uint8_t)dn;
         if (a.trunc) ev(a.trunc + fo, ui) = (uint8_t)tr;
         if (a.trunc_id) ev(a.trunc_id + fo, ui) = (int8_t)id;
-        if (a.info) ev(a.info + (PD_INFO_GLOAD) * N, ui) = gl;
+        if (a.info) ev(a.info + (PD_INFO_GLOAD) * N, uo) = gl;
     }
     // ---- the env's bookkeeping for the next step: auto-reset in registers, or carry on
     if (ended) {
