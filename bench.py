@@ -214,14 +214,23 @@ def main():
     ap.add_argument("--no-wind", action="store_true")
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--secondary", type=int, default=1, help="also time the other precision")
-    ap.add_argument("--workload", choices=["c3", "c4", "c5"], default="c3",
-                    help="c3: env-steps/s headline; c4: PSO generations with the fused actor; "
+    ap.add_argument("--workload", choices=["c2", "c3", "c4", "c5"], default="c3",
+                    help="c3: env-steps/s headline; c2: 4096 envs, no wind, no tilt (--integrator); "
+                         "c4: PSO generations with the fused actor; "
                          "c5: SAC collection (actor + env + RCCL transition gather + replay buffer)")
+    ap.add_argument("--integrator", choices=["reference", "rk4"], default="reference",
+                    help="rk4: BASELINE c2's RK4 dt=0.01 s, NOT the reference's integrator (non-parity)")
     ap.add_argument("--particles", type=int, default=32768, help="c4: particles per GPU")
     ap.add_argument("--fuse", type=int, default=16,
                     help="c3: env-steps per k_step launch (pd_step_n; 1 = one pd_step launch per step)")
     ap.add_argument("--graph", type=int, default=1, help="c5: replay the collection step as a HIP graph")
     args = ap.parse_args()
+    if args.workload == "c2":
+        args.no_wind = True
+        if args.envs == 65536:
+            args.envs = 4096
+    if args.integrator == "rk4" and args.workload != "c2":
+        ap.error("--integrator rk4 is the non-parity c2 mode: use --workload c2")
 
     import torch
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -253,7 +262,8 @@ def main():
         env = pdenv.PoweredDescentEnv(
             n, flight_phase=args.phase, mode=mode, precision=precision, device=local,
             enable_wind=not args.no_wind, stochastic_wind=not args.no_wind, wind_percentile=None,
-            auto_reset=True, tilt_sigma_rad=math.radians(1.0), seed=1234, env_offset=shard_offset(rank, n))
+            auto_reset=True, tilt_sigma_rad=0.0 if args.workload == "c2" else math.radians(1.0), seed=1234,
+            env_offset=shard_offset(rank, n), integrator=args.integrator)
         env.flush_every = 16
         T = args.warmup + args.steps
         F = max(1, args.fuse)
@@ -322,7 +332,7 @@ def main():
     traffic = None
     mix = None
     pmc = os.path.join(REPO, "profiles", "pmc_traffic.json")
-    if os.path.exists(pmc):
+    if os.path.exists(pmc) and args.workload == "c3":   # the committed PMC passes profile c3
         try:
             summ = json.load(open(pmc))
             # PMC figures are per launch of the profiled run's env-steps-per-launch: rescale to F
@@ -346,9 +356,14 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": args.precision,
-        "data": "synthetic (uniform float32 random actions in HBM; reference initial state + N(0,1deg) pitch tilt)",
+        "data": "synthetic (uniform float32 random actions in HBM; reference initial state" +
+                (" + N(0,1deg) pitch tilt)" if args.workload == "c3" else ")"),
         "config": {"workload": "c3: 65536 envs/GPU, landing_burn_pure_throttle, rtd_rl reward, wind (VK gusts + "
-                               "percentile profile) + tilt, auto-reset",
+                               "percentile profile) + tilt, auto-reset" if args.workload == "c3" else
+                               f"c2: {main_res['n']} envs/GPU, landing_burn_pure_throttle, rtd_rl reward, no wind, "
+                               f"no tilt, auto-reset, integrator {args.integrator}" +
+                               (" (RK4 dt=0.01 s: NOT the reference's integrator, non-parity)"
+                                if args.integrator == "rk4" else " (semi-implicit Euler 4 x 0.025 s)"),
                    "envs_per_gpu": main_res["n"], "global_envs": n_total, "parallelism": f"env-shard x{world}"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": 8000.0, "unit": "GB/s",
                      "frac": achieved / 8000.0, "traffic": traffic,
@@ -366,7 +381,7 @@ def main():
         op = "f32" if args.precision == "f64" else "f64"
         out["secondary"] = {"dtype": op, "value": whole_job_rate(other["n"], world, args.steps, other["wall"]),
                             "kernel_avg_ms": other["kern_avg_ms"]}
-    if args.cpu_baseline and world == 1:
+    if args.cpu_baseline and world == 1 and args.workload == "c3":
         sys.path.insert(0, os.path.join(REPO, "oracle"))
         import numpy as np
         import oracle

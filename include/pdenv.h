@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define PD_ABI_VERSION 3
+#define PD_ABI_VERSION 4   /* 4: pd_config.integrator (was padding) */
 #define PD_MAX_PTS 256      /* aero scatter points per table */
 #define PD_MAX_COLS 5       /* AoA columns per aero table */
 #define PD_MAX_TAB 64       /* grid-fin table length */
@@ -64,6 +64,15 @@ typedef enum {
  * arity mismatch in rtd_pso.py:38,107,141). */
 typedef enum { PD_RTD_RL = 0, PD_RTD_PSO = 1, PD_RTD_NONE = 2 } pd_rtd;
 typedef enum { PD_F64 = 0, PD_F32 = 1 } pd_precision;
+/* Integrator of the physics sub-steps.  PD_INTEG_REFERENCE is the reference's semi-implicit Euler
+ * (compile_physics, rockets_physics.py:909-957 / 803-861) and the only mode with reference
+ * parity.  PD_INTEG_RK4 is NOT the reference: BASELINE config c2's "RK4 dt=0.01 s" (SURVEY 8(d)
+ * c2, "benchmarked separately, labelled non-parity"), classical RK4 over (x, y, vx, vy, theta,
+ * theta_dot, mass, mass_propellant) with rocket_physics_fcn's forces at every stage, 10 x 0.01 s
+ * per 0.1 s env step; landing_burn_pure_throttle without wind only (the von Karman gusts are a
+ * discrete-time process), no policy rollouts.  Checked against the oracle's restatement
+ * (orc_physics, ORC_INTEG_RK4), not against the reference. */
+typedef enum { PD_INTEG_REFERENCE = 0, PD_INTEG_RK4 = 1 } pd_integrator;
 
 /* One neighbourhood-aero table: scatter points grouped by AoA column, Mach-sorted inside. */
 typedef struct {
@@ -139,7 +148,8 @@ typedef struct {
     double dt;                 /* physics dt of phases 2..6, compile_physics(dt, phase) (0 = the env's 0.1) */
     double discount_factor;    /* rtd_rl landing_burn reward scale (1-g)/(1-g^L) and the Pcontrol
                                   alive bonus 0.01 (1-g) (rtd_rl.py:267, 472); rl_wrapped_env_pytorch kwargs */
-    int32_t trajectory_length, pad3;
+    int32_t trajectory_length;
+    int32_t integrator;        /* pd_integrator (ABI 4; 0 = the reference's) */
 } pd_config;
 
 /* Info tap of pd_step: the quantities of the LAST physics sub-step that rocket_physics_fcn puts in

@@ -22,6 +22,7 @@ I32 = C.c_int32
 
 PURE_THROTTLE, LANDING_BURN, PCONTROL, BALLISTIC, FLIP, SUBSONIC, SUPERSONIC = range(7)
 RTD_RL, RTD_PSO, RTD_NONE = 0, 1, 2
+INTEG_REFERENCE, INTEG_RK4 = 0, 1   # pd_oracle.h ORC_INTEG_*
 PHASE_NAMES = ["landing_burn_pure_throttle", "landing_burn", "landing_burn_pure_throttle_Pcontrol",
                "ballistic_arc_descent", "flip_over_boostbackburn", "subsonic", "supersonic"]
 ACTION_DIM = [1, 4, 1, 1, 1, 2, 2]
@@ -74,7 +75,7 @@ class OrcEnv(C.Structure):
                 ("fu", D * 2), ("fv", D * 2), ("noise_slotted", I32), ("noise_used", I32), ("dt", D),
                 ("rng_philox", I32), ("wind_prof", I32), ("rng_g", C.c_uint64), ("rng_ep", C.c_uint32),
                 ("rng_ts", C.c_uint32), ("seed_lo", C.c_uint32), ("seed_hi", C.c_uint32),
-                ("cur_sub", I32), ("pad3", I32)]
+                ("cur_sub", I32), ("integrator", I32)]
 
 
 class OrcOut(C.Structure):
@@ -224,8 +225,9 @@ class Oracle:
 
     def __init__(self, phase=PURE_THROTTLE, rtd=RTD_RL, wind=False, stochastic=False,
                  sigma_u=0.0, sigma_v=0.0, wind_percentile=50, pack=None, discount_factor=0.99,
-                 trajectory_length=100, dt=0.0):
+                 trajectory_length=100, dt=0.0, integrator=0):
         self.L = lib()
+        self.integrator = int(integrator)   # INTEG_RK4: the non-parity RK4 mode (orc_physics)
         self.P = make_params(pack, wind_percentile)
         self.P.rl_discount, self.P.rl_traj_len = float(discount_factor), int(trajectory_length)
         self.dt = float(dt)
@@ -242,6 +244,7 @@ class Oracle:
                          float(self.su), float(self.sv))
         self.E.noise_slotted = int(getattr(self, "slotted", 0))
         self.E.dt = self.dt
+        self.E.integrator = self.integrator
         return np.array(self.E.s[:])
 
     @property

@@ -369,8 +369,11 @@ static void vk_step(const double* Ad, const double* Bd, double sigma, double* s,
  * rocket_physics_fcn (rockets_physics.py:455-704) with the landing-burn control laws
  * force_moment_decomposer_landing_burn_throttle_only (:340-400) and
  * force_moment_decomposer_landing_burn_gimballed (:168-269). */
+/* One rocket_physics_fcn call (rockets_physics.py:455-704).  kout == NULL: the reference's
+ * semi-implicit Euler update of E->s at dt.  kout != NULL (the non-parity RK4 mode): E->s is left
+ * alone and kout receives d/dt of (x, y, vx, vy, theta, theta_dot, mass, mass_propellant). */
 static void substep(const orc_params* P, orc_env* E, int phase, const double* u, int f32,
-                    double dt, double dt_act, const double* noise2, double* info) {
+                    double dt, double dt_act, const double* noise2, double* info, double* kout) {
     double* s = E->s;
     double x = s[0], y = s[1], vx = s[2], vy = s[3], th = s[4], thd = s[5], ga = s[6], al = s[7];
     double m = s[8], mp = s[9], t = s[10];
@@ -619,17 +622,12 @@ static void substep(const orc_params* P, orc_env* E, int phase, const double* u,
         fx = aero_x + cfx + Fwx; fy = aero_y + cfy + Fwy;
     }
     double vxd = fx / m, vyd = fy / m - g;
-    vx += vxd * dt; vy += vyd * dt; x += vx * dt; y += vy * dt;
     double mz_tot = cm + aero_m + Mw;
     double thdd = mz_tot / inertia;
-    thd += thdd * dt; th += thd * dt;
-    ga = atan2(vy, vx);
-    if (th > 2 * PI) th -= 2 * PI;
-    if (ga < 0) ga = 2 * PI + ga;
-    al = th - ga;
-    mp -= mdot_dt; m -= mdot_dt; t += dt;
-    s[0] = x; s[1] = y; s[2] = vx; s[3] = vy; s[4] = th; s[5] = thd; s[6] = ga; s[7] = al;
-    s[8] = m; s[9] = mp; s[10] = t;
+    if (kout) {
+        kout[0] = vx; kout[1] = vy; kout[2] = vxd; kout[3] = vyd; kout[4] = thd; kout[5] = thdd;
+        kout[6] = -mdot_info; kout[7] = -mdot_info;
+    }
     if (info) {
         info[ORC_I_RHO] = rho; info[ORC_I_P] = patm; info[ORC_I_A] = a; info[ORC_I_MACH] = mach;
         info[ORC_I_Q] = q; info[ORC_I_CL] = CL; info[ORC_I_CD] = CD; info[ORC_I_MDOT] = mdot_info;
@@ -640,6 +638,16 @@ static void substep(const orc_params* P, orc_env* E, int phase, const double* u,
         info[ORC_I_GIMBAL_DEG] = gimbal_deg_out; info[ORC_I_DCMD_L] = ac.dcmd_l; info[ORC_I_DCMD_R] = ac.dcmd_r;
         info[ORC_I_DRAG] = drag; info[ORC_I_LIFT] = lift;
     }
+    if (kout) return;
+    vx += vxd * dt; vy += vyd * dt; x += vx * dt; y += vy * dt;
+    thd += thdd * dt; th += thd * dt;
+    ga = atan2(vy, vx);
+    if (th > 2 * PI) th -= 2 * PI;
+    if (ga < 0) ga = 2 * PI + ga;
+    al = th - ga;
+    mp -= mdot_dt; m -= mdot_dt; t += dt;
+    s[0] = x; s[1] = y; s[2] = vx; s[3] = vy; s[4] = th; s[5] = thd; s[6] = ga; s[7] = al;
+    s[8] = m; s[9] = mp; s[10] = t;
 }
 
 int orc_physics(const orc_params* P, orc_env* E, int phase, const double* u, int f32,
@@ -648,17 +656,53 @@ int orc_physics(const orc_params* P, orc_env* E, int phase, const double* u, int
      * landing_burn physics dt = 0.1 x4 with actuator dt 0.025 (:803-861) */
     double dt = phase == ORC_PHASE_PURE_THROTTLE ? 0.025 : 0.1;
     E->noise_used = 0;
+    if (E->integrator == ORC_INTEG_RK4) {
+        /* NOT the reference's integrator: BASELINE config c2's "RK4 dt=0.01 s" (SURVEY 8(d) c2),
+         * classical RK4 over (x, y, vx, vy, theta, theta_dot, mass, mass_propellant) with the
+         * forces of rocket_physics_fcn at each stage, 10 x 0.01 s per 0.1 s env step; gamma and
+         * alpha follow the stage velocity (gamma = atan2(vy, vx) in [0, 2 pi), alpha = theta -
+         * gamma), theta wrapped once per 0.01 s.  Pure throttle without wind only.  libpdenv's
+         * k_step<..., RK4> runs the same operations in the same order. */
+        if (phase != ORC_PHASE_PURE_THROTTLE || E->wind_on) return -1;
+        static const int idx[8] = {0, 1, 2, 3, 4, 5, 8, 9};
+        /* h: 0.01 s; E->dt > 0 overrides it (convergence tests), 0.1 / h steps */
+        const double h = E->dt > 0 ? E->dt : 0.01;
+        const int n_rk = (int)llround(0.1 / h);
+        double* s = E->s;
+        for (int n = 0; n < n_rk; ++n) {
+            double b[8], acc[8], k[8];
+            for (int i = 0; i < 8; ++i) b[i] = s[idx[i]];
+            for (int st = 0; st < 4; ++st) {
+                E->cur_sub = 4 * n + st;
+                substep(P, E, phase, u, f32, h, 0.025, NULL, info, k);
+                for (int i = 0; i < 8; ++i)
+                    acc[i] = st == 0 ? k[i] : (st == 3 ? acc[i] + k[i] : acc[i] + 2.0 * k[i]);
+                if (st < 3) {
+                    const double c = st == 2 ? h : 0.5 * h;
+                    for (int i = 0; i < 8; ++i) s[idx[i]] = b[i] + c * k[i];
+                } else {
+                    for (int i = 0; i < 8; ++i) s[idx[i]] = b[i] + (h / 6.0) * acc[i];
+                    if (s[4] > 2 * PI) s[4] -= 2 * PI;
+                    s[10] += h;
+                }
+                double ga = atan2(s[3], s[2]);
+                if (ga < 0) ga = 2 * PI + ga;
+                s[6] = ga; s[7] = s[4] - ga;
+            }
+        }
+        return 0;
+    }
     if (phase >= ORC_PHASE_PCONTROL) {
         /* the other phases: one call of rocket_physics_fcn at the env dt (:728-802, :959-997);
          * actuator filters at the same dt */
         double d = E->dt > 0 ? E->dt : 0.1;
         E->cur_sub = 0;
-        substep(P, E, phase, u, f32, d, d, noise, info);
+        substep(P, E, phase, u, f32, d, d, noise, info, NULL);
         return 0;
     }
     for (int k = 0; k < 4; ++k) {
         E->cur_sub = k;
-        substep(P, E, phase, u, f32, dt, 0.025, noise ? (E->noise_slotted ? noise + 2 * k : noise) : NULL, info);
+        substep(P, E, phase, u, f32, dt, 0.025, noise ? (E->noise_slotted ? noise + 2 * k : noise) : NULL, info, NULL);
     }
     if (phase == ORC_PHASE_LANDING_BURN && info) {
         /* base_environment.py:122-124: prevs <- filtered gimbal, fin COMMANDS */

@@ -25,12 +25,19 @@ constexpr bool KW = PD_KW != 0;
 
 // RL and PD_RTD_NONE share the RL instantiation; PSO exists for the two landing burns, with the
 // policy-rollout (fused actor) kernels.  -DPD_KLPE=n (experiments): the RL kernel at n lanes only.
-#ifdef PD_KLPE
+#if defined(PD_KRK4)
+// the non-parity RK4 mode (pure throttle, no wind; -DPD_KPH=0 -DPD_KW=0): LPE 2 and 16
+static_assert(PD_KPH == 0 && PD_KW == 0, "RK4 unit: pure throttle without wind");
+template void launch_step<KR, 0, 0, false, 2, true>(const StepArgs<KR>&, hipStream_t);
+template void launch_step<KR, 0, 0, false, 16, true>(const StepArgs<KR>&, hipStream_t);
+template void launch_step<KR, 0, 1, false, 2, true>(const StepArgs<KR>&, hipStream_t);
+template void launch_step<KR, 0, 1, false, 16, true>(const StepArgs<KR>&, hipStream_t);
+#elif defined(PD_KLPE)
 template void launch_step<KR, PD_KPH, 0, KW, PD_KLPE>(const StepArgs<KR>&, hipStream_t);
 #else
 PD_INST_STEP(0)
 #endif
-#if PD_KPH < 2 && !defined(PD_KLPE)
+#if PD_KPH < 2 && !defined(PD_KLPE) && !defined(PD_KRK4)
 PD_INST_STEP(1)
 template void launch_policy_lpe<KR, PD_KPH, KW, 2>(const StepArgs<KR>&, int64_t, hipStream_t);
 template void launch_policy_lpe<KR, PD_KPH, KW, 4>(const StepArgs<KR>&, int64_t, hipStream_t);

@@ -103,7 +103,7 @@ template <typename R> struct StepArgs {
 };
 
 // Kernel launchers, explicitly instantiated in the kstep_*.hip translation units.
-template <typename R, int PH, int RT, bool W, int LPE> void launch_step(const StepArgs<R>& a, hipStream_t s);
+template <typename R, int PH, int RT, bool W, int LPE, bool RK = false> void launch_step(const StepArgs<R>& a, hipStream_t s);
 template <typename R, int PH, bool W, int LPE> void launch_policy_lpe(const StepArgs<R>& a, int64_t n_launch,
                                                                       hipStream_t s);
 

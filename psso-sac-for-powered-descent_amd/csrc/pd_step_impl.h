@@ -861,7 +861,11 @@ __device__ __forceinline__ TabView<R> tab_view(DP<R>& P, const R* tab, int table
 // envs).  The env's state is loaded once into registers (its g-load ring into LDS), the steps
 // run in registers with their per-step outputs written as they go (row f of every [F][N]
 // output), auto-reset happens in registers, and the state is stored once at the end.
-template <typename R, int PHASE, int RTD, bool WIND, int LPE, int POL = 0>
+// RK4 (pd_config.integrator = PD_INTEG_RK4, pure throttle without wind): NOT the reference's
+// integrator -- BASELINE config c2's "RK4 dt=0.01 s", classical RK4 over (x, y, vx, vy, theta,
+// theta_dot, m, m_prop) with rocket_physics_fcn's forces at each stage, 10 x 0.01 s per env step;
+// the loop body below runs once per stage (oracle: orc_physics, ORC_INTEG_RK4, same order)
+template <typename R, int PHASE, int RTD, bool WIND, int LPE, int POL = 0, bool RK4 = false>
 // waves_per_eu(2): caps VGPR+AGPR at 256 so the f64 kernel keeps two waves per SIMD
 #ifndef PD_WPE
 #define PD_WPE 2
@@ -991,8 +995,9 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
     const int AD = PHASE == 2 ? (ascent ? 2 : 1) : A;   // row stride of the action array
     // pure throttle 4 x 0.025 s, landing_burn 4 x 0.1 s (actuators 0.025 s); the other phases
     // one call of rocket_physics_fcn at dt, actuators at the same dt (rockets_physics.py:728-997)
-    constexpr int NSUB = PHASE == 2 ? 1 : 4;
-    const R dt = PHASE == 0 ? R(0.025) : (PHASE == 1 ? R(0.1) : (R)a.dt_aux);
+    static_assert(!RK4 || (PHASE == 0 && !WIND && !POL), "RK4: pure throttle, no wind, no policy");
+    constexpr int NSUB = RK4 ? 40 : (PHASE == 2 ? 1 : 4);
+    const R dt = RK4 ? R(0.01) : (PHASE == 0 ? R(0.025) : (PHASE == 1 ? R(0.1) : (R)a.dt_aux));
     const R dt_act = PHASE == 2 ? dt : R(0.025);
     PD_T(t_loaded);
     PD_ACC(1, t_loaded - t_staged);
@@ -1086,9 +1091,11 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
         ev(a.info + (size_t)k * (size_t)N, u) = v;
     };
 
+    R rkb[8], rka[8];   // RK4: the 0.01 s step's base state and its k1 + 2 k2 + 2 k3 + k4
 #pragma unroll 1
     for (int sub = 0; sub < NSUB; ++sub) {
         PD_T(t_sub);
+        const int stage = RK4 ? (sub & 3) : 0;
         DP<R>& P = *params<R>(a.P);
         const bool tap_sub = tap && sub == NSUB - 1;
         R x = e.s[0], y = e.s[1], vx = e.s[2], vy = e.s[3], th = e.s[4], thd = e.s[5], ga = e.s[6], al = e.s[7];
@@ -1444,6 +1451,24 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
         div_pair<LPE, R>(mz, I, P.grav_R, P.grav_R + y, role, thdd, grq);
         const R gr = P.grav_g0 * (grq * grq);
         const R vyd = vyq - gr;
+        if constexpr (RK4) {
+            const R kd[8] = {vx, vy, vxd, vyd, thd, thdd, -md_info, -md_info};
+            R sv[8] = {x, y, vx, vy, th, thd, m, mp};
+            if (stage == 0) {
+#pragma unroll
+                for (int k = 0; k < 8; ++k) rkb[k] = sv[k];
+            }
+#pragma unroll
+            for (int k = 0; k < 8; ++k) rka[k] = stage == 0 ? kd[k] : (stage == 3 ? rka[k] + kd[k] : rka[k] + R(2) * kd[k]);
+            const R c = stage == 3 ? dt / R(6) : (stage == 2 ? dt : R(0.5) * dt);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) sv[k] = rkb[k] + c * (stage == 3 ? rka[k] : kd[k]);
+            x = sv[0]; y = sv[1]; vx = sv[2]; vy = sv[3]; th = sv[4]; thd = sv[5]; m = sv[6]; mp = sv[7];
+            if (stage == 3 && th > Cst<R>::two_pi) th -= Cst<R>::two_pi;
+            ga = atan2(vy, vx);
+            if (ga < R(0)) ga = Cst<R>::two_pi + ga;
+            al = th - ga;
+        } else {
         vx += vxd * dt; vy += vyd * dt; x += vx * dt; y += vy * dt;
         thd += thdd * dt; th += thd * dt;
         ga = atan2(vy, vx);
@@ -1451,12 +1476,14 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
         if (ga < R(0)) ga = Cst<R>::two_pi + ga;
         al = th - ga;
         mp -= mdot_dt; m -= mdot_dt;
+        }
         if (tap_sub) {
             info(PD_INFO_CF_X, cfx); info(PD_INFO_CF_Y, cfy); info(PD_INFO_GRAVITY, gr); info(PD_INFO_VX_DOT, vxd);
             info(PD_INFO_VY_DOT, vyd); info(PD_INFO_MOMENTS, mz); info(PD_INFO_THETA_DDOT, thdd);
         }
         e.s[0] = x; e.s[1] = y; e.s[2] = vx; e.s[3] = vy; e.s[4] = th; e.s[5] = thd; e.s[6] = ga; e.s[7] = al;
-        e.s[8] = m; e.s[9] = mp; e.s[10] = e.s[10] + dt;
+        e.s[8] = m; e.s[9] = mp;
+        if (!RK4 || stage == 3) e.s[10] = e.s[10] + dt;
         PD_T(t_subend);
         PD_ACC(4, t_subend - t_aero1);
     }
@@ -1721,9 +1748,9 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
 }
 
 // ---------------------------------------------------------------- launchers
-template <typename R, int PH, int RT, bool W, int LPE> void launch_step(const StepArgs<R>& a, hipStream_t s) {
+template <typename R, int PH, int RT, bool W, int LPE, bool RK> void launch_step(const StepArgs<R>& a, hipStream_t s) {
     unsigned grid = (unsigned)((a.n * LPE + kStepBlock - 1) / kStepBlock);
-    hipLaunchKernelGGL((k_step<R, PH, RT, W, LPE>), dim3(grid), dim3(kStepBlock), 0, s, a);
+    hipLaunchKernelGGL((k_step<R, PH, RT, W, LPE, 0, RK>), dim3(grid), dim3(kStepBlock), 0, s, a);
 }
 
 template <typename R, int PH, bool W, int LPE> void launch_policy_lpe(const StepArgs<R>& a, int64_t n_launch,

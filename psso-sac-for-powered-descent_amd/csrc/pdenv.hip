@@ -866,6 +866,10 @@ pd_status validate(const pd_params* p, const pd_config* c) {
             return fail(PD_ERR_INVALID, "ascent phases need the reference trajectory (ref_y/x/vx/vy, n_ref >= 2)");
     }
     if (c->precision != PD_F64 && c->precision != PD_F32) return fail(PD_ERR_INVALID, "bad precision");
+    if (c->integrator != PD_INTEG_REFERENCE && c->integrator != PD_INTEG_RK4) return fail(PD_ERR_INVALID, "bad integrator");
+    if (c->integrator == PD_INTEG_RK4 && (c->phase != PD_PHASE_PURE_THROTTLE || c->enable_wind))
+        return fail(PD_ERR_UNSUPPORTED, "the RK4 integrator (non-parity, BASELINE c2) exists for "
+                                        "landing_burn_pure_throttle without wind only");
     // the neighbourhood payloads carry each pair slot's column AoA as a byte (pd_common.h)
     for (const pd_aero_table* t : {&p->cd, &p->cl})
         for (int k = 0; k < t->n_cols; ++k)
@@ -1041,6 +1045,11 @@ template <typename R> void dispatch_step(const pd_env* e, const StepArgs<R>& a, 
     int ph = e->cfg.phase, l = e->lpe;
     bool pso = e->cfg.rtd == PD_RTD_PSO;   // RL and NONE share the RL instantiation (NONE zeroes the rtd)
     bool w = e->cfg.enable_wind != 0;
+    if (e->cfg.integrator == PD_INTEG_RK4) {   // pure throttle, no wind (validated); LPE 2 or 16
+        if (pso) { if (l <= 2) launch_step<R, 0, 1, false, 2, true>(a, s); else launch_step<R, 0, 1, false, 16, true>(a, s); }
+        else { if (l <= 2) launch_step<R, 0, 0, false, 2, true>(a, s); else launch_step<R, 0, 0, false, 16, true>(a, s); }
+        return;
+    }
     if (ph == 0 && !pso) { if (w) launch_lpe<R, 0, 0, true>(l, a, s); else launch_lpe<R, 0, 0, false>(l, a, s); }
     else if (ph == 0) { if (w) launch_lpe<R, 0, 1, true>(l, a, s); else launch_lpe<R, 0, 1, false>(l, a, s); }
     else if (ph == 1 && pso) { if (w) launch_lpe<R, 1, 1, true>(l, a, s); else launch_lpe<R, 1, 1, false>(l, a, s); }
@@ -1224,6 +1233,7 @@ pd_status pd_create(const pd_params* params, const pd_config* cfg, pd_env** out)
                                      : (cfg->n_envs <= 4096 ? 16 : (cfg->n_envs <= 8192 ? 8 : (cfg->n_envs <= 16384 ? 4 : 2)));
     if (const char* lv = getenv("PDENV_LPE"); lv && *lv && cfg->lanes_per_env == 0) e->lpe = atoi(lv);   // experiments
     if (e->lpe != 1 && e->lpe != 2 && e->lpe != 4 && e->lpe != 8 && e->lpe != 16) { delete e; return fail(PD_ERR_INVALID, "lanes_per_env must be 0, 1, 2, 4, 8 or 16"); }
+    if (cfg->integrator == PD_INTEG_RK4) e->lpe = e->lpe <= 2 ? 2 : 16;   // the RK4 instantiations
     st = cfg->precision == PD_F64 ? create_impl<double>(params, cfg, e) : create_impl<float>(params, cfg, e);
     if (st != PD_OK) { pd_destroy(e); return st; }
     *out = e;
@@ -1292,6 +1302,7 @@ pd_status pd_rollout_policy(pd_env* e, const float* weights, int32_t n_params, i
                             int32_t* steps, int32_t check_every, void* stream) {
     if (!e || !weights || !fitness || max_steps < 0) return fail(PD_ERR_INVALID, "bad policy rollout args");
     if (e->cfg.rtd != PD_RTD_PSO) return fail(PD_ERR_UNSUPPORTED, "policy rollouts need rtd = PD_RTD_PSO");
+    if (e->cfg.integrator != PD_INTEG_REFERENCE) return fail(PD_ERR_UNSUPPORTED, "policy rollouts use the reference integrator");
     int want = e->cfg.phase == PD_PHASE_PURE_THROTTLE ? PD_ACTOR_PARAMS_PURE_THROTTLE : PD_ACTOR_PARAMS_LANDING_BURN;
     if (n_params != want) return fail(PD_ERR_INVALID, "n_params does not match the phase's actor");
     PD_HIP(hipSetDevice(e->device));

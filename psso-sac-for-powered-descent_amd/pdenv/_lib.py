@@ -77,7 +77,7 @@ class PdConfig(C.Structure):
                 ("seed", U64), ("env_offset", U64), ("enable_wind", I32), ("stochastic_wind", I32),
                 ("wind_percentile", I32), ("auto_reset", I32), ("tilt_sigma_rad", D),
                 ("action_f64", I32), ("lanes_per_env", I32),
-                ("dt", D), ("discount_factor", D), ("trajectory_length", I32), ("pad3", I32)]
+                ("dt", D), ("discount_factor", D), ("trajectory_length", I32), ("integrator", I32)]
 
 
 EXPORTS = ["pd_abi_version", "pd_sizeof_params", "pd_sizeof_config", "pd_last_error", "pd_device_count", "pd_create",
@@ -86,7 +86,7 @@ EXPORTS = ["pd_abi_version", "pd_sizeof_params", "pd_sizeof_config", "pd_last_er
            "pd_set_gload_window", "pd_get_gload_window", "pd_set_wind_sigmas", "pd_get_wind_state",
            "pd_set_wind_state", "pd_get_counters", "pd_set_counters", "pd_checkpoint_size", "pd_checkpoint_save",
            "pd_checkpoint_load", "pd_counters", "pd_stats", "pd_atmosphere", "pd_obs_dim", "pd_action_dim"]
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 _lib = None
 

@@ -30,6 +30,9 @@ def units(extra=()):
     for r, ph, w in KSTEP:
         u.append((os.path.join(OBJ, f"kstep_r{r}_p{ph}_w{w}.o"), "kstep.hip",
                   [f"-DPD_KR={r}", f"-DPD_KPH={ph}", f"-DPD_KW={w}"]))
+    for r in (0, 1):   # the non-parity RK4 kernels (pure throttle, no wind) in units of their own
+        u.append((os.path.join(OBJ, f"kstep_r{r}_rk4.o"), "kstep.hip", [f"-DPD_KR={r}", "-DPD_KPH=0", "-DPD_KW=0",
+                                                                        "-DPD_KRK4=1"]))
     return [(o, os.path.join(CSRC, s), list(d) + list(extra)) for o, s, d in u]
 
 

@@ -22,6 +22,7 @@ PHASES = {"landing_burn_pure_throttle": L.PURE_THROTTLE, "landing_burn": L.LANDI
           "landing_burn_ACS": L.LANDING_BURN_ACS}
 # 'physics': compile_physics stepping only (reward 0, never done/truncated)
 MODES = {"rl": L.RTD_RL, "pso": L.RTD_PSO, "physics": L.RTD_NONE}
+INTEGRATORS = {"reference": 0, "rk4": 1}   # pd_integrator (PD_INTEG_REFERENCE, PD_INTEG_RK4)
 # (phase, mode) pairs whose reference env raises TypeError at the first step (include/pdenv.h)
 UNSTEPPABLE = {("landing_burn_ACS", m) for m in MODES} | {("flip_over_boostbackburn", "rl")} | \
     {(p, "pso") for p in PHASES if p not in ("landing_burn_pure_throttle", "landing_burn")}
@@ -39,7 +40,10 @@ class PoweredDescentEnv:
     def __init__(self, n_envs, flight_phase="landing_burn_pure_throttle", mode="rl", precision="f64",
                  device=0, enable_wind=False, stochastic_wind=False, wind_percentile=50,
                  auto_reset=False, tilt_sigma_rad=0.0, seed=0, env_offset=0, action_f64=False,
-                 params=None, lanes_per_env=0, dt=0.0, discount_factor=0.99, trajectory_length=100):
+                 params=None, lanes_per_env=0, dt=0.0, discount_factor=0.99, trajectory_length=100,
+                 integrator="reference"):
+        # integrator "rk4": NOT the reference's (semi-implicit Euler) -- BASELINE config c2's
+        # "RK4 dt=0.01 s", pure throttle without wind only; see include/pdenv.h pd_integrator
         if flight_phase not in PHASES:
             raise ValueError(f"flight_phase must be one of {list(PHASES)} (got {flight_phase!r})")
         if mode not in MODES:
@@ -79,6 +83,10 @@ class PoweredDescentEnv:
         cfg.dt = float(dt)
         cfg.discount_factor = float(discount_factor) if discount_factor is not None else 0.0
         cfg.trajectory_length = int(trajectory_length) if trajectory_length is not None else 0
+        if integrator not in INTEGRATORS:
+            raise ValueError(f"integrator must be one of {list(INTEGRATORS)} (got {integrator!r})")
+        cfg.integrator = INTEGRATORS[integrator]
+        self.integrator = integrator
         self.cfg = cfg
         handle = C.c_void_p()
         with torch.cuda.device(self.device):
