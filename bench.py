@@ -242,7 +242,9 @@ def main():
     if backend != "nccl":
         local %= max(1, torch.cuda.device_count())
     dist = None
-    if world > 1:
+    # PD_BENCH_DIST=1: initialise the process group (and run every collective) even at one rank,
+    # to exercise the RCCL path on a single GPU
+    if world > 1 or os.environ.get("PD_BENCH_DIST") == "1":
         import torch.distributed as dist
         torch.cuda.set_device(local)
         if backend == "nccl":

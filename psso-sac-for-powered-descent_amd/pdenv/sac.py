@@ -154,7 +154,7 @@ def transition_slab(obs, action, reward, next_obs, done):
 
 def gather_slabs(slab, dist=None):
     """All ranks' slabs concatenated in rank order (all_gather_into_tensor; RCCL on GPU ranks)."""
-    if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
+    if dist is None or not dist.is_initialized():
         return slab
     out = torch.empty((dist.get_world_size() * slab.shape[0], slab.shape[1]), dtype=slab.dtype,
                       device=slab.device)
