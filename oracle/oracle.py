@@ -115,6 +115,7 @@ def lib():
         L.orc_inertia.argtypes = [P(OrcParams), D, P(D), P(D)]
         L.orc_reset.restype = None
         L.orc_reset.argtypes = [P(OrcParams), P(OrcEnv), P(D), C.c_int, C.c_int, D, D]
+        L.orc_wind_at.restype = D; L.orc_wind_at.argtypes = [P(OrcParams), C.c_int, D]
         L.orc_step.restype = C.c_int
         L.orc_step.argtypes = [P(OrcParams), P(OrcEnv), C.c_int, C.c_int, P(D), C.c_int, P(D), P(OrcOut)]
         L.orc_physics.restype = C.c_int

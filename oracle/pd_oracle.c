@@ -277,6 +277,15 @@ static double wind_profile(const orc_params* P, const orc_env* E, double y) {
     return np_interp(xa, ya, n, km);
 }
 
+/* The profile of percentile 50 + prof at altitude y (m): the interpolation wind_profile uses
+ * (tests against HorizontalWindSpeed.compile_horizontal_fixed_wind) */
+double orc_wind_at(const orc_params* P, int prof, double y) {
+    orc_env E;
+    memset(&E, 0, sizeof(E));
+    E.wind_prof = prof;
+    return wind_profile(P, &E, y);
+}
+
 /* ---------------------------------------------------------------- the device's random draws
  * Restatement of libpdenv's scheme (test infrastructure, so that a stochastic env can be
  * followed env for env): Philox4x32-10 (Salmon et al., SC'11; constants of the Random123

@@ -432,6 +432,27 @@ def phases(rp, rl_env_cls):
     save("ref_phases.npz", **out)
 
 
+def wind_profiles_ref():
+    """HorizontalWindSpeed.compile_horizontal_fixed_wind for every percentile the envs use
+    (WindModel: float(np.random.randint(50, 99)); the wrappers' horiontal_wind_percentile, an
+    int, 50..99), at altitudes across and beyond each profile: a 0..50 km grid, every profile
+    node and its neighbours 1 m either side, and negative altitudes."""
+    os.chdir(REF)
+    sys.path[:0] = [os.path.join(HERE, "shims"), REF]
+    with contextlib.redirect_stdout(io.StringIO()):
+        from src.envs.wind.HorizontalWindSpeed import compile_horizontal_fixed_wind, extract_horizontal_wind_data
+        wd, _ = extract_horizontal_wind_data()
+    nodes = np.unique(np.concatenate([v["altitude_km"] for v in wd.values()])) * 1000.0
+    y = np.unique(np.concatenate([np.linspace(0.0, 50000.0, 401), nodes, nodes - 1.0, nodes + 1.0,
+                                  [-500.0, -1.0, 60000.0, 1e6]]))
+    pct = np.arange(50, 100)
+    speed = np.empty((len(pct), len(y)))
+    for i, p in enumerate(pct):
+        f = compile_horizontal_fixed_wind(float(p))
+        speed[i] = [float(f(v)) for v in y]
+    save("ref_wind_profiles.npz", percentile=pct, y=y, speed=speed)
+
+
 def main():
     print("recorded fixtures", file=sys.stderr)
     recorded()
@@ -443,12 +464,15 @@ def main():
     print("wind episodes", file=sys.stderr); wind_episodes(rl_env_cls)
     print("PSO objective", file=sys.stderr); pso_objective(import_reference.pso_wrapped_env)
     print("other phases", file=sys.stderr); recorded_phases(); phases(rp, rl_env_cls)
+    print("wind profiles", file=sys.stderr); wind_profiles_ref()
 
 
 if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "pso":     # only the PSO-objective fixture
         _, _, _, _, _ = import_reference()
         pso_objective(import_reference.pso_wrapped_env)
+    elif len(sys.argv) > 1 and sys.argv[1] == "wind":     # only the wind-profile fixture
+        wind_profiles_ref()
     elif len(sys.argv) > 1 and sys.argv[1] == "phases":     # only the other-phases fixture
         recorded_phases()
         rp, _, _, rl_env_cls, _ = import_reference()

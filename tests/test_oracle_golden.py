@@ -245,3 +245,20 @@ def test_oracle_episode_chaos_bound(oracle_mod):
         late.append(d.max())
     assert max(early) <= 1e-12, early
     assert np.mean(np.array(late) > 1e-4) >= 0.25 and max(late) > 1e-3, late
+
+
+def test_wind_profiles_every_percentile(oracle_mod):
+    """The horizontal wind of every percentile 50..99 (the param pack's 50 profiles, which the
+    device stages into LDS) against HorizontalWindSpeed.compile_horizontal_fixed_wind(float(p))
+    of the imported reference (ref_wind_profiles.npz): across 0..50 km, at every profile node
+    and 1 m either side, below ground and above the top node.  interp1d and np.interp differ
+    only by rounding at a node (interp1d interpolates from the left neighbour)."""
+    import ctypes as C
+    O = oracle_mod
+    d = golden("ref_wind_profiles.npz")
+    P = O.make_params()
+    L = O.lib()
+    for i, p in enumerate(d["percentile"]):
+        got = np.array([L.orc_wind_at(C.byref(P), int(p) - 50, float(y)) for y in d["y"]])
+        ref = d["speed"][i]
+        assert np.abs(got - ref).max() <= 1e-12 * max(1.0, np.abs(ref).max()), (int(p), np.abs(got - ref).max())
