@@ -1129,6 +1129,9 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
                 if (y < P.vk_y_threshold && a.stochastic) {
                     double w0, w1;
                     if (a.noise) { w0 = ev(a.noise + 2 * sub, ui * 8); w1 = ev(a.noise + 2 * sub + 1, ui * 8); }
+#ifdef PD_EXP_NOGUST   // experiment: no gust draws (wrong values; timing bound)
+                    else { w0 = 0.1 * (double)e.ts; w1 = 0.2; }
+#else
                     else {
                         // vonkarman.py:34: one np.random.randn() per filter step, u then v (gauss_pair:
                         // Philox counter (env, episode, step, sub-step), reproducible by the oracle)
@@ -1136,6 +1139,7 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
                                          a.seed_lo, a.seed_hi);
                         gauss_pair(r, (const double*)(uint64_t)&P.logtab.invc[0], (const double*)(uint64_t)&P.logtab.logc[0], w0, w1);
                     }
+#endif
                     // vonkarman.py:33-36: state = Ad @ state + Bd * w  (Bd = sigma * Bd(sigma=1))
                     R n0 = (P.vk_Ad_u[0] * e.fu0 + P.vk_Ad_u[1] * e.fu1) + (e.sgu * P.vk_Bd_u[0]) * (R)w0;
                     R n1 = (P.vk_Ad_u[2] * e.fu0 + P.vk_Ad_u[3] * e.fu1) + (e.sgu * P.vk_Bd_u[1]) * (R)w0;
