@@ -123,9 +123,7 @@ def bench_sac(args, world, rank, local, dist):
         col.step()
     wall = timed_region(lambda k: col.step(), args.steps, torch.cuda.synchronize, dist, env.device)
     if rank != 0:
-        if dist:
-            dist.destroy_process_group()
-        return
+        return None
     out = {
         "metric": "SAC collection env-steps/sec (c5: actor + env + RCCL gather + prioritized replay buffer)",
         "value": whole_job_rate(n, world, args.steps, wall), "unit": "env-steps/s",
@@ -137,9 +135,7 @@ def bench_sac(args, world, rank, local, dist):
                    "envs_per_gpu": n, "global_envs": n * world, "parallelism": f"env-shard x{world} + all_gather"},
         "replay_buffer_size": len(buf), "hip_graph": args.graph == 1,
     }
-    print(json.dumps(out))
-    if dist:
-        dist.destroy_process_group()
+    return out
 
 
 def bench_pso(args, world, rank, local, dist):
@@ -170,9 +166,7 @@ def bench_pso(args, world, rank, local, dist):
     if dist:
         dist.all_reduce(tot)
     if rank != 0:
-        if dist:
-            dist.destroy_process_group()
-        return
+        return None
     mean_len = int(tot.item()) / (P * world)
     eps = whole_job_rate(P, world, args.steps, wall)
     out = {
@@ -198,9 +192,24 @@ def bench_pso(args, world, rank, local, dist):
         out["cpu_baseline"] = {"value": len(Wc) / dt, "unit": "particle-episodes/s", "cores": 1, "kind": "port",
                                "sample": f"oracle/pd_oracle.c orc_rollout_policy, {len(Wc)} particles "
                                          f"({int(st.sum())} env-steps), 1 host thread, {dt:.1f} s"}
-    print(json.dumps(out))
-    if dist:
-        dist.destroy_process_group()
+    return out
+
+
+def other_workloads(args, local):
+    """BASELINE configs c4 and c5 at their per-GPU sizes, run after the c3 line's measurement in
+    the same process (one GPU, no process group), so that the default run records them too:
+    short runs, summarised beside the headline line (`python bench.py --workload c4|c5` gives
+    the full lines)."""
+    res = {}
+    for wl, kw in (("c4", dict(steps=4, warmup=2, cpu_baseline=0)), ("c5", dict(steps=256, warmup=32))):
+        sub = argparse.Namespace(**{**vars(args), **kw, "workload": wl})
+        try:
+            o = (bench_pso if wl == "c4" else bench_sac)(sub, 1, 0, local, None)
+            res[wl] = {k: o[k] for k in ("metric", "value", "unit", "steps", "warmup", "ms_per_step", "dtype")}
+            res[wl]["size_per_gpu"] = o["config"].get("particles_per_gpu", o["config"].get("envs_per_gpu"))
+        except Exception as exc:      # reported, never hides the headline line
+            res[wl] = {"error": repr(exc)[:300]}
+    return res
 
 
 def main():
@@ -224,6 +233,8 @@ def main():
     ap.add_argument("--fuse", type=int, default=16,
                     help="c3: env-steps per k_step launch (pd_step_n; 1 = one pd_step launch per step)")
     ap.add_argument("--graph", type=int, default=1, help="c5: replay the collection step as a HIP graph")
+    ap.add_argument("--others", type=int, default=1,
+                    help="c3 at one GPU: also run short c4 and c5 measurements (summarised in the line)")
     args = ap.parse_args()
     if args.workload == "c2":
         args.no_wind = True
@@ -253,10 +264,13 @@ def main():
             dist.init_process_group(backend)
     torch.cuda.set_device(local)
     import pdenv
-    if args.workload == "c4":
-        return bench_pso(args, world, rank, local, dist)
-    if args.workload == "c5":
-        return bench_sac(args, world, rank, local, dist)
+    if args.workload in ("c4", "c5"):
+        out = (bench_pso if args.workload == "c4" else bench_sac)(args, world, rank, local, dist)
+        if out is not None:
+            print(json.dumps(out))
+        if dist:
+            dist.destroy_process_group()
+        return
 
     def run(precision):
         n = args.envs
@@ -399,6 +413,8 @@ def main():
                                "sample": f"oracle/pd_oracle.c scalar port on {thr} host threads (static env "
                                          f"partition), {ne} envs x {ns} steps of the same workload "
                                          f"(wind+tilt+auto-reset), {dt:.1f} s"}
+    if args.others and world == 1 and args.workload == "c3" and args.envs == 65536:
+        out["other_workloads"] = other_workloads(args, local)
     print(json.dumps(out))
     if dist:
         dist.destroy_process_group()

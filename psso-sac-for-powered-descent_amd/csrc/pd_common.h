@@ -10,30 +10,66 @@ namespace pd {
 constexpr int kNbr = 50;            // RBFInterpolator(neighbors=50), aerodynamic_coefficients.py:59
 constexpr int kSys = kNbr + 3;      // + degree-1 polynomial tail (TPS default degree)
 constexpr int kCols = 5;            // AoA columns of each V2 table
-// Payload of one neighbourhood (binary64 words).  The 50 terms are stored as pair slots: a
-// window of consecutive table points (one column's Mach run) is cut into pairs (p, p + 1), an
-// odd window's last point padded with a zero-coefficient partner, so that one 16-byte LDS read
-// (the point table holds (Mach_p, Mach_p+1) per entry) serves two terms that share the
-// column's AoA.  50 points in <= 5 windows (an even number of them odd) fill <= 27 slots, padded
-// to 30 = six chunks of five slots (the evaluation unit, see rbf_eval / rbf_balanced).
-//   [0, 60)   coefficients, slot k at 2k, 2k + 1 (zero for padding)
-//   [60, 63)  degree-1 polynomial coefficients
-//   [63, 67)  shift0, shift1, scale0, scale1
-//   [67, 76)  72 index bytes: per slot its entry (first point) and the column's integer AoA,
-//             see pair_entry_pos / pair_aoa_pos (padding slots: entry 0, AoA 0)
-constexpr int kPairsUsed = 27;   // slots a neighbourhood can fill
-constexpr int kChunks = 6;       // chunks of five slots (ten terms) per payload
+// Payload of one neighbourhood (binary64 words).  The 50 terms are stored as 25 pair slots:
+// a window of consecutive table points (one column's Mach run) is cut into pairs (p, p + 1), so
+// that one 16-byte LDS read (the point table holds (Mach_p, Mach_p+1) per entry) serves two
+// terms that share the column's AoA.  50 points in <= 5 windows leave an even number (<= 4) of
+// odd windows; their last points are paired across columns ("cross" slots, two points with their
+// own entries and AoAs).  Slot 5c + 4 (the last of each chunk of five) is a general slot whose
+// second point has its own index bytes: cross slot x sits at 5x + 4, the window pairs fill the
+// other positions in order (see slot_of_pair).  Five chunks of five slots, no padding.
+//   [0, 50)   coefficients, slot k at 2k, 2k + 1
+//   [50, 53)  degree-1 polynomial coefficients
+//   [53, 57)  shift0, shift1, scale0, scale1
+//   [57, 65)  60 index bytes, 12 per chunk: per slot its first point's entry and the column's
+//             integer AoA (pair_entry_pos / pair_aoa_pos), then the general slot's second point
+//             (entry, AoA) at second_entry_pos / second_aoa_pos
+//   [65]      padding (16-byte stride)
+constexpr int kChunks = 5;       // chunks of five slots (ten terms) per payload
 constexpr int kPairs = 5 * kChunks;
+constexpr int kPairsUsed = kPairs;
 constexpr int kPayPoly = 2 * kPairs;
 constexpr int kPaySS = kPayPoly + 3;
 constexpr int kPayIdx = kPaySS + 4;
 constexpr int kPayIdxBytes = 12 * kChunks;
-constexpr int kPay = kPayIdx + kPayIdxBytes / 8;
+constexpr int kPay = (kPayIdx + (kPayIdxBytes + 7) / 8 + 1) & ~1;
 // Byte positions in the index area: slot 5c + u (chunk c of five) at 12c + 2u (entry) and
-// 12c + 2u + 1 (AoA), so that a chunk's ten bytes are one 12-byte (3-dword) load issued with its
-// ten coefficients.
+// 12c + 2u + 1 (AoA); the chunk's general slot (u = 4) has its second point at 12c + 10 / 11, so
+// that a chunk's twelve bytes are one 3-dword load issued with its ten coefficients.
 PD_HD constexpr int pair_entry_pos(int k) { return 12 * (k / 5) + 2 * (k % 5); }
 PD_HD constexpr int pair_aoa_pos(int k) { return pair_entry_pos(k) + 1; }
+PD_HD constexpr bool slot_general(int k) { return k % 5 == 4; }
+PD_HD constexpr int second_entry_pos(int k) { return 12 * (k / 5) + 10; }
+PD_HD constexpr int second_aoa_pos(int k) { return 12 * (k / 5) + 11; }
+// Slot of the np-th window pair when nx cross slots take the general positions 4, 9, ... first.
+PD_HD int slot_of_pair(int np, int nx) {
+    int cnt = -1;
+    for (int k = 0; k < kPairs; ++k) {
+        if (slot_general(k) && k / 5 < nx) continue;
+        if (++cnt == np) return k;
+    }
+    return -1;
+}
+// Where term t of a neighbourhood's window order (columns in order, Mach-sorted within) goes:
+// slot k and position i (coefficient 2k + i).  len: the five window lengths.
+PD_HD void term_slot(const int len[kCols], int t, int& k, int& i) {
+    int acc = 0, np = 0, nodd = 0, nx = 0;
+    for (int c = 0; c < kCols; ++c) nodd += len[c] & 1;
+    nx = nodd / 2;
+    int odd_before = 0;
+    for (int c = 0; c < kCols; ++c) {
+        if (t < acc + len[c]) {
+            const int off = t - acc;
+            if (off < (len[c] & ~1)) { k = slot_of_pair(np + off / 2, nx); i = off & 1; }
+            else { k = 5 * (odd_before / 2) + 4; i = odd_before & 1; }
+            return;
+        }
+        acc += len[c];
+        np += len[c] / 2;
+        odd_before += len[c] & 1;
+    }
+    k = -1; i = 0;
+}
 constexpr int kKeyLoBits = 6, kKeyLenBits = 6, kKeyField = kKeyLoBits + kKeyLenBits;
 constexpr uint64_t kEmptyKey = ~0ull;
 
@@ -245,16 +281,16 @@ PD_HD int solve_neighbourhood(const double* mach, const double* coef, const int*
     }
     for (int j = 0; j < kPay; ++j) payload[j] = 0.0;
     uint8_t* ib = (uint8_t*)(payload + kPayIdx);
-    int t = 0, slot0 = 0;
-    for (int c = 0; c < kCols; ++c) {
+    int t = 0;
+    for (int c = 0; c < kCols; ++c)
         for (int i = 0; i < len[c]; ++i, ++t) {
-            const int k = slot0 + i / 2;
-            payload[2 * k + (i & 1)] = b[t];
-            if ((i & 1) == 0) { ib[pair_entry_pos(k)] = idx[t]; ib[pair_aoa_pos(k)] = (uint8_t)col_aoa[c]; }
+            int k, pos;
+            term_slot(len, t, k, pos);
+            if (k < 0) return -1;
+            payload[2 * k + pos] = b[t];
+            if (pos == 0) { ib[pair_entry_pos(k)] = idx[t]; ib[pair_aoa_pos(k)] = (uint8_t)col_aoa[c]; }
+            else if (slot_general(k)) { ib[second_entry_pos(k)] = idx[t]; ib[second_aoa_pos(k)] = (uint8_t)col_aoa[c]; }
         }
-        slot0 += (len[c] + 1) / 2;
-    }
-    if (slot0 > kPairsUsed) return -1;
     for (int j = 0; j < 3; ++j) payload[kPayPoly + j] = b[kNbr + j];
     payload[kPaySS + 0] = sh0; payload[kPaySS + 1] = sh1;
     payload[kPaySS + 2] = sc0; payload[kPaySS + 3] = sc1;
@@ -262,8 +298,8 @@ PD_HD int solve_neighbourhood(const double* mach, const double* coef, const int*
 }
 
 // Payload in a handle's precision: coefficients converted, index bytes copied.  Stride in R
-// units: kPay = 76 (binary64) or 88 (binary32: 67 values + 72 bytes = 18 floats + padding).
-template <typename R> constexpr int pay_stride() { return sizeof(R) == 8 ? kPay : 88; }
+// units: kPay = 66 (binary64) or 72 (binary32: 57 values + 60 bytes = 15 floats, 16-byte stride).
+template <typename R> constexpr int pay_stride() { return sizeof(R) == 8 ? kPay : 72; }
 template <typename R> PD_HD void pay_store(const double* src, R* dst) {
     for (int j = 0; j < kPayIdx; ++j) dst[j] = (R)src[j];
     for (int j = kPayIdx; j < pay_stride<R>(); ++j) dst[j] = R(0);

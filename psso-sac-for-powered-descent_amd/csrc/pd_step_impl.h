@@ -93,20 +93,21 @@ __device__ __forceinline__ R chunk_sum(const R pp[10], const uint32_t w[3], cons
 #ifndef PD_RBF_UNPHASED
     if constexpr (sizeof(R) == 8) {
         R2 v[5];
-        R da2[5];
+        R da2[6];
+        R m5;     // the general slot's (u = 4) second point: its own entry and AoA
 #pragma unroll
-        for (int u = 0; u < 5; ++u) {
+        for (int u = 0; u < 6; ++u) {
             const uint32_t h = w[u >> 1] >> (16 * (u & 1));
-            v[u] = pt[h & 0xffu];
+            if (u < 5) v[u] = pt[h & 0xffu]; else m5 = pt[h & 0xffu].x;
             const R da = a - (R)((h >> 8) & 0xffu);
             da2[u] = da * da;
         }
         R d2[10];
 #pragma unroll
         for (int u = 0; u < 5; ++u) {
-            const R dm0 = M - v[u].x, dm1 = M - v[u].y;
+            const R dm0 = M - v[u].x, dm1 = M - (u == 4 ? m5 : v[u].y);
             d2[2 * u] = fma(dm0, dm0, da2[u]);
-            d2[2 * u + 1] = fma(dm1, dm1, da2[u]);
+            d2[2 * u + 1] = fma(dm1, dm1, da2[u == 4 ? 5 : u]);
         }
 #ifdef PD_EXP_NOLOG
 #pragma unroll
@@ -124,6 +125,9 @@ __device__ __forceinline__ R chunk_sum(const R pp[10], const uint32_t w[3], cons
     } else
 #endif
     {
+        const uint32_t h5 = w[2] >> 16;           // the general slot's second point
+        const R m5 = pt[h5 & 0xffu].x;
+        const R da5 = a - (R)((h5 >> 8) & 0xffu);
 #pragma unroll
         for (int u = 0; u < 5; ++u) {
             const uint32_t h = w[u >> 1] >> (16 * (u & 1));
@@ -132,8 +136,8 @@ __device__ __forceinline__ R chunk_sum(const R pp[10], const uint32_t w[3], cons
             const R da2 = da * da;
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
-                const R dm = M - (i ? v.y : v.x);
-                const R d2 = fma(dm, dm, da2);
+                const R dm = M - (i ? (u == 4 ? m5 : v.y) : v.x);
+                const R d2 = fma(dm, dm, (u == 4 && i) ? da5 * da5 : da2);
 #ifdef PD_EXP_NOLOG
                 const R l = d2;
 #else
@@ -205,27 +209,28 @@ __device__ __forceinline__ R rbf_eval(const PD_AS1 R* __restrict__ pay, const R*
     R s0 = R(0), s1 = R(0);
 #pragma unroll 1
     for (int k0 = part; k0 < kPairsUsed; k0 += 5 * nparts) {
-        uint32_t e[5], ao[5];
+        uint32_t ix[5];   // the slot's two points: entry | AoA << 8 | entry2 << 16 | AoA2 << 24
         R c0[5], c1[5];
 #pragma unroll
         for (int u = 0; u < 5; ++u) {
             const int k = k0 + u * nparts;
             const bool ok = k < kPairsUsed;
             const int kk = ok ? k : 0;
-            e[u] = ib[pair_entry_pos(kk)];
-            ao[u] = ib[pair_aoa_pos(kk)];
+            const uint32_t e = ib[pair_entry_pos(kk)], ao = ib[pair_aoa_pos(kk)];
+            const uint32_t e2 = slot_general(kk) ? (uint32_t)ib[second_entry_pos(kk)] : e + 1;
+            const uint32_t ao2 = slot_general(kk) ? (uint32_t)ib[second_aoa_pos(kk)] : ao;
+            ix[u] = e | ao << 8 | e2 << 16 | ao2 << 24;
             c0[u] = ok ? pay[2 * kk] : R(0);
             c1[u] = ok ? pay[2 * kk + 1] : R(0);
         }
 #pragma unroll
         for (int u = 0; u < 5; ++u) {
-            const R2 v = pt[e[u]];
-            const R da = a - (R)ao[u];
-            const R da2 = da * da;
+            const R m0 = pt[ix[u] & 0xffu].x, m1 = pt[(ix[u] >> 16) & 0xffu].x;
+            const R da = a - (R)((ix[u] >> 8) & 0xffu), db = a - (R)(ix[u] >> 24);
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
-                const R dm = M - (i ? v.y : v.x);
-                const R d2 = fma(dm, dm, da2);
+                const R dm = M - (i ? m1 : m0);
+                const R d2 = fma(dm, dm, i ? db * db : da * da);
                 const R l = eval_log4<R>(sizeof(R) == 8 ? d2 : (d2 > R(1e-30) ? d2 : R(1e-30)));
                 if (i) s1 = fma(d2 * c1[u], l, s1); else s0 = fma(d2 * c0[u], l, s0);
             }
@@ -260,18 +265,19 @@ __device__ __forceinline__ void solve_wave(DP<R>& P, int table, unsigned long lo
     const PD_AS4 double* aoa = table ? P.cl_aoa_d : P.cd_aoa_d;
     int lo[kCols], len[kCols];
     key_unpack(key, lo, len);
-    // lane < 50: term `lane` of the window order, column c, window offset off, pair slot my_slot
-    int my_idx = 0, my_c = 0, my_off = 0, my_slot = 0;
+    // lane < 50: term `lane` of the window order, column c, window offset off; its pair slot
+    // my_slot and position my_pos (term_slot, the host packing's map)
+    int my_idx = 0, my_c = 0, my_slot = 0, my_pos = 0;
     if (lane < kNbr) {
-        int c = 0, off = lane, acc = 0, sl0 = 0, sl = 0;
+        int c = 0, off = lane, acc = 0;
 #pragma unroll
         for (int q = 0; q < kCols; ++q) {
-            if (lane >= acc && lane < acc + len[q]) { c = q; off = lane - acc; sl = sl0; }
+            if (lane >= acc && lane < acc + len[q]) { c = q; off = lane - acc; }
             acc += len[q];
-            sl0 += (len[q] + 1) / 2;
         }
         int idx = start[c] + lo[c] + off;
-        my_idx = idx; my_c = c; my_off = off; my_slot = sl + off / 2;
+        term_slot(len, lane, my_slot, my_pos);
+        my_idx = idx; my_c = c;
         ym[lane] = mach[idx]; ya[lane] = aoa[c]; yd[lane] = coef[idx];
     }
     wave_mem_sync();
@@ -340,8 +346,9 @@ __device__ __forceinline__ void solve_wave(DP<R>& P, int table, unsigned long lo
     wave_mem_sync();
     PD_AS1 uint8_t* ib = (PD_AS1 uint8_t*)(pay + kPayIdx);
     if (lane < kNbr) {
-        pay[2 * my_slot + (my_off & 1)] = singular ? (double)NAN : b[lane];
-        if ((my_off & 1) == 0) { ib[pair_entry_pos(my_slot)] = (uint8_t)my_idx; ib[pair_aoa_pos(my_slot)] = (uint8_t)aoa[my_c]; }
+        pay[2 * my_slot + my_pos] = singular ? (double)NAN : b[lane];
+        if (my_pos == 0) { ib[pair_entry_pos(my_slot)] = (uint8_t)my_idx; ib[pair_aoa_pos(my_slot)] = (uint8_t)aoa[my_c]; }
+        else if (slot_general(my_slot)) { ib[second_entry_pos(my_slot)] = (uint8_t)my_idx; ib[second_aoa_pos(my_slot)] = (uint8_t)aoa[my_c]; }
     } else if (lane < kSys) {
         pay[kPayPoly + lane - kNbr] = singular ? (double)NAN : b[lane];
     } else if (lane == kSys) pay[kPaySS + 0] = sh0;

@@ -328,8 +328,9 @@ void build_taylor(const pd_aero_table& t, int li, DevParams<R>& D, std::vector<R
                 for (int i = 0; i < 2; ++i) {
                     const double c = pay[2 * k + i];
                     if (c == 0.0) continue;
-                    const int pidx = ib[pair_entry_pos(k)] + i;
-                    const long double da = a - (long double)ib[pair_aoa_pos(k)];
+                    const bool g2 = i == 1 && slot_general(k);   // a general slot's second point
+                    const int pidx = g2 ? ib[second_entry_pos(k)] : ib[pair_entry_pos(k)] + i;
+                    const long double da = a - (long double)ib[g2 ? second_aoa_pos(k) : pair_aoa_pos(k)];
                     m[nt] = t.mach[pidx]; dl2[nt] = da * da; cf[nt] = c;
                     const long double u0 = x0 - m[nt];
                     z2[nt] = u0 * u0 + dl2[nt];

@@ -21,17 +21,17 @@ for s in $STAGES; do
     smoke) stage smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) stage bench 600 python bench.py ;;
     bench32) stage bench32 600 python bench.py --precision f32 ;;
-    prof) stage prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 96 --warmup 16 --cpu-baseline 0 --secondary 0 ;;
-    prof32) stage prof32 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof32 -o run -- python3 bench.py --steps 96 --warmup 16 --cpu-baseline 0 --secondary 0 --precision f32 ;;
+    prof) stage prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 96 --warmup 16 --cpu-baseline 0 --secondary 0 --others 0 ;;
+    prof32) stage prof32 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof32 -o run -- python3 bench.py --steps 96 --warmup 16 --cpu-baseline 0 --secondary 0 --others 0 --precision f32 ;;
     sweep) stage sweep 600 python tools/sweep.py ;;
-    pmc) stage pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run -- python3 bench.py --steps 32 --warmup 16 --cpu-baseline 0 --secondary 0
-         stage pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o run -- python3 bench.py --steps 32 --warmup 16 --cpu-baseline 0 --secondary 0 ;;
-    pmc32) stage pmc_fetch32 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch32 -o run -- python3 bench.py --steps 32 --warmup 16 --cpu-baseline 0 --secondary 0 --precision f32
-         stage pmc_write32 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write32 -o run -- python3 bench.py --steps 32 --warmup 16 --cpu-baseline 0 --secondary 0 --precision f32 ;;
-    pmcmix) stage pmc_mix 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64 SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES --output-format csv -d gpurun_out/pmc_mix -o run -- python3 bench.py --steps 32 --warmup 16 --cpu-baseline 0 --secondary 0
-         stage pmc_mix2 300 rocprofv3 --pmc SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_LDS SQ_INSTS_SALU SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/pmc_mix2 -o run -- python3 bench.py --steps 32 --warmup 16 --cpu-baseline 0 --secondary 0 ;;
+    pmc) stage pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run -- python3 bench.py --steps 32 --warmup 16 --cpu-baseline 0 --secondary 0 --others 0
+         stage pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o run -- python3 bench.py --steps 32 --warmup 16 --cpu-baseline 0 --secondary 0 --others 0 ;;
+    pmc32) stage pmc_fetch32 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch32 -o run -- python3 bench.py --steps 32 --warmup 16 --cpu-baseline 0 --secondary 0 --others 0 --precision f32
+         stage pmc_write32 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write32 -o run -- python3 bench.py --steps 32 --warmup 16 --cpu-baseline 0 --secondary 0 --others 0 --precision f32 ;;
+    pmcmix) stage pmc_mix 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64 SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES --output-format csv -d gpurun_out/pmc_mix -o run -- python3 bench.py --steps 32 --warmup 16 --cpu-baseline 0 --secondary 0 --others 0
+         stage pmc_mix2 300 rocprofv3 --pmc SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_LDS SQ_INSTS_SALU SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/pmc_mix2 -o run -- python3 bench.py --steps 32 --warmup 16 --cpu-baseline 0 --secondary 0 --others 0 ;;
     avail) stage avail 300 rocprofv3 --list-avail ;;
-    pmcv) stage pmc_valu 600 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES --output-format csv -d gpurun_out/pmc_valu -o run -- python3 bench.py --steps 32 --warmup 16 --cpu-baseline 0 --secondary 0 ;;
+    pmcv) stage pmc_valu 600 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES --output-format csv -d gpurun_out/pmc_valu -o run -- python3 bench.py --steps 32 --warmup 16 --cpu-baseline 0 --secondary 0 --others 0 ;;
   esac
 done
 echo "=== done"
