@@ -204,40 +204,21 @@ __device__ __forceinline__ R rbf_eval(const PD_AS1 R* __restrict__ pay, const R*
         }
         return rbf_finish<R>(pay, tot, M, a);
     }
-    // LPE >= 4: this lane's slots (its terms accumulated as in a chunk: even / odd)
-    const PD_AS1 uint8_t* ib = (const PD_AS1 uint8_t*)iw;
-    R s0 = R(0), s1 = R(0);
+    // LPE >= 4: this lane's chunks part, part + nparts, ... (the chunk sums of the LPE 2 path;
+    // the caller adds the parts with shuffles)
+    R tot = R(0);
 #pragma unroll 1
-    for (int k0 = part; k0 < kPairsUsed; k0 += 5 * nparts) {
-        uint32_t ix[5];   // the slot's two points: entry | AoA << 8 | entry2 << 16 | AoA2 << 24
-        R c0[5], c1[5];
+    for (int c = part; c < kChunks; c += nparts) {
+        R pp[10];
+        uint32_t w[3];
 #pragma unroll
-        for (int u = 0; u < 5; ++u) {
-            const int k = k0 + u * nparts;
-            const bool ok = k < kPairsUsed;
-            const int kk = ok ? k : 0;
-            const uint32_t e = ib[pair_entry_pos(kk)], ao = ib[pair_aoa_pos(kk)];
-            const uint32_t e2 = slot_general(kk) ? (uint32_t)ib[second_entry_pos(kk)] : e + 1;
-            const uint32_t ao2 = slot_general(kk) ? (uint32_t)ib[second_aoa_pos(kk)] : ao;
-            ix[u] = e | ao << 8 | e2 << 16 | ao2 << 24;
-            c0[u] = ok ? pay[2 * kk] : R(0);
-            c1[u] = ok ? pay[2 * kk + 1] : R(0);
-        }
+        for (int u = 0; u < 10; ++u) pp[u] = pay[10 * c + u];
 #pragma unroll
-        for (int u = 0; u < 5; ++u) {
-            const R m0 = pt[ix[u] & 0xffu].x, m1 = pt[(ix[u] >> 16) & 0xffu].x;
-            const R da = a - (R)((ix[u] >> 8) & 0xffu), db = a - (R)(ix[u] >> 24);
-#pragma unroll
-            for (int i = 0; i < 2; ++i) {
-                const R dm = M - (i ? m1 : m0);
-                const R d2 = fma(dm, dm, i ? db * db : da * da);
-                const R l = eval_log4<R>(sizeof(R) == 8 ? d2 : (d2 > R(1e-30) ? d2 : R(1e-30)));
-                if (i) s1 = fma(d2 * c1[u], l, s1); else s0 = fma(d2 * c0[u], l, s0);
-            }
-        }
+        for (int u = 0; u < 3; ++u) w[u] = iw[3 * c + u];
+        tot = tot + chunk_sum<R, R2>(pp, w, pt, M, a);
     }
-    if (part == 0) return rbf_finish<R>(pay, s0 + s1, M, a);
-    return R(0.125) * (s0 + s1);
+    if (part == 0) return rbf_finish<R>(pay, tot, M, a);
+    return R(0.125) * tot;
 }
 
 // Orders this wave's global-memory accesses (the solve scratch is written and read back by the
