@@ -201,7 +201,7 @@ def other_workloads(args, local):
     short runs, summarised beside the headline line (`python bench.py --workload c4|c5` gives
     the full lines)."""
     res = {}
-    for wl, kw in (("c4", dict(steps=4, warmup=2, cpu_baseline=0)), ("c5", dict(steps=256, warmup=32))):
+    for wl, kw in (("c5", dict(steps=192, warmup=32)), ("c4", dict(steps=4, warmup=2, cpu_baseline=0))):
         sub = argparse.Namespace(**{**vars(args), **kw, "workload": wl})
         try:
             o = (bench_pso if wl == "c4" else bench_sac)(sub, 1, 0, local, None)
@@ -397,6 +397,9 @@ def main():
         op = "f32" if args.precision == "f64" else "f64"
         out["secondary"] = {"dtype": op, "value": whole_job_rate(other["n"], world, args.steps, other["wall"]),
                             "kernel_avg_ms": other["kern_avg_ms"]}
+    # (before the CPU baseline: its host threads must not share the CPU with these launch-bound runs)
+    if args.others and world == 1 and args.workload == "c3" and args.envs == 65536:
+        out["other_workloads"] = other_workloads(args, local)
     if args.cpu_baseline and world == 1 and args.workload == "c3":
         sys.path.insert(0, os.path.join(REPO, "oracle"))
         import numpy as np
@@ -413,8 +416,6 @@ def main():
                                "sample": f"oracle/pd_oracle.c scalar port on {thr} host threads (static env "
                                          f"partition), {ne} envs x {ns} steps of the same workload "
                                          f"(wind+tilt+auto-reset), {dt:.1f} s"}
-    if args.others and world == 1 and args.workload == "c3" and args.envs == 65536:
-        out["other_workloads"] = other_workloads(args, local)
     print(json.dumps(out))
     if dist:
         dist.destroy_process_group()

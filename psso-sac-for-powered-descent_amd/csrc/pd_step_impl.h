@@ -593,12 +593,18 @@ __device__ __forceinline__ R taylor_eval(const PD_AS1 R* __restrict__ rec, R M, 
 
 // Per-wave LDS of the balanced evaluation: the wave's payload queries by rank (Mach, AoA
 // abscissa, table << 31 | slot) and the chunk sums of each
-template <typename R> struct BalLds {
-    alignas(16) R part[kChunks * 64];
-    R qm[64];
-    R qa[64];
-    unsigned long long qp[64];   // payload address | table (bit 0)
+template <typename R, int NQ = 64> struct BalLds {   // NQ = 64: one wave; 256: the workgroup
+    alignas(16) R part[kChunks * NQ];
+    R qm[NQ];
+    R qa[NQ];
+    unsigned long long qp[NQ];   // payload address | table (bit 0)
+    int wcnt[NQ / 64];           // (workgroup) each wave's payload-query count
 };
+#ifdef PD_WG_BAL
+constexpr bool kWgBal = true;
+#else
+constexpr bool kWgBal = false;
+#endif
 __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -610,22 +616,39 @@ __device__ __forceinline__ void wave_lds_sync() {
 // in order -- the bits of rbf_eval (nparts = 1), whichever lanes computed the chunks.  `mid` runs
 // once the first round's loads are in flight (the caller's own latency-bound work overlaps
 // them).  Called by the converged wave.
-template <typename R, typename Mid>
-__device__ __forceinline__ R rbf_balanced(DP<R>& P, BalLds<R>& B, const R* tab, bool mine, int table, int slot,
+// NQ = 256 (PD_WG_BAL): the same over the workgroup's four waves -- the queries ranked across
+// the waves (each wave's count through LDS), their chunks dealt to all 256 lanes; three
+// workgroup barriers per call, so every wave of the workgroup must make the same calls
+// (k_step without policy rollouts: no wave leaves early).
+template <typename R, int NQ, typename Mid>
+__device__ __forceinline__ R rbf_balanced(DP<R>& P, BalLds<R, NQ>& B, const R* tab, bool mine, int table, int slot,
                                           R M, R aq, Mid&& mid) {
     using R2 = typename std::conditional<sizeof(R) == 8, double2, float2>::type;
     const unsigned long long mask = __ballot(mine);
-    if (mask == 0ull) { mid(); return R(0); }
-    const int lane = (int)__lane_id();
-    const int n = __popcll(mask);
-    const int rank = __popcll(mask & ((1ull << lane) - 1ull));
+    int lane = (int)__lane_id();
+    int n = __popcll(mask);
+    int rank = __popcll(mask & ((1ull << lane) - 1ull));
+    if constexpr (NQ == 64) {
+        if (mask == 0ull) { mid(); return R(0); }
+    } else {
+        const int w = (int)threadIdx.x >> 6;
+        if (lane == 0) B.wcnt[w] = n;
+        __syncthreads();
+        int base = 0, tot = 0;
+#pragma unroll
+        for (int k = 0; k < NQ / 64; ++k) { const int c = B.wcnt[k]; base += k < w ? c : 0; tot += c; }
+        if (tot == 0) { mid(); return R(0); }   // (workgroup-uniform)
+        rank += base;
+        n = tot;
+        lane = (int)threadIdx.x;
+    }
     const PD_AS1 R* pcd = gbl(P.pay_cd);
     const PD_AS1 R* pcl = gbl(P.pay_cl);
     const PD_AS1 R* own = (table ? pcl : pcd) + (size_t)(mine ? slot : 0) * pay_stride<R>();
     if (mine) { B.qm[rank] = M; B.qa[rank] = aq; B.qp[rank] = (unsigned long long)(uint64_t)own | (unsigned long long)table; }
-    wave_lds_sync();
+    if constexpr (NQ == 64) wave_lds_sync(); else __syncthreads();
     const int total = kChunks * n;
-    const int K = (total + 63) >> 6;
+    const int K = (total + NQ - 1) / NQ;
     // chunk g's coefficients / index words / point table / query
     struct Buf { R pp[10]; uint32_t w[3]; const R2* pt; R M, a; };
     auto fetch = [&](int g, Buf& b) {
@@ -654,15 +677,15 @@ __device__ __forceinline__ R rbf_balanced(DP<R>& P, BalLds<R>& B, const R* tab, 
     // two rounds per trip, ping-pong buffers: each round's loads are requested one round early
 #pragma unroll 1
     for (int k = 0; k < K; k += 2) {
-        const int g = (k << 6) + lane;
-        fetch(k + 1 < K ? g + 64 : g, b1);
+        const int g = k * NQ + lane;
+        fetch(k + 1 < K ? g + NQ : g, b1);
         run(g, b0);
         if (k + 1 < K) {
-            fetch(k + 2 < K ? g + 128 : g + 64, b0);
-            run(g + 64, b1);
+            fetch(k + 2 < K ? g + 2 * NQ : g + NQ, b0);
+            run(g + NQ, b1);
         }
     }
-    wave_lds_sync();
+    if constexpr (NQ == 64) wave_lds_sync(); else __syncthreads();
     R val = R(0);
     if (mine) {
         const R* pr = B.part + kChunks * rank;
@@ -671,7 +694,8 @@ __device__ __forceinline__ R rbf_balanced(DP<R>& P, BalLds<R>& B, const R* tab, 
         for (int c = 1; c < kChunks; ++c) tot = tot + pr[c];
         val = rbf_finish_f<R>(pf, tot, M, aq);
     }
-    wave_lds_sync();   // (B is reused by the next call)
+    // (B is reused by the next call; with NQ = 256 the next call's first two barriers order it)
+    if constexpr (NQ == 64) wave_lds_sync();
     return val;
 }
 
@@ -679,9 +703,9 @@ __device__ __forceinline__ R rbf_balanced(DP<R>& P, BalLds<R>& B, const R* tab, 
 // the other table hits by the balanced payload sums, misses by the cooperative solve (whose
 // evaluation, rbf_eval, has the balanced sums' bits).  Lanes with act = false (past the batch,
 // frozen policy envs) only take part.
-template <typename R, typename Pre>
+template <typename R, int NQ, typename Pre>
 __device__ __forceinline__ R rbf2(const StepArgs<R>& a, DP<R>& P, int table, const TabView<R>& t, const LineLds<R>& ln,
-                                  RbfCache<R>& cache, R M, R aq, bool act, BalLds<R>& B, const R* tab,
+                                  RbfCache<R>& cache, R M, R aq, bool act, BalLds<R, NQ>& B, const R* tab,
                                   Pre&& pre, unsigned long long* stamp = nullptr) {
 #ifdef PD_STAMP
     const unsigned long long s0 = __builtin_amdgcn_s_memtime();
@@ -699,7 +723,7 @@ __device__ __forceinline__ R rbf2(const StepArgs<R>& a, DP<R>& P, int table, con
 #endif
     const bool full = act && !tay && slot >= 0;
     R vt = R(0);
-    const R vb = rbf_balanced<R>(P, B, tab, full, table, slot, M, aq, [&]() {
+    const R vb = rbf_balanced<R, NQ>(P, B, tab, full, table, slot, M, aq, [&]() {
         if (tay) vt = taylor_eval<R>(gbl(P.tay) + (size_t)tr.piece * kTayStride, M, tr.cell);
     });
     R val = full ? vb : vt;
@@ -806,7 +830,7 @@ __device__ __forceinline__ void actor_forward(const float* __restrict__ W, int64
 #endif
 
 // ---------------------------------------------------------------- LDS of one step workgroup
-template <typename R, bool WIND, int EPB, bool BAL = false> struct StepLds {
+template <typename R, bool WIND, int EPB, bool BAL = false, bool WG = false> struct StepLds {
     // table points as (Mach_p, Mach_p+1) entries, C_D's 256 then C_L's: one 16-byte LDS read per
     // payload pair slot (smach[2p] is point p's Mach for the neighbourhood search)
     alignas(16) R tab[1024];
@@ -817,7 +841,7 @@ template <typename R, bool WIND, int EPB, bool BAL = false> struct StepLds {
     R wsp[WIND ? 800 : 1];
     LineLds<R> lines;
     R gwin[10][EPB];              // the g-load ring of each env of the workgroup (register-resident launches)
-    BalLds<R> bal[BAL ? kStepBlock / 64 : 1];   // LPE 2: per-wave balanced-sum space
+    BalLds<R, WG ? kStepBlock : 64> bal[BAL && !WG ? kStepBlock / 64 : 1];   // LPE 2: balanced-sum space (per wave / workgroup)
 };
 
 template <typename R>
@@ -860,11 +884,15 @@ template <typename R, int PHASE, int RTD, bool WIND, int LPE, int POL = 0, bool 
 #endif
 __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_WPE))) void k_step(StepArgs<R> a) {
     constexpr int EPB = kStepBlock / LPE;   // envs per workgroup
-    __shared__ StepLds<R, WIND, EPB, LPE == 2> L;
+    constexpr bool WG = kWgBal && LPE == 2 && !POL;   // workgroup-balanced sums (no wave leaves early)
+    __shared__ StepLds<R, WIND, EPB, LPE == 2, WG> L;
 #ifdef PD_STAMP
     unsigned long long acc_[17] = {};   // [7], [8]: rbf2 lookup, evaluation; [9..12] lookup parts; [13..16] post-aero parts
 #endif
     PD_T(t_start);
+#ifdef PD_EXP_WAVEMAX   // experiment: per-wave lifetime, max and sum over waves (stats[16], [17])
+    const unsigned long long w_start = __builtin_amdgcn_s_memtime();
+#endif
     // envs this launch steps: all N, or (POL) the compacted live list; a workgroup past its end
     // leaves before staging the tables (workgroup-uniform)
     int64_t n_act = a.n;
@@ -1162,7 +1190,7 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
                 R v;
                 if constexpr (LPE == 2)
                     v = rbf2<R>(a, P, my_table, tab_view<R>(P, L.tab, my_table), L.lines, cA, mach,
-                                my_table ? aq_cl : aq_cd, live, L.bal[threadIdx.x >> 6], L.tab, wind_block
+                                my_table ? aq_cl : aq_cd, live, L.bal[WG ? 0 : threadIdx.x >> 6], L.tab, wind_block
 #ifdef PD_STAMP
                                 , acc_ + 7
 #endif
@@ -1724,6 +1752,13 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
     // ---- the env's state back to HBM, once (policy rollouts: also when its episode ends)
     PD_T(t_store);
     store_all();
+#ifdef PD_EXP_WAVEMAX
+    {
+        __builtin_amdgcn_s_waitcnt(0);
+        const unsigned long long w_len = __builtin_amdgcn_s_memtime() - w_start;
+        if (__lane_id() == 0) { atomicMax(&a.pend.stats[16], w_len); atomicAdd(&a.pend.stats[17], w_len); atomicAdd(&a.pend.stats[18], 1ull); }
+    }
+#endif
 #ifdef PD_STAMP
     PD_T(t_end);
     PD_ACC(6, t_end - t_store);

@@ -116,9 +116,10 @@ class DevicePrioritizedReplayBuffer(DeviceReplayBuffer):
         b = min(slab.shape[0], self.capacity)
         if self.position + b <= self.capacity:                 # no wrap: one fill
             self.priorities[self.position:self.position + b] = self.max_priority
-        else:
-            idx = (self.position + torch.arange(b, device=self.data.device)) % self.capacity
-            self.priorities[idx] = self.max_priority
+        else:                                                  # wrap: the tail, then the head
+            k = self.capacity - self.position
+            self.priorities[self.position:] = self.max_priority
+            self.priorities[:b - k] = self.max_priority
         super().add_batch(slab)
 
     def sample(self, batch_size, generator=None):
