@@ -32,6 +32,12 @@ outs = (torch.empty(F, n, env.obs_dim, dtype=env.dtype, **kw), torch.empty(F, n,
 for k in range(8):
     env.step_n_raw(acts[k * F:(k + 1) * F], outs)
 torch.cuda.synchronize()
+if os.environ.get("STATS"):      # the counters after the warmup launches (to difference)
+    import ctypes as C
+    from pdenv import _lib as L
+    v0 = (L.I64 * 32)()
+    L.check(env.lib.pd_stats(env.h, v0, 32))
+    print(json.dumps({"stats_warm": list(v0)}), flush=True)
 ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(launches)]
 t0 = time.perf_counter()
 for k in range(launches):
