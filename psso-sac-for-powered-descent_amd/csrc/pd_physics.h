@@ -151,21 +151,11 @@ __device__ __forceinline__ double log4_from(int e1, double m1, double2 c) {
 template <> __device__ __forceinline__ double eval_log<double>(double x) {
     // x = 2^e1 m1, m1 in [0.5, 1) (v_frexp_*); cell from the top 10 mantissa bits;
     // r = m1 (2 invc) - 1 = m invc - 1; log x = e1 ln2 + (logc - ln2) + log1p(r)
-#ifndef PD_LOG_BITS   // (bit-operation extraction: measured 2.6 % slower)
+    // (v_frexp_*: extracting exponent and mantissa by bit operations measured 2.6 % slower)
     const int e1 = __builtin_amdgcn_frexp_exp(x);
     const double m1 = __builtin_amdgcn_frexp_mant(x);
     const uint32_t hi = (uint32_t)(__double_as_longlong(x) >> 32);
-#else
-    const uint64_t b = (uint64_t)__double_as_longlong(x);
-    const uint32_t hi = (uint32_t)(b >> 32);
-    const int e1 = (int)(hi >> 20) - 1022;
-    const double m1 = __longlong_as_double((long long)((b & 0x000fffffffffffffull) | 0x3fe0000000000000ull));
-#endif
-#ifdef PD_EXP_LOGCELL0   // experiment: every lane reads cell 0 (no bank conflicts; wrong values)
-    const uint32_t off = 0u;
-#else
     const uint32_t off = (hi >> (16 - kLogBitsD)) & ((kLogCellsD - 1) << 4);   // cell * 16 bytes
-#endif
     const double2 c = *(const double2*)((const char*)s_logtab + off);
     return 0.25 * log4_from(e1, m1, c);
 }
@@ -204,11 +194,7 @@ template <typename R> __device__ __forceinline__ void pd_sincos(R x, R& s, R& c)
     s = sin(x); c = cos(x);
 }
 template <> __device__ __forceinline__ void pd_sincos<double>(double x, double& s, double& c) {
-#ifdef PD_LIB_TRIG
-    s = sin(x); c = cos(x);
-#else
     sincos_fd(x, s, c);
-#endif
 }
 
 // ---------------------------------------------------------------- atmosphere

@@ -90,7 +90,6 @@ template <typename R> struct LineLds {
 template <typename R, typename R2>
 __device__ __forceinline__ R chunk_sum(const R pp[10], const uint32_t w[3], const R2* pt, R M, R a) {
     R s0 = R(0), s1 = R(0);
-#ifndef PD_RBF_UNPHASED
     if constexpr (sizeof(R) == 8) {
         R2 v[5];
         R da2[6];
@@ -109,10 +108,6 @@ __device__ __forceinline__ R chunk_sum(const R pp[10], const uint32_t w[3], cons
             d2[2 * u] = fma(dm0, dm0, da2[u]);
             d2[2 * u + 1] = fma(dm1, dm1, da2[u == 4 ? 5 : u]);
         }
-#ifdef PD_EXP_NOLOG
-#pragma unroll
-        for (int k = 0; k < 10; ++k) { if (k & 1) s1 = fma(d2[k] * pp[k], d2[k], s1); else s0 = fma(d2[k] * pp[k], d2[k], s0); }
-#else
         LogPart lp[10];
 #pragma unroll
         for (int k = 0; k < 10; ++k) lp[k] = log_start(d2[k]);
@@ -121,10 +116,7 @@ __device__ __forceinline__ R chunk_sum(const R pp[10], const uint32_t w[3], cons
             const R wk = d2[k] * pp[k];
             if (k & 1) s1 = fma(wk, log4_finish(lp[k]), s1); else s0 = fma(wk, log4_finish(lp[k]), s0);
         }
-#endif
-    } else
-#endif
-    {
+    } else {
         const uint32_t h5 = w[2] >> 16;           // the general slot's second point
         const R m5 = pt[h5 & 0xffu].x;
         const R da5 = a - (R)((h5 >> 8) & 0xffu);
@@ -138,11 +130,7 @@ __device__ __forceinline__ R chunk_sum(const R pp[10], const uint32_t w[3], cons
             for (int i = 0; i < 2; ++i) {
                 const R dm = M - (i ? (u == 4 ? m5 : v.y) : v.x);
                 const R d2 = fma(dm, dm, (u == 4 && i) ? da5 * da5 : da2);
-#ifdef PD_EXP_NOLOG
-                const R l = d2;
-#else
                 const R l = eval_log4<R>(sizeof(R) == 8 ? d2 : (d2 > R(1e-30) ? d2 : R(1e-30)));
-#endif
                 if (i) s1 = fma(d2 * pp[2 * u + 1], l, s1); else s0 = fma(d2 * pp[2 * u], l, s0);
             }
         }
@@ -187,11 +175,8 @@ __device__ __forceinline__ R rbf_eval(const PD_AS1 R* __restrict__ pay, const R*
 #pragma unroll
         for (int u = 0; u < 3; ++u) wn[u] = iw[u];
         R tot = R(0);
-#ifndef PD_EXP_CHUNKS   // experiment: fewer chunks per query (wrong values; timing bound)
-#define PD_EXP_CHUNKS kChunks
-#endif
 #pragma unroll 1
-        for (int c = 0; c < PD_EXP_CHUNKS; ++c) {
+        for (int c = 0; c < kChunks; ++c) {
             R pp[10];
             uint32_t w[3];
             const int cn = c + 1 < kChunks ? c + 1 : c;   // (the last chunk reloads itself)
@@ -422,11 +407,7 @@ __device__ __forceinline__ int rbf_lookup(const StepArgs<R>& a, DP<R>& P, int ta
     unsigned long long gkey = 0ull;
     int gsl0 = -1;
     R um = R(0), ua = R(0);
-#ifdef PD_EXP_NOGRID   // experiment: interior queries verify the cached key (no grid)
-    const bool use_grid = false;
-#else
     const bool use_grid = t.grid_key != nullptr;
-#endif
     if (use_grid) {
         R fm = M * t.grid_inv_dm, fa = (aq - t.grid_a0) * t.grid_inv_da;
         int im = fm < R(0) ? 0 : (fm >= R(t.grid_nm) ? t.grid_nm - 1 : (int)fm);
@@ -500,37 +481,13 @@ __device__ __forceinline__ int rbf_lookup(const StepArgs<R>& a, DP<R>& P, int ta
     PD_LST(1);
     unsigned long long key = ckey;
     int slot = cslot;
-#ifdef PD_EXP_COUNT
-    atomicAdd(&a.pend.stats[24], 1ull);
-    atomicAdd(&a.pend.stats[25], (unsigned long long)(li < 0));
-    atomicAdd(&a.pend.stats[26], (unsigned long long)(li < 0 && trusted));
-#endif
-#ifdef PD_EXP_TRUSTCHECK
-    const bool check_trusted = trusted;
-    trusted = false;
-#endif
     if (!trusted) {
         int lo[kCols], len[kCols];
         key_unpack(ckey, lo, len);
         // keys store lo=0 for empty columns; knn_windows uses insertion points for those
-#ifndef PD_EXP_NOKNN
-#ifdef PD_EXP_COUNT
-        int iters = knn_windows<R>(t.smach, t.start, t.n, t.aoa, M, aq, lo, len);
-        atomicAdd(&a.pend.stats[4], 1ull);
-        atomicAdd(&a.pend.stats[5], (unsigned long long)(li >= 0));
-        atomicAdd(&a.pend.stats[6], (unsigned long long)iters);
-        atomicAdd(&a.pend.stats[27], (unsigned long long)(key_pack(lo, len) != ckey));
-        atomicAdd(&a.pend.stats[28 + table], 1ull);
-#else
         knn_windows<R>(t.smach, t.start, t.n, t.aoa, M, aq, lo, len);
-#endif
-#endif
         key = key_pack(lo, len);
         slot = key == ckey ? cslot : -1;
-#ifdef PD_EXP_TRUSTCHECK
-        atomicAdd(&a.pend.stats[4], (unsigned long long)check_trusted);
-        atomicAdd(&a.pend.stats[7], (unsigned long long)(check_trusted && key != ckey));
-#endif
     }
     PD_LST(2);
     if (slot < 0) {
@@ -593,18 +550,13 @@ __device__ __forceinline__ R taylor_eval(const PD_AS1 R* __restrict__ rec, R M, 
 
 // Per-wave LDS of the balanced evaluation: the wave's payload queries by rank (Mach, AoA
 // abscissa, table << 31 | slot) and the chunk sums of each
-template <typename R, int NQ = 64> struct BalLds {   // NQ = 64: one wave; 256: the workgroup
-    alignas(16) R part[kChunks * NQ];
-    R qm[NQ];
-    R qa[NQ];
-    unsigned long long qp[NQ];   // payload address | table (bit 0)
-    int wcnt[NQ / 64];           // (workgroup) each wave's payload-query count
+template <typename R> struct BalLds {
+    alignas(16) R part[kChunks * 64];
+    R qm[64];
+    R qa[64];
+    unsigned long long qp[64];   // payload address | table (bit 0)
+    int wcnt[1];
 };
-#ifdef PD_WG_BAL
-constexpr bool kWgBal = true;
-#else
-constexpr bool kWgBal = false;
-#endif
 __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -615,38 +567,23 @@ __device__ __forceinline__ void wave_lds_sync() {
 // rounds instead of six per query); each chunk_sum goes to LDS and the query's lane adds its six
 // in order -- the bits of rbf_eval (nparts = 1), whichever lanes computed the chunks.  `mid` runs
 // once the first round's loads are in flight (the caller's own latency-bound work overlaps
-// them).  Called by the converged wave.
-// NQ = 256 (PD_WG_BAL): the same over the workgroup's four waves -- the queries ranked across
-// the waves (each wave's count through LDS), their chunks dealt to all 256 lanes; three
-// workgroup barriers per call, so every wave of the workgroup must make the same calls
-// (k_step without policy rollouts: no wave leaves early).
-template <typename R, int NQ, typename Mid>
-__device__ __forceinline__ R rbf_balanced(DP<R>& P, BalLds<R, NQ>& B, const R* tab, bool mine, int table, int slot,
+// them).  Called by the converged wave.  (Dealing over the workgroup's four waves instead,
+// with three workgroup barriers per call, measured 9 % slower: DESIGN.md s6.)
+template <typename R, typename Mid>
+__device__ __forceinline__ R rbf_balanced(DP<R>& P, BalLds<R>& B, const R* tab, bool mine, int table, int slot,
                                           R M, R aq, Mid&& mid) {
     using R2 = typename std::conditional<sizeof(R) == 8, double2, float2>::type;
+    constexpr int NQ = 64;
     const unsigned long long mask = __ballot(mine);
-    int lane = (int)__lane_id();
-    int n = __popcll(mask);
-    int rank = __popcll(mask & ((1ull << lane) - 1ull));
-    if constexpr (NQ == 64) {
-        if (mask == 0ull) { mid(); return R(0); }
-    } else {
-        const int w = (int)threadIdx.x >> 6;
-        if (lane == 0) B.wcnt[w] = n;
-        __syncthreads();
-        int base = 0, tot = 0;
-#pragma unroll
-        for (int k = 0; k < NQ / 64; ++k) { const int c = B.wcnt[k]; base += k < w ? c : 0; tot += c; }
-        if (tot == 0) { mid(); return R(0); }   // (workgroup-uniform)
-        rank += base;
-        n = tot;
-        lane = (int)threadIdx.x;
-    }
+    const int lane = (int)__lane_id();
+    const int n = __popcll(mask);
+    const int rank = __popcll(mask & ((1ull << lane) - 1ull));
+    if (mask == 0ull) { mid(); return R(0); }
     const PD_AS1 R* pcd = gbl(P.pay_cd);
     const PD_AS1 R* pcl = gbl(P.pay_cl);
     const PD_AS1 R* own = (table ? pcl : pcd) + (size_t)(mine ? slot : 0) * pay_stride<R>();
     if (mine) { B.qm[rank] = M; B.qa[rank] = aq; B.qp[rank] = (unsigned long long)(uint64_t)own | (unsigned long long)table; }
-    if constexpr (NQ == 64) wave_lds_sync(); else __syncthreads();
+    wave_lds_sync();
     const int total = kChunks * n;
     const int K = (total + NQ - 1) / NQ;
     // chunk g's coefficients / index words / point table / query
@@ -685,7 +622,7 @@ __device__ __forceinline__ R rbf_balanced(DP<R>& P, BalLds<R, NQ>& B, const R* t
             run(g + NQ, b1);
         }
     }
-    if constexpr (NQ == 64) wave_lds_sync(); else __syncthreads();
+    wave_lds_sync();
     R val = R(0);
     if (mine) {
         const R* pr = B.part + kChunks * rank;
@@ -694,8 +631,8 @@ __device__ __forceinline__ R rbf_balanced(DP<R>& P, BalLds<R, NQ>& B, const R* t
         for (int c = 1; c < kChunks; ++c) tot = tot + pr[c];
         val = rbf_finish_f<R>(pf, tot, M, aq);
     }
-    // (B is reused by the next call; with NQ = 256 the next call's first two barriers order it)
-    if constexpr (NQ == 64) wave_lds_sync();
+    // (B is reused by the next call)
+    wave_lds_sync();
     return val;
 }
 
@@ -703,9 +640,9 @@ __device__ __forceinline__ R rbf_balanced(DP<R>& P, BalLds<R, NQ>& B, const R* t
 // the other table hits by the balanced payload sums, misses by the cooperative solve (whose
 // evaluation, rbf_eval, has the balanced sums' bits).  Lanes with act = false (past the batch,
 // frozen policy envs) only take part.
-template <typename R, int NQ, typename Pre>
+template <typename R, typename Pre>
 __device__ __forceinline__ R rbf2(const StepArgs<R>& a, DP<R>& P, int table, const TabView<R>& t, const LineLds<R>& ln,
-                                  RbfCache<R>& cache, R M, R aq, bool act, BalLds<R, NQ>& B, const R* tab,
+                                  RbfCache<R>& cache, R M, R aq, bool act, BalLds<R>& B, const R* tab,
                                   Pre&& pre, unsigned long long* stamp = nullptr) {
 #ifdef PD_STAMP
     const unsigned long long s0 = __builtin_amdgcn_s_memtime();
@@ -716,14 +653,10 @@ __device__ __forceinline__ R rbf2(const StepArgs<R>& a, DP<R>& P, int table, con
     const unsigned long long s1 = __builtin_amdgcn_s_memtime();
     stamp[0] += s1 - s0;
 #endif
-#ifndef PD_EXP_NOTAYLOR
     const bool tay = act && tr.piece >= 0;
-#else
-    const bool tay = false;
-#endif
     const bool full = act && !tay && slot >= 0;
     R vt = R(0);
-    const R vb = rbf_balanced<R, NQ>(P, B, tab, full, table, slot, M, aq, [&]() {
+    const R vb = rbf_balanced<R>(P, B, tab, full, table, slot, M, aq, [&]() {
         if (tay) vt = taylor_eval<R>(gbl(P.tay) + (size_t)tr.piece * kTayStride, M, tr.cell);
     });
     R val = full ? vb : vt;
@@ -732,18 +665,6 @@ __device__ __forceinline__ R rbf2(const StepArgs<R>& a, DP<R>& P, int table, con
     stamp[1] += s2 - s1;
 #endif
     const bool miss = act && !tay && slot < 0;
-#ifdef PD_EXP_BALCOUNT   // experiment: Taylor / balanced / miss lanes, balanced rounds, calls
-    {
-        const unsigned long long mt = __ballot(tay), mf = __ballot(full), mm = __ballot(miss);
-        if (__lane_id() == 0) {
-            atomicAdd(&a.pend.stats[17], (unsigned long long)__popcll(mt));
-            atomicAdd(&a.pend.stats[18], (unsigned long long)__popcll(mf));
-            atomicAdd(&a.pend.stats[19], (unsigned long long)__popcll(mm));
-            atomicAdd(&a.pend.stats[20], (unsigned long long)((kChunks * __popcll(mf) + 63) >> 6));
-            atomicAdd(&a.pend.stats[21], 1ull);
-        }
-    }
-#endif
     if (__ballot(miss)) {
         R mv = rbf_miss_wave<R>(a, P, table, t.smach, cache.key, M, aq, 0, 1, miss);
         if (miss) val = mv;
@@ -830,7 +751,7 @@ __device__ __forceinline__ void actor_forward(const float* __restrict__ W, int64
 #endif
 
 // ---------------------------------------------------------------- LDS of one step workgroup
-template <typename R, bool WIND, int EPB, bool BAL = false, bool WG = false> struct StepLds {
+template <typename R, bool WIND, int EPB, bool BAL = false> struct StepLds {
     // table points as (Mach_p, Mach_p+1) entries, C_D's 256 then C_L's: one 16-byte LDS read per
     // payload pair slot (smach[2p] is point p's Mach for the neighbourhood search)
     alignas(16) R tab[1024];
@@ -841,7 +762,7 @@ template <typename R, bool WIND, int EPB, bool BAL = false, bool WG = false> str
     R wsp[WIND ? 800 : 1];
     LineLds<R> lines;
     R gwin[10][EPB];              // the g-load ring of each env of the workgroup (register-resident launches)
-    BalLds<R, WG ? kStepBlock : 64> bal[BAL && !WG ? kStepBlock / 64 : 1];   // LPE 2: balanced-sum space (per wave / workgroup)
+    BalLds<R> bal[BAL ? kStepBlock / 64 : 1];   // LPE 2: balanced-sum space per wave
 };
 
 template <typename R>
@@ -884,15 +805,11 @@ template <typename R, int PHASE, int RTD, bool WIND, int LPE, int POL = 0, bool 
 #endif
 __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_WPE))) void k_step(StepArgs<R> a) {
     constexpr int EPB = kStepBlock / LPE;   // envs per workgroup
-    constexpr bool WG = kWgBal && LPE == 2 && !POL;   // workgroup-balanced sums (no wave leaves early)
-    __shared__ StepLds<R, WIND, EPB, LPE == 2, WG> L;
+    __shared__ StepLds<R, WIND, EPB, LPE == 2> L;
 #ifdef PD_STAMP
     unsigned long long acc_[17] = {};   // [7], [8]: rbf2 lookup, evaluation; [9..12] lookup parts; [13..16] post-aero parts
 #endif
     PD_T(t_start);
-#ifdef PD_EXP_WAVEMAX   // experiment: per-wave lifetime, max and sum over waves (stats[16], [17])
-    const unsigned long long w_start = __builtin_amdgcn_s_memtime();
-#endif
     // envs this launch steps: all N, or (POL) the compacted live list; a workgroup past its end
     // leaves before staging the tables (workgroup-uniform)
     int64_t n_act = a.n;
@@ -1054,12 +971,10 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
     }
     };
     const int nf = a.n_fused;   // policy rollouts: finished envs freeze, stored at their last step
-#ifndef PD_NO_ATM_CARRY
     // the atmosphere and speed of the state a step ends in, computed by its rtd, are the next
     // step's first sub-step's (same y, vx, vy; bit-identical): carried unless the env reset
     R k_rho = R(0), k_patm = R(0), k_asnd = R(0), k_speed = R(0);
     bool k_have = false;
-#endif
 #pragma unroll 1
     for (int f = 0; f < nf; ++f) {
     const size_t fo = (size_t)f * (size_t)N;
@@ -1094,11 +1009,7 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
     const R gprev = e.act0, dlprev = e.act1, drprev = e.act2;
     bool nan_hit = false;
     // info tap (single-step launches): the last sub-step's quantities (rockets_physics.py:649-702)
-#ifdef PD_EXP_NOTAP
-    const bool tap = false;
-#else
     const bool tap = a.info != nullptr && role == 0 && live;
-#endif
     // (the lane offset is laundered per use so that the 49 loop-invariant store addresses are
     // formed inside the taken branch, not hoisted out of the loops and kept live: 92 VGPRs)
     auto info = [&](int k, R v) {
@@ -1118,11 +1029,8 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
         R m = e.s[8], mp = e.s[9];
         // rocket_physics_fcn (rockets_physics.py:455-704)
         R rho, patm, asnd, speed;
-#ifndef PD_NO_ATM_CARRY
         if (sub == 0 && k_have) { rho = k_rho; patm = k_patm; asnd = k_asnd; speed = k_speed; }
-        else
-#endif
-        {
+        else {
             atmosphere<R>(P, L.isa, y, rho, patm, asnd);
             speed = sqrt(vx * vx + vy * vy);
         }
@@ -1145,9 +1053,6 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
                 if (y < P.vk_y_threshold && a.stochastic) {
                     double w0, w1;
                     if (a.noise) { w0 = ev(a.noise + 2 * sub, ui * 8); w1 = ev(a.noise + 2 * sub + 1, ui * 8); }
-#ifdef PD_EXP_NOGUST   // experiment: no gust draws (wrong values; timing bound)
-                    else { w0 = 0.1 * (double)e.ts; w1 = 0.2; }
-#else
                     else {
                         // vonkarman.py:34: one np.random.randn() per filter step, u then v (gauss_pair:
                         // Philox counter (env, episode, step, sub-step), reproducible by the oracle)
@@ -1155,7 +1060,6 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
                                          a.seed_lo, a.seed_hi);
                         gauss_pair(r, (const double*)(uint64_t)&P.logtab.invc[0], (const double*)(uint64_t)&P.logtab.logc[0], w0, w1);
                     }
-#endif
                     // vonkarman.py:33-36: state = Ad @ state + Bd * w  (Bd = sigma * Bd(sigma=1))
                     R n0 = (P.vk_Ad_u[0] * e.fu0 + P.vk_Ad_u[1] * e.fu1) + (e.sgu * P.vk_Bd_u[0]) * (R)w0;
                     R n1 = (P.vk_Ad_u[2] * e.fu0 + P.vk_Ad_u[3] * e.fu1) + (e.sgu * P.vk_Bd_u[1]) * (R)w0;
@@ -1171,7 +1075,6 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
         R CL = R(0), CD = R(0);
         PD_T(t_aero0);
         PD_ACC(2, t_aero0 - t_sub);
-#ifndef PD_EXP_NORBF
         {
             // evaluated convergently by every lane; results of lanes that need none (speed of
             // sound 0 above 81 km, |deg(deg(alpha))| < 1e-6 for C_L) are discarded
@@ -1190,7 +1093,7 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
                 R v;
                 if constexpr (LPE == 2)
                     v = rbf2<R>(a, P, my_table, tab_view<R>(P, L.tab, my_table), L.lines, cA, mach,
-                                my_table ? aq_cl : aq_cd, live, L.bal[WG ? 0 : threadIdx.x >> 6], L.tab, wind_block
+                                my_table ? aq_cl : aq_cd, live, L.bal[threadIdx.x >> 6], L.tab, wind_block
 #ifdef PD_STAMP
                                 , acc_ + 7
 #endif
@@ -1213,7 +1116,6 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
                 CL = (!have || cl_zero) ? R(0) : (cl_sgn < R(0) ? -vcl : vcl);
             }
         }
-#endif
         PD_T(t_aero1);
         PD_ACC(3, t_aero1 - t_aero0);
         R q = R(0.5) * rho * (speed * speed);
@@ -1225,11 +1127,7 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
         else inertia<R>(P, R(1) - fpc, x_cog, I);
         R d_thrust = x_cog + P.engine_height;
         R d_cp_cg = x_cog - (ascent ? P.cop_ascent : P.cop);
-#ifndef PD_EXP_NORBF
         if constexpr (LPE != 2) wind_block();
-#else
-        wind_block();
-#endif
 #ifdef PD_STAMP
         PD_T(t_p1); acc_[9 + 4] += t_p1 - t_aero1;
 #endif
@@ -1540,9 +1438,7 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
     R rho, pa_, as_;
     atmosphere<R>(P2, L.isa, y, rho, pa_, as_);
     R speed = v;
-#ifndef PD_NO_ATM_CARRY
     k_rho = rho; k_patm = pa_; k_asnd = as_; k_speed = v;
-#endif
     R q = R(0.5) * rho * (speed * speed);
     int tr = 0, id = 0, dn = 0;
     R rew = R(0);
@@ -1690,9 +1586,7 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
     PD_ACC(5, t_rtd - t_loop);
     // ---- outputs of step f (role 0 of the env's lane group)
     const bool ended = !POL && a.auto_reset && (dn || tr);
-#ifndef PD_NO_ATM_CARRY
     k_have = !ended;
-#endif
     if (role == 0 && live) {
         // (loop-invariant addresses from a laundered offset: formed here, not held across the loop)
         uint32_t uo = ui;
@@ -1752,13 +1646,6 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
     // ---- the env's state back to HBM, once (policy rollouts: also when its episode ends)
     PD_T(t_store);
     store_all();
-#ifdef PD_EXP_WAVEMAX
-    {
-        __builtin_amdgcn_s_waitcnt(0);
-        const unsigned long long w_len = __builtin_amdgcn_s_memtime() - w_start;
-        if (__lane_id() == 0) { atomicMax(&a.pend.stats[16], w_len); atomicAdd(&a.pend.stats[17], w_len); atomicAdd(&a.pend.stats[18], 1ull); }
-    }
-#endif
 #ifdef PD_STAMP
     PD_T(t_end);
     PD_ACC(6, t_end - t_store);
