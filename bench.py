@@ -81,15 +81,20 @@ def whole_job_rate(n_per_rank, world, steps, wall_max):
     return n_per_rank * world * steps / wall_max
 
 
-def timed_region(step_fn, steps, sync, dist=None, device="cpu"):
-    """barrier + sync, exactly `steps` calls of step_fn(k), sync + barrier; max wall over ranks."""
+def timed_region(step_fn, steps, sync, dist=None, device="cpu", pre=None, post=None):
+    """barrier + sync, exactly `steps` calls of step_fn(k), sync + barrier; max wall over ranks.
+    pre()/post() run right after the clock starts / before the closing sync (stream events)."""
     import torch
     if dist:
         dist.barrier()
     sync()
     t0 = time.perf_counter()
+    if pre:
+        pre()
     for k in range(steps):
         step_fn(k)
+    if post:
+        post()
     sync()
     if dist:
         dist.barrier()
@@ -212,6 +217,168 @@ def other_workloads(args, local):
     return res
 
 
+DESCENT_BURN_IN = 640   # c3-descent: untimed steps before the warmup (a steady mix of episode phases)
+
+
+def c3_actions(T, n, gen, device, descent):
+    """Synthetic float32 actions [T, n, 1] resident in HBM.  c3: U(-1, 1) for every env (under
+    this law every episode truncates on max-q near 17 km, rtd_rl.py:229-231, id 4).  c3-descent:
+    the 3:1 high-throttle mix of tests/test_gpu_c3.py -- U(0.5, 1) on three envs in four (they
+    descend through the 15 km gust ceiling, full_wind_model.py:37, towards the landing logic,
+    rtd_rl.py:194-206), U(-1, 1) on every fourth."""
+    import torch
+    u = torch.rand(T, n, 1, generator=gen, device=device)
+    if not descent:
+        return (u * 2 - 1).contiguous()
+    hi = (torch.arange(n, device=device) % 4 != 0).view(1, n, 1)
+    return torch.where(hi, 0.5 + 0.5 * u, 2 * u - 1).contiguous()
+
+
+def workload_counts(d, n, steps, lpe):
+    """What the timed launches did, from the step kernel's counters (pd_stats words 32-39,
+    differenced over the timed region): gust-band sub-steps, resets, table queries by path."""
+    sub = n * steps * 4
+    out = {"env_substeps": sub, "gust_substeps": d["gust_substeps"], "gust_steps_frac": d["gust_substeps"] / sub,
+           "resets": d["resets"], "resets_per_1k_env_steps": 1e3 * d["resets"] / (n * steps),
+           "rbf_misses_solved": d["rbf_misses"]}
+    if lpe == 2:
+        q = 2 * sub      # one C_D and one C_L query per env sub-step
+        out.update({"table_queries": q, "q_line_frac": d["q_line"] / q, "q_interior_frac": 1 - d["q_line"] / q,
+                    "q_verified_frac": d["q_verified"] / q, "q_taylor_frac": d["q_taylor"] / q,
+                    "q_balanced_frac": d["q_balanced"] / q, "q_miss_frac": d["q_miss"] / q,
+                    "balanced_rounds_per_wave_substep": d["balanced_rounds"] / (sub * 2 / 64)})
+    return out
+
+
+def run_c3(args, precision, local, rank, dist, descent=False, launch_base=0):
+    """One c3 (or c3-descent) measurement on this rank's handle.  Returns the raw timings."""
+    import torch
+    import pdenv
+    n = args.envs
+    mode = "rl" if args.phase == "landing_burn_pure_throttle" else "pso"
+    env = pdenv.PoweredDescentEnv(
+        n, flight_phase=args.phase, mode=mode, precision=precision, device=local,
+        enable_wind=not args.no_wind, stochastic_wind=not args.no_wind, wind_percentile=None,
+        auto_reset=True, tilt_sigma_rad=0.0 if args.workload == "c2" else math.radians(1.0), seed=1234,
+        env_offset=shard_offset(rank, n), integrator=args.integrator)
+    env.flush_every = 16
+    burn = DESCENT_BURN_IN if descent else 0
+    W = burn + args.warmup
+    T = W + args.steps
+    F = max(1, args.fuse)
+    g = torch.Generator(device=env.device).manual_seed(42 + rank)
+    acts = c3_actions(T, n, g, env.device, descent)
+    launches = [0]
+    if F > 1:
+        # pd_step_n: F env-steps per launch, every step's outputs written (rows of [F, N, ...]
+        # buffers reused chunk to chunk, as the per-step loop reuses one [N, ...] buffer)
+        kw = dict(device=env.device)
+        outs = (torch.empty(F, n, env.obs_dim, dtype=env.dtype, **kw), torch.empty(F, n, dtype=env.dtype, **kw),
+                torch.empty(F, n, dtype=torch.uint8, **kw), torch.empty(F, n, dtype=torch.uint8, **kw),
+                torch.empty(F, n, dtype=torch.int8, **kw))
+        os.environ["PDENV_FUSE"] = str(F)
+
+        def chunk(t0, t1):
+            env.step_n_raw(acts[t0:t1], tuple(o[:t1 - t0] for o in outs))
+            launches[0] += 1
+    else:
+        def chunk(t0, t1):
+            env.step_raw(acts[t0])
+            launches[0] += 1
+    bounds = lambda a, b: [(t, min(t + F, b)) for t in range(a, b, F)]
+    for t0, t1 in bounds(0, W):
+        chunk(t0, t1)
+    torch.cuda.synchronize()
+    # timed region: exactly K env-steps (ceil(K / F) launches), nothing else on the stream but
+    # the miss flush after each launch and one event at either end (device time of the region)
+    tb = bounds(W, T)
+    blob = env.checkpoint()          # every per-env buffer at the start of the timed region
+    s0 = env.stats()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    first_timed = launch_base + launches[0]
+    wall = timed_region(lambda k: chunk(*tb[k]), len(tb), torch.cuda.synchronize, dist, env.device,
+                        pre=e0.record, post=e1.record)
+    dev_ms = e0.elapsed_time(e1)
+    s1 = env.stats()
+    # kernel duration: the timed region's launches replayed from the checkpoint (the same
+    # actions and per-env state; the aero tables keep what the timed region inserted, so the
+    # replay solves fewer misses -- both counts are reported), each launch with its miss flush
+    # between a pair of HIP events on the stream the kernel runs on
+    env.restore(blob)
+    first_replay = launch_base + launches[0]
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in tb]
+    for k, b in enumerate(tb):
+        ev[k][0].record()
+        chunk(*b)
+        ev[k][1].record()
+    torch.cuda.synchronize()
+    s2 = env.stats()
+    kern = [a.elapsed_time(b) for a, b in ev]
+    full = [m for m, (t0, t1) in zip(kern, tb) if t1 - t0 == F]
+    d = {k: s1[k] - s0[k] for k in s1}
+    res = dict(wall=wall, dev_ms=dev_ms, kern_total_ms=sum(kern), kern_launches=len(kern),
+               kern_avg_full_ms=(sum(full) / len(full)) if full else None, fuse=F, n=n,
+               obs_dim=env.obs_dim, act_dim=env.action_dim, burn_in=burn,
+               # (lanes per env: pd_create's default, 2 above 16 384 envs)
+               counts=workload_counts(d, n, args.steps, 2 if n > 16384 else 0),
+               replay_misses=s2["rbf_misses"] - s1["rbf_misses"],
+               launch_index={"kernel": f"k_step<{'double' if precision == 'f64' else 'float'}>",
+                             "timed": [first_timed, first_timed + len(tb)],
+                             "replay": [first_replay, first_replay + len(tb)]},
+               nan_events=s2["nan_events"])
+    res["launches_total"] = launches[0]
+    env.close()
+    return res
+
+
+def c3_summary(args, r, world, precision, pmc=None):
+    """The measured quantities of one run_c3 result (the headline line's fields)."""
+    wind = not args.no_wind
+    bpe = algorithmic_bytes(precision, args.phase, wind)
+    F, n, K = r["fuse"], r["n"], args.steps
+    ibpe = implementation_bytes(precision, args.phase, wind, r["obs_dim"], r["act_dim"], F)
+    kern_s = r["kern_total_ms"] * 1e-3
+    achieved = bpe * n * K / kern_s / 1e9
+    traffic = None
+    mix = None
+    if pmc:
+        scale = F / float(pmc.get("env_steps_per_launch", 1))
+        traffic = pmc.get(f"{precision}_bytes_per_launch")
+        traffic = traffic * scale if traffic is not None else None
+        mix = pmc.get("f64_valu_mix_per_launch") if precision == "f64" else None
+        if mix:
+            mix = {k: v * scale for k, v in mix.items()}
+    out = {
+        "value": whole_job_rate(n, world, K, r["wall"]),
+        "ms_per_step": r["wall"] / K * 1e3,
+        "device_ms_per_step": r["dev_ms"] / K,
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": 8000.0, "unit": "GB/s",
+                     "frac": achieved / 8000.0, "traffic": traffic,
+                     "bytes_per_env_step": bpe, "bytes_source": "SURVEY.md 8(d) algorithmic count",
+                     "implementation_bytes_per_env_step": round(ibpe, 1),
+                     "kernel": "k_step", "kernel_ms_per_step": r["kern_total_ms"] / K,
+                     "kernel_avg_ms": r["kern_avg_full_ms"], "kernel_launches_timed": r["kern_launches"],
+                     "env_steps_per_launch": F, "envs_per_launch": n,
+                     "kernel_timing": "the timed region's launches replayed from its checkpoint, HIP events per "
+                                      "launch (k_step + its miss flush) on the launch stream",
+                     "note": "VALU/latency-bound elementwise ODE (no MFMA); see DESIGN.md"},
+        "workload_counts": r["counts"],
+        "replay_rbf_misses": r["replay_misses"],
+        "launch_index": r["launch_index"],
+    }
+    if mix and n == 65536:
+        out["valu_roofline"] = valu_roofline(mix, r["kern_avg_full_ms"] or r["kern_total_ms"] / r["kern_launches"])
+    return out
+
+
+def load_pmc(name):
+    p = os.path.join(REPO, "profiles", name)
+    try:
+        return json.load(open(p)) if os.path.exists(p) else None
+    except Exception:
+        return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -223,9 +390,11 @@ def main():
     ap.add_argument("--no-wind", action="store_true")
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--secondary", type=int, default=1, help="also time the other precision")
-    ap.add_argument("--workload", choices=["c2", "c3", "c4", "c5"], default="c3",
-                    help="c3: env-steps/s headline; c2: 4096 envs, no wind, no tilt (--integrator); "
-                         "c4: PSO generations with the fused actor; "
+    ap.add_argument("--descent", type=int, default=1, help="c3: also measure c3-descent (nested in the line)")
+    ap.add_argument("--workload", choices=["c2", "c3", "c3-descent", "c4", "c5"], default="c3",
+                    help="c3: env-steps/s headline (uniform random actions); c3-descent: c3 with the 3:1 "
+                         "high-throttle action mix after a burn-in (gust band, landings); c2: 4096 envs, no "
+                         "wind, no tilt (--integrator); c4: PSO generations with the fused actor; "
                          "c5: SAC collection (actor + env + RCCL transition gather + replay buffer)")
     ap.add_argument("--integrator", choices=["reference", "rk4"], default="reference",
                     help="rk4: BASELINE c2's RK4 dt=0.01 s, NOT the reference's integrator (non-parity)")
@@ -263,7 +432,6 @@ def main():
         else:
             dist.init_process_group(backend)
     torch.cuda.set_device(local)
-    import pdenv
     if args.workload in ("c4", "c5"):
         out = (bench_pso if args.workload == "c4" else bench_sac)(args, world, rank, local, dist)
         if out is not None:
@@ -272,135 +440,70 @@ def main():
             dist.destroy_process_group()
         return
 
-    def run(precision):
-        n = args.envs
-        mode = "rl" if args.phase == "landing_burn_pure_throttle" else "pso"
-        env = pdenv.PoweredDescentEnv(
-            n, flight_phase=args.phase, mode=mode, precision=precision, device=local,
-            enable_wind=not args.no_wind, stochastic_wind=not args.no_wind, wind_percentile=None,
-            auto_reset=True, tilt_sigma_rad=0.0 if args.workload == "c2" else math.radians(1.0), seed=1234,
-            env_offset=shard_offset(rank, n), integrator=args.integrator)
-        env.flush_every = 16
-        T = args.warmup + args.steps
-        F = max(1, args.fuse)
-        KT = 8                  # full launches of the separate kernel-duration pass
-        g = torch.Generator(device=env.device).manual_seed(42 + rank)
-        acts = (torch.rand(max(T, args.warmup + KT * F), n, env.action_dim, generator=g, device=env.device) * 2 - 1).contiguous()
-        if F > 1:
-            # pd_step_n: F env-steps per launch, every step's outputs written (rows of [F, N, ...]
-            # buffers reused chunk to chunk, as the per-step loop reuses one [N, ...] buffer)
-            kw = dict(device=env.device)
-            outs = (torch.empty(F, n, env.obs_dim, dtype=env.dtype, **kw), torch.empty(F, n, dtype=env.dtype, **kw),
-                    torch.empty(F, n, dtype=torch.uint8, **kw), torch.empty(F, n, dtype=torch.uint8, **kw),
-                    torch.empty(F, n, dtype=torch.int8, **kw))
-            os.environ["PDENV_FUSE"] = str(F)
-
-            def chunk(t0, t1):
-                k = t1 - t0
-                env.step_n_raw(acts[t0:t1], tuple(o[:k] for o in outs))
-        else:
-            def chunk(t0, t1):
-                env.step_raw(acts[t0])
-        bounds = lambda a, b: [(t, min(t + F, b)) for t in range(a, b, F)]
-        for t0, t1 in bounds(0, args.warmup):
-            chunk(t0, t1)
-        torch.cuda.synchronize()
-        # timed region: exactly K env-steps (ceil(K / F) launches), nothing else on the stream (a
-        # per-launch event pair costs ~10 us of GPU time, so the kernel-duration pass is separate)
-        tb = bounds(args.warmup, T)
-        blob = env.checkpoint()          # every per-env buffer at the start of the timed region
-        wall = timed_region(lambda k: chunk(*tb[k]), len(tb), torch.cuda.synchronize, dist, env.device)
-        # kernel duration: the timed region's launches replayed from the checkpoint (the same
-        # work, bit for bit), extended by the following actions to at least KT full launches,
-        # with HIP events around each launch (and its miss flush) on the stream the kernel runs on
-        env.restore(blob)
-        nfull = max(KT, args.steps // F)
-        full = [(args.warmup + k * F, args.warmup + (k + 1) * F) for k in range(nfull)]
-        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in full]
-        for k, b in enumerate(full):
-            ev[k][0].record()
-            chunk(*b)
-            ev[k][1].record()
-        torch.cuda.synchronize()
-        kern_ms = sorted(a.elapsed_time(b) for a, b in ev)
-        c = env.counters()
-        res = dict(wall=wall, kern_avg_ms=sum(kern_ms) / len(kern_ms), kern_med_ms=kern_ms[len(kern_ms) // 2], fuse=F,
-                   kern_launches=len(kern_ms),
-                   n=n, obs_dim=env.obs_dim, act_dim=env.action_dim, counters=c)
-        env.close()
-        return res
-
-    main_res = run(args.precision)
+    descent_main = args.workload == "c3-descent"
+    main_res = run_c3(args, args.precision, local, rank, dist, descent=descent_main)
+    base = main_res["launches_total"]
+    desc = None
+    if args.workload == "c3" and args.descent:
+        desc = run_c3(args, args.precision, local, rank, dist, descent=True, launch_base=base)
+        base += desc["launches_total"]
     other = None
     if args.secondary:
-        other = run("f32" if args.precision == "f64" else "f64")
+        other = run_c3(args, "f32" if args.precision == "f64" else "f64", local, rank, dist, descent=descent_main)
     if rank != 0:
         if dist:
             dist.destroy_process_group()
         return
     n_total = main_res["n"] * world
-    value = whole_job_rate(main_res["n"], world, args.steps, main_res["wall"])
     wind = not args.no_wind
-    bpe = algorithmic_bytes(args.precision, args.phase, wind)
-    F = main_res["fuse"]
-    ibpe = implementation_bytes(args.precision, args.phase, wind, main_res["obs_dim"], main_res["act_dim"], F)
-    achieved = bpe * main_res["n"] * F / (main_res["kern_avg_ms"] * 1e-3) / 1e9
-    traffic = None
-    mix = None
-    pmc = os.path.join(REPO, "profiles", "pmc_traffic.json")
-    if os.path.exists(pmc) and args.workload == "c3":   # the committed PMC passes profile c3
-        try:
-            summ = json.load(open(pmc))
-            # PMC figures are per launch of the profiled run's env-steps-per-launch: rescale to F
-            scale = F / float(summ.get("env_steps_per_launch", 1))
-            traffic = summ.get(f"{args.precision}_bytes_per_launch")
-            traffic = traffic * scale if traffic is not None else None
-            mix = summ.get("f64_valu_mix_per_launch") if args.precision == "f64" else None
-            if mix:
-                mix = {k: v * scale for k, v in mix.items()}
-        except Exception:
-            traffic = None
+    pmc = None
+    if args.workload == "c3":
+        pmc = load_pmc("pmc_traffic.json")          # the committed PMC passes of the c3 workload
+    elif descent_main:
+        pmc = load_pmc("pmc_c3_descent.json")
+    summ = c3_summary(args, main_res, world, args.precision, pmc)
+    wl = {"c3": "c3: 65536 envs/GPU, landing_burn_pure_throttle, rtd_rl reward, wind (percentile profile drawn "
+                "per reset + VK gusts below 15 km) + tilt, auto-reset, uniform random actions",
+          "c3-descent": f"c3-descent: the c3 configuration with the 3:1 high-throttle action mix, timed after "
+                        f"{DESCENT_BURN_IN} burn-in + {args.warmup} warmup steps (episodes in every phase of the "
+                        f"descent: gust band, landing logic)",
+          "c2": f"c2: {main_res['n']} envs/GPU, landing_burn_pure_throttle, rtd_rl reward, no wind, no tilt, "
+                f"auto-reset, integrator {args.integrator}" +
+                (" (RK4 dt=0.01 s: NOT the reference's integrator, non-parity)" if args.integrator == "rk4"
+                 else " (semi-implicit Euler 4 x 0.025 s)")}[args.workload]
     out = {
         "metric": "env-steps/sec at 65 536 parallel envs; achieved HBM GB/s vs peak",
-        "value": value,
+        "value": summ["value"],
         "unit": "env-steps/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": main_res["wall"] / args.steps * 1e3,
+        "ms_per_step": summ["ms_per_step"],
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": args.precision,
-        "data": "synthetic (uniform float32 random actions in HBM; reference initial state" +
-                (" + N(0,1deg) pitch tilt)" if args.workload == "c3" else ")"),
-        "config": {"workload": "c3: 65536 envs/GPU, landing_burn_pure_throttle, rtd_rl reward, wind (VK gusts + "
-                               "percentile profile) + tilt, auto-reset" if args.workload == "c3" else
-                               f"c2: {main_res['n']} envs/GPU, landing_burn_pure_throttle, rtd_rl reward, no wind, "
-                               f"no tilt, auto-reset, integrator {args.integrator}" +
-                               (" (RK4 dt=0.01 s: NOT the reference's integrator, non-parity)"
-                                if args.integrator == "rk4" else " (semi-implicit Euler 4 x 0.025 s)"),
-                   "envs_per_gpu": main_res["n"], "global_envs": n_total, "parallelism": f"env-shard x{world}"},
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": 8000.0, "unit": "GB/s",
-                     "frac": achieved / 8000.0, "traffic": traffic,
-                     "bytes_per_env_step": bpe, "bytes_source": "SURVEY.md 8(d) algorithmic count",
-                     "implementation_bytes_per_env_step": round(ibpe, 1),
-                     "kernel": "k_step", "kernel_avg_ms": main_res["kern_avg_ms"],
-                     "kernel_launches_timed": main_res["kern_launches"],
-                     "env_steps_per_launch": F, "envs_per_launch": main_res["n"],
-                     "note": "VALU/transcendental-bound elementwise ODE (no MFMA); see DESIGN.md"},
-        "rbf_table_misses": main_res["counters"]["rbf_misses"],
+        "data": "synthetic (float32 actions in HBM; reference initial state" +
+                (" + N(0,1deg) pitch tilt)" if args.workload != "c2" else ")"),
+        "config": {"workload": wl, "envs_per_gpu": main_res["n"], "global_envs": n_total,
+                   "parallelism": f"env-shard x{world}"},
     }
-    if mix and args.envs == 65536 and args.phase == "landing_burn_pure_throttle" and not args.no_wind:
-        out["valu_roofline"] = valu_roofline(mix, main_res["kern_avg_ms"])
+    out.update({k: v for k, v in summ.items() if k not in ("value", "ms_per_step")})
+    out["rbf_table_misses"] = main_res["counts"]["rbf_misses_solved"]
+    if desc is not None:
+        ds = c3_summary(args, desc, world, args.precision, load_pmc("pmc_c3_descent.json"))
+        ds["workload"] = (f"c3-descent: 3:1 high-throttle action mix, {DESCENT_BURN_IN} burn-in + {args.warmup} "
+                          f"warmup steps, then {args.steps} timed")
+        out["c3_descent"] = ds
     if other is not None:
         op = "f32" if args.precision == "f64" else "f64"
         out["secondary"] = {"dtype": op, "value": whole_job_rate(other["n"], world, args.steps, other["wall"]),
-                            "kernel_avg_ms": other["kern_avg_ms"]}
+                            "kernel_ms_per_step": other["kern_total_ms"] / args.steps,
+                            "launch_index": other["launch_index"]}
     # (before the CPU baseline: its host threads must not share the CPU with these launch-bound runs)
     if args.others and world == 1 and args.workload == "c3" and args.envs == 65536:
         out["other_workloads"] = other_workloads(args, local)
-    if args.cpu_baseline and world == 1 and args.workload == "c3":
+    if args.cpu_baseline and world == 1 and args.workload in ("c3", "c3-descent"):
         sys.path.insert(0, os.path.join(REPO, "oracle"))
         import numpy as np
         import oracle
@@ -414,8 +517,8 @@ def main():
         dt = time.perf_counter() - t0
         out["cpu_baseline"] = {"value": nsteps / dt, "unit": "env-steps/s", "cores": thr, "kind": "port",
                                "sample": f"oracle/pd_oracle.c scalar port on {thr} host threads (static env "
-                                         f"partition), {ne} envs x {ns} steps of the same workload "
-                                         f"(wind+tilt+auto-reset), {dt:.1f} s"}
+                                         f"partition), {ne} envs x {ns} steps of the c3 workload "
+                                         f"(wind+tilt+auto-reset, uniform random actions), {dt:.1f} s"}
     print(json.dumps(out))
     if dist:
         dist.destroy_process_group()

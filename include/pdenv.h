@@ -264,7 +264,8 @@ pd_status pd_get_gload_window(pd_env* env, void* vprev, void* window, uint8_t* l
 pd_status pd_set_wind_sigmas(pd_env* env, const double* sig, void* stream);
 /* Wind state (vonkarman.py:33-36 filter states, full_wind_model.py percentile): filters [4][N]
  * (u0 u1 v0 v1, handle precision), sigmas [2][N] (handle precision), profile [N] uint8
- * (percentile - 50).  Any pointer may be NULL. */
+ * (percentile - 50).  Any pointer may be NULL.  pd_set_wind_state returns PD_ERR_INVALID, writing
+ * nothing, if a profile byte is >= PD_N_WIND_PROFILES (it synchronises the stream to check). */
 pd_status pd_get_wind_state(pd_env* env, void* filters, void* sigmas, uint8_t* profile, void* stream);
 pd_status pd_set_wind_state(pd_env* env, const void* filters, const void* sigmas, const uint8_t* profile, void* stream);
 /* Episode bookkeeping: episode counter and step-within-episode [N] uint32 (the Philox counter
@@ -275,7 +276,8 @@ pd_status pd_set_counters(pd_env* env, const uint32_t* episode, const uint32_t* 
 /* Checkpoint of every per-env buffer (state, g-load window, actuator memory, wind, counters,
  * aero caches, episode flags) as one opaque device blob of pd_checkpoint_size() bytes: save
  * into, load from a device buffer.  Restoring into a handle of the same configuration continues
- * bit-identically (the Philox draws depend only on (seed, env, episode, step)). */
+ * bit-identically (the Philox draws depend only on (seed, env, episode, step)).  Loading a blob
+ * whose wind profile bytes are out of range returns PD_ERR_INVALID and loads nothing. */
 size_t pd_checkpoint_size(const pd_env* env);
 pd_status pd_checkpoint_save(pd_env* env, void* blob, void* stream);
 pd_status pd_checkpoint_load(pd_env* env, const void* blob, void* stream);
@@ -286,8 +288,15 @@ pd_status pd_counters(pd_env* env, int64_t* rbf_misses, int64_t* table_entries_c
  * altitudes [n] (handle precision): out [3][n] = density, pressure, speed of sound.  Used by the
  * facade's maximum_velocity (env_wrapped_rl_pytorch.py:60-66). */
 pd_status pd_atmosphere(pd_env* env, const void* altitude, void* out, int64_t n, void* stream);
-/* All device statistics words (up to n): 0 misses, 1 NaN events, 2/3 table entries C_D/C_L,
- * 16 solved neighbourhoods not queued (queue full; solved again until a later flush). */
+/* All device statistics words (up to n, at most PD_N_STATS): 0 misses, 1 NaN events, 2/3 table
+ * entries C_D/C_L, 16 solved neighbourhoods not queued (queue full; solved again until a later
+ * flush).  Workload counters of the step kernel, summed over every launch since create:
+ * 32 env sub-steps inside the gust band (stochastic wind, y < 15 km), 33 in-kernel auto-resets;
+ * with 2 lanes per env (one table query per lane and sub-step): 34 queries on a clamped line,
+ * 35 queries whose candidate neighbourhood was verified by the swap search, 36 queries evaluated
+ * from a Taylor piece, 37 by the balanced chunk sums, 38 missed (device solve), 39 balanced-sum
+ * rounds.  Host sync. */
+#define PD_N_STATS 48
 pd_status pd_stats(pd_env* env, int64_t* out, int32_t n);
 /* Observation / action widths of the handle. */
 int pd_obs_dim(const pd_env* env);

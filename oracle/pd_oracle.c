@@ -365,7 +365,7 @@ void orc_gauss_pair(orc_u32x4 r, double* z0, double* z1) {
     *z0 = rho * c;
     *z1 = rho * s;
 }
-enum { ORC_TAG_WIND_SUB = 0, ORC_TAG_RESET = 16, ORC_TAG_TILT = 17 };
+enum { ORC_TAG_WIND_SUB = 0, ORC_TAG_RESET = 16, ORC_TAG_TILT = 17, ORC_TAG_PROF = 18 };
 
 static void vk_step(const double* Ad, const double* Bd, double sigma, double* s, double w) {
     /* vonkarman.py:33-36: state = Ad @ state + Bd * w, Bd = sigma * Bd(sigma=1) */
@@ -732,9 +732,10 @@ void orc_reset(const orc_params* P, orc_env* E, const double* s0, int wind_on, i
 }
 
 /* base_environment.py:80-97 with the device's draws (libpdenv reset_values): the phase's initial
- * state, pitch tilt N(0, tilt) (theta += tilt z, alpha = theta - gamma), sigma_u ~ U(0.5, 2.25),
- * sigma_v ~ U(1.25, 2.0) (vonkarman.py:60-66) and the percentile randint(50, 99)
- * (full_wind_model.py:27-33) unless fixed. */
+ * state, pitch tilt N(0, tilt) (theta += tilt z, alpha = theta - gamma; tag ORC_TAG_TILT),
+ * sigma_u ~ U(0.5, 2.25) and sigma_v ~ U(1.25, 2.0) (vonkarman.py:60-66; tag ORC_TAG_RESET) and
+ * the percentile randint(50, 99) (full_wind_model.py:27-33; tag ORC_TAG_PROF) unless fixed --
+ * three independent draws, as the reference's three np.random calls are. */
 void orc_reset_philox(const orc_params* P, orc_env* E, int phase, uint64_t seed, uint64_t g,
                       uint32_t episode, int wind_on, int wind_stoch, int fixed_prof, double tilt) {
     double s0[11];
@@ -752,7 +753,13 @@ void orc_reset_philox(const orc_params* P, orc_env* E, int phase, uint64_t seed,
     const double su = 0.5 + (2.25 - 0.5) * orc_u01(r.x, r.y);
     const double sv = 1.25 + (2.0 - 1.25) * orc_u01(r.z, r.w);
     orc_reset(P, E, s0, wind_on, wind_stoch, su, sv);
-    E->wind_prof = wind_on ? (fixed_prof >= 0 ? fixed_prof : (int)((r.x ^ r.w) % 49u)) : -1;
+    E->wind_prof = -1;
+    if (wind_on && fixed_prof >= 0) E->wind_prof = fixed_prof;
+    else if (wind_on) {
+        /* the percentile's own draw (tag ORC_TAG_PROF): floor(49 u / 2^32), u one Philox word */
+        orc_u32x4 cp = {(uint32_t)g, (uint32_t)(g >> 32) ^ episode, 0u, ORC_TAG_PROF};
+        E->wind_prof = (int)(((uint64_t)orc_philox(cp, klo, khi).x * 49u) >> 32);
+    }
     E->rng_philox = 1;
     E->rng_g = g; E->rng_ep = episode; E->rng_ts = 0;
     E->seed_lo = klo; E->seed_hi = khi;

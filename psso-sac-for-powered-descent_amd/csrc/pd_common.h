@@ -331,6 +331,9 @@ PD_HD double u01(uint32_t hi, uint32_t lo) {
 constexpr uint32_t kTagWindSub = 0;   // +substep 0..3
 constexpr uint32_t kTagReset = 16;
 constexpr uint32_t kTagTilt = 17;
+constexpr uint32_t kTagProf = 18;      // the wind percentile (its own draw: independent of the sigmas)
+// randint(50, 99) - 50 from one Philox word: floor(49 u / 2^32) (multiply-shift; bias < 1.2e-8)
+PD_HD int prof_draw(uint32_t u) { return (int)(((uint64_t)u * 49u) >> 32); }
 
 // ---------------------------------------------------------------- sine and cosine together
 // Binary64 sin and cos of one angle in one pass: reduction by pi/2 to a double-double r + y

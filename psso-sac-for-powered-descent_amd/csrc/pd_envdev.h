@@ -40,9 +40,10 @@ template <typename R> struct EnvRegs {
 // base_environment.py:80-97 (reset) with the build's perturbations, for env g in episode
 // `episode`: the initial state (load_initial_states.py:56-62) + pitch tilt N(0, tilt_sigma)
 // (Philox tag kTagTilt, alpha = theta - gamma); actuator memory, g-load window and wind filters
-// zeroed; sigma_u, sigma_v ~ U (VKDisturbanceGenerator._new_filters, vonkarman.py:60-66) and
-// the percentile randint(50, 99) (WindModel.compile_horizontal_fixed_wind,
-// full_wind_model.py:27-33) from Philox tag kTagReset.  invc/logc: the log_tab cells (element
+// zeroed; sigma_u, sigma_v ~ U (VKDisturbanceGenerator._new_filters, vonkarman.py:60-66) from
+// Philox tag kTagReset, and the percentile randint(50, 99) (WindModel.compile_horizontal_fixed_wind,
+// full_wind_model.py:27-33) from its own draw, tag kTagProf (the reference draws the three from
+// independent np.random calls).  invc/logc: the log_tab cells (element
 // stride S: 2 for the step kernel's interleaved LDS copy).
 template <typename R, int S = 1>
 __device__ __forceinline__ void reset_values(DP<R>& P, const StepArgs<R>& a, uint64_t g, uint32_t episode,
@@ -61,12 +62,22 @@ __device__ __forceinline__ void reset_values(DP<R>& P, const StepArgs<R>& a, uin
     e.act0 = R(0); e.act1 = R(0); e.act2 = R(0);
     e.tid = 0;
     e.ep = episode; e.ts = 0;
-    u32x4 r = philox({(uint32_t)g, (uint32_t)(g >> 32) ^ episode, 0u, kTagReset}, a.seed_lo, a.seed_hi);
-    const double su = P.sigma_u_lo + (P.sigma_u_hi - P.sigma_u_lo) * u01(r.x, r.y);
-    const double sv = P.sigma_v_lo + (P.sigma_v_hi - P.sigma_v_lo) * u01(r.z, r.w);
+    // the sigmas' draw and the percentile's draw: one Philox instance for both (register pressure)
+    double su = 0.0, sv = 0.0;
+    uint32_t pw = 0u;
+#pragma unroll 1
+    for (int t = 0; t < 2; ++t) {
+        const u32x4 r = philox({(uint32_t)g, (uint32_t)(g >> 32) ^ episode, 0u, t ? kTagProf : kTagReset}, a.seed_lo, a.seed_hi);
+        if (t == 0) {
+            su = P.sigma_u_lo + (P.sigma_u_hi - P.sigma_u_lo) * u01(r.x, r.y);
+            sv = P.sigma_v_lo + (P.sigma_v_hi - P.sigma_v_lo) * u01(r.z, r.w);
+        } else {
+            pw = r.x;
+        }
+    }
     e.fu0 = R(0); e.fu1 = R(0); e.fv0 = R(0); e.fv1 = R(0);
     e.sgu = (R)su; e.sgv = (R)sv;
-    e.prof = a.fixed_prof >= 0 ? a.fixed_prof : (int)((r.x ^ r.w) % 49u);   // randint(50, 99) - 50
+    e.prof = a.fixed_prof >= 0 ? a.fixed_prof : prof_draw(pw);
 }
 
 }  // namespace pd

@@ -37,14 +37,34 @@ struct GridBisect {
 #define PD_GRID_SUB 8
 #endif
 constexpr int kGridSub = PD_GRID_SUB;   // sub-cells per refined cell side
-constexpr int kStats = 32;            // pend.stats words (see Stat)
+constexpr int kStats = 48;            // pend.stats words (see Stat)
 
 // pend.stats[] words
 enum Stat {
-    kStMisses = 0, kStNan = 1, kStInsCd = 2, kStInsCl = 3,       // 4..7 PD_EXP_* counters
-    kStStamp = 8,                                                 // 8..15 PD_STAMP sections
+    kStMisses = 0, kStNan = 1, kStInsCd = 2, kStInsCl = 3,
+    kStStamp = 8,                                                 // 8..15, 22..31: PD_STAMP section clocks
     kStDropped = 16,
-    kStCount = 24   // 24..29 PD_EXP_COUNT: queries, interior, interior trusted, key changed, untrusted C_D / C_L
+    // workload counters of the step kernel (k_step, every launch; per-wave sums in scalar
+    // registers, one atomic per counter and wave at the end): what the launches actually did
+    kStWork = 32,
+    kStGust = kStWork + 0,       // env sub-steps inside the gust band (stochastic wind, y < vk_y_threshold)
+    kStResets = kStWork + 1,     // in-kernel auto-resets
+    kStQLine = kStWork + 2,      // LPE 2 table queries on a clamped line (|alpha_eff| clamps the table)
+    kStQVerify = kStWork + 3,    // LPE 2 queries whose candidate neighbourhood the swap search verified
+    kStQTaylor = kStWork + 4,    // LPE 2 queries evaluated from a Taylor piece
+    kStQBal = kStWork + 5,       // LPE 2 queries evaluated by the balanced chunk sums
+    kStQMiss = kStWork + 6,      // LPE 2 queries whose neighbourhood was not in the tables (device solve)
+    kStBalRounds = kStWork + 7,  // balanced-sum rounds (per wave and call: ceil(5 n / 64))
+    kNWork = 8
+};
+
+// Per-wave workload counts, wave-uniform (every update is a popcount of a ballot), packed as
+// 16-bit fields into two 64-bit scalars (counter k: word k / 4, bits 16 (k % 4)); flushed to
+// pend.stats at least every 16 fused steps (a field then holds at most 64 x 16 x 4 = 4096)
+struct WaveCount {
+    uint64_t w[2];
+    __device__ __forceinline__ void add(int k, uint32_t v) { w[k >> 2] += (uint64_t)v << (16 * (k & 3)); }
+    __device__ __forceinline__ uint32_t get(int k) const { return (uint32_t)(w[k >> 2] >> (16 * (k & 3))) & 0xffffu; }
 };
 
 // ---------------------------------------------------------------- per-env device buffers

@@ -380,7 +380,8 @@ __device__ __forceinline__ R rbf_miss_wave(const StepArgs<R>& a, DP<R>& P, int t
 // candidate is trusted (strictly inside its interval/exact cell) it is VERIFIED (and repaired by
 // the swap search) against the exact distances before it is used.
 // A query's Taylor piece on a clamped line (rbf2): its record index and cell, piece < 0: none
-struct TayRef { int piece, cell; };
+// (line, verify: the query was on a clamped line / its candidate was verified, for the counters)
+struct TayRef { int piece, cell; bool line, verify; };
 
 struct NoPre { __device__ void operator()() const {} };
 
@@ -481,6 +482,7 @@ __device__ __forceinline__ int rbf_lookup(const StepArgs<R>& a, DP<R>& P, int ta
     PD_LST(1);
     unsigned long long key = ckey;
     int slot = cslot;
+    if (tay != nullptr) { tay->line = on_line; tay->verify = !trusted; }
     if (!trusted) {
         int lo[kCols], len[kCols];
         key_unpack(ckey, lo, len);
@@ -643,11 +645,11 @@ __device__ __forceinline__ R rbf_balanced(DP<R>& P, BalLds<R>& B, const R* tab, 
 template <typename R, typename Pre>
 __device__ __forceinline__ R rbf2(const StepArgs<R>& a, DP<R>& P, int table, const TabView<R>& t, const LineLds<R>& ln,
                                   RbfCache<R>& cache, R M, R aq, bool act, BalLds<R>& B, const R* tab,
-                                  Pre&& pre, unsigned long long* stamp = nullptr) {
+                                  WaveCount& wc, Pre&& pre, unsigned long long* stamp = nullptr) {
 #ifdef PD_STAMP
     const unsigned long long s0 = __builtin_amdgcn_s_memtime();
 #endif
-    TayRef tr{-1, 0};
+    TayRef tr{-1, 0, false, false};
     const int slot = rbf_lookup<R>(a, P, table, t, ln, cache, M, aq, &tr, stamp ? stamp + 2 : nullptr, pre);
 #ifdef PD_STAMP
     const unsigned long long s1 = __builtin_amdgcn_s_memtime();
@@ -665,6 +667,15 @@ __device__ __forceinline__ R rbf2(const StepArgs<R>& a, DP<R>& P, int table, con
     stamp[1] += s2 - s1;
 #endif
     const bool miss = act && !tay && slot < 0;
+    {
+        const int nf = __popcll(__ballot(full));
+        wc.add(kStQLine - kStWork, __popcll(__ballot(act && tr.line)));
+        wc.add(kStQVerify - kStWork, __popcll(__ballot(act && tr.verify)));
+        wc.add(kStQTaylor - kStWork, __popcll(__ballot(tay)));
+        wc.add(kStQBal - kStWork, nf);
+        wc.add(kStQMiss - kStWork, __popcll(__ballot(miss)));
+        wc.add(kStBalRounds - kStWork, (kChunks * nf + 63) >> 6);
+    }
     if (__ballot(miss)) {
         R mv = rbf_miss_wave<R>(a, P, table, t.smach, cache.key, M, aq, 0, 1, miss);
         if (miss) val = mv;
@@ -971,6 +982,15 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
     }
     };
     const int nf = a.n_fused;   // policy rollouts: finished envs freeze, stored at their last step
+    WaveCount wc{};             // this wave's workload counts (flushed every 16 steps and at the end)
+    auto flush_counts = [&]() {
+        if (__lane_id() == 0) {
+#pragma unroll
+            for (int k = 0; k < kNWork; ++k)
+                if (wc.get(k)) atomicAdd(&a.pend.stats[kStWork + k], (unsigned long long)wc.get(k));
+        }
+        wc.w[0] = 0; wc.w[1] = 0;
+    };
     // the atmosphere and speed of the state a step ends in, computed by its rtd, are the next
     // step's first sub-step's (same y, vx, vy; bit-identical): carried unless the env reset
     R k_rho = R(0), k_patm = R(0), k_asnd = R(0), k_speed = R(0);
@@ -1027,6 +1047,7 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
         const bool tap_sub = tap && sub == NSUB - 1;
         R x = e.s[0], y = e.s[1], vx = e.s[2], vy = e.s[3], th = e.s[4], thd = e.s[5], ga = e.s[6], al = e.s[7];
         R m = e.s[8], mp = e.s[9];
+        if constexpr (WIND) wc.add(kStGust - kStWork, __popcll(__ballot(role == 0 && live && a.stochastic && y < P.vk_y_threshold)));
         // rocket_physics_fcn (rockets_physics.py:455-704)
         R rho, patm, asnd, speed;
         if (sub == 0 && k_have) { rho = k_rho; patm = k_patm; asnd = k_asnd; speed = k_speed; }
@@ -1093,7 +1114,7 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
                 R v;
                 if constexpr (LPE == 2)
                     v = rbf2<R>(a, P, my_table, tab_view<R>(P, L.tab, my_table), L.lines, cA, mach,
-                                my_table ? aq_cl : aq_cd, live, L.bal[threadIdx.x >> 6], L.tab, wind_block
+                                my_table ? aq_cl : aq_cd, live, L.bal[threadIdx.x >> 6], L.tab, wc, wind_block
 #ifdef PD_STAMP
                                 , acc_ + 7
 #endif
@@ -1586,6 +1607,7 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
     PD_ACC(5, t_rtd - t_loop);
     // ---- outputs of step f (role 0 of the env's lane group)
     const bool ended = !POL && a.auto_reset && (dn || tr);
+    wc.add(kStResets - kStWork, __popcll(__ballot(ended && role == 0 && live)));
     k_have = !ended;
     if (role == 0 && live) {
         // (loop-invariant addresses from a laundered offset: formed here, not held across the loop)
@@ -1626,6 +1648,7 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
         // with the wave, convergent for the cooperative miss solve, but write nothing)
         if (live && (dn || tr)) { store_all(); live = false; }
     }
+    if ((f & 15) == 15 && f + 1 < nf) flush_counts();
     }   // fused steps
     if constexpr (POL) {
         // done-mask compaction: the envs whose episode goes on, in lane order, appended to the
@@ -1646,6 +1669,7 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
     // ---- the env's state back to HBM, once (policy rollouts: also when its episode ends)
     PD_T(t_store);
     store_all();
+    flush_counts();
 #ifdef PD_STAMP
     PD_T(t_end);
     PD_ACC(6, t_end - t_store);

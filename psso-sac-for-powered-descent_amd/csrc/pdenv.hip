@@ -1447,11 +1447,28 @@ pd_status pd_get_wind_state(pd_env* e, void* filters, void* sigmas, uint8_t* pro
     return PD_OK;
 }
 
+// The wind profile bytes of n envs (device memory) are all valid ids (percentile - 50 in 0..49):
+// k_step indexes the LDS profiles and wind_n[] with them.  Stream-ordered read-back (setters only).
+static pd_status check_profiles(const uint8_t* dev, size_t n, hipStream_t s) {
+    std::vector<uint8_t> h(n);
+    PD_HIP(hipMemcpyAsync(h.data(), dev, n, hipMemcpyDeviceToHost, s));
+    PD_HIP(hipStreamSynchronize(s));
+    for (size_t i = 0; i < n; ++i)
+        if (h[i] >= PD_N_WIND_PROFILES)
+            return fail(PD_ERR_INVALID, "wind profile id " + std::to_string(h[i]) + " of env " + std::to_string(i) +
+                                            " out of range (percentile must be 50..99)");
+    return PD_OK;
+}
+
 pd_status pd_set_wind_state(pd_env* e, const void* filters, const void* sigmas, const uint8_t* profile, void* stream) {
     if (!e) return fail(PD_ERR_INVALID, "null env");
     PD_HIP(hipSetDevice(e->device));
     hipStream_t s = (hipStream_t)stream;
     const size_t N = (size_t)e->cfg.n_envs;
+    if (profile) {   // refused before anything is written
+        pd_status st = check_profiles(profile, N, s);
+        if (st != PD_OK) return st;
+    }
     if (filters) PD_HIP(hipMemcpyAsync(e->wind, filters, 4 * N * e->rsize, hipMemcpyDeviceToDevice, s));
     if (sigmas) PD_HIP(hipMemcpyAsync((char*)e->wind + 4 * N * e->rsize, sigmas, 2 * N * e->rsize, hipMemcpyDeviceToDevice, s));
     if (profile) PD_HIP(hipMemcpyAsync(e->wprof, profile, N, hipMemcpyDeviceToDevice, s));
@@ -1521,6 +1538,14 @@ pd_status pd_checkpoint_load(pd_env* e, const void* blob, void* stream) {
     void* p[16]; size_t b[16];
     int n = checkpoint_fields(e, p, b);
     size_t off = 0;
+    for (int k = 0; k < n; ++k) {   // a blob with invalid wind profile ids is refused before loading
+        if (p[k] == e->wprof) {
+            pd_status st = check_profiles((const uint8_t*)blob + off, b[k], (hipStream_t)stream);
+            if (st != PD_OK) return st;
+        }
+        off += align16(b[k]);
+    }
+    off = 0;
     for (int k = 0; k < n; ++k) {
         PD_HIP(hipMemcpyAsync(p[k], (const char*)blob + off, b[k], hipMemcpyDeviceToDevice, (hipStream_t)stream));
         off += align16(b[k]);

@@ -338,7 +338,12 @@ class PoweredDescentEnv:
         kw = dict(device=self.device)
         f = None if filters is None else torch.as_tensor(filters, dtype=self.dtype).to(**kw).reshape(self.n, 4).t().contiguous()
         s = None if sigmas is None else torch.as_tensor(sigmas, dtype=self.dtype).to(**kw).reshape(self.n, 2).t().contiguous()
-        pr = None if percentile is None else (torch.as_tensor(percentile).to(**kw).reshape(self.n) - 50).to(torch.uint8).contiguous()
+        pr = None
+        if percentile is not None:
+            p = torch.as_tensor(percentile).to(**kw).reshape(self.n)
+            if bool(((p < 50) | (p > 99)).any()):
+                raise ValueError("percentile must be in 50..99 (full_wind_model.py:29 draws randint(50, 99))")
+            pr = (p - 50).to(torch.uint8).contiguous()
         L.check(self.lib.pd_set_wind_state(self.h, _ptr(f), _ptr(s), _ptr(pr), _stream(self.device)))
         torch.cuda.current_stream(self.device).synchronize()
 
@@ -358,12 +363,18 @@ class PoweredDescentEnv:
         L.check(self.lib.pd_atmosphere(self.h, _ptr(alt), _ptr(out), int(alt.numel()), _stream(self.device)))
         return out[0], out[1], out[2]
 
+    WORK_COUNTERS = ("gust_substeps", "resets", "q_line", "q_verified", "q_taylor", "q_balanced", "q_miss",
+                     "balanced_rounds")
+
     def stats(self):
-        """Device statistics words (pd_stats): misses, NaN events, table entries, dropped queue entries."""
-        v = (L.I64 * 32)()
-        L.check(self.lib.pd_stats(self.h, v, 32))
-        return {"rbf_misses": v[0], "nan_events": v[1], "table_entries_cd": v[2], "table_entries_cl": v[3],
-                "miss_queue_dropped": v[16]}
+        """Device statistics words (pd_stats): misses, NaN events, table entries, dropped queue
+        entries, and the step kernel's workload counters since create (include/pdenv.h pd_stats)."""
+        v = (L.I64 * 48)()
+        L.check(self.lib.pd_stats(self.h, v, 48))
+        out = {"rbf_misses": v[0], "nan_events": v[1], "table_entries_cd": v[2], "table_entries_cl": v[3],
+               "miss_queue_dropped": v[16]}
+        out.update({k: v[32 + j] for j, k in enumerate(self.WORK_COUNTERS)})
+        return out
 
     def counters(self):
         v = [L.I64() for _ in range(4)]

@@ -16,12 +16,14 @@ stage() {  # name, seconds, command...
 STAGES=${STAGES:-"tests smoke bench prof"}
 for s in $STAGES; do
   case $s in
+    draws) stage gpu_draws 600 python -u -m pytest tests/test_gpu_draws.py tests/test_gpu_c3.py -x -v --timeout 300 --timeout-method thread ;;
     tests) stage gpu_tests 900 python -u -m pytest tests/ -m gpu -x -q --timeout 120 --timeout-method thread ;;
     testsall) stage gpu_tests 900 python -u -m pytest tests/ -m gpu -q --timeout 120 --timeout-method thread ;;
     smoke) stage smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) stage bench 600 python bench.py ;;
     bench32) stage bench32 600 python bench.py --precision f32 ;;
-    prof) stage prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 96 --warmup 16 --cpu-baseline 0 --secondary 0 --others 0 ;;
+    prof) stage prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 192 --warmup 32 --cpu-baseline 0 --secondary 0 --others 0 --descent 1 ;;
+    profdrv) stage profdrv 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/profdrv -o run -- python3 bench.py --steps 20 --warmup 5 --cpu-baseline 0 --secondary 0 --others 0 --descent 1 ;;
     prof32) stage prof32 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof32 -o run -- python3 bench.py --steps 96 --warmup 16 --cpu-baseline 0 --secondary 0 --others 0 --precision f32 ;;
     sweep) stage sweep 600 python tools/sweep.py ;;
     pmc) stage pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run -- python3 bench.py --steps 32 --warmup 16 --cpu-baseline 0 --secondary 0 --others 0
