@@ -235,8 +235,10 @@ def c3_actions(T, n, gen, device, descent):
 
 
 def workload_counts(d, n, steps, lpe):
-    """What the timed launches did, from the step kernel's counters (pd_stats words 32-39,
-    differenced over the timed region): gust-band sub-steps, resets, table queries by path."""
+    """What the timed launches did, from the step kernel's counters (pd_stats words 32-39) over a
+    counting replay of exactly the timed launches (pd_count_work; the replay starts from the
+    timed region's checkpoint with the same actions, so it steps the same envs through the same
+    states): gust-band sub-steps, resets, table queries by path."""
     sub = n * steps * 4
     out = {"env_substeps": sub, "gust_substeps": d["gust_substeps"], "gust_steps_frac": d["gust_substeps"] / sub,
            "resets": d["resets"], "resets_per_1k_env_steps": 1e3 * d["resets"] / (n * steps),
@@ -246,7 +248,10 @@ def workload_counts(d, n, steps, lpe):
         out.update({"table_queries": q, "q_line_frac": d["q_line"] / q, "q_interior_frac": 1 - d["q_line"] / q,
                     "q_verified_frac": d["q_verified"] / q, "q_taylor_frac": d["q_taylor"] / q,
                     "q_balanced_frac": d["q_balanced"] / q, "q_miss_frac": d["q_miss"] / q,
-                    "balanced_rounds_per_wave_substep": d["balanced_rounds"] / (sub * 2 / 64)})
+                    "balanced_rounds_per_wave_substep": d["balanced_rounds"] / (sub * 2 / 64),
+                    "q_refined_frac": d["q_refined"] / q, "q_bisect_frac": d["q_bisect"] / q,
+                    "wave_substeps_refined_frac": d["wave_substeps_refined"] / (sub * 2 / 64),
+                    "wave_substeps_bisect_frac": d["wave_substeps_bisect"] / (sub * 2 / 64)})
     return out
 
 
@@ -313,9 +318,19 @@ def run_c3(args, precision, local, rank, dist, descent=False, launch_base=0):
         ev[k][1].record()
     torch.cuda.synchronize()
     s2 = env.stats()
+    # workload counts: the same launches once more with the step kernel's counters on (counting
+    # costs a few per cent, so neither timed pass counts)
+    env.restore(blob)
+    env.count_work(True)
+    for b in tb:
+        chunk(*b)
+    torch.cuda.synchronize()
+    env.count_work(False)
+    s3 = env.stats()
     kern = [a.elapsed_time(b) for a, b in ev]
     full = [m for m, (t0, t1) in zip(kern, tb) if t1 - t0 == F]
-    d = {k: s1[k] - s0[k] for k in s1}
+    d = {k: s3[k] - s2[k] for k in env.WORK_COUNTERS}
+    d["rbf_misses"] = s1["rbf_misses"] - s0["rbf_misses"]     # solved in the timed region itself
     res = dict(wall=wall, dev_ms=dev_ms, kern_total_ms=sum(kern), kern_launches=len(kern),
                kern_avg_full_ms=(sum(full) / len(full)) if full else None, fuse=F, n=n,
                obs_dim=env.obs_dim, act_dim=env.action_dim, burn_in=burn,
@@ -325,7 +340,7 @@ def run_c3(args, precision, local, rank, dist, descent=False, launch_base=0):
                launch_index={"kernel": f"k_step<{'double' if precision == 'f64' else 'float'}>",
                              "timed": [first_timed, first_timed + len(tb)],
                              "replay": [first_replay, first_replay + len(tb)]},
-               nan_events=s2["nan_events"])
+               nan_events=s3["nan_events"])
     res["launches_total"] = launches[0]
     env.close()
     return res
@@ -399,7 +414,7 @@ def main():
     ap.add_argument("--integrator", choices=["reference", "rk4"], default="reference",
                     help="rk4: BASELINE c2's RK4 dt=0.01 s, NOT the reference's integrator (non-parity)")
     ap.add_argument("--particles", type=int, default=32768, help="c4: particles per GPU")
-    ap.add_argument("--fuse", type=int, default=16,
+    ap.add_argument("--fuse", type=int, default=64,
                     help="c3: env-steps per k_step launch (pd_step_n; 1 = one pd_step launch per step)")
     ap.add_argument("--graph", type=int, default=1, help="c5: replay the collection step as a HIP graph")
     ap.add_argument("--others", type=int, default=1,

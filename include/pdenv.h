@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define PD_ABI_VERSION 4   /* 4: pd_config.integrator (was padding) */
+#define PD_ABI_VERSION 5   /* 4: pd_config.integrator (was padding); 5: pd_count_work */
 #define PD_MAX_PTS 256      /* aero scatter points per table */
 #define PD_MAX_COLS 5       /* AoA columns per aero table */
 #define PD_MAX_TAB 64       /* grid-fin table length */
@@ -202,7 +202,7 @@ pd_status pd_step(pd_env* env, const void* actions, void* obs, void* reward, uin
  * phases: obs [n_steps][N][O], reward [n_steps][N], done/truncated/trunc_id [n_steps][N] receive
  * every step's outputs (any may be NULL).  Replaces a Python loop over
  * rocket_environment_pre_wrap.step (base_environment.py:99-154) with fused launches: each launch
- * runs up to 16 steps (PDENV_FUSE) of every env in one kernel, so the LDS table staging and the
+ * runs up to 64 steps (PDENV_FUSE, 1..256) of every env in one kernel, so the LDS table staging and the
  * launch tail are paid once per launch, followed by the miss flush.  Results are bit-identical
  * to n_steps pd_step calls.  No host synchronisation. */
 pd_status pd_step_n(pd_env* env, const void* actions, int32_t n_steps, void* obs, void* reward, uint8_t* done,
@@ -290,14 +290,22 @@ pd_status pd_counters(pd_env* env, int64_t* rbf_misses, int64_t* table_entries_c
 pd_status pd_atmosphere(pd_env* env, const void* altitude, void* out, int64_t n, void* stream);
 /* All device statistics words (up to n, at most PD_N_STATS): 0 misses, 1 NaN events, 2/3 table
  * entries C_D/C_L, 16 solved neighbourhoods not queued (queue full; solved again until a later
- * flush).  Workload counters of the step kernel, summed over every launch since create:
+ * flush).  Workload counters of the step kernel, summed over every launch made with counting on
+ * (pd_count_work) since create:
  * 32 env sub-steps inside the gust band (stochastic wind, y < 15 km), 33 in-kernel auto-resets;
  * with 2 lanes per env (one table query per lane and sub-step): 34 queries on a clamped line,
  * 35 queries whose candidate neighbourhood was verified by the swap search, 36 queries evaluated
  * from a Taylor piece, 37 by the balanced chunk sums, 38 missed (device solve), 39 balanced-sum
- * rounds.  Host sync. */
+ * rounds, 40 interior queries in a refined grid cell, 41 ... in a sub-cell split by a bisector,
+ * 42 / 43 wave sub-steps with at least one such query.  Host sync. */
 #define PD_N_STATS 48
 pd_status pd_stats(pd_env* env, int64_t* out, int32_t n);
+/* Workload counting (pd_stats words 32-43) on (enable != 0) or off (the default) for the handle's
+ * following step launches with 2 lanes per env (the default above 16 384 envs; other launches
+ * count nothing).  A diagnostic: on, the launches run a counting instantiation of the step kernel
+ * (a ballot and an LDS add per counter per sub-step, a few per cent slower); off, the product
+ * kernel has no counting code.  Results do not change. */
+pd_status pd_count_work(pd_env* env, int32_t enable);
 /* Observation / action widths of the handle. */
 int pd_obs_dim(const pd_env* env);
 int pd_action_dim(const pd_env* env);

@@ -44,8 +44,8 @@ enum Stat {
     kStMisses = 0, kStNan = 1, kStInsCd = 2, kStInsCl = 3,
     kStStamp = 8,                                                 // 8..15, 22..31: PD_STAMP section clocks
     kStDropped = 16,
-    // workload counters of the step kernel (k_step, every launch; per-wave sums in scalar
-    // registers, one atomic per counter and wave at the end): what the launches actually did
+    // workload counters of the step kernel (launches with counting on, pd_count_work: per-wave
+    // sums in LDS, one atomic per counter and wave at the end): what the launches did
     kStWork = 32,
     kStGust = kStWork + 0,       // env sub-steps inside the gust band (stochastic wind, y < vk_y_threshold)
     kStResets = kStWork + 1,     // in-kernel auto-resets
@@ -55,16 +55,26 @@ enum Stat {
     kStQBal = kStWork + 5,       // LPE 2 queries evaluated by the balanced chunk sums
     kStQMiss = kStWork + 6,      // LPE 2 queries whose neighbourhood was not in the tables (device solve)
     kStBalRounds = kStWork + 7,  // balanced-sum rounds (per wave and call: ceil(5 n / 64))
-    kNWork = 8
+    kStQRefined = kStWork + 8,   // LPE 2 interior queries in a refined grid cell (a dependent sub-cell load)
+    kStQBisect = kStWork + 9,    // ... whose sub-cell is split by a bisector (a third dependent load)
+    kStWRefined = kStWork + 10,  // wave sub-steps with at least one refined-cell query
+    kStWBisect = kStWork + 11,   // wave sub-steps with at least one bisector query
+    kNWork = 12
 };
 
-// Per-wave workload counts, wave-uniform (every update is a popcount of a ballot), packed as
-// 16-bit fields into two 64-bit scalars (counter k: word k / 4, bits 16 (k % 4)); flushed to
-// pend.stats at least every 16 fused steps (a field then holds at most 64 x 16 x 4 = 4096)
+// Per-wave workload counts in LDS (nullptr: counting off, the launch pays one scalar branch per
+// site).  Every update is the popcount of a ballot, added by lane 0 of the converged wave.
 struct WaveCount {
-    uint64_t w[2];
-    __device__ __forceinline__ void add(int k, uint32_t v) { w[k >> 2] += (uint64_t)v << (16 * (k & 3)); }
-    __device__ __forceinline__ uint32_t get(int k) const { return (uint32_t)(w[k >> 2] >> (16 * (k & 3))) & 0xffffu; }
+    uint32_t* w;
+    __device__ __forceinline__ void add(int k, bool pred) {
+        if (w) {
+            const uint32_t v = (uint32_t)__popcll(__ballot(pred));
+            if (__lane_id() == 0) w[k] += v;
+        }
+    }
+    __device__ __forceinline__ void add_n(int k, uint32_t v) {
+        if (w && __lane_id() == 0) w[k] += v;
+    }
 };
 
 // ---------------------------------------------------------------- per-env device buffers
@@ -120,6 +130,7 @@ template <typename R> struct StepArgs {
     double dt_aux;                   // physics dt of phases 2..6 (compile_physics(dt, phase))
     int rtd_none;                    // PD_RTD_NONE: physics stepping only (reward/done/trunc 0)
     int n_fused;                     // env-steps per launch (actions/outputs: [n_fused][N] rows)
+    int count_work;                  // workload counters on (pd_count_work; diagnostic launches)
 };
 
 // Kernel launchers, explicitly instantiated in the kstep_*.hip translation units.

@@ -380,8 +380,9 @@ __device__ __forceinline__ R rbf_miss_wave(const StepArgs<R>& a, DP<R>& P, int t
 // candidate is trusted (strictly inside its interval/exact cell) it is VERIFIED (and repaired by
 // the swap search) against the exact distances before it is used.
 // A query's Taylor piece on a clamped line (rbf2): its record index and cell, piece < 0: none
-// (line, verify: the query was on a clamped line / its candidate was verified, for the counters)
-struct TayRef { int piece, cell; bool line, verify; };
+// (line, verify, refined, bisect: the query was on a clamped line / its candidate was verified /
+// it read a refined cell's sub-cell / a bisector record -- for the workload counters)
+struct TayRef { int piece, cell; bool line, verify, refined, bisect; };
 
 struct NoPre { __device__ void operator()() const {} };
 
@@ -453,6 +454,7 @@ __device__ __forceinline__ int rbf_lookup(const StepArgs<R>& a, DP<R>& P, int ta
         if (sizeof(R) == 8 && gsl >= 0 && (gsl & kGridRefine)) {
             // a cell that straddles neighbourhood regions: its sub-cell (binary64 handles; the
             // binary32 handle's rounding is too coarse for sub-cell margins and verifies instead)
+            if (tay != nullptr) tay->refined = true;
             const int ref = gsl & (kGridRefine - 1);
             const R sm = um * R(kGridSub), sa = ua * R(kGridSub);
             int jm = (int)sm, ja = (int)sa;
@@ -464,6 +466,7 @@ __device__ __forceinline__ int rbf_lookup(const StepArgs<R>& a, DP<R>& P, int ta
             um = sm - (R)jm; ua = sa - (R)ja;
             if (gsl >= 0 && (gsl & kGridBisect)) {
                 // two regions split by one bisector: the query's side (trusted off the line)
+                if (tay != nullptr) tay->bisect = true;
                 const PD_AS1 GridBisect& b = t.sub_bis[gsl & (kGridBisect - 1)];
                 const double sv = fma(b.nx, (double)M, fma(b.ny, (double)aq, -b.c));
                 const bool side_a = sv < 0.0;
@@ -649,7 +652,7 @@ __device__ __forceinline__ R rbf2(const StepArgs<R>& a, DP<R>& P, int table, con
 #ifdef PD_STAMP
     const unsigned long long s0 = __builtin_amdgcn_s_memtime();
 #endif
-    TayRef tr{-1, 0, false, false};
+    TayRef tr{-1, 0, false, false, false, false};
     const int slot = rbf_lookup<R>(a, P, table, t, ln, cache, M, aq, &tr, stamp ? stamp + 2 : nullptr, pre);
 #ifdef PD_STAMP
     const unsigned long long s1 = __builtin_amdgcn_s_memtime();
@@ -667,14 +670,18 @@ __device__ __forceinline__ R rbf2(const StepArgs<R>& a, DP<R>& P, int table, con
     stamp[1] += s2 - s1;
 #endif
     const bool miss = act && !tay && slot < 0;
-    {
+    if (wc.w) {
         const int nf = __popcll(__ballot(full));
-        wc.add(kStQLine - kStWork, __popcll(__ballot(act && tr.line)));
-        wc.add(kStQVerify - kStWork, __popcll(__ballot(act && tr.verify)));
-        wc.add(kStQTaylor - kStWork, __popcll(__ballot(tay)));
-        wc.add(kStQBal - kStWork, nf);
-        wc.add(kStQMiss - kStWork, __popcll(__ballot(miss)));
-        wc.add(kStBalRounds - kStWork, (kChunks * nf + 63) >> 6);
+        wc.add(kStQLine - kStWork, act && tr.line);
+        wc.add(kStQVerify - kStWork, act && tr.verify);
+        wc.add(kStQTaylor - kStWork, tay);
+        wc.add_n(kStQBal - kStWork, nf);
+        wc.add(kStQMiss - kStWork, miss);
+        wc.add_n(kStBalRounds - kStWork, (kChunks * nf + 63) >> 6);
+        wc.add(kStQRefined - kStWork, act && tr.refined);
+        wc.add(kStQBisect - kStWork, act && tr.bisect);
+        wc.add_n(kStWRefined - kStWork, __ballot(act && tr.refined) != 0ull);
+        wc.add_n(kStWBisect - kStWork, __ballot(act && tr.bisect) != 0ull);
     }
     if (__ballot(miss)) {
         R mv = rbf_miss_wave<R>(a, P, table, t.smach, cache.key, M, aq, 0, 1, miss);
@@ -773,6 +780,8 @@ template <typename R, bool WIND, int EPB, bool BAL = false> struct StepLds {
     R wsp[WIND ? 800 : 1];
     LineLds<R> lines;
     R gwin[10][EPB];              // the g-load ring of each env of the workgroup (register-resident launches)
+    uint32_t work[kStepBlock / 64][kNWork];   // per-wave workload counts (counting launches)
+    double wnx[WIND ? 2 : 1][WIND ? kStepBlock : 1];   // each lane's gust normals of the next (odd) sub-step
     BalLds<R> bal[BAL ? kStepBlock / 64 : 1];   // LPE 2: balanced-sum space per wave
 };
 
@@ -809,7 +818,9 @@ __device__ __forceinline__ TabView<R> tab_view(DP<R>& P, const R* tab, int table
 // integrator -- BASELINE config c2's "RK4 dt=0.01 s", classical RK4 over (x, y, vx, vy, theta,
 // theta_dot, m, m_prop) with rocket_physics_fcn's forces at each stage, 10 x 0.01 s per env step;
 // the loop body below runs once per stage (oracle: orc_physics, ORC_INTEG_RK4, same order)
-template <typename R, int PHASE, int RTD, bool WIND, int LPE, int POL = 0, bool RK4 = false>
+// CNT: the counting instantiation (pd_count_work; LPE 2 step kernels): without it every counting
+// site folds away
+template <typename R, int PHASE, int RTD, bool WIND, int LPE, int POL = 0, bool RK4 = false, bool CNT = false>
 // waves_per_eu(2): caps VGPR+AGPR at 256 so the f64 kernel keeps two waves per SIMD
 #ifndef PD_WPE
 #define PD_WPE 2
@@ -867,6 +878,7 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
         for (int t = threadIdx.x; t < 2 * kLogCellsD; t += kStepBlock) {
             s_logtab[t] = P.logtab_d.cell[t];
         }
+        if (threadIdx.x < (kStepBlock / 64) * kNWork) (&L.work[0][0])[threadIdx.x] = 0u;
     }
     __syncthreads();
     PD_T(t_staged);
@@ -982,15 +994,7 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
     }
     };
     const int nf = a.n_fused;   // policy rollouts: finished envs freeze, stored at their last step
-    WaveCount wc{};             // this wave's workload counts (flushed every 16 steps and at the end)
-    auto flush_counts = [&]() {
-        if (__lane_id() == 0) {
-#pragma unroll
-            for (int k = 0; k < kNWork; ++k)
-                if (wc.get(k)) atomicAdd(&a.pend.stats[kStWork + k], (unsigned long long)wc.get(k));
-        }
-        wc.w[0] = 0; wc.w[1] = 0;
-    };
+    WaveCount wc{CNT ? L.work[threadIdx.x >> 6] : nullptr};   // this wave's workload counts (CNT)
     // the atmosphere and speed of the state a step ends in, computed by its rtd, are the next
     // step's first sub-step's (same y, vx, vy; bit-identical): carried unless the env reset
     R k_rho = R(0), k_patm = R(0), k_asnd = R(0), k_speed = R(0);
@@ -1038,6 +1042,7 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
         ev(a.info + (size_t)k * (size_t)N, u) = v;
     };
 
+    bool wpre = false;   // the odd sub-step's gust normals are in L.wnx (drawn with the even one's)
     R rkb[8], rka[8];   // RK4: the 0.01 s step's base state and its k1 + 2 k2 + 2 k3 + k4
 #pragma unroll 1
     for (int sub = 0; sub < NSUB; ++sub) {
@@ -1047,7 +1052,7 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
         const bool tap_sub = tap && sub == NSUB - 1;
         R x = e.s[0], y = e.s[1], vx = e.s[2], vy = e.s[3], th = e.s[4], thd = e.s[5], ga = e.s[6], al = e.s[7];
         R m = e.s[8], mp = e.s[9];
-        if constexpr (WIND) wc.add(kStGust - kStWork, __popcll(__ballot(role == 0 && live && a.stochastic && y < P.vk_y_threshold)));
+        if constexpr (WIND) wc.add(kStGust - kStWork, role == 0 && live && a.stochastic && y < P.vk_y_threshold);
         // rocket_physics_fcn (rockets_physics.py:455-704)
         R rho, patm, asnd, speed;
         if (sub == 0 && k_have) { rho = k_rho; patm = k_patm; asnd = k_asnd; speed = k_speed; }
@@ -1071,15 +1076,38 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
                 R km = y / R(1000);
                 int wn = P.wind_n[e.prof];
                 ug = np_interp<R>(walt, wsp, wn, km);
-                if (y < P.vk_y_threshold && a.stochastic) {
-                    double w0, w1;
-                    if (a.noise) { w0 = ev(a.noise + 2 * sub, ui * 8); w1 = ev(a.noise + 2 * sub + 1, ui * 8); }
-                    else {
-                        // vonkarman.py:34: one np.random.randn() per filter step, u then v (gauss_pair:
-                        // Philox counter (env, episode, step, sub-step), reproducible by the oracle)
+                const bool gust = y < P.vk_y_threshold && a.stochastic;
+                if (gust) {
+                    double w0 = 0.0, w1 = 0.0;
+                    // vonkarman.py:34: one np.random.randn() per filter step, u then v (gauss_pair:
+                    // Philox counter (env, episode, step, sub-step), reproducible by the oracle)
+                    const double* lic = (const double*)(uint64_t)&P.logtab.invc[0];
+                    const double* llc = (const double*)(uint64_t)&P.logtab.logc[0];
+                    bool drawn = false;
+                    if (a.noise) { w0 = ev(a.noise + 2 * sub, ui * 8); w1 = ev(a.noise + 2 * sub + 1, ui * 8); drawn = true; }
+                    else if constexpr (LPE >= 2 && NSUB == 4) {
+                        if ((sub & 1) == 0) {
+                            // the env's lane pair draws sub-steps sub and sub + 1 at once: the same
+                            // code on two counters, results swapped (the same bits as one draw per
+                            // sub-step; the odd sub-step's pair waits in LDS)
+                            const int odd = role & 1;
+                            u32x4 r = philox({(uint32_t)g, (uint32_t)(g >> 32) ^ e.ep, e.ts, kTagWindSub + (uint32_t)(sub + odd)},
+                                             a.seed_lo, a.seed_hi);
+                            double z0, z1;
+                            gauss_pair(r, lic, llc, z0, z1);
+                            const double o0 = pair_swap(z0), o1 = pair_swap(z1);
+                            w0 = odd ? o0 : z0; w1 = odd ? o1 : z1;
+                            L.wnx[0][threadIdx.x] = odd ? z0 : o0; L.wnx[1][threadIdx.x] = odd ? z1 : o1;
+                            drawn = true;
+                        } else if (wpre) {
+                            w0 = L.wnx[0][threadIdx.x]; w1 = L.wnx[1][threadIdx.x];
+                            drawn = true;
+                        }
+                    }
+                    if (!drawn) {   // (one draw per sub-step; paired: an env that entered the band mid-pair)
                         u32x4 r = philox({(uint32_t)g, (uint32_t)(g >> 32) ^ e.ep, e.ts, kTagWindSub + (uint32_t)sub},
                                          a.seed_lo, a.seed_hi);
-                        gauss_pair(r, (const double*)(uint64_t)&P.logtab.invc[0], (const double*)(uint64_t)&P.logtab.logc[0], w0, w1);
+                        gauss_pair(r, lic, llc, w0, w1);
                     }
                     // vonkarman.py:33-36: state = Ad @ state + Bd * w  (Bd = sigma * Bd(sigma=1))
                     R n0 = (P.vk_Ad_u[0] * e.fu0 + P.vk_Ad_u[1] * e.fu1) + (e.sgu * P.vk_Bd_u[0]) * (R)w0;
@@ -1091,6 +1119,7 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
                     ug = ug + e.fu1;
                     vg = e.fv1;
                 }
+                wpre = gust && (sub & 1) == 0;
             }
         };
         R CL = R(0), CD = R(0);
@@ -1607,7 +1636,7 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
     PD_ACC(5, t_rtd - t_loop);
     // ---- outputs of step f (role 0 of the env's lane group)
     const bool ended = !POL && a.auto_reset && (dn || tr);
-    wc.add(kStResets - kStWork, __popcll(__ballot(ended && role == 0 && live)));
+    wc.add(kStResets - kStWork, ended && role == 0 && live);
     k_have = !ended;
     if (role == 0 && live) {
         // (loop-invariant addresses from a laundered offset: formed here, not held across the loop)
@@ -1648,7 +1677,6 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
         // with the wave, convergent for the cooperative miss solve, but write nothing)
         if (live && (dn || tr)) { store_all(); live = false; }
     }
-    if ((f & 15) == 15 && f + 1 < nf) flush_counts();
     }   // fused steps
     if constexpr (POL) {
         // done-mask compaction: the envs whose episode goes on, in lane order, appended to the
@@ -1669,7 +1697,11 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
     // ---- the env's state back to HBM, once (policy rollouts: also when its episode ends)
     PD_T(t_store);
     store_all();
-    flush_counts();
+    if (wc.w && __lane_id() == 0) {
+#pragma unroll
+        for (int k = 0; k < kNWork; ++k)
+            if (wc.w[k]) atomicAdd(&a.pend.stats[kStWork + k], (unsigned long long)wc.w[k]);
+    }
 #ifdef PD_STAMP
     PD_T(t_end);
     PD_ACC(6, t_end - t_store);
@@ -1688,6 +1720,12 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
 // ---------------------------------------------------------------- launchers
 template <typename R, int PH, int RT, bool W, int LPE, bool RK> void launch_step(const StepArgs<R>& a, hipStream_t s) {
     unsigned grid = (unsigned)((a.n * LPE + kStepBlock - 1) / kStepBlock);
+    if constexpr (LPE == 2 && !RK) {
+        if (a.count_work) {
+            hipLaunchKernelGGL((k_step<R, PH, RT, W, LPE, 0, RK, true>), dim3(grid), dim3(kStepBlock), 0, s, a);
+            return;
+        }
+    }
     hipLaunchKernelGGL((k_step<R, PH, RT, W, LPE, 0, RK>), dim3(grid), dim3(kStepBlock), 0, s, a);
 }
 

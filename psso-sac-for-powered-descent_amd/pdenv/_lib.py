@@ -85,8 +85,9 @@ EXPORTS = ["pd_abi_version", "pd_sizeof_params", "pd_sizeof_config", "pd_last_er
            "pd_flush_misses", "pd_observe", "pd_get_state", "pd_set_state", "pd_get_actuators", "pd_set_actuators",
            "pd_set_gload_window", "pd_get_gload_window", "pd_set_wind_sigmas", "pd_get_wind_state",
            "pd_set_wind_state", "pd_get_counters", "pd_set_counters", "pd_checkpoint_size", "pd_checkpoint_save",
-           "pd_checkpoint_load", "pd_counters", "pd_stats", "pd_atmosphere", "pd_obs_dim", "pd_action_dim"]
-ABI_VERSION = 4
+           "pd_checkpoint_load", "pd_counters", "pd_stats", "pd_count_work", "pd_atmosphere", "pd_obs_dim",
+           "pd_action_dim"]
+ABI_VERSION = 5
 
 _lib = None
 
@@ -128,6 +129,7 @@ def load(path=None):
     L.pd_set_gload_window.argtypes = [vp, vp, vp, vp, vp]
     L.pd_counters.argtypes = [vp, P(I64), P(I64), P(I64), P(I64)]
     L.pd_stats.argtypes = [vp, P(I64), I32]
+    L.pd_count_work.argtypes = [vp, I32]
     L.pd_atmosphere.argtypes = [vp, vp, vp, I64, vp]
     L.pd_get_gload_window.argtypes = [vp, vp, vp, vp, vp, vp]
     L.pd_get_wind_state.argtypes = [vp, vp, vp, vp, vp]
@@ -141,7 +143,8 @@ def load(path=None):
     L.pd_action_dim.argtypes = [vp]; L.pd_action_dim.restype = C.c_int
     for name in ("pd_create", "pd_destroy", "pd_reset", "pd_step", "pd_step_n", "pd_rollout", "pd_rollout_policy", "pd_pso_step", "pd_flush_misses", "pd_observe",
                  "pd_get_state", "pd_set_state", "pd_get_actuators", "pd_set_actuators",
-                 "pd_set_wind_sigmas", "pd_set_gload_window", "pd_counters", "pd_stats", "pd_get_gload_window",
+                 "pd_set_wind_sigmas", "pd_set_gload_window", "pd_counters", "pd_stats", "pd_count_work",
+                 "pd_get_gload_window",
                  "pd_get_wind_state", "pd_set_wind_state", "pd_get_counters", "pd_set_counters",
                  "pd_checkpoint_save", "pd_checkpoint_load", "pd_atmosphere"):
         getattr(L, name).restype = C.c_int

@@ -24,7 +24,7 @@ FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fP
 KSTEP = [(r, ph, w) for r in (0, 1) for ph in (0, 1, 2) for w in (0, 1)]
 
 
-def units(extra=()):
+def units():
     """(object path, source, defines) of every translation unit."""
     u = [(os.path.join(OBJ, "pdenv.o"), "pdenv.hip", []), (os.path.join(OBJ, "pdpso.o"), "pdpso.hip", [])]
     for r, ph, w in KSTEP:
@@ -33,7 +33,7 @@ def units(extra=()):
     for r in (0, 1):   # the non-parity RK4 kernels (pure throttle, no wind) in units of their own
         u.append((os.path.join(OBJ, f"kstep_r{r}_rk4.o"), "kstep.hip", [f"-DPD_KR={r}", "-DPD_KPH=0", "-DPD_KW=0",
                                                                         "-DPD_KRK4=1"]))
-    return [(o, os.path.join(CSRC, s), list(d) + list(extra)) for o, s, d in u]
+    return [(o, os.path.join(CSRC, s), list(d)) for o, s, d in u]
 
 
 def sources():
@@ -61,14 +61,15 @@ def _compile(job, verbose):
     return obj
 
 
-def build(force=False, verbose=True, jobs=None, extra=()):
+def build(force=False, verbose=True, jobs=None):
     """Compile stale objects in parallel (at most `jobs`, default the CPU count capped at 16) and
-    link libpdenv.so.  `extra`: additional hipcc flags (experiments; forces a rebuild)."""
-    if not force and not extra and up_to_date():
+    link libpdenv.so.  (Experiment builds go through build_variant, into their own directory
+    and library, never into these objects.)"""
+    if not force and up_to_date():
         return OUT
     os.makedirs(OBJ, exist_ok=True)
     newest = _newest_source()
-    todo = [u for u in units(extra) if force or extra or not os.path.exists(u[0]) or os.path.getmtime(u[0]) < newest]
+    todo = [u for u in units() if force or not os.path.exists(u[0]) or os.path.getmtime(u[0]) < newest]
     jobs = jobs or min(16, os.cpu_count() or 4)
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
         list(ex.map(lambda j: _compile(j, verbose), todo))
@@ -83,17 +84,34 @@ if __name__ == "__main__":
     build(force="--force" in sys.argv)
 
 
-def build_variant(name, defines, unit=(0, 0, 1)):
+def build_variant(name, defines, unit=(0, 0, 1), patch=None):
     """Experiments: libpdenv_<name>.so with the step-kernel object of `unit` (precision, phase
-    family, wind; default the c3 one) compiled with extra `defines`, the other objects shared
-    with the main build (which must be current).  Returns the library path."""
+    family, wind; default the c3 one) compiled with extra `defines` -- and, given `patch` (a
+    unified diff against csrc/, e.g. tools/experiments/*.patch), from a patched copy of the
+    sources, so that experiments stay out of the product source -- the other objects shared with
+    the main build (which must be current).  Returns the library path."""
+    import shutil
+    import tempfile
     build(verbose=False)
     r, ph, w = unit
     odir = os.path.join(ROOT, "build", "obj_" + name)
     os.makedirs(odir, exist_ok=True)
     obj = os.path.join(odir, f"kstep_r{r}_p{ph}_w{w}.o")
-    _compile((obj, os.path.join(CSRC, "kstep.hip"), [f"-DPD_KR={r}", f"-DPD_KPH={ph}", f"-DPD_KW={w}"] + list(defines)),
-             False)
+    src = os.path.join(CSRC, "kstep.hip")
+    tmp = None
+    if patch:
+        # the copy keeps the tree shape (csrc/ next to ../../include) so that includes resolve
+        tmp = tempfile.mkdtemp(prefix="pdvar_")
+        shutil.copytree(CSRC, os.path.join(tmp, "p", "csrc"))
+        shutil.copytree(os.path.join(os.path.dirname(ROOT), "include"), os.path.join(tmp, "include"))
+        subprocess.run(["patch", "-s", "-t", "-p2", "-d", os.path.join(tmp, "p", "csrc"), "-i", os.path.abspath(patch)],
+                       check=True)
+        src = os.path.join(tmp, "p", "csrc", "kstep.hip")
+    try:
+        _compile((obj, src, [f"-DPD_KR={r}", f"-DPD_KPH={ph}", f"-DPD_KW={w}"] + list(defines)), False)
+    finally:
+        if tmp:
+            shutil.rmtree(tmp, ignore_errors=True)
     out = os.path.join(PKG, f"libpdenv_{name}.so")
     objs = [obj if os.path.basename(u[0]) == os.path.basename(obj) else u[0] for u in units()]
     subprocess.run([HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", out] + objs, check=True)

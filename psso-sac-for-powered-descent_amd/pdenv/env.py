@@ -363,8 +363,13 @@ class PoweredDescentEnv:
         L.check(self.lib.pd_atmosphere(self.h, _ptr(alt), _ptr(out), int(alt.numel()), _stream(self.device)))
         return out[0], out[1], out[2]
 
+    def count_work(self, enable=True):
+        """Workload counting of the following step launches on/off (pd_count_work; a diagnostic
+        that costs the launches a few per cent): stats() then reports what they did."""
+        L.check(self.lib.pd_count_work(self.h, int(bool(enable))))
+
     WORK_COUNTERS = ("gust_substeps", "resets", "q_line", "q_verified", "q_taylor", "q_balanced", "q_miss",
-                     "balanced_rounds")
+                     "balanced_rounds", "q_refined", "q_bisect", "wave_substeps_refined", "wave_substeps_bisect")
 
     def stats(self):
         """Device statistics words (pd_stats): misses, NaN events, table entries, dropped queue

@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
-"""Time the c3 workload through pd_step_n (16 fused env-steps per launch) with the library named by
-PDENV_LIB (default the in-tree one): one JSON line with the event-timed k_step launch average and
-the wall ms per env-step.  N, LAUNCHES, PREC, LPE, PHASE from the environment."""
+"""Time the c3 workload through pd_step_n (F fused env-steps per launch, FUSE, default 16) with the
+library named by PDENV_LIB (default the in-tree one): one JSON line with the event-timed k_step
+launch average, the wall ms per env-step and the step kernel's workload counters over the timed
+launches.  N, LAUNCHES, PREC, LPE, PHASE from the environment; DESCENT=1: the c3-descent action
+mix (bench.py c3_actions) after bench.py's burn-in."""
 import json
 import math
 import os
@@ -15,7 +17,12 @@ import pdenv  # noqa: E402
 
 n = int(os.environ.get("N", "65536"))
 launches = int(os.environ.get("LAUNCHES", "24"))
-F = 16
+F = int(os.environ.get("FUSE", "16"))
+os.environ["PDENV_FUSE"] = str(F)
+descent = os.environ.get("DESCENT") == "1"
+sys.path.insert(0, REPO)
+import bench  # noqa: E402
+burn = bench.DESCENT_BURN_IN if descent else 0
 phase = os.environ.get("PHASE", "landing_burn_pure_throttle")
 t_c = time.perf_counter()
 env = pdenv.PoweredDescentEnv(n, flight_phase=phase, mode="rl" if phase == "landing_burn_pure_throttle" else "pso",
@@ -24,14 +31,17 @@ env = pdenv.PoweredDescentEnv(n, flight_phase=phase, mode="rl" if phase == "land
                               lanes_per_env=int(os.environ.get("LPE", "0")))
 t_create = time.perf_counter() - t_c
 g = torch.Generator(device="cuda").manual_seed(42)
-acts = (torch.rand((launches + 8) * F, n, env.action_dim, generator=g, device="cuda") * 2 - 1).contiguous()
+acts = bench.c3_actions(burn + (launches + 8) * F, n, g, "cuda", descent)
 kw = dict(device="cuda")
 outs = (torch.empty(F, n, env.obs_dim, dtype=env.dtype, **kw), torch.empty(F, n, dtype=env.dtype, **kw),
         torch.empty(F, n, dtype=torch.uint8, **kw), torch.empty(F, n, dtype=torch.uint8, **kw),
         torch.empty(F, n, dtype=torch.int8, **kw))
-for k in range(8):
-    env.step_n_raw(acts[k * F:(k + 1) * F], outs)
+for t0 in range(0, burn + 8 * F, F):
+    env.step_n_raw(acts[t0:min(t0 + F, burn + 8 * F)], outs)
 torch.cuda.synchronize()
+acts = acts[burn:]
+env.count_work(os.environ.get("COUNT") == "1")   # counting costs a few per cent: off unless asked
+w0 = env.stats()
 if os.environ.get("STATS"):      # the counters after the warmup launches (to difference)
     import ctypes as C
     from pdenv import _lib as L
@@ -47,7 +57,11 @@ for k in range(launches):
 torch.cuda.synchronize()
 wall = time.perf_counter() - t0
 ms = sorted(a.elapsed_time(b) for a, b in ev)
-print(json.dumps({"lib": os.path.basename(os.environ.get("PDENV_LIB", "libpdenv.so")), "n": n,
+w1 = env.stats()
+work = {k: w1[k] - w0[k] for k in env.WORK_COUNTERS}
+work["gust_steps_frac"] = work["gust_substeps"] / (n * launches * F * 4)
+print(json.dumps({"lib": os.path.basename(os.environ.get("PDENV_LIB", "libpdenv.so")), "n": n, "fuse": F,
+                  "descent": descent, "work": work,
                   "launch_ms_avg": sum(ms) / len(ms), "launch_ms_med": ms[len(ms) // 2],
                   "ms_per_step": sum(ms) / len(ms) / F, "wall_ms_per_step": wall * 1e3 / (launches * F),
                   "misses": env.counters()["rbf_misses"], "create_s": round(t_create, 2)}), flush=True)

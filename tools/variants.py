@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Build experiment variants of libpdenv (c3 step-kernel object only) in parallel:
-python tools/variants.py name=-DFOO,-DBAR name2=-DBAZ ..."""
+python tools/variants.py name=-DFOO,-DBAR name2=patch:tools/experiments/no_gust.patch ...
+(patch:<file> compiles a patched copy of csrc/; the product sources are never modified)"""
 import concurrent.futures as cf
 import os
 import sys
@@ -13,5 +14,9 @@ if __name__ == "__main__":
     b.build(verbose=False)
     specs = [a.split("=", 1) for a in sys.argv[1:]]
     with cf.ThreadPoolExecutor(max_workers=8) as ex:
-        for p in ex.map(lambda s: b.build_variant(s[0], [d for d in s[1].split(",") if d]), specs):
+        def one(sp):
+            items = [d for d in sp[1].split(",") if d]
+            patch = next((d[6:] for d in items if d.startswith("patch:")), None)
+            return b.build_variant(sp[0], [d for d in items if not d.startswith("patch:")], patch=patch)
+        for p in ex.map(one, specs):
             print(p)
