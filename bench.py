@@ -206,7 +206,7 @@ def other_workloads(args, local):
     short runs, summarised beside the headline line (`python bench.py --workload c4|c5` gives
     the full lines)."""
     res = {}
-    for wl, kw in (("c5", dict(steps=192, warmup=32)), ("c4", dict(steps=4, warmup=2, cpu_baseline=0))):
+    for wl, kw in (("c5", dict(steps=192, warmup=32)), ("c4", dict(steps=16, warmup=2, cpu_baseline=0))):
         sub = argparse.Namespace(**{**vars(args), **kw, "workload": wl})
         try:
             o = (bench_pso if wl == "c4" else bench_sac)(sub, 1, 0, local, None)

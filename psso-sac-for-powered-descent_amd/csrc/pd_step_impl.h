@@ -719,43 +719,63 @@ template <typename R> __device__ __forceinline__ R cl_query(R ae, R& sgn, bool& 
 // parameter-major [P][N] so that every load is coalesced across the envs of a wave.
 // Each output is the sequential sum over inputs (no FMA) plus the bias; tanh is evaluated in
 // binary64 and rounded (the oracle restates the same order: oracle/pd_oracle.c orc_actor).
+// The parameters are read in memory order through one running per-lane byte offset from the
+// single SGPR base of W (weight q of this lane's particle at ui * 4 + q * 4 N; N * P * 4 < 2^32,
+// validated by pd_rollout_policy), laundered after each step so that no offset is precomputed
+// and held: with constant 64-bit addresses the compiler kept ~370 SGPR pairs live and spilled
+// them.  Each output is still its own sequential sum plus the bias (the loads of a layer's
+// weights come first, then its biases).
 template <int IN, int NL, int OUT>
 __device__ __forceinline__ void actor_forward(const float* __restrict__ W, int64_t N, uint32_t ui,
                                               const float* x, float* y) {
     constexpr int H = 8;
     float h[H], g[H];
-    int64_t p = 0;
+    uint32_t sv = (uint32_t)N * 4u;
+    uint32_t off = ui * 4u;
+    asm volatile("" : "+v"(sv), "+v"(off));
+    auto next = [&]() {
+        const float v = *(const PD_AS1 float*)((const PD_AS1 char*)(uint64_t)W + off);
+        off += sv;
+        asm volatile("" : "+v"(off));
+        return v;
+    };
 #pragma unroll
     for (int j = 0; j < H; ++j) {
         float acc = 0.f;
 #pragma unroll
-        for (int k = 0; k < IN; ++k) acc = acc + ev(W + (p + j * IN + k) * N, ui) * x[k];
-        acc = acc + ev(W + (p + H * IN + j) * N, ui);
+        for (int k = 0; k < IN; ++k) acc = acc + next() * x[k];
+        g[j] = acc;
+    }
+#pragma unroll
+    for (int j = 0; j < H; ++j) {
+        const float acc = g[j] + next();
         h[j] = acc < 0.f ? 0.f : acc;
     }
-    p += H * IN + H;
 #pragma unroll
     for (int l = 0; l < NL; ++l) {
 #pragma unroll
         for (int j = 0; j < H; ++j) {
             float acc = 0.f;
 #pragma unroll
-            for (int k = 0; k < H; ++k) acc = acc + ev(W + (p + j * H + k) * N, ui) * h[k];
-            acc = acc + ev(W + (p + H * H + j) * N, ui);
-            g[j] = acc < 0.f ? 0.f : acc;
+            for (int k = 0; k < H; ++k) acc = acc + next() * h[k];
+            g[j] = acc;
         }
 #pragma unroll
-        for (int j = 0; j < H; ++j) h[j] = g[j];
-        p += H * H + H;
+        for (int j = 0; j < H; ++j) {
+            const float acc = g[j] + next();
+            h[j] = acc < 0.f ? 0.f : acc;
+        }
     }
+    float o[OUT];
 #pragma unroll
     for (int j = 0; j < OUT; ++j) {
         float acc = 0.f;
 #pragma unroll
-        for (int k = 0; k < H; ++k) acc = acc + ev(W + (p + j * H + k) * N, ui) * h[k];
-        acc = acc + ev(W + (p + H * OUT + j) * N, ui);
-        y[j] = (float)tanh((double)acc);
+        for (int k = 0; k < H; ++k) acc = acc + next() * h[k];
+        o[j] = acc;
     }
+#pragma unroll
+    for (int j = 0; j < OUT; ++j) y[j] = (float)tanh((double)(o[j] + next()));
 }
 
 // PD_STAMP (diagnostic builds only): per-wave shader-clock sections of k_step, summed into

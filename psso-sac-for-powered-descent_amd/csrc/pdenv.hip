@@ -1060,10 +1060,11 @@ template <typename R> void dispatch_step(const pd_env* e, const StepArgs<R>& a, 
     else { if (w) launch_lpe<R, 2, 0, true>(l, a, s); else launch_lpe<R, 2, 0, false>(l, a, s); }
 }
 
-template <typename R, int PH, bool W> void launch_policy(const StepArgs<R>& a, int lpe, int64_t n_launch, hipStream_t s) {
-    if (lpe >= 8) launch_policy_lpe<R, PH, W, 8>(a, n_launch, s);
-    else if (lpe == 4) launch_policy_lpe<R, PH, W, 4>(a, n_launch, s);
-    else launch_policy_lpe<R, PH, W, 2>(a, n_launch, s);
+// Policy rollouts run at 2 lanes per env whatever the handle's step LPE (the per-lane actor and
+// the LPE 2 table path fit 256 VGPRs without scratch; the LPE 4/8 variants spilled 36-172 B)
+constexpr int kPolicyLpe = 2;
+template <typename R, int PH, bool W> void launch_policy(const StepArgs<R>& a, int64_t n_launch, hipStream_t s) {
+    launch_policy_lpe<R, PH, W, kPolicyLpe>(a, n_launch, s);
 }
 
 template <typename R> void launch_insert(pd_env* e, hipStream_t s) {
@@ -1120,7 +1121,7 @@ pd_status rollout_policy_impl(pd_env* e, const float* w, int32_t max_steps, void
     int dev_cus = 256;
     (void)hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, e->device);
     const char* force = getenv("PDENV_COMPACT");
-    a.use_list = force && *force ? (atoi(force) != 0) : (N * e->lpe > (int64_t)dev_cus * 512);
+    a.use_list = force && *force ? (atoi(force) != 0) : (N * kPolicyLpe > (int64_t)dev_cus * 512);
     int64_t n_launch = N;
     int checks = 0;
     // F policy steps per launch (an episode that ends inside a launch is stored at its last step
@@ -1133,8 +1134,8 @@ pd_status rollout_policy_impl(pd_env* e, const float* w, int32_t max_steps, void
         t += a.n_fused;
         a.list_in = e->live[l & 1]; a.list_out = e->live[(l + 1) & 1];
         a.cnt_in = e->live_cnt + l % 3; a.cnt_out = e->live_cnt + (l + 1) % 3; a.cnt_zero = e->live_cnt + (l + 2) % 3;
-        if (e->cfg.phase == PD_PHASE_PURE_THROTTLE) { if (wind) launch_policy<R, 0, true>(a, e->lpe, n_launch, s); else launch_policy<R, 0, false>(a, e->lpe, n_launch, s); }
-        else { if (wind) launch_policy<R, 1, true>(a, e->lpe, n_launch, s); else launch_policy<R, 1, false>(a, e->lpe, n_launch, s); }
+        if (e->cfg.phase == PD_PHASE_PURE_THROTTLE) { if (wind) launch_policy<R, 0, true>(a, n_launch, s); else launch_policy<R, 0, false>(a, n_launch, s); }
+        else { if (wind) launch_policy<R, 1, true>(a, n_launch, s); else launch_policy<R, 1, false>(a, n_launch, s); }
         PD_HIP(hipGetLastError());
         if (F >= 16 || (l & (16 / F - 1)) == 16 / F - 1) launch_insert<R>(e, s);
         if (check_launches > 0 && (l + 1) % check_launches == 0 && t < max_steps) {
@@ -1308,6 +1309,9 @@ pd_status pd_rollout_policy(pd_env* e, const float* weights, int32_t n_params, i
     if (e->cfg.integrator != PD_INTEG_REFERENCE) return fail(PD_ERR_UNSUPPORTED, "policy rollouts use the reference integrator");
     int want = e->cfg.phase == PD_PHASE_PURE_THROTTLE ? PD_ACTOR_PARAMS_PURE_THROTTLE : PD_ACTOR_PARAMS_LANDING_BURN;
     if (n_params != want) return fail(PD_ERR_INVALID, "n_params does not match the phase's actor");
+    // the kernel addresses the parameter-major weights [P][N] with 32-bit per-lane byte offsets
+    if ((uint64_t)e->cfg.n_envs * (uint64_t)n_params * 4ull >= (1ull << 32))
+        return fail(PD_ERR_INVALID, "policy rollouts: n_envs x n_params x 4 must be below 2^32 bytes");
     PD_HIP(hipSetDevice(e->device));
     return e->rsize == 8 ? rollout_policy_impl<double>(e, weights, max_steps, fitness, steps, check_every, (hipStream_t)stream)
                          : rollout_policy_impl<float>(e, weights, max_steps, fitness, steps, check_every, (hipStream_t)stream);

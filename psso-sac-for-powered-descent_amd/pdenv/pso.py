@@ -66,17 +66,21 @@ def reinit_keep(pbf, swarm, n_swarms, keep_n):
 
 def migration_moves(swarm, n_swarms, n_migrants, rng):
     """migrate_particles' decisions (particle_swarm_optimisation.py:545-553) on the global
-    membership `swarm` (subswarm id per global particle): [(particle, new subswarm)]."""
-    members = [list(torch.nonzero(swarm == s).flatten().cpu().numpy()) for s in range(n_swarms)]
+    membership `swarm` (subswarm id per global particle): [(particle, new subswarm)].  The member
+    lists are NumPy index arrays (one read-back of the membership; pop = delete, append = concat,
+    the same order as the reference's Python lists)."""
+    sw = swarm.cpu().numpy() if torch.is_tensor(swarm) else np.asarray(swarm)
+    members = [np.flatnonzero(sw == s) for s in range(n_swarms)]
     moves = []
     for i in range(n_swarms):
         if len(members[i]) > 1:
             for _ in range(n_migrants):
                 k = rng.randrange(len(members[i]))
-                g = members[i].pop(k)
+                g = int(members[i][k])
+                members[i] = np.delete(members[i], k)
                 t = rng.choice([j for j in range(n_swarms) if j != i])
-                members[t].append(g)
-                moves.append((int(g), t))
+                members[t] = np.append(members[t], g)
+                moves.append((g, t))
     return moves
 
 
@@ -128,12 +132,17 @@ class ParticleSubswarmOptimisationGPU:
         self.x32 = self.x.float().contiguous()
         gid = torch.arange(self.offset, self.offset + self.P, device=self.device)
         self.swarm = (gid // self.sub_size).to(torch.int32).contiguous()
+        # subswarm / global bests stay on the device: a generation reads nothing back
         self.sb = torch.zeros(self.S, self.D, dtype=torch.float64, device=self.device)
-        self.sbf = [math.inf] * self.S
-        self.gbf, self.gb = math.inf, None
+        self.sbf_t = torch.full((self.S,), math.inf, dtype=torch.float64, device=self.device)
+        self.gbf_t = torch.full((), math.inf, dtype=torch.float64, device=self.device)
+        self.gb_t = torch.zeros(self.D, dtype=torch.float64, device=self.device)
+        self._cols = torch.arange(self.S, device=self.device)
         self.w = self.p["w_start"]
         self.env = PoweredDescentEnv(self.P, self.flight_phase, **self.env_kw) if self.P > 0 else None
-        self._aux = {}
+        # share_information evaluates 1..S-1 moved subswarm bests: one handle of S - 1 envs made
+        # here (creating a handle inside a generation costs tens of ms), candidates padded to it
+        self._aux = {self.S - 1: PoweredDescentEnv(self.S - 1, self.flight_phase, **self.env_kw)} if self.S > 1 else {}
         self.last_fitness = None
 
     def _env_for(self, n):
@@ -156,17 +165,32 @@ class ParticleSubswarmOptimisationGPU:
         return fit.double(), steps
 
     # ------------------------------------------------------------------ one generation
+    # host views of the device bests (each read synchronises; the generation itself never reads)
+    @property
+    def sbf(self):
+        return [float(v) for v in self.sbf_t.cpu()]
+
+    @property
+    def gbf(self):
+        return float(self.gbf_t)
+
+    @property
+    def gb(self):
+        return None if not math.isfinite(self.gbf) else self.gb_t.clone()
+
     def _swarm_minima(self, fit):
-        """Per subswarm: (min fitness, its position) over all ranks, first particle on ties."""
-        f = torch.full((self.S,), math.inf, dtype=torch.float64, device=self.device)
-        pos = torch.zeros(self.S, self.D, dtype=torch.float64, device=self.device)
-        for s in range(self.S):
-            m = self.swarm == s
-            if bool(m.any()):
-                fs = torch.where(m, fit, torch.full_like(fit, math.inf))
-                i = int(torch.argmin(fs))
-                f[s] = fs[i]
-                pos[s] = self.x[:, i]
+        """Per subswarm: (min fitness, its position) over all ranks, first particle on ties -- a
+        segmented argmin on the device ([S, P] masked fitness, torch.argmin takes the first
+        minimum), no host synchronisation.  A subswarm with no particle here reports +inf."""
+        if self.P > 0:
+            m = self.swarm.long()[None, :] == self._cols[:, None]                       # [S, P]
+            fs = torch.where(m, fit[None, :], torch.full_like(fit, math.inf)[None, :])
+            i = torch.argmin(fs, dim=1)                                                 # [S]
+            f = fs.gather(1, i[:, None]).squeeze(1)
+            pos = self.x.index_select(1, i).t().contiguous()                            # [S, D]
+        else:
+            f = torch.full((self.S,), math.inf, dtype=torch.float64, device=self.device)
+            pos = torch.zeros(self.S, self.D, dtype=torch.float64, device=self.device)
         if self.dist:
             fa = [torch.empty_like(f) for _ in range(self.world)]
             pa = [torch.empty_like(pos) for _ in range(self.world)]
@@ -183,14 +207,16 @@ class ParticleSubswarmOptimisationGPU:
         fit, _ = self.evaluate(self.x32)
         self.last_fitness = fit
         f, pos = self._swarm_minima(fit)
-        for s in range(self.S):                                 # :442-444
-            if float(f[s]) < self.sbf[s]:
-                self.sbf[s] = float(f[s])
-                self.sb[s] = pos[s]
-        for s in range(self.S):                                 # :474-477
-            if self.sbf[s] < self.gbf:
-                self.gbf = self.sbf[s]
-                self.gb = self.sb[s].clone()
+        # :442-444 per subswarm: a strictly better minimum replaces the subswarm best
+        better = f < self.sbf_t
+        self.sbf_t = torch.where(better, f, self.sbf_t)
+        self.sb = torch.where(better[:, None], pos, self.sb)
+        # :474-477 subswarms in order, strictly better replaces: the first subswarm holding the
+        # minimum, if it beats the global best
+        j = torch.argmin(self.sbf_t)
+        upd = self.sbf_t[j] < self.gbf_t
+        self.gbf_t = torch.where(upd, self.sbf_t[j], self.gbf_t)
+        self.gb_t = torch.where(upd, self.sb[j], self.gb_t)
         self.w = self.p["w_start"] - (self.p["w_start"] - self.p["w_end"]) * gen / self.p["generations"]
         if self.P > 0:
             L.check(self.lib.pd_pso_step(self.P, self.D, _ptr(fit), _ptr(self.pbf), _ptr(self.x), _ptr(self.v),
@@ -215,18 +241,20 @@ class ParticleSubswarmOptimisationGPU:
         """:521-543: for every subswarm but the best, with probability 1/2 its best position moves
         30 % toward the best subswarm's; the moved position is re-evaluated and its fitness kept
         only if better (the position is kept either way, as in the reference)."""
-        best = int(np.argmin(self.sbf))
+        best = int(np.argmin(self.sbf))                         # (one read-back: the rng draws depend on it)
         moved = [i for i in range(self.S) if i != best and self.rng.random() < 0.5]
         if not moved:
             return
         for i in moved:
             self.sb[i] = (1 - 0.3) * self.sb[i] + 0.3 * self.sb[best]
-        cand = self.sb[moved].t().float().contiguous()          # [D][k]
+        pad = moved + [moved[0]] * (self.S - 1 - len(moved))  # (padded to the share handle's size)
+        cand = self.sb[pad].t().float().contiguous()            # [D][S-1]
         fit, _ = self.evaluate(cand)
+        fit = fit[:len(moved)]
         self.share_log = (moved, fit.clone())
-        for k, i in enumerate(moved):
-            if float(fit[k]) < self.sbf[i]:
-                self.sbf[i] = float(fit[k])
+        mv = torch.tensor(moved, device=self.device)
+        old = self.sbf_t[mv]
+        self.sbf_t[mv] = torch.where(fit < old, fit, old)
 
     def migrate_particles(self):
         """:545-553: number_of_migrants random particles of every subswarm (with > 1 member) move

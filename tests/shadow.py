@@ -123,3 +123,69 @@ def check_stats(stats, tol_rew=1e-9, tol_obs=1e-6, tol_filt=1e-12):
     assert stats["max_rew"] <= tol_rew, stats["max_rew"]
     assert stats["max_obs"] <= tol_obs, stats["max_obs"]
     assert stats["max_filt"] <= tol_filt, stats["max_filt"]
+
+
+def policy_snapshots(env, W, K):
+    """pd_rollout_policy with max_steps = k for k = 0..K (the rollout is deterministic: the state
+    after k policy steps of a longer rollout): per k the handle's complete per-env state, the
+    fitness (-sum of rewards) and the episode lengths, host numpy, all particles."""
+    import torch
+    out = []
+    Wt = torch.as_tensor(W, device=env.device)
+    for k in range(K + 1):
+        fit, steps = env.rollout_policy(Wt, max_steps=k)
+        vp, ring, ln, hd = env.gload_window()
+        _, _, tid = env.episode_counters()
+        out.append({"s": env.state.cpu().numpy(), "act": env.actuators.cpu().numpy(), "vprev": vp.cpu().numpy(),
+                     "ring": ring.cpu().numpy(), "len": ln.cpu().numpy(), "head": hd.cpu().numpy(),
+                     "tid": tid.cpu().numpy(), "fit": fit.cpu().numpy(), "steps": steps.cpu().numpy()})
+    return out
+
+
+def shadow_policy(oracle_mod, snaps, W, idx, phase):
+    """Teacher-forced parity of a policy rollout (fused actor + env step + PSO reward, no wind)
+    on particles `idx`: for every policy step k -> k + 1 a particle takes, the oracle loads the
+    device's complete state after k steps, runs its actor (orc_actor: the same binary32 order)
+    and one env step (orc_step, rtd_pso), and must equal the device after k + 1 steps: state per
+    TOL_STEP, reward (fitness difference) <= 1e-9 + 1e-12 |fitness|, done/truncated (an ended
+    episode is frozen: its length stops growing) and the truncation id exactly."""
+    L = oracle_mod.lib()
+    P = oracle_mod.params()
+    o = oracle_mod.OrcOut()
+    E = oracle_mod.OrcEnv()
+    stats = dict(steps=0, ended=0, max_err=np.zeros(11), max_rew=0.0, trunc_ids=set())
+    K = len(snaps) - 1
+    for j in idx:
+        for k in range(K - 1):
+            a, b, c = snaps[k], snaps[k + 1], snaps[k + 2]
+            if int(b["steps"][j]) != k + 1:      # the episode ended before this step
+                break
+            L.orc_reset(C.byref(P), C.byref(E), None, 0, 0, C.c_double(1.0), C.c_double(1.0))
+            for q in range(11):
+                E.s[q] = float(a["s"][j, q])
+            E.prev_s[2] = float(a["vprev"][j])
+            n, h = int(a["len"][j]), int(a["head"][j])
+            for q in range(10):
+                E.gwin[q] = float(a["ring"][j, q if n < 10 else (h + q) % 10])
+            E.gwin_len = n
+            E.trunc_id = int(a["tid"][j])
+            E.gimbal_prev, E.dl_prev, E.dr_prev = (float(v) for v in a["act"][j])
+            u = oracle_mod.actor(phase, W[j], a["s"][j]).astype(np.float64)
+            ua = (C.c_double * 4)(*(list(u) + [0.0] * (4 - len(u))))
+            L.orc_step(C.byref(P), C.byref(E), phase, 1, ua, 1, None, C.byref(o))
+            ctx = f"particle {j} step {k}"
+            so = np.array(E.s[:])
+            err = np.abs(b["s"][j] - so) / np.maximum(np.abs(so), 1e-3)
+            stats["max_err"] = np.maximum(stats["max_err"], err)
+            rew = float(a["fit"][j]) - float(b["fit"][j])
+            stats["max_rew"] = max(stats["max_rew"], abs(rew - o.reward))
+            assert abs(rew - o.reward) <= 1e-9 + 1e-12 * abs(float(b["fit"][j])), (ctx, rew, o.reward)
+            ended = bool(o.done or o.trunc)
+            assert (int(c["steps"][j]) == k + 1) == ended, (ctx, int(c["steps"][j]), ended)
+            assert int(b["tid"][j]) == o.trunc_id, ctx
+            stats["steps"] += 1
+            if ended:
+                stats["ended"] += 1
+                stats["trunc_ids"].add(o.trunc_id)
+                break
+    return stats

@@ -245,3 +245,28 @@ def test_c4_per_gpu_share_32768_particles(pd, oracle_mod):
     x0 = opt.x.clone()
     opt.generation(0)
     assert not torch.equal(x0, opt.x) and bool((opt.x.abs() <= 1.5).all())
+
+
+def test_c4_policy_rollout_shadowed(pd, oracle_mod):
+    """c4's per-GPU share (32 768 landing_burn particles ~ U(-1.5, 1.5), the fused actor +
+    compaction kernel) teacher-forced at EVERY policy step until every sampled episode ends: 128
+    sampled particles (both ends of the batch and spread through it); per step the oracle's
+    actor + env step from the device's complete state must equal the device's next state,
+    reward, done/truncated and truncation id (tests/shadow.py shadow_policy).  The ensemble
+    bounds of test_c4_per_gpu_share_32768_particles stay as a secondary, free-running check."""
+    import torch
+    from shadow import policy_snapshots, shadow_policy, TOL_STEP, ST
+    N = 32768
+    W = np.random.default_rng(17).uniform(-1.5, 1.5, (N, 372)).astype(np.float32)
+    env = pd.PoweredDescentEnv(N, flight_phase="landing_burn", mode="pso")
+    _, steps = env.rollout_policy(torch.tensor(W), max_steps=2200)
+    idx = np.unique(np.concatenate([np.arange(16), np.arange(N - 16, N), np.linspace(16, N - 17, 96).astype(int)]))
+    K = int(steps.cpu().numpy()[idx].max()) + 1
+    assert K <= 400, K                      # (the sampled episodes all end: snapshots cost O(K^2) steps)
+    snaps = policy_snapshots(env, W, K)
+    assert (snaps[K]["steps"][idx] < K).all()
+    st = shadow_policy(oracle_mod, snaps, W, idx, 1)
+    bad = {ST[k]: float(st["max_err"][k]) for k in range(11) if st["max_err"][k] > TOL_STEP[k]}
+    assert not bad, bad
+    assert st["ended"] == len(idx), (st["ended"], len(idx))     # every sampled episode followed to its end
+    assert st["steps"] >= 10 * len(idx), st["steps"]

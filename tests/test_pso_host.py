@@ -1,0 +1,46 @@
+"""CPU checks of the PSO driver's host-side decisions (pdenv/pso.py)."""
+import os
+import random
+import sys
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "psso-sac-for-powered-descent_amd"))
+
+
+def _moves_lists(swarm, n_swarms, n_migrants, rng):
+    """particle_swarm_optimisation.py:545-553 with Python lists, as the reference keeps them."""
+    members = [list(np.flatnonzero(np.asarray(swarm) == s)) for s in range(n_swarms)]
+    moves = []
+    for i in range(n_swarms):
+        if len(members[i]) > 1:
+            for _ in range(n_migrants):
+                k = rng.randrange(len(members[i]))
+                g = members[i].pop(k)
+                t = rng.choice([j for j in range(n_swarms) if j != i])
+                members[t].append(g)
+                moves.append((int(g), t))
+    return moves
+
+
+def test_migration_moves_equal_list_restatement():
+    """The NumPy member arrays take the same decisions as the reference's lists (pop/append
+    order, rng stream) for random memberships, subswarm counts and migrant numbers, including
+    subswarms with one member or none (and, like the reference, fail when a subswarm's own
+    migrants empty it: the len > 1 check precedes the migrant loop)."""
+    from pdenv.pso import migration_moves
+    for seed in range(200):
+        r = np.random.default_rng(seed)
+        S = int(r.integers(2, 6))
+        n = int(r.integers(0, 40))
+        sw = torch.tensor(r.integers(0, S, n), dtype=torch.int32)
+        k = int(r.integers(1, 4))
+        out = []
+        for f, arg in ((migration_moves, sw), (_moves_lists, sw.numpy())):
+            try:
+                out.append(f(arg, S, k, random.Random(seed)))
+            except ValueError as e:    # a subswarm emptied by its own migrants: both raise
+                out.append(type(e))
+        assert out[0] == out[1], seed

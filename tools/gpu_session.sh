@@ -23,6 +23,8 @@ for s in $STAGES; do
     bench) stage bench 600 python bench.py ;;
     bench32) stage bench32 600 python bench.py --precision f32 ;;
     prof) stage prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 192 --warmup 32 --cpu-baseline 0 --secondary 0 --others 0 --descent 1 ;;
+    profc4) stage profc4 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/profc4 -o run -- python3 bench.py --workload c4 --steps 16 --warmup 2 --cpu-baseline 0 ;;
+    profc5) stage profc5 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/profc5 -o run -- python3 bench.py --workload c5 --steps 192 --warmup 32 ;;
     profdrv) stage profdrv 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/profdrv -o run -- python3 bench.py --steps 20 --warmup 5 --cpu-baseline 0 --secondary 0 --others 0 --descent 1 ;;
     prof32) stage prof32 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof32 -o run -- python3 bench.py --steps 96 --warmup 16 --cpu-baseline 0 --secondary 0 --others 0 --precision f32 ;;
     sweep) stage sweep 600 python tools/sweep.py ;;
