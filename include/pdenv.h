@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define PD_ABI_VERSION 5   /* 4: pd_config.integrator (was padding); 5: pd_count_work */
+#define PD_ABI_VERSION 5   /* 4: pd_config.integrator (was padding); 5: pd_count_work, pd_step_sac */
 #define PD_MAX_PTS 256      /* aero scatter points per table */
 #define PD_MAX_COLS 5       /* AoA columns per aero table */
 #define PD_MAX_TAB 64       /* grid-fin table length */
@@ -207,6 +207,20 @@ pd_status pd_step(pd_env* env, const void* actions, void* obs, void* reward, uin
  * to n_steps pd_step calls.  No host synchronisation. */
 pd_status pd_step_n(pd_env* env, const void* actions, int32_t n_steps, void* obs, void* reward, uint8_t* done,
                     uint8_t* truncated, int8_t* trunc_id, void* stream);
+/* One SAC data-collection step (sac_pytorch_powered_descent.py:160-183 for N envs) in one
+ * launch.  The action is sampled in the kernel from the caller's actor heads, as Actor.sample
+ * does it (sac_pytorch.py:161-179) in binary32: a = tanh(mean + exp(clamp(log_std, log_std_min,
+ * log_std_max)) * eps) * max_action, or tanh(mean) * max_action when eps is NULL (deterministic);
+ * mean, log_std, eps [N][A] float32 (eps: standard normals, e.g. torch.randn).  Then the env steps
+ * as pd_step (auto-reset per config) and the kernel epilogue writes, all float32 and any of them
+ * NULL: action [N][A]; slab [N][2 S + A + 2], the replay buffer's transition row
+ * state | action | reward | next_state | done (sac_pytorch.py:27-35; next_state the terminal
+ * observation before any reset, done without truncation, as the driver stores them,
+ * sac_pytorch_powered_descent.py:170-176); obs32 [N][S], the observation the actor sees next
+ * (after any auto-reset).  RL landing-burn handles (PD_PHASE_PURE_THROTTLE / PD_PHASE_LANDING_BURN,
+ * rtd RL or NONE, reference integrator) with float32 actions only.  No host synchronisation. */
+pd_status pd_step_sac(pd_env* env, const float* mean, const float* log_std, const float* eps, float log_std_min,
+                      float log_std_max, float max_action, float* action, float* slab, float* obs32, void* stream);
 /* Multi-step rollout with device-resident actions [T][N][A]: the fused launches of pd_step_n
  * (per-step launches for the other phases), rewards accumulated into reward_sum [N] (may be
  * NULL), no per-step outputs.  No host synchronisation. */

@@ -298,11 +298,9 @@ __device__ __forceinline__ R hyper_interp(DP<R>& P, int col, R mach) {
 __host__ __device__ constexpr int obs_dim(int kind) {
     return kind == 2 || kind == 3 ? 5 : (kind == 4 ? 1 : (kind == 5 ? 4 : (kind == 7 ? 8 : 2)));
 }
-template <typename R>
-__device__ __forceinline__ void obs_write(DP<R>& P, int kind, const R* s, R* out, uint32_t idx) {
-    const int d = obs_dim(kind);
-    PD_AS1 char* o = (PD_AS1 char*)(uint64_t)out;
-    auto put = [&](int k, R v) { *(PD_AS1 R*)(o + (uint32_t)(idx * (uint32_t)(d * sizeof(R)) + k * (uint32_t)sizeof(R))) = v; };
+// obs_eval: the observation's components to put(k, value); obs_write: to row idx of out [N][dim]
+template <typename R, typename Put>
+__device__ __forceinline__ void obs_eval(DP<R>& P, int kind, const R* s, Put&& put) {
     if (kind == 0) {
         put(0, (R(1) - (R)(float)s[1] / P.norm_y) * R(2) - R(1));
         put(1, (R(1) - (R)(float)s[3] / P.norm_vy) * R(2) - R(1));
@@ -325,6 +323,14 @@ __device__ __forceinline__ void obs_write(DP<R>& P, int kind, const R* s, R* out
             put(k, (R)(float)((R)(float)s[j] / P.norm_ph[k]));
         }
     }
+}
+template <typename R>
+__device__ __forceinline__ void obs_write(DP<R>& P, int kind, const R* s, R* out, uint32_t idx) {
+    const int d = obs_dim(kind);
+    PD_AS1 char* o = (PD_AS1 char*)(uint64_t)out;
+    obs_eval<R>(P, kind, s, [&](int k, R v) {
+        *(PD_AS1 R*)(o + (uint32_t)(idx * (uint32_t)(d * sizeof(R)) + k * (uint32_t)sizeof(R))) = v;
+    });
 }
 
 // ---------------------------------------------------------------- tables in LDS

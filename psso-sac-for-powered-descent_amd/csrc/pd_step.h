@@ -131,6 +131,12 @@ template <typename R> struct StepArgs {
     int rtd_none;                    // PD_RTD_NONE: physics stepping only (reward/done/trunc 0)
     int n_fused;                     // env-steps per launch (actions/outputs: [n_fused][N] rows)
     int count_work;                  // workload counters on (pd_count_work; diagnostic launches)
+    // pd_step_sac (single-step launches): the action sampled from the actor's heads in the kernel,
+    // tanh(mean + exp(clamp(log_std, lo, hi)) eps) max (eps NULL: tanh(mean) max), and float32
+    // outputs: the action, the transition row [N][2S + A + 2] and the next observation [N][S]
+    const float* sac_mean; const float* sac_logstd; const float* sac_eps;
+    float sac_lo, sac_hi, sac_max;
+    float* sac_act; float* slab; float* obs32;
 };
 
 // Kernel launchers, explicitly instantiated in the kstep_*.hip translation units.

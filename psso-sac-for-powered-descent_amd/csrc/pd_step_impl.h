@@ -839,8 +839,10 @@ __device__ __forceinline__ TabView<R> tab_view(DP<R>& P, const R* tab, int table
 // theta_dot, m, m_prop) with rocket_physics_fcn's forces at each stage, 10 x 0.01 s per env step;
 // the loop body below runs once per stage (oracle: orc_physics, ORC_INTEG_RK4, same order)
 // CNT: the counting instantiation (pd_count_work; LPE 2 step kernels): without it every counting
-// site folds away
-template <typename R, int PHASE, int RTD, bool WIND, int LPE, int POL = 0, bool RK4 = false, bool CNT = false>
+// site folds away.  SAC: the pd_step_sac instantiation (RL landing burns): action sampling from
+// the actor heads and the float32 transition-slab / next-observation epilogue
+template <typename R, int PHASE, int RTD, bool WIND, int LPE, int POL = 0, bool RK4 = false, bool CNT = false,
+          bool SAC = false>
 // waves_per_eu(2): caps VGPR+AGPR at 256 so the f64 kernel keeps two waves per SIMD
 #ifndef PD_WPE
 #define PD_WPE 2
@@ -1042,12 +1044,37 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
                           (float)(e.s[3] / Q.norm_vy), (float)tanh(Q.k_theta_pso * (e.s[4] - Cst<R>::pi / R(2)))};
             actor_forward<5, 4, 4>(a.policy_w, N, uw, x, uf);
         }
+    } else if constexpr (SAC) {
+        // Actor.sample (sac_pytorch.py:161-179) on the caller's two heads, in binary32 as torch
+        // computes it: log_std clamped (forward), std = exp, x = mean + std * eps (rsample),
+        // action = tanh(x) * max_action; eps NULL: tanh(mean) * max_action (deterministic)
+#pragma unroll
+        for (int k = 0; k < A; ++k) if (k < AD) {
+            const float m = ldv(a.sac_mean + k, ui * AD);
+            float xk = m;
+            if (a.sac_eps) {
+                float ls = ldv(a.sac_logstd + k, ui * AD);
+                ls = ls < a.sac_lo ? a.sac_lo : (ls > a.sac_hi ? a.sac_hi : ls);
+                const float sd = expf(ls);
+                xk = m + sd * ldv(a.sac_eps + k, ui * AD);
+            }
+            uf[k] = tanhf(xk) * a.sac_max;
+            if (a.sac_act && role == 0 && live) ev(a.sac_act + k, ui * AD) = uf[k];
+        }
     } else if (a.act_f64) {
 #pragma unroll
         for (int k = 0; k < A; ++k) if (k < AD) ud[k] = ldv((const double*)a.actions + fo * AD + k, ui * AD);
     } else {
 #pragma unroll
         for (int k = 0; k < A; ++k) if (k < AD) uf[k] = ldv((const float*)a.actions + fo * AD + k, ui * AD);
+    }
+    // pd_step_sac: the transition row of this step starts with the observation of its start state
+    constexpr int kObsKind = RTD == 1 ? (PHASE == 0 ? 1 : 2) : (PHASE == 0 ? 0 : (PHASE == 1 ? 3 : -1));
+    if (SAC && a.slab && role == 0 && live) {
+        DP<R>& Q = *params<R>(a.P);
+        const int ok = kObsKind >= 0 ? kObsKind : Q.obs_kind;
+        const uint32_t W = 2u * (uint32_t)obs_dim(ok) + (uint32_t)AD + 2u;
+        obs_eval<R>(Q, ok, e.s, [&](int k, R v) { ev(a.slab, ui * W + (uint32_t)k) = (float)v; });
     }
     R gdeg_out = e.act0, dcmdl_out = e.act1, dcmdr_out = e.act2;
     const R gprev = e.act0, dlprev = e.act1, drprev = e.act2;
@@ -1664,8 +1691,7 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
         asm volatile("" : "+v"(uo));
         if (a.obs) {
             // the wrappers' observation (obs_write kinds); compile-time for the landing burns
-            constexpr int kind = RTD == 1 ? (PHASE == 0 ? 1 : 2) : (PHASE == 0 ? 0 : (PHASE == 1 ? 3 : -1));
-            const int ok = kind >= 0 ? kind : P2.obs_kind;
+            const int ok = kObsKind >= 0 ? kObsKind : P2.obs_kind;
             obs_write<R>(P2, ok, s, a.obs + fo * obs_dim(ok), uo);
         }
         if (a.reward) ev(a.reward + fo, ui) = rew;
@@ -1680,6 +1706,18 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
         if (a.trunc) ev(a.trunc + fo, ui) = (uint8_t)tr;
         if (a.trunc_id) ev(a.trunc_id + fo, ui) = (int8_t)id;
         if (a.info) ev(a.info + (PD_INFO_GLOAD) * N, uo) = gl;
+        if (SAC && a.slab) {
+            // state | action | reward | next_state (terminal, before any reset) | done: the
+            // replay buffer's row (sac_pytorch.py:27-35; done without truncation, as the driver
+            // stores it, sac_pytorch_powered_descent.py:170-176)
+            const int ok = kObsKind >= 0 ? kObsKind : P2.obs_kind;
+            const uint32_t S = (uint32_t)obs_dim(ok), W = 2u * S + (uint32_t)AD + 2u, r0 = uo * W;
+#pragma unroll
+            for (int k = 0; k < A; ++k) if (k < AD) ev(a.slab, r0 + S + (uint32_t)k) = uf[k];
+            ev(a.slab, r0 + S + (uint32_t)AD) = (float)rew;
+            obs_eval<R>(P2, ok, s, [&](int k, R v) { ev(a.slab, r0 + S + (uint32_t)AD + 1u + (uint32_t)k) = (float)v; });
+            ev(a.slab, r0 + 2u * S + (uint32_t)AD + 1u) = (float)dn;
+        }
     }
     // ---- the env's bookkeeping for the next step: auto-reset in registers, or carry on
     if (ended) {
@@ -1691,6 +1729,11 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
         e.tid = id;
         e.ts = e.ts + 1;
         e.act0 = gdeg_out; e.act1 = dcmdl_out; e.act2 = dcmdr_out;
+    }
+    if (SAC && a.obs32 && role == 0 && live) {   // pd_step_sac: what the actor sees next (after any reset)
+        const int ok = kObsKind >= 0 ? kObsKind : P2.obs_kind;
+        const uint32_t S = (uint32_t)obs_dim(ok);
+        obs_eval<R>(P2, ok, e.s, [&](int k, R v) { ev(a.obs32, ui * S + (uint32_t)k) = (float)v; });
     }
     if constexpr (POL) {
         // an episode that ended is stored now and its lanes freeze (they go on computing in step
@@ -1741,8 +1784,14 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
 template <typename R, int PH, int RT, bool W, int LPE, bool RK> void launch_step(const StepArgs<R>& a, hipStream_t s) {
     unsigned grid = (unsigned)((a.n * LPE + kStepBlock - 1) / kStepBlock);
     if constexpr (LPE == 2 && !RK) {
-        if (a.count_work) {
+        if (a.count_work && !a.sac_mean) {
             hipLaunchKernelGGL((k_step<R, PH, RT, W, LPE, 0, RK, true>), dim3(grid), dim3(kStepBlock), 0, s, a);
+            return;
+        }
+    }
+    if constexpr (RT == 0 && PH <= 1 && !RK) {
+        if (a.sac_mean) {
+            hipLaunchKernelGGL((k_step<R, PH, RT, W, LPE, 0, RK, false, true>), dim3(grid), dim3(kStepBlock), 0, s, a);
             return;
         }
     }

@@ -1072,14 +1072,26 @@ template <typename R> void launch_insert(pd_env* e, hipStream_t s) {
                        e->keys_cl, (R*)e->pay_cl, e->logcap_cl);
 }
 
+// pd_step_sac's inputs and float32 outputs (see include/pdenv.h)
+struct SacIO {
+    const float *mean, *log_std, *eps;
+    float lo, hi, max_action;
+    float *action, *slab, *obs32;
+};
+
 template <typename R>
 pd_status step_impl(pd_env* e, const void* actions, void* obs, void* reward, uint8_t* done, uint8_t* trunc,
                     int8_t* tid, const double* noise, void* info, void* reward_sum, hipStream_t s,
-                    int n_fused = 1) {
+                    int n_fused = 1, const SacIO* sac = nullptr) {
     StepArgs<R> a = make_args<R>(e);
     a.actions = actions; a.obs = (R*)obs; a.reward = (R*)reward; a.done = done; a.trunc = trunc; a.trunc_id = tid;
     a.noise = noise; a.info = (R*)info; a.reward_sum = (R*)reward_sum;
     a.n_fused = n_fused;
+    if (sac) {
+        a.sac_mean = sac->mean; a.sac_logstd = sac->log_std; a.sac_eps = sac->eps;
+        a.sac_lo = sac->lo; a.sac_hi = sac->hi; a.sac_max = sac->max_action;
+        a.sac_act = sac->action; a.slab = sac->slab; a.obs32 = sac->obs32;
+    }
     dispatch_step<R>(e, a, s);
     PD_HIP(hipGetLastError());
     return PD_OK;
@@ -1273,6 +1285,23 @@ pd_status pd_step(pd_env* e, const void* actions, void* obs, void* reward, uint8
     if (e->rsize == 8)
         return step_impl<double>(e, actions, obs, reward, done, truncated, trunc_id, noise, info, nullptr, (hipStream_t)stream);
     return step_impl<float>(e, actions, obs, reward, done, truncated, trunc_id, noise, info, nullptr, (hipStream_t)stream);
+}
+
+pd_status pd_step_sac(pd_env* e, const float* mean, const float* log_std, const float* eps, float log_std_min,
+                      float log_std_max, float max_action, float* action, float* slab, float* obs32, void* stream) {
+    if (!e || !mean) return fail(PD_ERR_INVALID, "null env/mean");
+    if (eps && !log_std) return fail(PD_ERR_INVALID, "pd_step_sac: eps given without log_std");
+    if (e->cfg.action_f64) return fail(PD_ERR_UNSUPPORTED, "pd_step_sac: float32 actions only (action_f64 = 0)");
+    if (e->cfg.rtd == PD_RTD_PSO || e->cfg.integrator != PD_INTEG_REFERENCE ||
+        (e->cfg.phase != PD_PHASE_PURE_THROTTLE && e->cfg.phase != PD_PHASE_LANDING_BURN))
+        return fail(PD_ERR_UNSUPPORTED, "pd_step_sac: the RL landing burns (reference integrator) only");
+    PD_HIP(hipSetDevice(e->device));
+    const SacIO io{mean, log_std, eps, log_std_min, log_std_max, max_action, action, slab, obs32};
+    if (e->rsize == 8)
+        return step_impl<double>(e, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
+                                 (hipStream_t)stream, 1, &io);
+    return step_impl<float>(e, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
+                            (hipStream_t)stream, 1, &io);
 }
 
 pd_status pd_step_n(pd_env* e, const void* actions, int32_t n_steps, void* obs, void* reward, uint8_t* done,

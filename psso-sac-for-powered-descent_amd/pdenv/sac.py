@@ -168,12 +168,16 @@ class SACCollector:
     learner-rank buffer append.  `obs` always holds the observation the actor sees next (the
     post-auto-reset observation of envs whose episode ended).
 
-    use_graph=True captures actor + env step + slab + observe into one HIP graph (the step is
-    ~20 small launches; replaying a graph removes their launch gaps).  The gather and the
-    buffer append run eagerly after each replay; the aero-miss flush runs every 16 steps."""
+    fused=True (default): the actor's MLP and heads in PyTorch, eps by torch.randn, then ONE
+    kernel (pd_step_sac) samples the action from the heads, steps the envs and writes the
+    transition slab and the next float32 observation -- no slab cat, no casts, no observe.
+    fused=False: Actor.sample, pd_step, transition_slab, pd_observe (the unfused reference path).
+    use_graph=True captures the step into one HIP graph (replaying removes the launch gaps).
+    The gather and the buffer append run eagerly after each replay; the aero-miss flush runs
+    every 16 steps."""
 
     def __init__(self, env, actor, buffer=None, dist=None, learner_rank=0, generator=None,
-                 deterministic=False, use_graph=False, flush_every=16):
+                 deterministic=False, use_graph=False, flush_every=16, fused=True):
         self.env, self.actor, self.buffer, self.dist = env, actor, buffer, dist
         self.learner_rank, self.generator, self.deterministic = learner_rank, generator, deterministic
         self.rank = dist.get_rank() if dist is not None and dist.is_initialized() else 0
@@ -182,10 +186,23 @@ class SACCollector:
         self.steps = 0
         self.graph = None
         self.use_graph = use_graph
+        self.fused = fused
+        S, A = env.obs_dim, env.action_dim
+        self._slab_buf = torch.empty(env.n, 2 * S + A + 2, dtype=torch.float32, device=self.obs.device)
+        self.action = torch.empty(env.n, A, dtype=torch.float32, device=self.obs.device)
 
     def _body(self):
-        """actor -> pd_step -> slab -> observe into self.obs; returns the slab (no syncs)."""
+        """actor -> env step -> slab and next obs into self.obs; returns the slab (no syncs)."""
         gen = None if self.use_graph else self.generator
+        if self.fused:
+            f = self.actor.shared_net(self.obs)
+            mean, log_std = self.actor.mean(f), self.actor.log_std(f)     # (the kernel clamps log_std)
+            eps = None
+            if not self.deterministic:
+                eps = torch.randn(mean.shape, device=mean.device, dtype=mean.dtype, generator=gen)
+            self.env.step_sac(mean, log_std, eps, self.actor.log_std_min, self.actor.log_std_max,
+                              self.actor.max_action, action=self.action, slab=self._slab_buf, obs32=self.obs)
+            return self._slab_buf
         act, _ = self.actor.sample(self.obs, deterministic=self.deterministic, generator=gen, with_log_prob=False)
         act = act.float().contiguous()
         self.env.step_raw_noflush(act)

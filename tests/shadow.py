@@ -163,7 +163,8 @@ def shadow_policy(oracle_mod, snaps, W, idx, phase):
             L.orc_reset(C.byref(P), C.byref(E), None, 0, 0, C.c_double(1.0), C.c_double(1.0))
             for q in range(11):
                 E.s[q] = float(a["s"][j, q])
-            E.prev_s[2] = float(a["vprev"][j])
+                E.prev_s[q] = 0.0
+            E.prev_s[2] = float(a["vprev"][j])           # |v_prev| = sqrt(fl(vprev^2)) exactly
             n, h = int(a["len"][j]), int(a["head"][j])
             for q in range(10):
                 E.gwin[q] = float(a["ring"][j, q if n < 10 else (h + q) % 10])

@@ -500,6 +500,41 @@ def test_pso_driver_generations_vs_numpy(pd):
     assert np.array_equal(opt.swarm.cpu().numpy(), swarm)
 
 
+def test_sac_step_fused_sampling_and_slab(pd):
+    """pd_step_sac (c5's fused step): the action sampled in the kernel from the actor heads equals
+    torch's Actor.sample arithmetic (clamp, exp, mean + std eps, tanh, x max_action) to 3 float32
+    ulps, and with that action a twin env stepped by pd_step gives the slab's reward, next
+    observation and done and the next observation bit for bit (the slab's state is the float32
+    observation the actor saw)."""
+    import torch
+    from pdenv.sac import Actor
+    torch.manual_seed(3)
+    N = 2048
+    actor = Actor(2, 1).cuda()
+    env = make(pd, N, mode="rl", auto_reset=True, seed=9, tilt_sigma_rad=0.05)
+    twin = make(pd, N, mode="rl", auto_reset=True, seed=9, tilt_sigma_rad=0.05)
+    obs = env.reset().float().contiguous()
+    twin.reset()
+    g = torch.Generator(device="cuda").manual_seed(5)
+    act = torch.empty(N, 1, device="cuda")
+    slab = torch.empty(N, 7, device="cuda")
+    for t in range(60):
+        with torch.no_grad():
+            f = actor.shared_net(obs)
+            mean, ls = actor.mean(f), actor.log_std(f)
+        eps = torch.randn(mean.shape, device="cuda", generator=g)
+        ref = torch.tanh(mean + torch.clamp(ls, -20.0, 2.0).exp() * eps) * 1.0
+        seen = obs.clone()
+        env.step_sac(mean, ls, eps, -20.0, 2.0, 1.0, action=act, slab=slab, obs32=obs)
+        assert (act - ref).abs().max() <= 2e-7, (t, float((act - ref).abs().max()))
+        o, r, d, _, _ = twin.step(act)
+        assert torch.equal(slab[:, :2], seen) and torch.equal(slab[:, 2:3], act)
+        assert torch.equal(slab[:, 3], r.float()) and torch.equal(slab[:, 4:6], o.float())
+        assert torch.equal(slab[:, 6], d.float())
+        assert torch.equal(obs, twin.observe().float()), t        # post-auto-reset observation
+    assert int(twin.episode_counters()[0].max()) >= 1 or bool(d.any())
+
+
 def test_sac_collector_graph_equals_eager(pd):
     """The HIP-graph collection step stores exactly the transitions of the eager step
     (deterministic actor, twin envs, 40 steps including auto-resets and miss flushes)."""

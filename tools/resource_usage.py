@@ -3,7 +3,7 @@
 (hipcc -Rpass-analysis=kernel-resource-usage on each kstep translation unit of pdenv/build.py).
   python tools/resource_usage.py [out.txt]
 Prints one row per kernel: precision, phase family, rtd, wind, lanes per env, policy, RK4,
-counting; VGPRs, spilled VGPRs, scratch bytes per lane, LDS bytes, waves per SIMD."""
+counting, SAC; VGPRs, spilled VGPRs, scratch bytes per lane, LDS bytes, waves per SIMD."""
 import concurrent.futures as cf
 import os
 import re
@@ -36,18 +36,18 @@ def unit_report(job):
 
 
 def decode(name):
-    m = re.match(r"_ZN2pd6k_stepI([df])Li(\d+)ELi(\d+)ELb(\d)ELi(\d+)ELi(\d+)ELb(\d)ELb(\d)E", name)
+    m = re.match(r"_ZN2pd6k_stepI([df])Li(\d+)ELi(\d+)ELb(\d)ELi(\d+)ELi(\d+)ELb(\d)ELb(\d)ELb(\d)E", name)
     if not m:
         return None
-    r, ph, rt, w, lpe, pol, rk, cnt = m.groups()
-    return (("f64" if r == "d" else "f32"), int(ph), int(rt), int(w), int(lpe), int(pol), int(rk), int(cnt))
+    r, ph, rt, w, lpe, pol, rk, cnt, sac = m.groups()
+    return (("f64" if r == "d" else "f32"), int(ph), int(rt), int(w), int(lpe), int(pol), int(rk), int(cnt), int(sac))
 
 
 def main():
     jobs = [u for u in b.units() if "kstep" in u[0]]
     with cf.ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 4)) as ex:
         allrows = [r for rows in ex.map(unit_report, jobs) for r in rows]
-    out = ["prec phase rtd wind lpe pol rk4 cnt | vgpr spill scratch lds waves"]
+    out = ["prec phase rtd wind lpe pol rk4 cnt sac | vgpr spill scratch lds waves"]
     seen = set()
     for r in sorted(allrows, key=lambda r: decode(r["name"]) or ()):
         k = decode(r["name"])
