@@ -211,7 +211,9 @@ pd_status pd_step_n(pd_env* env, const void* actions, int32_t n_steps, void* obs
  * launch.  The action is sampled in the kernel from the caller's actor heads, as Actor.sample
  * does it (sac_pytorch.py:161-179) in binary32: a = tanh(mean + exp(clamp(log_std, log_std_min,
  * log_std_max)) * eps) * max_action, or tanh(mean) * max_action when eps is NULL (deterministic);
- * mean, log_std, eps [N][A] float32 (eps: standard normals, e.g. torch.randn).  Then the env steps
+ * mean, log_std: float32 rows of head_stride floats (0: A), e.g. both heads of one [N][2A] GEMM
+ * with log_std = mean + A and head_stride 2A; eps [N][A] float32 standard normals (e.g.
+ * torch.randn).  Then the env steps
  * as pd_step (auto-reset per config) and the kernel epilogue writes, all float32 and any of them
  * NULL: action [N][A]; slab [N][2 S + A + 2], the replay buffer's transition row
  * state | action | reward | next_state | done (sac_pytorch.py:27-35; next_state the terminal
@@ -219,8 +221,9 @@ pd_status pd_step_n(pd_env* env, const void* actions, int32_t n_steps, void* obs
  * sac_pytorch_powered_descent.py:170-176); obs32 [N][S], the observation the actor sees next
  * (after any auto-reset).  RL landing-burn handles (PD_PHASE_PURE_THROTTLE / PD_PHASE_LANDING_BURN,
  * rtd RL or NONE, reference integrator) with float32 actions only.  No host synchronisation. */
-pd_status pd_step_sac(pd_env* env, const float* mean, const float* log_std, const float* eps, float log_std_min,
-                      float log_std_max, float max_action, float* action, float* slab, float* obs32, void* stream);
+pd_status pd_step_sac(pd_env* env, const float* mean, const float* log_std, int32_t head_stride, const float* eps,
+                      float log_std_min, float log_std_max, float max_action, float* action, float* slab, float* obs32,
+                      void* stream);
 /* Multi-step rollout with device-resident actions [T][N][A]: the fused launches of pd_step_n
  * (per-step launches for the other phases), rewards accumulated into reward_sum [N] (may be
  * NULL), no per-step outputs.  No host synchronisation. */
@@ -254,6 +257,21 @@ pd_status pd_pso_step(int64_t n_particles, int32_t dim, const double* fitness, d
                       const int32_t* swarm, const double* lower, const double* upper, double w, double c1,
                       double c2, uint64_t seed, uint32_t generation, uint64_t particle_offset,
                       float* position_f32, void* stream);
+/* Per subswarm s < n_swarms, the first particle of minimal fitness among those with swarm[p] ==
+ * s (NumPy argmin order: a NaN first, ties to the lower index; the per-subswarm np.argmin of
+ * particle_swarm_optimisation.py:437-444): min_fitness [n_swarms] and its position min_position
+ * [n_swarms][dim] (from position [dim][n_particles]); +inf and zeros for a subswarm without
+ * particles.  One workgroup per subswarm; no host synchronisation. */
+pd_status pd_pso_swarm_minima(int64_t n_particles, int32_t dim, int32_t n_swarms, const double* fitness,
+                              const int32_t* swarm, const double* position, double* min_fitness,
+                              double* min_position, void* stream);
+/* The subswarm and global bests after a generation (particle_swarm_optimisation.py:442-444,
+ * :474-477), on the device: subswarm s takes (min_fitness[s], min_position[s]) if strictly better;
+ * then the first subswarm holding the smallest best replaces global_best(_fitness) if strictly
+ * better.  swarm_best [n_swarms][dim], global_best [dim], the fitnesses [n_swarms] / [1]. */
+pd_status pd_pso_update_bests(int32_t n_swarms, int32_t dim, const double* min_fitness, const double* min_position,
+                              double* swarm_best_fitness, double* swarm_best, double* global_best_fitness,
+                              double* global_best, void* stream);
 /* Insert the aero neighbourhoods solved on device since the last flush into the handle's
  * tables (one tiny kernel; a no-op when nothing missed).  Call every few steps: a missed
  * neighbourhood is solved exactly on every lookup until it is flushed. */

@@ -136,6 +136,7 @@ template <typename R> struct StepArgs {
     // outputs: the action, the transition row [N][2S + A + 2] and the next observation [N][S]
     const float* sac_mean; const float* sac_logstd; const float* sac_eps;
     float sac_lo, sac_hi, sac_max;
+    uint32_t sac_hs;                 // row stride of mean / log_std in floats (both heads in one [N][2A] array: 2A)
     float* sac_act; float* slab; float* obs32;
 };
 

@@ -1050,10 +1050,10 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
         // action = tanh(x) * max_action; eps NULL: tanh(mean) * max_action (deterministic)
 #pragma unroll
         for (int k = 0; k < A; ++k) if (k < AD) {
-            const float m = ldv(a.sac_mean + k, ui * AD);
+            const float m = ldv(a.sac_mean + k, ui * a.sac_hs);
             float xk = m;
             if (a.sac_eps) {
-                float ls = ldv(a.sac_logstd + k, ui * AD);
+                float ls = ldv(a.sac_logstd + k, ui * a.sac_hs);
                 ls = ls < a.sac_lo ? a.sac_lo : (ls > a.sac_hi ? a.sac_hi : ls);
                 const float sd = expf(ls);
                 xk = m + sd * ldv(a.sac_eps + k, ui * AD);

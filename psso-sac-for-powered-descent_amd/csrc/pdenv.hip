@@ -1077,6 +1077,7 @@ struct SacIO {
     const float *mean, *log_std, *eps;
     float lo, hi, max_action;
     float *action, *slab, *obs32;
+    uint32_t head_stride;
 };
 
 template <typename R>
@@ -1091,6 +1092,7 @@ pd_status step_impl(pd_env* e, const void* actions, void* obs, void* reward, uin
         a.sac_mean = sac->mean; a.sac_logstd = sac->log_std; a.sac_eps = sac->eps;
         a.sac_lo = sac->lo; a.sac_hi = sac->hi; a.sac_max = sac->max_action;
         a.sac_act = sac->action; a.slab = sac->slab; a.obs32 = sac->obs32;
+        a.sac_hs = sac->head_stride;
     }
     dispatch_step<R>(e, a, s);
     PD_HIP(hipGetLastError());
@@ -1287,16 +1289,19 @@ pd_status pd_step(pd_env* e, const void* actions, void* obs, void* reward, uint8
     return step_impl<float>(e, actions, obs, reward, done, truncated, trunc_id, noise, info, nullptr, (hipStream_t)stream);
 }
 
-pd_status pd_step_sac(pd_env* e, const float* mean, const float* log_std, const float* eps, float log_std_min,
-                      float log_std_max, float max_action, float* action, float* slab, float* obs32, void* stream) {
+pd_status pd_step_sac(pd_env* e, const float* mean, const float* log_std, int32_t head_stride, const float* eps,
+                      float log_std_min, float log_std_max, float max_action, float* action, float* slab, float* obs32,
+                      void* stream) {
     if (!e || !mean) return fail(PD_ERR_INVALID, "null env/mean");
+    if (head_stride != 0 && head_stride < e->act_dim) return fail(PD_ERR_INVALID, "pd_step_sac: head_stride < action dim");
     if (eps && !log_std) return fail(PD_ERR_INVALID, "pd_step_sac: eps given without log_std");
     if (e->cfg.action_f64) return fail(PD_ERR_UNSUPPORTED, "pd_step_sac: float32 actions only (action_f64 = 0)");
     if (e->cfg.rtd == PD_RTD_PSO || e->cfg.integrator != PD_INTEG_REFERENCE ||
         (e->cfg.phase != PD_PHASE_PURE_THROTTLE && e->cfg.phase != PD_PHASE_LANDING_BURN))
         return fail(PD_ERR_UNSUPPORTED, "pd_step_sac: the RL landing burns (reference integrator) only");
     PD_HIP(hipSetDevice(e->device));
-    const SacIO io{mean, log_std, eps, log_std_min, log_std_max, max_action, action, slab, obs32};
+    const SacIO io{mean, log_std, eps, log_std_min, log_std_max, max_action, action, slab, obs32,
+                   (uint32_t)(head_stride ? head_stride : e->act_dim)};
     if (e->rsize == 8)
         return step_impl<double>(e, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
                                  (hipStream_t)stream, 1, &io);

@@ -58,6 +58,68 @@ __global__ __launch_bounds__(kPsoBlock) void k_pso_best(int64_t P, const double*
     if (p < P && fit[p] < pbf[p]) pbf[p] = fit[p];
 }
 
+// NumPy's argmin order: a NaN beats everything (the first NaN), else the smaller value, ties to
+// the lower index
+__device__ __forceinline__ bool argmin_better(double a, int64_t ia, double b, int64_t ib) {
+    const bool na = a != a, nb = b != b;
+    if (na || nb) return na && (!nb || ia < ib);
+    return a < b || (a == b && ia < ib);
+}
+
+// Per subswarm s (one workgroup each): the first particle of minimal fitness among those with
+// swarm[p] == s, its fitness and position (:437-441's np.argmin per subswarm); +inf and a zero
+// position for a subswarm with no particle here.
+__global__ __launch_bounds__(kPsoBlock) void k_swarm_minima(int64_t P, int D, const double* __restrict__ fit,
+                                                            const int32_t* __restrict__ swarm,
+                                                            const double* __restrict__ x, double* __restrict__ min_f,
+                                                            double* __restrict__ min_pos) {
+    __shared__ double sf[kPsoBlock];
+    __shared__ int64_t si[kPsoBlock];
+    const int s = blockIdx.x;
+    double bf = __builtin_inf();
+    int64_t bi = -1;
+    for (int64_t p = threadIdx.x; p < P; p += kPsoBlock)
+        if (swarm[p] == s && (bi < 0 || argmin_better(fit[p], p, bf, bi))) { bf = fit[p]; bi = p; }
+    sf[threadIdx.x] = bf; si[threadIdx.x] = bi;
+    __syncthreads();
+    for (int o = kPsoBlock / 2; o > 0; o >>= 1) {
+        if (threadIdx.x < o) {
+            const double f2 = sf[threadIdx.x + o];
+            const int64_t i2 = si[threadIdx.x + o];
+            if (i2 >= 0 && (si[threadIdx.x] < 0 || argmin_better(f2, i2, sf[threadIdx.x], si[threadIdx.x]))) {
+                sf[threadIdx.x] = f2; si[threadIdx.x] = i2;
+            }
+        }
+        __syncthreads();
+    }
+    const int64_t i = si[0];
+    if (threadIdx.x == 0) min_f[s] = i >= 0 ? sf[0] : __builtin_inf();
+    for (int d = threadIdx.x; d < D; d += kPsoBlock) min_pos[(int64_t)s * D + d] = i >= 0 ? x[(int64_t)d * P + i] : 0.0;
+}
+
+// :442-444 and :474-477 (one workgroup): subswarm s takes a strictly better minimum; then the
+// first subswarm holding the smallest best replaces the global best if strictly better.
+__global__ __launch_bounds__(kPsoBlock) void k_update_bests(int S, int D, const double* __restrict__ min_f,
+                                                            const double* __restrict__ min_pos, double* __restrict__ sbf,
+                                                            double* __restrict__ sb, double* __restrict__ gbf,
+                                                            double* __restrict__ gb) {
+    for (int s = 0; s < S; ++s) {
+        const bool better = min_f[s] < sbf[s];
+        if (better)
+            for (int d = threadIdx.x; d < D; d += kPsoBlock) sb[(int64_t)s * D + d] = min_pos[(int64_t)s * D + d];
+        __syncthreads();
+        if (better && threadIdx.x == 0) sbf[s] = min_f[s];
+        __syncthreads();
+    }
+    int j = 0;
+    for (int s = 1; s < S; ++s) if (sbf[s] < sbf[j]) j = s;
+    if (sbf[j] < *gbf) {
+        for (int d = threadIdx.x; d < D; d += kPsoBlock) gb[d] = sb[(int64_t)j * D + d];
+        __syncthreads();
+        if (threadIdx.x == 0) *gbf = sbf[j];
+    }
+}
+
 }  // namespace
 
 namespace pd {
@@ -81,6 +143,30 @@ pd_status pd_pso_step(int64_t n_particles, int32_t dim, const double* fitness, d
     hipLaunchKernelGGL(k_pso_best, dim3((unsigned)((n_particles + kPsoBlock - 1) / kPsoBlock)), dim3(kPsoBlock), 0, s,
                        n_particles, fitness, best_fitness);
     if (hipGetLastError() != hipSuccess) return set_error(PD_ERR_HIP, "pd_pso_step: launch failed");
+    return PD_OK;
+}
+
+pd_status pd_pso_swarm_minima(int64_t n_particles, int32_t dim, int32_t n_swarms, const double* fitness,
+                              const int32_t* swarm, const double* position, double* min_fitness, double* min_position,
+                              void* stream) {
+    if (n_particles < 0 || dim <= 0 || n_swarms <= 0 || n_swarms > 65535 || !min_fitness || !min_position ||
+        (n_particles > 0 && (!fitness || !swarm || !position)))
+        return set_error(PD_ERR_INVALID, "pd_pso_swarm_minima: bad arguments");
+    hipLaunchKernelGGL(k_swarm_minima, dim3((unsigned)n_swarms), dim3(kPsoBlock), 0, (hipStream_t)stream, n_particles,
+                       dim, fitness, swarm, position, min_fitness, min_position);
+    if (hipGetLastError() != hipSuccess) return set_error(PD_ERR_HIP, "pd_pso_swarm_minima: launch failed");
+    return PD_OK;
+}
+
+pd_status pd_pso_update_bests(int32_t n_swarms, int32_t dim, const double* min_fitness, const double* min_position,
+                              double* swarm_best_fitness, double* swarm_best, double* global_best_fitness,
+                              double* global_best, void* stream) {
+    if (n_swarms <= 0 || dim <= 0 || !min_fitness || !min_position || !swarm_best_fitness || !swarm_best ||
+        !global_best_fitness || !global_best)
+        return set_error(PD_ERR_INVALID, "pd_pso_update_bests: bad arguments");
+    hipLaunchKernelGGL(k_update_bests, dim3(1), dim3(kPsoBlock), 0, (hipStream_t)stream, n_swarms, dim, min_fitness,
+                       min_position, swarm_best_fitness, swarm_best, global_best_fitness, global_best);
+    if (hipGetLastError() != hipSuccess) return set_error(PD_ERR_HIP, "pd_pso_update_bests: launch failed");
     return PD_OK;
 }
 

@@ -86,7 +86,7 @@ EXPORTS = ["pd_abi_version", "pd_sizeof_params", "pd_sizeof_config", "pd_last_er
            "pd_set_gload_window", "pd_get_gload_window", "pd_set_wind_sigmas", "pd_get_wind_state",
            "pd_set_wind_state", "pd_get_counters", "pd_set_counters", "pd_checkpoint_size", "pd_checkpoint_save",
            "pd_checkpoint_load", "pd_counters", "pd_stats", "pd_count_work", "pd_atmosphere", "pd_obs_dim",
-           "pd_action_dim", "pd_step_sac"]
+           "pd_action_dim", "pd_step_sac", "pd_pso_swarm_minima", "pd_pso_update_bests"]
 ABI_VERSION = 5
 
 _lib = None
@@ -116,11 +116,13 @@ def load(path=None):
     L.pd_step.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
     L.pd_step_n.argtypes = [vp, vp, I32, vp, vp, vp, vp, vp, vp]
     F32 = C.c_float
-    L.pd_step_sac.argtypes = [vp, vp, vp, vp, F32, F32, F32, vp, vp, vp, vp]
+    L.pd_step_sac.argtypes = [vp, vp, vp, I32, vp, F32, F32, F32, vp, vp, vp, vp]
     L.pd_rollout.argtypes = [vp, vp, I32, vp, vp]
     L.pd_rollout_policy.argtypes = [vp, vp, I32, I32, vp, vp, I32, vp]
     L.pd_pso_step.argtypes = [I64, I32, vp, vp, vp, vp, vp, vp, vp, vp, vp, C.c_double, C.c_double, C.c_double,
                               U64, C.c_uint32, U64, vp, vp]
+    L.pd_pso_swarm_minima.argtypes = [I64, I32, I32, vp, vp, vp, vp, vp, vp]
+    L.pd_pso_update_bests.argtypes = [I32, I32, vp, vp, vp, vp, vp, vp, vp]
     L.pd_observe.argtypes = [vp, vp, vp]
     L.pd_flush_misses.argtypes = [vp, vp]
     L.pd_get_state.argtypes = [vp, vp, vp]
@@ -143,7 +145,8 @@ def load(path=None):
     L.pd_checkpoint_load.argtypes = [vp, vp, vp]
     L.pd_obs_dim.argtypes = [vp]; L.pd_obs_dim.restype = C.c_int
     L.pd_action_dim.argtypes = [vp]; L.pd_action_dim.restype = C.c_int
-    for name in ("pd_create", "pd_destroy", "pd_reset", "pd_step", "pd_step_n", "pd_step_sac", "pd_rollout", "pd_rollout_policy", "pd_pso_step", "pd_flush_misses", "pd_observe",
+    for name in ("pd_create", "pd_destroy", "pd_reset", "pd_step", "pd_step_n", "pd_step_sac", "pd_rollout", "pd_rollout_policy", "pd_pso_step",
+                 "pd_pso_swarm_minima", "pd_pso_update_bests", "pd_flush_misses", "pd_observe",
                  "pd_get_state", "pd_set_state", "pd_get_actuators", "pd_set_actuators",
                  "pd_set_wind_sigmas", "pd_set_gload_window", "pd_counters", "pd_stats", "pd_count_work",
                  "pd_get_gload_window",

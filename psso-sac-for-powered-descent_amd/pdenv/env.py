@@ -158,14 +158,23 @@ class PoweredDescentEnv:
                                  _stream(self.device)))
 
     def step_sac(self, mean, log_std, eps, log_std_min=-20.0, log_std_max=2.0, max_action=1.0, action=None,
-                 slab=None, obs32=None):
+                 slab=None, obs32=None, heads=None):
         """One SAC collection step in one launch (pd_step_sac): the action sampled in the kernel
-        from the actor's heads (mean, log_std, eps: contiguous float32 [N, A] device tensors; eps
-        None = deterministic), the env step, and float32 outputs written by the kernel epilogue
-        into the given tensors: action [N, A], slab [N, 2S + A + 2] (state | action | reward |
-        next_state | done) and obs32 [N, S] (the next observation, after any auto-reset).
+        from the actor's heads (mean, log_std, eps: contiguous float32 [N, A] device tensors; or
+        heads [N, 2A] = mean | log_std of one GEMM, with mean = log_std = None; eps None =
+        deterministic), the env step, and float32 outputs written by the kernel epilogue into the
+        given tensors: action [N, A], slab [N, 2S + A + 2] (state | action | reward | next_state |
+        done) and obs32 [N, S] (the next observation, after any auto-reset).
         No copies, allocations or syncs."""
-        L.check(self.lib.pd_step_sac(self.h, _ptr(mean), _ptr(log_std), _ptr(eps), float(log_std_min),
+        hs = 0
+        if heads is not None:
+            A = self.action_dim
+            mean = C.c_void_p(heads.data_ptr())
+            log_std = C.c_void_p(heads.data_ptr() + 4 * A)
+            hs = 2 * A
+        else:
+            mean, log_std = _ptr(mean), _ptr(log_std)
+        L.check(self.lib.pd_step_sac(self.h, mean, log_std, hs, _ptr(eps), float(log_std_min),
                                      float(log_std_max), float(max_action), _ptr(action), _ptr(slab), _ptr(obs32),
                                      _stream(self.device)))
         self._steps += 1

@@ -180,17 +180,13 @@ class ParticleSubswarmOptimisationGPU:
 
     def _swarm_minima(self, fit):
         """Per subswarm: (min fitness, its position) over all ranks, first particle on ties -- a
-        segmented argmin on the device ([S, P] masked fitness, torch.argmin takes the first
-        minimum), no host synchronisation.  A subswarm with no particle here reports +inf."""
-        if self.P > 0:
-            m = self.swarm.long()[None, :] == self._cols[:, None]                       # [S, P]
-            fs = torch.where(m, fit[None, :], torch.full_like(fit, math.inf)[None, :])
-            i = torch.argmin(fs, dim=1)                                                 # [S]
-            f = fs.gather(1, i[:, None]).squeeze(1)
-            pos = self.x.index_select(1, i).t().contiguous()                            # [S, D]
-        else:
-            f = torch.full((self.S,), math.inf, dtype=torch.float64, device=self.device)
-            pos = torch.zeros(self.S, self.D, dtype=torch.float64, device=self.device)
+        segmented argmin on the device (pd_pso_swarm_minima: one workgroup per subswarm), no host
+        synchronisation.  A subswarm with no particle here reports +inf."""
+        f = torch.empty(self.S, dtype=torch.float64, device=self.device)
+        pos = torch.empty(self.S, self.D, dtype=torch.float64, device=self.device)
+        L.check(self.lib.pd_pso_swarm_minima(self.P, self.D, self.S, _ptr(fit) if self.P else None,
+                                             _ptr(self.swarm) if self.P else None, _ptr(self.x) if self.P else None,
+                                             _ptr(f), _ptr(pos), _stream(self.device)))
         if self.dist:
             fa = [torch.empty_like(f) for _ in range(self.world)]
             pa = [torch.empty_like(pos) for _ in range(self.world)]
@@ -207,16 +203,11 @@ class ParticleSubswarmOptimisationGPU:
         fit, _ = self.evaluate(self.x32)
         self.last_fitness = fit
         f, pos = self._swarm_minima(fit)
-        # :442-444 per subswarm: a strictly better minimum replaces the subswarm best
-        better = f < self.sbf_t
-        self.sbf_t = torch.where(better, f, self.sbf_t)
-        self.sb = torch.where(better[:, None], pos, self.sb)
-        # :474-477 subswarms in order, strictly better replaces: the first subswarm holding the
-        # minimum, if it beats the global best
-        j = torch.argmin(self.sbf_t)
-        upd = self.sbf_t[j] < self.gbf_t
-        self.gbf_t = torch.where(upd, self.sbf_t[j], self.gbf_t)
-        self.gb_t = torch.where(upd, self.sb[j], self.gb_t)
+        # :442-444 per subswarm: a strictly better minimum replaces the subswarm best; :474-477
+        # subswarms in order, strictly better replaces: the first subswarm holding the minimum,
+        # if it beats the global best (pd_pso_update_bests, one workgroup)
+        L.check(self.lib.pd_pso_update_bests(self.S, self.D, _ptr(f), _ptr(pos), _ptr(self.sbf_t), _ptr(self.sb),
+                                             _ptr(self.gbf_t), _ptr(self.gb_t), _stream(self.device)))
         self.w = self.p["w_start"] - (self.p["w_start"] - self.p["w_end"]) * gen / self.p["generations"]
         if self.P > 0:
             L.check(self.lib.pd_pso_step(self.P, self.D, _ptr(fit), _ptr(self.pbf), _ptr(self.x), _ptr(self.v),

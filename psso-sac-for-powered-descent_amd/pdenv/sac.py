@@ -10,6 +10,7 @@ learner itself (critic/actor updates) is the caller's, as in the reference.
 """
 import torch
 import torch.nn as nn
+import torch.nn.functional as F
 
 
 class Actor(nn.Module):
@@ -168,9 +169,11 @@ class SACCollector:
     learner-rank buffer append.  `obs` always holds the observation the actor sees next (the
     post-auto-reset observation of envs whose episode ended).
 
-    fused=True (default): the actor's MLP and heads in PyTorch, eps by torch.randn, then ONE
-    kernel (pd_step_sac) samples the action from the heads, steps the envs and writes the
-    transition slab and the next float32 observation -- no slab cat, no casts, no observe.
+    fused=True (default): the actor's MLP in PyTorch with both heads as ONE GEMM (a [2A, H]
+    copy of the mean and log_std weights, refreshed whenever the actor's parameters change),
+    eps by torch.randn, then ONE kernel (pd_step_sac) samples the action from the heads, steps
+    the envs and writes the transition slab and the next float32 observation -- no slab cat, no
+    casts, no observe.
     fused=False: Actor.sample, pd_step, transition_slab, pd_observe (the unfused reference path).
     use_graph=True captures the step into one HIP graph (replaying removes the launch gaps).
     The gather and the buffer append run eagerly after each replay; the aero-miss flush runs
@@ -190,18 +193,35 @@ class SACCollector:
         S, A = env.obs_dim, env.action_dim
         self._slab_buf = torch.empty(env.n, 2 * S + A + 2, dtype=torch.float32, device=self.obs.device)
         self.action = torch.empty(env.n, A, dtype=torch.float32, device=self.obs.device)
+        H = actor.mean.in_features
+        self._head_w = torch.empty(2 * A, H, dtype=torch.float32, device=self.obs.device)
+        self._head_b = torch.empty(2 * A, dtype=torch.float32, device=self.obs.device)
+        self._head_ver = None
+        self._refresh_heads()
+
+    def _refresh_heads(self):
+        """The fused head weights follow the actor: re-copied (in place, so a captured graph sees
+        them) whenever a head parameter was modified (its version counter moved)."""
+        ps = (self.actor.mean.weight, self.actor.mean.bias, self.actor.log_std.weight, self.actor.log_std.bias)
+        ver = tuple((id(p), p._version) for p in ps)
+        if ver != self._head_ver:
+            with torch.no_grad():
+                self._head_w.copy_(torch.cat([ps[0], ps[2]]))
+                self._head_b.copy_(torch.cat([ps[1], ps[3]]))
+            self._head_ver = ver
 
     def _body(self):
         """actor -> env step -> slab and next obs into self.obs; returns the slab (no syncs)."""
         gen = None if self.use_graph else self.generator
         if self.fused:
             f = self.actor.shared_net(self.obs)
-            mean, log_std = self.actor.mean(f), self.actor.log_std(f)     # (the kernel clamps log_std)
+            heads = F.linear(f, self._head_w, self._head_b)             # mean | log_std (the kernel clamps)
             eps = None
             if not self.deterministic:
-                eps = torch.randn(mean.shape, device=mean.device, dtype=mean.dtype, generator=gen)
-            self.env.step_sac(mean, log_std, eps, self.actor.log_std_min, self.actor.log_std_max,
-                              self.actor.max_action, action=self.action, slab=self._slab_buf, obs32=self.obs)
+                eps = torch.randn(self.action.shape, device=f.device, dtype=f.dtype, generator=gen)
+            self.env.step_sac(None, None, eps, self.actor.log_std_min, self.actor.log_std_max,
+                              self.actor.max_action, action=self.action, slab=self._slab_buf, obs32=self.obs,
+                              heads=heads)
             return self._slab_buf
         act, _ = self.actor.sample(self.obs, deterministic=self.deterministic, generator=gen, with_log_prob=False)
         act = act.float().contiguous()
@@ -221,6 +241,8 @@ class SACCollector:
 
     @torch.no_grad()
     def step(self):
+        if self.fused:
+            self._refresh_heads()
         if not self.use_graph:
             return self._finish(self._body())
         if self.graph is None:

@@ -448,6 +448,51 @@ def test_pso_step_matches_numpy(pd):
     assert np.array_equal(x32.cpu().numpy(), xn.astype(np.float32))
 
 
+def test_pso_swarm_minima_and_bests_vs_numpy(pd):
+    """pd_pso_swarm_minima (NumPy argmin order per subswarm: a NaN first, ties to the lower
+    index, +inf for an empty subswarm) and pd_pso_update_bests (strictly better replaces; the
+    first subswarm holding the minimum feeds the global best) against NumPy."""
+    import torch
+    from pdenv import _lib as L
+    from pdenv.env import _ptr
+    lib = L.load()
+    rng = np.random.default_rng(12)
+    for trial in range(6):
+        P, D, S = int(rng.integers(1, 5000)), int(rng.integers(1, 400)), int(rng.integers(1, 6))
+        fit = np.round(rng.normal(size=P), 1)                  # many ties
+        if trial % 2:
+            fit[rng.integers(0, P, 3)] = np.nan
+        sw = rng.integers(0, S, P).astype(np.int32)
+        if trial == 3:
+            sw[sw == S - 1] = 0                                 # an empty subswarm
+        x = rng.normal(size=(D, P))
+        T = {k: torch.tensor(v, device="cuda") for k, v in dict(fit=fit, sw=sw, x=x).items()}
+        mf = torch.empty(S, dtype=torch.float64, device="cuda")
+        mp = torch.empty(S, D, dtype=torch.float64, device="cuda")
+        L.check(lib.pd_pso_swarm_minima(P, D, S, _ptr(T["fit"]), _ptr(T["sw"]), _ptr(T["x"]), _ptr(mf), _ptr(mp), None))
+        sbf = torch.tensor(rng.normal(size=S), device="cuda"); sb = torch.tensor(rng.normal(size=(S, D)), device="cuda")
+        gbf = torch.tensor(0.5, dtype=torch.float64, device="cuda"); gb = torch.zeros(D, dtype=torch.float64, device="cuda")
+        sbf0, sb0 = sbf.cpu().numpy().copy(), sb.cpu().numpy().copy()
+        L.check(lib.pd_pso_update_bests(S, D, _ptr(mf), _ptr(mp), _ptr(sbf), _ptr(sb), _ptr(gbf), _ptr(gb), None))
+        torch.cuda.synchronize()
+        ef, ep = np.full(S, np.inf), np.zeros((S, D))
+        for s in range(S):
+            idx = np.flatnonzero(sw == s)
+            if len(idx):
+                i = idx[np.argmin(fit[idx])]
+                ef[s], ep[s] = fit[i], x[:, i]
+        assert np.array_equal(mf.cpu().numpy(), ef, equal_nan=True) and np.array_equal(mp.cpu().numpy(), ep)
+        for s in range(S):
+            if ef[s] < sbf0[s]:
+                sbf0[s], sb0[s] = ef[s], ep[s]
+        assert np.array_equal(sbf.cpu().numpy(), sbf0) and np.array_equal(sb.cpu().numpy(), sb0)
+        g, gv = 0.5, np.zeros(D)
+        for s in range(S):
+            if sbf0[s] < g:
+                g, gv = sbf0[s], sb0[s]
+        assert float(gbf) == g and np.array_equal(gb.cpu().numpy(), gv)
+
+
 def test_pso_driver_generations_vs_numpy(pd):
     """Three generations of the device subswarm PSO (evaluation, subswarm/global bests, inertia
     schedule, update, share_information and migrate_particles at generation 2) against a NumPy
@@ -525,7 +570,11 @@ def test_sac_step_fused_sampling_and_slab(pd):
         eps = torch.randn(mean.shape, device="cuda", generator=g)
         ref = torch.tanh(mean + torch.clamp(ls, -20.0, 2.0).exp() * eps) * 1.0
         seen = obs.clone()
-        env.step_sac(mean, ls, eps, -20.0, 2.0, 1.0, action=act, slab=slab, obs32=obs)
+        if t % 2:
+            env.step_sac(mean, ls, eps, -20.0, 2.0, 1.0, action=act, slab=slab, obs32=obs)
+        else:                               # both heads in one [N, 2] array (head_stride 2)
+            env.step_sac(None, None, eps, -20.0, 2.0, 1.0, action=act, slab=slab, obs32=obs,
+                         heads=torch.cat([mean, ls], dim=1).contiguous())
         assert (act - ref).abs().max() <= 2e-7, (t, float((act - ref).abs().max()))
         o, r, d, _, _ = twin.step(act)
         assert torch.equal(slab[:, :2], seen) and torch.equal(slab[:, 2:3], act)
