@@ -1026,6 +1026,10 @@ template <typename R> pd_status create_impl(const pd_params* p, const pd_config*
     PD_HIP(hipMemset(e->pend.solve_lock, 0, (size_t)kSolveSlots * 4));
     unsigned long long stats0[kStats] = {0, 0, (unsigned long long)tcd.entries, (unsigned long long)tcl.entries};
     PD_HIP(hipMemcpy(e->pend.stats, stats0, sizeof(stats0), hipMemcpyHostToDevice));
+    // the policy rollouts' pinned live-count words and events, made here: a first pinned
+    // allocation inside a timed rollout cost ~170 ms (the PSO driver's share handle)
+    PD_HIP(hipHostMalloc((void**)&e->host_cnt, 2 * sizeof(uint32_t), hipHostMallocDefault));
+    for (hipEvent_t& ev : e->cnt_ev) PD_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
     StepArgs<R> a = make_args<R>(e);
     unsigned grid = (unsigned)((N + kBlock - 1) / kBlock);
     hipLaunchKernelGGL(k_reset<R>, dim3(grid), dim3(kBlock), 0, 0, a, (const uint8_t*)nullptr);
@@ -1125,10 +1129,7 @@ pd_status rollout_policy_impl(pd_env* e, const float* w, int32_t max_steps, void
     // behind: at a check the count is copied to pinned memory under an event, and the host
     // waits for the PREVIOUS check's event, with check_every launches still queued behind it
     // (no bubble); at most 2 * check_every nearly empty launches run after the last episode.
-    if (check_every > 0 && !e->host_cnt) {
-        PD_HIP(hipHostMalloc((void**)&e->host_cnt, 2 * sizeof(uint32_t), hipHostMallocDefault));
-        for (hipEvent_t& ev : e->cnt_ev) PD_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-    }
+    if (check_every > 0 && !e->host_cnt) return fail(PD_ERR_HIP, "policy rollout: no pinned live-count words");
     // The list pays off once the grid no longer fits the chip in one round (a launch then costs
     // the rounds its waves need); below that the launch time is one wave's, and reading the
     // state and actor weights through the list (gathers) only costs.  PDENV_COMPACT=0/1 forces.

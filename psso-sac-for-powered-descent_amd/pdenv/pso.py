@@ -144,6 +144,24 @@ class ParticleSubswarmOptimisationGPU:
         # here (creating a handle inside a generation costs tens of ms), candidates padded to it
         self._aux = {self.S - 1: PoweredDescentEnv(self.S - 1, self.flight_phase, **self.env_kw)} if self.S > 1 else {}
         self.last_fitness = None
+        self._warm_share_path()
+
+    def _warm_share_path(self):
+        """share_information's tensor operations once on scratch copies (no rng draws, no state
+        change): the first launch of a kernel in a process loads its code object, which cost a
+        timed generation 50-180 ms when the first non-empty share came."""
+        if self.S < 2:
+            return
+        sb, sbf = self.sb.clone(), self.sbf_t.clone()
+        moved = [0]
+        sb[0] = (1 - 0.3) * sb[0] + 0.3 * sb[self.S - 1]
+        pad = moved + [moved[0]] * (self.S - 1 - len(moved))
+        cand = sb[pad].t().float().contiguous()
+        fit = torch.zeros(cand.shape[1], dtype=torch.float64, device=self.device)[:len(moved)]
+        mv = torch.tensor(moved, device=self.device)
+        old = sbf[mv]
+        sbf[mv] = torch.where(fit < old, fit, old)
+        torch.cuda.synchronize(self.device)
 
     def _env_for(self, n):
         if self.env is not None and self.env.n == n:
