@@ -101,7 +101,6 @@ struct Pending {
     double* pay;                 // [cap][kPay]
     unsigned long long* stats;   // [kStats]
     double* solve_ws;            // [kSolveSlots][kScratch] exact-solve scratch (global memory)
-    unsigned long long* solve_tag;   // [kSolveSlots] (table << 63 | key) whose payload the slot holds
     int* solve_lock;             // [kSolveSlots]
 };
 

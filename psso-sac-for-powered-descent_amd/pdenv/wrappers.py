@@ -101,13 +101,23 @@ def info_dict(flight_phase, ex, state, actions, params, i=0):
 _ATM = {}
 
 
-def maximum_velocity(y, vy):
+def _atm_env(device):
+    """One 1-env handle per device for the scalar ISA helper, closed at interpreter exit."""
+    if device not in _ATM:
+        if not _ATM:
+            import atexit
+            atexit.register(lambda: [e.close() for e in _ATM.values()])
+        _ATM[device] = PoweredDescentEnv(1, "landing_burn_pure_throttle", mode="rl", device=device)
+    return _ATM[device]
+
+
+def maximum_velocity(y, vy, device=None):
     """env_wrapped_rl_pytorch.py:60-66: sqrt(2 p / rho) of the ISA at altitude y (the handle's
     device atmosphere, pd_atmosphere), or vy above the ISA's top.  The SAC driver imports it as
-    maximum_velocity_lambda (sac_pytorch_powered_descent.py:11, used at :370)."""
-    if "env" not in _ATM:
-        _ATM["env"] = PoweredDescentEnv(1, "landing_burn_pure_throttle", mode="rl")
-    rho, p, a = _ATM["env"].atmosphere(torch.tensor([float(y)], dtype=torch.float64))
+    maximum_velocity_lambda (sac_pytorch_powered_descent.py:11, used at :370).  Evaluated on
+    `device` (default: the current torch device, so each rank of a multi-GPU job uses its own)."""
+    dev = torch.cuda.current_device() if device is None else int(device)
+    rho, p, a = _atm_env(dev).atmosphere(torch.tensor([float(y)], dtype=torch.float64))
     rho, p, a = float(rho[0]), float(p[0]), float(a[0])
     if a != 0:
         return math.sqrt(2 * p / rho)
