@@ -138,6 +138,28 @@ __device__ __forceinline__ R chunk_sum(const R pp[10], const uint32_t w[3], cons
     return s0 + s1;
 }
 
+// One parity half of chunk_sum: h = 0 its even terms (each slot's first point), h = 1 its odd
+// terms (second points; the general slot's from its own entry), accumulated in chunk_sum's order
+// with the same operations, so that chunk_sum(...) == chunk_half(.., 0) + chunk_half(.., 1) bit
+// for bit (the balanced sums' last round deals half-chunks when it is at most half full).
+template <typename R, typename R2>
+__device__ __forceinline__ R chunk_half(const R pp[10], const uint32_t w[3], const R2* pt, R M, R a, int h) {
+    R s = R(0);
+#pragma unroll
+    for (int u = 0; u < 5; ++u) {
+        const uint32_t hw = w[u >> 1] >> (16 * (u & 1));
+        const uint32_t hs = (h && u == 4) ? (w[2] >> 16) : hw;          // the general slot's second point
+        const R2 v = pt[hs & 0xffu];
+        const R m = (h && u < 4) ? v.y : v.x;
+        const R da = a - (R)((hs >> 8) & 0xffu);
+        const R dm = M - m;
+        const R d2 = fma(dm, dm, da * da);
+        if constexpr (sizeof(R) == 8) s = fma(d2 * pp[2 * u + h], log4_finish(log_start(d2)), s);
+        else s = fma(d2 * pp[2 * u + h], eval_log4<R>(d2 > R(1e-30) ? d2 : R(1e-30)), s);
+    }
+    return s;
+}
+
 // The payload's degree-1 polynomial added to the scaled kernel sum (the same order everywhere);
 // f: the payload's fields [kPayPoly, kPayPoly + 7) (poly coefficients, shifts, scales)
 template <typename R>
@@ -590,7 +612,13 @@ __device__ __forceinline__ R rbf_balanced(DP<R>& P, BalLds<R>& B, const R* tab, 
     if (mine) { B.qm[rank] = M; B.qa[rank] = aq; B.qp[rank] = (unsigned long long)(uint64_t)own | (unsigned long long)table; }
     wave_lds_sync();
     const int total = kChunks * n;
-    const int K = (total + NQ - 1) / NQ;
+    // full rounds of 64 chunks; a remainder of at most 32 chunks goes as 64 half-chunks in one
+    // half-cost round (chunk_half, the same bits), a larger one as one more full round
+    const int Kfull = total / NQ, rem = total - Kfull * NQ;
+    const bool halfr = rem > 0 && rem <= NQ / 2;
+    const int K = Kfull + (rem > NQ / 2 ? 1 : 0);
+    // this lane's chunk in round r (round K: the half round's chunk, whose lane pair splits it)
+    auto gidx = [&](int r) { return r < K ? r * NQ + lane : Kfull * NQ + (lane >> 1); };
     // chunk g's coefficients / index words / point table / query
     struct Buf { R pp[10]; uint32_t w[3]; const R2* pt; R M, a; };
     auto fetch = [&](int g, Buf& b) {
@@ -611,7 +639,7 @@ __device__ __forceinline__ R rbf_balanced(DP<R>& P, BalLds<R>& B, const R* tab, 
         if (g < total) B.part[g] = cs;
     };
     Buf b0, b1;
-    fetch(lane, b0);
+    fetch(gidx(0), b0);
     R pf[7];   // the own query's polynomial fields, requested with the first round
 #pragma unroll
     for (int u = 0; u < 7; ++u) pf[u] = own[kPayPoly + u];
@@ -620,12 +648,29 @@ __device__ __forceinline__ R rbf_balanced(DP<R>& P, BalLds<R>& B, const R* tab, 
 #pragma unroll 1
     for (int k = 0; k < K; k += 2) {
         const int g = k * NQ + lane;
-        fetch(k + 1 < K ? g + NQ : g, b1);
+        fetch(gidx(k + 1), b1);
         run(g, b0);
         if (k + 1 < K) {
-            fetch(k + 2 < K ? g + 2 * NQ : g + NQ, b0);
+            fetch(gidx(k + 2), b0);
             run(g + NQ, b1);
         }
+    }
+    if (halfr) {
+        // the half round (its data fetched by the last full round, or up front): lane 2j + h
+        // sums half h of chunk Kfull * 64 + j; the query abscissae B.qm are no longer read, so
+        // they hold the halves until the pairs are added
+        const bool odd = K & 1;     // (element-wise selects: a reference to b0 / b1 would put both in scratch)
+        R hp[10];
+        uint32_t hwd[3];
+#pragma unroll
+        for (int u = 0; u < 10; ++u) hp[u] = odd ? b1.pp[u] : b0.pp[u];
+#pragma unroll
+        for (int u = 0; u < 3; ++u) hwd[u] = odd ? b1.w[u] : b0.w[u];
+        const R hsum = chunk_half<R, R2>(hp, hwd, odd ? b1.pt : b0.pt, odd ? b1.M : b0.M, odd ? b1.a : b0.a, lane & 1);
+        wave_lds_sync();
+        B.qm[lane] = hsum;
+        wave_lds_sync();
+        if (lane < rem) B.part[Kfull * NQ + lane] = B.qm[2 * lane] + B.qm[2 * lane + 1];
     }
     wave_lds_sync();
     R val = R(0);
