@@ -361,8 +361,8 @@ def c3_summary(args, r, world, precision, pmc=None):
         traffic = pmc.get(f"{precision}_bytes_per_launch")
         traffic = traffic * scale if traffic is not None else None
         mix = pmc.get("f64_valu_mix_per_launch") if precision == "f64" else None
-        if mix:
-            mix = {k: v * scale for k, v in mix.items()}
+        if mix:   # (instruction counts scale with the steps per launch; the wave count does not)
+            mix = {k: (v * scale if k != "SQ_WAVES" else v) for k, v in mix.items()}
     out = {
         "value": whole_job_rate(n, world, K, r["wall"]),
         "ms_per_step": r["wall"] / K * 1e3,

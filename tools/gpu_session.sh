@@ -21,6 +21,7 @@ for s in $STAGES; do
     testsall) stage gpu_tests 900 python -u -m pytest tests/ -m gpu -q --timeout 120 --timeout-method thread ;;
     smoke) stage smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) stage bench 600 python bench.py ;;
+    benchdrv) stage benchdrv 600 python bench.py --steps 20 --warmup 5 ;;
     bench32) stage bench32 600 python bench.py --precision f32 ;;
     prof) stage prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 192 --warmup 32 --cpu-baseline 0 --secondary 0 --others 0 --descent 1 ;;
     profc4) stage profc4 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/profc4 -o run -- python3 bench.py --workload c4 --steps 16 --warmup 2 --cpu-baseline 0 ;;
