@@ -355,8 +355,8 @@ __device__ __forceinline__ void solve_wave(DP<R>& P, int table, unsigned long lo
 // Each distinct (table, key) missed by the wave is solved cooperatively into the workgroup's
 // global scratch slot (under the slot's lock), evaluated by the lanes that need it, and queued
 // for insertion into the device table (pd_flush_misses).  Called by the converged wave.
-template <typename R>
-__device__ __forceinline__ R rbf_miss_wave(const StepArgs<R>& a, DP<R>& P, int table, const R* spt,
+template <typename R, typename AT>
+__device__ __forceinline__ R rbf_miss_wave(const AT& a, DP<R>& P, int table, const R* spt,
                                            unsigned long long key, R M, R aq,
                                            int part, int nparts, bool need) {
     R val = R(0);
@@ -410,8 +410,8 @@ struct NoPre { __device__ void operator()() const {} };
 
 // pre(): the caller's work that does not depend on the tables, run while the grid loads are in
 // flight
-template <typename R, typename Pre = NoPre>
-__device__ __forceinline__ int rbf_lookup(const StepArgs<R>& a, DP<R>& P, int table, const TabView<R>& t,
+template <typename R, typename Pre = NoPre, typename AT>
+__device__ __forceinline__ int rbf_lookup(const AT& a, DP<R>& P, int table, const TabView<R>& t,
                                           const LineLds<R>& ln, RbfCache<R>& cache, R M, R aq,
                                           TayRef* tay = nullptr, unsigned long long* st = nullptr,
                                           Pre&& pre = Pre()) {
@@ -536,8 +536,8 @@ __device__ __forceinline__ int rbf_lookup(const StepArgs<R>& a, DP<R>& P, int ta
 
 // This lane's share of the RBF value of `table` at (M, aq): lookup, evaluation, and the
 // wave-cooperative solve of missed neighbourhoods.
-template <typename R>
-__device__ __forceinline__ R rbf(const StepArgs<R>& a, DP<R>& P, int table, const TabView<R>& t, const LineLds<R>& ln,
+template <typename R, typename AT>
+__device__ __forceinline__ R rbf(const AT& a, DP<R>& P, int table, const TabView<R>& t, const LineLds<R>& ln,
                                  RbfCache<R>& cache, R M, R aq, int part, int nparts) {
     const int slot = rbf_lookup<R>(a, P, table, t, ln, cache, M, aq);
     const unsigned long long key = cache.key;
@@ -690,8 +690,8 @@ __device__ __forceinline__ R rbf_balanced(DP<R>& P, BalLds<R>& B, const R* tab, 
 // the other table hits by the balanced payload sums, misses by the cooperative solve (whose
 // evaluation, rbf_eval, has the balanced sums' bits).  Lanes with act = false (past the batch,
 // frozen policy envs) only take part.
-template <typename R, typename Pre>
-__device__ __forceinline__ R rbf2(const StepArgs<R>& a, DP<R>& P, int table, const TabView<R>& t, const LineLds<R>& ln,
+template <typename R, typename Pre, typename AT>
+__device__ __forceinline__ R rbf2(const AT& a, DP<R>& P, int table, const TabView<R>& t, const LineLds<R>& ln,
                                   RbfCache<R>& cache, R M, R aq, bool act, BalLds<R>& B, const R* tab,
                                   WaveCount& wc, Pre&& pre, unsigned long long* stamp = nullptr) {
 #ifdef PD_STAMP
@@ -892,7 +892,9 @@ template <typename R, int PHASE, int RTD, bool WIND, int LPE, int POL = 0, bool 
 #ifndef PD_WPE
 #define PD_WPE 2
 #endif
-__global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_WPE))) void k_step(StepArgs<R> a) {
+__global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_WPE))) void k_step(StepArgs<R> a_) {
+    SA<R>& a = kargs<R>();
+    static_assert(sizeof(a_) > 0);
     constexpr int EPB = kStepBlock / LPE;   // envs per workgroup
     __shared__ StepLds<R, WIND, EPB, LPE == 2> L;
 #ifdef PD_STAMP
@@ -1068,6 +1070,7 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
     bool k_have = false;
 #pragma unroll 1
     for (int f = 0; f < nf; ++f) {
+    SA<R>& a = kargs<R>();
     const size_t fo = (size_t)f * (size_t)N;
     float uf[A];
     double ud[A];
@@ -1128,10 +1131,14 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
     const bool tap = a.info != nullptr && role == 0 && live;
     // (the lane offset is laundered per use so that the 49 loop-invariant store addresses are
     // formed inside the taken branch, not hoisted out of the loops and kept live: 92 VGPRs)
+    // (and the row base is laundered too: hoisted, the 49 uniform row bases a.info + k N were
+    // kept in scalar registers -- spilled into VGPR lanes from the prologue on)
     auto info = [&](int k, R v) {
         uint32_t u = ui;
-        asm volatile("" : "+v"(u));
-        ev(a.info + (size_t)k * (size_t)N, u) = v;
+        uint32_t blo = (uint32_t)(uint64_t)a.info, bhi = (uint32_t)((uint64_t)a.info >> 32);
+        asm volatile("" : "+v"(u), "+s"(blo), "+s"(bhi));
+        R* base = (R*)(((uint64_t)bhi << 32) | blo);
+        ev(base + (size_t)k * (size_t)N, u) = v;
     };
 
     bool wpre = false;   // the odd sub-step's gust normals are in L.wnx (drawn with the even one's)
@@ -1140,6 +1147,7 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
     for (int sub = 0; sub < NSUB; ++sub) {
         PD_T(t_sub);
         const int stage = RK4 ? (sub & 3) : 0;
+        SA<R>& a = kargs<R>();
         DP<R>& P = *params<R>(a.P);
         const bool tap_sub = tap && sub == NSUB - 1;
         R x = e.s[0], y = e.s[1], vx = e.s[2], vy = e.s[3], th = e.s[4], thd = e.s[5], ga = e.s[6], al = e.s[7];
@@ -1183,7 +1191,7 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
                             // code on two counters, results swapped (the same bits as one draw per
                             // sub-step; the odd sub-step's pair waits in LDS)
                             const int odd = role & 1;
-                            u32x4 r = philox({(uint32_t)g, (uint32_t)(g >> 32) ^ e.ep, e.ts, kTagWindSub + (uint32_t)(sub + odd)},
+                            u32x4 r = philox_k({(uint32_t)g, (uint32_t)(g >> 32) ^ e.ep, e.ts, kTagWindSub + (uint32_t)(sub + odd)},
                                              a.seed_lo, a.seed_hi);
                             double z0, z1;
                             gauss_pair(r, lic, llc, z0, z1);
@@ -1197,7 +1205,7 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
                         }
                     }
                     if (!drawn) {   // (one draw per sub-step; paired: an env that entered the band mid-pair)
-                        u32x4 r = philox({(uint32_t)g, (uint32_t)(g >> 32) ^ e.ep, e.ts, kTagWindSub + (uint32_t)sub},
+                        u32x4 r = philox_k({(uint32_t)g, (uint32_t)(g >> 32) ^ e.ep, e.ts, kTagWindSub + (uint32_t)sub},
                                          a.seed_lo, a.seed_hi);
                         gauss_pair(r, lic, llc, w0, w1);
                     }
