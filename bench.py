@@ -247,6 +247,7 @@ def workload_counts(d, n, steps, lpe):
         q = 2 * sub      # one C_D and one C_L query per env sub-step
         out.update({"table_queries": q, "q_line_frac": d["q_line"] / q, "q_interior_frac": 1 - d["q_line"] / q,
                     "q_verified_frac": d["q_verified"] / q, "q_taylor_frac": d["q_taylor"] / q,
+                    "q_cell_frac": d["q_cell"] / q,
                     "q_balanced_frac": d["q_balanced"] / q, "q_miss_frac": d["q_miss"] / q,
                     "balanced_rounds_per_wave_substep": d["balanced_rounds"] / (sub * 2 / 64),
                     "q_refined_frac": d["q_refined"] / q, "q_bisect_frac": d["q_bisect"] / q,

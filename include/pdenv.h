@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define PD_ABI_VERSION 5   /* 4: pd_config.integrator (was padding); 5: pd_count_work, pd_step_sac */
+#define PD_ABI_VERSION 6   /* 4: pd_config.integrator (was padding); 5: pd_count_work, pd_step_sac; 6: cell pieces (pd_cell_piece_info, stats word 44) */
 #define PD_MAX_PTS 256      /* aero scatter points per table */
 #define PD_MAX_COLS 5       /* AoA columns per aero table */
 #define PD_MAX_TAB 64       /* grid-fin table length */
@@ -329,7 +329,8 @@ pd_status pd_atmosphere(pd_env* env, const void* altitude, void* out, int64_t n,
  * 35 queries whose candidate neighbourhood was verified by the swap search, 36 queries evaluated
  * from a Taylor piece, 37 by the balanced chunk sums, 38 missed (device solve), 39 balanced-sum
  * rounds, 40 interior queries in a refined grid cell, 41 ... in a sub-cell split by a bisector,
- * 42 / 43 wave sub-steps with at least one such query.  Host sync. */
+ * 42 / 43 wave sub-steps with at least one such query, 44 queries evaluated from a cell piece.
+ * Host sync. */
 #define PD_N_STATS 48
 pd_status pd_stats(pd_env* env, int64_t* out, int32_t n);
 /* Workload counting (pd_stats words 32-43) on (enable != 0) or off (the default) for the handle's
@@ -338,6 +339,14 @@ pd_status pd_stats(pd_env* env, int64_t* out, int32_t n);
  * (a ballot and an LDS add per counter per sub-step, a few per cent slower); off, the product
  * kernel has no counting code.  Results do not change. */
 pd_status pd_count_work(pd_env* env, int32_t enable);
+/* Cell pieces of one table (0: C_D, 1: C_L), host only (no device needed): the polynomial + exact-
+ * term records that binary64 handles evaluate interior queries from (not a
+ * reference interface: the test hook behind them).  Built once per process and table.
+ * out[0] pieces, [1] rejected by the build's check, [2] worst checked error relative to
+ * sum |c_j phi_j|, [3] build seconds, [4] records, [5] nm, [6] na, [7] a0, [8] a1 (the grid),
+ * [9] degree, [10] exact terms, [11] record stride; piece >= 0 (an exact cell's piece is at its
+ * cell index im na + ia): its record at out[16 ...] (n_out >= 16 + stride). */
+pd_status pd_cell_piece_info(const pd_params* params, int32_t table, int64_t piece, double* out, int32_t n_out);
 /* Observation / action widths of the handle. */
 int pd_obs_dim(const pd_env* env);
 int pd_action_dim(const pd_env* env);

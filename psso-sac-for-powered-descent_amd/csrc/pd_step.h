@@ -22,6 +22,17 @@ constexpr int kSolveSlots = 1024;     // global-memory LU scratch slots (one per
 constexpr int kGridExact = 1 << 30;   // grid_slot flag: every point of the cell has its key
 constexpr int kGridRefine = 1 << 29;  // grid_slot flag: the cell is refined, low bits = its sub-grid
 constexpr int kGridBisect = 1 << 28;  // sub_slot flag: two regions split by one bisector, low bits = its record
+constexpr int kGridPiece = 1 << 27;   // grid_slot flag (exact cells of binary64 handles): the cell has its cell piece
+
+// Cell pieces (binary64 handles): the thin-plate sum of one neighbourhood over one interior grid
+// cell as a polynomial of total degree kCellDeg in the cell coordinates (u, v) in [-1, 1]^2 plus
+// its kCellExact terms nearest to the cell (pdenv.hip build_cell_pieces).  Record: the
+// coefficients row by row (u^i, i = kCellDeg .. 0; within a row v^j, j = kCellDeg - i .. 0), then
+// per exact term (Mach, coefficient / 8, AoA), padded to 16 bytes.
+constexpr int kCellDeg = 8;
+constexpr int kCellCoef = (kCellDeg + 1) * (kCellDeg + 2) / 2;
+constexpr int kCellExact = 4;
+constexpr int kCellStride = (kCellCoef + 3 * kCellExact + 1) & ~1;
 
 // A sub-cell holding two 50-NN regions A, B whose keys differ by one point swap (p in A, q in B):
 // s(x) = n . x - c < 0 on A's side (p nearer than q).  Each side's slot carries kGridExact only if
@@ -31,7 +42,7 @@ struct GridBisect {
     double nx, ny, c, tau;
     unsigned long long key_a, key_b;
     int slot_a, slot_b;
-    int pad[2];
+    int piece_a, piece_b;   // each side's cell piece (binary64 handles; -1: none)
 };
 #ifndef PD_GRID_SUB
 #define PD_GRID_SUB 8
@@ -59,7 +70,8 @@ enum Stat {
     kStQBisect = kStWork + 9,    // ... whose sub-cell is split by a bisector (a third dependent load)
     kStWRefined = kStWork + 10,  // wave sub-steps with at least one refined-cell query
     kStWBisect = kStWork + 11,   // wave sub-steps with at least one bisector query
-    kNWork = 12
+    kStQCell = kStWork + 12,     // LPE 2 queries evaluated from a cell piece
+    kNWork = 13
 };
 
 // Per-wave workload counts in LDS (nullptr: counting off, the launch pays one scalar branch per

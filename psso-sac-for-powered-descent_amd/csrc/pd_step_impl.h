@@ -63,6 +63,8 @@ template <typename R> struct TabView {
     const PD_AS1 unsigned long long* sub_key;
     const PD_AS1 int* sub_slot;
     const PD_AS1 GridBisect* sub_bis;
+    const PD_AS1 double* cell_pc;   // cell pieces (binary64 handles; nullptr: none)
+    const PD_AS1 int* sub_piece;
     int grid_nm, grid_na;
     R grid_a0, grid_inv_da, grid_inv_dm;
 };
@@ -403,8 +405,9 @@ __device__ __forceinline__ R rbf_miss_wave(const AT& a, DP<R>& P, int table, con
 // the swap search) against the exact distances before it is used.
 // A query's Taylor piece on a clamped line (rbf2): its record index and cell, piece < 0: none
 // (line, verify, refined, bisect: the query was on a clamped line / its candidate was verified /
-// it read a refined cell's sub-cell / a bisector record -- for the workload counters)
-struct TayRef { int piece, cell; bool line, verify, refined, bisect; };
+// it read a refined cell's sub-cell / a bisector record -- for the workload counters).  cp: a
+// trusted interior query's cell piece (-1 none), cu, cv: its position in the cell, [0, 1)
+struct TayRef { int piece, cell; bool line, verify, refined, bisect; int cp; double cu, cv; };
 
 struct NoPre { __device__ void operator()() const {} };
 
@@ -429,7 +432,7 @@ __device__ __forceinline__ int rbf_lookup(const AT& a, DP<R>& P, int table, cons
     // the interior grid cell's candidate is requested by every lane first (its global loads are
     // in flight during the line search; lanes on a line discard it)
     unsigned long long gkey = 0ull;
-    int gsl0 = -1;
+    int gsl0 = -1, gcell = 0;
     R um = R(0), ua = R(0);
     const bool use_grid = t.grid_key != nullptr;
     if (use_grid) {
@@ -437,9 +440,9 @@ __device__ __forceinline__ int rbf_lookup(const AT& a, DP<R>& P, int table, cons
         int im = fm < R(0) ? 0 : (fm >= R(t.grid_nm) ? t.grid_nm - 1 : (int)fm);
         int ia = fa < R(0) ? 0 : (fa >= R(t.grid_na) ? t.grid_na - 1 : (int)fa);
         if (!(fm == fm) || !(fa == fa)) { im = 0; ia = 0; }   // NaN queries
-        const int cell = im * t.grid_na + ia;
-        gkey = t.grid_key[cell];
-        gsl0 = t.grid_slot[cell];
+        gcell = im * t.grid_na + ia;
+        gkey = t.grid_key[gcell];
+        gsl0 = t.grid_slot[gcell];
         um = fm - (R)im; ua = fa - (R)ia;     // position in the cell, [0, 1)
     }
     pre();
@@ -472,6 +475,10 @@ __device__ __forceinline__ int rbf_lookup(const AT& a, DP<R>& P, int table, cons
     } else if (use_grid) {
         ckey = gkey;
         int gsl = gsl0;
+        // the cell piece (LPE 2 binary64 handles): an exact cell's own, else its sub-cell's
+        const bool pieces = tay != nullptr && t.cell_pc != nullptr;
+        const R cu = um, cv = ua;
+        int cpc = pieces && gsl >= 0 && !(gsl & kGridRefine) && (gsl & kGridPiece) ? gcell : -1;
         if (sizeof(R) != 8 && gsl >= 0 && (gsl & kGridRefine)) gsl = -1;   // centre key, verified
         if (sizeof(R) == 8 && gsl >= 0 && (gsl & kGridRefine)) {
             // a cell that straddles neighbourhood regions: its sub-cell (binary64 handles; the
@@ -485,6 +492,7 @@ __device__ __forceinline__ int rbf_lookup(const AT& a, DP<R>& P, int table, cons
             const int sc = (ref * kGridSub + jm) * kGridSub + ja;
             ckey = t.sub_key[sc];
             gsl = t.sub_slot[sc];
+            if (pieces) cpc = t.sub_piece[sc];
             um = sm - (R)jm; ua = sa - (R)ja;
             if (gsl >= 0 && (gsl & kGridBisect)) {
                 // two regions split by one bisector: the query's side (trusted off the line)
@@ -496,13 +504,15 @@ __device__ __forceinline__ int rbf_lookup(const AT& a, DP<R>& P, int table, cons
                 ckey = side_a ? b.key_a : b.key_b;
                 if (!(fabs(sv) > 3.0 * b.tau) && sl >= 0) sl &= ~kGridExact;
                 gsl = sl;
+                if (pieces) cpc = side_a ? b.piece_a : b.piece_b;
             }
         }
-        cslot = gsl < 0 ? -1 : (gsl & (kGridRefine - 1));
+        cslot = gsl < 0 ? -1 : (gsl & (kGridPiece - 1));
         // every point of an exact cell has the cell's key (convexity of 50-NN regions); the
         // rounding margin keeps queries on a cell edge on the verified path
         const R eps = sizeof(R) == 8 ? R(1e-9) : R(1e-4);
         trusted = gsl >= 0 && (gsl & kGridExact) && um > eps && R(1) - um > eps && ua > eps && R(1) - ua > eps;
+        if (pieces && trusted && cpc >= 0) { tay->cp = cpc; tay->cu = (double)cu; tay->cv = (double)cv; }
     }
     PD_LST(1);
     unsigned long long key = ckey;
@@ -571,6 +581,32 @@ __device__ __forceinline__ R taylor_eval(const PD_AS1 R* __restrict__ rec, R M, 
         const R dm = M - x[0];
         const R d2 = fma(dm, dm, x[2]);
         f = fma(x[1] * d2, eval_log4<R>(sizeof(R) == 8 ? d2 : (d2 > R(1e-30) ? d2 : R(1e-30))), f);
+    }
+    return f;
+}
+
+// An interior query's value from its cell piece (pd_step.h kCellDeg, pdenv.hip
+// build_cell_pieces): the polynomial in the cell coordinates u = 2 cu - 1, v = 2 cv - 1 (Horner
+// in u over the rows' polynomials in v) plus the exact terms.  The host checks every piece at
+// points of its cell in this order of operations.
+__device__ __forceinline__ double cell_eval(const PD_AS1 double* __restrict__ rec, double M, double aq, double cu,
+                                            double cv) {
+    const double u = 2.0 * cu - 1.0, v = 2.0 * cv - 1.0;
+    double f = 0.0;
+    int q = 0;
+#pragma unroll
+    for (int i = kCellDeg; i >= 0; --i) {
+        double qi = rec[q++];
+#pragma unroll
+        for (int j = kCellDeg - i - 1; j >= 0; --j) qi = fma(qi, v, rec[q++]);
+        f = i == kCellDeg ? qi : fma(f, u, qi);
+    }
+#pragma unroll
+    for (int e = 0; e < kCellExact; ++e) {
+        const PD_AS1 double* x = rec + kCellCoef + 3 * e;
+        const double dm = M - x[0], da = aq - x[2];
+        const double d2 = fma(dm, dm, da * da);
+        f = fma(x[1] * d2, eval_log4<double>(d2), f);
     }
     return f;
 }
@@ -697,29 +733,40 @@ __device__ __forceinline__ R rbf2(const AT& a, DP<R>& P, int table, const TabVie
 #ifdef PD_STAMP
     const unsigned long long s0 = __builtin_amdgcn_s_memtime();
 #endif
-    TayRef tr{-1, 0, false, false, false, false};
+    TayRef tr{-1, 0, false, false, false, false, -1, 0.0, 0.0};
     const int slot = rbf_lookup<R>(a, P, table, t, ln, cache, M, aq, &tr, stamp ? stamp + 2 : nullptr, pre);
 #ifdef PD_STAMP
     const unsigned long long s1 = __builtin_amdgcn_s_memtime();
     stamp[0] += s1 - s0;
 #endif
     const bool tay = act && tr.piece >= 0;
-    const bool full = act && !tay && slot >= 0;
+    const bool cel = act && tr.cp >= 0;   // (binary64 handles only)
+    const bool full = act && !tay && !cel && slot >= 0;
     R vt = R(0);
-    const R vb = rbf_balanced<R>(P, B, tab, full, table, slot, M, aq, [&]() {
+    R vb;
+    if constexpr (sizeof(R) == 8) {
+        // with cell pieces the payload sums are rare (verified queries): the pieces first, then
+        // the balanced sums of the lanes left, if any
         if (tay) vt = taylor_eval<R>(gbl(P.tay) + (size_t)tr.piece * kTayStride, M, tr.cell);
-    });
+        if (cel) vt = cell_eval(t.cell_pc + (size_t)tr.cp * kCellStride, M, aq, tr.cu, tr.cv);
+        vb = rbf_balanced<R>(P, B, tab, full, table, slot, M, aq, []() {});
+    } else {
+        vb = rbf_balanced<R>(P, B, tab, full, table, slot, M, aq, [&]() {
+            if (tay) vt = taylor_eval<R>(gbl(P.tay) + (size_t)tr.piece * kTayStride, M, tr.cell);
+        });
+    }
     R val = full ? vb : vt;
 #ifdef PD_STAMP
     const unsigned long long s2 = __builtin_amdgcn_s_memtime();
     stamp[1] += s2 - s1;
 #endif
-    const bool miss = act && !tay && slot < 0;
+    const bool miss = act && !tay && !cel && slot < 0;
     if (wc.w) {
         const int nf = __popcll(__ballot(full));
         wc.add(kStQLine - kStWork, act && tr.line);
         wc.add(kStQVerify - kStWork, act && tr.verify);
         wc.add(kStQTaylor - kStWork, tay);
+        wc.add(kStQCell - kStWork, cel);
         wc.add_n(kStQBal - kStWork, nf);
         wc.add(kStQMiss - kStWork, miss);
         wc.add_n(kStBalRounds - kStWork, (kChunks * nf + 63) >> 6);
@@ -866,6 +913,8 @@ __device__ __forceinline__ TabView<R> tab_view(DP<R>& P, const R* tab, int table
     t.sub_key = gbl(P.sub_key[table]);
     t.sub_slot = gbl(P.sub_slot[table]);
     t.sub_bis = gbl((const GridBisect*)P.sub_bis[table]);
+    t.cell_pc = gbl(P.cell_pc[table]);
+    t.sub_piece = gbl(P.sub_piece[table]);
     t.grid_nm = P.grid_nm[table];
     t.grid_na = P.grid_na[table];
     t.grid_a0 = P.grid_a0[table];

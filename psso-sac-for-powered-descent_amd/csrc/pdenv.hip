@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -613,10 +614,31 @@ const GridKeys& grid_keys(const pd_aero_table& t, double a0, double a1, int nm, 
 // skip the verification.  A cell whose corners disagree is refined into kGridSub x kGridSub
 // sub-cells with the same construction (flagged kGridRefine, its sub-grid index in the low
 // bits), so that only queries near a region boundary are verified on the device.
+// The interior candidate grid of table tb (0: C_D, 1: C_L): Mach [0, 10] x AoA abscissa [a0, a1]
+// (C_D in [-radians(10), radians(10)], C_L in [0, 10]) in nm x na cells.  800 x 32 / 800 x 400
+// cells, refined cells in 8 x 8 sub-cells, two-region sub-cells split by their bisector: < 0.1 %
+// of queries verified (measured against 400 x 200 and 1600 x 800)
+void grid_geometry(int tb, int& nm, int& na, double& a0, double& a1) {
+    int d[4] = {800, 32, 800, 400};
+    if (const char* g = getenv("PDENV_GRID")) {   // experiments: "nm_cd,na_cd,nm_cl,na_cl"
+        int v[4];
+        if (sscanf(g, "%d,%d,%d,%d", &v[0], &v[1], &v[2], &v[3]) == 4 && v[0] > 0 && v[1] > 0 && v[2] > 0 && v[3] > 0)
+            for (int k = 0; k < 4; ++k) d[k] = v[k];
+    }
+    nm = d[2 * tb]; na = d[2 * tb + 1];
+    a0 = tb ? 0.0 : -10.0 * kDeg2Rad;
+    a1 = tb ? 10.0 : 10.0 * kDeg2Rad;
+}
+
+struct CellPieces;
+bool cell_ok(const CellPieces* cp, int64_t cell);
+int cell_bis(const CellPieces* cp, int bi, bool side_b);
+
 template <typename R>
 pd_status build_grid(const pd_aero_table& t, double a0, double a1, int nm, int na, Table<R>& T,
                      std::vector<unsigned long long>& gk, std::vector<int>& gs,
-                     std::vector<unsigned long long>& sk, std::vector<int>& ss, std::vector<GridBisect>& bs) {
+                     std::vector<unsigned long long>& sk, std::vector<int>& ss, std::vector<GridBisect>& bs,
+                     const CellPieces* cp = nullptr) {
     const GridKeys& g = grid_keys(t, a0, a1, nm, na);
     const int S = kGridSub;
     gk.assign((size_t)nm * na, 0); gs.assign((size_t)nm * na, -1);
@@ -630,6 +652,7 @@ pd_status build_grid(const pd_aero_table& t, double a0, double a1, int nm, int n
             const uint64_t key = g.centre[(size_t)im * na + ia];
             gk[(size_t)im * na + ia] = key;
             gs[(size_t)im * na + ia] = slot_of(key, true);   // refined cells overwritten below
+            if (gs[(size_t)im * na + ia] >= 0 && cell_ok(cp, (int64_t)im * na + ia)) gs[(size_t)im * na + ia] |= kGridPiece;
         }
     const int64_t nr = (int64_t)g.refined.size();
     if (nr >= kGridRefine) return fail(PD_ERR_INVALID, "too many refined grid cells");
@@ -653,11 +676,306 @@ pd_status build_grid(const pd_aero_table& t, double a0, double a1, int nm, int n
                     const int sa = table_insert<R>(t, T, h.key_a, work, pay), sb = table_insert<R>(t, T, h.key_b, work, pay);
                     b.slot_a = sa < 0 ? -1 : (sa | (h.ok_a ? kGridExact : 0));
                     b.slot_b = sb < 0 ? -1 : (sb | (h.ok_b ? kGridExact : 0));
+                    b.piece_a = cell_bis(cp, bi, false); b.piece_b = cell_bis(cp, bi, true);
                     ss[q] = kGridBisect | (int)bs.size();
                     bs.push_back(b);
                 }
             }
     }
+    return PD_OK;
+}
+
+// ---------------------------------------------------------------- cell pieces
+// Interior queries of the binary64 handle are evaluated from cell pieces (pd_step.h kCellDeg):
+// for every interior grid cell and every neighbourhood that owns part of it, the thin-plate sum
+// s(x) = sum_j c_j phi(|x - y_j|) + poly(x) of that neighbourhood restricted to the cell.  s is
+// analytic over the cell except at the table points themselves (phi = r^2 log r), so the
+// kCellExact points nearest to the cell centre stay exact terms and the rest, with scipy's
+// degree-1 polynomial, is a polynomial of total degree kCellDeg in the cell coordinates (u, v) in
+// [-1, 1]^2 (the device's 2 (M inv_dm - im) - 1 and 2 ((a - a0) inv_da - ia) - 1): the least-
+// squares fit (long double Householder QR, once) on the cell's 10 x 10 tensor Chebyshev grid of
+// the far terms evaluated there.  Every piece is then evaluated as the device does (binary64
+// Horner, exact terms) at 8 quasi-random points of the cell and compared with the long double
+// sum of all 50 terms: a piece whose error exceeds kCellTol relative to sum |c_j phi_j| is not
+// used (the query goes to the payload sum).  Pure functions of the table and the grid: built once
+// per process (threads over pieces) and cached, like the grid keys.
+constexpr double kCellTol = 1e-14;
+constexpr int kCellNodes = 10;
+
+struct CellPieces {
+    std::vector<double> rec;          // [n][kCellStride]: exact cells at their cell index, then refined cells' pieces
+    std::vector<uint8_t> cell_ok;     // [nm na] the exact cell's own piece is valid
+    std::vector<int> sub_piece;       // [refined][S][S] piece of an exact sub-cell's key (-1 none)
+    std::vector<int> bis_a, bis_b;    // per GridKeys bisector record: each trusted side's piece
+    double max_rel = 0, build_s = 0;
+    int64_t pieces = 0, rejected = 0;
+};
+
+// The fit operator: pinv[c][node] of the (node x coefficient) monomial design matrix, columns in
+// record order (u^i v^j, i = kCellDeg .. 0, j = kCellDeg - i .. 0), nodes (k, l) -> (x_k, x_l)
+const std::vector<long double>& cell_fit_operator() {
+    static std::vector<long double> pinv;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        const int NN = kCellNodes * kCellNodes, NC = kCellCoef;
+        long double x[kCellNodes];
+        for (int k = 0; k < kCellNodes; ++k) x[k] = cosl((2 * k + 1) * 3.141592653589793238462643383279502884L / (2 * kCellNodes));
+        std::vector<long double> A((size_t)NN * NC), Q((size_t)NN * NN, 0.0L);
+        for (int k = 0; k < kCellNodes; ++k)
+            for (int l = 0; l < kCellNodes; ++l) {
+                int c = 0;
+                for (int i = kCellDeg; i >= 0; --i)
+                    for (int j = kCellDeg - i; j >= 0; --j) A[(size_t)(k * kCellNodes + l) * NC + c++] = powl(x[k], i) * powl(x[l], j);
+            }
+        for (int r = 0; r < NN; ++r) Q[(size_t)r * NN + r] = 1.0L;   // accumulates Q^T
+        for (int c = 0; c < NC; ++c) {
+            long double nrm = 0.0L;
+            for (int r = c; r < NN; ++r) nrm += A[(size_t)r * NC + c] * A[(size_t)r * NC + c];
+            nrm = sqrtl(nrm);
+            const long double alpha = A[(size_t)c * NC + c] > 0 ? -nrm : nrm;
+            std::vector<long double> v(NN, 0.0L);
+            for (int r = c; r < NN; ++r) v[r] = A[(size_t)r * NC + c];
+            v[c] -= alpha;
+            long double vv = 0.0L;
+            for (int r = c; r < NN; ++r) vv += v[r] * v[r];
+            if (vv == 0.0L) continue;
+            for (int cc = c; cc < NC; ++cc) {
+                long double d = 0.0L;
+                for (int r = c; r < NN; ++r) d += v[r] * A[(size_t)r * NC + cc];
+                d = 2.0L * d / vv;
+                for (int r = c; r < NN; ++r) A[(size_t)r * NC + cc] -= d * v[r];
+            }
+            for (int cc = 0; cc < NN; ++cc) {
+                long double d = 0.0L;
+                for (int r = c; r < NN; ++r) d += v[r] * Q[(size_t)r * NN + cc];
+                d = 2.0L * d / vv;
+                for (int r = c; r < NN; ++r) Q[(size_t)r * NN + cc] -= d * v[r];
+            }
+        }
+        // R X = (Q^T)[0:NC]  ->  X = pinv
+        pinv.assign((size_t)NC * NN, 0.0L);
+        for (int cc = 0; cc < NN; ++cc)
+            for (int c = NC - 1; c >= 0; --c) {
+                long double s = Q[(size_t)c * NN + cc];
+                for (int k = c + 1; k < NC; ++k) s -= A[(size_t)c * NC + k] * pinv[(size_t)k * NN + cc];
+                pinv[(size_t)c * NN + cc] = s / A[(size_t)c * NC + c];
+            }
+    });
+    return pinv;
+}
+
+// The terms of a neighbourhood's payload (Mach, AoA, coefficient) and its polynomial
+struct NbrTerms {
+    int nt = 0;
+    double m[2 * kPairs], a[2 * kPairs], c[2 * kPairs];
+    double p0 = 0, p1 = 0, p2 = 0, sh0 = 0, sh1 = 0, sc0 = 1, sc1 = 1;
+    bool ok = false;
+};
+NbrTerms nbr_terms(const pd_aero_table& t, uint64_t key) {
+    NbrTerms T;
+    std::vector<double> work(kScratch), pay(kPay);
+    double aoa[kCols];
+    for (int c = 0; c < kCols; ++c) aoa[c] = t.col_aoa[c];
+    if (solve_neighbourhood(t.mach, t.coef, t.col_start, aoa, key, work.data(), pay.data()) != 0) return T;
+    const uint8_t* ib = (const uint8_t*)(pay.data() + kPayIdx);
+    for (int k = 0; k < kPairs; ++k)
+        for (int i = 0; i < 2; ++i) {
+            const double c = pay[2 * k + i];
+            if (c == 0.0) continue;
+            const bool g2 = i == 1 && slot_general(k);
+            T.m[T.nt] = t.mach[g2 ? ib[second_entry_pos(k)] : ib[pair_entry_pos(k)] + i];
+            T.a[T.nt] = ib[g2 ? second_aoa_pos(k) : pair_aoa_pos(k)];
+            T.c[T.nt] = c;
+            ++T.nt;
+        }
+    T.p0 = pay[kPayPoly]; T.p1 = pay[kPayPoly + 1]; T.p2 = pay[kPayPoly + 2];
+    T.sh0 = pay[kPaySS + 0]; T.sh1 = pay[kPaySS + 1]; T.sc0 = pay[kPaySS + 2]; T.sc1 = pay[kPaySS + 3];
+    T.ok = true;
+    return T;
+}
+
+// One piece: key's sum over cell (im, ia) into rec; returns the validation error (relative to
+// sum |c_j phi_j|), or +inf if the neighbourhood did not solve
+double make_cell_piece(const NbrTerms& T, int im, int ia, double dm, double da, double a0, double* rec) {
+    if (!T.ok) return INFINITY;
+    const std::vector<long double>& pinv = cell_fit_operator();
+    const double cm = (im + 0.5) * dm, ca = a0 + (ia + 0.5) * da, hm = 0.5 * dm, ha = 0.5 * da;
+    // exact terms: the kCellExact nearest to the centre (ties by term order)
+    int ex[kCellExact];
+    bool is_ex[2 * kPairs] = {};
+    for (int e = 0; e < kCellExact; ++e) {
+        int best = -1;
+        double bd = 0;
+        for (int j = 0; j < T.nt; ++j) {
+            if (is_ex[j]) continue;
+            const double d = (cm - T.m[j]) * (cm - T.m[j]) + (ca - T.a[j]) * (ca - T.a[j]);
+            if (best < 0 || d < bd) { best = j; bd = d; }
+        }
+        ex[e] = best;
+        if (best >= 0) is_ex[best] = true;
+    }
+    const int NN = kCellNodes * kCellNodes;
+    long double F[kCellNodes * kCellNodes];
+    long double xn[kCellNodes];
+    for (int k = 0; k < kCellNodes; ++k) xn[k] = cosl((2 * k + 1) * 3.141592653589793238462643383279502884L / (2 * kCellNodes));
+    for (int k = 0; k < kCellNodes; ++k)
+        for (int l = 0; l < kCellNodes; ++l) {
+            const long double M = cm + xn[k] * hm, a = ca + xn[l] * ha;
+            long double s = T.p0 + (M - T.sh0) / T.sc0 * T.p1 + (a - T.sh1) / T.sc1 * T.p2;
+            for (int j = 0; j < T.nt; ++j) {
+                if (is_ex[j]) continue;
+                const long double dmj = M - T.m[j], daj = a - T.a[j], d2 = dmj * dmj + daj * daj;
+                if (d2 > 0) s += 0.5L * T.c[j] * d2 * (long double)std::log((double)d2);
+            }
+            F[k * kCellNodes + l] = s;
+        }
+    for (int c = 0; c < kCellCoef; ++c) {
+        long double s = 0.0L;
+        for (int r = 0; r < NN; ++r) s += pinv[(size_t)c * NN + r] * F[r];
+        rec[c] = (double)s;
+    }
+    for (int e = 0; e < kCellExact; ++e) {
+        double* x = rec + kCellCoef + 3 * e;
+        if (ex[e] < 0) { x[0] = 0.0; x[1] = 0.0; x[2] = 1e3; continue; }
+        x[0] = T.m[ex[e]]; x[1] = T.c[ex[e]] * 0.125; x[2] = T.a[ex[e]];
+    }
+    for (int c = kCellCoef + 3 * kCellExact; c < kCellStride; ++c) rec[c] = 0.0;
+    // validation: 8 Halton (2, 3) points of the cell, evaluated in the device's order
+    double worst = 0.0;
+    for (int q = 1; q <= 8; ++q) {
+        double h2 = 0, h3 = 0, f2 = 0.5, f3 = 1.0 / 3;
+        for (int n = q; n; n >>= 1, f2 *= 0.5) h2 += f2 * (n & 1);
+        for (int n = q; n; n /= 3, f3 /= 3) h3 += f3 * (n % 3);
+        const double u = 2 * h2 - 1, v = 2 * h3 - 1, M = cm + u * hm, a = ca + v * ha;
+        double f = 0.0;
+        int c = 0;
+        for (int i = kCellDeg; i >= 0; --i) {
+            double qi = rec[c++];
+            for (int j = kCellDeg - i - 1; j >= 0; --j) qi = std::fma(qi, v, rec[c++]);
+            f = i == kCellDeg ? qi : std::fma(f, u, qi);
+        }
+        for (int e = 0; e < kCellExact; ++e) {
+            const double* x = rec + kCellCoef + 3 * e;
+            const double dmx = M - x[0], dax = a - x[2], d2 = std::fma(dmx, dmx, dax * dax);
+            if (d2 > 0) f = std::fma(x[1] * d2, 4.0 * std::log(d2), f);
+        }
+        long double exact = T.p0 + ((long double)M - T.sh0) / T.sc0 * T.p1 + ((long double)a - T.sh1) / T.sc1 * T.p2, mag = 0.0L;
+        for (int j = 0; j < T.nt; ++j) {
+            const long double dmj = M - T.m[j], daj = a - T.a[j], d2 = dmj * dmj + daj * daj;
+            const long double ph = d2 > 0 ? 0.5L * T.c[j] * d2 * logl(d2) : 0.0L;
+            exact += ph; mag += fabsl(ph);
+        }
+        worst = std::max(worst, (double)(fabsl((long double)f - exact) / (mag + fabsl(exact) + 1e-300L)));
+    }
+    return worst;
+}
+
+const CellPieces& cell_pieces(const pd_aero_table& t, double a0, double a1, int nm, int na) {
+    static std::mutex mu;
+    static std::map<uint64_t, CellPieces> cache;
+    uint64_t h = 1469598103934665603ull;
+    auto mix = [&](const void* p, size_t n) {
+        for (size_t i = 0; i < n; ++i) { h ^= ((const uint8_t*)p)[i]; h *= 1099511628211ull; }
+    };
+    mix(&t, sizeof(t)); mix(&a0, 8); mix(&a1, 8); mix(&nm, 4); mix(&na, 4);
+    const GridKeys& g = grid_keys(t, a0, a1, nm, na);
+    std::lock_guard<std::mutex> lock(mu);
+    auto it = cache.find(h);
+    if (it != cache.end()) return it->second;
+    const auto t0 = std::chrono::steady_clock::now();
+    CellPieces& cp = cache[h];
+    const int S = kGridSub;
+    const double dm = 10.0 / nm, da = (a1 - a0) / na;
+    const int64_t ncell = (int64_t)nm * na, nr = (int64_t)g.refined.size();
+    // the pieces: (cell, key) pairs -- exact cells at their index, then each refined cell's keys
+    // (its exact sub-cells' and trusted bisector sides'), one piece per distinct key
+    std::vector<std::pair<int, uint64_t>> job((size_t)ncell);
+    std::vector<uint8_t> refined(ncell, 0);
+    for (int r : g.refined) refined[r] = 1;
+    for (int64_t c = 0; c < ncell; ++c) job[c] = {(int)c, g.centre[c]};
+    cp.sub_piece.assign((size_t)nr * S * S, -1);
+    cp.bis_a.assign(g.bis.size(), -1);
+    cp.bis_b.assign(g.bis.size(), -1);
+    for (int64_t r = 0; r < nr; ++r) {
+        std::map<uint64_t, int> own;
+        auto piece_of = [&](uint64_t key) {
+            auto f = own.find(key);
+            if (f != own.end()) return f->second;
+            const int p = (int)job.size();
+            job.push_back({g.refined[r], key});
+            own[key] = p;
+            return p;
+        };
+        const int im = g.refined[r] / na, ia = g.refined[r] % na;
+        (void)im; (void)ia;
+        for (int q = 0; q < S * S; ++q) {
+            const size_t sq = (size_t)r * S * S + q;
+            const int jm = q / S, ja = q % S;
+            const uint64_t key = g.sub_centre[sq];
+            bool exact = true;
+            for (int c = 0; c < 4 && exact; ++c)
+                exact = g.sub_corner[((size_t)r * (S + 1) + jm + (c >> 1)) * (S + 1) + ja + (c & 1)] == key;
+            if (exact) cp.sub_piece[sq] = piece_of(key);
+            const int bi = g.sub_bis[sq];
+            if (!exact && bi >= 0) {
+                if (g.bis[bi].ok_a) cp.bis_a[bi] = piece_of(g.bis[bi].key_a);
+                if (g.bis[bi].ok_b) cp.bis_b[bi] = piece_of(g.bis[bi].key_b);
+            }
+        }
+    }
+    // the neighbourhoods' terms, solved once per key
+    std::map<uint64_t, int> kidx;
+    std::vector<uint64_t> keys;
+    for (auto& j : job)
+        if (kidx.emplace(j.second, (int)keys.size()).second) keys.push_back(j.second);
+    std::vector<NbrTerms> terms(keys.size());
+    parallel_for((int64_t)keys.size(), [&](int64_t k) { terms[k] = nbr_terms(t, keys[k]); });
+    cell_fit_operator();
+    cp.rec.assign(job.size() * kCellStride, 0.0);
+    std::vector<double> err(job.size());
+    parallel_for((int64_t)job.size(), [&](int64_t p) {
+        const int c = job[p].first;
+        if (p < ncell && refined[c]) { err[p] = INFINITY; return; }   // (a refined cell's own index: unused)
+        err[p] = make_cell_piece(terms[kidx.at(job[p].second)], c / na, c % na, dm, da, a0, cp.rec.data() + (size_t)p * kCellStride);
+    });
+    auto valid = [&](int p) { return p >= 0 && err[p] <= kCellTol; };
+    cp.cell_ok.assign(ncell, 0);
+    for (int64_t c = 0; c < ncell; ++c) cp.cell_ok[c] = !refined[c] && valid((int)c);
+    for (auto& s : cp.sub_piece) if (!valid(s)) s = -1;
+    for (auto& s : cp.bis_a) if (!valid(s)) s = -1;
+    for (auto& s : cp.bis_b) if (!valid(s)) s = -1;
+    for (size_t p = 0; p < job.size(); ++p) {
+        if ((int64_t)p < ncell && refined[job[p].first]) continue;
+        ++cp.pieces;
+        if (err[p] <= kCellTol) cp.max_rel = std::max(cp.max_rel, err[p]);
+        else ++cp.rejected;
+    }
+    cp.build_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    return cp;
+}
+bool cell_ok(const CellPieces* cp, int64_t cell) { return cp != nullptr && cp->cell_ok[cell]; }
+int cell_bis(const CellPieces* cp, int bi, bool side_b) { return cp == nullptr ? -1 : (side_b ? cp->bis_b[bi] : cp->bis_a[bi]); }
+
+// The device copy of a table's cell pieces: one per device and process, shared read-only by the
+// handles (never freed; ~0.2 GB of the 288 GB)
+pd_status cell_pieces_device(const CellPieces& cp, const double** rec, const int** sub) {
+    static std::mutex mu;
+    static std::map<std::pair<const void*, int>, std::pair<void*, void*>> m;
+    int dev = 0;
+    PD_HIP(hipGetDevice(&dev));
+    std::lock_guard<std::mutex> lock(mu);
+    auto k = std::make_pair((const void*)&cp, dev);
+    auto it = m.find(k);
+    if (it == m.end()) {
+        void *dr = nullptr, *ds = nullptr;
+        PD_HIP(hipMalloc(&dr, std::max<size_t>(cp.rec.size(), 1) * 8));
+        PD_HIP(hipMalloc(&ds, std::max<size_t>(cp.sub_piece.size(), 1) * 4));
+        if (!cp.rec.empty()) PD_HIP(hipMemcpy(dr, cp.rec.data(), cp.rec.size() * 8, hipMemcpyHostToDevice));
+        if (!cp.sub_piece.empty()) PD_HIP(hipMemcpy(ds, cp.sub_piece.data(), cp.sub_piece.size() * 4, hipMemcpyHostToDevice));
+        it = m.emplace(k, std::make_pair(dr, ds)).first;
+    }
+    *rec = (const double*)it->second.first;
+    *sub = (const int*)it->second.second;
     return PD_OK;
 }
 
@@ -929,18 +1247,22 @@ template <typename R> pd_status create_impl(const pd_params* p, const pd_config*
     std::vector<unsigned long long> gk[2], sk[2];
     std::vector<int> gs[2], ss[2];
     std::vector<GridBisect> bs[2];
-    // 800 x 32 / 800 x 400 cells, refined cells in 8 x 8 sub-cells, two-region sub-cells split by
-    // their bisector: < 0.1 % of queries verified (measured against 400 x 200 and 1600 x 800)
-    int gnm[2] = {800, 800}, gna[2] = {32, 400};
-    if (const char* g = getenv("PDENV_GRID")) {   // experiments: "nm_cd,na_cd,nm_cl,na_cl"
-        int v[4];
-        if (sscanf(g, "%d,%d,%d,%d", &v[0], &v[1], &v[2], &v[3]) == 4 && v[0] > 0 && v[1] > 0 && v[2] > 0 && v[3] > 0) {
-            gnm[0] = v[0]; gna[0] = v[1]; gnm[1] = v[2]; gna[1] = v[3];
-        }
+    int gnm[2], gna[2];
+    double ga0[2], ga1[2];
+    for (int tb = 0; tb < 2; ++tb) grid_geometry(tb, gnm[tb], gna[tb], ga0[tb], ga1[tb]);
+    // cell pieces for the binary64 handle's interior queries (PDENV_CELL_PIECES=0: payload sums only)
+    const CellPieces* cps[2] = {nullptr, nullptr};
+    const char* cpe = getenv("PDENV_CELL_PIECES");
+    if (sizeof(R) == 8 && !(cpe && cpe[0] == '0')) {
+        cps[0] = &cell_pieces(p->cd, ga0[0], ga1[0], gnm[0], gna[0]);
+        cps[1] = &cell_pieces(p->cl, ga0[1], ga1[1], gnm[1], gna[1]);
     }
-    const double ga0[2] = {-10.0 * kDeg2Rad, 0.0}, ga1[2] = {10.0 * kDeg2Rad, 10.0};
-    if ((st = build_grid<R>(p->cd, ga0[0], ga1[0], gnm[0], gna[0], tcd, gk[0], gs[0], sk[0], ss[0], bs[0])) != PD_OK) return st;
-    if ((st = build_grid<R>(p->cl, ga0[1], ga1[1], gnm[1], gna[1], tcl, gk[1], gs[1], sk[1], ss[1], bs[1])) != PD_OK) return st;
+    if ((st = build_grid<R>(p->cd, ga0[0], ga1[0], gnm[0], gna[0], tcd, gk[0], gs[0], sk[0], ss[0], bs[0], cps[0])) != PD_OK) return st;
+    if ((st = build_grid<R>(p->cl, ga0[1], ga1[1], gnm[1], gna[1], tcl, gk[1], gs[1], sk[1], ss[1], bs[1], cps[1])) != PD_OK) return st;
+    for (int tb = 0; tb < 2; ++tb) {
+        D.cell_pc[tb] = nullptr; D.sub_piece[tb] = nullptr;
+        if (cps[tb] && (st = cell_pieces_device(*cps[tb], &D.cell_pc[tb], &D.sub_piece[tb])) != PD_OK) return st;
+    }
     if (getenv("PDENV_TAY_DEBUG"))
         for (int tb = 0; tb < 2; ++tb) {
             int64_t nref = 0, nne = 0, nce = 0;
@@ -949,6 +1271,8 @@ template <typename R> pd_status create_impl(const pd_params* p, const pd_config*
             for (int v : ss[tb]) nne += v < 0 || !(v & kGridExact);
             for (auto& b : bs[tb]) { nbs += 1; nbs2 += (b.slot_a >= 0 && (b.slot_a & kGridExact)) + (b.slot_b >= 0 && (b.slot_b & kGridExact)); }
             fprintf(stderr, "pdenv grid %d: %lld bisector sub-cells, %lld trusted sides\n", tb, (long long)nbs, (long long)nbs2);
+            if (cps[tb]) fprintf(stderr, "pdenv grid %d: %lld cell pieces (%.1f MB), %lld rejected, max error %.2e of sum |c phi|, built in %.2f s\n", tb,
+                                 (long long)cps[tb]->pieces, cps[tb]->rec.size() * 8e-6, (long long)cps[tb]->rejected, cps[tb]->max_rel, cps[tb]->build_s);
             fprintf(stderr, "pdenv grid %d: %d x %d cells, %lld refined, %lld non-exact cells, %lld of %zu sub-cells non-exact\n", tb,
                     gnm[tb], gna[tb], (long long)nref, (long long)nce, (long long)nne, ss[tb].size());
         }
@@ -1218,6 +1542,25 @@ pd_status step_n_impl(pd_env* e, const void* actions, int32_t n_steps, void* obs
 extern "C" {
 
 int pd_abi_version(void) { return PD_ABI_VERSION; }
+pd_status pd_cell_piece_info(const pd_params* p, int32_t table, int64_t piece, double* out, int32_t n_out) {
+    if (!p || !out || n_out < 16 || (table != 0 && table != 1)) return fail(PD_ERR_INVALID, "pd_cell_piece_info: bad arguments");
+    const pd_aero_table& t = table ? p->cl : p->cd;
+    if (t.n_pts < kNbr || t.n_pts > PD_MAX_PTS || t.n_cols != kCols) return fail(PD_ERR_INVALID, "pd_cell_piece_info: bad table");
+    int nm, na;
+    double a0, a1;
+    grid_geometry(table, nm, na, a0, a1);
+    const CellPieces& cp = cell_pieces(t, a0, a1, nm, na);
+    const double v[12] = {(double)cp.pieces, (double)cp.rejected, cp.max_rel, cp.build_s, (double)(cp.rec.size() / kCellStride),
+                          (double)nm, (double)na, a0, a1, (double)kCellDeg, (double)kCellExact, (double)kCellStride};
+    for (int k = 0; k < 16; ++k) out[k] = k < 12 ? v[k] : 0.0;
+    if (piece >= 0) {
+        if ((size_t)(piece + 1) * kCellStride > cp.rec.size() || n_out < 16 + kCellStride)
+            return fail(PD_ERR_INVALID, "pd_cell_piece_info: piece out of range or out too short");
+        std::memcpy(out + 16, cp.rec.data() + (size_t)piece * kCellStride, kCellStride * sizeof(double));
+    }
+    return PD_OK;
+}
+
 size_t pd_sizeof_params(void) { return sizeof(pd_params); }
 size_t pd_sizeof_config(void) { return sizeof(pd_config); }
 const char* pd_last_error(void) { return g_err.c_str(); }

@@ -86,8 +86,8 @@ EXPORTS = ["pd_abi_version", "pd_sizeof_params", "pd_sizeof_config", "pd_last_er
            "pd_set_gload_window", "pd_get_gload_window", "pd_set_wind_sigmas", "pd_get_wind_state",
            "pd_set_wind_state", "pd_get_counters", "pd_set_counters", "pd_checkpoint_size", "pd_checkpoint_save",
            "pd_checkpoint_load", "pd_counters", "pd_stats", "pd_count_work", "pd_atmosphere", "pd_obs_dim",
-           "pd_action_dim", "pd_step_sac", "pd_pso_swarm_minima", "pd_pso_update_bests"]
-ABI_VERSION = 5
+           "pd_action_dim", "pd_step_sac", "pd_pso_swarm_minima", "pd_pso_update_bests", "pd_cell_piece_info"]
+ABI_VERSION = 6
 
 _lib = None
 
@@ -134,6 +134,7 @@ def load(path=None):
     L.pd_counters.argtypes = [vp, P(I64), P(I64), P(I64), P(I64)]
     L.pd_stats.argtypes = [vp, P(I64), I32]
     L.pd_count_work.argtypes = [vp, I32]
+    L.pd_cell_piece_info.argtypes = [P(PdParams), I32, I64, P(C.c_double), I32]
     L.pd_atmosphere.argtypes = [vp, vp, vp, I64, vp]
     L.pd_get_gload_window.argtypes = [vp, vp, vp, vp, vp, vp]
     L.pd_get_wind_state.argtypes = [vp, vp, vp, vp, vp]
@@ -151,7 +152,7 @@ def load(path=None):
                  "pd_set_wind_sigmas", "pd_set_gload_window", "pd_counters", "pd_stats", "pd_count_work",
                  "pd_get_gload_window",
                  "pd_get_wind_state", "pd_set_wind_state", "pd_get_counters", "pd_set_counters",
-                 "pd_checkpoint_save", "pd_checkpoint_load", "pd_atmosphere"):
+                 "pd_checkpoint_save", "pd_checkpoint_load", "pd_atmosphere", "pd_cell_piece_info"):
         getattr(L, name).restype = C.c_int
     L.pd_sizeof_params.restype = C.c_size_t
     L.pd_sizeof_config.restype = C.c_size_t

@@ -391,7 +391,8 @@ class PoweredDescentEnv:
         L.check(self.lib.pd_count_work(self.h, int(bool(enable))))
 
     WORK_COUNTERS = ("gust_substeps", "resets", "q_line", "q_verified", "q_taylor", "q_balanced", "q_miss",
-                     "balanced_rounds", "q_refined", "q_bisect", "wave_substeps_refined", "wave_substeps_bisect")
+                     "balanced_rounds", "q_refined", "q_bisect", "wave_substeps_refined", "wave_substeps_bisect",
+                     "q_cell")
 
     def stats(self):
         """Device statistics words (pd_stats): misses, NaN events, table entries, dropped queue

@@ -6,6 +6,8 @@ Tolerances (fp64 handle): teacher-forced single env-step <= 1e-10 relative per c
 per-channel range; the attitude channels are chaotic).  fp32 handle:
 teacher-forced <= 1e-4 relative on non-attitude channels.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -143,8 +145,14 @@ def test_device_solve_bit_identical(pd, precision, lpe):
     A = torch.rand(T, N, 1, device="cuda", generator=g) * 2 - 1
     kw = dict(precision=precision, lanes_per_env=lpe, enable_wind=True, stochastic_wind=True,
               wind_percentile=None, auto_reset=True, tilt_sigma_rad=0.02, seed=9)
-    full = make(pd, N, **kw)
-    cut = make(pd, N, params=pd.Params().restrict_keys(4, 4), **kw)
+    # payload sums only: with cell pieces (binary64, the default) interior queries of both handles
+    # would take the pieces whatever the tables hold
+    os.environ["PDENV_CELL_PIECES"] = "0"
+    try:
+        full = make(pd, N, **kw)
+        cut = make(pd, N, params=pd.Params().restrict_keys(4, 4), **kw)
+    finally:
+        del os.environ["PDENV_CELL_PIECES"]
     for t in range(T):
         o1, r1, d1, *_ = full.step(A[t])
         o2, r2, d2, *_ = cut.step(A[t])
@@ -152,6 +160,42 @@ def test_device_solve_bit_identical(pd, precision, lpe):
     assert torch.equal(full.state, cut.state)
     assert cut.counters()["rbf_misses"] > 100
     assert full.counters()["rbf_misses"] < cut.counters()["rbf_misses"]
+
+
+def test_cell_pieces_match_payload_sums(pd):
+    """Binary64 handles evaluate trusted interior queries from cell pieces: the
+    same first steps with the pieces (default) and with the payload sums only
+    (PDENV_CELL_PIECES=0) from the same seeded states, |alpha| mostly inside the interior band
+    (pitch tilt sigma 0.002 rad): C_D and C_L agree to rounding (1e-12 relative) on the first
+    step, the states to the per-step tolerance after it; the counting launches report the piece
+    path taken."""
+    import torch
+    N, T = 8192, 6
+    g = torch.Generator(device="cuda").manual_seed(21)
+    A = torch.rand(T, N, 1, device="cuda", generator=g) * 0.5 + 0.5
+    kw = dict(lanes_per_env=2, enable_wind=False, auto_reset=False, tilt_sigma_rad=0.002, seed=5)
+    pc = make(pd, N, **kw)
+    os.environ["PDENV_CELL_PIECES"] = "0"
+    try:
+        ps = make(pd, N, **kw)
+    finally:
+        del os.environ["PDENV_CELL_PIECES"]
+    pc.count_work(True)
+    for t in range(T):
+        _, r1, _, _, x1 = pc.step(A[t], info=True)
+        _, r2, _, _, x2 = ps.step(A[t], info=True)
+        # the first step from identical states: the coefficients to rounding; later steps start
+        # from states that differ by that rounding (the per-step tolerances of s3)
+        for k in ("CD", "CL"):
+            d = (x1[k] - x2[k]).abs() / x2[k].abs().clamp_min(1e-3)
+            assert float(d.max()) <= (1e-12 if t == 0 else 1e-9), (t, k, float(d.max()))
+        ds = (pc.state - ps.state).abs() / ps.state.abs().clamp_min(1e-3)
+        assert float(ds.max()) <= 1e-9, (t, float(ds.max()))
+    st = pc.stats()
+    interior = 2 * 4 * N * T - st["q_line"]        # 2 tables x 4 sub-steps per env step
+    assert interior > 0.1 * 2 * 4 * N * T, st
+    assert st["q_cell"] >= 0.99 * interior - st["q_verified"], st   # every trusted interior query
+    assert ps.stats()["q_cell"] == 0
 
 
 def test_env_shards_equal_single_handle(pd):
