@@ -6,8 +6,8 @@ landing_burn_pure_throttle with the SAC driver's reward (rtd_rl), the horizontal
 profile + von Karman gusts (percentile drawn per reset, as WindModel(given_percentile=None)),
 initial pitch perturbation N(0, 1 deg), synthetic uniform float32 random actions resident in
 HBM, auto-reset on done/truncated.  One timed "step" = one env.step() of all envs (4 physics
-sub-steps + g-load window + truncated/done/reward + obs written per step); by default 16
-consecutive steps run in one k_step launch (pd_step_n, --fuse 16), --fuse 1 launches per step.
+sub-steps + g-load window + truncated/done/reward + obs written per step); by default 128
+consecutive steps run in one k_step launch (pd_step_n, --fuse 128), --fuse 1 launches per step.
 
 Multi-GPU: one process per GPU (torchrun), each rank steps its own contiguous env shard
 (env_offset = rank * N); the env batch shards with no data-path collective, so scaling is
@@ -415,7 +415,7 @@ def main():
     ap.add_argument("--integrator", choices=["reference", "rk4"], default="reference",
                     help="rk4: BASELINE c2's RK4 dt=0.01 s, NOT the reference's integrator (non-parity)")
     ap.add_argument("--particles", type=int, default=32768, help="c4: particles per GPU")
-    ap.add_argument("--fuse", type=int, default=64,
+    ap.add_argument("--fuse", type=int, default=128,
                     help="c3: env-steps per k_step launch (pd_step_n; 1 = one pd_step launch per step)")
     ap.add_argument("--graph", type=int, default=1, help="c5: replay the collection step as a HIP graph")
     ap.add_argument("--others", type=int, default=1,

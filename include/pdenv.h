@@ -202,7 +202,7 @@ pd_status pd_step(pd_env* env, const void* actions, void* obs, void* reward, uin
  * phases: obs [n_steps][N][O], reward [n_steps][N], done/truncated/trunc_id [n_steps][N] receive
  * every step's outputs (any may be NULL).  Replaces a Python loop over
  * rocket_environment_pre_wrap.step (base_environment.py:99-154) with fused launches: each launch
- * runs up to 64 steps (PDENV_FUSE, 1..256) of every env in one kernel, so the LDS table staging and the
+ * runs up to 128 steps (PDENV_FUSE, 1..256) of every env in one kernel, so the LDS table staging and the
  * launch tail are paid once per launch, followed by the miss flush.  Results are bit-identical
  * to n_steps pd_step calls.  No host synchronisation. */
 pd_status pd_step_n(pd_env* env, const void* actions, int32_t n_steps, void* obs, void* reward, uint8_t* done,

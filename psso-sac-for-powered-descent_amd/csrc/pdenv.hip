@@ -1509,7 +1509,8 @@ int policy_fuse() {
 // device is re-solved at most this many steps before it is in the tables (PDENV_FUSE overrides).
 int fuse_chunk() {
     const char* s = getenv("PDENV_FUSE");
-    int k = s && *s ? atoi(s) : 64;   // (c3 ms per env-step, rocm 7.2: 16 -> 0.0450, 32 -> 0.0442, 64 -> 0.0421)
+    int k = s && *s ? atoi(s) : 128;   // (c3 ms per env-step, payload sums: 16 -> 0.0450, 32 -> 0.0442, 64 -> 0.0421;
+                                       //  cell pieces: 64 -> 0.0341, 128 -> 0.0335, 256 -> 0.0337)
     return k < 1 ? 1 : (k > 256 ? 256 : k);
 }
 
