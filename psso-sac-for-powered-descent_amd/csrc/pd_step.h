@@ -29,9 +29,15 @@ constexpr int kGridPiece = 1 << 27;   // grid_slot flag (exact cells of binary64
 // its kCellExact terms nearest to the cell (pdenv.hip build_cell_pieces).  Record: the
 // coefficients row by row (u^i, i = kCellDeg .. 0; within a row v^j, j = kCellDeg - i .. 0), then
 // per exact term (Mach, coefficient / 8, AoA), padded to 16 bytes.
-constexpr int kCellDeg = 8;
+#ifndef PD_CELL_DEG
+#define PD_CELL_DEG 8
+#endif
+#ifndef PD_CELL_EXACT
+#define PD_CELL_EXACT 4
+#endif
+constexpr int kCellDeg = PD_CELL_DEG;
 constexpr int kCellCoef = (kCellDeg + 1) * (kCellDeg + 2) / 2;
-constexpr int kCellExact = 4;
+constexpr int kCellExact = PD_CELL_EXACT;
 constexpr int kCellStride = (kCellCoef + 3 * kCellExact + 1) & ~1;
 
 // A sub-cell holding two 50-NN regions A, B whose keys differ by one point swap (p in A, q in B):

@@ -84,12 +84,13 @@ if __name__ == "__main__":
     build(force="--force" in sys.argv)
 
 
-def build_variant(name, defines, unit=(0, 0, 1), patch=None):
+def build_variant(name, defines, unit=(0, 0, 1), patch=None, host=False):
     """Experiments: libpdenv_<name>.so with the step-kernel object of `unit` (precision, phase
     family, wind; default the c3 one) compiled with extra `defines` -- and, given `patch` (a
     unified diff against csrc/, e.g. tools/experiments/*.patch), from a patched copy of the
     sources, so that experiments stay out of the product source -- the other objects shared with
-    the main build (which must be current).  Returns the library path."""
+    the main build (which must be current); host=True also compiles the host unit (pdenv.hip)
+    with them.  Returns the library path."""
     import shutil
     import tempfile
     build(verbose=False)
@@ -107,12 +108,16 @@ def build_variant(name, defines, unit=(0, 0, 1), patch=None):
         subprocess.run(["patch", "-s", "-t", "-p2", "-d", os.path.join(tmp, "p", "csrc"), "-i", os.path.abspath(patch)],
                        check=True)
         src = os.path.join(tmp, "p", "csrc", "kstep.hip")
+    hobj = os.path.join(odir, "pdenv.o")
     try:
         _compile((obj, src, [f"-DPD_KR={r}", f"-DPD_KPH={ph}", f"-DPD_KW={w}"] + list(defines)), False)
+        if host:
+            _compile((hobj, os.path.join(os.path.dirname(src), "pdenv.hip"), list(defines)), False)
     finally:
         if tmp:
             shutil.rmtree(tmp, ignore_errors=True)
     out = os.path.join(PKG, f"libpdenv_{name}.so")
-    objs = [obj if os.path.basename(u[0]) == os.path.basename(obj) else u[0] for u in units()]
+    objs = [obj if os.path.basename(u[0]) == os.path.basename(obj) else
+            (hobj if host and os.path.basename(u[0]) == "pdenv.o" else u[0]) for u in units()]
     subprocess.run([HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", out] + objs, check=True)
     return out
