@@ -106,6 +106,7 @@ template <typename R> struct DevParams {
     // cell's piece at its cell index, a refined cell's at sub_piece[sub-cell] (-1: none)
     const double* cell_pc[2];
     const int* sub_piece[2];
+    const uint32_t* fine[2];           // fine index (pd_step.h kFinePiece; nullptr: none)
     R line_bp[4][kLineMax];
     int line_slot[4][kLineMax + 1];
     unsigned long long line_key[4][kLineMax + 1];

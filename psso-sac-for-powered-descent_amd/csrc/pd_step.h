@@ -23,12 +23,20 @@ constexpr int kGridExact = 1 << 30;   // grid_slot flag: every point of the cell
 constexpr int kGridRefine = 1 << 29;  // grid_slot flag: the cell is refined, low bits = its sub-grid
 constexpr int kGridBisect = 1 << 28;  // sub_slot flag: two regions split by one bisector, low bits = its record
 constexpr int kGridPiece = 1 << 27;   // grid_slot flag (exact cells of binary64 handles): the cell has its cell piece
+// Fine index (binary64 handles with cell pieces): one word per sub-cell of every cell (kGridSub x
+// kGridSub per cell, Mach-major over the whole grid), read in place of the cell record: a piece
+// the sub-cell's points all use, or the bisector record splitting it; 0: the cell/sub-cell records
+constexpr uint32_t kFinePiece = 1u << 30;
+constexpr uint32_t kFineBisect = 1u << 29;
+constexpr uint32_t kFineRefined = 1u << 28;    // (the sub-cell belongs to a refined cell: workload counters)
+constexpr uint32_t kFineIndex = kFineRefined - 1u;
 
 // Cell pieces (binary64 handles): the thin-plate sum of one neighbourhood over one interior grid
 // cell as a polynomial of total degree kCellDeg in the cell coordinates (u, v) in [-1, 1]^2 plus
 // its kCellExact terms nearest to the cell (pdenv.hip build_cell_pieces).  Record: the
 // coefficients row by row (u^i, i = kCellDeg .. 0; within a row v^j, j = kCellDeg - i .. 0), then
-// per exact term (Mach, coefficient / 8, AoA), padded to 16 bytes.
+// per exact term (Mach, coefficient / 8, AoA), then the neighbourhood's key (its bits), padded to 16
+// bytes.
 #ifndef PD_CELL_DEG
 #define PD_CELL_DEG 8
 #endif
@@ -38,7 +46,8 @@ constexpr int kGridPiece = 1 << 27;   // grid_slot flag (exact cells of binary64
 constexpr int kCellDeg = PD_CELL_DEG;
 constexpr int kCellCoef = (kCellDeg + 1) * (kCellDeg + 2) / 2;
 constexpr int kCellExact = PD_CELL_EXACT;
-constexpr int kCellStride = (kCellCoef + 3 * kCellExact + 1) & ~1;
+constexpr int kCellKey = kCellCoef + 3 * kCellExact;
+constexpr int kCellStride = (kCellKey + 2) & ~1;
 
 // A sub-cell holding two 50-NN regions A, B whose keys differ by one point swap (p in A, q in B):
 // s(x) = n . x - c < 0 on A's side (p nearer than q).  Each side's slot carries kGridExact only if

@@ -65,6 +65,7 @@ template <typename R> struct TabView {
     const PD_AS1 GridBisect* sub_bis;
     const PD_AS1 double* cell_pc;   // cell pieces (binary64 handles; nullptr: none)
     const PD_AS1 int* sub_piece;
+    const PD_AS1 uint32_t* fine;    // fine index (nullptr: none)
     int grid_nm, grid_na;
     R grid_a0, grid_inv_da, grid_inv_dm;
 };
@@ -406,8 +407,9 @@ __device__ __forceinline__ R rbf_miss_wave(const AT& a, DP<R>& P, int table, con
 // A query's Taylor piece on a clamped line (rbf2): its record index and cell, piece < 0: none
 // (line, verify, refined, bisect: the query was on a clamped line / its candidate was verified /
 // it read a refined cell's sub-cell / a bisector record -- for the workload counters).  cp: a
-// trusted interior query's cell piece (-1 none), cu, cv: its position in the cell, [0, 1)
-struct TayRef { int piece, cell; bool line, verify, refined, bisect; int cp; double cu, cv; };
+// trusted interior query's cell piece (-1 none), cu, cv: its position in the cell, [0, 1); fine:
+// the piece came from the fine index (the cached key is then the piece's)
+struct TayRef { int piece, cell; bool line, verify, refined, bisect; int cp; double cu, cv; bool fine; };
 
 struct NoPre { __device__ void operator()() const {} };
 
@@ -435,15 +437,30 @@ __device__ __forceinline__ int rbf_lookup(const AT& a, DP<R>& P, int table, cons
     int gsl0 = -1, gcell = 0;
     R um = R(0), ua = R(0);
     const bool use_grid = t.grid_key != nullptr;
+    // binary64 handles with cell pieces read the query's sub-cell word of the fine index instead
+    // of the cell record: one dependent load to the piece (or its bisector record) for refined
+    // cells too; the cell / sub-cell records only when it does not settle the query
+    const bool fine_path = sizeof(R) == 8 && tay != nullptr && t.fine != nullptr;
+    uint32_t fe = 0u;
+    R fsm = R(0), fsa = R(0);
     if (use_grid) {
         R fm = M * t.grid_inv_dm, fa = (aq - t.grid_a0) * t.grid_inv_da;
         int im = fm < R(0) ? 0 : (fm >= R(t.grid_nm) ? t.grid_nm - 1 : (int)fm);
         int ia = fa < R(0) ? 0 : (fa >= R(t.grid_na) ? t.grid_na - 1 : (int)fa);
         if (!(fm == fm) || !(fa == fa)) { im = 0; ia = 0; }   // NaN queries
         gcell = im * t.grid_na + ia;
-        gkey = t.grid_key[gcell];
-        gsl0 = t.grid_slot[gcell];
         um = fm - (R)im; ua = fa - (R)ia;     // position in the cell, [0, 1)
+        if (fine_path) {
+            const R sm = um * R(kGridSub), sa = ua * R(kGridSub);
+            int jm = (int)sm, ja = (int)sa;
+            jm = jm < 0 ? 0 : (jm > kGridSub - 1 ? kGridSub - 1 : jm);
+            ja = ja < 0 ? 0 : (ja > kGridSub - 1 ? kGridSub - 1 : ja);
+            fe = t.fine[(uint32_t)(im * kGridSub + jm) * (uint32_t)(t.grid_na * kGridSub) + (uint32_t)(ia * kGridSub + ja)];
+            fsm = sm - (R)jm; fsa = sa - (R)ja;
+        } else {
+            gkey = t.grid_key[gcell];
+            gsl0 = t.grid_slot[gcell];
+        }
     }
     pre();
     if (on_line) {
@@ -473,6 +490,32 @@ __device__ __forceinline__ int rbf_lookup(const AT& a, DP<R>& P, int table, cons
         }
         PD_LST(0);
     } else if (use_grid) {
+        bool fast = false;
+        if (fine_path) {
+            // a piece every point of the sub-cell uses (the margin keeps queries on a sub-cell
+            // edge on the record path), or the side of its bisector, trusted off the line
+            const R eps = R(1e-9);
+            const bool inside = fsm > eps && R(1) - fsm > eps && fsa > eps && R(1) - fsa > eps;
+            int cpf = -1;
+            if (fe & kFinePiece) cpf = (int)(fe & kFineIndex);
+            else if (fe & kFineBisect) {
+                const PD_AS1 GridBisect& b = t.sub_bis[fe & kFineIndex];
+                const double sv = fma(b.nx, (double)M, fma(b.ny, (double)aq, -b.c));
+                const int side = sv < 0.0 ? b.piece_a : b.piece_b;
+                if (fabs(sv) > 3.0 * b.tau) cpf = side;
+            }
+            if (inside && cpf >= 0) {
+                fast = true;
+                trusted = true;
+                cslot = -1;
+                tay->cp = cpf; tay->cu = (double)um; tay->cv = (double)ua; tay->fine = true;
+                tay->refined = (fe & kFineRefined) != 0u; tay->bisect = (fe & kFineBisect) != 0u;
+            } else {
+                gkey = t.grid_key[gcell];
+                gsl0 = t.grid_slot[gcell];
+            }
+        }
+        if (!fast) {
         ckey = gkey;
         int gsl = gsl0;
         // the cell piece (LPE 2 binary64 handles): an exact cell's own, else its sub-cell's
@@ -513,6 +556,7 @@ __device__ __forceinline__ int rbf_lookup(const AT& a, DP<R>& P, int table, cons
         const R eps = sizeof(R) == 8 ? R(1e-9) : R(1e-4);
         trusted = gsl >= 0 && (gsl & kGridExact) && um > eps && R(1) - um > eps && ua > eps && R(1) - ua > eps;
         if (pieces && trusted && cpc >= 0) { tay->cp = cpc; tay->cu = (double)cu; tay->cv = (double)cv; }
+        }
     }
     PD_LST(1);
     unsigned long long key = ckey;
@@ -527,7 +571,7 @@ __device__ __forceinline__ int rbf_lookup(const AT& a, DP<R>& P, int table, cons
         slot = key == ckey ? cslot : -1;
     }
     PD_LST(2);
-    if (slot < 0) {
+    if (slot < 0 && !(tay != nullptr && tay->fine)) {   // (a fine-index piece needs no slot)
         uint32_t mask = (1u << t.logcap) - 1u;
         uint32_t h = key_hash(key, t.logcap);
         for (uint32_t probe = 0; probe <= mask; ++probe) {
@@ -733,7 +777,7 @@ __device__ __forceinline__ R rbf2(const AT& a, DP<R>& P, int table, const TabVie
 #ifdef PD_STAMP
     const unsigned long long s0 = __builtin_amdgcn_s_memtime();
 #endif
-    TayRef tr{-1, 0, false, false, false, false, -1, 0.0, 0.0};
+    TayRef tr{-1, 0, false, false, false, false, -1, 0.0, 0.0, false};
     const int slot = rbf_lookup<R>(a, P, table, t, ln, cache, M, aq, &tr, stamp ? stamp + 2 : nullptr, pre);
 #ifdef PD_STAMP
     const unsigned long long s1 = __builtin_amdgcn_s_memtime();
@@ -748,7 +792,11 @@ __device__ __forceinline__ R rbf2(const AT& a, DP<R>& P, int table, const TabVie
         // with cell pieces the payload sums are rare (verified queries): the pieces first, then
         // the balanced sums of the lanes left, if any
         if (tay) vt = taylor_eval<R>(gbl(P.tay) + (size_t)tr.piece * kTayStride, M, tr.cell);
-        if (cel) vt = cell_eval(t.cell_pc + (size_t)tr.cp * kCellStride, M, aq, tr.cu, tr.cv);
+        if (cel) {
+            const PD_AS1 double* rec = t.cell_pc + (size_t)tr.cp * kCellStride;
+            vt = cell_eval(rec, M, aq, tr.cu, tr.cv);
+            if (tr.fine) cache.key = *(const PD_AS1 unsigned long long*)(rec + kCellKey);
+        }
         vb = rbf_balanced<R>(P, B, tab, full, table, slot, M, aq, []() {});
     } else {
         vb = rbf_balanced<R>(P, B, tab, full, table, slot, M, aq, [&]() {
@@ -915,6 +963,7 @@ __device__ __forceinline__ TabView<R> tab_view(DP<R>& P, const R* tab, int table
     t.sub_bis = gbl((const GridBisect*)P.sub_bis[table]);
     t.cell_pc = gbl(P.cell_pc[table]);
     t.sub_piece = gbl(P.sub_piece[table]);
+    t.fine = gbl(P.fine[table]);
     t.grid_nm = P.grid_nm[table];
     t.grid_na = P.grid_na[table];
     t.grid_a0 = P.grid_a0[table];

@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -632,6 +633,7 @@ void grid_geometry(int tb, int& nm, int& na, double& a0, double& a1) {
 
 struct CellPieces;
 bool cell_ok(const CellPieces* cp, int64_t cell);
+bool fine_is(const CellPieces* cp, int im, int ia, int jm, int ja, int na, uint32_t want);
 int cell_bis(const CellPieces* cp, int bi, bool side_b);
 
 template <typename R>
@@ -677,6 +679,9 @@ pd_status build_grid(const pd_aero_table& t, double a0, double a1, int nm, int n
                     b.slot_a = sa < 0 ? -1 : (sa | (h.ok_a ? kGridExact : 0));
                     b.slot_b = sb < 0 ? -1 : (sb | (h.ok_b ? kGridExact : 0));
                     b.piece_a = cell_bis(cp, bi, false); b.piece_b = cell_bis(cp, bi, true);
+                    if (cp && !fine_is(cp, g.refined[r] / na, g.refined[r] % na, jm, ja, na,
+                                       kFineBisect | kFineRefined | (uint32_t)bs.size()))
+                        return fail(PD_ERR_INVALID, "cell pieces: fine index does not match the bisector records");
                     ss[q] = kGridBisect | (int)bs.size();
                     bs.push_back(b);
                 }
@@ -707,6 +712,7 @@ struct CellPieces {
     std::vector<uint8_t> cell_ok;     // [nm na] the exact cell's own piece is valid
     std::vector<int> sub_piece;       // [refined][S][S] piece of an exact sub-cell's key (-1 none)
     std::vector<int> bis_a, bis_b;    // per GridKeys bisector record: each trusted side's piece
+    std::vector<uint32_t> fine;       // [nm S][na S] fine index (pd_step.h kFinePiece)
     double max_rel = 0, build_s = 0;
     int64_t pieces = 0, rejected = 0;
 };
@@ -936,7 +942,10 @@ const CellPieces& cell_pieces(const pd_aero_table& t, double a0, double a1, int 
     parallel_for((int64_t)job.size(), [&](int64_t p) {
         const int c = job[p].first;
         if (p < ncell && refined[c]) { err[p] = INFINITY; return; }   // (a refined cell's own index: unused)
-        err[p] = make_cell_piece(terms[kidx.at(job[p].second)], c / na, c % na, dm, da, a0, cp.rec.data() + (size_t)p * kCellStride);
+        double* rec = cp.rec.data() + (size_t)p * kCellStride;
+        err[p] = make_cell_piece(terms[kidx.at(job[p].second)], c / na, c % na, dm, da, a0, rec);
+        const uint64_t key = job[p].second;
+        std::memcpy(rec + kCellKey, &key, 8);
     });
     auto valid = [&](int p) { return p >= 0 && err[p] <= kCellTol; };
     cp.cell_ok.assign(ncell, 0);
@@ -950,32 +959,75 @@ const CellPieces& cell_pieces(const pd_aero_table& t, double a0, double a1, int 
         if (err[p] <= kCellTol) cp.max_rel = std::max(cp.max_rel, err[p]);
         else ++cp.rejected;
     }
+    // the fine index: per sub-cell of every cell the piece all its points use, or the bisector
+    // record splitting it (numbered as build_grid numbers them: refined cells, then sub-cells in
+    // order, every non-exact sub-cell with a bisector)
+    {
+        std::vector<int> ridx(ncell, -1);
+        for (int64_t r = 0; r < nr; ++r) ridx[g.refined[r]] = (int)r;
+        std::vector<int64_t> bs_of((size_t)nr * S * S, -1);
+        int64_t nbs = 0;
+        for (int64_t r = 0; r < nr; ++r)
+            for (int q = 0; q < S * S; ++q) {
+                const size_t sq = (size_t)r * S * S + q;
+                const int jm = q / S, ja = q % S;
+                bool exact = true;
+                for (int c = 0; c < 4 && exact; ++c)
+                    exact = g.sub_corner[((size_t)r * (S + 1) + jm + (c >> 1)) * (S + 1) + ja + (c & 1)] == g.sub_centre[sq];
+                if (!exact && g.sub_bis[sq] >= 0 && nbs < (int64_t)kGridBisect) bs_of[sq] = nbs++;
+            }
+        cp.fine.assign((size_t)nm * S * na * S, 0u);
+        parallel_for(nm, [&](int64_t im) {
+            for (int ia = 0; ia < na; ++ia) {
+                const int64_t c = im * na + ia;
+                for (int jm = 0; jm < S; ++jm)
+                    for (int ja = 0; ja < S; ++ja) {
+                        uint32_t e = 0u;
+                        if (!refined[c]) {
+                            if (cp.cell_ok[c]) e = kFinePiece | (uint32_t)c;
+                        } else {
+                            const size_t sq = (size_t)ridx[c] * S * S + jm * S + ja;
+                            if (cp.sub_piece[sq] >= 0) e = kFinePiece | kFineRefined | (uint32_t)cp.sub_piece[sq];
+                            else if (bs_of[sq] >= 0) e = kFineBisect | kFineRefined | (uint32_t)bs_of[sq];
+                        }
+                        cp.fine[(size_t)(im * S + jm) * ((size_t)na * S) + (size_t)ia * S + ja] = e;
+                    }
+            }
+        });
+    }
     cp.build_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     return cp;
 }
 bool cell_ok(const CellPieces* cp, int64_t cell) { return cp != nullptr && cp->cell_ok[cell]; }
+bool fine_is(const CellPieces* cp, int im, int ia, int jm, int ja, int na, uint32_t want) {
+    const int S = kGridSub;
+    return cp->fine[(size_t)(im * S + jm) * ((size_t)na * S) + (size_t)ia * S + ja] == want;
+}
 int cell_bis(const CellPieces* cp, int bi, bool side_b) { return cp == nullptr ? -1 : (side_b ? cp->bis_b[bi] : cp->bis_a[bi]); }
 
 // The device copy of a table's cell pieces: one per device and process, shared read-only by the
 // handles (never freed; ~0.2 GB of the 288 GB)
-pd_status cell_pieces_device(const CellPieces& cp, const double** rec, const int** sub) {
+pd_status cell_pieces_device(const CellPieces& cp, const double** rec, const int** sub, const uint32_t** fine) {
     static std::mutex mu;
-    static std::map<std::pair<const void*, int>, std::pair<void*, void*>> m;
+    static std::map<std::pair<const void*, int>, std::array<void*, 3>> m;
     int dev = 0;
     PD_HIP(hipGetDevice(&dev));
     std::lock_guard<std::mutex> lock(mu);
     auto k = std::make_pair((const void*)&cp, dev);
     auto it = m.find(k);
     if (it == m.end()) {
-        void *dr = nullptr, *ds = nullptr;
+        void *dr = nullptr, *ds = nullptr, *df = nullptr;
         PD_HIP(hipMalloc(&dr, std::max<size_t>(cp.rec.size(), 1) * 8));
         PD_HIP(hipMalloc(&ds, std::max<size_t>(cp.sub_piece.size(), 1) * 4));
+        PD_HIP(hipMalloc(&df, std::max<size_t>(cp.fine.size(), 1) * 4));
         if (!cp.rec.empty()) PD_HIP(hipMemcpy(dr, cp.rec.data(), cp.rec.size() * 8, hipMemcpyHostToDevice));
         if (!cp.sub_piece.empty()) PD_HIP(hipMemcpy(ds, cp.sub_piece.data(), cp.sub_piece.size() * 4, hipMemcpyHostToDevice));
-        it = m.emplace(k, std::make_pair(dr, ds)).first;
+        if (!cp.fine.empty()) PD_HIP(hipMemcpy(df, cp.fine.data(), cp.fine.size() * 4, hipMemcpyHostToDevice));
+        it = m.emplace(k, std::array<void*, 3>{dr, ds, df}).first;
     }
-    *rec = (const double*)it->second.first;
-    *sub = (const int*)it->second.second;
+    *rec = (const double*)it->second[0];
+    *sub = (const int*)it->second[1];
+    *fine = (const uint32_t*)it->second[2];
     return PD_OK;
 }
 
@@ -1250,7 +1302,9 @@ template <typename R> pd_status create_impl(const pd_params* p, const pd_config*
     int gnm[2], gna[2];
     double ga0[2], ga1[2];
     for (int tb = 0; tb < 2; ++tb) grid_geometry(tb, gnm[tb], gna[tb], ga0[tb], ga1[tb]);
-    // cell pieces for the binary64 handle's interior queries (PDENV_CELL_PIECES=0: payload sums only)
+    // cell pieces for the binary64 handle's interior queries (PDENV_CELL_PIECES=0: payload sums
+    // only).  The binary32 handle keeps its balanced binary32 sums: measured with the pieces of its
+    // exact cells (evaluated in binary64), c3 took 0.0426 ms per env-step against 0.0400
     const CellPieces* cps[2] = {nullptr, nullptr};
     const char* cpe = getenv("PDENV_CELL_PIECES");
     if (sizeof(R) == 8 && !(cpe && cpe[0] == '0')) {
@@ -1259,9 +1313,12 @@ template <typename R> pd_status create_impl(const pd_params* p, const pd_config*
     }
     if ((st = build_grid<R>(p->cd, ga0[0], ga1[0], gnm[0], gna[0], tcd, gk[0], gs[0], sk[0], ss[0], bs[0], cps[0])) != PD_OK) return st;
     if ((st = build_grid<R>(p->cl, ga0[1], ga1[1], gnm[1], gna[1], tcl, gk[1], gs[1], sk[1], ss[1], bs[1], cps[1])) != PD_OK) return st;
+    // the fine index (PDENV_FINE=0: cell and sub-cell records only)
+    const char* fne = getenv("PDENV_FINE");
     for (int tb = 0; tb < 2; ++tb) {
-        D.cell_pc[tb] = nullptr; D.sub_piece[tb] = nullptr;
-        if (cps[tb] && (st = cell_pieces_device(*cps[tb], &D.cell_pc[tb], &D.sub_piece[tb])) != PD_OK) return st;
+        D.cell_pc[tb] = nullptr; D.sub_piece[tb] = nullptr; D.fine[tb] = nullptr;
+        if (cps[tb] && (st = cell_pieces_device(*cps[tb], &D.cell_pc[tb], &D.sub_piece[tb], &D.fine[tb])) != PD_OK) return st;
+        if (fne && fne[0] == '0') D.fine[tb] = nullptr;
     }
     if (getenv("PDENV_TAY_DEBUG"))
         for (int tb = 0; tb < 2; ++tb) {

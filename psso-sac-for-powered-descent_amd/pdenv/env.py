@@ -222,7 +222,7 @@ class PoweredDescentEnv:
 
     def step_n(self, actions, outputs=True):
         """T consecutive env-steps over device-resident actions [T, N, A] (pd_step_n: fused
-        launches of up to 16 steps each, then the miss flush), the same results as T step()
+        launches of up to 128 steps each, then the miss flush), the same results as T step()
         calls.  Landing-burn phases only.  outputs=True returns per-step
         (obs [T, N, O], reward [T, N], done [T, N], truncated [T, N], trunc_id [T, N]);
         outputs=False writes nothing per step and returns None."""

@@ -198,6 +198,32 @@ def test_cell_pieces_match_payload_sums(pd):
     assert ps.stats()["q_cell"] == 0
 
 
+def test_fine_index_bit_identical(pd):
+    """The fine index (one word per sub-cell naming the piece or bisector that settles the query,
+    read in place of the cell record) picks the same piece as the cell / sub-cell records, so
+    with and without it (PDENV_FINE=0) the c3 workload -- wind, gusts below 15 km, tilt,
+    auto-reset -- is bit-identical over 2 fused launches of 64 steps."""
+    import torch
+    N, T = 16384, 128
+    g = torch.Generator(device="cuda").manual_seed(31)
+    A = torch.rand(T, N, 1, device="cuda", generator=g) * 2 - 1
+    A[:, : 3 * N // 4] = A[:, : 3 * N // 4] * 0.25 + 0.75      # 3/4 of the envs fly high throttle
+    kw = dict(lanes_per_env=2, enable_wind=True, stochastic_wind=True, wind_percentile=None,
+              auto_reset=True, tilt_sigma_rad=0.02, seed=13)
+    fine = make(pd, N, **kw)
+    os.environ["PDENV_FINE"] = "0"
+    try:
+        rec = make(pd, N, **kw)
+    finally:
+        del os.environ["PDENV_FINE"]
+    for t0 in range(0, T, 64):
+        o1 = fine.step_n(A[t0:t0 + 64])
+        o2 = rec.step_n(A[t0:t0 + 64])
+        for x, y in zip(o1, o2):
+            assert torch.equal(x, y), t0
+    assert torch.equal(fine.state, rec.state)
+
+
 def test_env_shards_equal_single_handle(pd):
     """Multi-GPU layout on one device: two handles over contiguous shards (env_offset = rank*n,
     as bench.py assigns them) reproduce the single N-env handle bit for bit, wind + tilt +

@@ -20,7 +20,8 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(REPO, "gpurun_out")
 PROF = os.path.join(REPO, "profiles")
 TAG = sys.argv[1] if len(sys.argv) > 1 else "r03"
-LAUNCHES = int(os.environ.get("LAUNCHES", "4"))
+LAUNCHES = int(os.environ.get("LAUNCHES", "3"))
+FUSE = int(os.environ.get("FUSE", "128"))
 
 
 def timed_dispatch_means(path):
@@ -39,15 +40,15 @@ def timed_dispatch_means(path):
 def pmc_summary(wl):
     d = {}
     for p in (1, 2, 3, 4):
-        f = os.path.join(OUT, f"pmc64_{wl}_p{p}", "run_counter_collection.csv")
+        f = os.path.join(OUT, f"pmcF_{wl}_p{p}", "run_counter_collection.csv")
         if os.path.exists(f):
             m, n = timed_dispatch_means(f)
             d.update(m)
             d["launches_averaged"] = n
     if not d:
         return None
-    s = {"env_steps_per_launch": 64, "source": f"tools/pmc_r03b.sh (rocprofv3 --pmc, one counter set per run) over "
-                                              f"tools/time_fused.py {'DESCENT=1 ' if wl == 'desc' else ''}FUSE=64; means "
+    s = {"env_steps_per_launch": FUSE, "source": f"tools/pmc_r03b.sh (rocprofv3 --pmc, one counter set per run) over "
+                                              f"tools/time_fused.py {'DESCENT=1 ' if wl == 'desc' else ''}FUSE={FUSE}; means "
                                               f"of the {d.get('launches_averaged')} timed k_step launches"}
     if "FETCH_SIZE" in d and "WRITE_SIZE" in d:
         s["f64_fetch_kib_per_launch"] = d["FETCH_SIZE"]
