@@ -311,16 +311,24 @@ class pso_wrapped_env:
         self.experience_buffer = []
 
     def objective_function(self, individual, max_steps=None):
+        """env_wrapped_ea.py:199-222, including its experience_buffer tuples: from the second step
+        on, (state after the previous step, previous action, previous reward, state after this
+        step, this action) -- the reference's own pairing, kept as is."""
         self.individual_update_model(individual)
         state = self.env.reset()
         total, t = 0.0, 0
+        prev = None
         while True:
             action = self.actor.forward(state)
             state, reward, done, truncated, info = self.env.step(action)
             total -= reward
             t += 1
+            if prev is not None:
+                self.experience_buffer.append((prev[0], prev[1], prev[2], state, action))
+            prev = (state, action, reward)
             if done or truncated or (max_steps and t >= max_steps):
                 break
+        self.last_objective_steps = t
         self.episode_idx += 1
         return total
 

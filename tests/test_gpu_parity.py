@@ -343,6 +343,17 @@ def test_pso_facade_batch_objective(pd):
     assert fit.shape == (256,) and np.isfinite(fit).all()
     f0 = w.objective_function(X[0], max_steps=400)
     assert np.isfinite(f0)
+    # experience_buffer as env_wrapped_ea.py:209-218 fills it: one tuple per step after the first,
+    # each pairing the previous step's (state, action, reward) with this step's (state, action)
+    import torch
+    buf = w.experience_buffer
+    n = w.last_objective_steps
+    assert len(buf) == n - 1
+    for later, earlier in zip(buf[1:], buf[:-1]):
+        assert np.array_equal(later[0], earlier[3]) and torch.equal(later[1], earlier[4])
+        assert isinstance(later[2], float)
+    w.reset()
+    assert w.experience_buffer == []
 
 
 @pytest.mark.parametrize("phase,pidx", [("landing_burn_pure_throttle", 0), ("landing_burn", 1)])
