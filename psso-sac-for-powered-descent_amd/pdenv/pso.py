@@ -144,7 +144,25 @@ class ParticleSubswarmOptimisationGPU:
         # here (creating a handle inside a generation costs tens of ms), candidates padded to it
         self._aux = {self.S - 1: PoweredDescentEnv(self.S - 1, self.flight_phase, **self.env_kw)} if self.S > 1 else {}
         self.last_fitness = None
+        self._pending = None           # a share's candidates, evaluated with the next generation
+        self._share_log = None
+        self.share_history = []        # (generation, moved subswarms, their candidates' fitness)
+        self._make_merged_handle()
         self._warm_share_path()
+
+    def _mergeable(self):
+        """share_information's candidates ride along with the next generation's rollout (S - 1 more
+        envs in one launch sequence instead of a latency-bound rollout of their own) unless the
+        wind is stochastic: a candidate's noise then depends on its env index, which must be the
+        same on every rank."""
+        return self.S > 1 and self.P > 0 and not (self.env_kw["enable_wind"] and self.env_kw["stochastic_wind"])
+
+    def _make_merged_handle(self):
+        n = self.P + self.S - 1
+        for k in [k for k in self._aux if k not in (self.S - 1, n)]:   # (a merged handle of an earlier P)
+            self._aux.pop(k).close()
+        if self._mergeable() and n not in self._aux:
+            self._aux[n] = PoweredDescentEnv(n, self.flight_phase, **self.env_kw)
 
     def _warm_share_path(self):
         """share_information's tensor operations once on scratch copies (no rng draws, no state
@@ -161,6 +179,12 @@ class ParticleSubswarmOptimisationGPU:
         mv = torch.tensor(moved, device=self.device)
         old = sbf[mv]
         sbf[mv] = torch.where(fit < old, fit, old)
+        sb[mv] = (1 - 0.3) * sb[mv] + 0.3 * sb[self.S - 1]
+        if self._mergeable():
+            torch.cat([self.x32, cand], dim=1)
+        if self.P > 0:
+            sw = self.swarm.clone()
+            sw.index_put_((mv,), torch.zeros(1, dtype=sw.dtype, device=self.device))
         torch.cuda.synchronize(self.device)
 
     def _env_for(self, n):
@@ -183,18 +207,45 @@ class ParticleSubswarmOptimisationGPU:
         return fit.double(), steps
 
     # ------------------------------------------------------------------ one generation
-    # host views of the device bests (each read synchronises; the generation itself never reads)
+    # host views of the device bests (each read synchronises; the generation itself never reads);
+    # a read first completes a pending share, so that what it shows is what the reference's
+    # share_information leaves behind
     @property
     def sbf(self):
+        self.flush_share()
         return [float(v) for v in self.sbf_t.cpu()]
 
     @property
     def gbf(self):
+        self.flush_share()
         return float(self.gbf_t)
 
     @property
     def gb(self):
         return None if not math.isfinite(self.gbf) else self.gb_t.clone()
+
+    @property
+    def share_log(self):
+        """(moved subswarms, their candidates' fitness) of the last share_information."""
+        self.flush_share()
+        return self._share_log
+
+    def flush_share(self, fit=None):
+        """Complete a pending share_information (:533-541): the candidates' fitness (`fit`, from
+        the merged rollout; else evaluated now on the share handle) replaces a subswarm's best
+        fitness when strictly better."""
+        if self._pending is None:
+            return
+        gen, moved, cand = self._pending
+        self._pending = None
+        if fit is None:
+            fit, _ = self.evaluate(cand)
+        fit = fit[:len(moved)]
+        self._share_log = (moved, fit.clone())
+        self.share_history.append((gen, moved, self._share_log[1]))
+        mv = torch.tensor(moved, device=self.device)
+        old = self.sbf_t[mv]
+        self.sbf_t[mv] = torch.where(fit < old, fit, old)
 
     def _swarm_minima(self, fit):
         """Per subswarm: (min fitness, its position) over all ranks, first particle on ties -- a
@@ -218,7 +269,17 @@ class ParticleSubswarmOptimisationGPU:
         return f, pos
 
     def generation(self, gen):
-        fit, _ = self.evaluate(self.x32)
+        if self._pending is not None and self._mergeable():
+            # the previous generation's share candidates as S - 1 more envs of this rollout (each
+            # env's episode is independent of the batch: the same fitness bits as on their own);
+            # their bests are updated before this generation's (the reference's order)
+            cand = self._pending[2]
+            fit_all, _ = self.evaluate(torch.cat([self.x32, cand], dim=1))
+            fit = fit_all[:self.P]
+            self.flush_share(fit_all[self.P:])
+        else:
+            self.flush_share()
+            fit, _ = self.evaluate(self.x32)
         self.last_fitness = fit
         f, pos = self._swarm_minima(fit)
         # :442-444 per subswarm: a strictly better minimum replaces the subswarm best; :474-477
@@ -232,6 +293,7 @@ class ParticleSubswarmOptimisationGPU:
                                          _ptr(self.pb), _ptr(self.sb), _ptr(self.swarm), _ptr(self.lower),
                                          _ptr(self.upper), float(self.w), float(self.p["c1"]), float(self.p["c2"]),
                                          self.seed, gen, self.offset, _ptr(self.x32), _stream(self.device)))
+        self._gen = gen
         if gen % self.p["communication_freq"] == 0 and gen > 0:
             self.share_information()
         if gen % self.p["migration_freq"] == 0 and gen > 0:
@@ -243,6 +305,7 @@ class ParticleSubswarmOptimisationGPU:
     def run(self, generations=None):
         for gen in range(generations if generations is not None else self.p["generations"]):
             self.generation(gen)
+        self.flush_share()
         return self.gb, self.gbf
 
     # ------------------------------------------------------------------ share / migrate / re-init
@@ -254,16 +317,12 @@ class ParticleSubswarmOptimisationGPU:
         moved = [i for i in range(self.S) if i != best and self.rng.random() < 0.5]
         if not moved:
             return
-        for i in moved:
-            self.sb[i] = (1 - 0.3) * self.sb[i] + 0.3 * self.sb[best]
+        mv = torch.tensor(moved, device=self.device)
+        self.sb[mv] = (1 - 0.3) * self.sb[mv] + 0.3 * self.sb[best]
         pad = moved + [moved[0]] * (self.S - 1 - len(moved))  # (padded to the share handle's size)
         cand = self.sb[pad].t().float().contiguous()            # [D][S-1]
-        fit, _ = self.evaluate(cand)
-        fit = fit[:len(moved)]
-        self.share_log = (moved, fit.clone())
-        mv = torch.tensor(moved, device=self.device)
-        old = self.sbf_t[mv]
-        self.sbf_t[mv] = torch.where(fit < old, fit, old)
+        # evaluated with the next generation's rollout (or on the next read of the bests)
+        self._pending = (getattr(self, "_gen", None), moved, cand)
 
     def migrate_particles(self):
         """:545-553: number_of_migrants random particles of every subswarm (with > 1 member) move
@@ -271,9 +330,14 @@ class ParticleSubswarmOptimisationGPU:
         draw the same choices); each rank applies those that hit its own particles."""
         sw = all_gather_var(self.swarm, self.dist)
         moves = migration_moves(sw, self.S, self.p["number_of_migrants"], self.rng)
-        for g, t in moves:
+        mine = {}
+        for g, t in moves:                                       # (a later move of a particle wins)
             if self.offset <= g < self.offset + self.P:
-                self.swarm[g - self.offset] = t
+                mine[g - self.offset] = t
+        if mine:
+            idx = torch.tensor(list(mine.keys()), device=self.device)
+            self.swarm.index_put_((idx,), torch.tensor(list(mine.values()), dtype=self.swarm.dtype,
+                                                       device=self.device))
 
     def re_initialise_swarms(self):
         """:360-370: every subswarm keeps its re_initialise_number_of_particles // S best
@@ -293,3 +357,4 @@ class ParticleSubswarmOptimisationGPU:
         if self.env is not None:
             self.env.close()
         self.env = PoweredDescentEnv(self.P, self.flight_phase, **self.env_kw) if self.P > 0 else None
+        self._make_merged_handle()

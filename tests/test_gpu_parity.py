@@ -574,6 +574,35 @@ def test_pso_swarm_minima_and_bests_vs_numpy(pd):
         assert float(gbf) == g and np.array_equal(gb.cpu().numpy(), gv)
 
 
+def test_pso_share_merged_into_next_rollout(pd):
+    """share_information's candidates ride along with the next generation's rollout (S - 1 more
+    envs): with a share every generation, the run equals one that evaluates every share's
+    candidates on their own handle, bit for bit (candidate fitness, bests, swarm state)."""
+    import torch
+    from pdenv.pso import ParticleSubswarmOptimisationGPU
+    prm = dict(generations=6, communication_freq=1, migration_freq=2, num_sub_swarms=3, re_initialise_generation=99)
+    runs, sizes = [], []
+    for merge in (True, False):
+        opt = ParticleSubswarmOptimisationGPU("landing_burn", pso_params=prm, pop_size=96, seed=7, max_steps=300)
+        if not merge:
+            opt._mergeable = lambda: False
+        seen = []
+        ev = opt.evaluate
+        opt.evaluate = lambda x32, ev=ev, seen=seen: (seen.append(x32.shape[1]), ev(x32))[1]
+        for g in range(6):
+            opt.generation(g)
+        opt.flush_share()
+        runs.append(opt)
+        sizes.append(seen)
+    a, b = runs
+    assert 96 + 2 in sizes[0] and 96 + 2 not in sizes[1]       # the merged rollout ran (and only there)
+    assert len(a.share_history) == len(b.share_history) >= 3
+    for (ga, ma, fa), (gb, mb, fb) in zip(a.share_history, b.share_history):
+        assert ga == gb and ma == mb and torch.equal(fa, fb)
+    for k in ("x", "v", "pb", "pbf", "swarm", "sb", "sbf_t", "gbf_t", "gb_t"):
+        assert torch.equal(getattr(a, k), getattr(b, k)), k
+
+
 def test_pso_driver_generations_vs_numpy(pd):
     """Three generations of the device subswarm PSO (evaluation, subswarm/global bests, inertia
     schedule, update, share_information and migrate_particles at generation 2) against a NumPy
