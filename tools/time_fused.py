@@ -25,10 +25,12 @@ import bench  # noqa: E402
 burn = bench.DESCENT_BURN_IN if descent else 0
 phase = os.environ.get("PHASE", "landing_burn_pure_throttle")
 t_c = time.perf_counter()
+wind = os.environ.get("WIND", "1") == "1"      # WIND=0 TILT=0: the c2 workload (INTEG=rk4: its RK4 mode)
 env = pdenv.PoweredDescentEnv(n, flight_phase=phase, mode="rl" if phase == "landing_burn_pure_throttle" else "pso",
-                              precision=os.environ.get("PREC", "f64"), enable_wind=True, stochastic_wind=True,
-                              wind_percentile=None, auto_reset=True, tilt_sigma_rad=math.radians(1.0), seed=1234,
-                              lanes_per_env=int(os.environ.get("LPE", "0")))
+                              precision=os.environ.get("PREC", "f64"), enable_wind=wind, stochastic_wind=wind,
+                              wind_percentile=None, auto_reset=True,
+                              tilt_sigma_rad=math.radians(1.0) if os.environ.get("TILT", "1") == "1" else 0.0, seed=1234,
+                              lanes_per_env=int(os.environ.get("LPE", "0")), integrator=os.environ.get("INTEG", "reference"))
 t_create = time.perf_counter() - t_c
 g = torch.Generator(device="cuda").manual_seed(42)
 acts = bench.c3_actions(burn + (launches + 8) * F, n, g, "cuda", descent)
@@ -60,7 +62,8 @@ ms = sorted(a.elapsed_time(b) for a, b in ev)
 w1 = env.stats()
 work = {k: w1[k] - w0[k] for k in env.WORK_COUNTERS}
 work["gust_steps_frac"] = work["gust_substeps"] / (n * launches * F * 4)
-print(json.dumps({"lib": os.path.basename(os.environ.get("PDENV_LIB", "libpdenv.so")), "n": n, "fuse": F, "cell_pieces": os.environ.get("PDENV_CELL_PIECES", "1") != "0", "fine": os.environ.get("PDENV_FINE", "1") != "0",
+print(json.dumps({"lib": os.path.basename(os.environ.get("PDENV_LIB", "libpdenv.so")), "n": n, "fuse": F,
+                  "lpe": int(os.environ.get("LPE", "0")), "wind": wind, "integrator": os.environ.get("INTEG", "reference"), "cell_pieces": os.environ.get("PDENV_CELL_PIECES", "1") != "0", "fine": os.environ.get("PDENV_FINE", "1") != "0",
                   "descent": descent, "work": work,
                   "launch_ms_avg": sum(ms) / len(ms), "launch_ms_med": ms[len(ms) // 2],
                   "ms_per_step": sum(ms) / len(ms) / F, "wall_ms_per_step": wall * 1e3 / (launches * F),
