@@ -52,23 +52,26 @@ def implementation_bytes(precision, phase, wind, obs_dim, act_dim, fuse):
     return 2 * state / fuse + per_step
 
 
-def valu_roofline(mix, kern_avg_ms, simds=1024, clock_hz=2.4e9, fp64_peak_tflops=78.6):
+def valu_roofline(mix, steps, kern_ms, simds=1024, clock_hz=2.4e9, fp64_peak_tflops=78.6):
     """The bound that actually limits k_step: vector-ALU issue.  `mix` is the
-    per-launch instruction mix of the same workload from rocprofv3 PMC passes
-    (profiles/pmc_traffic.json); the launch time is the one measured live.  Issue model of a
-    SIMD-32 (MI355X guide): a wave64 VALU instruction occupies 2 cycles, a binary64 one 4."""
-    f64 = sum(mix.get(f"SQ_INSTS_VALU_{k}_F64", 0.0) for k in ("ADD", "MUL", "FMA", "TRANS"))
-    valu = mix["SQ_INSTS_VALU"]
+    instruction mix per env-step (all envs) of the same workload from rocprofv3 PMC passes
+    (profiles/pmc_traffic.json), counted here over the `steps` env-steps of the timed launches,
+    whose kernel time `kern_ms` is the one measured live.  Issue model of a SIMD-32 (MI355X
+    guide): a wave64 VALU instruction occupies 2 cycles, a binary64 one 4."""
+    f64 = steps * sum(mix.get(f"SQ_INSTS_VALU_{k}_F64", 0.0) for k in ("ADD", "MUL", "FMA", "TRANS"))
+    valu = steps * mix["SQ_INSTS_VALU"]
     issue_cycles = 4.0 * f64 + 2.0 * (valu - f64)
-    sec = kern_avg_ms * 1e-3
-    flop = 64.0 * (mix.get("SQ_INSTS_VALU_ADD_F64", 0.0) + mix.get("SQ_INSTS_VALU_MUL_F64", 0.0)
-                   + mix.get("SQ_INSTS_VALU_TRANS_F64", 0.0) + 2.0 * mix.get("SQ_INSTS_VALU_FMA_F64", 0.0))
+    sec = kern_ms * 1e-3
+    flop = 64.0 * steps * (mix.get("SQ_INSTS_VALU_ADD_F64", 0.0) + mix.get("SQ_INSTS_VALU_MUL_F64", 0.0)
+                           + mix.get("SQ_INSTS_VALU_TRANS_F64", 0.0) + 2.0 * mix.get("SQ_INSTS_VALU_FMA_F64", 0.0))
     return {"bound": "valu", "achieved": issue_cycles / sec / 1e12, "peak": simds * clock_hz / 1e12,
             "unit": "T SIMD-issue-cycles/s", "frac": issue_cycles / (simds * clock_hz * sec),
-            "valu_insts_per_launch": valu, "f64_insts_per_launch": f64,
+            "valu_insts_per_env_step": mix["SQ_INSTS_VALU"], "f64_insts_per_env_step": f64 / steps,
+            "env_steps": steps, "kernel_ms": kern_ms,
             "fp64_tflops": flop / sec / 1e12, "fp64_peak_tflops": fp64_peak_tflops,
             "waves_per_launch": mix.get("SQ_WAVES"),
-            "source": "profiles/pmc_traffic.json f64_valu_mix_per_launch (rocprofv3 --pmc, 2 passes)"}
+            "source": "profiles/pmc_traffic.json f64_valu_mix_per_launch (rocprofv3 --pmc, 2 passes), "
+                      "per env-step"}
 
 
 def shard_offset(rank, n_per_rank):
@@ -355,26 +358,34 @@ def c3_summary(args, r, world, precision, pmc=None):
     ibpe = implementation_bytes(precision, args.phase, wind, r["obs_dim"], r["act_dim"], F)
     kern_s = r["kern_total_ms"] * 1e-3
     achieved = bpe * n * K / kern_s / 1e9
-    traffic = None
+    traffic = per_step = None
     mix = None
     if pmc:
-        scale = F / float(pmc.get("env_steps_per_launch", 1))
-        traffic = pmc.get(f"{precision}_bytes_per_launch")
-        traffic = traffic * scale if traffic is not None else None
+        # counter bytes per env-step, times the env-steps of the average timed launch
+        # (like `achieved`: the driver's short timed region may be one partial launch)
+        per_step = pmc.get(f"{precision}_bytes_per_launch")
+        per_step = per_step / float(pmc.get("env_steps_per_launch", 1)) if per_step is not None else None
+        traffic = per_step * K / r["kern_launches"] if per_step is not None else None
         mix = pmc.get("f64_valu_mix_per_launch") if precision == "f64" else None
-        if mix:   # (instruction counts scale with the steps per launch; the wave count does not)
-            mix = {k: (v * scale if k != "SQ_WAVES" else v) for k, v in mix.items()}
+        if mix:   # per env-step (the wave count is per launch)
+            ps = float(pmc.get("env_steps_per_launch", 1))
+            mix = {k: (v / ps if k != "SQ_WAVES" else v) for k, v in mix.items()}
     out = {
         "value": whole_job_rate(n, world, K, r["wall"]),
         "ms_per_step": r["wall"] / K * 1e3,
         "device_ms_per_step": r["dev_ms"] / K,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": 8000.0, "unit": "GB/s",
                      "frac": achieved / 8000.0, "traffic": traffic,
+                     "traffic_bytes_per_env_step": per_step / n if per_step is not None else None,
                      "bytes_per_env_step": bpe, "bytes_source": "SURVEY.md 8(d) algorithmic count",
                      "implementation_bytes_per_env_step": round(ibpe, 1),
                      "kernel": "k_step", "kernel_ms_per_step": r["kern_total_ms"] / K,
-                     "kernel_avg_ms": r["kern_avg_full_ms"], "kernel_launches_timed": r["kern_launches"],
-                     "env_steps_per_launch": F, "envs_per_launch": n,
+                     # (the average over the timed launches; a short timed region may be one
+                     # partial launch of K < F env-steps)
+                     "kernel_avg_ms": r["kern_total_ms"] / r["kern_launches"],
+                     "kernel_avg_full_launch_ms": r["kern_avg_full_ms"], "kernel_launches_timed": r["kern_launches"],
+                     "env_steps_per_launch": F, "env_steps_per_timed_launch": K / r["kern_launches"],
+                     "envs_per_launch": n,
                      "kernel_timing": "the timed region's launches replayed from its checkpoint, HIP events per "
                                       "launch (k_step + its miss flush) on the launch stream",
                      "note": "VALU/latency-bound elementwise ODE (no MFMA); see DESIGN.md"},
@@ -383,7 +394,9 @@ def c3_summary(args, r, world, precision, pmc=None):
         "launch_index": r["launch_index"],
     }
     if mix and n == 65536:
-        out["valu_roofline"] = valu_roofline(mix, r["kern_avg_full_ms"] or r["kern_total_ms"] / r["kern_launches"])
+        # over exactly the timed launches' env-steps and kernel time (a short timed region may be
+        # one partial launch)
+        out["valu_roofline"] = valu_roofline(mix, K, r["kern_total_ms"])
     return out
 
 
