@@ -338,8 +338,8 @@ def run_c3(args, precision, local, rank, dist, descent=False, launch_base=0):
     res = dict(wall=wall, dev_ms=dev_ms, kern_total_ms=sum(kern), kern_launches=len(kern),
                kern_avg_full_ms=(sum(full) / len(full)) if full else None, fuse=F, n=n,
                obs_dim=env.obs_dim, act_dim=env.action_dim, burn_in=burn,
-               # (lanes per env: pd_create's default, 2 above 16 384 envs)
-               counts=workload_counts(d, n, args.steps, 2 if n > 16384 else 0),
+               # (lanes per env: pd_create's default, 2 above 8 192 envs)
+               counts=workload_counts(d, n, args.steps, 2 if n > 8192 else 0),
                replay_misses=s2["rbf_misses"] - s1["rbf_misses"],
                launch_index={"kernel": f"k_step<{'double' if precision == 'f64' else 'float'}>",
                              "timed": [first_timed, first_timed + len(tb)],

@@ -1645,12 +1645,16 @@ pd_status pd_create(const pd_params* params, const pd_config* cfg, pd_env** out)
     e->obs_kind = obs_kind_of(cfg->phase, cfg->rtd);
     e->obs_dim = obs_dim(e->obs_kind);
     e->rsize = cfg->precision == PD_F64 ? 8 : 4;
-    // default lanes per env: about one wave per SIMD (n_envs x LPE ~ 65 536 lanes), at least 2.
-    // Below ~64k envs the step is bound by one wave's latency, and splitting each RBF over more
-    // lanes shortens it (measured, f64 ms/step: 4 096 envs LPE 16 0.049, 8 0.054, 2 0.071;
-    // 16 384 LPE 4 0.066, 8 0.067, 16 0.105; 32 768 LPE 2 0.072, 4 0.075; 65 536 LPE 2 best)
+    // default lanes per env.  Below ~64k envs the step is bound by one wave's latency: splitting
+    // each table's sum over LPE / 2 lanes shortens it, while LPE 2 alone has the Taylor lines,
+    // cell pieces and fine index.  Measured on the round-3 kernels (f64 ms per
+    // env-step, 128 steps per launch, wind / no wind; profiles/r03_exp_lpe_sweep.jsonl):
+    //   4 096: LPE 16 0.0221 / 0.0186, 8 0.0242, 2 0.0261 / 0.0237
+    //   8 192: LPE 8 0.0249 / 0.0210, 2 0.0260 / 0.0235, 4 0.0277 / 0.0241, 16 0.0274 / 0.0235
+    //  16 384: LPE 2 0.0261 / 0.0234, 4 0.0277 / 0.0240, 8 0.0306
+    //  32 768: LPE 2 0.0263, 4 0.0352; 65 536: LPE 2
     e->lpe = cfg->lanes_per_env != 0 ? cfg->lanes_per_env
-                                     : (cfg->n_envs <= 4096 ? 16 : (cfg->n_envs <= 8192 ? 8 : (cfg->n_envs <= 16384 ? 4 : 2)));
+                                     : (cfg->n_envs <= 4096 ? 16 : (cfg->n_envs <= 8192 ? 8 : 2));
     if (const char* lv = getenv("PDENV_LPE"); lv && *lv && cfg->lanes_per_env == 0) e->lpe = atoi(lv);   // experiments
     if (e->lpe != 1 && e->lpe != 2 && e->lpe != 4 && e->lpe != 8 && e->lpe != 16) { delete e; return fail(PD_ERR_INVALID, "lanes_per_env must be 0, 1, 2, 4, 8 or 16"); }
     if (cfg->integrator == PD_INTEG_RK4) e->lpe = e->lpe <= 2 ? 2 : 16;   // the RK4 instantiations
