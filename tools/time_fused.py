@@ -63,7 +63,7 @@ w1 = env.stats()
 work = {k: w1[k] - w0[k] for k in env.WORK_COUNTERS}
 work["gust_steps_frac"] = work["gust_substeps"] / (n * launches * F * 4)
 print(json.dumps({"lib": os.path.basename(os.environ.get("PDENV_LIB", "libpdenv.so")), "n": n, "fuse": F,
-                  "lpe": int(os.environ.get("LPE", "0")), "wind": wind, "integrator": os.environ.get("INTEG", "reference"), "cell_pieces": os.environ.get("PDENV_CELL_PIECES", "1") != "0", "fine": os.environ.get("PDENV_FINE", "1") != "0",
+                  "lpe": int(os.environ.get("LPE", "0")), "wind": wind, "integrator": os.environ.get("INTEG", "reference"), "cell_pieces": os.environ.get("PDENV_CELL_PIECES", "1") != "0", "fine": os.environ.get("PDENV_FINE", "1") != "0", "line_pieces": os.environ.get("PDENV_LINE_PIECES", "1") != "0",
                   "descent": descent, "work": work,
                   "launch_ms_avg": sum(ms) / len(ms), "launch_ms_med": ms[len(ms) // 2],
                   "ms_per_step": sum(ms) / len(ms) / F, "wall_ms_per_step": wall * 1e3 / (launches * F),
