@@ -23,6 +23,8 @@ for s in $STAGES; do
     bench) stage bench 600 python bench.py ;;
     benchdrv) stage benchdrv 600 python bench.py --steps 20 --warmup 5 ;;
     bench32) stage bench32 600 python bench.py --precision f32 ;;
+    c2) stage c2 600 python bench.py --workload c2 --cpu-baseline 0 ;;
+    c2rk4) stage c2rk4 600 python bench.py --workload c2 --integrator rk4 --cpu-baseline 0 ;;
     prof) stage prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 192 --warmup 32 --cpu-baseline 0 --secondary 0 --others 0 --descent 1 ;;
     profc4) stage profc4 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/profc4 -o run -- python3 bench.py --workload c4 --steps 16 --warmup 2 --cpu-baseline 0 ;;
     profc5) stage profc5 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/profc5 -o run -- python3 bench.py --workload c5 --steps 192 --warmup 32 ;;
