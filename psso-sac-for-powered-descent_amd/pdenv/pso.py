@@ -84,6 +84,17 @@ def migration_moves(swarm, n_swarms, n_migrants, rng):
     return moves
 
 
+def local_moves(moves, offset, n_local):
+    """The migration moves [(global particle, new subswarm)] that hit this rank's particles
+    [offset, offset + n_local), as {local index: subswarm}: a particle moved twice in one
+    migration ends in its last subswarm, as the reference's sequential list edits leave it."""
+    mine = {}
+    for g, t in moves:
+        if offset <= g < offset + n_local:
+            mine[g - offset] = t
+    return mine
+
+
 class ParticleSubswarmOptimisationGPU:
     """One rank's shard of the swarm.  Global particle g belongs to subswarm g // (pop / S)
     (initialize_swarms, :372-389); rank r holds particles [r*P_local, (r+1)*P_local)."""
@@ -330,10 +341,7 @@ class ParticleSubswarmOptimisationGPU:
         draw the same choices); each rank applies those that hit its own particles."""
         sw = all_gather_var(self.swarm, self.dist)
         moves = migration_moves(sw, self.S, self.p["number_of_migrants"], self.rng)
-        mine = {}
-        for g, t in moves:                                       # (a later move of a particle wins)
-            if self.offset <= g < self.offset + self.P:
-                mine[g - self.offset] = t
+        mine = local_moves(moves, self.offset, self.P)
         if mine:
             idx = torch.tensor(list(mine.keys()), device=self.device)
             self.swarm.index_put_((idx,), torch.tensor(list(mine.values()), dtype=self.swarm.dtype,

@@ -174,7 +174,7 @@ def _pso_uneven_worker(rank, world, port, out):
     the variable-size gathers and the migration decisions must still agree on every rank."""
     import random
     sys.path.insert(0, os.path.join(REPO, "psso-sac-for-powered-descent_amd"))
-    from pdenv.pso import all_gather_var, migration_moves, reinit_keep
+    from pdenv.pso import all_gather_var, local_moves, migration_moves, reinit_keep
     _init(rank, world, port)
     # global population of 12 in 2 subswarms; rank 0 holds 0..5, rank 1 holds 6..11
     g = torch.Generator().manual_seed(4)
@@ -188,6 +188,14 @@ def _pso_uneven_worker(rank, world, port, out):
     local = torch.tensor([0, 1, 0, 1, 1], dtype=torch.int32) if rank == 0 else torch.empty(0, dtype=torch.int32)
     sw = all_gather_var(local, dist)
     moves = migration_moves(sw, 2, 1, random.Random(9))
+    # each rank applies the moves that hit its own particles, a later move of a particle winning
+    offset, n = (0, 5) if rank == 0 else (5, 0)
+    applied = sw.clone()
+    for g, t in moves:
+        applied[g] = t
+    mine = local_moves(moves, offset, n)
+    assert all(applied[offset + i] == t for i, t in mine.items())
+    assert set(mine) == {g - offset for g, _ in moves if offset <= g < offset + n}
     out[rank] = (sw.tolist(), moves)
     dist.destroy_process_group()
 
@@ -201,3 +209,15 @@ def test_pso_uneven_shards_gather_and_migrate():
     assert out[0] == out[1]
     assert out[0][0] == [0, 1, 0, 1, 1]
     assert len(out[0][1]) == 2
+
+
+def test_pso_local_moves_later_move_wins():
+    """migrate_particles applies the moves that hit this rank's shard in one indexed write: a
+    particle the decisions move twice ends in its last subswarm (the reference edits its member
+    lists in order), and moves of other ranks' particles are left to them."""
+    sys.path.insert(0, os.path.join(REPO, "psso-sac-for-powered-descent_amd"))
+    from pdenv.pso import local_moves
+    moves = [(3, 1), (7, 0), (3, 2), (12, 1), (5, 0)]
+    assert local_moves(moves, 2, 5) == {1: 2, 3: 0}          # particles 2..6: 3 -> 1 -> 2, 5 -> 0
+    assert local_moves(moves, 7, 6) == {0: 0, 5: 1}          # particles 7..12
+    assert local_moves(moves, 20, 0) == {}
