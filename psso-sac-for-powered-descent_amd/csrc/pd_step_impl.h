@@ -943,8 +943,14 @@ template <typename R, bool WIND, int EPB, bool BAL = false> struct StepLds {
     uint32_t work[kStepBlock / 64][kNWork];   // per-wave workload counts (counting launches)
     double wnx[WIND ? 2 : 1][WIND ? kStepBlock : 1];   // each lane's gust normals of the next (odd) sub-step
     BalLds<R> bal[BAL ? kStepBlock / 64 : 1];   // LPE 2: balanced-sum space per wave
+    TabView<R> tdesc[2];          // each table's view, staged once: a lane's table is per lane
 };
 
+// A lane's table view from the workgroup's LDS copy (two entries; lanes of one wave read at most
+// two addresses): its fields then come from LDS, not from lane-indexed global loads of the
+// parameters at the head of every lookup
+template <typename R>
+__device__ __forceinline__ TabView<R> tab_view_lds(const TabView<R>* d, int table) { return d[table]; }
 template <typename R>
 __device__ __forceinline__ TabView<R> tab_view(DP<R>& P, const R* tab, int table) {
     TabView<R> t;
@@ -1046,6 +1052,7 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
             s_logtab[t] = P.logtab_d.cell[t];
         }
         if (threadIdx.x < (kStepBlock / 64) * kNWork) (&L.work[0][0])[threadIdx.x] = 0u;
+        if (threadIdx.x < 2) L.tdesc[threadIdx.x] = tab_view<R>(P, L.tab, (int)threadIdx.x);
     }
     __syncthreads();
     PD_T(t_staged);
@@ -1333,21 +1340,21 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
             if constexpr (LPE == 1) {
                 // (both sums interleaved in lockstep on one lane, 1 wave per SIMD with AGPR
                 // spill space, measured 14 % slower than these two calls)
-                R v = rbf<R>(a, P, 1, tab_view<R>(P, L.tab, 1), L.lines, cB, mach, aq_cl, 0, 1);
-                R w = rbf<R>(a, P, 0, tab_view<R>(P, L.tab, 0), L.lines, cA, mach, aq_cd, 0, 1);
+                R v = rbf<R>(a, P, 1, tab_view_lds<R>(L.tdesc, 1), L.lines, cB, mach, aq_cl, 0, 1);
+                R w = rbf<R>(a, P, 0, tab_view_lds<R>(L.tdesc, 0), L.lines, cA, mach, aq_cd, 0, 1);
                 CL = (!have || cl_zero) ? R(0) : (cl_sgn < R(0) ? -v : v);
                 CD = have ? w : R(0);
             } else {
                 R v;
                 if constexpr (LPE == 2)
-                    v = rbf2<R>(a, P, my_table, tab_view<R>(P, L.tab, my_table), L.lines, cA, mach,
+                    v = rbf2<R>(a, P, my_table, tab_view_lds<R>(L.tdesc, my_table), L.lines, cA, mach,
                                 my_table ? aq_cl : aq_cd, live, L.bal[threadIdx.x >> 6], L.tab, wc, wind_block
 #ifdef PD_STAMP
                                 , acc_ + 7
 #endif
                                 );
                 else
-                    v = rbf<R>(a, P, my_table, tab_view<R>(P, L.tab, my_table), L.lines, cA, mach,
+                    v = rbf<R>(a, P, my_table, tab_view_lds<R>(L.tdesc, my_table), L.lines, cA, mach,
                                my_table ? aq_cl : aq_cd, part, nparts);
                 if constexpr (nparts >= 2) v += __shfl_xor(v, 1);
                 if constexpr (nparts >= 4) v += __shfl_xor(v, 2);
