@@ -340,8 +340,11 @@ __device__ __forceinline__ void obs_write(DP<R>& P, int kind, const R* s, R* out
 
 // ---------------------------------------------------------------- tables in LDS
 // scipy interp1d._call_linear with fill_value='extrapolate' (grid_fin_aerodynamics.py:7-18)
+// (slope: the intervals' slopes (y[i] - y[i-1]) / (x[i] - x[i-1]) at index i, tabulated with the
+// same operation, or nullptr: computed here)
 template <typename R>
-__device__ __forceinline__ R grid_fin_ca(DP<R>& P, const R* sx, const R* sy, R mach, const uint16_t* lb = nullptr) {
+__device__ __forceinline__ R grid_fin_ca(DP<R>& P, const R* sx, const R* sy, R mach, const uint16_t* lb = nullptr,
+                                         const R* slope = nullptr) {
     if (mach < P.ca_min_mach) return P.ca_min_val;
     int n = P.ca_n;
     int lo = 0, hi = n;                       // lower_bound: first x >= mach
@@ -353,29 +356,30 @@ __device__ __forceinline__ R grid_fin_ca(DP<R>& P, const R* sx, const R* sy, R m
     }
     while (lo < hi) { int mid = (lo + hi) >> 1; if (sx[mid] < mach) lo = mid + 1; else hi = mid; }
     int idx = lo < 1 ? 1 : (lo > n - 1 ? n - 1 : lo);
-    R xl = sx[idx - 1], xh = sx[idx], yl = sy[idx - 1], yh = sy[idx];
-    R slope = (yh - yl) / (xh - xl);
-    return slope * (mach - xl) + yl;
+    R xl = sx[idx - 1], yl = sy[idx - 1];
+    const R sl = slope ? slope[idx] : (sy[idx] - yl) / (sx[idx] - xl);
+    return sl * (mach - xl) + yl;
 }
 
 // np.interp for an in-range query (numpy compiled_base.c arr_interp)
+// (slope: (y[j + 1] - y[j]) / (x[j + 1] - x[j]) tabulated at index j, or nullptr: computed here)
 template <typename R>
-__device__ __forceinline__ R np_interp(const R* x, const R* y, int n, R v) {
+__device__ __forceinline__ R np_interp(const R* x, const R* y, int n, R v, const R* slope = nullptr) {
     if (v < x[0]) return y[0];
     if (v >= x[n - 1]) return y[n - 1];
     int lo = 0, hi = n;                       // upper_bound: first x > v
     while (lo < hi) { int mid = (lo + hi) >> 1; if (x[mid] <= v) lo = mid + 1; else hi = mid; }
     int j = lo - 1;
     if (x[j] == v) return y[j];
-    R slope = (y[j + 1] - y[j]) / (x[j + 1] - x[j]);
-    return slope * (v - x[j]) + y[j];
+    const R sl = slope ? slope[j] : (y[j + 1] - y[j]) / (x[j + 1] - x[j]);
+    return sl * (v - x[j]) + y[j];
 }
 
 // grid_fin_aerodynamics.py:21-46: cn_alpha(M) * degrees(alpha)
 template <typename R>
-__device__ __forceinline__ R grid_fin_cn_alpha(DP<R>& P, const R* sx, const R* sy, R mach) {
+__device__ __forceinline__ R grid_fin_cn_alpha(DP<R>& P, const R* sx, const R* sy, R mach, const R* slope = nullptr) {
     if (mach < P.cn_min_mach) return P.cn_min_val;
-    if (mach <= P.cn_max_mach) return np_interp(sx, sy, P.cn_n, mach);
+    if (mach <= P.cn_max_mach) return np_interp(sx, sy, P.cn_n, mach, slope);
     return P.cn_max_val + P.cn_slope * (mach - P.cn_max_mach);
 }
 

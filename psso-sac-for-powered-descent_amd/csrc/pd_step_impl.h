@@ -934,6 +934,7 @@ template <typename R, bool WIND, int EPB, bool BAL = false> struct StepLds {
     // payload pair slot (smach[2p] is point p's Mach for the neighbourhood search)
     alignas(16) R tab[1024];
     R gf[256];                    // grid fins: ca_x, ca_y, cn_x, cn_y (64 each)
+    R gfs[128];                   // their interval slopes: C_a at the upper index, C_n at the lower
     uint16_t ca_lb[64];           // C_a search buckets
     R isa[9 * kIsaCols];          // ISA layers
     R walt[WIND ? 800 : 1];       // wind profiles [50][16]: altitude km, speed
@@ -1025,6 +1026,11 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
             L.gf[threadIdx.x] = P.ca_x[threadIdx.x]; L.gf[64 + threadIdx.x] = P.ca_y[threadIdx.x];
             L.gf[128 + threadIdx.x] = P.cn_x[threadIdx.x]; L.gf[192 + threadIdx.x] = P.cn_y[threadIdx.x];
             L.ca_lb[threadIdx.x] = P.ca_lb[threadIdx.x];
+            // the slopes grid_fin_ca / np_interp would compute, the same operation on the same
+            // operands (same bits); entries past a table's end are never read
+            const int i = threadIdx.x;
+            L.gfs[i] = i >= 1 ? (P.ca_y[i] - P.ca_y[i - 1]) / (P.ca_x[i] - P.ca_x[i - 1]) : R(0);
+            L.gfs[64 + i] = i < 63 ? (P.cn_y[i + 1] - P.cn_y[i]) / (P.cn_x[i + 1] - P.cn_x[i]) : R(0);
         }
         if (threadIdx.x < 9) {
             const int k = threadIdx.x;
@@ -1414,7 +1420,7 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
 #endif
         R T_full = P.T_e + (P.p_e - patm) * P.A_e;
         R qS = q * P.S_gf;
-        R Ca = grid_fin_ca<R>(P, L.gf, L.gf + 64, mach, L.ca_lb);
+        R Ca = grid_fin_ca<R>(P, L.gf, L.gf + 64, mach, L.ca_lb, L.gfs);
         R cfp, cfperp, cm, mdot_dt, md_info, thr_info;
         // info of the grid-fin ACS (acs_model.py:62-86): deflections, C_n of both fins, forces
         R i_dl = R(0), i_dr = R(0), i_cnl = R(0), i_cnr = R(0), i_gfperp = R(0), i_gfpar = R(0), i_gfm = R(0);
@@ -1443,7 +1449,7 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
                 mdot_dt = md * dt; md_info = md; thr_info = thr;
                 i_gfpar = qS * (Ca * R(4));
                 if (tap_sub) {   // C_n of the undeflected fins (acs_info only)
-                    const R cna = grid_fin_cn_alpha<R>(P, L.gf + 128, L.gf + 192, mach);
+                    const R cna = grid_fin_cn_alpha<R>(P, L.gf + 128, L.gf + 192, mach, L.gfs + 64);
                     i_cnl = cna * (ae * Cst<R>::rad2deg); i_cnr = i_cnl;
                 }
             } else if (aux == PD_PHASE_BALLISTIC_ARC) {
@@ -1516,7 +1522,7 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
             cfperp = R(0); cm = R(0);
             i_gfpar = acs_par;
             if (tap_sub) {   // C_n of the undeflected fins (acs_info only)
-                const R cna = grid_fin_cn_alpha<R>(P, L.gf + 128, L.gf + 192, mach);
+                const R cna = grid_fin_cn_alpha<R>(P, L.gf + 128, L.gf + 192, mach, L.gfs + 64);
                 i_cnl = cna * (ae * Cst<R>::rad2deg); i_cnr = i_cnl;
             }
         } else {
@@ -1566,7 +1572,7 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
             R dcl = cmd_l * Cst<R>::deg2rad, dcr = cmd_r * Cst<R>::deg2rad;
             R dl = dlprev + dt_act * ((-dlprev + dcl) / R(0.5));
             R dr = drprev + dt_act * ((-drprev + dcr) / R(0.5));
-            R cna = grid_fin_cn_alpha<R>(P, L.gf + 128, L.gf + 192, mach);
+            R cna = grid_fin_cn_alpha<R>(P, L.gf + 128, L.gf + 192, mach, L.gfs + 64);
             R CnL = cna * ((ae - dl) * Cst<R>::rad2deg);
             R CnR = cna * ((ae - dr) * Cst<R>::rad2deg);
             R cl_, cr_, sl_, sr_;
