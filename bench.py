@@ -221,6 +221,10 @@ def other_workloads(args, local):
 
 
 DESCENT_BURN_IN = 640   # c3-descent: untimed steps before the warmup (a steady mix of episode phases)
+# c3: untimed steps before the warmup, so that the timed window sees resets at their stationary
+# rate (every episode of the uniform-action law ends within ~200 steps); --c3-burn-in 0 gives the
+# fresh-episode window of rounds 1-3, which the line also reports as `c3_fresh`
+C3_BURN_IN = 640
 
 
 def c3_actions(T, n, gen, device, descent):
@@ -255,12 +259,16 @@ def workload_counts(d, n, steps, lpe):
                     "balanced_rounds_per_wave_substep": d["balanced_rounds"] / (sub * 2 / 64),
                     "q_refined_frac": d["q_refined"] / q, "q_bisect_frac": d["q_bisect"] / q,
                     "wave_substeps_refined_frac": d["wave_substeps_refined"] / (sub * 2 / 64),
-                    "wave_substeps_bisect_frac": d["wave_substeps_bisect"] / (sub * 2 / 64)})
+                    "wave_substeps_bisect_frac": d["wave_substeps_bisect"] / (sub * 2 / 64),
+                    # wave sub-steps whose lanes hold both clamped-line and interior queries (each
+                    # such wave runs both evaluation paths one after the other)
+                    "wave_substeps_mixed_frac": d["wave_substeps_mixed"] / (sub * 2 / 64)})
     return out
 
 
-def run_c3(args, precision, local, rank, dist, descent=False, launch_base=0):
-    """One c3 (or c3-descent) measurement on this rank's handle.  Returns the raw timings."""
+def run_c3(args, precision, local, rank, dist, descent=False, launch_base=0, burn=None):
+    """One c3 (or c3-descent) measurement on this rank's handle, after `burn` untimed steps
+    (default: c3-descent's, or --c3-burn-in).  Returns the raw timings."""
     import torch
     import pdenv
     n = args.envs
@@ -271,7 +279,8 @@ def run_c3(args, precision, local, rank, dist, descent=False, launch_base=0):
         auto_reset=True, tilt_sigma_rad=0.0 if args.workload == "c2" else math.radians(1.0), seed=1234,
         env_offset=shard_offset(rank, n), integrator=args.integrator)
     env.flush_every = 16
-    burn = DESCENT_BURN_IN if descent else 0
+    if burn is None:
+        burn = DESCENT_BURN_IN if descent else args.c3_burn_in
     W = burn + args.warmup
     T = W + args.steps
     F = max(1, args.fuse)
@@ -431,6 +440,10 @@ def main():
     ap.add_argument("--fuse", type=int, default=128,
                     help="c3: env-steps per k_step launch (pd_step_n; 1 = one pd_step launch per step)")
     ap.add_argument("--graph", type=int, default=1, help="c5: replay the collection step as a HIP graph")
+    ap.add_argument("--c3-burn-in", type=int, default=C3_BURN_IN,
+                    help="c3: untimed env-steps before the warmup (steady state: resets at their stationary rate)")
+    ap.add_argument("--fresh", type=int, default=1,
+                    help="c3: also measure the fresh-episode window (no burn-in), reported as c3_fresh")
     ap.add_argument("--others", type=int, default=1,
                     help="c3 at one GPU: also run short c4 and c5 measurements (summarised in the line)")
     args = ap.parse_args()
@@ -476,6 +489,10 @@ def main():
     if args.workload == "c3" and args.descent:
         desc = run_c3(args, args.precision, local, rank, dist, descent=True, launch_base=base)
         base += desc["launches_total"]
+    fresh = None
+    if args.workload == "c3" and args.fresh and args.c3_burn_in > 0:
+        fresh = run_c3(args, args.precision, local, rank, dist, launch_base=base, burn=0)
+        base += fresh["launches_total"]
     other = None
     if args.secondary:
         other = run_c3(args, "f32" if args.precision == "f64" else "f64", local, rank, dist, descent=descent_main)
@@ -492,7 +509,9 @@ def main():
         pmc = load_pmc("pmc_c3_descent.json")
     summ = c3_summary(args, main_res, world, args.precision, pmc)
     wl = {"c3": "c3: 65536 envs/GPU, landing_burn_pure_throttle, rtd_rl reward, wind (percentile profile drawn "
-                "per reset + VK gusts below 15 km) + tilt, auto-reset, uniform random actions",
+                "per reset + VK gusts below 15 km) + tilt, auto-reset, uniform random actions" +
+                (f"; timed at steady state after {args.c3_burn_in} untimed burn-in + {args.warmup} warmup steps"
+                 if args.c3_burn_in > 0 else "; timed on fresh episodes (no burn-in)"),
           "c3-descent": f"c3-descent: the c3 configuration with the 3:1 high-throttle action mix, timed after "
                         f"{DESCENT_BURN_IN} burn-in + {args.warmup} warmup steps (episodes in every phase of the "
                         f"descent: gust band, landing logic)",
@@ -524,6 +543,14 @@ def main():
         ds["workload"] = (f"c3-descent: 3:1 high-throttle action mix, {DESCENT_BURN_IN} burn-in + {args.warmup} "
                           f"warmup steps, then {args.steps} timed")
         out["c3_descent"] = ds
+    if fresh is not None:
+        fs = c3_summary(args, fresh, world, args.precision)
+        out["c3_fresh"] = {"value": fs["value"], "ms_per_step": fs["ms_per_step"],
+                           "kernel_ms_per_step": fs["roofline"]["kernel_ms_per_step"],
+                           "roofline_frac": fs["roofline"]["frac"], "workload_counts": fs["workload_counts"],
+                           "launch_index": fs["launch_index"],
+                           "workload": f"c3 on fresh episodes: no burn-in, {args.warmup} warmup steps, then "
+                                       f"{args.steps} timed (every env's first episode, 30 km down)"}
     if other is not None:
         op = "f32" if args.precision == "f64" else "f64"
         out["secondary"] = {"dtype": op, "value": whole_job_rate(other["n"], world, args.steps, other["wall"]),

@@ -258,10 +258,11 @@ pd_status pd_pso_step(int64_t n_particles, int32_t dim, const double* fitness, d
                       double c2, uint64_t seed, uint32_t generation, uint64_t particle_offset,
                       float* position_f32, void* stream);
 /* Per subswarm s < n_swarms, the first particle of minimal fitness among those with swarm[p] ==
- * s (NumPy argmin order: a NaN first, ties to the lower index; the per-subswarm np.argmin of
- * particle_swarm_optimisation.py:437-444): min_fitness [n_swarms] and its position min_position
- * [n_swarms][dim] (from position [dim][n_particles]); +inf and zeros for a subswarm without
- * particles.  One workgroup per subswarm; no host synchronisation. */
+ * s: the result of particle_swarm_optimisation.py:437-441's sequential `if fitness <
+ * subswarm_best` over the subswarm's particles in order (a NaN fitness never wins, ties keep the
+ * lower index): min_fitness [n_swarms] and its position min_position [n_swarms][dim] (from
+ * position [dim][n_particles]); +inf and zeros for a subswarm with no particle of non-NaN fitness.
+ * A two-pass segmented argmin over blocks of 1 024 particles; no host synchronisation. */
 pd_status pd_pso_swarm_minima(int64_t n_particles, int32_t dim, int32_t n_swarms, const double* fitness,
                               const int32_t* swarm, const double* position, double* min_fitness,
                               double* min_position, void* stream);
@@ -329,11 +330,11 @@ pd_status pd_atmosphere(pd_env* env, const void* altitude, void* out, int64_t n,
  * 35 queries whose candidate neighbourhood was verified by the swap search, 36 queries evaluated
  * from a Taylor piece, 37 by the balanced chunk sums, 38 missed (device solve), 39 balanced-sum
  * rounds, 40 interior queries in a refined grid cell, 41 ... in a sub-cell split by a bisector,
- * 42 / 43 wave sub-steps with at least one such query, 44 queries evaluated from a cell piece.
- * Host sync. */
+ * 42 / 43 wave sub-steps with at least one such query, 44 queries evaluated from a cell piece,
+ * 45 wave sub-steps holding both clamped-line and interior queries.  Host sync. */
 #define PD_N_STATS 48
 pd_status pd_stats(pd_env* env, int64_t* out, int32_t n);
-/* Workload counting (pd_stats words 32-43) on (enable != 0) or off (the default) for the handle's
+/* Workload counting (pd_stats words 32-45) on (enable != 0) or off (the default) for the handle's
  * following step launches with 2 lanes per env (the default above 16 384 envs; other launches
  * count nothing).  A diagnostic: on, the launches run a counting instantiation of the step kernel
  * (a ballot and an LDS add per counter per sub-step, a few per cent slower); off, the product

@@ -42,5 +42,8 @@ PD_INST_STEP(1)
 // (policy rollouts run at 2 lanes per env: the per-lane actor + the LPE 2 table path fit the
 // register file without scratch, which the LPE 4/8 variants did not)
 template void launch_policy_lpe<KR, PD_KPH, KW, 2>(const StepArgs<KR>&, int64_t, hipStream_t);
+// (LPE 4/8: the lanes-per-env sweep of the policy rollouts, PDENV_PLPE)
+template void launch_policy_lpe<KR, PD_KPH, KW, 4>(const StepArgs<KR>&, int64_t, hipStream_t);
+template void launch_policy_lpe<KR, PD_KPH, KW, 8>(const StepArgs<KR>&, int64_t, hipStream_t);
 #endif
 }  // namespace pd

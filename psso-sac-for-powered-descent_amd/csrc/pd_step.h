@@ -86,7 +86,8 @@ enum Stat {
     kStWRefined = kStWork + 10,  // wave sub-steps with at least one refined-cell query
     kStWBisect = kStWork + 11,   // wave sub-steps with at least one bisector query
     kStQCell = kStWork + 12,     // LPE 2 queries evaluated from a cell piece
-    kNWork = 13
+    kStWMixed = kStWork + 13,    // wave sub-steps holding both clamped-line and interior queries
+    kNWork = 14
 };
 
 // Per-wave workload counts in LDS (nullptr: counting off, the launch pays one scalar branch per

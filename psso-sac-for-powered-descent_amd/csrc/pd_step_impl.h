@@ -492,10 +492,14 @@ __device__ __forceinline__ int rbf_lookup(const AT& a, DP<R>& P, int table, cons
     } else if (use_grid) {
         bool fast = false;
         if (fine_path) {
-            // a piece every point of the sub-cell uses (the margin keeps queries on a sub-cell
-            // edge on the record path), or the side of its bisector, trusted off the line
+            // a piece every point of the sub-cell uses, or the side of its bisector, trusted off
+            // the line.  The margin is the record path's, so that both paths trust the same
+            // queries: a refined cell's sub-cell (and any bisector) in sub-cell coordinates, a
+            // non-refined exact cell in cell coordinates (its sub-cell edges are no boundary)
             const R eps = R(1e-9);
-            const bool inside = fsm > eps && R(1) - fsm > eps && fsa > eps && R(1) - fsa > eps;
+            const bool inside = (fe & kFineRefined)
+                ? (fsm > eps && R(1) - fsm > eps && fsa > eps && R(1) - fsa > eps)
+                : (um > eps && R(1) - um > eps && ua > eps && R(1) - ua > eps);
             int cpf = -1;
             if (fe & kFinePiece) cpf = (int)(fe & kFineIndex);
             else if (fe & kFineBisect) {
@@ -822,6 +826,7 @@ __device__ __forceinline__ R rbf2(const AT& a, DP<R>& P, int table, const TabVie
         wc.add(kStQBisect - kStWork, act && tr.bisect);
         wc.add_n(kStWRefined - kStWork, __ballot(act && tr.refined) != 0ull);
         wc.add_n(kStWBisect - kStWork, __ballot(act && tr.bisect) != 0ull);
+        wc.add_n(kStWMixed - kStWork, (__ballot(act && tr.line) != 0ull) && (__ballot(act && !tr.line) != 0ull));
     }
     if (__ballot(miss)) {
         R mv = rbf_miss_wave<R>(a, P, table, t.smach, cache.key, M, aq, 0, 1, miss);

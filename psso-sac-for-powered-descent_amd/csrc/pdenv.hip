@@ -1445,11 +1445,21 @@ template <typename R> void dispatch_step(const pd_env* e, const StepArgs<R>& a, 
     else { if (w) launch_lpe<R, 2, 0, true>(l, a, s); else launch_lpe<R, 2, 0, false>(l, a, s); }
 }
 
-// Policy rollouts run at 2 lanes per env whatever the handle's step LPE (the per-lane actor and
-// the LPE 2 table path fit 256 VGPRs without scratch; the LPE 4/8 variants spilled 36-172 B)
-constexpr int kPolicyLpe = 2;
+// Policy rollouts run at 2 lanes per env whatever the handle's step LPE: the per-lane actor and
+// the LPE 2 table path (Taylor lines, cell pieces) fit 256 VGPRs without scratch.  PDENV_PLPE=4/8
+// (experiments, the c4 lanes-per-env sweep) runs the LPE 4/8 instantiations, whose tables take the
+// split payload sums.
+int policy_lpe() {
+    const char* v = getenv("PDENV_PLPE");
+    const int l = v && *v ? atoi(v) : 2;
+    return l == 4 || l == 8 ? l : 2;
+}
 template <typename R, int PH, bool W> void launch_policy(const StepArgs<R>& a, int64_t n_launch, hipStream_t s) {
-    launch_policy_lpe<R, PH, W, kPolicyLpe>(a, n_launch, s);
+    switch (policy_lpe()) {
+        case 4: launch_policy_lpe<R, PH, W, 4>(a, n_launch, s); break;
+        case 8: launch_policy_lpe<R, PH, W, 8>(a, n_launch, s); break;
+        default: launch_policy_lpe<R, PH, W, 2>(a, n_launch, s); break;
+    }
 }
 
 template <typename R> void launch_insert(pd_env* e, hipStream_t s) {
@@ -1517,7 +1527,7 @@ pd_status rollout_policy_impl(pd_env* e, const float* w, int32_t max_steps, void
     int dev_cus = 256;
     (void)hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, e->device);
     const char* force = getenv("PDENV_COMPACT");
-    a.use_list = force && *force ? (atoi(force) != 0) : (N * kPolicyLpe > (int64_t)dev_cus * 512);
+    a.use_list = force && *force ? (atoi(force) != 0) : (N * policy_lpe() > (int64_t)dev_cus * 512);
     int64_t n_launch = N;
     int checks = 0;
     // F policy steps per launch (an episode that ends inside a launch is stored at its last step

@@ -14,6 +14,8 @@
 // pd_rollout_policy reads.  HBM-bound: 52 B per (particle, parameter).
 #include <hip/hip_runtime.h>
 
+#include <mutex>
+
 #include "../../include/pdenv.h"
 #include "pd_common.h"
 
@@ -58,29 +60,19 @@ __global__ __launch_bounds__(kPsoBlock) void k_pso_best(int64_t P, const double*
     if (p < P && fit[p] < pbf[p]) pbf[p] = fit[p];
 }
 
-// NumPy's argmin order: a NaN beats everything (the first NaN), else the smaller value, ties to
-// the lower index
+// The reference's sequential rule (:437-441): `if fitness < subswarm_best`, particle by particle,
+// so a NaN fitness never wins (every comparison with it is false) and on ties the first particle
+// stays.  Here: a NaN loses to anything, else the smaller value, ties to the lower index.
 __device__ __forceinline__ bool argmin_better(double a, int64_t ia, double b, int64_t ib) {
     const bool na = a != a, nb = b != b;
-    if (na || nb) return na && (!nb || ia < ib);
+    if (na || nb) return !na && nb;
     return a < b || (a == b && ia < ib);
 }
 
-// Per subswarm s (one workgroup each): the first particle of minimal fitness among those with
-// swarm[p] == s, its fitness and position (:437-441's np.argmin per subswarm); +inf and a zero
-// position for a subswarm with no particle here.
-__global__ __launch_bounds__(kPsoBlock) void k_swarm_minima(int64_t P, int D, const double* __restrict__ fit,
-                                                            const int32_t* __restrict__ swarm,
-                                                            const double* __restrict__ x, double* __restrict__ min_f,
-                                                            double* __restrict__ min_pos) {
-    __shared__ double sf[kPsoBlock];
-    __shared__ int64_t si[kPsoBlock];
-    const int s = blockIdx.x;
-    double bf = __builtin_inf();
-    int64_t bi = -1;
-    for (int64_t p = threadIdx.x; p < P; p += kPsoBlock)
-        if (swarm[p] == s && (bi < 0 || argmin_better(fit[p], p, bf, bi))) { bf = fit[p]; bi = p; }
-    sf[threadIdx.x] = bf; si[threadIdx.x] = bi;
+// Block-wide argmin of (f, i) pairs (i < 0: none), LDS tree with the rule above; every thread
+// gets the winner.
+__device__ __forceinline__ void block_argmin(double& f, int64_t& i, double* sf, int64_t* si) {
+    sf[threadIdx.x] = f; si[threadIdx.x] = i;
     __syncthreads();
     for (int o = kPsoBlock / 2; o > 0; o >>= 1) {
         if (threadIdx.x < o) {
@@ -92,9 +84,62 @@ __global__ __launch_bounds__(kPsoBlock) void k_swarm_minima(int64_t P, int D, co
         }
         __syncthreads();
     }
-    const int64_t i = si[0];
-    if (threadIdx.x == 0) min_f[s] = i >= 0 ? sf[0] : __builtin_inf();
-    for (int d = threadIdx.x; d < D; d += kPsoBlock) min_pos[(int64_t)s * D + d] = i >= 0 ? x[(int64_t)d * P + i] : 0.0;
+    f = sf[0]; i = si[0];
+    __syncthreads();
+}
+
+// Segmented argmin in two passes (the subswarm minima of :437-441).  Pass 1: block b takes
+// particles [b C, (b + 1) C) (C = kMinChunk, four per thread, coalesced) and writes, per subswarm
+// s, its first particle of minimal non-NaN fitness (index -1: none) to part[b][s].
+constexpr int kMinPer = 4;
+constexpr int kMinChunk = kMinPer * kPsoBlock;
+__global__ __launch_bounds__(kPsoBlock) void k_swarm_minima_part(int64_t P, int S, const double* __restrict__ fit,
+                                                                 const int32_t* __restrict__ swarm,
+                                                                 double* __restrict__ part_f,
+                                                                 int64_t* __restrict__ part_i) {
+    __shared__ double sf[kPsoBlock];
+    __shared__ int64_t si[kPsoBlock];
+    const int64_t base = (int64_t)blockIdx.x * kMinChunk + threadIdx.x;
+    double f[kMinPer];
+    int32_t sw[kMinPer];
+#pragma unroll
+    for (int k = 0; k < kMinPer; ++k) {
+        const int64_t p = base + (int64_t)k * kPsoBlock;
+        sw[k] = p < P ? swarm[p] : -1;
+        f[k] = p < P ? fit[p] : 0.0;
+    }
+    for (int s = 0; s < S; ++s) {
+        double bf = 0.0;
+        int64_t bi = -1;
+#pragma unroll
+        for (int k = 0; k < kMinPer; ++k)   // (increasing index: strictly better replaces)
+            if (sw[k] == s && f[k] == f[k] && (bi < 0 || f[k] < bf)) { bf = f[k]; bi = base + (int64_t)k * kPsoBlock; }
+        block_argmin(bf, bi, sf, si);
+        if (threadIdx.x == 0) { part_f[(int64_t)blockIdx.x * S + s] = bf; part_i[(int64_t)blockIdx.x * S + s] = bi; }
+    }
+}
+
+// Pass 2, one workgroup per subswarm s: the winner over the G pass-1 blocks (lower block = lower
+// index, so the rule above keeps the first particle), its fitness and position; +inf and a zero
+// position when no particle of s has a non-NaN fitness (the reference then keeps its best).
+__global__ __launch_bounds__(kPsoBlock) void k_swarm_minima_final(int64_t P, int D, int S, int64_t G,
+                                                                  const double* __restrict__ part_f,
+                                                                  const int64_t* __restrict__ part_i,
+                                                                  const double* __restrict__ x, double* __restrict__ min_f,
+                                                                  double* __restrict__ min_pos) {
+    __shared__ double sf[kPsoBlock];
+    __shared__ int64_t si[kPsoBlock];
+    const int s = blockIdx.x;
+    double bf = 0.0;
+    int64_t bi = -1;
+    for (int64_t b = threadIdx.x; b < G; b += kPsoBlock) {
+        const int64_t i2 = part_i[b * S + s];
+        const double f2 = part_f[b * S + s];
+        if (i2 >= 0 && (bi < 0 || argmin_better(f2, i2, bf, bi))) { bf = f2; bi = i2; }
+    }
+    block_argmin(bf, bi, sf, si);
+    if (threadIdx.x == 0) min_f[s] = bi >= 0 ? bf : __builtin_inf();
+    for (int d = threadIdx.x; d < D; d += kPsoBlock) min_pos[(int64_t)s * D + d] = bi >= 0 ? x[(int64_t)d * P + bi] : 0.0;
 }
 
 // :442-444 and :474-477 (one workgroup): subswarm s takes a strictly better minimum; then the
@@ -126,6 +171,14 @@ namespace pd {
 pd_status set_error(pd_status s, const char* m);   // pdenv.hip: the pd_last_error() message
 }
 
+namespace {
+// pd_pso_swarm_minima's pass-1 partials, per device
+constexpr int kMaxDevices = 64;
+struct MinScratch { double* f = nullptr; int64_t* i = nullptr; size_t cap = 0; };
+std::mutex g_min_mu;
+MinScratch g_min[kMaxDevices];
+}  // namespace
+
 extern "C" {
 
 pd_status pd_pso_step(int64_t n_particles, int32_t dim, const double* fitness, double* best_fitness, double* position,
@@ -152,8 +205,31 @@ pd_status pd_pso_swarm_minima(int64_t n_particles, int32_t dim, int32_t n_swarms
     if (n_particles < 0 || dim <= 0 || n_swarms <= 0 || n_swarms > 65535 || !min_fitness || !min_position ||
         (n_particles > 0 && (!fitness || !swarm || !position)))
         return set_error(PD_ERR_INVALID, "pd_pso_swarm_minima: bad arguments");
-    hipLaunchKernelGGL(k_swarm_minima, dim3((unsigned)n_swarms), dim3(kPsoBlock), 0, (hipStream_t)stream, n_particles,
-                       dim, fitness, swarm, position, min_fitness, min_position);
+    const int64_t G = (n_particles + kMinChunk - 1) / kMinChunk;
+    // pass-1 partials: a per-device scratch grown on demand (calls on one device are stream-ordered
+    // by the caller; the PSO driver issues them on one stream)
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices)
+        return set_error(PD_ERR_HIP, "pd_pso_swarm_minima: no device");
+    const size_t need = (size_t)(G > 0 ? G : 1) * (size_t)n_swarms;
+    {
+        std::lock_guard<std::mutex> lk(g_min_mu);
+        MinScratch& m = g_min[dev];
+        if (m.cap < need) {
+            if (m.f) { (void)hipFree(m.f); (void)hipFree(m.i); m.f = nullptr; m.i = nullptr; m.cap = 0; }
+            if (hipMalloc((void**)&m.f, need * sizeof(double)) != hipSuccess ||
+                hipMalloc((void**)&m.i, need * sizeof(int64_t)) != hipSuccess)
+                return set_error(PD_ERR_HIP, "pd_pso_swarm_minima: scratch allocation failed");
+            m.cap = need;
+        }
+    }
+    MinScratch& m = g_min[dev];
+    hipStream_t s = (hipStream_t)stream;
+    if (G > 0)
+        hipLaunchKernelGGL(k_swarm_minima_part, dim3((unsigned)G), dim3(kPsoBlock), 0, s, n_particles, n_swarms,
+                           fitness, swarm, m.f, m.i);
+    hipLaunchKernelGGL(k_swarm_minima_final, dim3((unsigned)n_swarms), dim3(kPsoBlock), 0, s, n_particles, dim,
+                       n_swarms, G, m.f, m.i, position, min_fitness, min_position);
     if (hipGetLastError() != hipSuccess) return set_error(PD_ERR_HIP, "pd_pso_swarm_minima: launch failed");
     return PD_OK;
 }

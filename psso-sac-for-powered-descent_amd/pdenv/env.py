@@ -392,7 +392,7 @@ class PoweredDescentEnv:
 
     WORK_COUNTERS = ("gust_substeps", "resets", "q_line", "q_verified", "q_taylor", "q_balanced", "q_miss",
                      "balanced_rounds", "q_refined", "q_bisect", "wave_substeps_refined", "wave_substeps_bisect",
-                     "q_cell")
+                     "q_cell", "wave_substeps_mixed")
 
     def stats(self):
         """Device statistics words (pd_stats): misses, NaN events, table entries, dropped queue

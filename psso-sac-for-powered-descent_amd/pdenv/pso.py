@@ -259,9 +259,11 @@ class ParticleSubswarmOptimisationGPU:
         self.sbf_t[mv] = torch.where(fit < old, fit, old)
 
     def _swarm_minima(self, fit):
-        """Per subswarm: (min fitness, its position) over all ranks, first particle on ties -- a
-        segmented argmin on the device (pd_pso_swarm_minima: one workgroup per subswarm), no host
-        synchronisation.  A subswarm with no particle here reports +inf."""
+        """Per subswarm: (min fitness, its position) over all ranks, first particle on ties, a NaN
+        fitness never chosen (the reference's sequential strict '<') -- a two-pass segmented
+        argmin on the device (pd_pso_swarm_minima), no host synchronisation.  A subswarm with no
+        particle of non-NaN fitness here reports +inf (so a rank's minima never hold a NaN, and
+        torch.argmin over the ranks picks the lowest rank among equal minima)."""
         f = torch.empty(self.S, dtype=torch.float64, device=self.device)
         pos = torch.empty(self.S, self.D, dtype=torch.float64, device=self.device)
         L.check(self.lib.pd_pso_swarm_minima(self.P, self.D, self.S, _ptr(fit) if self.P else None,

@@ -224,6 +224,41 @@ def test_fine_index_bit_identical(pd):
     assert torch.equal(fine.state, rec.state)
 
 
+def test_fine_index_cell_edge_margins(pd):
+    """Queries placed a fraction of the 1e-9 trust margin inside an interior cell's Mach edge
+    (2e-10 .. 8e-10 cell widths, both edges, 120 cells): the fine index applies the record
+    path's margin in the coordinates the record path uses (cell coordinates for a non-refined
+    cell), so one step from these states is bit-identical with and without it (PDENV_FINE=0).
+    With the sub-cell margin on every word (round 3) the queries in (1.25e-10, 1e-9] cell widths
+    of a non-refined cell's edge took its piece with the index and the payload sums without."""
+    import torch
+    probe = make(pd, 1)
+    y = 12000.0
+    a = float(probe.atmosphere(torch.tensor([y], dtype=torch.float64, device="cuda"))[2][0])
+    w = 10.0 / 800.0                                            # C_D / C_L interior cells in Mach
+    cells = np.arange(40, 760, 6)
+    frac = np.array([2e-10, 5e-10, 8e-10, 1 - 2e-10, 1 - 5e-10, 1 - 8e-10])
+    M = ((cells[:, None] + frac[None, :]) * w).ravel()
+    n = len(M)
+    s = np.tile(probe.state.cpu().numpy()[0], (n, 1))
+    s[:, 1], s[:, 2], s[:, 3] = y, 0.0, -M * a                  # speed = |vy| exactly, Mach ~ M
+    s[:, 6] = 1.5 * np.pi                                       # gamma of a vertical descent
+    ae = np.radians(0.05)                                       # both tables interior (|deg(ae)| < radians(10))
+    s[:, 4] = s[:, 6] - np.pi - ae                              # alpha_eff = gamma - theta - pi
+    s[:, 7] = s[:, 4] - s[:, 6]
+    outs = []
+    for fine in ("1", "0"):
+        os.environ["PDENV_FINE"] = fine
+        try:
+            env = make(pd, n, lanes_per_env=2)
+        finally:
+            del os.environ["PDENV_FINE"]
+        env.set_state(torch.tensor(s, device="cuda"))
+        o = env.step(torch.zeros(n, 1, device="cuda"))
+        outs.append((env.state.clone(), o[1].clone()))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+
+
 def test_env_shards_equal_single_handle(pd):
     """Multi-GPU layout on one device: two handles over contiguous shards (env_offset = rank*n,
     as bench.py assigns them) reproduce the single N-env handle bit for bit, wind + tilt +
@@ -530,22 +565,29 @@ def test_pso_step_matches_numpy(pd):
 
 
 def test_pso_swarm_minima_and_bests_vs_numpy(pd):
-    """pd_pso_swarm_minima (NumPy argmin order per subswarm: a NaN first, ties to the lower
-    index, +inf for an empty subswarm) and pd_pso_update_bests (strictly better replaces; the
-    first subswarm holding the minimum feeds the global best) against NumPy."""
+    """pd_pso_swarm_minima (the reference's sequential `if fitness < subswarm_best` per subswarm,
+    particle_swarm_optimisation.py:437-441: a NaN never wins, ties keep the lower index, +inf for
+    a subswarm with no particle of non-NaN fitness) and pd_pso_update_bests (strictly better
+    replaces; the first subswarm holding the minimum feeds the global best) against a Python
+    restatement of that loop.  Sizes cross the 1 024-particle blocks of the two-pass argmin."""
     import torch
     from pdenv import _lib as L
     from pdenv.env import _ptr
     lib = L.load()
     rng = np.random.default_rng(12)
-    for trial in range(6):
+    for trial in range(8):
         P, D, S = int(rng.integers(1, 5000)), int(rng.integers(1, 400)), int(rng.integers(1, 6))
+        if trial == 6:
+            P = 40000                                           # 40 pass-1 blocks
         fit = np.round(rng.normal(size=P), 1)                  # many ties
         if trial % 2:
             fit[rng.integers(0, P, 3)] = np.nan
+            fit[0] = np.nan                                     # a NaN first in its subswarm
         sw = rng.integers(0, S, P).astype(np.int32)
         if trial == 3:
             sw[sw == S - 1] = 0                                 # an empty subswarm
+        if trial == 5 and S > 1:
+            fit[sw == 1] = np.nan                               # a subswarm of NaNs only
         x = rng.normal(size=(D, P))
         T = {k: torch.tensor(v, device="cuda") for k, v in dict(fit=fit, sw=sw, x=x).items()}
         mf = torch.empty(S, dtype=torch.float64, device="cuda")
@@ -558,11 +600,13 @@ def test_pso_swarm_minima_and_bests_vs_numpy(pd):
         torch.cuda.synchronize()
         ef, ep = np.full(S, np.inf), np.zeros((S, D))
         for s in range(S):
-            idx = np.flatnonzero(sw == s)
-            if len(idx):
-                i = idx[np.argmin(fit[idx])]
-                ef[s], ep[s] = fit[i], x[:, i]
-        assert np.array_equal(mf.cpu().numpy(), ef, equal_nan=True) and np.array_equal(mp.cpu().numpy(), ep)
+            best, bi = np.inf, -1
+            for p in np.flatnonzero(sw == s):                   # the reference's loop
+                if bi < 0 and not np.isnan(fit[p]) or fit[p] < best:
+                    best, bi = fit[p], p
+            if bi >= 0:
+                ef[s], ep[s] = best, x[:, bi]
+        assert np.array_equal(mf.cpu().numpy(), ef) and np.array_equal(mp.cpu().numpy(), ep)
         for s in range(S):
             if ef[s] < sbf0[s]:
                 sbf0[s], sb0[s] = ef[s], ep[s]

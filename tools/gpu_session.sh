@@ -31,6 +31,10 @@ for s in $STAGES; do
     profdrv) stage profdrv 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/profdrv -o run -- python3 bench.py --steps 20 --warmup 5 --cpu-baseline 0 --secondary 0 --others 0 --descent 1 ;;
     prof32) stage prof32 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof32 -o run -- python3 bench.py --steps 96 --warmup 16 --cpu-baseline 0 --secondary 0 --others 0 --precision f32 ;;
     sweep) stage sweep 600 python tools/sweep.py ;;
+    plpe) stage plpe 600 python tools/policy_lpe_sweep.py ;;
+    c4) stage c4 600 python bench.py --workload c4 ;;
+    c5) stage c5 600 python bench.py --workload c5 ;;
+    c3d) stage c3d 600 python bench.py --workload c3-descent --secondary 0 --cpu-baseline 0 ;;
     pmc) stage pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run -- python3 bench.py --steps 32 --warmup 16 --cpu-baseline 0 --secondary 0 --others 0
          stage pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o run -- python3 bench.py --steps 32 --warmup 16 --cpu-baseline 0 --secondary 0 --others 0 ;;
     pmc32) stage pmc_fetch32 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch32 -o run -- python3 bench.py --steps 32 --warmup 16 --cpu-baseline 0 --secondary 0 --others 0 --precision f32
