@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define PD_ABI_VERSION 6   /* 4: pd_config.integrator (was padding); 5: pd_count_work, pd_step_sac; 6: cell pieces (pd_cell_piece_info, stats word 44) */
+#define PD_ABI_VERSION 7   /* 4: pd_config.integrator (was padding); 5: pd_count_work, pd_step_sac; 6: cell pieces (pd_cell_piece_info, stats word 44); 7: pd_step_sac_ring, pd_sac_actor, stats word 45 */
 #define PD_MAX_PTS 256      /* aero scatter points per table */
 #define PD_MAX_COLS 5       /* AoA columns per aero table */
 #define PD_MAX_TAB 64       /* grid-fin table length */
@@ -224,6 +224,36 @@ pd_status pd_step_n(pd_env* env, const void* actions, int32_t n_steps, void* obs
 pd_status pd_step_sac(pd_env* env, const float* mean, const float* log_std, int32_t head_stride, const float* eps,
                       float log_std_min, float log_std_max, float max_action, float* action, float* slab, float* obs32,
                       void* stream);
+/* pd_step_sac with the rest of the collection step folded into the same launch (c5):
+ *  heads   : [N][2A] float32, mean | log_std as Actor.forward's two heads leave them (unclamped),
+ *            e.g. from pd_sac_actor
+ *  deterministic != 0: a = tanh(mean) * max_action; else eps ~ N(0, 1) is drawn in the kernel
+ *            (torch.randn's role in Normal.rsample, sac_pytorch.py:170-172): Philox4x32-10 keyed
+ *            by the handle's seed, counter (env, episode, step, tag 19 + a/2), Box-Muller as the
+ *            wind gusts; eps_out [N][A] (may be NULL) receives the draws
+ *  ring    : the replay buffer's transition rows [capacity][2S + A + 2] float32 (sac_pytorch.py:
+ *            12-49); with ring_state != NULL env i's row goes to (ring_state[0] + i) mod capacity,
+ *            priorities[row] = *max_priority (PrioritizedReplayBuffer.add, sac_pytorch.py:76-83;
+ *            priorities may be NULL), and the launch's last workgroup sets ring_state[0] (position)
+ *            += N mod capacity, ring_state[1] (size) = min(size + N, capacity); ring_state[2] is
+ *            its workgroup counter and must be 0 between launches (capacity >= N).  With
+ *            ring_state NULL, ring is a [N][2S + A + 2] slab (pd_step_sac's).
+ *  action, obs32: as pd_step_sac.  No host synchronisation; the position lives on the device, so
+ *  a captured graph replays correctly. */
+pd_status pd_step_sac_ring(pd_env* env, const float* heads, int32_t deterministic, float log_std_min,
+                           float log_std_max, float max_action, float* eps_out, float* action, float* ring,
+                           int64_t capacity, long long* ring_state, float* priorities, const float* max_priority,
+                           float* obs32, void* stream);
+/* The SAC Actor's forward pass (sac_pytorch.py:129-159) for n float32 observations [n][state_dim]
+ * in one launch: Linear(S, H) ReLU, (n_hidden_layers - 1) x [Linear(H, H) ReLU] on MFMA
+ * (v_mfma_f32_16x16x4_f32), then the mean and log_std heads into heads [n][2A] (mean | log_std,
+ * unclamped: pd_step_sac_ring clamps).  params: a host array of 2 (n_hidden_layers + 2) device
+ * pointers, the torch parameters in named_parameters() order (weight [out][in] row-major, bias):
+ * shared_net layers, then mean, then log_std.  hidden 128, 256 or 512 (else PD_ERR_UNSUPPORTED),
+ * state_dim <= 16, action_dim <= 8, n_hidden_layers <= 8.  f32 sums in another order than
+ * torch's GEMMs: equal to f32 rounding.  Runs on the current HIP device. */
+pd_status pd_sac_actor(int64_t n, int32_t state_dim, int32_t hidden, int32_t n_hidden_layers, int32_t action_dim,
+                       const float* obs, const float* const* params, float* heads, void* stream);
 /* Multi-step rollout with device-resident actions [T][N][A]: the fused launches of pd_step_n
  * (per-step launches for the other phases), rewards accumulated into reward_sum [N] (may be
  * NULL), no per-step outputs.  No host synchronisation. */

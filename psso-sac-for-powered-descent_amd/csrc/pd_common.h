@@ -332,6 +332,7 @@ constexpr uint32_t kTagWindSub = 0;   // +substep 0..3
 constexpr uint32_t kTagReset = 16;
 constexpr uint32_t kTagTilt = 17;
 constexpr uint32_t kTagProf = 18;      // the wind percentile (its own draw: independent of the sigmas)
+constexpr uint32_t kTagSacEps = 19;    // +a/2: pd_step_sac_ring's rsample noise of action components a, a+1
 // randint(50, 99) - 50 from one Philox word: floor(49 u / 2^32) (multiply-shift; bias < 1.2e-8)
 PD_HD int prof_draw(uint32_t u) { return (int)(((uint64_t)u * 49u) >> 32); }
 
@@ -360,6 +361,53 @@ PD_HD void sincos_fd(double x, double& s, double& c) {
     const int q = (int)(long long)k & 3;
     s = q == 0 ? sn : (q == 1 ? cs : (q == 2 ? -sn : -cs));
     c = q == 0 ? cs : (q == 1 ? -sn : (q == 2 ? -cs : sn));
+}
+
+// atan2(y, x) in binary64: fdlibm's e_atan2.c / s_atan.c (public domain; the same reduction
+// intervals, polynomial and atan(c) hi/lo pairs) with the ratio and its reduction fused into ONE
+// division: for t = |y/x| in interval id, atan(t) = atan(c_id) + atan(N/D) with
+//   id -1 (t < 7/16)        N = |y|,               D = |x|
+//   id 0  (t < 11/16)       N = 2|y| - |x|,        D = 2|x| + |y|          (c = 1/2)
+//   id 1  (t < 19/16)       N = |y| - |x|,         D = |y| + |x|           (c = 1)
+//   id 2  (t < 39/16)       N = fma(-1.5, |x|, |y|), D = fma(1.5, |y|, |x|) (c = 3/2)
+//   id 3                    N = -|x|,              D = |y|                 (c = inf)
+// (fdlibm divides y/x first and then reduces the rounded ratio: a second division and one more
+// rounding; the numerators above are exact by Sterbenz's lemma or one fused rounding).  Then
+// fdlibm's quadrant rule.  <= 1 ulp against glibc's atan2 (tests/test_atan2.py, 4e6 arguments
+// over the descent's range and beyond); about half the device library's instructions.  Zeros,
+// infinities and NaNs take the library atan2.
+PD_HD double atan2_fd(double y, double x) {
+    const double ax = fabs(x), ay = fabs(y);
+    if (!(ax > 0.0 && ay > 0.0 && ax < __builtin_huge_val() && ay < __builtin_huge_val())) return atan2(y, x);
+    const int id = ay < 0.4375 * ax ? -1 : (ay < 0.6875 * ax ? 0 : (ay < 1.1875 * ax ? 1 : (ay < 2.4375 * ax ? 2 : 3)));
+    double n, d, hi, lo;
+    if (id < 0) { n = ay; d = ax; hi = 0.0; lo = 0.0; }
+    else if (id == 0) { n = 2.0 * ay - ax; d = 2.0 * ax + ay; hi = 4.63647609000806093515e-01; lo = 2.26987774529616870924e-17; }
+    else if (id == 1) { n = ay - ax; d = ay + ax; hi = 7.85398163397448278999e-01; lo = 3.06161699786838301793e-17; }
+    else if (id == 2) { n = fma(-1.5, ax, ay); d = fma(1.5, ay, ax); hi = 9.82793723247329054082e-01; lo = 1.39033110312309984516e-17; }
+    else { n = -ax; d = ay; hi = 1.57079632679489655800e+00; lo = 6.12323399573676603587e-17; }
+    const double t = n / d;
+    // the quotient's rounding error, (n - t d) / d (exact remainder by one FMA; the reciprocal
+    // only needs a few bits: the term is below half an ulp of t)
+    const double et = fma(-t, d, n) * (1.0 / d);
+    const double z = t * t, w = z * z;
+    const double s1 = z * (3.33333333333329318027e-01 + w * (1.42857142725034663711e-01 + w * (9.09088713343650656196e-02 +
+                      w * (6.66107313738753120669e-02 + w * (4.97687799461593236017e-02 + w * 1.62858201153657823623e-02)))));
+    const double s2 = w * (-1.99999999998764832476e-01 + w * (-1.11111104054623557880e-01 + w * (-7.69187620504482999495e-02 +
+                      w * (-5.83357013379057348645e-02 + w * -3.65315727442169155270e-02))));
+    // atan(|y / x|) = hi + t + (lo + et - t (s1 + s2)) as a double-double (ah, al): hi + t by
+    // TwoSum, the small terms added to its error
+    const double sh = hi + t, sb = sh - hi;
+    const double se = (hi - (sh - sb)) + (t - sb);
+    const double small = se + ((lo + et) - t * (s1 + s2));
+    const double ah = sh + small, al = small - (ah - sh);
+    const double pi = 3.1415926535897931160e+00, pi_lo = 1.2246467991473531772e-16;
+    if (x > 0.0) return y > 0.0 ? ah + al : -(ah + al);
+    // x < 0: pi - atan (y > 0) or atan - pi (y < 0), again as TwoSum + the low parts
+    const double ph = pi - ah, pb = ph - pi;
+    const double pe = (pi - (ph - pb)) + (-ah - pb);
+    const double r = ph + (pe + (pi_lo - al));
+    return y > 0.0 ? r : -r;
 }
 
 // Two standard normals from one Philox4x32-10 block by Box-Muller in binary64:

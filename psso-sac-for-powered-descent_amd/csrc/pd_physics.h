@@ -19,6 +19,33 @@ template <> struct Cst<float> {
     static constexpr float inf = __builtin_huge_valf();
 };
 
+// a / b for a divisor known ahead of the call -- a literal or a per-handle parameter -- given
+// rb = RN(1/b), its correctly rounded reciprocal (a compile-time or host division).  Markstein's
+// correction step returns the IEEE quotient RN(a / b): with rb within half an ulp of 1/b,
+// q = RN(a rb) is within one ulp of a/b, r = a - b q is exact (one FMA) and RN(q + r rb) = RN(a/b)
+// (Markstein's theorem; finite a and b away from underflow and overflow, as every divisor here
+// is).  The last step is computed negated, -RN(-r rb - q), so that a zero numerator keeps its
+// sign.  Three VALU operations, three deep, where a general division is the ten-deep
+// v_div_scale / v_rcp / Newton / v_div_fmas / v_div_fixup sequence.  tests/test_markstein.py
+// checks it bit for bit against IEEE division for every divisor it replaces.  PD_MARKSTEIN=0
+// (experiments) divides.
+#ifndef PD_MARKSTEIN
+#define PD_MARKSTEIN 1
+#endif
+template <typename R> __device__ __forceinline__ R div_known(R a, R b, R rb) {
+#if PD_MARKSTEIN
+    const R q = a * rb;
+    const R r = fma(-b, q, a);
+    return -fma(-r, rb, -q);
+#else
+    (void)rb;
+    return a / b;
+#endif
+}
+// the reciprocal of a literal divisor, folded at compile time in R's precision
+template <typename R> constexpr R rcp_c(R b) { return R(1) / b; }
+#define PD_DIVC(R_, a, b) div_known<R_>((a), R_(b), rcp_c<R_>(R_(b)))
+
 constexpr int kLineMax = 96;   // breakpoints per clamped query line
 // line search buckets: Mach [0, 10) in kLineBuckets; bucket b's breakpoint index range (lo, hi),
 // lo = #{bp < b w - 1e-4}, hi = #{bp < (b + 1) w + 1e-4}, packed lo | hi << 8
@@ -77,6 +104,9 @@ template <typename R> struct DevParams {
     LogTable logtab;   // log_tab cells (pd_common.h): the Box-Muller draws (oracle-restated)
     LogTableD logtab_d;   // eval_log cells, staged into LDS by the step kernel
     R y0_rl, m0_rl;
+    // correctly rounded reciprocals of the divisors above (div_known): 1 / m_prop0, y0_rl, m0_rl,
+    // norm_y, norm_vy, norm_x, norm_vx
+    R inv_m_prop0, inv_y0_rl, inv_m0_rl, inv_norm_y, inv_norm_vy, inv_norm_x, inv_norm_vx;
     // neighbourhood hash tables
     const unsigned long long* keys_cd;
     const unsigned long long* keys_cl;
@@ -202,6 +232,18 @@ template <> __device__ __forceinline__ void pd_sincos<double>(double x, double& 
     sincos_fd(x, s, c);
 }
 
+// ---------------------------------------------------------------- flight-path angle
+// gamma = atan2(vy, vx) (rockets_physics.py:631): binary64 by atan2_fd (pd_common.h; <= 1 ulp of
+// glibc's, about half the device library's instructions), binary32 by the device library.
+// PD_ATAN2_FD=0 (experiments): the device library's atan2 for both.
+#ifndef PD_ATAN2_FD
+#define PD_ATAN2_FD 1
+#endif
+template <typename R> __device__ __forceinline__ R pd_atan2(R y, R x) { return atan2(y, x); }
+#if PD_ATAN2_FD
+template <> __device__ __forceinline__ double pd_atan2<double>(double y, double x) { return atan2_fd(y, x); }
+#endif
+
 // ---------------------------------------------------------------- atmosphere
 // atmosphere_dynamics.py:5-27 (ambiance ISA restated)
 template <typename R>
@@ -306,21 +348,25 @@ __host__ __device__ constexpr int obs_dim(int kind) {
 // obs_eval: the observation's components to put(k, value); obs_write: to row idx of out [N][dim]
 template <typename R, typename Put>
 __device__ __forceinline__ void obs_eval(DP<R>& P, int kind, const R* s, Put&& put) {
+    // (divisions by the normalisers through their reciprocals: div_known, the same quotients)
+    auto ny = [&](R v) { return div_known<R>(v, P.norm_y, P.inv_norm_y); };
+    auto nvy = [&](R v) { return div_known<R>(v, P.norm_vy, P.inv_norm_vy); };
     if (kind == 0) {
-        put(0, (R(1) - (R)(float)s[1] / P.norm_y) * R(2) - R(1));
-        put(1, (R(1) - (R)(float)s[3] / P.norm_vy) * R(2) - R(1));
+        put(0, (R(1) - ny((R)(float)s[1])) * R(2) - R(1));
+        put(1, (R(1) - nvy((R)(float)s[3])) * R(2) - R(1));
     } else if (kind == 1) {
-        put(0, s[1] / P.norm_y); put(1, s[3] / P.norm_vy);
+        put(0, ny(s[1])); put(1, nvy(s[3]));
     } else if (kind == 2) {
-        put(0, s[0] / P.norm_x); put(1, s[1] / P.norm_y); put(2, s[2] / P.norm_vx); put(3, s[3] / P.norm_vy);
+        put(0, div_known<R>(s[0], P.norm_x, P.inv_norm_x)); put(1, ny(s[1]));
+        put(2, div_known<R>(s[2], P.norm_vx, P.inv_norm_vx)); put(3, nvy(s[3]));
         put(4, tanh(P.k_theta_pso * (s[4] - Cst<R>::pi / R(2))));
     } else if (kind == 3) {
-        put(0, (R)(float)s[1] / P.norm_y); put(1, (R)(float)s[3] / P.norm_vy);
+        put(0, ny((R)(float)s[1])); put(1, nvy((R)(float)s[3]));
         put(2, tanh((R)(P.f_k_theta_rl * ((float)s[4] - P.f_pi_2))));
         put(3, tanh((R)(P.f_k_thetad_rl * (float)s[5])));
         put(4, tanh((R)(P.f_k_gamma_rl * ((float)s[6] - P.f_pi_3_2))));
     } else if (kind == 4) {
-        put(0, (R(1) - (R)(float)s[1] / P.norm_y) * R(2) - R(1));
+        put(0, (R(1) - ny((R)(float)s[1])) * R(2) - R(1));
     } else {
         const int n = kind == 5 ? 4 : (kind == 6 ? 2 : 8);
         for (int k = 0; k < n; ++k) {

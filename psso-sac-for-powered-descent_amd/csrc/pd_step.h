@@ -165,6 +165,17 @@ template <typename R> struct StepArgs {
     float sac_lo, sac_hi, sac_max;
     uint32_t sac_hs;                 // row stride of mean / log_std in floats (both heads in one [N][2A] array: 2A)
     float* sac_act; float* slab; float* obs32;
+    // pd_step_sac_ring: eps drawn in the kernel (Philox tag kTagSacEps; sac_eps then NULL), written
+    // to sac_eps_out when given; the transition rows into a replay ring of ring_cap rows at
+    // (ring_state[0] + i) mod ring_cap with prio[row] = *max_prio, and the launch's last workgroup
+    // advancing ring_state (0 position, 1 size, 2 the workgroup ticket); ring_state NULL: slab rows
+    // at i (pd_step_sac's layout)
+    int sac_draw;
+    float* sac_eps_out;
+    int64_t ring_cap;
+    long long* ring_state;
+    float* prio;
+    const float* max_prio;
 };
 
 // Kernel launchers, explicitly instantiated in the kstep_*.hip translation units.

@@ -1014,6 +1014,10 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
     // envs this launch steps: all N, or (POL) the compacted live list; a workgroup past its end
     // leaves before staging the tables (workgroup-uniform)
     int64_t n_act = a.n;
+    // ring mode of pd_step_sac_ring: the ring position this launch writes at (every workgroup
+    // reads it before the last one advances it, see the end of the kernel)
+    int64_t ring_pos0 = 0;
+    if constexpr (SAC) { if (a.ring_state) ring_pos0 = (int64_t)__atomic_load_n(a.ring_state, __ATOMIC_RELAXED); }
     if constexpr (POL) {
         if (blockIdx.x == 0 && threadIdx.x == 0) *a.cnt_zero = 0u;
         if (a.use_list) {
@@ -1212,15 +1216,37 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
         // Actor.sample (sac_pytorch.py:161-179) on the caller's two heads, in binary32 as torch
         // computes it: log_std clamped (forward), std = exp, x = mean + std * eps (rsample),
         // action = tanh(x) * max_action; eps NULL: tanh(mean) * max_action (deterministic)
+        // pd_step_sac_ring: eps ~ N(0, 1) drawn here (torch.randn's role), two components per
+        // Philox block, keyed by (env, episode, step) like the gust draws: the same bits on
+        // every lane of the env and in any launch order
+        float ed[A];
+#pragma unroll
+        for (int k = 0; k < A; ++k) ed[k] = 0.f;
+        if (a.sac_draw) {
+            DP<R>& Q = *params<R>(a.P);
+            const double* lic = (const double*)(uint64_t)&Q.logtab.invc[0];
+            const double* llc = (const double*)(uint64_t)&Q.logtab.logc[0];
+#pragma unroll
+            for (int k = 0; k < A; k += 2) if (k < AD) {
+                u32x4 r = philox_k({(uint32_t)g, (uint32_t)(g >> 32) ^ e.ep, e.ts, kTagSacEps + (uint32_t)(k >> 1)},
+                                   a.seed_lo, a.seed_hi);
+                double z0, z1;
+                gauss_pair(r, lic, llc, z0, z1);
+                ed[k] = (float)z0;
+                if (k + 1 < A) ed[k + 1] = (float)z1;
+            }
+        }
 #pragma unroll
         for (int k = 0; k < A; ++k) if (k < AD) {
             const float m = ldv(a.sac_mean + k, ui * a.sac_hs);
             float xk = m;
-            if (a.sac_eps) {
+            if (a.sac_eps || a.sac_draw) {
                 float ls = ldv(a.sac_logstd + k, ui * a.sac_hs);
                 ls = ls < a.sac_lo ? a.sac_lo : (ls > a.sac_hi ? a.sac_hi : ls);
                 const float sd = expf(ls);
-                xk = m + sd * ldv(a.sac_eps + k, ui * AD);
+                const float ek = a.sac_draw ? ed[k] : ldv(a.sac_eps + k, ui * AD);
+                xk = m + sd * ek;
+                if (a.sac_eps_out && role == 0 && live) ev(a.sac_eps_out + k, ui * AD) = ek;
             }
             uf[k] = tanhf(xk) * a.sac_max;
             if (a.sac_act && role == 0 && live) ev(a.sac_act + k, ui * AD) = uf[k];
@@ -1233,12 +1259,19 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
         for (int k = 0; k < A; ++k) if (k < AD) uf[k] = ldv((const float*)a.actions + fo * AD + k, ui * AD);
     }
     // pd_step_sac: the transition row of this step starts with the observation of its start state
+    // (row srow: the env's, or in ring mode its row of the replay ring, (position + i) mod capacity)
     constexpr int kObsKind = RTD == 1 ? (PHASE == 0 ? 1 : 2) : (PHASE == 0 ? 0 : (PHASE == 1 ? 3 : -1));
+    uint32_t srow = ui;
+    if (SAC && a.ring_state) {
+        const int64_t rp = ring_pos0 + (int64_t)i;
+        srow = (uint32_t)(rp >= a.ring_cap ? rp - a.ring_cap : rp);
+    }
     if (SAC && a.slab && role == 0 && live) {
         DP<R>& Q = *params<R>(a.P);
         const int ok = kObsKind >= 0 ? kObsKind : Q.obs_kind;
         const uint32_t W = 2u * (uint32_t)obs_dim(ok) + (uint32_t)AD + 2u;
-        obs_eval<R>(Q, ok, e.s, [&](int k, R v) { ev(a.slab, ui * W + (uint32_t)k) = (float)v; });
+        obs_eval<R>(Q, ok, e.s, [&](int k, R v) { ev(a.slab, srow * W + (uint32_t)k) = (float)v; });
+        if (a.prio) ev(a.prio, srow) = *a.max_prio;
     }
     R gdeg_out = e.act0, dcmdl_out = e.act1, dcmdr_out = e.act2;
     const R gprev = e.act0, dlprev = e.act1, drprev = e.act2;
@@ -1289,7 +1322,7 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
                 // WindModel.__call__ (full_wind_model.py:35-43)
                 const R* walt = L.walt + e.prof * 16;
                 const R* wsp = L.wsp + e.prof * 16;
-                R km = y / R(1000);
+                R km = PD_DIVC(R, y, 1000);
                 int wn = P.wind_n[e.prof];
                 ug = np_interp<R>(walt, wsp, wn, km);
                 const bool gust = y < P.vk_y_threshold && a.stochastic;
@@ -1385,7 +1418,7 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
         PD_T(t_aero1);
         PD_ACC(3, t_aero1 - t_aero0);
         R q = R(0.5) * rho * (speed * speed);
-        R fpc = (P.m_prop0 - mp) / P.m_prop0;
+        R fpc = div_known<R>(P.m_prop0 - mp, P.m_prop0, P.inv_m_prop0);
         if (fpc == R(0)) fpc = R(1e-6);
         R x_cog, I;
         // subrocket_0 (full rocket) closures for the ascent, subrocket_2 after (:748-750, :772-774)
@@ -1649,13 +1682,13 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
             for (int k = 0; k < 8; ++k) sv[k] = rkb[k] + c * (stage == 3 ? rka[k] : kd[k]);
             x = sv[0]; y = sv[1]; vx = sv[2]; vy = sv[3]; th = sv[4]; thd = sv[5]; m = sv[6]; mp = sv[7];
             if (stage == 3 && th > Cst<R>::two_pi) th -= Cst<R>::two_pi;
-            ga = atan2(vy, vx);
+            ga = pd_atan2<R>(vy, vx);
             if (ga < R(0)) ga = Cst<R>::two_pi + ga;
             al = th - ga;
         } else {
         vx += vxd * dt; vy += vyd * dt; x += vx * dt; y += vy * dt;
         thd += thdd * dt; th += thd * dt;
-        ga = atan2(vy, vx);
+        ga = pd_atan2<R>(vy, vx);
         if (th > Cst<R>::two_pi) th -= Cst<R>::two_pi;
         if (ga < R(0)) ga = Cst<R>::two_pi + ga;
         al = th - ga;
@@ -1679,7 +1712,7 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
     DP<R>& P2 = *params<R>(a.P);
     const R* s = e.s;
     R v = sqrt(s[2] * s[2] + s[3] * s[3]);
-    R gl_new = fabs(v - e.vprev) / R(0.1) * R(1) / R(9.81);
+    R gl_new = PD_DIVC(R, PD_DIVC(R, fabs(v - e.vprev), 0.1) * R(1), 9.81);
     int glen = e.glen, ghead = e.ghead;
     int wslot;
     if (glen < 10) { wslot = glen; glen += 1; }
@@ -1697,7 +1730,7 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
 #pragma unroll
     for (int k = 0; k < 10; ++k)
         if (k < glen) gsum += gv[k];
-    R gl = gsum / R(10);
+    R gl = PD_DIVC(R, gsum, 10);
 
     // ---- truncated -> done -> reward (rtd_rl.py:190-336 / rtd_pso.py:172-317)
     R x = s[0], y = s[1], vx = s[2], vy = s[3], th = s[4], ga = s[6], mp = s[9];
@@ -1722,15 +1755,16 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
         if constexpr (PHASE == 0) {   // pure-throttle reward (rtd_rl.py:272-336)
             R sp = hypot(vx, vy);
             R qr = R(0.5) * rho * (sp * sp);
-            if (qr > R(60000)) { R e_ = (qr - R(60000)) / (R(65000) - R(60000)); R e2 = e_ * e_; rew -= R(1) * (e2 > R(1) ? R(1) : e2); }
+            // (divisions by literals and by y0 / m0 through their reciprocals: div_known)
+            if (qr > R(60000)) { R e_ = PD_DIVC(R, qr - R(60000), 5000); R e2 = e_ * e_; rew -= R(1) * (e2 > R(1) ? R(1) : e2); }
             if (gl > R(5.5)) { R e_ = (gl - R(5.5)) / (R(6) - R(5.5)); R e2 = e_ * e_; rew -= R(1) * (e2 > R(1) ? R(1) : e2); }
-            R prog = (P2.y0_rl - y) / P2.y0_rl;
+            R prog = div_known<R>(P2.y0_rl - y, P2.y0_rl, P2.inv_y0_rl);
             R wp = (qr <= R(60000) && gl <= R(5.5)) ? R(0.5) : R(0.5) * R(0.1);
             rew += wp * prog;
-            if (y < R(100)) rew += R(5.5) * (R(1) - fabs(vy) / R(50));
-            if (dn && !tr) rew += R(400) * mp / P2.m0_rl;
-            else if (tr && y > R(0)) rew -= R(50) * (fabs(y) / P2.y0_rl);
-            else if (tr && y < R(0)) rew -= R(50) * (fabs(vy) / R(10));
+            if (y < R(100)) rew += R(5.5) * (R(1) - PD_DIVC(R, fabs(vy), 50));
+            if (dn && !tr) rew += div_known<R>(R(400) * mp, P2.m0_rl, P2.inv_m0_rl);
+            else if (tr && y > R(0)) rew -= R(50) * div_known<R>(fabs(y), P2.y0_rl, P2.inv_y0_rl);
+            else if (tr && y < R(0)) rew -= R(50) * PD_DIVC(R, fabs(vy), 10);
             if (!dn || !(tr && y < R(0))) rew = rew < R(-10) ? R(-10) : (rew > R(10) ? R(10) : rew);
         } else {                      // landing_burn / ACS reward (rtd_rl.py:243-269), u0 = actions[0]
             R aef = fabs(ga - th - Cst<R>::pi);
@@ -1880,7 +1914,7 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
             // replay buffer's row (sac_pytorch.py:27-35; done without truncation, as the driver
             // stores it, sac_pytorch_powered_descent.py:170-176)
             const int ok = kObsKind >= 0 ? kObsKind : P2.obs_kind;
-            const uint32_t S = (uint32_t)obs_dim(ok), W = 2u * S + (uint32_t)AD + 2u, r0 = uo * W;
+            const uint32_t S = (uint32_t)obs_dim(ok), W = 2u * S + (uint32_t)AD + 2u, r0 = srow * W;
 #pragma unroll
             for (int k = 0; k < A; ++k) if (k < AD) ev(a.slab, r0 + S + (uint32_t)k) = uf[k];
             ev(a.slab, r0 + S + (uint32_t)AD) = (float)rew;
@@ -1929,6 +1963,22 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
     // ---- the env's state back to HBM, once (policy rollouts: also when its episode ends)
     PD_T(t_store);
     store_all();
+    if constexpr (SAC) {
+        // ring mode: the launch's last workgroup (a ticket per workgroup, taken after all of its
+        // ring rows are written and its position read) advances the ring's position and size
+        if (a.ring_state) {
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                const unsigned long long t = atomicAdd((unsigned long long*)&a.ring_state[2], 1ull);
+                if (t == (unsigned long long)gridDim.x - 1ull) {
+                    const int64_t np = ring_pos0 + N, sz = (int64_t)a.ring_state[1] + N;
+                    a.ring_state[0] = (long long)(np >= a.ring_cap ? np - a.ring_cap : np);
+                    a.ring_state[1] = (long long)(sz > a.ring_cap ? a.ring_cap : sz);
+                    a.ring_state[2] = 0;
+                }
+            }
+        }
+    }
     if (wc.w && __lane_id() == 0) {
 #pragma unroll
         for (int k = 0; k < kNWork; ++k)

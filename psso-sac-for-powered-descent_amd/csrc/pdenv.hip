@@ -1182,6 +1182,10 @@ template <typename R> void fill_params(const pd_params* p, const pd_config* c, D
     log_table_fill(D.logtab);
     log_table_fill(D.logtab_d);
     D.y0_rl = (R)p->state0[1]; D.m0_rl = (R)p->state0[8];
+    // the divisors' correctly rounded reciprocals (div_known): one IEEE division each, in R
+    D.inv_m_prop0 = R(1) / D.m_prop0; D.inv_y0_rl = R(1) / D.y0_rl; D.inv_m0_rl = R(1) / D.m0_rl;
+    D.inv_norm_y = R(1) / D.norm_y; D.inv_norm_vy = R(1) / D.norm_vy; D.inv_norm_x = R(1) / D.norm_x;
+    D.inv_norm_vx = R(1) / D.norm_vx;
     // ---- phase of the handle: its initial state, observation, and the constants of the
     // other compile_physics phases (rockets_physics.py:17-166,402-451,728-802,959-997)
     D.phase = c->phase;
@@ -1473,6 +1477,13 @@ struct SacIO {
     float lo, hi, max_action;
     float *action, *slab, *obs32;
     uint32_t head_stride;
+    // pd_step_sac_ring
+    int draw = 0;
+    float* eps_out = nullptr;
+    int64_t ring_cap = 0;
+    long long* ring_state = nullptr;
+    float* prio = nullptr;
+    const float* max_prio = nullptr;
 };
 
 template <typename R>
@@ -1488,6 +1499,8 @@ pd_status step_impl(pd_env* e, const void* actions, void* obs, void* reward, uin
         a.sac_lo = sac->lo; a.sac_hi = sac->hi; a.sac_max = sac->max_action;
         a.sac_act = sac->action; a.slab = sac->slab; a.obs32 = sac->obs32;
         a.sac_hs = sac->head_stride;
+        a.sac_draw = sac->draw; a.sac_eps_out = sac->eps_out;
+        a.ring_cap = sac->ring_cap; a.ring_state = sac->ring_state; a.prio = sac->prio; a.max_prio = sac->max_prio;
     }
     dispatch_step<R>(e, a, s);
     PD_HIP(hipGetLastError());
@@ -1718,6 +1731,38 @@ pd_status pd_step_sac(pd_env* e, const float* mean, const float* log_std, int32_
     PD_HIP(hipSetDevice(e->device));
     const SacIO io{mean, log_std, eps, log_std_min, log_std_max, max_action, action, slab, obs32,
                    (uint32_t)(head_stride ? head_stride : e->act_dim)};
+    if (e->rsize == 8)
+        return step_impl<double>(e, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
+                                 (hipStream_t)stream, 1, &io);
+    return step_impl<float>(e, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
+                            (hipStream_t)stream, 1, &io);
+}
+
+pd_status pd_step_sac_ring(pd_env* e, const float* heads, int32_t deterministic, float log_std_min, float log_std_max,
+                           float max_action, float* eps_out, float* action, float* ring, int64_t capacity,
+                           long long* ring_state, float* priorities, const float* max_priority, float* obs32,
+                           void* stream) {
+    if (!e || !heads) return fail(PD_ERR_INVALID, "null env/heads");
+    if (e->cfg.action_f64) return fail(PD_ERR_UNSUPPORTED, "pd_step_sac_ring: float32 actions only (action_f64 = 0)");
+    if (e->cfg.rtd == PD_RTD_PSO || e->cfg.integrator != PD_INTEG_REFERENCE ||
+        (e->cfg.phase != PD_PHASE_PURE_THROTTLE && e->cfg.phase != PD_PHASE_LANDING_BURN))
+        return fail(PD_ERR_UNSUPPORTED, "pd_step_sac_ring: the RL landing burns (reference integrator) only");
+    const int64_t N = e->cfg.n_envs;
+    const int64_t W = 2 * (int64_t)e->obs_dim + e->act_dim + 2;
+    if (ring_state) {
+        if (!ring || capacity < N) return fail(PD_ERR_INVALID, "pd_step_sac_ring: ring mode needs ring and capacity >= n_envs");
+        if (capacity * W >= (1ll << 32)) return fail(PD_ERR_INVALID, "pd_step_sac_ring: capacity x row width must be below 2^32");
+        if (priorities && !max_priority) return fail(PD_ERR_INVALID, "pd_step_sac_ring: priorities without max_priority");
+    }
+    PD_HIP(hipSetDevice(e->device));
+    const int A = e->act_dim;
+    SacIO io{heads, heads + A, nullptr, log_std_min, log_std_max, max_action, action, ring, obs32, (uint32_t)(2 * A)};
+    io.draw = deterministic ? 0 : 1;
+    io.eps_out = deterministic ? nullptr : eps_out;
+    io.ring_cap = ring_state ? capacity : 0;
+    io.ring_state = ring_state;
+    io.prio = ring_state ? priorities : nullptr;
+    io.max_prio = max_priority;
     if (e->rsize == 8)
         return step_impl<double>(e, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
                                  (hipStream_t)stream, 1, &io);

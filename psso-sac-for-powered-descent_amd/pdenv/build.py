@@ -2,7 +2,7 @@
 
 The step kernel is instantiated per (precision, phase family, wind) in 12 objects from
 csrc/kstep.hip, compiled in parallel with the host unit (pdenv.hip) and the PSO kernels
-(pdpso.hip), then linked into one shared library.  Objects are rebuilt when any source is
+(pdpso.hip) and the SAC actor (pdsac.hip), then linked into one shared library.  Objects are rebuilt when any source is
 newer than them."""
 import concurrent.futures as cf
 import os
@@ -26,7 +26,8 @@ KSTEP = [(r, ph, w) for r in (0, 1) for ph in (0, 1, 2) for w in (0, 1)]
 
 def units():
     """(object path, source, defines) of every translation unit."""
-    u = [(os.path.join(OBJ, "pdenv.o"), "pdenv.hip", []), (os.path.join(OBJ, "pdpso.o"), "pdpso.hip", [])]
+    u = [(os.path.join(OBJ, "pdenv.o"), "pdenv.hip", []), (os.path.join(OBJ, "pdpso.o"), "pdpso.hip", []),
+         (os.path.join(OBJ, "pdsac.o"), "pdsac.hip", [])]
     for r, ph, w in KSTEP:
         u.append((os.path.join(OBJ, f"kstep_r{r}_p{ph}_w{w}.o"), "kstep.hip",
                   [f"-DPD_KR={r}", f"-DPD_KPH={ph}", f"-DPD_KW={w}"]))

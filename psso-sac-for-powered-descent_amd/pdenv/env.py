@@ -179,6 +179,22 @@ class PoweredDescentEnv:
                                      _stream(self.device)))
         self._steps += 1
 
+    def step_sac_ring(self, heads, log_std_min=-20.0, log_std_max=2.0, max_action=1.0, deterministic=False,
+                      ring=None, capacity=0, ring_state=None, priorities=None, max_priority=None, action=None,
+                      obs32=None, eps_out=None):
+        """One SAC collection step in one launch (pd_step_sac_ring): the action sampled in the
+        kernel from heads [N, 2A] (mean | log_std, unclamped; eps drawn in the kernel unless
+        deterministic), the env step, and the transition rows written into `ring` -- the replay
+        buffer's [capacity, 2S + A + 2] rows at its device-held position ring_state (int64 [3]:
+        position, size, 0), with priorities[row] = max_priority[0] -- or, ring_state None, into
+        ring as a [N, 2S + A + 2] slab.  action [N, A], obs32 [N, S] (next observation) and
+        eps_out [N, A] as given.  No copies, allocations or syncs."""
+        L.check(self.lib.pd_step_sac_ring(self.h, _ptr(heads), int(bool(deterministic)), float(log_std_min),
+                                          float(log_std_max), float(max_action), _ptr(eps_out), _ptr(action),
+                                          _ptr(ring), int(capacity), _ptr(ring_state), _ptr(priorities),
+                                          _ptr(max_priority), _ptr(obs32), _stream(self.device)))
+        self._steps += 1
+
     def observe_raw(self):
         """pd_observe into the preallocated obs buffer (no copy); returns that buffer."""
         L.check(self.lib.pd_observe(self.h, _ptr(self._obs), _stream(self.device)))

@@ -8,9 +8,14 @@ for the pure-throttle task), and `all_gather_into_tensor` (backend "nccl" = RCCL
 concatenates the slabs in rank order; the learner rank appends them to its ring buffer.  The
 learner itself (critic/actor updates) is the caller's, as in the reference.
 """
+import ctypes as C
+
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
+
+from . import _lib as L
+from .env import _ptr, _stream
 
 
 class Actor(nn.Module):
@@ -58,6 +63,25 @@ class DeviceReplayBuffer:
         self.data = torch.zeros(self.capacity, self.width, dtype=torch.float32, device=device)
         self.position = 0
         self.size = 0
+        # the ring's position and size on the device (int64: position, size, pd_step_sac_ring's
+        # workgroup counter): the collection kernel writes its rows there and advances them, the
+        # host mirrors (position, size) by note_appended
+        self.state_dev = torch.zeros(3, dtype=torch.int64, device=device)
+
+    def _sync_state_dev(self):
+        self.state_dev.copy_(torch.tensor([self.position, self.size, 0], dtype=torch.int64))
+
+    def note_appended(self, b):
+        """The host mirror of b rows appended on the device (pd_step_sac_ring)."""
+        self.position = (self.position + b) % self.capacity
+        self.size = min(self.size + b, self.capacity)
+
+    def rows(self, start, b):
+        """The b ring rows from start (a view unless they wrap)."""
+        end = start + b
+        if end <= self.capacity:
+            return self.data[start:end]
+        return torch.cat([self.data[start:], self.data[:end - self.capacity]])
 
     def add_batch(self, slab):
         """slab [B, 2S + A + 2] = state | action | reward | next_state | done (float32)."""
@@ -73,6 +97,7 @@ class DeviceReplayBuffer:
             self.data[:b - k] = slab[k:]
         self.position = end % self.capacity
         self.size = min(self.size + b, self.capacity)
+        self._sync_state_dev()
 
     def add(self, state, action, reward, next_state, done):
         """The reference's one-transition add (sac_pytorch.py:27-35)."""
@@ -112,6 +137,7 @@ class DevicePrioritizedReplayBuffer(DeviceReplayBuffer):
         self.beta_increment = (1.0 - beta) / beta_annealing_steps
         self.priorities = torch.zeros(self.capacity, dtype=torch.float32, device=device)
         self.max_priority = 1.0
+        self.max_prio_dev = torch.ones(1, dtype=torch.float32, device=device)   # (read by pd_step_sac_ring)
 
     def add_batch(self, slab):
         b = min(slab.shape[0], self.capacity)
@@ -145,6 +171,7 @@ class DevicePrioritizedReplayBuffer(DeviceReplayBuffer):
         p = td_errors.detach().reshape(-1).abs().float() + self.epsilon
         self.priorities[indices] = p
         self.max_priority = max(self.max_priority, float(p.max()))
+        self.max_prio_dev.fill_(self.max_priority)
 
 
 def transition_slab(obs, action, reward, next_obs, done):
@@ -164,26 +191,73 @@ def gather_slabs(slab, dist=None):
     return out
 
 
+class ActorKernel:
+    """The Actor's forward pass as one pd_sac_actor launch (the shared MLP on MFMA and both heads,
+    activations in LDS): obs [N, S] float32 -> heads [N, 2A] (mean | log_std, unclamped).  Reads
+    the actor's parameter tensors in place (no copies: an optimizer step or an in-place update of
+    any kind is seen by the next call; a captured graph keeps the parameter addresses it saw, so
+    replacing a parameter tensor -- `.data = ...` -- needs a re-capture).  supported(actor) tells
+    whether the shapes fit the kernel (hidden 128/256/512, <= 8 hidden layers, S <= 16, A <= 8,
+    float32 parameters on the device)."""
+
+    def __init__(self, actor):
+        self.actor = actor
+        self.lib = L.load()
+        lins = [m for m in actor.shared_net if isinstance(m, nn.Linear)]
+        self.S, self.H, self.A = lins[0].in_features, lins[0].out_features, actor.mean.out_features
+        self.nl = len(lins)
+        self.params = [t for m in lins for t in (m.weight, m.bias)] + [actor.mean.weight, actor.mean.bias,
+                                                                       actor.log_std.weight, actor.log_std.bias]
+        self._ptrs = (C.c_void_p * len(self.params))()
+
+    @staticmethod
+    def supported(actor):
+        lins = [m for m in actor.shared_net if isinstance(m, nn.Linear)]
+        acts = [m for m in actor.shared_net if not isinstance(m, nn.Linear)]
+        if not lins or len(lins) > 8 or any(not isinstance(m, nn.ReLU) for m in acts) or len(acts) != len(lins):
+            return False
+        H = lins[0].out_features
+        ps = [p for m in lins for p in (m.weight, m.bias)] + list(actor.mean.parameters()) + list(actor.log_std.parameters())
+        return (H in (128, 256, 512) and lins[0].in_features <= 16 and actor.mean.out_features <= 8
+                and all(m.in_features == H and m.out_features == H for m in lins[1:])
+                and all(p.dtype == torch.float32 and p.is_cuda and p.is_contiguous() for p in ps))
+
+    def __call__(self, obs, heads):
+        for k, t in enumerate(self.params):
+            self._ptrs[k] = t.data_ptr()
+        L.check(self.lib.pd_sac_actor(int(obs.shape[0]), self.S, self.H, self.nl, self.A, _ptr(obs), self._ptrs,
+                                      _ptr(heads), _stream(obs.device)))
+        return heads
+
+
 class SACCollector:
-    """One collection step of N envs on this rank: actor sample -> env step -> slab -> gather ->
-    learner-rank buffer append.  `obs` always holds the observation the actor sees next (the
+    """One collection step of N envs on this rank: actor -> env step -> transition rows -> (gather)
+    -> learner-rank buffer.  `obs` always holds the observation the actor sees next (the
     post-auto-reset observation of envs whose episode ended).
 
-    fused=True (default): the actor's MLP in PyTorch with both heads as ONE GEMM (a [2A, H]
-    copy of the mean and log_std weights, refreshed whenever the actor's parameters change),
-    eps by torch.randn, then ONE kernel (pd_step_sac) samples the action from the heads, steps
-    the envs and writes the transition slab and the next float32 observation -- no slab cat, no
-    casts, no observe.
-    fused=False: Actor.sample, pd_step, transition_slab, pd_observe (the unfused reference path).
-    use_graph=True captures the step into one HIP graph (replaying removes the launch gaps).
-    The gather and the buffer append run eagerly after each replay; the aero-miss flush runs
-    every 16 steps."""
+    fused=True (default): TWO launches per step.
+      1. pd_sac_actor: the reference Actor's MLP and both heads in one kernel (ActorKernel; for
+         actor shapes it does not cover, PyTorch's shared_net and one GEMM over both heads).
+      2. pd_step_sac_ring: the action sampled from the heads in the step kernel (eps drawn there,
+         Philox; torch.randn's role), the env step, and the transition rows written by the
+         kernel epilogue straight into the learner's replay ring at the ring's device-held
+         position, with the new rows' priorities set to the buffer's max priority; the next
+         float32 observation into `obs`.  On several ranks the rows go to a local slab instead and
+         `all_gather_into_tensor` (RCCL) appends them on the learner rank.
+    fused=False: Actor.sample, pd_step, transition_slab, pd_observe, buffer.add_batch (the unfused
+    reference path, eps from torch.randn with `generator`).
+    use_graph=True captures the step into one HIP graph (replaying removes the launch gaps; the
+    ring position lives on the device, so replays append in order).  The gather runs eagerly after
+    each replay; the aero-miss flush every flush_every steps.
+    step() returns the step's transition rows: a view of the replay ring's rows (valid until the
+    ring wraps onto them) in ring mode, else a fresh tensor."""
 
     def __init__(self, env, actor, buffer=None, dist=None, learner_rank=0, generator=None,
                  deterministic=False, use_graph=False, flush_every=16, fused=True):
         self.env, self.actor, self.buffer, self.dist = env, actor, buffer, dist
         self.learner_rank, self.generator, self.deterministic = learner_rank, generator, deterministic
         self.rank = dist.get_rank() if dist is not None and dist.is_initialized() else 0
+        self.multi = dist is not None and dist.is_initialized() and dist.get_world_size() > 1
         self.obs = env.reset().float().contiguous()
         self.flush_every = flush_every
         self.steps = 0
@@ -191,38 +265,46 @@ class SACCollector:
         self.use_graph = use_graph
         self.fused = fused
         S, A = env.obs_dim, env.action_dim
-        self._slab_buf = torch.empty(env.n, 2 * S + A + 2, dtype=torch.float32, device=self.obs.device)
-        self.action = torch.empty(env.n, A, dtype=torch.float32, device=self.obs.device)
+        dev = self.obs.device
+        self._slab_buf = torch.empty(env.n, 2 * S + A + 2, dtype=torch.float32, device=dev)
+        self.action = torch.empty(env.n, A, dtype=torch.float32, device=dev)
+        self.heads = torch.empty(env.n, 2 * A, dtype=torch.float32, device=dev)
+        self.eps_out = None           # [N, A] to receive the kernel's eps draws (tests)
+        self.kernel = ActorKernel(actor) if fused and ActorKernel.supported(actor) else None
         H = actor.mean.in_features
-        self._head_w = torch.empty(2 * A, H, dtype=torch.float32, device=self.obs.device)
-        self._head_b = torch.empty(2 * A, dtype=torch.float32, device=self.obs.device)
-        self._head_ver = None
-        self._refresh_heads()
+        self._head_w = torch.empty(2 * A, H, dtype=torch.float32, device=dev)
+        self._head_b = torch.empty(2 * A, dtype=torch.float32, device=dev)
+        # ring mode: this process holds the buffer and steps every env of the job
+        self.ring = fused and buffer is not None and not self.multi and buffer.capacity >= env.n
 
-    def _refresh_heads(self):
-        """The fused head weights follow the actor: re-copied (in place, so a captured graph sees
-        them) whenever a head parameter was modified (its version counter moved)."""
-        ps = (self.actor.mean.weight, self.actor.mean.bias, self.actor.log_std.weight, self.actor.log_std.bias)
-        ver = tuple((id(p), p._version) for p in ps)
-        if ver != self._head_ver:
-            with torch.no_grad():
-                self._head_w.copy_(torch.cat([ps[0], ps[2]]))
-                self._head_b.copy_(torch.cat([ps[1], ps[3]]))
-            self._head_ver = ver
+    def _heads(self):
+        if self.kernel is not None:
+            return self.kernel(self.obs, self.heads)
+        # (shapes pd_sac_actor does not cover) torch's MLP and one GEMM over both heads, the
+        # head weights copied on every step (inside a captured graph too: never stale)
+        a = self.actor
+        torch.cat([a.mean.weight, a.log_std.weight], out=self._head_w)
+        torch.cat([a.mean.bias, a.log_std.bias], out=self._head_b)
+        f = a.shared_net(self.obs)
+        return torch.addmm(self._head_b, f, self._head_w.t(), out=self.heads)
 
     def _body(self):
-        """actor -> env step -> slab and next obs into self.obs; returns the slab (no syncs)."""
-        gen = None if self.use_graph else self.generator
+        """actor -> env step -> transition rows and next obs into self.obs (no syncs); returns
+        the local slab, or None when the rows went straight into the replay ring."""
         if self.fused:
-            f = self.actor.shared_net(self.obs)
-            heads = F.linear(f, self._head_w, self._head_b)             # mean | log_std (the kernel clamps)
-            eps = None
-            if not self.deterministic:
-                eps = torch.randn(self.action.shape, device=f.device, dtype=f.dtype, generator=gen)
-            self.env.step_sac(None, None, eps, self.actor.log_std_min, self.actor.log_std_max,
-                              self.actor.max_action, action=self.action, slab=self._slab_buf, obs32=self.obs,
-                              heads=heads)
+            heads = self._heads()
+            a = self.actor
+            kw = dict(deterministic=self.deterministic, action=self.action, obs32=self.obs, eps_out=self.eps_out)
+            if self.ring:
+                b = self.buffer
+                self.env.step_sac_ring(heads, a.log_std_min, a.log_std_max, a.max_action, ring=b.data,
+                                       capacity=b.capacity, ring_state=b.state_dev,
+                                       priorities=getattr(b, "priorities", None),
+                                       max_priority=getattr(b, "max_prio_dev", None), **kw)
+                return None
+            self.env.step_sac_ring(heads, a.log_std_min, a.log_std_max, a.max_action, ring=self._slab_buf, **kw)
             return self._slab_buf
+        gen = None if self.use_graph else self.generator
         act, _ = self.actor.sample(self.obs, deterministic=self.deterministic, generator=gen, with_log_prob=False)
         act = act.float().contiguous()
         self.env.step_raw_noflush(act)
@@ -234,15 +316,17 @@ class SACCollector:
         self.steps += 1
         if self.steps % self.flush_every == 0:
             self.env.flush()
+        if slab is None:                                       # ring mode: the rows are in place
+            start = self.buffer.position
+            self.buffer.note_appended(self.env.n)
+            return self.buffer.rows(start, self.env.n)
         full = gather_slabs(slab, self.dist)
         if self.rank == self.learner_rank and self.buffer is not None:
             self.buffer.add_batch(full)
-        return full
+        return full.clone() if full is self._slab_buf else full
 
     @torch.no_grad()
     def step(self):
-        if self.fused:
-            self._refresh_heads()
         if not self.use_graph:
             return self._finish(self._body())
         if self.graph is None:

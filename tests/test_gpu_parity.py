@@ -738,9 +738,90 @@ def test_sac_step_fused_sampling_and_slab(pd):
     assert int(twin.episode_counters()[0].max()) >= 1 or bool(d.any())
 
 
-def test_sac_collector_graph_equals_eager(pd):
-    """The HIP-graph collection step stores exactly the transitions of the eager step
-    (deterministic actor, twin envs, 40 steps including auto-resets and miss flushes)."""
+@pytest.mark.parametrize("S,A,H,L", [(2, 1, 256, 2), (5, 4, 256, 3), (2, 1, 128, 1), (5, 4, 512, 2)])
+def test_sac_actor_kernel_vs_torch(pd, S, A, H, L):
+    """pd_sac_actor (the Actor's shared MLP on MFMA and both heads in one launch) against the
+    reference Actor's forward in PyTorch (sac_pytorch.py:129-159): f32 heads equal to f32
+    rounding (the sums run in another order; max |d| <= 2e-5 + 1e-4 |ref|), over observations
+    spanning the normalised range and a batch that is not a multiple of the 16-env tile."""
+    import torch
+    from pdenv.sac import Actor, ActorKernel
+    torch.manual_seed(11)
+    n = 4096 + 5
+    actor = Actor(S, A, hidden_dim=H, n_hidden_layers=L).cuda()
+    assert ActorKernel.supported(actor)
+    obs = (torch.rand(n, S, device="cuda") * 4 - 2).contiguous()
+    heads = torch.full((n, 2 * A), float("nan"), device="cuda")
+    ActorKernel(actor)(obs, heads)
+    with torch.no_grad():
+        f = actor.shared_net(obs)
+        ref = torch.cat([actor.mean(f), actor.log_std(f)], dim=1)
+    d = (heads - ref).abs()
+    assert torch.isfinite(heads).all()
+    assert (d <= 2e-5 + 1e-4 * ref.abs()).all(), float(d.max())
+
+
+def test_sac_ring_step_draws_rows_priorities(pd):
+    """pd_step_sac_ring (c5's step kernel): eps is drawn in the kernel (N(0, 1): moments and a
+    KS bound over 64 k draws; new draws every step), the action equals torch's Actor.sample
+    arithmetic on the kernel's heads and eps to 2e-7, the transition rows land in the replay
+    ring at the device-held position -- wrapping, since the capacity is 1.5 N + 7 -- with the
+    buffer's max priority, the position and size advance, and a twin env stepped by pd_step
+    with the same actions gives the rows' reward, next observation and done bit for bit."""
+    import torch
+    from scipy import stats
+    from pdenv.sac import Actor, ActorKernel, DevicePrioritizedReplayBuffer
+    torch.manual_seed(5)
+    N = 4096
+    actor = Actor(2, 1).cuda()
+    env = make(pd, N, mode="rl", auto_reset=True, seed=21, tilt_sigma_rad=0.05)
+    twin = make(pd, N, mode="rl", auto_reset=True, seed=21, tilt_sigma_rad=0.05)
+    cap = N + N // 2 + 7
+    buf = DevicePrioritizedReplayBuffer(cap, 2, 1, "cuda")
+    buf.max_prio_dev.fill_(2.5)
+    obs = env.reset().float().contiguous()
+    twin.reset()
+    kern = ActorKernel(actor)
+    heads = torch.empty(N, 2, device="cuda")
+    act = torch.empty(N, 1, device="cuda")
+    eps = torch.empty(N, 1, device="cuda")
+    draws, prev = [], None
+    for t in range(16):
+        seen = obs.clone()
+        kern(obs, heads)
+        h = heads.clone()
+        pos = buf.position
+        env.step_sac_ring(heads, -20.0, 2.0, 1.0, ring=buf.data, capacity=cap, ring_state=buf.state_dev,
+                          priorities=buf.priorities, max_priority=buf.max_prio_dev, action=act, obs32=obs,
+                          eps_out=eps)
+        buf.note_appended(N)
+        st = buf.state_dev.cpu().tolist()
+        assert st == [buf.position, buf.size, 0], (t, st)
+        ref = torch.tanh(h[:, :1] + torch.clamp(h[:, 1:], -20.0, 2.0).exp() * eps)
+        assert (act - ref).abs().max() <= 2e-7, (t, float((act - ref).abs().max()))
+        rows = buf.rows(pos, N)
+        o, r, d, _, _ = twin.step(act)
+        assert torch.equal(rows[:, :2], seen) and torch.equal(rows[:, 2:3], act)
+        assert torch.equal(rows[:, 3], r.float()) and torch.equal(rows[:, 4:6], o.float())
+        assert torch.equal(rows[:, 6], d.float())
+        idx = (torch.arange(N, device="cuda") + pos) % cap
+        assert (buf.priorities[idx] == 2.5).all()
+        assert torch.equal(obs, twin.observe().float()), t
+        if prev is not None:
+            assert not torch.equal(eps, prev)
+        prev = eps.clone()
+        draws.append(eps.cpu().numpy().ravel())
+    z = np.concatenate(draws)
+    assert abs(z.mean()) < 0.02 and abs(z.std() - 1) < 0.02
+    assert stats.kstest(z, "norm").pvalue > 1e-4
+    assert len(buf) == cap
+
+
+@pytest.mark.parametrize("deterministic", [True, False])
+def test_sac_collector_graph_equals_eager(pd, deterministic):
+    """The HIP-graph collection step stores exactly the transitions of the eager step (twin envs,
+    40 steps including auto-resets and miss flushes; the stochastic actor too, its eps being
+    drawn in the kernel from the env's counters)."""
     import torch
     from pdenv.sac import Actor, DeviceReplayBuffer, SACCollector
     torch.manual_seed(0)
@@ -750,7 +831,7 @@ def test_sac_collector_graph_equals_eager(pd):
     for g in (False, True):
         env = make(pd, N, mode="rl", auto_reset=True, seed=6, tilt_sigma_rad=0.05)
         buf = DeviceReplayBuffer(64 * N, 2, 1, "cuda")
-        col = SACCollector(env, actor, buf, deterministic=True, use_graph=g)
+        col = SACCollector(env, actor, buf, deterministic=deterministic, use_graph=g)
         for _ in range(40):
             col.step()
         torch.cuda.synchronize()
