@@ -375,7 +375,9 @@ pd_status pd_count_work(pd_env* env, int32_t enable);
  * reference interface: the test hook behind them).  Built once per process and table.
  * out[0] pieces, [1] rejected by the build's check, [2] worst checked error relative to
  * sum |c_j phi_j|, [3] build seconds, [4] records, [5] nm, [6] na, [7] a0, [8] a1 (the grid),
- * [9] degree, [10] exact terms, [11] record stride; piece >= 0 (an exact cell's piece is at its
+ * [9] degree, [10] exact terms, [11] record stride, [12] pieces the binary32 check rejects (of the
+ * binary64-valid), [13] its worst error relative to sum |c_j phi_j| + |s|, [14] / [15] exact cells
+ * with a valid binary64 / binary32 piece; piece >= 0 (an exact cell's piece is at its
  * cell index im na + ia): its record at out[16 ...] (n_out >= 16 + stride). */
 pd_status pd_cell_piece_info(const pd_params* params, int32_t table, int64_t piece, double* out, int32_t n_out);
 /* Observation / action widths of the handle. */

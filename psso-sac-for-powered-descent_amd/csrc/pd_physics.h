@@ -132,9 +132,9 @@ template <typename R> struct DevParams {
     const unsigned long long* sub_key[2];
     const int* sub_slot[2];
     const void* sub_bis[2];          // GridBisect records (pd_step.h) of the kGridBisect sub-cells
-    // cell pieces (binary64 handles, pd_step.h kCellStride doubles each; nullptr: none): an exact
+    // cell pieces (pd_step.h cell_stride<R>() words each, in R; nullptr: none): an exact
     // cell's piece at its cell index, a refined cell's at sub_piece[sub-cell] (-1: none)
-    const double* cell_pc[2];
+    const R* cell_pc[2];
     const int* sub_piece[2];
     const uint32_t* fine[2];           // fine index (pd_step.h kFinePiece; nullptr: none)
     R line_bp[4][kLineMax];

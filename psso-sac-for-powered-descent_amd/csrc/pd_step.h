@@ -48,6 +48,12 @@ constexpr int kCellCoef = (kCellDeg + 1) * (kCellDeg + 2) / 2;
 constexpr int kCellExact = PD_CELL_EXACT;
 constexpr int kCellKey = kCellCoef + 3 * kCellExact;
 constexpr int kCellStride = (kCellKey + 2) & ~1;
+// binary32 handles: the same record in floats, the key's 8 bytes at an 8-byte aligned float index,
+// the stride a multiple of 4 floats (16 bytes)
+constexpr int kCellKeyF = (kCellKey + 1) & ~1;
+constexpr int kCellStrideF = (kCellKeyF + 2 + 3) & ~3;
+template <typename R> constexpr int cell_stride() { return sizeof(R) == 8 ? kCellStride : kCellStrideF; }
+template <typename R> constexpr int cell_key() { return sizeof(R) == 8 ? kCellKey : kCellKeyF; }
 
 // A sub-cell holding two 50-NN regions A, B whose keys differ by one point swap (p in A, q in B):
 // s(x) = n . x - c < 0 on A's side (p nearer than q).  Each side's slot carries kGridExact only if

@@ -63,7 +63,7 @@ template <typename R> struct TabView {
     const PD_AS1 unsigned long long* sub_key;
     const PD_AS1 int* sub_slot;
     const PD_AS1 GridBisect* sub_bis;
-    const PD_AS1 double* cell_pc;   // cell pieces (binary64 handles; nullptr: none)
+    const PD_AS1 R* cell_pc;        // cell pieces (cell_stride<R>() words each; nullptr: none)
     const PD_AS1 int* sub_piece;
     const PD_AS1 uint32_t* fine;    // fine index (nullptr: none)
     int grid_nm, grid_na;
@@ -437,10 +437,10 @@ __device__ __forceinline__ int rbf_lookup(const AT& a, DP<R>& P, int table, cons
     int gsl0 = -1, gcell = 0;
     R um = R(0), ua = R(0);
     const bool use_grid = t.grid_key != nullptr;
-    // binary64 handles with cell pieces read the query's sub-cell word of the fine index instead
-    // of the cell record: one dependent load to the piece (or its bisector record) for refined
-    // cells too; the cell / sub-cell records only when it does not settle the query
-    const bool fine_path = sizeof(R) == 8 && tay != nullptr && t.fine != nullptr;
+    // handles with cell pieces read the query's sub-cell word of the fine index instead of the
+    // cell record: one dependent load to the piece (or its bisector record) for refined cells
+    // too; the cell / sub-cell records only when it does not settle the query
+    const bool fine_path = tay != nullptr && t.fine != nullptr;
     uint32_t fe = 0u;
     R fsm = R(0), fsa = R(0);
     if (use_grid) {
@@ -495,10 +495,12 @@ __device__ __forceinline__ int rbf_lookup(const AT& a, DP<R>& P, int table, cons
             // a piece every point of the sub-cell uses, or the side of its bisector, trusted off
             // the line.  The margin is the record path's, so that both paths trust the same
             // queries: a refined cell's sub-cell (and any bisector) in sub-cell coordinates, a
-            // non-refined exact cell in cell coordinates (its sub-cell edges are no boundary)
-            const R eps = R(1e-9);
+            // non-refined exact cell in cell coordinates (its sub-cell edges are no boundary).
+            // Binary32 handles: 1e-4 cell widths as their record path, and 1e-3 sub-cell widths
+            // (the binary32 position's rounding is ~5e-5 cell widths at the grid's far end)
+            const R eps = sizeof(R) == 8 ? R(1e-9) : R(1e-4), eps_sub = sizeof(R) == 8 ? R(1e-9) : R(1e-3);
             const bool inside = (fe & kFineRefined)
-                ? (fsm > eps && R(1) - fsm > eps && fsa > eps && R(1) - fsa > eps)
+                ? (fsm > eps_sub && R(1) - fsm > eps_sub && fsa > eps_sub && R(1) - fsa > eps_sub)
                 : (um > eps && R(1) - um > eps && ua > eps && R(1) - ua > eps);
             int cpf = -1;
             if (fe & kFinePiece) cpf = (int)(fe & kFineIndex);
@@ -637,24 +639,26 @@ __device__ __forceinline__ R taylor_eval(const PD_AS1 R* __restrict__ rec, R M, 
 // build_cell_pieces): the polynomial in the cell coordinates u = 2 cu - 1, v = 2 cv - 1 (Horner
 // in u over the rows' polynomials in v) plus the exact terms.  The host checks every piece at
 // points of its cell in this order of operations.
-__device__ __forceinline__ double cell_eval(const PD_AS1 double* __restrict__ rec, double M, double aq, double cu,
-                                            double cv) {
-    const double u = 2.0 * cu - 1.0, v = 2.0 * cv - 1.0;
-    double f = 0.0;
+// (binary32 handles: the same order in binary32 on the rounded records, host-checked against the
+// binary64 pieces to 2e-6 of sum |c_j phi_j|; a zero distance is floored before the hardware log)
+template <typename R>
+__device__ __forceinline__ R cell_eval(const PD_AS1 R* __restrict__ rec, R M, R aq, R cu, R cv) {
+    const R u = R(2) * cu - R(1), v = R(2) * cv - R(1);
+    R f = R(0);
     int q = 0;
 #pragma unroll
     for (int i = kCellDeg; i >= 0; --i) {
-        double qi = rec[q++];
+        R qi = rec[q++];
 #pragma unroll
         for (int j = kCellDeg - i - 1; j >= 0; --j) qi = fma(qi, v, rec[q++]);
         f = i == kCellDeg ? qi : fma(f, u, qi);
     }
 #pragma unroll
     for (int e = 0; e < kCellExact; ++e) {
-        const PD_AS1 double* x = rec + kCellCoef + 3 * e;
-        const double dm = M - x[0], da = aq - x[2];
-        const double d2 = fma(dm, dm, da * da);
-        f = fma(x[1] * d2, eval_log4<double>(d2), f);
+        const PD_AS1 R* x = rec + kCellCoef + 3 * e;
+        const R dm = M - x[0], da = aq - x[2];
+        const R d2 = fma(dm, dm, da * da);
+        f = fma(x[1] * d2, eval_log4<R>(sizeof(R) == 8 ? d2 : (d2 > R(1e-30) ? d2 : R(1e-30))), f);
     }
     return f;
 }
@@ -792,14 +796,14 @@ __device__ __forceinline__ R rbf2(const AT& a, DP<R>& P, int table, const TabVie
     const bool full = act && !tay && !cel && slot >= 0;
     R vt = R(0);
     R vb;
-    if constexpr (sizeof(R) == 8) {
+    if (sizeof(R) == 8 || t.cell_pc != nullptr) {
         // with cell pieces the payload sums are rare (verified queries): the pieces first, then
         // the balanced sums of the lanes left, if any
         if (tay) vt = taylor_eval<R>(gbl(P.tay) + (size_t)tr.piece * kTayStride, M, tr.cell);
         if (cel) {
-            const PD_AS1 double* rec = t.cell_pc + (size_t)tr.cp * kCellStride;
-            vt = cell_eval(rec, M, aq, tr.cu, tr.cv);
-            if (tr.fine) cache.key = *(const PD_AS1 unsigned long long*)(rec + kCellKey);
+            const PD_AS1 R* rec = t.cell_pc + (size_t)tr.cp * cell_stride<R>();
+            vt = cell_eval<R>(rec, M, aq, (R)tr.cu, (R)tr.cv);
+            if (tr.fine) cache.key = *(const PD_AS1 unsigned long long*)(rec + cell_key<R>());
         }
         vb = rbf_balanced<R>(P, B, tab, full, table, slot, M, aq, []() {});
     } else {

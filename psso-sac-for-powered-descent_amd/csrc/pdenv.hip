@@ -632,9 +632,9 @@ void grid_geometry(int tb, int& nm, int& na, double& a0, double& a1) {
 }
 
 struct CellPieces;
-bool cell_ok(const CellPieces* cp, int64_t cell);
-bool fine_is(const CellPieces* cp, int im, int ia, int jm, int ja, int na, uint32_t want);
-int cell_bis(const CellPieces* cp, int bi, bool side_b);
+bool cell_ok(const CellPieces* cp, int64_t cell, bool f32);
+bool fine_is(const CellPieces* cp, int im, int ia, int jm, int ja, int na, uint32_t want, bool f32);
+int cell_bis(const CellPieces* cp, int bi, bool side_b, bool f32);
 
 template <typename R>
 pd_status build_grid(const pd_aero_table& t, double a0, double a1, int nm, int na, Table<R>& T,
@@ -643,6 +643,7 @@ pd_status build_grid(const pd_aero_table& t, double a0, double a1, int nm, int n
                      const CellPieces* cp = nullptr) {
     const GridKeys& g = grid_keys(t, a0, a1, nm, na);
     const int S = kGridSub;
+    const bool f32 = sizeof(R) == 4;
     gk.assign((size_t)nm * na, 0); gs.assign((size_t)nm * na, -1);
     std::vector<double> work(kScratch), pay(kPay);
     auto slot_of = [&](uint64_t key, bool exact) {
@@ -654,7 +655,7 @@ pd_status build_grid(const pd_aero_table& t, double a0, double a1, int nm, int n
             const uint64_t key = g.centre[(size_t)im * na + ia];
             gk[(size_t)im * na + ia] = key;
             gs[(size_t)im * na + ia] = slot_of(key, true);   // refined cells overwritten below
-            if (gs[(size_t)im * na + ia] >= 0 && cell_ok(cp, (int64_t)im * na + ia)) gs[(size_t)im * na + ia] |= kGridPiece;
+            if (gs[(size_t)im * na + ia] >= 0 && cell_ok(cp, (int64_t)im * na + ia, f32)) gs[(size_t)im * na + ia] |= kGridPiece;
         }
     const int64_t nr = (int64_t)g.refined.size();
     if (nr >= kGridRefine) return fail(PD_ERR_INVALID, "too many refined grid cells");
@@ -671,16 +672,18 @@ pd_status build_grid(const pd_aero_table& t, double a0, double a1, int nm, int n
                 sk[q] = key;
                 ss[q] = slot_of(key, exact);
                 const int bi = g.sub_bis[q];
-                if (!exact && bi >= 0 && sizeof(R) == 8 && bs.size() < (size_t)kGridBisect) {
+                // (binary32 handles read the bisector records through the fine index only: their
+                // record path verifies refined cells)
+                if (!exact && bi >= 0 && (sizeof(R) == 8 || cp) && bs.size() < (size_t)kGridBisect) {
                     const BisectHost& h = g.bis[bi];
                     GridBisect b{};
                     b.nx = h.nx; b.ny = h.ny; b.c = h.c; b.tau = h.tau; b.key_a = h.key_a; b.key_b = h.key_b;
                     const int sa = table_insert<R>(t, T, h.key_a, work, pay), sb = table_insert<R>(t, T, h.key_b, work, pay);
                     b.slot_a = sa < 0 ? -1 : (sa | (h.ok_a ? kGridExact : 0));
                     b.slot_b = sb < 0 ? -1 : (sb | (h.ok_b ? kGridExact : 0));
-                    b.piece_a = cell_bis(cp, bi, false); b.piece_b = cell_bis(cp, bi, true);
+                    b.piece_a = cell_bis(cp, bi, false, f32); b.piece_b = cell_bis(cp, bi, true, f32);
                     if (cp && !fine_is(cp, g.refined[r] / na, g.refined[r] % na, jm, ja, na,
-                                       kFineBisect | kFineRefined | (uint32_t)bs.size()))
+                                       kFineBisect | kFineRefined | (uint32_t)bs.size(), f32))
                         return fail(PD_ERR_INVALID, "cell pieces: fine index does not match the bisector records");
                     ss[q] = kGridBisect | (int)bs.size();
                     bs.push_back(b);
@@ -715,7 +718,29 @@ struct CellPieces {
     std::vector<uint32_t> fine;       // [nm S][na S] fine index (pd_step.h kFinePiece)
     double max_rel = 0, build_s = 0;
     int64_t pieces = 0, rejected = 0;
+    std::vector<double> err;          // per piece: the binary64 check's error (INFINITY: unused slot)
+    std::vector<double> scale;        // per piece: the largest sum |c_j phi_j| + |s| at its check points
+    std::vector<int> cell_of;         // per piece: its grid cell
+    // the fine index's inputs (kept for the binary32 variant)
+    int nm = 0, na = 0;
+    double a0 = 0, dm = 0, da = 0;
+    std::vector<uint8_t> refined;
+    std::vector<int> ridx;
+    std::vector<int64_t> bs_of;
+    // binary32 handles (ensure_f32): the records in floats (kCellStrideF), each checked in binary32
+    // against its binary64 piece; validity, sub-cell pieces, bisector sides and fine index of
+    // the pieces that pass
+    bool have32 = false;
+    std::vector<float> rec32;
+    std::vector<uint8_t> cell_ok32;
+    std::vector<int> sub_piece32, bis_a32, bis_b32;
+    std::vector<uint32_t> fine32;
+    double max_rel32 = 0;
+    int64_t rejected32 = 0;
 };
+// binary32 pieces: error bound relative to sum |c_j phi_j| + |s| (the binary32 balanced payload
+// sums, which these replace, round at ~50 eps_32 of the same scale)
+constexpr double kCellTol32 = 2e-6;
 
 // The fit operator: pinv[c][node] of the (node x coefficient) monomial design matrix, columns in
 // record order (u^i v^j, i = kCellDeg .. 0, j = kCellDeg - i .. 0), nodes (k, l) -> (x_k, x_l)
@@ -802,7 +827,8 @@ NbrTerms nbr_terms(const pd_aero_table& t, uint64_t key) {
 
 // One piece: key's sum over cell (im, ia) into rec; returns the validation error (relative to
 // sum |c_j phi_j|), or +inf if the neighbourhood did not solve
-double make_cell_piece(const NbrTerms& T, int im, int ia, double dm, double da, double a0, double* rec) {
+double make_cell_piece(const NbrTerms& T, int im, int ia, double dm, double da, double a0, double* rec,
+                       double* scale = nullptr) {
     if (!T.ok) return INFINITY;
     const std::vector<long double>& pinv = cell_fit_operator();
     const double cm = (im + 0.5) * dm, ca = a0 + (ia + 0.5) * da, hm = 0.5 * dm, ha = 0.5 * da;
@@ -872,8 +898,80 @@ double make_cell_piece(const NbrTerms& T, int im, int ia, double dm, double da, 
             exact += ph; mag += fabsl(ph);
         }
         worst = std::max(worst, (double)(fabsl((long double)f - exact) / (mag + fabsl(exact) + 1e-300L)));
+        if (scale) *scale = std::max(*scale, (double)(mag + fabsl(exact)));
     }
     return worst;
+}
+
+// A piece record in binary32 (kCellStrideF floats, the key's bits at kCellKeyF) and its check:
+// evaluated as the binary32 device does (Horner in fmaf, exact terms with the hardware log2) at
+// the binary64 check's 8 points, against the binary64 record there; returns |error| / scale
+double make_cell_piece_f32(const double* rec, int im, int ia, double dm, double da, double a0, double scale,
+                           float* out) {
+    for (int c = 0; c < kCellStrideF; ++c) out[c] = 0.0f;
+    for (int c = 0; c < kCellKey; ++c) out[c] = (float)rec[c];
+    std::memcpy(out + kCellKeyF, rec + kCellKey, 8);
+    const double cm = (im + 0.5) * dm, ca = a0 + (ia + 0.5) * da, hm = 0.5 * dm, ha = 0.5 * da;
+    double worst = 0.0;
+    for (int q = 1; q <= 8; ++q) {
+        double h2 = 0, h3 = 0, f2 = 0.5, f3 = 1.0 / 3;
+        for (int n = q; n; n >>= 1, f2 *= 0.5) h2 += f2 * (n & 1);
+        for (int n = q; n; n /= 3, f3 /= 3) h3 += f3 * (n % 3);
+        const float u = (float)(2 * h2 - 1), v = (float)(2 * h3 - 1);
+        const float M = (float)(cm + u * hm), a = (float)(ca + v * ha);
+        float f = 0.0f;
+        int c = 0;
+        for (int i = kCellDeg; i >= 0; --i) {
+            float qi = out[c++];
+            for (int j = kCellDeg - i - 1; j >= 0; --j) qi = std::fma(qi, v, out[c++]);
+            f = i == kCellDeg ? qi : std::fma(f, u, qi);
+        }
+        for (int e = 0; e < kCellExact; ++e) {
+            const float* x = out + kCellCoef + 3 * e;
+            const float dmx = M - x[0], dax = a - x[2], d2 = std::fma(dmx, dmx, dax * dax);
+            f = std::fma(x[1] * d2, std::log2(d2 > 1e-30f ? d2 : 1e-30f) * (4.0f * 0.693147180559945309f), f);
+        }
+        // the binary64 record at the same point
+        const double uu = u, vv = v, MM = M, aa = a;
+        double g = 0.0;
+        c = 0;
+        for (int i = kCellDeg; i >= 0; --i) {
+            double qi = rec[c++];
+            for (int j = kCellDeg - i - 1; j >= 0; --j) qi = std::fma(qi, vv, rec[c++]);
+            g = i == kCellDeg ? qi : std::fma(g, uu, qi);
+        }
+        for (int e = 0; e < kCellExact; ++e) {
+            const double* x = rec + kCellCoef + 3 * e;
+            const double dmx = MM - x[0], dax = aa - x[2], d2 = std::fma(dmx, dmx, dax * dax);
+            if (d2 > 0) g = std::fma(x[1] * d2, 4.0 * std::log(d2), g);
+        }
+        worst = std::max(worst, std::fabs((double)f - g) / (scale + 1e-300));
+    }
+    return worst;
+}
+
+// The fine index of one precision's valid pieces (cell_ok, sub_piece) over the grid of cp
+void build_fine(const CellPieces& cp, const std::vector<uint8_t>& cell_ok, const std::vector<int>& sub_piece,
+                std::vector<uint32_t>& fine) {
+    const int S = kGridSub, nm = cp.nm, na = cp.na;
+    fine.assign((size_t)nm * S * na * S, 0u);
+    parallel_for(nm, [&](int64_t im) {
+        for (int ia = 0; ia < na; ++ia) {
+            const int64_t c = im * na + ia;
+            for (int jm = 0; jm < S; ++jm)
+                for (int ja = 0; ja < S; ++ja) {
+                    uint32_t e = 0u;
+                    if (!cp.refined[c]) {
+                        if (cell_ok[c]) e = kFinePiece | (uint32_t)c;
+                    } else {
+                        const size_t sq = (size_t)cp.ridx[c] * S * S + jm * S + ja;
+                        if (sub_piece[sq] >= 0) e = kFinePiece | kFineRefined | (uint32_t)sub_piece[sq];
+                        else if (cp.bs_of[sq] >= 0) e = kFineBisect | kFineRefined | (uint32_t)cp.bs_of[sq];
+                    }
+                    fine[(size_t)(im * S + jm) * ((size_t)na * S) + (size_t)ia * S + ja] = e;
+                }
+        }
+    });
 }
 
 const CellPieces& cell_pieces(const pd_aero_table& t, double a0, double a1, int nm, int na) {
@@ -938,12 +1036,16 @@ const CellPieces& cell_pieces(const pd_aero_table& t, double a0, double a1, int 
     parallel_for((int64_t)keys.size(), [&](int64_t k) { terms[k] = nbr_terms(t, keys[k]); });
     cell_fit_operator();
     cp.rec.assign(job.size() * kCellStride, 0.0);
-    std::vector<double> err(job.size());
+    cp.err.assign(job.size(), INFINITY);
+    cp.scale.assign(job.size(), 0.0);
+    cp.cell_of.resize(job.size());
+    std::vector<double>& err = cp.err;
     parallel_for((int64_t)job.size(), [&](int64_t p) {
         const int c = job[p].first;
+        cp.cell_of[p] = c;
         if (p < ncell && refined[c]) { err[p] = INFINITY; return; }   // (a refined cell's own index: unused)
         double* rec = cp.rec.data() + (size_t)p * kCellStride;
-        err[p] = make_cell_piece(terms[kidx.at(job[p].second)], c / na, c % na, dm, da, a0, rec);
+        err[p] = make_cell_piece(terms[kidx.at(job[p].second)], c / na, c % na, dm, da, a0, rec, &cp.scale[p]);
         const uint64_t key = job[p].second;
         std::memcpy(rec + kCellKey, &key, 8);
     });
@@ -962,10 +1064,12 @@ const CellPieces& cell_pieces(const pd_aero_table& t, double a0, double a1, int 
     // the fine index: per sub-cell of every cell the piece all its points use, or the bisector
     // record splitting it (numbered as build_grid numbers them: refined cells, then sub-cells in
     // order, every non-exact sub-cell with a bisector)
+    cp.nm = nm; cp.na = na; cp.a0 = a0; cp.dm = dm; cp.da = da;
+    cp.refined = refined;
+    cp.ridx.assign(ncell, -1);
+    for (int64_t r = 0; r < nr; ++r) cp.ridx[g.refined[r]] = (int)r;
+    cp.bs_of.assign((size_t)nr * S * S, -1);
     {
-        std::vector<int> ridx(ncell, -1);
-        for (int64_t r = 0; r < nr; ++r) ridx[g.refined[r]] = (int)r;
-        std::vector<int64_t> bs_of((size_t)nr * S * S, -1);
         int64_t nbs = 0;
         for (int64_t r = 0; r < nr; ++r)
             for (int q = 0; q < S * S; ++q) {
@@ -974,58 +1078,86 @@ const CellPieces& cell_pieces(const pd_aero_table& t, double a0, double a1, int 
                 bool exact = true;
                 for (int c = 0; c < 4 && exact; ++c)
                     exact = g.sub_corner[((size_t)r * (S + 1) + jm + (c >> 1)) * (S + 1) + ja + (c & 1)] == g.sub_centre[sq];
-                if (!exact && g.sub_bis[sq] >= 0 && nbs < (int64_t)kGridBisect) bs_of[sq] = nbs++;
+                if (!exact && g.sub_bis[sq] >= 0 && nbs < (int64_t)kGridBisect) cp.bs_of[sq] = nbs++;
             }
-        cp.fine.assign((size_t)nm * S * na * S, 0u);
-        parallel_for(nm, [&](int64_t im) {
-            for (int ia = 0; ia < na; ++ia) {
-                const int64_t c = im * na + ia;
-                for (int jm = 0; jm < S; ++jm)
-                    for (int ja = 0; ja < S; ++ja) {
-                        uint32_t e = 0u;
-                        if (!refined[c]) {
-                            if (cp.cell_ok[c]) e = kFinePiece | (uint32_t)c;
-                        } else {
-                            const size_t sq = (size_t)ridx[c] * S * S + jm * S + ja;
-                            if (cp.sub_piece[sq] >= 0) e = kFinePiece | kFineRefined | (uint32_t)cp.sub_piece[sq];
-                            else if (bs_of[sq] >= 0) e = kFineBisect | kFineRefined | (uint32_t)bs_of[sq];
-                        }
-                        cp.fine[(size_t)(im * S + jm) * ((size_t)na * S) + (size_t)ia * S + ja] = e;
-                    }
-            }
-        });
     }
+    build_fine(cp, cp.cell_ok, cp.sub_piece, cp.fine);
     cp.build_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     return cp;
 }
-bool cell_ok(const CellPieces* cp, int64_t cell) { return cp != nullptr && cp->cell_ok[cell]; }
-bool fine_is(const CellPieces* cp, int im, int ia, int jm, int ja, int na, uint32_t want) {
-    const int S = kGridSub;
-    return cp->fine[(size_t)(im * S + jm) * ((size_t)na * S) + (size_t)ia * S + ja] == want;
+bool cell_ok(const CellPieces* cp, int64_t cell, bool f32) {
+    return cp != nullptr && (f32 ? cp->cell_ok32[cell] : cp->cell_ok[cell]);
 }
-int cell_bis(const CellPieces* cp, int bi, bool side_b) { return cp == nullptr ? -1 : (side_b ? cp->bis_b[bi] : cp->bis_a[bi]); }
+bool fine_is(const CellPieces* cp, int im, int ia, int jm, int ja, int na, uint32_t want, bool f32) {
+    const int S = kGridSub;
+    return (f32 ? cp->fine32 : cp->fine)[(size_t)(im * S + jm) * ((size_t)na * S) + (size_t)ia * S + ja] == want;
+}
+int cell_bis(const CellPieces* cp, int bi, bool side_b, bool f32) {
+    if (cp == nullptr) return -1;
+    if (f32) return side_b ? cp->bis_b32[bi] : cp->bis_a32[bi];
+    return side_b ? cp->bis_b[bi] : cp->bis_a[bi];
+}
+
+// The binary32 variant of cp (once per process and table): every binary64-valid piece rounded to
+// floats and checked in binary32 (make_cell_piece_f32); the pieces within kCellTol32 keep their
+// places, the others drop out of the binary32 validity, sub-cell, bisector and fine-index tables
+// (their queries take the record path: verified, payload sums)
+void ensure_f32(CellPieces& cp) {
+    static std::mutex mu;
+    std::lock_guard<std::mutex> lock(mu);
+    if (cp.have32) return;
+    const int64_t np = (int64_t)cp.err.size();
+    cp.rec32.assign((size_t)np * kCellStrideF, 0.0f);
+    std::vector<double> e32(np, INFINITY);
+    parallel_for(np, [&](int64_t p) {
+        if (!(cp.err[p] <= kCellTol)) return;
+        const int c = cp.cell_of[p];
+        e32[p] = make_cell_piece_f32(cp.rec.data() + (size_t)p * kCellStride, c / cp.na, c % cp.na, cp.dm, cp.da,
+                                     cp.a0, cp.scale[p], cp.rec32.data() + (size_t)p * kCellStrideF);
+    });
+    auto ok = [&](int p) { return p >= 0 && e32[p] <= kCellTol32; };
+    const int64_t ncell = (int64_t)cp.cell_ok.size();
+    cp.cell_ok32.assign(ncell, 0);
+    for (int64_t c = 0; c < ncell; ++c) cp.cell_ok32[c] = cp.cell_ok[c] && ok((int)c);
+    cp.sub_piece32 = cp.sub_piece; cp.bis_a32 = cp.bis_a; cp.bis_b32 = cp.bis_b;
+    for (auto* v : {&cp.sub_piece32, &cp.bis_a32, &cp.bis_b32})
+        for (auto& x : *v) if (!ok(x)) x = -1;
+    for (int64_t p = 0; p < np; ++p) {
+        if (!(cp.err[p] <= kCellTol)) continue;
+        if (e32[p] <= kCellTol32) cp.max_rel32 = std::max(cp.max_rel32, e32[p]);
+        else ++cp.rejected32;
+    }
+    build_fine(cp, cp.cell_ok32, cp.sub_piece32, cp.fine32);
+    cp.have32 = true;
+}
 
 // The device copy of a table's cell pieces: one per device and process, shared read-only by the
 // handles (never freed; ~0.2 GB of the 288 GB)
-pd_status cell_pieces_device(const CellPieces& cp, const double** rec, const int** sub, const uint32_t** fine) {
+template <typename R>
+pd_status cell_pieces_device(const CellPieces& cp, const R** rec, const int** sub, const uint32_t** fine) {
     static std::mutex mu;
     static std::map<std::pair<const void*, int>, std::array<void*, 3>> m;
+    const bool f32 = sizeof(R) == 4;
+    const auto& rv = f32 ? (const void*)cp.rec32.data() : (const void*)cp.rec.data();
+    const size_t rbytes = f32 ? cp.rec32.size() * 4 : cp.rec.size() * 8;
+    const std::vector<int>& sp = f32 ? cp.sub_piece32 : cp.sub_piece;
+    const std::vector<uint32_t>& fn = f32 ? cp.fine32 : cp.fine;
     int dev = 0;
     PD_HIP(hipGetDevice(&dev));
     std::lock_guard<std::mutex> lock(mu);
-    auto k = std::make_pair((const void*)&cp, dev);
+    auto k = std::make_pair((const void*)(f32 ? (const void*)&cp.rec32 : (const void*)&cp.rec), dev);
     auto it = m.find(k);
     if (it == m.end()) {
         void *dr = nullptr, *ds = nullptr, *df = nullptr;
-        PD_HIP(hipMalloc(&dr, std::max<size_t>(cp.rec.size(), 1) * 8));
-        PD_HIP(hipMalloc(&ds, std::max<size_t>(cp.sub_piece.size(), 1) * 4));
-        PD_HIP(hipMalloc(&df, std::max<size_t>(cp.fine.size(), 1) * 4));
-        if (!cp.rec.empty()) PD_HIP(hipMemcpy(dr, cp.rec.data(), cp.rec.size() * 8, hipMemcpyHostToDevice));
-        if (!cp.sub_piece.empty()) PD_HIP(hipMemcpy(ds, cp.sub_piece.data(), cp.sub_piece.size() * 4, hipMemcpyHostToDevice));
-        if (!cp.fine.empty()) PD_HIP(hipMemcpy(df, cp.fine.data(), cp.fine.size() * 4, hipMemcpyHostToDevice));
+        PD_HIP(hipMalloc(&dr, std::max<size_t>(rbytes, 8)));
+        PD_HIP(hipMalloc(&ds, std::max<size_t>(sp.size(), 1) * 4));
+        PD_HIP(hipMalloc(&df, std::max<size_t>(fn.size(), 1) * 4));
+        if (rbytes) PD_HIP(hipMemcpy(dr, rv, rbytes, hipMemcpyHostToDevice));
+        if (!sp.empty()) PD_HIP(hipMemcpy(ds, sp.data(), sp.size() * 4, hipMemcpyHostToDevice));
+        if (!fn.empty()) PD_HIP(hipMemcpy(df, fn.data(), fn.size() * 4, hipMemcpyHostToDevice));
         it = m.emplace(k, std::array<void*, 3>{dr, ds, df}).first;
     }
-    *rec = (const double*)it->second[0];
+    *rec = (const R*)it->second[0];
     *sub = (const int*)it->second[1];
     *fine = (const uint32_t*)it->second[2];
     return PD_OK;
@@ -1306,14 +1438,16 @@ template <typename R> pd_status create_impl(const pd_params* p, const pd_config*
     int gnm[2], gna[2];
     double ga0[2], ga1[2];
     for (int tb = 0; tb < 2; ++tb) grid_geometry(tb, gnm[tb], gna[tb], ga0[tb], ga1[tb]);
-    // cell pieces for the binary64 handle's interior queries (PDENV_CELL_PIECES=0: payload sums
-    // only).  The binary32 handle keeps its balanced binary32 sums: measured with the pieces of its
-    // exact cells (evaluated in binary64), c3 took 0.0426 ms per env-step against 0.0400
+    // cell pieces for the interior queries (PDENV_CELL_PIECES=0: payload sums only): binary64
+    // records for binary64 handles, their binary32 roundings (each checked in binary32,
+    // ensure_f32) for binary32 handles
     const CellPieces* cps[2] = {nullptr, nullptr};
     const char* cpe = getenv("PDENV_CELL_PIECES");
-    if (sizeof(R) == 8 && !(cpe && cpe[0] == '0')) {
-        cps[0] = &cell_pieces(p->cd, ga0[0], ga1[0], gnm[0], gna[0]);
-        cps[1] = &cell_pieces(p->cl, ga0[1], ga1[1], gnm[1], gna[1]);
+    if (!(cpe && cpe[0] == '0')) {
+        CellPieces* c0 = const_cast<CellPieces*>(&cell_pieces(p->cd, ga0[0], ga1[0], gnm[0], gna[0]));
+        CellPieces* c1 = const_cast<CellPieces*>(&cell_pieces(p->cl, ga0[1], ga1[1], gnm[1], gna[1]));
+        if (sizeof(R) == 4) { ensure_f32(*c0); ensure_f32(*c1); }
+        cps[0] = c0; cps[1] = c1;
     }
     if ((st = build_grid<R>(p->cd, ga0[0], ga1[0], gnm[0], gna[0], tcd, gk[0], gs[0], sk[0], ss[0], bs[0], cps[0])) != PD_OK) return st;
     if ((st = build_grid<R>(p->cl, ga0[1], ga1[1], gnm[1], gna[1], tcl, gk[1], gs[1], sk[1], ss[1], bs[1], cps[1])) != PD_OK) return st;
@@ -1321,7 +1455,7 @@ template <typename R> pd_status create_impl(const pd_params* p, const pd_config*
     const char* fne = getenv("PDENV_FINE");
     for (int tb = 0; tb < 2; ++tb) {
         D.cell_pc[tb] = nullptr; D.sub_piece[tb] = nullptr; D.fine[tb] = nullptr;
-        if (cps[tb] && (st = cell_pieces_device(*cps[tb], &D.cell_pc[tb], &D.sub_piece[tb], &D.fine[tb])) != PD_OK) return st;
+        if (cps[tb] && (st = cell_pieces_device<R>(*cps[tb], &D.cell_pc[tb], &D.sub_piece[tb], &D.fine[tb])) != PD_OK) return st;
         if (fne && fne[0] == '0') D.fine[tb] = nullptr;
     }
     if (getenv("PDENV_TAY_DEBUG"))
@@ -1630,10 +1764,16 @@ pd_status pd_cell_piece_info(const pd_params* p, int32_t table, int64_t piece, d
     int nm, na;
     double a0, a1;
     grid_geometry(table, nm, na, a0, a1);
-    const CellPieces& cp = cell_pieces(t, a0, a1, nm, na);
-    const double v[12] = {(double)cp.pieces, (double)cp.rejected, cp.max_rel, cp.build_s, (double)(cp.rec.size() / kCellStride),
-                          (double)nm, (double)na, a0, a1, (double)kCellDeg, (double)kCellExact, (double)kCellStride};
-    for (int k = 0; k < 16; ++k) out[k] = k < 12 ? v[k] : 0.0;
+    CellPieces& cp = const_cast<CellPieces&>(cell_pieces(t, a0, a1, nm, na));
+    ensure_f32(cp);
+    int64_t ok32 = 0;
+    for (uint8_t c : cp.cell_ok32) ok32 += c;
+    int64_t ok64 = 0;
+    for (uint8_t c : cp.cell_ok) ok64 += c;
+    const double v[16] = {(double)cp.pieces, (double)cp.rejected, cp.max_rel, cp.build_s, (double)(cp.rec.size() / kCellStride),
+                          (double)nm, (double)na, a0, a1, (double)kCellDeg, (double)kCellExact, (double)kCellStride,
+                          (double)cp.rejected32, cp.max_rel32, (double)ok64, (double)ok32};
+    for (int k = 0; k < 16; ++k) out[k] = v[k];
     if (piece >= 0) {
         if ((size_t)(piece + 1) * kCellStride > cp.rec.size() || n_out < 16 + kCellStride)
             return fail(PD_ERR_INVALID, "pd_cell_piece_info: piece out of range or out too short");

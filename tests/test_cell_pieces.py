@@ -104,3 +104,17 @@ def test_cell_pieces_vs_numpy_restatement(lib_params, tb, name):
     # the same class as the binary64 direct sum's rounding (and the scipy solve's, which differs
     # from the library's LU in the last bits of the coefficients)
     assert max(errs) <= 2e-15, max(errs)
+
+
+@pytest.mark.parametrize("tb", [0, 1])
+def test_cell_pieces_binary32(lib_params, tb):
+    """The binary32 handle's pieces (ensure_f32): every binary64-valid piece rounded to floats and
+    evaluated as the binary32 kernel does (fmaf Horner, hardware log2 for the exact terms) at its
+    check points; the ones within 2e-6 of sum |c_j phi_j| + |s| are used.  Nearly all pass, so the
+    binary32 handle's interior queries take pieces (not the payload sums) almost everywhere."""
+    L, P = lib_params
+    info = _info(L, P, tb)
+    pieces, rejected32, max32, ok64, ok32 = info[0], info[12], info[13], info[14], info[15]
+    assert 0 < max32 <= 2e-6
+    assert rejected32 <= 0.01 * pieces, (rejected32, pieces)
+    assert ok32 >= 0.99 * ok64, (ok32, ok64)

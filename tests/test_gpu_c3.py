@@ -211,3 +211,59 @@ def test_info_tap_vs_oracle(pd, oracle_mod):
                 if k in FORCE_KEYS:
                     scale = max(scale, info["dynamic_pressure"] * A_FRONT)
                 assert abs(gv - ov) <= 1e-9 * scale, (tag, i, k, gv, ov)
+
+
+def test_c3_f32_handle_shadowed(pd, oracle_mod):
+    """The binary32 handle (the throughput precision: Taylor lines and binary32 cell pieces
+    through the fine index) on the c3 workload at full size, 65 536 envs x 240
+    steps; 96 sampled envs teacher-forced against the binary64 oracle at every step from the
+    handle's own (binary32) state: y, vy, mass, propellant and time within 1e-5 of max(|x|, 1)
+    (test_f32_teacher_forced's bound), the other channels within 2e-4, reward within 1e-4,
+    done/truncated/trunc_id equal in >= 99.5 % of the sampled steps (a binary32 quantity can sit
+    on the other side of a threshold); auto-resets within 1e-6 of the oracle's (the same Philox
+    draws; the binary32 reset adds the tilt in binary32) with the same wind percentile."""
+    import ctypes as C
+    import torch
+    from shadow import snapshot, _load
+    N, T, seed = 65536, 240, 1234
+    A = c3_actions(T, N, 7).cuda()
+    idx = c3_sample(N)
+    env = c3_env(pd, N, seed=seed, precision="f32")
+    L, P = oracle_mod.lib(), oracle_mod.params()
+    E, E2, o = oracle_mod.OrcEnv(), oracle_mod.OrcEnv(), oracle_mod.OrcOut()
+    it = torch.as_tensor(idx, device="cuda")
+    snap = snapshot(env, it)
+    keep = [1, 3, 8, 9, 10]
+    worst = np.zeros(11)
+    wrew, flips, n, resets = 0.0, 0, 0, 0
+    for t in range(T):
+        obs, rew, dn, tr, ex = env.step(A[t])
+        after = snapshot(env, it)
+        g_rew, g_dn, g_tr = rew[it].double().cpu().numpy(), dn[it].cpu().numpy(), tr[it].cpu().numpy()
+        a = A[t][it].cpu().numpy().astype(np.float64)
+        for j, g in enumerate(idx):
+            _load(L, P, E, snap, j, 0, seed, g, -1, math.radians(1.0))
+            u = (C.c_double * 4)(float(a[j, 0]), 0.0, 0.0, 0.0)
+            L.orc_step(C.byref(P), C.byref(E), 0, 0, u, 1, None, C.byref(o))
+            n += 1
+            if bool(g_dn[j]) != bool(o.done) or bool(g_tr[j]) != bool(o.trunc):
+                flips += 1
+                continue
+            wrew = max(wrew, abs(float(g_rew[j]) - o.reward))
+            if o.done or o.trunc:
+                resets += 1
+                L.orc_reset_philox(C.byref(P), C.byref(E2), 0, seed, int(g), (int(snap["ep"][j]) + 1) & 0xFFFFFFFF, 1, 1,
+                                   -1, math.radians(1.0))
+                ref = np.array(E2.s[:])   # (the binary32 reset adds the tilt in binary32)
+                assert (np.abs(after["s"][j] - ref) <= 1e-6 * np.maximum(np.abs(ref), 1.0)).all(), (t, g)
+                assert int(after["prof"][j]) == E2.wind_prof and int(after["ep"][j]) == int(snap["ep"][j]) + 1
+            else:
+                so = np.array(E.s[:])
+                worst = np.maximum(worst, np.abs(after["s"][j].astype(np.float64) - so) / np.maximum(np.abs(so), 1.0))
+        snap = after
+    assert worst[keep].max() <= 1e-5, dict(zip([ST[k] for k in keep], worst[keep]))
+    assert worst.max() <= 2e-4, dict(zip(ST, worst))
+    assert wrew <= 1e-4, wrew
+    assert flips <= 0.005 * n, (flips, n)
+    assert resets >= len(idx) // 2, resets
+    assert env.counters()["nan_events"] == 0

@@ -4,12 +4,12 @@
 # ran -- whatever its exit status -- is never started again.
 #   tools/gpurun_retry.sh LOG TIMEOUT 'command'
 log=$1; tmo=$2; shift 2
-for try in 1 2 3 4 5 6 7 8; do
+for try in $(seq 1 ${GPURUN_TRIES:-30}); do
   /usr/local/graft/bin/gpurun --timeout "$tmo" -- "$@" > "$log" 2>&1
   rc=$?
   if [ $rc -eq 3 ] || grep -q "status=transient" "$log"; then
     echo "[retry] no box (try $try, rc=$rc); waiting" >> "$log.retries"
-    sleep 200
+    sleep ${GPURUN_WAIT:-240}
     continue
   fi
   exit $rc
