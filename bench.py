@@ -74,6 +74,32 @@ def valu_roofline(mix, steps, kern_ms, simds=1024, clock_hz=2.4e9, fp64_peak_tfl
                       "per env-step"}
 
 
+def flop_roofline(oc, wc, n, steps, kern_ms, peak_tflops=78.6):
+    """Algorithmic binary64 FLOPs of the timed launches over their kernel time, against the FP64
+    vector peak: profiles/opcount.json's exact counts per unit (tools/opcount.cpp: the step's
+    arithmetic over a counting scalar type; add/sub/mul/div/sqrt 1, fma 2) weighted by what the
+    launches did (workload_counts: gust-band sub-steps and the table queries by path).  Per
+    env-step: 3 sub-steps with their own atmosphere and one reusing the rtd's, the wind profile
+    on each, the gust block on the gust-band ones, 8 table queries (2 tables x 4 sub-steps) by
+    path (clamped line: Taylor piece; interior: cell piece, + the side test in a bisector
+    sub-cell; verified: payload sums), and the step tail (g-load window, rtd, observation)."""
+    u = oc["units"]
+    f = lambda k, key="flops": u[k][key]
+    per_q = {key: wc["q_taylor_frac"] * f("q_line", key) + wc["q_cell_frac"] * f("q_piece", key)
+             + wc["q_bisect_frac"] * (f("q_bisect", key) - f("q_piece", key)) + wc["q_balanced_frac"] * f("q_payload", key)
+             for key in ("flops", "transcendentals")}
+    per = {key: 3 * f("substep", key) + f("substep_first", key) + 4 * f("wind_profile", key)
+                + 4 * wc["gust_steps_frac"] * f("gust", key) + 8 * per_q[key] + f("step_tail", key)
+           for key in ("flops", "transcendentals")}
+    achieved = per["flops"] * n * steps / (kern_ms * 1e-3) / 1e12
+    return {"bound": "fp64", "achieved": achieved, "peak": peak_tflops, "unit": "TFLOP/s",
+            "frac": achieved / peak_tflops, "flops_per_env_step": per["flops"],
+            "transcendentals_per_env_step": per["transcendentals"],
+            "query_flops_mean": per_q["flops"],
+            "source": "profiles/opcount.json (tools/opcount.cpp, checked by tests/test_opcount.py) x this "
+                      "window's workload_counts; the algorithm's arithmetic, not the instructions issued"}
+
+
 def shard_offset(rank, n_per_rank):
     """Global index of a rank's first env: contiguous shards, disjoint Philox streams."""
     return rank * n_per_rank
@@ -406,6 +432,10 @@ def c3_summary(args, r, world, precision, pmc=None):
         # over exactly the timed launches' env-steps and kernel time (a short timed region may be
         # one partial launch)
         out["valu_roofline"] = valu_roofline(mix, K, r["kern_total_ms"])
+    oc = load_pmc("opcount.json")
+    if oc and precision == "f64" and args.phase == "landing_burn_pure_throttle" and not args.no_wind \
+            and "q_taylor_frac" in r["counts"]:
+        out["flop_roofline"] = flop_roofline(oc, r["counts"], n, K, r["kern_total_ms"])
     return out
 
 

@@ -14,9 +14,13 @@ run() {  # name, seconds, command...
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
   return 0
 }
+if [ "${PART:-1}" = 1 ]; then
 run atan2 60 tools/bin/atan2_gpu_check
-run gpu_tests 900 python -u -m pytest tests/ -m gpu -x -q --timeout 120 --timeout-method thread
-run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+run gpu_tests 900 python -u -m pytest tests/ -m gpu --maxfail=6 -v --timeout 180 --timeout-method thread
+run smoke 200 python -c "import __graft_entry__ as g; g.smoke()"
+echo "=== done"
+exit 0
+fi
 for d in 0 1; do
   VARIANTS="base base0 nomk noat" FUSE=128 LAUNCHES=6 DESCENT=$d run exp_div_atan2_d$d 600 bash tools/exp_session.sh
 done
