@@ -137,6 +137,8 @@ def lib():
                                          C.c_int, P(C.c_float), C.c_int, C.c_int, C.c_int, C.c_int, D, C.c_uint64,
                                          P(D), P(C.c_uint8), P(C.c_uint8), P(C.c_int8), P(D), C.c_int, P(D),
                                          C.c_int, P(C.c_int64)]
+        L.orc_set_qlog.restype = None
+        L.orc_set_qlog.argtypes = [C.c_void_p]
         L.orc_gauss_pair.restype = None
         L.orc_gauss_pair.argtypes = [OrcU32x4, P(D), P(D)]
         L.orc_philox.restype = OrcU32x4
@@ -322,10 +324,11 @@ def rollout(phase, rtd, n_env, n_steps, actions_f32, auto_reset=True, wind=False
 
 
 def rollout_philox(phase, rtd, g, ep0, actions_f32, auto_reset=True, wind=True, stochastic=True, fixed_prof=-1,
-                   tilt=0.0, seed=0, obs_dim=2, threads=8, outputs=True):
+                   tilt=0.0, seed=0, obs_dim=2, threads=8, outputs=True, qclass=None):
     """The envs with global indices g (first episode ep0) under the device's Philox draw scheme,
     T steps of actions [T, n, A] float32: per-step reward/done/trunc/trunc_id [T, n], obs
-    [T, n, obs_dim] and the final state [n, 11] (outputs=False: only (sum, env-steps))."""
+    [T, n, obs_dim] and the final state [n, 11] (outputs=False: only (sum, env-steps)).
+    qclass: a uint8 [T, n, 4] array that receives each sub-step's table path (orc_set_qlog)."""
     acts = np.ascontiguousarray(actions_f32, dtype=np.float32)
     T, n = acts.shape[0], acts.shape[1]
     g = np.ascontiguousarray(g, dtype=np.uint64)
@@ -335,12 +338,19 @@ def rollout_philox(phase, rtd, g, ep0, actions_f32, auto_reset=True, wind=True, 
                trunc_id=np.zeros((T, n), np.int8), obs=np.zeros((T, n, max(obs_dim, 1))), state=np.zeros((n, 11)))
     ptr = lambda a, t: a.ctypes.data_as(P(t)) if outputs else None
     steps = C.c_int64()
-    acc = lib().orc_rollout_philox(C.byref(params()), phase, rtd, n, g.ctypes.data_as(P(C.c_uint64)),
+    if qclass is not None:
+        assert qclass.dtype == np.uint8 and qclass.shape == (T, n, 4) and qclass.flags.c_contiguous
+        lib().orc_set_qlog(qclass.ctypes.data)
+    try:
+        acc = lib().orc_rollout_philox(C.byref(params()), phase, rtd, n, g.ctypes.data_as(P(C.c_uint64)),
                                    ep0.ctypes.data_as(P(C.c_uint32)), T, acts.ctypes.data_as(P(C.c_float)),
                                    int(auto_reset), int(wind), int(stochastic), int(fixed_prof), float(tilt), int(seed),
                                    ptr(out["reward"], D), ptr(out["done"], C.c_uint8), ptr(out["trunc"], C.c_uint8),
                                    ptr(out["trunc_id"], C.c_int8), ptr(out["obs"], D), int(obs_dim),
                                    ptr(out["state"], D), int(threads), C.byref(steps))
+    finally:
+        if qclass is not None:
+            lib().orc_set_qlog(None)
     if not outputs:
         return acc, steps.value
     return out

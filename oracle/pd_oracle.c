@@ -381,6 +381,14 @@ static void vk_step(const double* Ad, const double* Bd, double sigma, double* s,
 /* One rocket_physics_fcn call (rockets_physics.py:455-704).  kout == NULL: the reference's
  * semi-implicit Euler update of E->s at dt.  kout != NULL (the non-parity RK4 mode): E->s is left
  * alone and kout receives d/dt of (x, y, vx, vy, theta, theta_dot, mass, mass_propellant). */
+/* Analysis hook (tools/regime_persistence.py; nothing on the parity path reads it): when a log
+ * is set, each Euler sub-step of orc_rollout_philox records which table path its two queries
+ * take: 1 = the clamped lines (|degrees(alpha_eff)| > radians(10), both tables clamp), 2 = the
+ * interior grids, 0 = no query (a == 0). */
+static uint8_t* g_qlog;
+static __thread uint8_t* g_qlog_step;
+void orc_set_qlog(uint8_t* buf) { g_qlog = buf; }
+
 static void substep(const orc_params* P, orc_env* E, int phase, const double* u, int f32,
                     double dt, double dt_act, const double* noise2, double* info, double* kout) {
     double* s = E->s;
@@ -402,6 +410,8 @@ static void substep(const orc_params* P, orc_env* E, int phase, const double* u,
     double d_thrust = x_cog + P->engine_height;
     double ae = (vy < 0) ? ga - th - PI : al;
     double d_cp_cg = x_cog - (ascent ? P->cop_ascent : P->cop);
+    if (g_qlog_step && !kout && E->cur_sub >= 0 && E->cur_sub < 4)
+        g_qlog_step[E->cur_sub] = a == 0.0 ? 0 : (fabs(degrees(ae)) > radians(10.0) ? 1 : 2);
     double ug = 0.0, vg = 0.0;
     if (E->wind_on) {
         ug = wind_profile(P, E, y);
@@ -1094,7 +1104,9 @@ static void philox_range(philox_job* j) {
         for (int t = 0; t < j->n_steps; ++t) {
             double u[4] = {0, 0, 0, 0};
             for (int k = 0; k < A; ++k) u[k] = j->actions[((size_t)t * j->n + i) * A + k];
+            g_qlog_step = g_qlog ? g_qlog + ((size_t)t * j->n + i) * 4 : NULL;
             orc_step(P, &E, j->phase, j->rtd, u, 1, NULL, &o);
+            g_qlog_step = NULL;
             acc += o.reward; ++steps;
             const size_t at = (size_t)t * j->n + i;
             if (j->reward) j->reward[at] = o.reward;

@@ -22,7 +22,7 @@ echo "=== done"
 exit 0
 fi
 for d in 0 1; do
-  VARIANTS="base base0 nomk noat" FUSE=128 LAUNCHES=6 DESCENT=$d run exp_div_atan2_d$d 600 bash tools/exp_session.sh
+  VARIANTS="base nowqx base0 nomk noat" FUSE=128 LAUNCHES=6 DESCENT=$d run exp_div_atan2_d$d 600 bash tools/exp_session.sh
 done
 run benchdrv 600 python bench.py --steps 20 --warmup 5
 run bench 600 python bench.py
