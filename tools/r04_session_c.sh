@@ -1,0 +1,41 @@
+#!/bin/bash
+# Round-4 session C, in parts (PART=1|2|3), each under its own gpurun call:
+#   1: the round-4 kernel changes timed against variants built without each (c3 and c3-descent,
+#      128 steps per launch, two interleaved rounds): nowqx = no workgroup query exchange
+#      (-DPD_WQX=0), nomk = IEEE divisions for the known divisors (-DPD_MARKSTEIN=0), noat = the
+#      device library's atan2 (-DPD_ATAN2_FD=0); then c2 (4 096 envs, no wind) at LPE 16 / 8 / 2.
+#   2: the bench lines (driver command, defaults, c4, c5), the policy lanes-per-env sweep, and
+#      rocprofv3 kernel traces of the default, driver-command, c4 and c5 runs.
+#   3: PMC passes (tools/pmc_r03b.sh: traffic, instruction mix, waits and LDS, c3 and c3-descent).
+# Variants: python -c "from pdenv import build as b; b.build_variant('nowqx', ['-DPD_WQX=0'])" etc.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+run() {  # name, seconds, command...
+  local name=$1 secs=$2; shift 2
+  echo "=== $name ($(date +%T))"
+  timeout -k 10 "$secs" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "    rc=$rc"; tail -n 3 "gpurun_out/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
+  return 0
+}
+case "${PART:-1}" in
+1)
+  for d in 1 0; do
+    VARIANTS="base nowqx nomk noat" FUSE=128 LAUNCHES=6 DESCENT=$d run exp_r04_d$d 500 bash tools/exp_session.sh
+  done
+  for l in 16 8 2; do
+    N=4096 WIND=0 TILT=0 LPE=$l FUSE=128 LAUNCHES=6 run c2_lpe$l 200 python tools/time_fused.py
+  done ;;
+2)
+  run benchdrv 400 python bench.py --steps 20 --warmup 5
+  run bench 400 python bench.py
+  run c4 300 python bench.py --workload c4
+  run c5 300 python bench.py --workload c5
+  run plpe 300 python tools/policy_lpe_sweep.py
+  STAGES="prof profdrv profc4 profc5" run profs 900 bash tools/gpu_session.sh ;;
+3)
+  run pmc 900 bash tools/pmc_r03b.sh ;;
+esac
+echo "=== done"
