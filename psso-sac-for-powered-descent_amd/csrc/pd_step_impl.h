@@ -413,9 +413,10 @@ struct TayRef { int piece, cell; bool line, verify, refined, bisect; int cp; dou
 
 struct NoPre { __device__ void operator()() const {} };
 
-// PD_WQX=0 builds the LPE-2 step kernels without the workgroup query exchange (rbf2_exchange)
+// PD_WQX=1 (experiments) builds the LPE-2 pure-throttle step kernels with the workgroup query
+// exchange (rbf2_exchange); measured 20-25 % slower than the per-lane path
 #ifndef PD_WQX
-#define PD_WQX 1
+#define PD_WQX 0
 #endif
 
 // pre(): the caller's work that does not depend on the tables, run while the grid loads are in
@@ -599,24 +600,6 @@ __device__ __forceinline__ int rbf_lookup(const AT& a, DP<R>& P, int table, cons
     return slot;
 }
 
-// This lane's share of the RBF value of `table` at (M, aq): lookup, evaluation, and the
-// wave-cooperative solve of missed neighbourhoods.
-template <typename R, typename AT>
-__device__ __forceinline__ R rbf(const AT& a, DP<R>& P, int table, const TabView<R>& t, const LineLds<R>& ln,
-                                 RbfCache<R>& cache, R M, R aq, int part, int nparts) {
-    const int slot = rbf_lookup<R>(a, P, table, t, ln, cache, M, aq);
-    const unsigned long long key = cache.key;
-    R val = R(0);
-    if (slot >= 0) val = rbf_eval<R>(t.pay + (int64_t)slot * pay_stride<R>(), t.smach, M, aq, part, nparts);
-    // Misses (a neighbourhood outside the pre-enumerated tables) take the wave-cooperative
-    // exact solve; the loop in rbf_miss_wave runs only when some lane of the wave missed
-    if (__ballot(slot < 0)) {
-        R mv = rbf_miss_wave<R>(a, P, table, t.smach, key, M, aq, part, nparts, slot < 0);
-        if (slot < 0) val = mv;
-    }
-    return val;
-}
-
 // ---------------------------------------------------------------- LPE 2: Taylor lines + balanced sums
 // A clamped-line query's value from its Taylor piece (pdenv.hip build_taylor): the degree-
 // kTayDeg polynomial in M - (cell centre) plus the piece's exact terms.
@@ -666,6 +649,44 @@ __device__ __forceinline__ R cell_eval(const PD_AS1 R* __restrict__ rec, R M, R 
         f = fma(x[1] * d2, eval_log4<R>(sizeof(R) == 8 ? d2 : (d2 > R(1e-30) ? d2 : R(1e-30))), f);
     }
     return f;
+}
+
+// This lane's share of the RBF value of `table` at (M, aq): lookup, evaluation, and the
+// wave-cooperative solve of missed neighbourhoods.
+// Trusted clamped-line queries take their Taylor piece and trusted interior queries their cell
+// piece (handles with pieces), as rbf2 does: every lane of the table's group evaluates the same
+// piece (one pass of the instruction stream for all of them) and part 0 returns it, the other
+// parts 0 -- the caller's shuffle sum then adds exact zeros.  The other queries split the payload
+// sum over the parts.  PCS = false: payload sums for every hit (the kernels where the piece code
+// would spill: wind, RK4, policy and run-time-phase instantiations); PD_PIECES_LPE=0
+// (experiments): false everywhere.
+#ifndef PD_PIECES_LPE
+#define PD_PIECES_LPE 1
+#endif
+template <bool PCS, typename R, typename AT>
+__device__ __forceinline__ R rbf(const AT& a, DP<R>& P, int table, const TabView<R>& t, const LineLds<R>& ln,
+                                 RbfCache<R>& cache, R M, R aq, int part, int nparts) {
+    TayRef tr{-1, 0, false, false, false, false, -1, 0.0, 0.0, false};
+    const int slot = rbf_lookup<R>(a, P, table, t, ln, cache, M, aq, (PCS && PD_PIECES_LPE) ? &tr : nullptr);
+    const bool tay = tr.piece >= 0;
+    const bool cel = tr.cp >= 0;
+    R val = R(0);
+    if (tay) val = taylor_eval<R>(gbl(P.tay) + (size_t)tr.piece * kTayStride, M, tr.cell);
+    if (cel) {
+        const PD_AS1 R* rec = t.cell_pc + (size_t)tr.cp * cell_stride<R>();
+        val = cell_eval<R>(rec, M, aq, (R)tr.cu, (R)tr.cv);
+        if (tr.fine) cache.key = *(const PD_AS1 unsigned long long*)(rec + cell_key<R>());
+    }
+    if ((tay || cel) && part != 0) val = R(0);
+    if (!tay && !cel && slot >= 0) val = rbf_eval<R>(t.pay + (int64_t)slot * pay_stride<R>(), t.smach, M, aq, part, nparts);
+    // Misses (a neighbourhood outside the pre-enumerated tables) take the wave-cooperative
+    // exact solve; the loop in rbf_miss_wave runs only when some lane of the wave missed
+    const bool miss = !tay && !cel && slot < 0;
+    if (__ballot(miss)) {
+        R mv = rbf_miss_wave<R>(a, P, table, t.smach, cache.key, M, aq, part, nparts, miss);
+        if (miss) val = mv;
+    }
+    return val;
 }
 
 // Per-wave LDS of the balanced evaluation: the wave's payload queries by rank (Mach, AoA
@@ -1226,6 +1247,8 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
     // one call of rocket_physics_fcn at dt, actuators at the same dt (rockets_physics.py:728-997)
     static_assert(!RK4 || (PHASE == 0 && !WIND && !POL), "RK4: pure throttle, no wind, no policy");
     constexpr int NSUB = RK4 ? 40 : (PHASE == 2 ? 1 : 4);
+    // LPE != 2: pieces for the trusted queries (rbf) where they fit the register file (c2, c5)
+    constexpr bool kPcs = !WIND && !RK4 && POL == 0 && (PHASE == 0 || (PHASE == 1 && !SAC));
     const R dt = RK4 ? R(0.01) : (PHASE == 0 ? R(0.025) : (PHASE == 1 ? R(0.1) : (R)a.dt_aux));
     const R dt_act = PHASE == 2 ? dt : R(0.025);
     PD_T(t_loaded);
@@ -1468,8 +1491,8 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
             if constexpr (LPE == 1) {
                 // (both sums interleaved in lockstep on one lane, 1 wave per SIMD with AGPR
                 // spill space, measured 14 % slower than these two calls)
-                R v = rbf<R>(a, P, 1, tab_view_lds<R>(L.tdesc, 1), L.lines, cB, mach, aq_cl, 0, 1);
-                R w = rbf<R>(a, P, 0, tab_view_lds<R>(L.tdesc, 0), L.lines, cA, mach, aq_cd, 0, 1);
+                R v = rbf<kPcs, R>(a, P, 1, tab_view_lds<R>(L.tdesc, 1), L.lines, cB, mach, aq_cl, 0, 1);
+                R w = rbf<kPcs, R>(a, P, 0, tab_view_lds<R>(L.tdesc, 0), L.lines, cA, mach, aq_cd, 0, 1);
                 CL = (!have || cl_zero) ? R(0) : (cl_sgn < R(0) ? -v : v);
                 CD = have ? w : R(0);
             } else {
@@ -1488,8 +1511,8 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
 #endif
                                 );
                 else
-                    v = rbf<R>(a, P, my_table, tab_view_lds<R>(L.tdesc, my_table), L.lines, cA, mach,
-                               my_table ? aq_cl : aq_cd, part, nparts);
+                    v = rbf<kPcs, R>(a, P, my_table, tab_view_lds<R>(L.tdesc, my_table), L.lines, cA, mach,
+                                     my_table ? aq_cl : aq_cd, part, nparts);
                 if constexpr (nparts >= 2) v += __shfl_xor(v, 1);
                 if constexpr (nparts >= 4) v += __shfl_xor(v, 2);
                 if constexpr (nparts >= 8) v += __shfl_xor(v, 4);

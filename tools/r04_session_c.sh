@@ -37,5 +37,17 @@ case "${PART:-1}" in
   STAGES="prof profdrv profc4 profc5" run profs 900 bash tools/gpu_session.sh ;;
 3)
   run pmc 900 bash tools/pmc_r03b.sh ;;
+4)
+  # after part 1 (the exchange 20-25 % slower, atan2_fd slower than the library's): base = no
+  # exchange; at0 = library atan2, mk0 = IEEE divisions, wqx1 = the exchange; c2 (4 096 envs, no
+  # wind): pieces at LPE 16 / 8 (base) against payload sums (c2pl0) and the library atan2 (c2at0)
+  run gpu_lpe_tests 400 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 200 --timeout-method thread \
+      -k "batched_random or ragged or step_n_fused or sac or device_solve or cell_pieces"
+  for d in 1 0; do
+    VARIANTS="base at0 mk0 wqx1" FUSE=128 LAUNCHES=6 DESCENT=$d run exp_r04b_d$d 500 bash tools/exp_session.sh
+  done
+  for l in 16 8; do
+    VARIANTS="base c2pl0 c2at0" N=4096 WIND=0 TILT=0 LPE=$l FUSE=128 LAUNCHES=6 run exp_r04b_c2_lpe$l 300 bash tools/exp_session.sh
+  done ;;
 esac
 echo "=== done"
