@@ -233,11 +233,11 @@ template <> __device__ __forceinline__ void pd_sincos<double>(double x, double& 
 }
 
 // ---------------------------------------------------------------- flight-path angle
-// gamma = atan2(vy, vx) (rockets_physics.py:631): binary64 by atan2_fd (pd_common.h; <= 1 ulp of
-// glibc's, about half the device library's instructions), binary32 by the device library.
-// PD_ATAN2_FD=0 (experiments): the device library's atan2 for both.
+// gamma = atan2(vy, vx) (rockets_physics.py:631): the device library's atan2.  PD_ATAN2_FD=1
+// (experiments) takes atan2_fd (pd_common.h; <= 1 ulp of glibc's, one division) for binary64:
+// measured 3 % slower on c3 and c3-descent, 5 % on c2 (profiles/r04_exp_s2_variants.jsonl).
 #ifndef PD_ATAN2_FD
-#define PD_ATAN2_FD 1
+#define PD_ATAN2_FD 0
 #endif
 template <typename R> __device__ __forceinline__ R pd_atan2(R y, R x) { return atan2(y, x); }
 #if PD_ATAN2_FD

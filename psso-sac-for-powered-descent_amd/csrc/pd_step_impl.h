@@ -658,7 +658,7 @@ __device__ __forceinline__ R cell_eval(const PD_AS1 R* __restrict__ rec, R M, R 
 // piece (one pass of the instruction stream for all of them) and part 0 returns it, the other
 // parts 0 -- the caller's shuffle sum then adds exact zeros.  The other queries split the payload
 // sum over the parts.  PCS = false: payload sums for every hit (the kernels where the piece code
-// would spill: wind, RK4, policy and run-time-phase instantiations); PD_PIECES_LPE=0
+// would spill: wind, RK4, run-time-phase and landing-burn SAC instantiations); PD_PIECES_LPE=0
 // (experiments): false everywhere.
 #ifndef PD_PIECES_LPE
 #define PD_PIECES_LPE 1
@@ -1247,8 +1247,10 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
     // one call of rocket_physics_fcn at dt, actuators at the same dt (rockets_physics.py:728-997)
     static_assert(!RK4 || (PHASE == 0 && !WIND && !POL), "RK4: pure throttle, no wind, no policy");
     constexpr int NSUB = RK4 ? 40 : (PHASE == 2 ? 1 : 4);
-    // LPE != 2: pieces for the trusted queries (rbf) where they fit the register file (c2, c5)
-    constexpr bool kPcs = !WIND && !RK4 && POL == 0 && (PHASE == 0 || (PHASE == 1 && !SAC));
+    // LPE != 2: pieces for the trusted queries (rbf) where they fit the register file without
+    // spilling (no wind, no RK4, not the landing-burn SAC kernel): c2, c5, the policy sweep
+    // (LPE 16 measured 6 % slower with them: its split payload sum is as short as a piece)
+    constexpr bool kPcs = !WIND && !RK4 && LPE <= 8 && (PHASE == 0 || (PHASE == 1 && !SAC));
     const R dt = RK4 ? R(0.01) : (PHASE == 0 ? R(0.025) : (PHASE == 1 ? R(0.1) : (R)a.dt_aux));
     const R dt_act = PHASE == 2 ? dt : R(0.025);
     PD_T(t_loaded);

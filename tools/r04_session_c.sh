@@ -49,5 +49,21 @@ case "${PART:-1}" in
   for l in 16 8; do
     VARIANTS="base c2pl0 c2at0" N=4096 WIND=0 TILT=0 LPE=$l FUSE=128 LAUNCHES=6 run exp_r04b_c2_lpe$l 300 bash tools/exp_session.sh
   done ;;
+5)
+  # the build with the measured defaults (no exchange, library atan2, pieces at LPE 4/8): the GPU
+  # suite and smoke, c3 / c3-descent at LPE 1 and 2, the bench lines
+  run gpu_tests 600 python -u -m pytest tests/ -m gpu -x -q --timeout 200 --timeout-method thread
+  run smoke 200 python -c "import __graft_entry__ as g; g.smoke()"
+  for d in 0 1; do for l in 2 1; do
+    LPE=$l FUSE=128 LAUNCHES=6 DESCENT=$d run lpe_c3_d${d}_l$l 200 python tools/time_fused.py
+  done; done
+  run benchdrv 300 python bench.py --steps 20 --warmup 5
+  run bench 400 python bench.py ;;
+6)
+  run c4 300 python bench.py --workload c4
+  run c5 300 python bench.py --workload c5
+  run c2 300 python bench.py --workload c2 --cpu-baseline 0
+  run plpe 300 python tools/policy_lpe_sweep.py
+  STAGES="prof profdrv profc4 profc5" run profs 700 bash tools/gpu_session.sh ;;
 esac
 echo "=== done"
