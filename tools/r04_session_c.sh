@@ -65,5 +65,13 @@ case "${PART:-1}" in
   run c2 300 python bench.py --workload c2 --cpu-baseline 0
   run plpe 300 python tools/policy_lpe_sweep.py
   STAGES="prof profdrv profc4 profc5" run profs 700 bash tools/gpu_session.sh ;;
+7)
+  # PD_STAMP section clocks of the c3 kernel (libpdenv_stamp.so: build_variant('stamp',
+  # ['-DPD_STAMP'])), then the PMC passes (traffic, instruction mix, waits / LDS)
+  for d in 0 1; do
+    STATS=1 DESCENT=$d FUSE=128 LAUNCHES=3 PDENV_LIB=psso-sac-for-powered-descent_amd/pdenv/libpdenv_stamp.so \
+      run stamp_d$d 200 python tools/time_fused.py
+  done
+  run pmc 900 bash tools/pmc_r03b.sh ;;
 esac
 echo "=== done"
