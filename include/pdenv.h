@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define PD_ABI_VERSION 7   /* 4: pd_config.integrator (was padding); 5: pd_count_work, pd_step_sac; 6: cell pieces (pd_cell_piece_info, stats word 44); 7: pd_step_sac_ring, pd_sac_actor, stats word 45 */
+#define PD_ABI_VERSION 8   /* 4: pd_config.integrator (was padding); 5: pd_count_work, pd_step_sac; 6: cell pieces (pd_cell_piece_info, stats word 44); 7: pd_step_sac_ring, pd_sac_actor, stats word 45; 8: pd_step_sac_fused, pd_smooth_tables */
 #define PD_MAX_PTS 256      /* aero scatter points per table */
 #define PD_MAX_COLS 5       /* AoA columns per aero table */
 #define PD_MAX_TAB 64       /* grid-fin table length */
@@ -254,6 +254,20 @@ pd_status pd_step_sac_ring(pd_env* env, const float* heads, int32_t deterministi
  * torch's GEMMs: equal to f32 rounding.  Runs on the current HIP device. */
 pd_status pd_sac_actor(int64_t n, int32_t state_dim, int32_t hidden, int32_t n_hidden_layers, int32_t action_dim,
                        const float* obs, const float* const* params, float* heads, void* stream);
+/* The whole SAC collection step (sac_pytorch_powered_descent.py:160-183: actor.sample on the
+ * current observation, env.step, buffer.add) in ONE launch: pd_sac_actor's forward pass
+ * (sac_pytorch.py:129-159) runs in the step kernel's prologue for each workgroup's 16 envs, on
+ * obs32 [N][S] as the previous step (or pd_observe) left it, then pd_step_sac_ring follows with
+ * those heads (same arguments and semantics; obs32 is overwritten with the next observation).
+ * hidden / n_hidden_layers / params as pd_sac_actor; heads [N][2A] (may be NULL) receives the
+ * heads.  Handles stepping 16 lanes per env (the default up to 4 096 envs) with hidden <= 256
+ * take the single launch; others run pd_sac_actor + pd_step_sac_ring (two launches, the same
+ * bits).  No host synchronisation. */
+pd_status pd_step_sac_fused(pd_env* env, int32_t hidden, int32_t n_hidden_layers, const float* const* params,
+                            float* heads, int32_t deterministic, float log_std_min, float log_std_max,
+                            float max_action, float* eps_out, float* action, float* ring, int64_t capacity,
+                            long long* ring_state, float* priorities, const float* max_priority, float* obs32,
+                            void* stream);
 /* Multi-step rollout with device-resident actions [T][N][A]: the fused launches of pd_step_n
  * (per-step launches for the other phases), rewards accumulated into reward_sum [N] (may be
  * NULL), no per-step outputs.  No host synchronisation. */
@@ -380,6 +394,13 @@ pd_status pd_count_work(pd_env* env, int32_t enable);
  * with a valid binary64 / binary32 piece; piece >= 0 (an exact cell's piece is at its
  * cell index im na + ia): its record at out[16 ...] (n_out >= 16 + stride). */
 pd_status pd_cell_piece_info(const pd_params* params, int32_t table, int64_t piece, double* out, int32_t n_out);
+/* The step kernel's tabulated smooth functions, built and evaluated on the host in the device's
+ * order and precision (test hook; no device needed): the ISA atmosphere (atmosphere_dynamics.py:
+ * 5-27; rho, p, a into atm_out [n_alt][3]) at geometric altitudes alt, and the stage-2 mass
+ * properties (rocket_dimensions.py:167-196; x_cog, I into inr_out [n_fill][2]) at fills in (0, 1];
+ * max_rel[0..1]: the builders' worst relative error against the long double formulas. */
+pd_status pd_smooth_tables(const pd_params* params, int32_t precision, const double* alt, int64_t n_alt,
+                           double* atm_out, const double* fill, int64_t n_fill, double* inr_out, double* max_rel);
 /* Observation / action widths of the handle. */
 int pd_obs_dim(const pd_env* env);
 int pd_action_dim(const pd_env* env);

@@ -11,6 +11,7 @@
 
 #include "../../include/pdenv.h"
 #include "pd_physics.h"
+#include "pd_sac_mlp.h"
 
 namespace pd {
 
@@ -183,6 +184,12 @@ template <typename R> struct StepArgs {
     long long* ring_state;
     float* prio;
     const float* max_prio;
+    // pd_step_sac_fused (16 lanes per env): the actor's forward pass for the workgroup's 16 envs
+    // in the kernel prologue (pd_sac_mlp.h sac_mlp_tile) on obs32 as the previous step left it, the
+    // heads into LDS (and into sac_heads_out [N][2A] when given); sac_mlp.H = 0: heads from
+    // sac_mean / sac_logstd
+    SacMlp sac_mlp;
+    float* sac_heads_out;
 };
 
 // Kernel launchers, explicitly instantiated in the kstep_*.hip translation units.

@@ -1122,6 +1122,26 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
     // reads it before the last one advances it, see the end of the kernel)
     int64_t ring_pos0 = 0;
     if constexpr (SAC) { if (a.ring_state) ring_pos0 = (int64_t)__atomic_load_n(a.ring_state, __ATOMIC_RELAXED); }
+    // pd_step_sac_fused (16 lanes per env: the workgroup's 16 envs are one MLP tile): the actor's
+    // heads of this step from the observation the previous step left in obs32, into s_sach (read
+    // by the sampling below; the staging barrier orders them), before anything else of the step
+    constexpr bool kSacMlp = SAC && LPE == 16;
+    __shared__ __attribute__((aligned(16))) float s_mlp[kSacMlp ? sac_mlp_lds_floats<256>() : 1];
+    __shared__ float s_sach[kSacMlp ? kSacTile * 16 : 1];
+    if constexpr (kSacMlp) {
+        const int H = a.sac_mlp.H;   // (grid-uniform: the barriers inside are reached by every thread)
+        if (H) {
+            const int64_t e0 = (int64_t)blockIdx.x * kSacTile;
+            const int A2 = a.sac_mlp.A;
+            auto put = [&](int e, int o, float v) {
+                s_sach[e * 16 + (o < A2 ? o : 8 + o - A2)] = v;
+                if (a.sac_heads_out && e0 + e < a.n) a.sac_heads_out[(e0 + e) * 2 * A2 + o] = v;
+            };
+            if (H == 128) sac_mlp_tile<128>(a.sac_mlp, a.n, e0, s_mlp, put);
+            else sac_mlp_tile<256>(a.sac_mlp, a.n, e0, s_mlp, put);
+            __syncthreads();   // (s_mlp is free again; the heads wait for the staging barrier)
+        }
+    }
     if constexpr (POL) {
         if (blockIdx.x == 0 && threadIdx.x == 0) *a.cnt_zero = 0u;
         if (a.use_list) {
@@ -1345,12 +1365,13 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
                 if (k + 1 < A) ed[k + 1] = (float)z1;
             }
         }
+        const bool mlp = kSacMlp && a.sac_mlp.H != 0;   // heads from the prologue's LDS rows
 #pragma unroll
         for (int k = 0; k < A; ++k) if (k < AD) {
-            const float m = ldv(a.sac_mean + k, ui * a.sac_hs);
+            const float m = mlp ? s_sach[le * 16 + k] : ldv(a.sac_mean + k, ui * a.sac_hs);
             float xk = m;
             if (a.sac_eps || a.sac_draw) {
-                float ls = ldv(a.sac_logstd + k, ui * a.sac_hs);
+                float ls = mlp ? s_sach[le * 16 + 8 + k] : ldv(a.sac_logstd + k, ui * a.sac_hs);
                 ls = ls < a.sac_lo ? a.sac_lo : (ls > a.sac_hi ? a.sac_hi : ls);
                 const float sd = expf(ls);
                 const float ek = a.sac_draw ? ed[k] : ldv(a.sac_eps + k, ui * AD);
@@ -1538,7 +1559,7 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
         R x_cog, I;
         // subrocket_0 (full rocket) closures for the ascent, subrocket_2 after (:748-750, :772-774)
         if (ascent) inertia_full<R>(P, R(1) - fpc, x_cog, I);
-        else inertia<R>(P, R(1) - fpc, x_cog, I);
+        else inertia_fast<R>(P, R(1) - fpc, x_cog, I);
         R d_thrust = x_cog + P.engine_height;
         R d_cp_cg = x_cog - (ascent ? P.cop_ascent : P.cop);
         if constexpr (LPE != 2) wind_block();
@@ -2117,18 +2138,22 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
 // ---------------------------------------------------------------- launchers
 template <typename R, int PH, int RT, bool W, int LPE, bool RK> void launch_step(const StepArgs<R>& a, hipStream_t s) {
     unsigned grid = (unsigned)((a.n * LPE + kStepBlock - 1) / kStepBlock);
+    // the SAC instantiation: heads from the caller (sac_mean) or from the kernel's own actor
+    // prologue (sac_mlp.H, pd_step_sac_fused: sac_mean is then NULL and a.actions too)
+    const bool sac = a.sac_mean != nullptr || a.sac_mlp.H != 0;
     if constexpr (LPE == 2 && !RK) {
-        if (a.count_work && !a.sac_mean) {
+        if (a.count_work && !sac) {
             hipLaunchKernelGGL((k_step<R, PH, RT, W, LPE, 0, RK, true>), dim3(grid), dim3(kStepBlock), 0, s, a);
             return;
         }
     }
     if constexpr (RT == 0 && PH <= 1 && !RK) {
-        if (a.sac_mean) {
+        if (sac) {
             hipLaunchKernelGGL((k_step<R, PH, RT, W, LPE, 0, RK, false, true>), dim3(grid), dim3(kStepBlock), 0, s, a);
             return;
         }
     }
+    if (sac) return;   // (no SAC instantiation for this kernel family: pdenv.hip refuses such handles first)
     hipLaunchKernelGGL((k_step<R, PH, RT, W, LPE, 0, RK>), dim3(grid), dim3(kStepBlock), 0, s, a);
 }
 

@@ -294,6 +294,180 @@ pd_status build_line(const pd_aero_table& t, double a, Table<R>& T, int li, DevP
 // >= 0.024 past the two nearest AoA-10 points), so the truncation is below binary64 rounding;
 // every piece is checked at five points against the long double sum and a line whose worst
 // error exceeds 1e-13 relative to sum |c_j phi_j| is left to the exact path (tay_off = -1).
+// ---------------------------------------------------------------- smooth-function tables
+// Least-squares fit of a degree-deg polynomial in t = x - c to f on [lo, hi] (c the centre), from
+// 4 (deg + 1) Chebyshev nodes, in long double (monomials in s = t / h on [-1, 1]: well conditioned
+// at these degrees); coefficients of t^k into out[0..deg].
+template <typename F>
+void fit_poly_ld(F&& f, long double lo, long double hi, int deg, long double* out) {
+    const int M = 4 * (deg + 1), n = deg + 1;
+    const long double c = (lo + hi) / 2, h = (hi - lo) / 2;
+    long double A[12][12] = {}, b[12] = {};
+    for (int m = 0; m < M; ++m) {
+        const long double s = cosl(3.14159265358979323846264338327950288L * (m + 0.5L) / M);
+        const long double v = f(c + h * s);
+        long double pw[12];
+        pw[0] = 1;
+        for (int k = 1; k < n; ++k) pw[k] = pw[k - 1] * s;
+        for (int i = 0; i < n; ++i) {
+            b[i] += pw[i] * v;
+            for (int j = 0; j < n; ++j) A[i][j] += pw[i] * pw[j];
+        }
+    }
+    for (int k = 0; k < n; ++k) {   // Gaussian elimination with partial pivoting (normal equations)
+        int pv = k;
+        for (int i = k + 1; i < n; ++i) if (fabsl(A[i][k]) > fabsl(A[pv][k])) pv = i;
+        for (int j = 0; j < n; ++j) std::swap(A[k][j], A[pv][j]);
+        std::swap(b[k], b[pv]);
+        for (int i = k + 1; i < n; ++i) {
+            const long double l = A[i][k] / A[k][k];
+            for (int j = k; j < n; ++j) A[i][j] -= l * A[k][j];
+            b[i] -= l * b[k];
+        }
+    }
+    long double x[12];
+    for (int i = n - 1; i >= 0; --i) {
+        long double s = b[i];
+        for (int j = i + 1; j < n; ++j) s -= A[i][j] * x[j];
+        x[i] = s / A[i][i];
+    }
+    long double hk = 1;
+    for (int k = 0; k < n; ++k) { out[k] = x[k] / hk; hk *= h; }
+}
+
+// The device's Horner evaluation of coefficients q[0..deg] (in R) at t, in R
+template <typename R> R horner_host(const R* q, int deg, R t) {
+    R f = q[deg];
+    for (int k = deg - 1; k >= 0; --k) f = (R)std::fma((double)f, (double)t, (double)q[k]);
+    return f;
+}
+
+// The ISA atmosphere of atmosphere_dynamics.py:5-27 (ambiance restated, as the device's exact
+// path and the oracle compute it) in long double, in layer i: rho, p, a at geometric altitude y
+struct AtmLd { long double rho, p, a; };
+AtmLd atm_exact_ld(const pd_params* P, int i, long double y) {
+    const long double r = P->isa_r, R_ = P->isa_R, g0 = P->isa_g0;
+    const long double H = r * y / (r + y), dH = H - (long double)P->isa_Hb[i];
+    const long double Tb = P->isa_Tb[i], b = P->isa_beta[i], pb = P->isa_pb[i];
+    const long double T = Tb + b * dH;
+    const long double p = b != 0 ? pb * powl(1 + b / Tb * dH, -g0 / (b * R_)) : pb * expl(-g0 / (R_ * Tb) * dH);
+    return {p / (R_ * T), p, sqrtl((long double)P->isa_kappa * R_ * T)};
+}
+
+// rho, p, a as piecewise polynomials in the geometric altitude (atmosphere_tab, pd_physics.h):
+// cells of kAtmW metres over [0, isa_alt_max); a cell holds its piece and, past a layer boundary
+// inside it (H = Hb: a kink of T, and a jump of p by the rounding of the tabulated pb), a second
+// piece, with the boundary's Hb as the split (record word 1).  Every piece is
+// checked at 33 points in R arithmetic (the device's Horner order) against the long double ISA;
+// the worst relative error goes to max_rel (binary64: 2e-16 typical, 2e-15 at worst next to a
+// layer boundary -- the closed form's own binary64 rounding is up to 5e-15 there, the pow of
+// 1 + b/Tb dH rounded once amplified by its exponent, about 34).
+template <typename R>
+void build_atm_table(const pd_params* P, std::vector<R>& out, int& n_cells, double& max_rel) {
+    const double w = kAtmW, top = P->isa_alt_max;
+    n_cells = (int)std::ceil(top / w);
+    out.assign((size_t)n_cells * kAtmStride, R(0));
+    max_rel = 0;
+    const long double r = P->isa_r;
+    auto layer_of = [&](long double y) {
+        const long double H = r * y / (r + y);
+        int i = 0;
+        for (int k = 0; k < 9; ++k) if ((long double)P->isa_Hb[k] <= H) i = k;
+        return i;
+    };
+    for (int k = 0; k < n_cells; ++k) {
+        const long double lo = (long double)k * w, hi = std::min<long double>((long double)(k + 1) * w, top);
+        const int il = layer_of(lo), ih = layer_of(hi - 1e-9L);
+        long double split = hi;
+        if (ih != il) {   // the boundary y of H = Hb[ih]: y = r Hb / (r - Hb)
+            const long double Hb = P->isa_Hb[ih];
+            split = r * Hb / (r - Hb);
+        }
+        for (int half = 0; half < (ih != il ? 2 : 1); ++half) {
+            const long double a0 = half ? split : lo, a1 = half ? hi : split;
+            const int li = half ? ih : il;
+            R* rec = out.data() + (size_t)k * kAtmStride + half * kAtmRec;
+            long double q[3][kAtmDeg + 1];
+            for (int fn = 0; fn < 3; ++fn)
+                fit_poly_ld([&](long double y) { const AtmLd v = atm_exact_ld(P, li, y);
+                                                 return fn == 0 ? v.p : (fn == 1 ? v.rho : v.a); },
+                            a0, a1, kAtmDeg, q[fn]);
+            const long double c = (a0 + a1) / 2;
+            rec[0] = (R)c;
+            // the split as the layer's base H: the device takes the upper piece where the exact path
+            // takes the upper layer, Hb <= r alt / (r + alt) in R (the ISA's pb are rounded
+            // constants: p jumps by ~4e-6 across 47 km, so the side must be the exact path's)
+            rec[1] = half || ih == il ? (R)1e30 : (R)P->isa_Hb[ih];
+            for (int fn = 0; fn < 3; ++fn)
+                for (int j = 0; j <= kAtmDeg; ++j) rec[2 + fn * (kAtmDeg + 1) + j] = (R)q[fn][j];
+            for (int m = 0; m <= 32; ++m) {
+                const long double y = a0 + (a1 - a0) * (m == 0 ? 1e-6L : (m == 32 ? 0.999999L : m / 32.0L));
+                const AtmLd v = atm_exact_ld(P, li, y);
+                const R t = (R)y - rec[0];
+                const long double ex[3] = {v.p, v.rho, v.a};
+                for (int fn = 0; fn < 3; ++fn) {
+                    const R f = horner_host<R>(rec + 2 + fn * (kAtmDeg + 1), kAtmDeg, t);
+                    max_rel = std::max(max_rel, (double)(fabsl((long double)f - ex[fn]) / fabsl(ex[fn])));
+                }
+            }
+        }
+        if (ih == il) {   // (no second piece: the split never triggers; mirror the first anyway)
+            R* rec = out.data() + (size_t)k * kAtmStride;
+            std::copy(rec, rec + kAtmRec, rec + kAtmRec);
+        }
+    }
+}
+
+// The stage-2 mass properties x_cog(fill), I(fill) of inertia() (the stage_inertia closure,
+// rocket_dimensions.py:167-196) as piecewise polynomials over fill in [0, 1] (inertia_tab): kInrN
+// cells of degree kInrDeg, checked like the atmosphere's.
+template <typename R>
+void build_inertia_table(const DevParams<R>& D, const pd_params* P, std::vector<R>& out, double& max_rel) {
+    (void)D;
+    out.assign((size_t)kInrN * kInrStride, R(0));
+    max_rel = 0;
+    auto exact = [&](long double f, int which) {
+        const long double h_ox = P->h_ox, h_f = P->h_f, m_ox = P->m_ox, m_f = P->m_f, h_lower = P->h_lower;
+        const long double m_dry = P->m_dry, x_dry = P->x_dry, I_dry = P->I_dry;
+        const long double h_ox_t = h_ox * f, h_f_t = h_f * f, m_ox_t = m_ox * f, m_f_t = m_f * f;
+        const long double x_prop = (m_ox_t * (h_lower + h_ox_t / 2) + m_f_t * (h_lower + h_ox + h_f_t / 2)) / (m_ox_t + m_f_t);
+        const long double t1 = h_lower + h_ox_t / 2 - x_prop, t2 = h_lower + h_ox + h_f_t / 2 - x_prop;
+        const long double I_ox = m_ox_t * h_ox_t * h_ox_t / 12 + m_ox_t * t1 * t1;
+        const long double I_f = m_f_t * h_f_t * h_f_t / 12 + m_f_t * t2 * t2;
+        const long double mp_t = m_ox_t + m_f_t;
+        const long double x_wet = (m_dry * x_dry + mp_t * x_prop) / (m_dry + mp_t);
+        const long double t3 = x_dry - x_wet, t4 = x_prop - x_wet;
+        return which == 0 ? x_wet : (I_dry + m_dry * t3 * t3) + ((I_ox + I_f) + mp_t * t4 * t4);
+    };
+    for (int k = 0; k < kInrN; ++k) {
+        // (x_prop is 0/0 at fill 0: the first cell is fitted on (1e-6 w, w])
+        const long double lo = k == 0 ? 1e-6L / kInrN : (long double)k / kInrN, hi = (long double)(k + 1) / kInrN;
+        R* rec = out.data() + (size_t)k * kInrStride;
+        long double q[2][kInrDeg + 1];
+        for (int fn = 0; fn < 2; ++fn) fit_poly_ld([&](long double f) { return exact(f, fn); }, lo, hi, kInrDeg, q[fn]);
+        rec[0] = (R)(((long double)k + 0.5L) / kInrN);
+        // (the fit is about the interval's own centre; re-expand about the cell centre rec[0])
+        const long double c_fit = (lo + hi) / 2, dc = (long double)rec[0] - c_fit;
+        for (int fn = 0; fn < 2; ++fn) {
+            long double e[kInrDeg + 1] = {};   // q(t + dc) in powers of t (Taylor shift)
+            for (int j = kInrDeg; j >= 0; --j) {
+                for (int m = kInrDeg; m >= 1; --m) e[m] = e[m] * dc + e[m - 1];
+                e[0] = e[0] * dc + q[fn][j];
+            }
+            for (int j = 0; j <= kInrDeg; ++j) rec[1 + fn * (kInrDeg + 1) + j] = (R)e[j];
+        }
+        for (int m = 0; m <= 32; ++m) {
+            const long double f = lo + (hi - lo) * m / 32.0L;
+            const R t = (R)f - rec[0];
+            for (int fn = 0; fn < 2; ++fn) {
+                const R v = horner_host<R>(rec + 1 + fn * (kInrDeg + 1), kInrDeg, t);
+                const long double ex = exact(f, fn);
+                max_rel = std::max(max_rel, (double)(fabsl((long double)v - ex) / fabsl(ex)));
+            }
+        }
+    }
+}
+
 struct TayStats { double max_abs = 0, max_rel = 0; int64_t pieces = 0; };
 
 template <typename R>
@@ -1193,6 +1367,7 @@ struct pd_env {
     int count_work = 0; // workload counters on (pd_count_work)
     int wqx = 1;        // the LPE-2 query exchange's path sort (PDENV_WQX=0 at create: every lane
                         // serves its own query, the same code and bits; bit-identity test, timing)
+    float* sac_heads = nullptr;   // pd_step_sac_fused's two-launch path: the actor heads [N][2A]
 };
 
 namespace {
@@ -1434,6 +1609,30 @@ template <typename R> pd_status create_impl(const pd_params* p, const pd_config*
         if (!tay.empty()) PD_HIP(hipMemcpy(dt, tay.data(), tay.size() * sizeof(R), hipMemcpyHostToDevice));
         D.tay = (const R*)dt;
     }
+    // the atmosphere and the stage-2 mass properties as piecewise polynomials (PDENV_ATM_TAB=0:
+    // the exact formulas on the device)
+    if (const char* at = getenv("PDENV_ATM_TAB"); !(at && at[0] == '0')) {
+        std::vector<R> atm, inr;
+        int n_atm = 0;
+        double err_atm = 0, err_inr = 0;
+        build_atm_table<R>(p, atm, n_atm, err_atm);
+        build_inertia_table<R>(D, p, inr, err_inr);
+        if (getenv("PDENV_TAY_DEBUG"))
+            fprintf(stderr, "pdenv atmosphere table: %d cells, max rel err %.3g; inertia table: max rel err %.3g\n",
+                    n_atm, err_atm, err_inr);
+        const double tol = sizeof(R) == 8 ? 1e-14 : 4e-6;   // (else: the exact formulas; binary32: its y rounds by 8 mm at 80 km)
+        void* da;
+        if (err_atm <= tol) {
+            if ((st = dalloc(e, &da, atm.size() * sizeof(R)))) return st;
+            PD_HIP(hipMemcpy(da, atm.data(), atm.size() * sizeof(R), hipMemcpyHostToDevice));
+            D.atm_tab = (const R*)da; D.atm_n = n_atm; D.atm_inv_w = (R)(1.0 / kAtmW);
+        }
+        if (err_inr <= tol) {
+            if ((st = dalloc(e, &da, inr.size() * sizeof(R)))) return st;
+            PD_HIP(hipMemcpy(da, inr.data(), inr.size() * sizeof(R), hipMemcpyHostToDevice));
+            D.inr_tab = (const R*)da;
+        }
+    }
     // interior candidate grids: C_D abscissa in [-radians(10), radians(10)], C_L in [0, 10]
     std::vector<unsigned long long> gk[2], sk[2];
     std::vector<int> gs[2], ss[2];
@@ -1621,6 +1820,9 @@ struct SacIO {
     long long* ring_state = nullptr;
     float* prio = nullptr;
     const float* max_prio = nullptr;
+    // pd_step_sac_fused: the actor in the kernel prologue (mlp.H = 0: off)
+    SacMlp mlp{};
+    float* heads_out = nullptr;
 };
 
 template <typename R>
@@ -1638,6 +1840,7 @@ pd_status step_impl(pd_env* e, const void* actions, void* obs, void* reward, uin
         a.sac_hs = sac->head_stride;
         a.sac_draw = sac->draw; a.sac_eps_out = sac->eps_out;
         a.ring_cap = sac->ring_cap; a.ring_state = sac->ring_state; a.prio = sac->prio; a.max_prio = sac->max_prio;
+        a.sac_mlp = sac->mlp; a.sac_heads_out = sac->heads_out;
     }
     dispatch_step<R>(e, a, s);
     PD_HIP(hipGetLastError());
@@ -1760,6 +1963,52 @@ pd_status step_n_impl(pd_env* e, const void* actions, int32_t n_steps, void* obs
 extern "C" {
 
 int pd_abi_version(void) { return PD_ABI_VERSION; }
+
+extern "C++" {
+namespace {
+// the device's table evaluation (atmosphere / inertia_fast, pd_physics.h) on the host, in R
+template <typename R>
+void eval_smooth_tables(const pd_params* p, const double* alt, int64_t n_alt, double* atm_out, const double* fill,
+                        int64_t n_fill, double* inr_out, double* max_rel) {
+    std::vector<R> atm, inr;
+    int n_atm = 0;
+    DevParams<R> D;
+    std::memset(&D, 0, sizeof(D));
+    build_atm_table<R>(p, atm, n_atm, max_rel[0]);
+    build_inertia_table<R>(D, p, inr, max_rel[1]);
+    for (int64_t i = 0; i < n_alt; ++i) {
+        R y = (R)alt[i], al = y < R(0) ? R(0) : y, out[3] = {R(0), R(0), R(0)};
+        if (al < (R)p->isa_alt_max) {
+            int k = (int)(al * (R)(1.0 / kAtmW));
+            k = k > n_atm - 1 ? n_atm - 1 : k;
+            const R* rec = atm.data() + (size_t)k * kAtmStride;
+            if (rec[1] < R(1e29) && (R)p->isa_r * al / ((R)p->isa_r + al) >= rec[1]) rec += kAtmRec;
+            const R t = al - rec[0];
+            for (int fn = 0; fn < 3; ++fn) out[fn] = horner_host<R>(rec + 2 + fn * (kAtmDeg + 1), kAtmDeg, t);
+        }
+        atm_out[3 * i] = (double)out[1]; atm_out[3 * i + 1] = (double)out[0]; atm_out[3 * i + 2] = (double)out[2];
+    }
+    for (int64_t i = 0; i < n_fill; ++i) {
+        const R f = (R)fill[i];
+        int k = (int)(f * R(kInrN));
+        k = k > kInrN - 1 ? kInrN - 1 : (k < 0 ? 0 : k);
+        const R* rec = inr.data() + (size_t)k * kInrStride;
+        const R t = f - rec[0];
+        inr_out[2 * i] = (double)horner_host<R>(rec + 1, kInrDeg, t);
+        inr_out[2 * i + 1] = (double)horner_host<R>(rec + 2 + kInrDeg, kInrDeg, t);
+    }
+}
+}  // namespace
+}  // extern "C++"
+
+pd_status pd_smooth_tables(const pd_params* p, int32_t precision, const double* alt, int64_t n_alt, double* atm_out,
+                           const double* fill, int64_t n_fill, double* inr_out, double* max_rel) {
+    if (!p || !max_rel || n_alt < 0 || n_fill < 0 || (n_alt && (!alt || !atm_out)) || (n_fill && (!fill || !inr_out)))
+        return fail(PD_ERR_INVALID, "pd_smooth_tables: bad arguments");
+    if (precision == PD_F32) eval_smooth_tables<float>(p, alt, n_alt, atm_out, fill, n_fill, inr_out, max_rel);
+    else eval_smooth_tables<double>(p, alt, n_alt, atm_out, fill, n_fill, inr_out, max_rel);
+    return PD_OK;
+}
 pd_status pd_cell_piece_info(const pd_params* p, int32_t table, int64_t piece, double* out, int32_t n_out) {
     if (!p || !out || n_out < 16 || (table != 0 && table != 1)) return fail(PD_ERR_INVALID, "pd_cell_piece_info: bad arguments");
     const pd_aero_table& t = table ? p->cl : p->cd;
@@ -1907,6 +2156,69 @@ pd_status pd_step_sac_ring(pd_env* e, const float* heads, int32_t deterministic,
     io.ring_state = ring_state;
     io.prio = ring_state ? priorities : nullptr;
     io.max_prio = max_priority;
+    if (e->rsize == 8)
+        return step_impl<double>(e, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
+                                 (hipStream_t)stream, 1, &io);
+    return step_impl<float>(e, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
+                            (hipStream_t)stream, 1, &io);
+}
+
+pd_status pd_step_sac_fused(pd_env* e, int32_t hidden, int32_t n_hidden_layers, const float* const* params,
+                            float* heads, int32_t deterministic, float log_std_min, float log_std_max, float max_action,
+                            float* eps_out, float* action, float* ring, int64_t capacity, long long* ring_state,
+                            float* priorities, const float* max_priority, float* obs32, void* stream) {
+    if (!e || !params || !obs32) return fail(PD_ERR_INVALID, "pd_step_sac_fused: null env/params/obs32");
+    const int S = e->obs_dim, A = e->act_dim;
+    if (n_hidden_layers < 1 || n_hidden_layers > kSacMaxLayers || A > 8 || S > 16)
+        return fail(PD_ERR_INVALID, "pd_step_sac_fused: 1..8 hidden layers, state_dim <= 16, action_dim <= 8");
+    if (hidden != 128 && hidden != 256 && hidden != 512)
+        return fail(PD_ERR_UNSUPPORTED, "pd_step_sac_fused: hidden width 128, 256 or 512 only");
+    for (int k = 0; k < 2 * (n_hidden_layers + 2); ++k)
+        if (!params[k]) return fail(PD_ERR_INVALID, "pd_step_sac_fused: null parameter");
+    // one launch where the workgroup's envs are one MLP tile (16 lanes per env) and the tile's
+    // activations fit the kernel's LDS (hidden <= 256); else pd_sac_actor into `heads` (or the
+    // handle's scratch rows) and pd_step_sac_ring: two launches, the same heads bit for bit
+    if (e->lpe != 16 || hidden > 256) {
+        const int64_t N = e->cfg.n_envs;
+        float* h = heads;
+        if (!h) {
+            if (!e->sac_heads) {
+                PD_HIP(hipSetDevice(e->device));
+                PD_HIP(hipMalloc((void**)&e->sac_heads, (size_t)N * 2 * A * sizeof(float)));
+                e->allocs.push_back(e->sac_heads);
+            }
+            h = e->sac_heads;
+        }
+        PD_HIP(hipSetDevice(e->device));
+        const pd_status st = pd_sac_actor(N, S, hidden, n_hidden_layers, A, obs32, params, h, stream);
+        if (st != PD_OK) return st;
+        return pd_step_sac_ring(e, h, deterministic, log_std_min, log_std_max, max_action, eps_out, action, ring,
+                                capacity, ring_state, priorities, max_priority, obs32, stream);
+    }
+    if (e->cfg.action_f64) return fail(PD_ERR_UNSUPPORTED, "pd_step_sac_fused: float32 actions only (action_f64 = 0)");
+    if (e->cfg.rtd == PD_RTD_PSO || e->cfg.integrator != PD_INTEG_REFERENCE ||
+        (e->cfg.phase != PD_PHASE_PURE_THROTTLE && e->cfg.phase != PD_PHASE_LANDING_BURN))
+        return fail(PD_ERR_UNSUPPORTED, "pd_step_sac_fused: the RL landing burns (reference integrator) only");
+    const int64_t N = e->cfg.n_envs;
+    const int64_t W = 2 * (int64_t)S + A + 2;
+    if (ring_state) {
+        if (!ring || capacity < N) return fail(PD_ERR_INVALID, "pd_step_sac_fused: ring mode needs ring and capacity >= n_envs");
+        if (capacity * W >= (1ll << 32)) return fail(PD_ERR_INVALID, "pd_step_sac_fused: capacity x row width must be below 2^32");
+        if (priorities && !max_priority) return fail(PD_ERR_INVALID, "pd_step_sac_fused: priorities without max_priority");
+    }
+    PD_HIP(hipSetDevice(e->device));
+    SacIO io{nullptr, nullptr, nullptr, log_std_min, log_std_max, max_action, action, ring, obs32, (uint32_t)(2 * A)};
+    io.draw = deterministic ? 0 : 1;
+    io.eps_out = deterministic ? nullptr : eps_out;
+    io.ring_cap = ring_state ? capacity : 0;
+    io.ring_state = ring_state;
+    io.prio = ring_state ? priorities : nullptr;
+    io.max_prio = max_priority;
+    io.mlp.S = S; io.mlp.L = n_hidden_layers; io.mlp.A = A; io.mlp.H = hidden; io.mlp.obs = obs32;
+    for (int l = 0; l < n_hidden_layers; ++l) { io.mlp.w[l] = params[2 * l]; io.mlp.b[l] = params[2 * l + 1]; }
+    io.mlp.wm = params[2 * n_hidden_layers]; io.mlp.bm = params[2 * n_hidden_layers + 1];
+    io.mlp.ws = params[2 * n_hidden_layers + 2]; io.mlp.bs = params[2 * n_hidden_layers + 3];
+    io.heads_out = heads;
     if (e->rsize == 8)
         return step_impl<double>(e, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
                                  (hipStream_t)stream, 1, &io);

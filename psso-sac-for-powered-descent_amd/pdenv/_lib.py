@@ -87,8 +87,8 @@ EXPORTS = ["pd_abi_version", "pd_sizeof_params", "pd_sizeof_config", "pd_last_er
            "pd_set_wind_state", "pd_get_counters", "pd_set_counters", "pd_checkpoint_size", "pd_checkpoint_save",
            "pd_checkpoint_load", "pd_counters", "pd_stats", "pd_count_work", "pd_atmosphere", "pd_obs_dim",
            "pd_action_dim", "pd_step_sac", "pd_pso_swarm_minima", "pd_pso_update_bests", "pd_cell_piece_info",
-           "pd_step_sac_ring", "pd_sac_actor"]
-ABI_VERSION = 7
+           "pd_step_sac_ring", "pd_sac_actor", "pd_step_sac_fused", "pd_smooth_tables"]
+ABI_VERSION = 8
 
 _lib = None
 
@@ -120,6 +120,7 @@ def load(path=None):
     L.pd_step_sac.argtypes = [vp, vp, vp, I32, vp, F32, F32, F32, vp, vp, vp, vp]
     L.pd_step_sac_ring.argtypes = [vp, vp, I32, F32, F32, F32, vp, vp, vp, I64, vp, vp, vp, vp, vp]
     L.pd_sac_actor.argtypes = [I64, I32, I32, I32, I32, vp, vp, vp, vp]
+    L.pd_step_sac_fused.argtypes = [vp, I32, I32, vp, vp, I32, F32, F32, F32, vp, vp, vp, I64, vp, vp, vp, vp, vp]
     L.pd_rollout.argtypes = [vp, vp, I32, vp, vp]
     L.pd_rollout_policy.argtypes = [vp, vp, I32, I32, vp, vp, I32, vp]
     L.pd_pso_step.argtypes = [I64, I32, vp, vp, vp, vp, vp, vp, vp, vp, vp, C.c_double, C.c_double, C.c_double,
@@ -138,6 +139,7 @@ def load(path=None):
     L.pd_stats.argtypes = [vp, P(I64), I32]
     L.pd_count_work.argtypes = [vp, I32]
     L.pd_cell_piece_info.argtypes = [P(PdParams), I32, I64, P(C.c_double), I32]
+    L.pd_smooth_tables.argtypes = [P(PdParams), I32, vp, I64, vp, vp, I64, vp, vp]
     L.pd_atmosphere.argtypes = [vp, vp, vp, I64, vp]
     L.pd_get_gload_window.argtypes = [vp, vp, vp, vp, vp, vp]
     L.pd_get_wind_state.argtypes = [vp, vp, vp, vp, vp]

@@ -195,6 +195,23 @@ class PoweredDescentEnv:
                                           _ptr(max_priority), _ptr(obs32), _stream(self.device)))
         self._steps += 1
 
+    def step_sac_fused(self, hidden, n_hidden_layers, params, log_std_min=-20.0, log_std_max=2.0, max_action=1.0,
+                       deterministic=False, ring=None, capacity=0, ring_state=None, priorities=None,
+                       max_priority=None, action=None, obs32=None, eps_out=None, heads=None):
+        """The whole SAC collection step in one launch (pd_step_sac_fused): the actor's forward pass
+        in the step kernel's prologue on obs32 [N, S] (the observation the previous step left
+        there), then step_sac_ring's sampling, env step and transition rows, and the next
+        observation back into obs32.  params: a ctypes array of the actor's 2 (n_hidden_layers +
+        2) parameter pointers (pd_sac_actor's order); heads [N, 2A] receives the heads if given.
+        Handles that do not step 16 lanes per env run the actor as its own launch (same bits).
+        No copies, allocations or syncs."""
+        L.check(self.lib.pd_step_sac_fused(self.h, int(hidden), int(n_hidden_layers), params, _ptr(heads),
+                                           int(bool(deterministic)), float(log_std_min), float(log_std_max),
+                                           float(max_action), _ptr(eps_out), _ptr(action), _ptr(ring), int(capacity),
+                                           _ptr(ring_state), _ptr(priorities), _ptr(max_priority), _ptr(obs32),
+                                           _stream(self.device)))
+        self._steps += 1
+
     def observe_raw(self):
         """pd_observe into the preallocated obs buffer (no copy); returns that buffer."""
         L.check(self.lib.pd_observe(self.h, _ptr(self._obs), _stream(self.device)))

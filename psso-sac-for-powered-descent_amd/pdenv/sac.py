@@ -222,10 +222,15 @@ class ActorKernel:
                 and all(m.in_features == H and m.out_features == H for m in lins[1:])
                 and all(p.dtype == torch.float32 and p.is_cuda and p.is_contiguous() for p in ps))
 
-    def __call__(self, obs, heads):
+    def ptrs(self):
+        """The parameter pointers as pd_sac_actor / pd_step_sac_fused take them (read now: an
+        in-place update keeps them, a replaced tensor is picked up here)."""
         for k, t in enumerate(self.params):
             self._ptrs[k] = t.data_ptr()
-        L.check(self.lib.pd_sac_actor(int(obs.shape[0]), self.S, self.H, self.nl, self.A, _ptr(obs), self._ptrs,
+        return self._ptrs
+
+    def __call__(self, obs, heads):
+        L.check(self.lib.pd_sac_actor(int(obs.shape[0]), self.S, self.H, self.nl, self.A, _ptr(obs), self.ptrs(),
                                       _ptr(heads), _stream(obs.device)))
         return heads
 
@@ -235,15 +240,17 @@ class SACCollector:
     -> learner-rank buffer.  `obs` always holds the observation the actor sees next (the
     post-auto-reset observation of envs whose episode ended).
 
-    fused=True (default): TWO launches per step.
-      1. pd_sac_actor: the reference Actor's MLP and both heads in one kernel (ActorKernel; for
-         actor shapes it does not cover, PyTorch's shared_net and one GEMM over both heads).
-      2. pd_step_sac_ring: the action sampled from the heads in the step kernel (eps drawn there,
-         Philox; torch.randn's role), the env step, and the transition rows written by the
-         kernel epilogue straight into the learner's replay ring at the ring's device-held
-         position, with the new rows' priorities set to the buffer's max priority; the next
-         float32 observation into `obs`.  On several ranks the rows go to a local slab instead and
-         `all_gather_into_tensor` (RCCL) appends them on the learner rank.
+    fused=True (default): ONE launch per step where the actor fits the kernel (ActorKernel
+    shapes; pd_step_sac_fused): the reference Actor's MLP and both heads for each workgroup's 16
+    envs in the step kernel's prologue (MFMA hidden layers, activations in LDS), then the action
+    sampled from the heads (eps drawn there, Philox; torch.randn's role), the env step, and the
+    transition rows written by the kernel epilogue straight into the learner's replay ring at the
+    ring's device-held position, with the new rows' priorities set to the buffer's max priority;
+    the next float32 observation into `obs`.  (Handles that do not step 16 lanes per env: the
+    actor as its own launch, pd_sac_actor, the same bits.)  Actor shapes the kernel does not
+    cover: PyTorch's shared_net and one GEMM over both heads, then pd_step_sac_ring.  On several
+    ranks the rows go to a local slab instead and `all_gather_into_tensor` (RCCL) appends them
+    on the learner rank.
     fused=False: Actor.sample, pd_step, transition_slab, pd_observe, buffer.add_batch (the unfused
     reference path, eps from torch.randn with `generator`).
     use_graph=True captures the step into one HIP graph (replaying removes the launch gaps; the
@@ -270,6 +277,7 @@ class SACCollector:
         self.action = torch.empty(env.n, A, dtype=torch.float32, device=dev)
         self.heads = torch.empty(env.n, 2 * A, dtype=torch.float32, device=dev)
         self.eps_out = None           # [N, A] to receive the kernel's eps draws (tests)
+        self.heads_out = None         # [N, 2A] to receive the actor's heads (tests)
         self.kernel = ActorKernel(actor) if fused and ActorKernel.supported(actor) else None
         H = actor.mean.in_features
         self._head_w = torch.empty(2 * A, H, dtype=torch.float32, device=dev)
@@ -292,18 +300,21 @@ class SACCollector:
         """actor -> env step -> transition rows and next obs into self.obs (no syncs); returns
         the local slab, or None when the rows went straight into the replay ring."""
         if self.fused:
-            heads = self._heads()
             a = self.actor
             kw = dict(deterministic=self.deterministic, action=self.action, obs32=self.obs, eps_out=self.eps_out)
             if self.ring:
                 b = self.buffer
-                self.env.step_sac_ring(heads, a.log_std_min, a.log_std_max, a.max_action, ring=b.data,
-                                       capacity=b.capacity, ring_state=b.state_dev,
-                                       priorities=getattr(b, "priorities", None),
-                                       max_priority=getattr(b, "max_prio_dev", None), **kw)
-                return None
-            self.env.step_sac_ring(heads, a.log_std_min, a.log_std_max, a.max_action, ring=self._slab_buf, **kw)
-            return self._slab_buf
+                kw.update(ring=b.data, capacity=b.capacity, ring_state=b.state_dev,
+                          priorities=getattr(b, "priorities", None), max_priority=getattr(b, "max_prio_dev", None))
+            else:
+                kw.update(ring=self._slab_buf)
+            if self.kernel is not None:
+                k = self.kernel
+                self.env.step_sac_fused(k.H, k.nl, k.ptrs(), a.log_std_min, a.log_std_max, a.max_action,
+                                        heads=self.heads_out, **kw)
+            else:
+                self.env.step_sac_ring(self._heads(), a.log_std_min, a.log_std_max, a.max_action, **kw)
+            return None if self.ring else self._slab_buf
         gen = None if self.use_graph else self.generator
         act, _ = self.actor.sample(self.obs, deterministic=self.deterministic, generator=gen, with_log_prob=False)
         act = act.float().contiguous()

@@ -846,6 +846,55 @@ def test_sac_ring_step_draws_rows_priorities(pd):
     assert len(buf) == cap
 
 
+@pytest.mark.parametrize("S,A,H,L,lpe", [(2, 1, 256, 2, 0), (2, 1, 128, 3, 0), (5, 4, 256, 2, 16),
+                                          (2, 1, 256, 2, 2), (2, 1, 512, 2, 0)])
+def test_sac_fused_step_equals_two_launches(pd, S, A, H, L, lpe):
+    """pd_step_sac_fused (the Actor's MLP in the step kernel's prologue: c5's whole collection step
+    in one launch) against pd_sac_actor + pd_step_sac_ring on a twin env: the same heads, eps,
+    actions, replay-ring rows, priorities, ring position and next observations, bit for bit,
+    over 12 steps with auto-resets (ring wrapping: capacity 1.5 N + 3); a batch that is not a
+    multiple of the 16-env tile.  The handles that cannot take the one launch (2 lanes per env,
+    hidden 512) run the two launches inside pd_step_sac_fused: the same bits too."""
+    import torch
+    from pdenv.sac import Actor, ActorKernel, DevicePrioritizedReplayBuffer
+    torch.manual_seed(3)
+    N = 4096 - 9
+    phase = "landing_burn_pure_throttle" if A == 1 else "landing_burn"
+    actor = Actor(S, A, hidden_dim=H, n_hidden_layers=L).cuda()
+    assert ActorKernel.supported(actor)
+    kern = ActorKernel(actor)
+    envs, bufs, outs = [], [], []
+    for fused in (True, False):
+        env = make(pd, N, phase=phase, mode="rl", auto_reset=True, seed=17, tilt_sigma_rad=0.05, lanes_per_env=lpe)
+        cap = N + N // 2 + 3
+        buf = DevicePrioritizedReplayBuffer(cap, S, A, "cuda")
+        buf.max_prio_dev.fill_(1.75)
+        obs = env.reset().float().contiguous()
+        heads = torch.empty(N, 2 * A, device="cuda")
+        act = torch.empty(N, A, device="cuda")
+        eps = torch.empty(N, A, device="cuda")
+        rec = []
+        for t in range(12):
+            kw = dict(ring=buf.data, capacity=cap, ring_state=buf.state_dev, priorities=buf.priorities,
+                      max_priority=buf.max_prio_dev, action=act, obs32=obs, eps_out=eps)
+            if fused:
+                env.step_sac_fused(H, L, kern.ptrs(), actor.log_std_min, actor.log_std_max, actor.max_action,
+                                   heads=heads, **kw)
+            else:
+                kern(obs, heads)
+                env.step_sac_ring(heads, actor.log_std_min, actor.log_std_max, actor.max_action, **kw)
+            buf.note_appended(N)
+            rec.append((heads.clone(), eps.clone(), act.clone(), obs.clone(), buf.state_dev.clone()))
+        torch.cuda.synchronize()
+        envs.append(env); bufs.append(buf); outs.append(rec)
+    for t, (a, b) in enumerate(zip(*outs)):
+        for x, y in zip(a, b):
+            assert torch.equal(x, y), t
+    assert torch.equal(bufs[0].data, bufs[1].data) and torch.equal(bufs[0].priorities, bufs[1].priorities)
+    assert torch.equal(envs[0].state, envs[1].state)
+    assert int(envs[0].episode_counters()[0].max()) >= 1      # auto-resets happened
+
+
 @pytest.mark.parametrize("deterministic", [True, False])
 def test_sac_collector_graph_equals_eager(pd, deterministic):
     """The HIP-graph collection step stores exactly the transitions of the eager step (twin envs,

@@ -73,5 +73,23 @@ case "${PART:-1}" in
       run stamp_d$d 200 python tools/time_fused.py
   done
   run pmc 900 bash tools/pmc_r03b.sh ;;
+8)
+  # c5 in one launch (pd_step_sac_fused): its tests, the c5 line and its rocprofv3 trace
+  run gpu_sac_tests 400 python -u -m pytest tests/ -m gpu -x -q --timeout 200 --timeout-method thread -k "sac"
+  run c5 300 python bench.py --workload c5
+  STAGES="profc5" run profs 300 bash tools/gpu_session.sh ;;
+9)
+  # after the fault of part 8 (the SAC launcher dispatched the non-SAC kernel for pd_step_sac_fused:
+  # a NULL action pointer): the suite, smoke, the tabulated atmosphere / inertia timed against
+  # their exact formulas (PDENV_ATM_TAB=0), c5, c2 and the bench line
+  run gpu_tests 700 python -u -m pytest tests/ -m gpu -x -q --timeout 200 --timeout-method thread
+  run smoke 200 python -c "import __graft_entry__ as g; g.smoke()"
+  for r in 1 2; do for d in 0 1; do
+    FUSE=128 LAUNCHES=6 DESCENT=$d run atm_d${d}_r$r 200 python tools/time_fused.py
+    PDENV_ATM_TAB=0 FUSE=128 LAUNCHES=6 DESCENT=$d run atm0_d${d}_r$r 200 python tools/time_fused.py
+  done; done
+  run c5 300 python bench.py --workload c5
+  run c2 300 python bench.py --workload c2 --cpu-baseline 0
+  run bench 400 python bench.py ;;
 esac
 echo "=== done"
