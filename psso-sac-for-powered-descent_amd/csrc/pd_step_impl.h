@@ -1313,8 +1313,11 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
     };
     const int nf = a.n_fused;   // policy rollouts: finished envs freeze, stored at their last step
     WaveCount wc{CNT ? L.work[threadIdx.x >> 6] : nullptr};   // this wave's workload counts (CNT)
-    // the atmosphere and speed of the state a step ends in, computed by its rtd, are the next
-    // step's first sub-step's (same y, vx, vy; bit-identical): carried unless the env reset
+    // the atmosphere and speed of the state a sub-step ends in are computed right after its
+    // integration (their work -- the table loads -- overlapping atan2's) and carried: to the next
+    // sub-step, to the step's rtd after the last one, and on to the next step's first sub-step
+    // unless the env reset (same y, vx, vy: bit-identical).  RK4: the rtd's only, carried to the
+    // next step's first stage
     R k_rho = R(0), k_patm = R(0), k_asnd = R(0), k_speed = R(0);
     bool k_have = false;
 #pragma unroll 1
@@ -1434,7 +1437,7 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
         if constexpr (WIND) wc.add(kStGust - kStWork, role == 0 && live && a.stochastic && y < P.vk_y_threshold);
         // rocket_physics_fcn (rockets_physics.py:455-704)
         R rho, patm, asnd, speed;
-        if (sub == 0 && k_have) { rho = k_rho; patm = k_patm; asnd = k_asnd; speed = k_speed; }
+        if (RK4 ? (sub == 0 && k_have) : k_have) { rho = k_rho; patm = k_patm; asnd = k_asnd; speed = k_speed; }
         else {
             atmosphere<R>(P, L.isa, y, rho, patm, asnd);
             speed = sqrt(vx * vx + vy * vy);
@@ -1824,6 +1827,9 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
         } else {
         vx += vxd * dt; vy += vyd * dt; x += vx * dt; y += vy * dt;
         thd += thdd * dt; th += thd * dt;
+        atmosphere<R>(P, L.isa, y, k_rho, k_patm, k_asnd);
+        k_speed = sqrt(vx * vx + vy * vy);
+        k_have = true;
         ga = pd_atan2<R>(vy, vx);
         if (th > Cst<R>::two_pi) th -= Cst<R>::two_pi;
         if (ga < R(0)) ga = Cst<R>::two_pi + ga;
@@ -1847,7 +1853,7 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
     // oldest; the new entry is written first, then the window is read back in summation order
     DP<R>& P2 = *params<R>(a.P);
     const R* s = e.s;
-    R v = sqrt(s[2] * s[2] + s[3] * s[3]);
+    const R v = RK4 ? sqrt(s[2] * s[2] + s[3] * s[3]) : k_speed;   // (the same expression's bits)
     R gl_new = PD_DIVC(R, PD_DIVC(R, fabs(v - e.vprev), 0.1) * R(1), 9.81);
     int glen = e.glen, ghead = e.ghead;
     int wslot;
@@ -1871,9 +1877,13 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
     // ---- truncated -> done -> reward (rtd_rl.py:190-336 / rtd_pso.py:172-317)
     R x = s[0], y = s[1], vx = s[2], vy = s[3], th = s[4], ga = s[6], mp = s[9];
     R rho, pa_, as_;
-    atmosphere<R>(P2, L.isa, y, rho, pa_, as_);
+    if constexpr (RK4) {
+        atmosphere<R>(P2, L.isa, y, rho, pa_, as_);
+        k_rho = rho; k_patm = pa_; k_asnd = as_; k_speed = v;
+    } else {
+        rho = k_rho; pa_ = k_patm; as_ = k_asnd;   // (the last sub-step's, of this state)
+    }
     R speed = v;
-    k_rho = rho; k_patm = pa_; k_asnd = as_; k_speed = v;
     R q = R(0.5) * rho * (speed * speed);
     int tr = 0, id = 0, dn = 0;
     R rew = R(0);

@@ -1622,12 +1622,14 @@ template <typename R> pd_status create_impl(const pd_params* p, const pd_config*
                     n_atm, err_atm, err_inr);
         const double tol = sizeof(R) == 8 ? 1e-14 : 4e-6;   // (else: the exact formulas; binary32: its y rounds by 8 mm at 80 km)
         void* da;
-        if (err_atm <= tol) {
+        const char* ae = getenv("PDENV_ATM_ONLY");   // experiments: "inr" / "atm" keeps one table only
+        const bool want_atm = !(ae && ae[0] == 'i'), want_inr = !(ae && ae[0] == 'a');
+        if (want_atm && err_atm <= tol) {
             if ((st = dalloc(e, &da, atm.size() * sizeof(R)))) return st;
             PD_HIP(hipMemcpy(da, atm.data(), atm.size() * sizeof(R), hipMemcpyHostToDevice));
             D.atm_tab = (const R*)da; D.atm_n = n_atm; D.atm_inv_w = (R)(1.0 / kAtmW);
         }
-        if (err_inr <= tol) {
+        if (want_inr && err_inr <= tol) {
             if ((st = dalloc(e, &da, inr.size() * sizeof(R)))) return st;
             PD_HIP(hipMemcpy(da, inr.data(), inr.size() * sizeof(R), hipMemcpyHostToDevice));
             D.inr_tab = (const R*)da;

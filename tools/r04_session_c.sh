@@ -91,5 +91,28 @@ case "${PART:-1}" in
   run c5 300 python bench.py --workload c5
   run c2 300 python bench.py --workload c2 --cpu-baseline 0
   run bench 400 python bench.py ;;
+10)
+  # part 9: the tables made c3 / c3-descent slower (0.0330 / 0.0391 against 0.0315 / 0.0363) and
+  # c2, c4, c5, f32 faster: which table, and the code-size effect (notab: built without them)
+  L=psso-sac-for-powered-descent_amd/pdenv
+  for r in 1 2; do for d in 0 1; do
+    FUSE=128 LAUNCHES=6 DESCENT=$d run tab_both_d${d}_r$r 200 python tools/time_fused.py
+    PDENV_ATM_ONLY=inr FUSE=128 LAUNCHES=6 DESCENT=$d run tab_inr_d${d}_r$r 200 python tools/time_fused.py
+    PDENV_ATM_ONLY=atm FUSE=128 LAUNCHES=6 DESCENT=$d run tab_atm_d${d}_r$r 200 python tools/time_fused.py
+    PDENV_ATM_TAB=0 FUSE=128 LAUNCHES=6 DESCENT=$d run tab_none_d${d}_r$r 200 python tools/time_fused.py
+    PDENV_LIB=$L/libpdenv_notab.so FUSE=128 LAUNCHES=6 DESCENT=$d run tab_notab_d${d}_r$r 200 python tools/time_fused.py
+    # ro: each sub-step's end atmosphere computed before atan2 (its loads overlap atan2's work)
+    PDENV_LIB=$L/libpdenv_ro.so FUSE=128 LAUNCHES=6 DESCENT=$d run tab_ro_d${d}_r$r 200 python tools/time_fused.py
+    PDENV_LIB=$L/libpdenv_ro.so PDENV_ATM_ONLY=inr FUSE=128 LAUNCHES=6 DESCENT=$d run tab_roinr_d${d}_r$r 200 python tools/time_fused.py
+    PDENV_LIB=$L/libpdenv_ronotab.so FUSE=128 LAUNCHES=6 DESCENT=$d run tab_ronotab_d${d}_r$r 200 python tools/time_fused.py
+  done; done
+  for r in 1 2; do
+    N=4096 WIND=0 TILT=0 FUSE=128 LAUNCHES=6 run tab_c2_both_r$r 200 python tools/time_fused.py
+    PDENV_ATM_ONLY=inr N=4096 WIND=0 TILT=0 FUSE=128 LAUNCHES=6 run tab_c2_inr_r$r 200 python tools/time_fused.py
+    PDENV_LIB=$L/libpdenv_c2notab.so N=4096 WIND=0 TILT=0 FUSE=128 LAUNCHES=6 run tab_c2_notab_r$r 200 python tools/time_fused.py
+    PREC=f32 FUSE=128 LAUNCHES=6 run tab_f32_both_r$r 200 python tools/time_fused.py
+    PREC=f32 PDENV_ATM_ONLY=inr FUSE=128 LAUNCHES=6 run tab_f32_inr_r$r 200 python tools/time_fused.py
+    PREC=f32 PDENV_LIB=$L/libpdenv_f32notab.so FUSE=128 LAUNCHES=6 run tab_f32_notab_r$r 200 python tools/time_fused.py
+  done ;;
 esac
 echo "=== done"
