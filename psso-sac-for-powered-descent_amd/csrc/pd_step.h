@@ -165,7 +165,6 @@ template <typename R> struct StepArgs {
     int rtd_none;                    // PD_RTD_NONE: physics stepping only (reward/done/trunc 0)
     int n_fused;                     // env-steps per launch (actions/outputs: [n_fused][N] rows)
     int count_work;                  // workload counters on (pd_count_work; diagnostic launches)
-    int wqx;                         // LPE 2 step kernels: exchange queries by path (0: each lane its own)
     // pd_step_sac (single-step launches): the action sampled from the actor's heads in the kernel,
     // tanh(mean + exp(clamp(log_std, lo, hi)) eps) max (eps NULL: tanh(mean) max), and float32
     // outputs: the action, the transition row [N][2S + A + 2] and the next observation [N][S]

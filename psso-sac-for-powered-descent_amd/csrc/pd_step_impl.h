@@ -413,11 +413,6 @@ struct TayRef { int piece, cell; bool line, verify, refined, bisect; int cp; dou
 
 struct NoPre { __device__ void operator()() const {} };
 
-// PD_WQX=1 (experiments) builds the LPE-2 pure-throttle step kernels with the workgroup query
-// exchange (rbf2_exchange); measured 20-25 % slower than the per-lane path
-#ifndef PD_WQX
-#define PD_WQX 0
-#endif
 
 // pre(): the caller's work that does not depend on the tables, run while the grid loads are in
 // flight
@@ -865,79 +860,6 @@ __device__ __forceinline__ R rbf2(const AT& a, DP<R>& P, int table, const TabVie
     return val;
 }
 
-// ---------------------------------------------------------------- workgroup query exchange
-// The envs of a wave fly in different regimes: a wave sub-step almost always holds queries on
-// the clamped lines (Taylor pieces) AND interior queries (fine index -> cell piece), and runs
-// both paths one after the other.  Binning envs by path at launch boundaries cannot fix that:
-// an env changes path in ~11-15 % of its sub-steps, so after any sort the waves are mixed again
-// within one step (tools/regime_persistence.py, profiles/r04_regime_persistence.json).  Instead
-// the queries move, every sub-step: each lane publishes its query (table, M, abscissa, cache)
-// in the workgroup's LDS at a slot ordered by path -- line queries from slot 0 up, the others
-// from slot 255 down (one LDS atomic per wave and path) -- the workgroup barrier, each lane
-// then serves slot (wave * 64 + lane) through rbf2 and leaves the value and the updated cache
-// there, and after a second barrier each lane reads its own query's.  The four waves then hold
-// at most one mixed wave between them.  Every path of rbf2 gives a query the same bits on any
-// lane (the balanced sums are lane-independent, the pieces per lane), so the results are
-// bit-identical to rbf2 on the own lane (wqx = 0 keeps the identity mapping, same code).
-// The records live in the serving wave's BalLds: the query in `part` (read into registers
-// before rbf2 reuses it), the result in qm / qa / qp (written after rbf2's last use); the
-// two areas alternate between the two barriers, so that no write meets an unread value.
-template <typename R> struct XView {   // one wave's 64 exchange records inside its BalLds
-    R* qM; R* qA; unsigned long long* qK; uint32_t* qW;         // query: M, abscissa, cache key, word
-    R* rV; int* rS; unsigned long long* rK;                     // result: value, cache slot, key
-    __device__ explicit XView(BalLds<R>& B) {
-        char* p = (char*)&B.part[0];
-        qM = (R*)p; qA = (R*)(p + 64 * sizeof(R)); qK = (unsigned long long*)(p + 128 * sizeof(R));
-        qW = (uint32_t*)(p + 128 * sizeof(R) + 512);
-        rV = B.qm; rS = (int*)B.qa; rK = B.qp;
-    }
-};
-static_assert(sizeof(BalLds<double>::part) >= 128 * 8 + 512 + 256, "exchange query records do not fit");
-static_assert(sizeof(BalLds<float>::part) >= 128 * 4 + 512 + 256, "exchange query records do not fit");
-
-template <typename R, typename Pre, typename AT, typename LT>
-__device__ __forceinline__ R rbf2_exchange(const AT& a, DP<R>& P, LT& L, int table, RbfCache<R>& cache, R M, R aq,
-                                           bool act, WaveCount& wc, Pre&& pre, unsigned long long* stamp = nullptr) {
-    const int lane = (int)__lane_id();
-    const int w = (int)threadIdx.x >> 6;
-    int dest = (int)threadIdx.x;
-    if (a.wqx) {
-        const int l0 = 2 * table;   // (TabView::line0)
-        const bool line = aq == L.lines.a[l0] || aq == L.lines.a[l0 + 1];
-        const unsigned long long bl = __ballot(line);
-        const int nl = __popcll(bl);
-        const int rl = __popcll(bl & ((1ull << lane) - 1ull));
-        uint32_t bases = 0u;
-        if (lane == 0) bases = atomicAdd(&L.xq[0], (uint32_t)nl) | (atomicAdd(&L.xq[1], (uint32_t)(64 - nl)) << 16);
-        bases = (uint32_t)__builtin_amdgcn_readfirstlane((int)bases);
-        dest = line ? (int)(bases & 0xffffu) + rl : kStepBlock - 1 - ((int)(bases >> 16) + (lane - rl));
-    }
-    {
-        XView<R> x(L.bal[dest >> 6]);
-        const int s = dest & 63;
-        x.qM[s] = M; x.qA[s] = aq; x.qK[s] = cache.key;
-        x.qW[s] = (uint32_t)(cache.slot + 1) | ((uint32_t)table << 31) | ((uint32_t)act << 30);
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) { L.xq[0] = 0u; L.xq[1] = 0u; }   // (the next sub-step's adds come after the second barrier)
-    XView<R> x(L.bal[w]);
-    const R qm = x.qM[lane], qa = x.qA[lane];
-    const uint32_t qw = x.qW[lane];
-    RbfCache<R> qc;
-    qc.key = x.qK[lane];
-    qc.slot = (int)(qw & 0x3fffffffu) - 1;
-    const int qt = (int)(qw >> 31);
-    const R v = rbf2<R>(a, P, qt, tab_view_lds<R>(L.tdesc, qt), L.lines, qc, qm, qa, ((qw >> 30) & 1u) != 0u,
-                        L.bal[w], L.tab, wc, pre, stamp);
-    x.rV[lane] = v; x.rS[lane] = qc.slot; x.rK[lane] = qc.key;
-    __syncthreads();
-    XView<R> y(L.bal[dest >> 6]);
-    const int s = dest & 63;
-    cache.key = y.rK[s];
-    cache.slot = y.rS[s];
-    return y.rV[s];
-}
-
 // rocket_CD query: CD_func = rocket_CD(M, degrees(alpha)); clamp of the DEGREE value at
 // +-radians(10) (rockets_physics.py:712, aerodynamic_coefficients.py:105-115)
 template <typename R> __device__ __forceinline__ R cd_query(R ae) {
@@ -1053,7 +975,6 @@ template <typename R, bool WIND, int EPB, bool BAL = false> struct StepLds {
     double wnx[WIND ? 2 : 1][WIND ? kStepBlock : 1];   // each lane's gust normals of the next (odd) sub-step
     BalLds<R> bal[BAL ? kStepBlock / 64 : 1];   // LPE 2: balanced-sum space per wave
     TabView<R> tdesc[2];          // each table's view, staged once: a lane's table is per lane
-    uint32_t xq[2];               // LPE 2: the query exchange's line / interior slot counters
 };
 
 // A lane's table view from the workgroup's LDS copy (two entries; lanes of one wave read at most
@@ -1192,7 +1113,6 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
         }
         if (threadIdx.x < (kStepBlock / 64) * kNWork) (&L.work[0][0])[threadIdx.x] = 0u;
         if (threadIdx.x < 2) L.tdesc[threadIdx.x] = tab_view<R>(P, L.tab, (int)threadIdx.x);
-        if (threadIdx.x < 2) L.xq[threadIdx.x] = 0u;
     }
     __syncthreads();
     PD_T(t_staged);
@@ -1523,13 +1443,7 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
                 CD = have ? w : R(0);
             } else {
                 R v;
-                if constexpr (LPE == 2 && POL == 0 && PHASE == 0 && PD_WQX)   // (policy waves may leave early: no barriers)
-                    v = rbf2_exchange<R>(a, P, L, my_table, cA, mach, my_table ? aq_cl : aq_cd, live, wc, wind_block
-#ifdef PD_STAMP
-                                         , acc_ + 7
-#endif
-                                         );
-                else if constexpr (LPE == 2)
+                if constexpr (LPE == 2)
                     v = rbf2<R>(a, P, my_table, tab_view_lds<R>(L.tdesc, my_table), L.lines, cA, mach,
                                 my_table ? aq_cl : aq_cd, live, L.bal[threadIdx.x >> 6], L.tab, wc, wind_block
 #ifdef PD_STAMP

@@ -1365,8 +1365,6 @@ struct pd_env {
     int lpe = 2;   // lanes per env of the step kernel
     int obs_kind = 0;   // obs_write layout of the handle's observation
     int count_work = 0; // workload counters on (pd_count_work)
-    int wqx = 1;        // the LPE-2 query exchange's path sort (PDENV_WQX=0 at create: every lane
-                        // serves its own query, the same code and bits; bit-identity test, timing)
     float* sac_heads = nullptr;   // pd_step_sac_fused's two-launch path: the actor heads [N][2A]
 };
 
@@ -1417,7 +1415,6 @@ template <typename R> StepArgs<R> make_args(pd_env* e) {
     a.rtd_none = e->cfg.rtd == PD_RTD_NONE;
     a.n_fused = 1;
     a.count_work = e->count_work;
-    a.wqx = e->wqx;
     return a;
 }
 
@@ -2073,7 +2070,6 @@ pd_status pd_create(const pd_params* params, const pd_config* cfg, pd_env** out)
     e->lpe = cfg->lanes_per_env != 0 ? cfg->lanes_per_env
                                      : (cfg->n_envs <= 4096 ? 16 : (cfg->n_envs <= 8192 ? 8 : 2));
     if (const char* lv = getenv("PDENV_LPE"); lv && *lv && cfg->lanes_per_env == 0) e->lpe = atoi(lv);   // experiments
-    if (const char* xv = getenv("PDENV_WQX"); xv && xv[0] == '0') e->wqx = 0;
     if (e->lpe != 1 && e->lpe != 2 && e->lpe != 4 && e->lpe != 8 && e->lpe != 16) { delete e; return fail(PD_ERR_INVALID, "lanes_per_env must be 0, 1, 2, 4, 8 or 16"); }
     if (cfg->integrator == PD_INTEG_RK4) e->lpe = e->lpe <= 2 ? 2 : 16;   // the RK4 instantiations
     st = cfg->precision == PD_F64 ? create_impl<double>(params, cfg, e) : create_impl<float>(params, cfg, e);

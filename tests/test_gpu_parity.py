@@ -224,35 +224,6 @@ def test_fine_index_bit_identical(pd):
     assert torch.equal(fine.state, rec.state)
 
 
-@pytest.mark.parametrize("precision", ["f64", "f32"])
-def test_query_exchange_bit_identical(pd, precision):
-    """The workgroup query exchange (csrc/pd_step_impl.h rbf2_exchange: each sub-step's table
-    queries sorted by path over the workgroup's four waves, served by whichever lane gets the
-    slot) gives every query the bits its own lane computes (PDENV_WQX=0: the identity mapping,
-    same code): the c3 workload with a high-throttle majority -- wind, gusts, tilt, auto-reset,
-    both table paths in every wave -- over 2 fused launches of 64 steps and a partial last
-    workgroup (N = 16 384 + 37)."""
-    import torch
-    N, T = 16384 + 37, 128
-    g = torch.Generator(device="cuda").manual_seed(37)
-    A = torch.rand(T, N, 1, device="cuda", generator=g) * 2 - 1
-    A[:, : 3 * N // 4] = A[:, : 3 * N // 4] * 0.25 + 0.75
-    kw = dict(lanes_per_env=2, enable_wind=True, stochastic_wind=True, wind_percentile=None,
-              auto_reset=True, tilt_sigma_rad=0.02, seed=17, precision=precision)
-    xq = make(pd, N, **kw)
-    os.environ["PDENV_WQX"] = "0"
-    try:
-        own = make(pd, N, **kw)
-    finally:
-        del os.environ["PDENV_WQX"]
-    for t0 in range(0, T, 64):
-        o1 = xq.step_n(A[t0:t0 + 64])
-        o2 = own.step_n(A[t0:t0 + 64])
-        for x, y in zip(o1, o2):
-            assert torch.equal(x, y), t0
-    assert torch.equal(xq.state, own.state)
-
-
 def test_fine_index_cell_edge_margins(pd):
     """Queries placed a fraction of the 1e-9 trust margin inside an interior cell's Mach edge
     (2e-10 .. 8e-10 cell widths, both edges, 120 cells): the fine index applies the record
