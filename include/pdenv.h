@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define PD_ABI_VERSION 8   /* 4: pd_config.integrator (was padding); 5: pd_count_work, pd_step_sac; 6: cell pieces (pd_cell_piece_info, stats word 44); 7: pd_step_sac_ring, pd_sac_actor, stats word 45; 8: pd_step_sac_fused, pd_smooth_tables */
+#define PD_ABI_VERSION 8   /* 4: pd_config.integrator (was padding); 5: pd_count_work, pd_step_sac; 6: cell pieces (pd_cell_piece_info, stats word 44); 7: pd_step_sac_ring, pd_sac_actor, stats word 45; 8: pd_step_sac_fused, pd_atm_table */
 #define PD_MAX_PTS 256      /* aero scatter points per table */
 #define PD_MAX_COLS 5       /* AoA columns per aero table */
 #define PD_MAX_TAB 64       /* grid-fin table length */
@@ -394,13 +394,12 @@ pd_status pd_count_work(pd_env* env, int32_t enable);
  * with a valid binary64 / binary32 piece; piece >= 0 (an exact cell's piece is at its
  * cell index im na + ia): its record at out[16 ...] (n_out >= 16 + stride). */
 pd_status pd_cell_piece_info(const pd_params* params, int32_t table, int64_t piece, double* out, int32_t n_out);
-/* The step kernel's tabulated smooth functions, built and evaluated on the host in the device's
- * order and precision (test hook; no device needed): the ISA atmosphere (atmosphere_dynamics.py:
- * 5-27; rho, p, a into atm_out [n_alt][3]) at geometric altitudes alt, and the stage-2 mass
- * properties (rocket_dimensions.py:167-196; x_cog, I into inr_out [n_fill][2]) at fills in (0, 1];
- * max_rel[0..1]: the builders' worst relative error against the long double formulas. */
-pd_status pd_smooth_tables(const pd_params* params, int32_t precision, const double* alt, int64_t n_alt,
-                           double* atm_out, const double* fill, int64_t n_fill, double* inr_out, double* max_rel);
+/* The step kernel's tabulated ISA atmosphere (atmosphere_dynamics.py:5-27), built and evaluated on
+ * the host in the device's order and precision (test hook; no device needed): rho, p, a into
+ * atm_out [n_alt][3] at geometric altitudes alt; max_rel: the builder's worst relative error
+ * against the long double closed form. */
+pd_status pd_atm_table(const pd_params* params, int32_t precision, const double* alt, int64_t n_alt,
+                       double* atm_out, double* max_rel);
 /* Observation / action widths of the handle. */
 int pd_obs_dim(const pd_env* env);
 int pd_action_dim(const pd_env* env);

@@ -57,14 +57,12 @@ constexpr int kLineBuckets = 128;
 constexpr int kTayCells = 2048, kTayDeg = 10, kTayExact = 2;
 constexpr int kTayStride = kTayDeg + 1 + 3 * kTayExact + 1;
 
-// Tabulated smooth functions (pdenv.hip build_atm_table / build_inertia_table): the ISA rho, p, a
-// by geometric altitude in cells of kAtmW m (degree kAtmDeg in t = y - centre; a record is the
-// cell's piece -- centre, the base H of a layer boundary inside the cell or 1e30, coefficients
-// -- and then the upper layer's piece), and the
-// stage-2 mass properties x_cog, I by fill in kInrN cells of [0, 1] (degree kInrDeg)
+// The tabulated atmosphere (pdenv.hip build_atm_table): the ISA rho, p, a by geometric altitude
+// in cells of kAtmW m (degree kAtmDeg in t = y - centre; a record is the cell's piece -- centre,
+// the base H of a layer boundary inside the cell or 1e30, coefficients -- and then the upper
+// layer's piece)
 constexpr int kAtmDeg = 5, kAtmRec = 2 + 3 * (kAtmDeg + 1), kAtmStride = 2 * kAtmRec;
 constexpr double kAtmW = 100.0;
-constexpr int kInrN = 64, kInrDeg = 6, kInrStride = 1 + 2 * (kInrDeg + 1) + 1;
 
 // Address spaces of the step kernel's memory: the per-handle parameter block is read through a
 // constant-address-space view (uniform fields become scalar loads into SGPRs), the tables behind
@@ -163,12 +161,10 @@ template <typename R> struct DevParams {
     R hyper[12][9];                // ascent rtd hyper-parameters by Mach (rtd_rl.py:543-574)
     R terminal_mach;
     R rl_scale, alive_bonus, log_1p_max_ae;   // (1-g)/(1-g^L), 0.01 (1-g), log(1 + radians(20))
-    // tabulated atmosphere and stage-2 mass properties (atmosphere / inertia below; nullptr: the
-    // exact formulas)
+    // the tabulated atmosphere (atmosphere<R, true> below; nullptr: the exact formulas)
     const R* atm_tab;
     R atm_inv_w;
     int atm_n;
-    const R* inr_tab;
 };
 template <typename R> using DP = const PD_AS4 DevParams<R>;
 template <typename T> __device__ __forceinline__ const PD_AS1 T* gbl(const T* p) { return (const PD_AS1 T*)(uint64_t)p; }
@@ -261,17 +257,17 @@ template <> __device__ __forceinline__ double pd_atan2<double>(double y, double 
 
 // ---------------------------------------------------------------- atmosphere
 // atmosphere_dynamics.py:5-27 (ambiance ISA restated)
-// The table (build_atm_table: every piece within 2e-15 of the long double ISA in binary64, 2e-16
-// typical; the exact path's own rounding reaches 5e-15 where pow's exponent is large): one cell record, the upper layer's piece past a layer
-// boundary inside the cell, three Horner chains -- about a fifth of the exact path's instructions
-// (two divisions, exp, log, sqrt, the layer search).  PD_ATM_TAB=0 (experiments): exact path.
-#ifndef PD_ATM_TAB
-#define PD_ATM_TAB 1
-#endif
-template <typename R>
+// TAB: from the table (build_atm_table: every piece within 2e-15 of the long double ISA in
+// binary64, 2e-16 typical; the exact path's own rounding reaches 5e-15 where pow's exponent is
+// large): one cell record, the upper layer's piece past a layer boundary inside the cell, three
+// Horner chains -- about a fifth of the exact path's instructions (two divisions, exp, log, sqrt,
+// the layer search), but an L2 load at the head of the sub-step's chain.  Measured
+// (profiles/r04_exp_s10_tables.jsonl): c2 -2 %, binary32 c3 -5 %, binary64 c3 with wind +1.5 %;
+// the step kernel takes it where it pays (k_step kAtmTab).  No table uploaded: the exact path.
+template <typename R, bool TAB = true>
 __device__ __forceinline__ void atmosphere(DP<R>& P, const R* isa, R y, R& rho, R& p, R& a) {
     R alt = y < R(0) ? R(0) : y;
-    if (PD_ATM_TAB && P.atm_tab != nullptr) {
+    if (TAB && P.atm_tab != nullptr) {
         if (alt < P.isa_alt_max) {
             int k = (int)(alt * P.atm_inv_w);
             k = k > P.atm_n - 1 ? P.atm_n - 1 : k;
@@ -342,30 +338,6 @@ __device__ __forceinline__ void inertia(DP<R>& P, R fill, R& x_cog, R& I) {
     R t3 = P.x_dry - x_wet, t4 = x_prop - x_wet;
     x_cog = x_wet;
     I = (P.I_dry + P.m_dry * (t3 * t3)) + ((I_ox + I_f) + mp_t * (t4 * t4));
-}
-
-// inertia() from its table (build_inertia_table: x_cog and I within ~2e-16 relative of the long
-// double closure in binary64) for fill in (0, 1]; the closure itself elsewhere (fill 0 is its 0/0)
-template <typename R>
-__device__ __forceinline__ void inertia_fast(DP<R>& P, R fill, R& x_cog, R& I) {
-    if (PD_ATM_TAB && P.inr_tab != nullptr && fill > R(0) && fill <= R(1)) {
-        int k = (int)(fill * R(kInrN));
-        k = k > kInrN - 1 ? kInrN - 1 : k;
-        const PD_AS1 R* rec = gbl(P.inr_tab) + (uint32_t)k * (uint32_t)kInrStride;
-        R c[kInrStride - 1];
-#pragma unroll
-        for (int u = 0; u < kInrStride - 1; ++u) c[u] = rec[u];
-        const R t = fill - c[0];
-        R fx = c[1 + kInrDeg], fi = c[2 + 2 * kInrDeg];
-#pragma unroll
-        for (int j = kInrDeg - 1; j >= 0; --j) {
-            fx = fma(fx, t, c[1 + j]);
-            fi = fma(fi, t, c[2 + kInrDeg + j]);
-        }
-        x_cog = fx; I = fi;
-        return;
-    }
-    inertia<R>(P, fill, x_cog, I);
 }
 
 // full_rocket_inertia closure (rocket_dimensions.py:198-241), x_cog_inertia_subrocket_0_lambda of

@@ -1189,6 +1189,9 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
     constexpr int NSUB = RK4 ? 40 : (PHASE == 2 ? 1 : 4);
     // LPE != 2: pieces for the trusted queries (rbf) where they fit the register file without
     // spilling (no wind, no RK4, not the landing-burn SAC kernel): c2, c5, the policy sweep
+    // the tabulated atmosphere where it pays: binary32 handles and the windless kernels (c2, c4,
+    // c5); the binary64 wind kernels (c3) keep the exact path (pd_physics.h atmosphere)
+    constexpr bool kAtmTab = sizeof(R) == 4 || !WIND;
     // (LPE 16 measured 6 % slower with them: its split payload sum is as short as a piece)
     constexpr bool kPcs = !WIND && !RK4 && LPE <= 8 && (PHASE == 0 || (PHASE == 1 && !SAC));
     const R dt = RK4 ? R(0.01) : (PHASE == 0 ? R(0.025) : (PHASE == 1 ? R(0.1) : (R)a.dt_aux));
@@ -1359,7 +1362,7 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
         R rho, patm, asnd, speed;
         if (RK4 ? (sub == 0 && k_have) : k_have) { rho = k_rho; patm = k_patm; asnd = k_asnd; speed = k_speed; }
         else {
-            atmosphere<R>(P, L.isa, y, rho, patm, asnd);
+            atmosphere<R, kAtmTab>(P, L.isa, y, rho, patm, asnd);
             speed = sqrt(vx * vx + vy * vy);
         }
         R mach = R(0);
@@ -1476,7 +1479,7 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
         R x_cog, I;
         // subrocket_0 (full rocket) closures for the ascent, subrocket_2 after (:748-750, :772-774)
         if (ascent) inertia_full<R>(P, R(1) - fpc, x_cog, I);
-        else inertia_fast<R>(P, R(1) - fpc, x_cog, I);
+        else inertia<R>(P, R(1) - fpc, x_cog, I);
         R d_thrust = x_cog + P.engine_height;
         R d_cp_cg = x_cog - (ascent ? P.cop_ascent : P.cop);
         if constexpr (LPE != 2) wind_block();
@@ -1741,7 +1744,7 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
         } else {
         vx += vxd * dt; vy += vyd * dt; x += vx * dt; y += vy * dt;
         thd += thdd * dt; th += thd * dt;
-        atmosphere<R>(P, L.isa, y, k_rho, k_patm, k_asnd);
+        atmosphere<R, kAtmTab>(P, L.isa, y, k_rho, k_patm, k_asnd);
         k_speed = sqrt(vx * vx + vy * vy);
         k_have = true;
         ga = pd_atan2<R>(vy, vx);
@@ -1792,7 +1795,7 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
     R x = s[0], y = s[1], vx = s[2], vy = s[3], th = s[4], ga = s[6], mp = s[9];
     R rho, pa_, as_;
     if constexpr (RK4) {
-        atmosphere<R>(P2, L.isa, y, rho, pa_, as_);
+        atmosphere<R, kAtmTab>(P2, L.isa, y, rho, pa_, as_);
         k_rho = rho; k_patm = pa_; k_asnd = as_; k_speed = v;
     } else {
         rho = k_rho; pa_ = k_patm; as_ = k_asnd;   // (the last sub-step's, of this state)

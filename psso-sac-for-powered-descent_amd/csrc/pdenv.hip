@@ -418,56 +418,6 @@ void build_atm_table(const pd_params* P, std::vector<R>& out, int& n_cells, doub
     }
 }
 
-// The stage-2 mass properties x_cog(fill), I(fill) of inertia() (the stage_inertia closure,
-// rocket_dimensions.py:167-196) as piecewise polynomials over fill in [0, 1] (inertia_tab): kInrN
-// cells of degree kInrDeg, checked like the atmosphere's.
-template <typename R>
-void build_inertia_table(const DevParams<R>& D, const pd_params* P, std::vector<R>& out, double& max_rel) {
-    (void)D;
-    out.assign((size_t)kInrN * kInrStride, R(0));
-    max_rel = 0;
-    auto exact = [&](long double f, int which) {
-        const long double h_ox = P->h_ox, h_f = P->h_f, m_ox = P->m_ox, m_f = P->m_f, h_lower = P->h_lower;
-        const long double m_dry = P->m_dry, x_dry = P->x_dry, I_dry = P->I_dry;
-        const long double h_ox_t = h_ox * f, h_f_t = h_f * f, m_ox_t = m_ox * f, m_f_t = m_f * f;
-        const long double x_prop = (m_ox_t * (h_lower + h_ox_t / 2) + m_f_t * (h_lower + h_ox + h_f_t / 2)) / (m_ox_t + m_f_t);
-        const long double t1 = h_lower + h_ox_t / 2 - x_prop, t2 = h_lower + h_ox + h_f_t / 2 - x_prop;
-        const long double I_ox = m_ox_t * h_ox_t * h_ox_t / 12 + m_ox_t * t1 * t1;
-        const long double I_f = m_f_t * h_f_t * h_f_t / 12 + m_f_t * t2 * t2;
-        const long double mp_t = m_ox_t + m_f_t;
-        const long double x_wet = (m_dry * x_dry + mp_t * x_prop) / (m_dry + mp_t);
-        const long double t3 = x_dry - x_wet, t4 = x_prop - x_wet;
-        return which == 0 ? x_wet : (I_dry + m_dry * t3 * t3) + ((I_ox + I_f) + mp_t * t4 * t4);
-    };
-    for (int k = 0; k < kInrN; ++k) {
-        // (x_prop is 0/0 at fill 0: the first cell is fitted on (1e-6 w, w])
-        const long double lo = k == 0 ? 1e-6L / kInrN : (long double)k / kInrN, hi = (long double)(k + 1) / kInrN;
-        R* rec = out.data() + (size_t)k * kInrStride;
-        long double q[2][kInrDeg + 1];
-        for (int fn = 0; fn < 2; ++fn) fit_poly_ld([&](long double f) { return exact(f, fn); }, lo, hi, kInrDeg, q[fn]);
-        rec[0] = (R)(((long double)k + 0.5L) / kInrN);
-        // (the fit is about the interval's own centre; re-expand about the cell centre rec[0])
-        const long double c_fit = (lo + hi) / 2, dc = (long double)rec[0] - c_fit;
-        for (int fn = 0; fn < 2; ++fn) {
-            long double e[kInrDeg + 1] = {};   // q(t + dc) in powers of t (Taylor shift)
-            for (int j = kInrDeg; j >= 0; --j) {
-                for (int m = kInrDeg; m >= 1; --m) e[m] = e[m] * dc + e[m - 1];
-                e[0] = e[0] * dc + q[fn][j];
-            }
-            for (int j = 0; j <= kInrDeg; ++j) rec[1 + fn * (kInrDeg + 1) + j] = (R)e[j];
-        }
-        for (int m = 0; m <= 32; ++m) {
-            const long double f = lo + (hi - lo) * m / 32.0L;
-            const R t = (R)f - rec[0];
-            for (int fn = 0; fn < 2; ++fn) {
-                const R v = horner_host<R>(rec + 1 + fn * (kInrDeg + 1), kInrDeg, t);
-                const long double ex = exact(f, fn);
-                max_rel = std::max(max_rel, (double)(fabsl((long double)v - ex) / fabsl(ex)));
-            }
-        }
-    }
-}
-
 struct TayStats { double max_abs = 0, max_rel = 0; int64_t pieces = 0; };
 
 template <typename R>
@@ -1606,30 +1556,19 @@ template <typename R> pd_status create_impl(const pd_params* p, const pd_config*
         if (!tay.empty()) PD_HIP(hipMemcpy(dt, tay.data(), tay.size() * sizeof(R), hipMemcpyHostToDevice));
         D.tay = (const R*)dt;
     }
-    // the atmosphere and the stage-2 mass properties as piecewise polynomials (PDENV_ATM_TAB=0:
-    // the exact formulas on the device)
+    // the atmosphere as piecewise polynomials (PDENV_ATM_TAB=0: the exact formulas on the device)
     if (const char* at = getenv("PDENV_ATM_TAB"); !(at && at[0] == '0')) {
-        std::vector<R> atm, inr;
+        std::vector<R> atm;
         int n_atm = 0;
-        double err_atm = 0, err_inr = 0;
+        double err_atm = 0;
         build_atm_table<R>(p, atm, n_atm, err_atm);
-        build_inertia_table<R>(D, p, inr, err_inr);
-        if (getenv("PDENV_TAY_DEBUG"))
-            fprintf(stderr, "pdenv atmosphere table: %d cells, max rel err %.3g; inertia table: max rel err %.3g\n",
-                    n_atm, err_atm, err_inr);
-        const double tol = sizeof(R) == 8 ? 1e-14 : 4e-6;   // (else: the exact formulas; binary32: its y rounds by 8 mm at 80 km)
-        void* da;
-        const char* ae = getenv("PDENV_ATM_ONLY");   // experiments: "inr" / "atm" keeps one table only
-        const bool want_atm = !(ae && ae[0] == 'i'), want_inr = !(ae && ae[0] == 'a');
-        if (want_atm && err_atm <= tol) {
+        if (getenv("PDENV_TAY_DEBUG")) fprintf(stderr, "pdenv atmosphere table: %d cells, max rel err %.3g\n", n_atm, err_atm);
+        // (else: the exact formulas; binary32: its y rounds by 8 mm at 80 km, 1e-6 of p)
+        if (err_atm <= (sizeof(R) == 8 ? 1e-14 : 4e-6)) {
+            void* da;
             if ((st = dalloc(e, &da, atm.size() * sizeof(R)))) return st;
             PD_HIP(hipMemcpy(da, atm.data(), atm.size() * sizeof(R), hipMemcpyHostToDevice));
             D.atm_tab = (const R*)da; D.atm_n = n_atm; D.atm_inv_w = (R)(1.0 / kAtmW);
-        }
-        if (want_inr && err_inr <= tol) {
-            if ((st = dalloc(e, &da, inr.size() * sizeof(R)))) return st;
-            PD_HIP(hipMemcpy(da, inr.data(), inr.size() * sizeof(R), hipMemcpyHostToDevice));
-            D.inr_tab = (const R*)da;
         }
     }
     // interior candidate grids: C_D abscissa in [-radians(10), radians(10)], C_L in [0, 10]
@@ -1880,6 +1819,11 @@ pd_status rollout_policy_impl(pd_env* e, const float* w, int32_t max_steps, void
     (void)hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, e->device);
     const char* force = getenv("PDENV_COMPACT");
     a.use_list = force && *force ? (atoi(force) != 0) : (N * policy_lpe() > (int64_t)dev_cus * 512);
+    // every launch appends its survivors to the next list, so the rollout can switch to the list
+    // at any launch: once the live count read back falls to PDENV_COMPACT_AT x N (experiments;
+    // default off), the waves of the later launches hold live envs only
+    const char* cat = getenv("PDENV_COMPACT_AT");
+    const double compact_at = cat && *cat ? atof(cat) : 0.0;
     int64_t n_launch = N;
     int checks = 0;
     // F policy steps per launch (an episode that ends inside a launch is stored at its last step
@@ -1904,6 +1848,7 @@ pd_status rollout_policy_impl(pd_env* e, const float* w, int32_t max_steps, void
                 PD_HIP(hipEventSynchronize(e->cnt_ev[k ^ 1]));
                 const uint32_t live = ((volatile uint32_t*)e->host_cnt)[k ^ 1];
                 if (live == 0) break;
+                if (!a.use_list && compact_at > 0.0 && (double)live <= compact_at * (double)N) a.use_list = 1;
                 if (a.use_list) n_launch = live;
             }
             ++checks;
@@ -1965,16 +1910,12 @@ int pd_abi_version(void) { return PD_ABI_VERSION; }
 
 extern "C++" {
 namespace {
-// the device's table evaluation (atmosphere / inertia_fast, pd_physics.h) on the host, in R
+// the device's table evaluation (atmosphere<R, true>, pd_physics.h) on the host, in R
 template <typename R>
-void eval_smooth_tables(const pd_params* p, const double* alt, int64_t n_alt, double* atm_out, const double* fill,
-                        int64_t n_fill, double* inr_out, double* max_rel) {
-    std::vector<R> atm, inr;
+void eval_atm_table(const pd_params* p, const double* alt, int64_t n_alt, double* atm_out, double* max_rel) {
+    std::vector<R> atm;
     int n_atm = 0;
-    DevParams<R> D;
-    std::memset(&D, 0, sizeof(D));
-    build_atm_table<R>(p, atm, n_atm, max_rel[0]);
-    build_inertia_table<R>(D, p, inr, max_rel[1]);
+    build_atm_table<R>(p, atm, n_atm, *max_rel);
     for (int64_t i = 0; i < n_alt; ++i) {
         R y = (R)alt[i], al = y < R(0) ? R(0) : y, out[3] = {R(0), R(0), R(0)};
         if (al < (R)p->isa_alt_max) {
@@ -1987,25 +1928,15 @@ void eval_smooth_tables(const pd_params* p, const double* alt, int64_t n_alt, do
         }
         atm_out[3 * i] = (double)out[1]; atm_out[3 * i + 1] = (double)out[0]; atm_out[3 * i + 2] = (double)out[2];
     }
-    for (int64_t i = 0; i < n_fill; ++i) {
-        const R f = (R)fill[i];
-        int k = (int)(f * R(kInrN));
-        k = k > kInrN - 1 ? kInrN - 1 : (k < 0 ? 0 : k);
-        const R* rec = inr.data() + (size_t)k * kInrStride;
-        const R t = f - rec[0];
-        inr_out[2 * i] = (double)horner_host<R>(rec + 1, kInrDeg, t);
-        inr_out[2 * i + 1] = (double)horner_host<R>(rec + 2 + kInrDeg, kInrDeg, t);
-    }
 }
 }  // namespace
 }  // extern "C++"
 
-pd_status pd_smooth_tables(const pd_params* p, int32_t precision, const double* alt, int64_t n_alt, double* atm_out,
-                           const double* fill, int64_t n_fill, double* inr_out, double* max_rel) {
-    if (!p || !max_rel || n_alt < 0 || n_fill < 0 || (n_alt && (!alt || !atm_out)) || (n_fill && (!fill || !inr_out)))
-        return fail(PD_ERR_INVALID, "pd_smooth_tables: bad arguments");
-    if (precision == PD_F32) eval_smooth_tables<float>(p, alt, n_alt, atm_out, fill, n_fill, inr_out, max_rel);
-    else eval_smooth_tables<double>(p, alt, n_alt, atm_out, fill, n_fill, inr_out, max_rel);
+pd_status pd_atm_table(const pd_params* p, int32_t precision, const double* alt, int64_t n_alt, double* atm_out,
+                       double* max_rel) {
+    if (!p || !max_rel || n_alt < 0 || (n_alt && (!alt || !atm_out))) return fail(PD_ERR_INVALID, "pd_atm_table: bad arguments");
+    if (precision == PD_F32) eval_atm_table<float>(p, alt, n_alt, atm_out, max_rel);
+    else eval_atm_table<double>(p, alt, n_alt, atm_out, max_rel);
     return PD_OK;
 }
 pd_status pd_cell_piece_info(const pd_params* p, int32_t table, int64_t piece, double* out, int32_t n_out) {

@@ -87,7 +87,7 @@ EXPORTS = ["pd_abi_version", "pd_sizeof_params", "pd_sizeof_config", "pd_last_er
            "pd_set_wind_state", "pd_get_counters", "pd_set_counters", "pd_checkpoint_size", "pd_checkpoint_save",
            "pd_checkpoint_load", "pd_counters", "pd_stats", "pd_count_work", "pd_atmosphere", "pd_obs_dim",
            "pd_action_dim", "pd_step_sac", "pd_pso_swarm_minima", "pd_pso_update_bests", "pd_cell_piece_info",
-           "pd_step_sac_ring", "pd_sac_actor", "pd_step_sac_fused", "pd_smooth_tables"]
+           "pd_step_sac_ring", "pd_sac_actor", "pd_step_sac_fused", "pd_atm_table"]
 ABI_VERSION = 8
 
 _lib = None
@@ -139,7 +139,7 @@ def load(path=None):
     L.pd_stats.argtypes = [vp, P(I64), I32]
     L.pd_count_work.argtypes = [vp, I32]
     L.pd_cell_piece_info.argtypes = [P(PdParams), I32, I64, P(C.c_double), I32]
-    L.pd_smooth_tables.argtypes = [P(PdParams), I32, vp, I64, vp, vp, I64, vp, vp]
+    L.pd_atm_table.argtypes = [P(PdParams), I32, vp, I64, vp, vp]
     L.pd_atmosphere.argtypes = [vp, vp, vp, I64, vp]
     L.pd_get_gload_window.argtypes = [vp, vp, vp, vp, vp, vp]
     L.pd_get_wind_state.argtypes = [vp, vp, vp, vp, vp]
