@@ -114,5 +114,20 @@ case "${PART:-1}" in
     PREC=f32 PDENV_ATM_ONLY=inr FUSE=128 LAUNCHES=6 run tab_f32_inr_r$r 200 python tools/time_fused.py
     PREC=f32 PDENV_LIB=$L/libpdenv_f32notab.so FUSE=128 LAUNCHES=6 run tab_f32_notab_r$r 200 python tools/time_fused.py
   done ;;
+11)
+  # the build after part 10 (no inertia table; the atmosphere table for binary32 and the windless
+  # kernels only): the suite, smoke, the kernels timed, c4 with the live list switched on mid-rollout
+  # (PDENV_COMPACT_AT) or from the start (PDENV_COMPACT=1), c5, the bench line
+  run gpu_tests 700 python -u -m pytest tests/ -m gpu -x -q --timeout 200 --timeout-method thread
+  run smoke 200 python -c "import __graft_entry__ as g; g.smoke()"
+  for d in 0 1; do FUSE=128 LAUNCHES=6 DESCENT=$d run k_d$d 200 python tools/time_fused.py; done
+  PREC=f32 FUSE=128 LAUNCHES=6 run k_f32 200 python tools/time_fused.py
+  N=4096 WIND=0 TILT=0 FUSE=128 LAUNCHES=6 run k_c2 200 python tools/time_fused.py
+  run c4 300 python bench.py --workload c4 --steps 32 --warmup 4 --cpu-baseline 0
+  PDENV_COMPACT_AT=0.5 run c4_at50 300 python bench.py --workload c4 --steps 32 --warmup 4 --cpu-baseline 0
+  PDENV_COMPACT_AT=0.2 run c4_at20 300 python bench.py --workload c4 --steps 32 --warmup 4 --cpu-baseline 0
+  PDENV_COMPACT=1 run c4_list 300 python bench.py --workload c4 --steps 32 --warmup 4 --cpu-baseline 0
+  run c5 300 python bench.py --workload c5
+  run bench 400 python bench.py ;;
 esac
 echo "=== done"
