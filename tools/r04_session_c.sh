@@ -129,5 +129,18 @@ case "${PART:-1}" in
   PDENV_COMPACT=1 run c4_list 300 python bench.py --workload c4 --steps 32 --warmup 4 --cpu-baseline 0
   run c5 300 python bench.py --workload c5
   run bench 400 python bench.py ;;
+12)
+  # the final build's measurement: the suite, smoke, the bench lines (defaults and the driver's
+  # command), c4 / c5 / c2, rocprofv3 kernel traces (default, driver command, c4, c5) and the PMC
+  # passes (c3, c3-descent); tools/collect_r03.py r04 reduces them into profiles/
+  run gpu_tests 700 python -u -m pytest tests/ -m gpu -x -q --timeout 200 --timeout-method thread
+  run smoke 200 python -c "import __graft_entry__ as g; g.smoke()"
+  run bench 400 python bench.py
+  run benchdrv 300 python bench.py --steps 20 --warmup 5
+  run c4 300 python bench.py --workload c4
+  run c5 300 python bench.py --workload c5
+  run c2 300 python bench.py --workload c2 --cpu-baseline 0
+  STAGES="prof profdrv profc4 profc5" run profs 600 bash tools/gpu_session.sh
+  run pmc 600 bash tools/pmc_r03b.sh ;;
 esac
 echo "=== done"
