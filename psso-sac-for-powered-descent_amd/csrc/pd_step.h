@@ -189,6 +189,9 @@ template <typename R> struct StepArgs {
     // sac_mean / sac_logstd
     SacMlp sac_mlp;
     float* sac_heads_out;
+    // list launches of a policy rollout: the live envs' parameters in list order, [P][N] (the
+    // launch copies them there once, so that its fused steps read them coalesced, not gathered)
+    float* policy_wc;
 };
 
 // Kernel launchers, explicitly instantiated in the kstep_*.hip translation units.

@@ -1234,6 +1234,20 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
         }
     }
     };
+    // policy rollouts stepping the live list: this launch's envs' actor parameters gathered once
+    // into list order (policy_wc), so that every fused step reads them coalesced -- gathered per
+    // step, the 372 scattered reads of each step cost more than the compaction saves
+    const bool wcopy = POL && a.use_list && a.policy_wc != nullptr;
+    if constexpr (POL) {
+        if (wcopy) {
+            constexpr int kP = PHASE == 0 ? PD_ACTOR_PARAMS_PURE_THROTTLE : PD_ACTOR_PARAMS_LANDING_BURN;
+            uint32_t src = ui, dst = (uint32_t)e_act;
+            asm volatile("" : "+v"(src), "+v"(dst));
+#pragma unroll 8
+            for (int q = 0; q < kP; ++q)
+                ev(a.policy_wc + (size_t)q * (size_t)N, dst) = ldv(a.policy_w + (size_t)q * (size_t)N, src);
+        }
+    }
     const int nf = a.n_fused;   // policy rollouts: finished envs freeze, stored at their last step
     WaveCount wc{CNT ? L.work[threadIdx.x >> 6] : nullptr};   // this wave's workload counts (CNT)
     // the atmosphere and speed of the state a sub-step ends in are computed right after its
@@ -1257,15 +1271,16 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
         DP<R>& Q = *params<R>(a.P);
         // the weights are the same every fused step: a laundered offset per step keeps their
         // 372 loads inside the loop (hoisted, they would be held in registers and spill)
-        uint32_t uw = ui;
+        uint32_t uw = wcopy ? (uint32_t)e_act : ui;
         asm volatile("" : "+v"(uw));
+        const float* W = wcopy ? a.policy_wc : a.policy_w;
         if constexpr (PHASE == 0) {
             float x[2] = {(float)(e.s[1] / Q.norm_y), (float)(e.s[3] / Q.norm_vy)};
-            actor_forward<2, 3, 1>(a.policy_w, N, uw, x, uf);
+            actor_forward<2, 3, 1>(W, N, uw, x, uf);
         } else {
             float x[5] = {(float)(e.s[0] / Q.norm_x), (float)(e.s[1] / Q.norm_y), (float)(e.s[2] / Q.norm_vx),
                           (float)(e.s[3] / Q.norm_vy), (float)tanh(Q.k_theta_pso * (e.s[4] - Cst<R>::pi / R(2)))};
-            actor_forward<5, 4, 4>(a.policy_w, N, uw, x, uf);
+            actor_forward<5, 4, 4>(W, N, uw, x, uf);
         }
     } else if constexpr (SAC) {
         // Actor.sample (sac_pytorch.py:161-179) on the caller's two heads, in binary32 as torch

@@ -1316,6 +1316,7 @@ struct pd_env {
     int obs_kind = 0;   // obs_write layout of the handle's observation
     int count_work = 0; // workload counters on (pd_count_work)
     float* sac_heads = nullptr;   // pd_step_sac_fused's two-launch path: the actor heads [N][2A]
+    float* pol_wc = nullptr;      // policy rollouts' list launches: the live envs' actor parameters
 };
 
 namespace {
@@ -1824,6 +1825,12 @@ pd_status rollout_policy_impl(pd_env* e, const float* w, int32_t max_steps, void
     // default off), the waves of the later launches hold live envs only
     const char* cat = getenv("PDENV_COMPACT_AT");
     const double compact_at = cat && *cat ? atof(cat) : 0.0;
+    // the list launches' parameter copy (policy_wc): [P][N] floats, made at the first rollout
+    if (!e->pol_wc) {
+        PD_HIP(hipMalloc((void**)&e->pol_wc, (size_t)PD_ACTOR_PARAMS_LANDING_BURN * (size_t)N * sizeof(float)));
+        e->allocs.push_back(e->pol_wc);
+    }
+    a.policy_wc = getenv("PDENV_NO_WCOPY") ? nullptr : e->pol_wc;   // (experiments: gathered per step)
     int64_t n_launch = N;
     int checks = 0;
     // F policy steps per launch (an episode that ends inside a launch is stored at its last step

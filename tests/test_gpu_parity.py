@@ -892,17 +892,20 @@ def test_sac_collector_graph_equals_eager(pd, deterministic):
 def test_policy_rollout_compaction_invariant(pd, monkeypatch):
     """Done-mask compaction: the live-env list is rebuilt inside every launch and, with the list
     in use (PDENV_COMPACT=1; by default only for grids larger than one chip round), later
-    launches are sized to the live count read back every check_every steps.  Fitness, episode
-    lengths and final states must be bit-identical with and without the list and whatever the
-    check interval (0 = never), and equal to those of envs stepped in their own handle (the
-    order of the list is irrelevant)."""
+    launches are sized to the live count read back every check_every steps, each launch copying
+    its envs' actor parameters into list order once (policy_wc).  Fitness, episode lengths and
+    final states must be bit-identical with and without the list, with the list switched on
+    mid-rollout (PDENV_COMPACT_AT), whatever the check interval (0 = never), and equal to those of
+    envs stepped in their own handle (the order of the list is irrelevant)."""
     import torch
     rng = np.random.default_rng(77)
     W = np.concatenate([rng.uniform(-1.5, 1.5, (700, 372)), rng.uniform(-0.3, 0.3, (324, 372))]).astype(np.float32)
     env = make(pd, len(W), phase="landing_burn", mode="pso")
     res = []
-    for force, ce in (("0", 8), ("1", 0), ("1", 1), ("1", 3), ("1", 8), ("1", 64), ("", 8)):
+    for force, ce, at in (("0", 8, ""), ("1", 0, ""), ("1", 1, ""), ("1", 3, ""), ("1", 8, ""), ("1", 64, ""),
+                          ("", 8, ""), ("0", 8, "0.5"), ("0", 8, "0.05")):
         monkeypatch.setenv("PDENV_COMPACT", force)
+        monkeypatch.setenv("PDENV_COMPACT_AT", at)     # (switched on mid-rollout at that live fraction)
         fit, steps = env.rollout_policy(torch.tensor(W), max_steps=300, check_every=ce)
         res.append((fit.cpu().numpy(), steps.cpu().numpy(), env.state.cpu().numpy()))
     for f, s, S in res[1:]:

@@ -142,5 +142,18 @@ case "${PART:-1}" in
   run c2 300 python bench.py --workload c2 --cpu-baseline 0
   STAGES="prof profdrv profc4 profc5" run profs 600 bash tools/gpu_session.sh
   run pmc 600 bash tools/pmc_r03b.sh ;;
+13)
+  # c4's list launches with the live envs' actor parameters copied once per launch (libpdenv_pwc:
+  # build_variant('pwc', [], unit=(0, 1, 0), host=True)): the compaction invariance test on it, then
+  # c4 with the list off / switched on at 50 % and 25 % live / on from the start
+  L=psso-sac-for-powered-descent_amd/pdenv/libpdenv_pwc.so
+  PDENV_LIB=$L run pwc_tests 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 200 --timeout-method thread \
+      -k "compaction_invariant or policy_rollout or pso_driver"
+  for r in 1 2; do
+    PDENV_LIB=$L run pwc_c4_off_r$r 300 python bench.py --workload c4 --steps 32 --warmup 4 --cpu-baseline 0
+    PDENV_LIB=$L PDENV_COMPACT_AT=0.5 run pwc_c4_at50_r$r 300 python bench.py --workload c4 --steps 32 --warmup 4 --cpu-baseline 0
+    PDENV_LIB=$L PDENV_COMPACT_AT=0.25 run pwc_c4_at25_r$r 300 python bench.py --workload c4 --steps 32 --warmup 4 --cpu-baseline 0
+    PDENV_LIB=$L PDENV_COMPACT=1 run pwc_c4_list_r$r 300 python bench.py --workload c4 --steps 32 --warmup 4 --cpu-baseline 0
+  done ;;
 esac
 echo "=== done"
