@@ -138,6 +138,9 @@ case "${PART:-1}" in
   run bench 400 python bench.py
   run benchdrv 300 python bench.py --steps 20 --warmup 5
   run c4 300 python bench.py --workload c4
+  # (the list launches with the parameter copy, switched on at 50 / 25 % live: PDENV_COMPACT_AT)
+  PDENV_COMPACT_AT=0.5 run c4_at50 300 python bench.py --workload c4 --cpu-baseline 0
+  PDENV_COMPACT_AT=0.25 run c4_at25 300 python bench.py --workload c4 --cpu-baseline 0
   run c5 300 python bench.py --workload c5
   run c2 300 python bench.py --workload c2 --cpu-baseline 0
   STAGES="prof profdrv profc4 profc5" run profs 600 bash tools/gpu_session.sh
