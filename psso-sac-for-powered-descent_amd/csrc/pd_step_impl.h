@@ -895,57 +895,115 @@ template <typename R> __device__ __forceinline__ R cl_query(R ae, R& sgn, bool& 
 // and held: with constant 64-bit addresses the compiler kept ~370 SGPR pairs live and spilled
 // them.  Each output is still its own sequential sum plus the bias (the loads of a layer's
 // weights come first, then its biases).
-template <int IN, int NL, int OUT>
+// SPLIT (LPE >= 2): the env's lane pair shares each layer -- lane half = 0 computes hidden units
+// 0-3 and half = 1 units 4-7 (each unit the same sequential sum from the same loads), then one DPP
+// swap per unit gives both lanes all eight; the output layer splits the same way when OUT is even.
+// Half the loads and arithmetic per lane, the same bits (which lane sums a unit does not enter).
+#ifndef PD_ACTOR_SPLIT
+#define PD_ACTOR_SPLIT 1   // (experiments: 0 = every lane the whole actor)
+#endif
+template <int IN, int NL, int OUT, bool SPLIT = false>
 __device__ __forceinline__ void actor_forward(const float* __restrict__ W, int64_t N, uint32_t ui,
-                                              const float* x, float* y) {
+                                              int half, const float* x, float* y) {
     constexpr int H = 8;
+    constexpr int HS = SPLIT ? H / 2 : H;                          // hidden units per lane
+    constexpr bool OSPLIT = SPLIT && OUT % 2 == 0;
+    constexpr int OS = OSPLIT ? OUT / 2 : OUT;                     // outputs per lane
     float h[H], g[H];
     uint32_t sv = (uint32_t)N * 4u;
-    uint32_t off = ui * 4u;
-    asm volatile("" : "+v"(sv), "+v"(off));
+    uint32_t o0 = ui * 4u;
+    uint32_t hv = SPLIT ? (uint32_t)half : 0u;
+    asm volatile("" : "+v"(sv), "+v"(o0), "+v"(hv));
+    uint32_t off = o0;
+    // the lane's running offset set to parameter p (+ its half's rows: `rows` parameters each)
+    auto seek = [&](int p, int rows) {
+        off = o0 + (uint32_t)p * sv;
+        if constexpr (SPLIT) off += hv * ((uint32_t)rows * sv);
+        asm volatile("" : "+v"(off));
+    };
     auto next = [&]() {
         const float v = *(const PD_AS1 float*)((const PD_AS1 char*)(uint64_t)W + off);
         off += sv;
         asm volatile("" : "+v"(off));
         return v;
     };
+    // both halves of a split layer on both lanes: own[j] is unit hs * HS + j of this lane's half
+    auto gather = [&](const float* own, float* full, int n) {
 #pragma unroll
-    for (int j = 0; j < H; ++j) {
+        for (int j = 0; j < (SPLIT ? H / 2 : H); ++j) {
+            if (j >= n) break;
+            if constexpr (SPLIT) {
+                const float oth = pair_swap(own[j]);
+                full[j] = hv ? oth : own[j];
+                full[n + j] = hv ? own[j] : oth;
+            } else {
+                full[j] = own[j];
+            }
+        }
+    };
+    int p = 0;
+    float hs[HS];
+    // layer 1: Linear(IN, 8)
+    seek(p, HS * IN);
+#pragma unroll
+    for (int j = 0; j < HS; ++j) {
         float acc = 0.f;
 #pragma unroll
         for (int k = 0; k < IN; ++k) acc = acc + next() * x[k];
         g[j] = acc;
     }
+    seek(p + H * IN, HS);
 #pragma unroll
-    for (int j = 0; j < H; ++j) {
+    for (int j = 0; j < HS; ++j) {
         const float acc = g[j] + next();
-        h[j] = acc < 0.f ? 0.f : acc;
+        hs[j] = acc < 0.f ? 0.f : acc;
+    }
+    p += H * IN + H;
+    if constexpr (SPLIT) gather(hs, h, HS);
+    else {
+#pragma unroll
+        for (int j = 0; j < H; ++j) h[j] = hs[j];
     }
 #pragma unroll
     for (int l = 0; l < NL; ++l) {
+        seek(p, HS * H);
 #pragma unroll
-        for (int j = 0; j < H; ++j) {
+        for (int j = 0; j < HS; ++j) {
             float acc = 0.f;
 #pragma unroll
             for (int k = 0; k < H; ++k) acc = acc + next() * h[k];
             g[j] = acc;
         }
+        seek(p + H * H, HS);
 #pragma unroll
-        for (int j = 0; j < H; ++j) {
+        for (int j = 0; j < HS; ++j) {
             const float acc = g[j] + next();
-            h[j] = acc < 0.f ? 0.f : acc;
+            hs[j] = acc < 0.f ? 0.f : acc;
+        }
+        p += H * H + H;
+        if constexpr (SPLIT) gather(hs, h, HS);
+        else {
+#pragma unroll
+            for (int j = 0; j < H; ++j) h[j] = hs[j];
         }
     }
-    float o[OUT];
+    float o[OS], ys[OS];
+    seek(p, OSPLIT ? OS * H : 0);
 #pragma unroll
-    for (int j = 0; j < OUT; ++j) {
+    for (int j = 0; j < OS; ++j) {
         float acc = 0.f;
 #pragma unroll
         for (int k = 0; k < H; ++k) acc = acc + next() * h[k];
         o[j] = acc;
     }
+    seek(p + OUT * H, OSPLIT ? OS : 0);
 #pragma unroll
-    for (int j = 0; j < OUT; ++j) y[j] = (float)tanh((double)(o[j] + next()));
+    for (int j = 0; j < OS; ++j) ys[j] = (float)tanh((double)(o[j] + next()));
+    if constexpr (OSPLIT) gather(ys, y, OS);
+    else {
+#pragma unroll
+        for (int j = 0; j < OUT; ++j) y[j] = ys[j];
+    }
 }
 
 // PD_STAMP (diagnostic builds only): per-wave shader-clock sections of k_step, summed into
@@ -1276,11 +1334,11 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
         const float* W = wcopy ? a.policy_wc : a.policy_w;
         if constexpr (PHASE == 0) {
             float x[2] = {(float)(e.s[1] / Q.norm_y), (float)(e.s[3] / Q.norm_vy)};
-            actor_forward<2, 3, 1>(W, N, uw, x, uf);
+            actor_forward<2, 3, 1, (PD_ACTOR_SPLIT && LPE >= 2)>(W, N, uw, role & 1, x, uf);
         } else {
             float x[5] = {(float)(e.s[0] / Q.norm_x), (float)(e.s[1] / Q.norm_y), (float)(e.s[2] / Q.norm_vx),
                           (float)(e.s[3] / Q.norm_vy), (float)tanh(Q.k_theta_pso * (e.s[4] - Cst<R>::pi / R(2)))};
-            actor_forward<5, 4, 4>(W, N, uw, x, uf);
+            actor_forward<5, 4, 4, (PD_ACTOR_SPLIT && LPE >= 2)>(W, N, uw, role & 1, x, uf);
         }
     } else if constexpr (SAC) {
         // Actor.sample (sac_pytorch.py:161-179) on the caller's two heads, in binary32 as torch

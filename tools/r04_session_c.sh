@@ -158,5 +158,19 @@ case "${PART:-1}" in
     PDENV_LIB=$L PDENV_COMPACT_AT=0.25 run pwc_c4_at25_r$r 300 python bench.py --workload c4 --steps 32 --warmup 4 --cpu-baseline 0
     PDENV_LIB=$L PDENV_COMPACT=1 run pwc_c4_list_r$r 300 python bench.py --workload c4 --steps 32 --warmup 4 --cpu-baseline 0
   done ;;
+14)
+  # the actor split over the env's lane pair (PD_ACTOR_SPLIT; libpdenv_nosplit: build_variant(
+  # 'nosplit', ['-DPD_ACTOR_SPLIT=0'], unit=(0, 1, 0)) has the landing-burn kernels without it):
+  # the policy tests, c4 with and without it (two rounds), the policy lanes-per-env sweep, a c4
+  # kernel trace (both libraries were built with the four-parameters-per-thread k_pso_step, reverted after)
+  L=psso-sac-for-powered-descent_amd/pdenv/libpdenv_nosplit.so
+  run split_tests 500 python -u -m pytest tests/ -m gpu -x -q --timeout 200 --timeout-method thread \
+      -k "policy or pso or compaction or actor or drivers"
+  for r in 1 2; do
+    run split_c4_r$r 300 python bench.py --workload c4 --steps 32 --warmup 4 --cpu-baseline 0
+    PDENV_LIB=$L run nosplit_c4_r$r 300 python bench.py --workload c4 --steps 32 --warmup 4 --cpu-baseline 0
+  done
+  run plpe 300 python tools/policy_lpe_sweep.py
+  STAGES="profc4" run profs 300 bash tools/gpu_session.sh ;;
 esac
 echo "=== done"
