@@ -899,6 +899,9 @@ template <typename R> __device__ __forceinline__ R cl_query(R ae, R& sgn, bool& 
 // 0-3 and half = 1 units 4-7 (each unit the same sequential sum from the same loads), then one DPP
 // swap per unit gives both lanes all eight; the output layer splits the same way when OUT is even.
 // Half the loads and arithmetic per lane, the same bits (which lane sums a unit does not enter).
+#ifndef PD_POL_EXIT
+#define PD_POL_EXIT 1   // (experiments: 0 = frozen waves run the launch's remaining steps)
+#endif
 #ifndef PD_ACTOR_SPLIT
 #define PD_ACTOR_SPLIT 1   // (experiments: 0 = every lane the whole actor)
 #endif
@@ -2078,6 +2081,10 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
         // an episode that ended is stored now and its lanes freeze (they go on computing in step
         // with the wave, convergent for the cooperative miss solve, but write nothing)
         if (live && (dn || tr)) { store_all(); live = false; }
+        // a wave whose episodes have all ended leaves the launch's remaining steps (no barrier
+        // follows; its lanes write nothing more): the launch then ends with its last live wave,
+        // not F steps after the swarm's last episode
+        if (PD_POL_EXIT && __ballot(live) == 0ull) break;
     }
     }   // fused steps
     if constexpr (POL) {

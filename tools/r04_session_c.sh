@@ -172,5 +172,37 @@ case "${PART:-1}" in
   done
   run plpe 300 python tools/policy_lpe_sweep.py
   STAGES="profc4" run profs 300 bash tools/gpu_session.sh ;;
+15)
+  # policy waves leave the launch once their episodes have all ended (PD_POL_EXIT; libpdenv_noexit:
+  # build_variant('noexit', ['-DPD_POL_EXIT=0'], unit=(0, 1, 0))): the policy tests, then c4 with and
+  # without it at 8 and 16 policy steps per launch (PDENV_PFUSE), two rounds
+  L=psso-sac-for-powered-descent_amd/pdenv/libpdenv_noexit.so
+  run exit_tests 500 python -u -m pytest tests/ -m gpu -x -q --timeout 200 --timeout-method thread \
+      -k "policy or pso or compaction or actor or drivers"
+  for r in 1 2; do
+    run exit_c4_f8_r$r 300 python bench.py --workload c4 --steps 32 --warmup 4 --cpu-baseline 0
+    PDENV_LIB=$L run noexit_c4_f8_r$r 300 python bench.py --workload c4 --steps 32 --warmup 4 --cpu-baseline 0
+    PDENV_PFUSE=16 run exit_c4_f16_r$r 300 python bench.py --workload c4 --steps 32 --warmup 4 --cpu-baseline 0
+    PDENV_PFUSE=16 PDENV_LIB=$L run noexit_c4_f16_r$r 300 python bench.py --workload c4 --steps 32 --warmup 4 --cpu-baseline 0
+  done ;;
+16)
+  # part 15 and the final measurement (part 12) in one call: the suite and smoke; c4 with and
+  # without the policy waves' exit at 8 / 16 policy steps per launch; the bench lines, c4 / c5 / c2,
+  # rocprofv3 kernel traces and the PMC passes of this build
+  L=psso-sac-for-powered-descent_amd/pdenv/libpdenv_noexit.so
+  run gpu_tests 600 python -u -m pytest tests/ -m gpu -x -q --timeout 200 --timeout-method thread
+  run smoke 200 python -c "import __graft_entry__ as g; g.smoke()"
+  for r in 1 2; do
+    run exit_c4_f8_r$r 200 python bench.py --workload c4 --steps 32 --warmup 4 --cpu-baseline 0
+    PDENV_LIB=$L run noexit_c4_f8_r$r 200 python bench.py --workload c4 --steps 32 --warmup 4 --cpu-baseline 0
+    PDENV_PFUSE=16 run exit_c4_f16_r$r 200 python bench.py --workload c4 --steps 32 --warmup 4 --cpu-baseline 0
+  done
+  run bench 300 python bench.py
+  run benchdrv 200 python bench.py --steps 20 --warmup 5
+  run c4 200 python bench.py --workload c4
+  run c5 200 python bench.py --workload c5
+  run c2 200 python bench.py --workload c2 --cpu-baseline 0
+  STAGES="prof profdrv profc4 profc5" run profs 500 bash tools/gpu_session.sh
+  run pmc 500 bash tools/pmc_r03b.sh ;;
 esac
 echo "=== done"
