@@ -204,5 +204,15 @@ case "${PART:-1}" in
   run c2 200 python bench.py --workload c2 --cpu-baseline 0
   STAGES="prof profdrv profc4 profc5" run profs 500 bash tools/gpu_session.sh
   run pmc 500 bash tools/pmc_r03b.sh ;;
+17)
+  # the default of 16 policy steps per launch (part 16: 8 -> 16 with the waves' exit, -5 %): the
+  # policy tests on it, c4 at 16 / 32 / 64 steps per launch (two rounds), the c4 line and its trace
+  run pf_tests 500 python -u -m pytest tests/ -m gpu -x -q --timeout 200 --timeout-method thread \
+      -k "policy or pso or compaction or actor or drivers"
+  for r in 1 2; do for f in 16 32 64; do
+    PDENV_PFUSE=$f run pf${f}_c4_r$r 200 python bench.py --workload c4 --steps 32 --warmup 4 --cpu-baseline 0
+  done; done
+  run c4 200 python bench.py --workload c4
+  STAGES="profc4" run profs 300 bash tools/gpu_session.sh ;;
 esac
 echo "=== done"
