@@ -1870,10 +1870,11 @@ pd_status rollout_policy_impl(pd_env* e, const float* w, int32_t max_steps, void
 // Policy steps per fused policy-rollout launch (PDENV_PFUSE overrides; a power of two <= 64).
 // A wave whose episodes have all ended leaves its launch (PD_POL_EXIT), so a longer launch costs
 // no frozen steps at the swarm's tail; it saves launches, their table staging and the count
-// checks between them (c4: 8 -> 1.66, 16 -> 1.57 ms per generation, profiles/r04_exp_s16_pol_exit.jsonl)
+// checks between them (c4: 8 -> 1.66, 16 -> 1.57, 32 -> 1.53-1.57, 64 -> 1.49-1.50 ms per generation,
+// profiles/r04_exp_s16_pol_exit.jsonl, r04_exp_s17_pfuse.jsonl)
 int policy_fuse() {
     const char* s = getenv("PDENV_PFUSE");
-    int k = s && *s ? atoi(s) : 16;
+    int k = s && *s ? atoi(s) : 64;
     int f = 1;
     while (f * 2 <= k && f < 64) f *= 2;
     return f;

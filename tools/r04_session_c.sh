@@ -214,5 +214,15 @@ case "${PART:-1}" in
   done; done
   run c4 200 python bench.py --workload c4
   STAGES="profc4" run profs 300 bash tools/gpu_session.sh ;;
+18)
+  # the final build (64 policy steps per launch, part 17): the suite and smoke, c4 (two rounds and
+  # the line), its trace, the bench lines
+  run gpu_tests 600 python -u -m pytest tests/ -m gpu -x -q --timeout 200 --timeout-method thread
+  run smoke 200 python -c "import __graft_entry__ as g; g.smoke()"
+  for r in 1 2; do run pf64_c4_r$r 200 python bench.py --workload c4 --steps 32 --warmup 4 --cpu-baseline 0; done
+  run c4 200 python bench.py --workload c4
+  run bench 300 python bench.py
+  run benchdrv 200 python bench.py --steps 20 --warmup 5
+  STAGES="profc4 prof profdrv" run profs 400 bash tools/gpu_session.sh ;;
 esac
 echo "=== done"
