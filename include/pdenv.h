@@ -280,11 +280,13 @@ pd_status pd_rollout(pd_env* env, const void* actions, int32_t n_steps, void* re
  *  weights : [n_params][N] float32, parameter-major (named_parameters() order per particle)
  *  n_params: PD_ACTOR_PARAMS_* for the handle's phase; the handle must have rtd = PD_RTD_PSO
  *  fitness : [N] (handle precision); steps: [N] int32 episode lengths (may be NULL)
- *  check_every: >0 = read the live-env count every that many steps, stop early when all envs
- *            are done, and size later launches to the live count (one host sync per check);
- *            0 = always max_steps launches over the full grid.
- * Each launch steps only the live envs: a compacted index list, rebuilt inside the step kernel
- * (wave ballot + prefix count, one atomic per wave), so finished particles cost nothing. */
+ *  check_every: >0 = read the live-env count every that many steps (at least once per launch),
+ *            stop early when all envs are done, and size later launches to the live count (one
+ *            host sync per check); 0 = always max_steps steps over the full grid.
+ * Each launch runs up to 64 fused steps (PDENV_PFUSE); a finished episode's lanes freeze and a
+ * wave whose episodes have all ended leaves the launch.  Grids beyond one chip round of lanes
+ * step only the live envs: a compacted index list, rebuilt inside the step kernel (wave ballot
+ * + prefix count, one atomic per wave).  Results do not depend on either. */
 pd_status pd_rollout_policy(pd_env* env, const float* weights, int32_t n_params, int32_t max_steps,
                             void* fitness, int32_t* steps, int32_t check_every, void* stream);
 /* One PSO generation's particle update on the device (particle_swarm_optimisation.py:437-441
