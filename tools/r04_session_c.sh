@@ -224,5 +224,10 @@ case "${PART:-1}" in
   run bench 300 python bench.py
   run benchdrv 200 python bench.py --steps 20 --warmup 5
   STAGES="profc4 prof profdrv" run profs 400 bash tools/gpu_session.sh ;;
+19)
+  # the committed tree as the round-end driver runs it: the GPU suite, smoke, the default bench line
+  run gpu_tests 600 python -u -m pytest tests/ -m gpu -x -q --timeout 200 --timeout-method thread
+  run smoke 200 python -c "import __graft_entry__ as g; g.smoke()"
+  run bench 300 python bench.py ;;
 esac
 echo "=== done"
