@@ -156,8 +156,29 @@ def bench_sac(args, world, rank, local, dist):
     for _ in range(args.warmup):
         col.step()
     wall = timed_region(lambda k: col.step(), args.steps, torch.cuda.synchronize, dist, env.device)
+    # the dominant kernel's device time: the same step replayed with a HIP event pair per step on
+    # the stream the graph (one k_step<SAC> launch) runs on; the miss flush every 16th step is
+    # outside the graph and outside the pairs
+    kern = []
+    for _ in range(min(args.steps, 64)):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        col.step()
+        e1.record()
+        kern.append((e0, e1))
+    torch.cuda.synchronize()
+    kern_ms = sorted(a.elapsed_time(b) for a, b in kern)
+    kern_avg = sum(kern_ms) / len(kern_ms)
     if rank != 0:
         return None
+    # per env-step: the env's algorithmic bytes (f64 pure throttle, no wind: SURVEY 8(d)), the
+    # transition row (2 S + A + 2 floats) and the next float32 observation, plus the actor's
+    # parameters once per launch shared by the n envs; FLOPs: the actor's three GEMMs (2 per MAC)
+    S, A, H = env.obs_dim, env.action_dim, actor.mean.in_features
+    n_par = sum(p.numel() for p in actor.parameters())
+    bpe = algorithmic_bytes(args.precision, "landing_burn_pure_throttle", False) + 4 * (2 * S + A + 2) + 4 * S \
+        + 4.0 * n_par / n
+    fpe = 2.0 * (S * H + H * H + 2 * H * A)
     out = {
         "metric": "SAC collection env-steps/sec (c5: actor + env + RCCL gather + prioritized replay buffer)",
         "value": whole_job_rate(n, world, args.steps, wall), "unit": "env-steps/s",
@@ -168,7 +189,31 @@ def bench_sac(args, world, rank, local, dist):
         "config": {"workload": "c5: SAC collection, landing_burn_pure_throttle, rtd_rl, auto-reset",
                    "envs_per_gpu": n, "global_envs": n * world, "parallelism": f"env-shard x{world} + all_gather"},
         "replay_buffer_size": len(buf), "hip_graph": args.graph == 1,
+        "roofline": {"bound": "hbm", "achieved": bpe * n / (kern_avg * 1e-3) / 1e9, "peak": 8000.0, "unit": "GB/s",
+                     "frac": bpe * n / (kern_avg * 1e-3) / 1e9 / 8000.0, "traffic": None,
+                     "bytes_per_env_step": round(bpe, 1), "kernel": "k_step<SAC> (pd_step_sac_fused: actor MLP + step)",
+                     "kernel_avg_ms": kern_avg, "kernel_med_ms": kern_ms[len(kern_ms) // 2], "kernel_launches": len(kern_ms),
+                     "kernel_timing": "HIP events around each replayed collection step (its graph: one k_step launch)",
+                     "bytes_source": "SURVEY 8(d) env bytes + transition row + next obs32 + actor parameters / n"},
+        "mfma_roofline": {"bound": "mfma", "achieved": fpe * n / (kern_avg * 1e-3) / 1e12, "peak": 157.3,
+                          "unit": "TFLOP/s", "frac": fpe * n / (kern_avg * 1e-3) / 1e12 / 157.3,
+                          "flops_per_env_step": fpe, "note": "the actor's GEMMs (fp32 MFMA peak) over the whole kernel "
+                                                             "time, which also steps the env"},
     }
+    if args.cpu_baseline and world == 1:
+        sys.path.insert(0, os.path.join(REPO, "oracle"))
+        import oracle
+        thr = max(1, min(int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)), os.cpu_count() or 1, 64))
+        ps = [p.detach().float().cpu().numpy() for p in actor.parameters()]
+        L_ = sum(1 for m in actor.shared_net if isinstance(m, torch.nn.Linear))
+        ne, ns = 16 * thr, 300
+        t0 = time.perf_counter()
+        _, nsteps = oracle.sac_collect(ne, ns, ps, H, L_, S, A, seed=1234, threads=thr)
+        dt = time.perf_counter() - t0
+        out["cpu_baseline"] = {"value": nsteps / dt, "unit": "env-steps/s", "cores": thr, "kind": "port",
+                               "sample": f"oracle/pd_oracle.c orc_sac_collect_mt: the same actor (binary32, sequential "
+                                         f"sums) + sampling + env step + transition row, {ne} envs x {ns} steps on "
+                                         f"{thr} host threads, {dt:.1f} s"}
     return out
 
 
@@ -184,6 +229,7 @@ def bench_pso(args, world, rank, local, dist):
     P = args.particles
     opt = ParticleSubswarmOptimisationGPU("landing_burn", pop_size=P * world, device=local, seed=1234,
                                           precision=args.precision, dist=dist,
+                                          tuning=dict(policy_list=args.policy_list),
                                           pso_params=dict(generations=args.warmup + args.steps,
                                                           re_initialise_generation=-1))
     for g in range(args.warmup):
@@ -195,7 +241,18 @@ def bench_pso(args, world, rank, local, dist):
         opt.generation(args.warmup + k)
     # episode lengths of the timed generations (a separate evaluation pass is not timed)
     wall = timed_region(one, args.steps, torch.cuda.synchronize, dist, opt.device)
-    _, steps = opt.evaluate(opt.x32)
+    # the dominant kernel: the policy rollout of the swarm's current positions (pd_rollout_policy:
+    # k_step<POL> launches until every episode ended), replayed with a HIP event pair per rollout
+    kern = []
+    for _ in range(max(1, min(args.steps, 8))):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        _, steps = opt.evaluate(opt.x32)
+        e1.record()
+        kern.append((e0, e1))
+    torch.cuda.synchronize()
+    kern_ms = sorted(a.elapsed_time(b) for a, b in kern)
+    kern_avg = sum(kern_ms) / len(kern_ms)
     tot += steps.sum()
     if dist:
         dist.all_reduce(tot)
@@ -203,6 +260,9 @@ def bench_pso(args, world, rank, local, dist):
         return None
     mean_len = int(tot.item()) / (P * world)
     eps = whole_job_rate(P, world, args.steps, wall)
+    # per particle-episode: the env's algorithmic bytes per env-step (f64 landing_burn, no wind:
+    # SURVEY 8(d)) x the episode's steps, + its 372 float32 actor parameters read once
+    bpp = mean_len * algorithmic_bytes(args.precision, "landing_burn", False) + 4 * 372
     out = {
         "metric": "PSO particle-episodes/sec (c4: fused actor rollouts + device swarm update)", "value": eps,
         "unit": "particle-episodes/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -214,18 +274,27 @@ def bench_pso(args, world, rank, local, dist):
                    "parallelism": f"particle-shard x{world} + subswarm-minimum all_gather"},
         "env_steps_per_s_est": eps * mean_len, "mean_episode_len_after": mean_len,
         "global_best_fitness": opt.gbf,
+        "roofline": {"bound": "hbm", "achieved": bpp * P / (kern_avg * 1e-3) / 1e9, "peak": 8000.0, "unit": "GB/s",
+                     "frac": bpp * P / (kern_avg * 1e-3) / 1e9 / 8000.0, "traffic": None,
+                     "bytes_per_particle_episode": round(bpp, 1), "kernel": "k_step<POL> (pd_rollout_policy)",
+                     "kernel_avg_ms": kern_avg, "kernel_med_ms": kern_ms[len(kern_ms) // 2], "rollouts": len(kern_ms),
+                     "kernel_timing": "HIP events around each replayed rollout of the swarm's positions (its reset, "
+                                      "k_step launches, count checks and miss flush)",
+                     "bytes_source": "SURVEY 8(d) landing_burn env bytes x mean episode length + the actor's parameters"},
     }
     if args.cpu_baseline and world == 1:
         sys.path.insert(0, os.path.join(REPO, "oracle"))
         import numpy as np
         import oracle
-        Wc = np.random.default_rng(0).uniform(-1.5, 1.5, (2048, 372)).astype(np.float32)
+        thr = max(1, min(int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)), os.cpu_count() or 1, 64))
+        Wc = np.random.default_rng(0).uniform(-1.5, 1.5, (1024 * thr, 372)).astype(np.float32)
         t0 = time.perf_counter()
-        _, st = oracle.rollout_policy(1, Wc, 2200)
+        _, st = oracle.rollout_policy(1, Wc, 2200, threads=thr)
         dt = time.perf_counter() - t0
-        out["cpu_baseline"] = {"value": len(Wc) / dt, "unit": "particle-episodes/s", "cores": 1, "kind": "port",
-                               "sample": f"oracle/pd_oracle.c orc_rollout_policy, {len(Wc)} particles "
-                                         f"({int(st.sum())} env-steps), 1 host thread, {dt:.1f} s"}
+        out["cpu_baseline"] = {"value": len(Wc) / dt, "unit": "particle-episodes/s", "cores": thr, "kind": "port",
+                               "sample": f"oracle/pd_oracle.c orc_rollout_policy_mt, {len(Wc)} particles of the same "
+                                         f"U(-1.5, 1.5) swarm law ({int(st.sum())} env-steps), {thr} host threads, "
+                                         f"{dt:.1f} s"}
     return out
 
 
@@ -320,7 +389,7 @@ def run_c3(args, precision, local, rank, dist, descent=False, launch_base=0, bur
         outs = (torch.empty(F, n, env.obs_dim, dtype=env.dtype, **kw), torch.empty(F, n, dtype=env.dtype, **kw),
                 torch.empty(F, n, dtype=torch.uint8, **kw), torch.empty(F, n, dtype=torch.uint8, **kw),
                 torch.empty(F, n, dtype=torch.int8, **kw))
-        os.environ["PDENV_FUSE"] = str(F)
+        env.set_tuning(step_fuse=F)
 
         def chunk(t0, t1):
             env.step_n_raw(acts[t0:t1], tuple(o[:t1 - t0] for o in outs))
@@ -469,6 +538,8 @@ def main():
     ap.add_argument("--particles", type=int, default=32768, help="c4: particles per GPU")
     ap.add_argument("--fuse", type=int, default=128,
                     help="c3: env-steps per k_step launch (pd_step_n; 1 = one pd_step launch per step)")
+    ap.add_argument("--policy-list", type=int, default=-1, choices=[-1, 0, 1],
+                    help="c4: the policy rollouts' live-list launches (pd_tuning.policy_list: -1 auto, 0 off, 1 on)")
     ap.add_argument("--graph", type=int, default=1, help="c5: replay the collection step as a HIP graph")
     ap.add_argument("--c3-burn-in", type=int, default=C3_BURN_IN,
                     help="c3: untimed env-steps before the warmup (steady state: resets at their stationary rate)")

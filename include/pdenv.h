@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define PD_ABI_VERSION 8   /* 4: pd_config.integrator (was padding); 5: pd_count_work, pd_step_sac; 6: cell pieces (pd_cell_piece_info, stats word 44); 7: pd_step_sac_ring, pd_sac_actor, stats word 45; 8: pd_step_sac_fused, pd_atm_table */
+#define PD_ABI_VERSION 9   /* 4: pd_config.integrator (was padding); 5: pd_count_work, pd_step_sac; 6: cell pieces (pd_cell_piece_info, stats word 44); 7: pd_step_sac_ring, pd_sac_actor, stats word 45; 8: pd_step_sac_fused, pd_atm_table; 9: pd_config.table_flags, pd_tuning, caller scratch for pd_pso_swarm_minima, state/action dims of pd_step_sac_fused */
 #define PD_MAX_PTS 256      /* aero scatter points per table */
 #define PD_MAX_COLS 5       /* AoA columns per aero table */
 #define PD_MAX_TAB 64       /* grid-fin table length */
@@ -73,6 +73,15 @@ typedef enum { PD_F64 = 0, PD_F32 = 1 } pd_precision;
  * discrete-time process), no policy rollouts.  Checked against the oracle's restatement
  * (orc_physics, ORC_INTEG_RK4), not against the reference. */
 typedef enum { PD_INTEG_REFERENCE = 0, PD_INTEG_RK4 = 1 } pd_integrator;
+/* pd_config.table_flags: how the aero and atmosphere lookups are served (results agree within the
+ * tolerances of DESIGN.md s4/s8; the cell-piece and fine-index switches give the same bits as
+ * their default, which the GPU tests check).  0 = the defaults. */
+typedef enum {
+    PD_TABLES_NO_CELL_PIECES = 1,   /* interior C_D/C_L queries by payload sums, not cell pieces */
+    PD_TABLES_NO_FINE_INDEX = 2,    /* cell pieces reached through the cell / sub-cell records only */
+    PD_TABLES_EXACT_ATMOSPHERE = 4, /* the ISA closed form on the device, never the tabulated pieces */
+    PD_TABLES_VERBOSE = 8           /* print the table builders' statistics to stderr at create */
+} pd_table_flags;
 
 /* One neighbourhood-aero table: scatter points grouped by AoA column, Mach-sorted inside. */
 typedef struct {
@@ -150,7 +159,21 @@ typedef struct {
                                   alive bonus 0.01 (1-g) (rtd_rl.py:267, 472); rl_wrapped_env_pytorch kwargs */
     int32_t trajectory_length;
     int32_t integrator;        /* pd_integrator (ABI 4; 0 = the reference's) */
+    int32_t table_flags;       /* pd_table_flags (ABI 9; 0 = the defaults) */
+    int32_t pad3;
 } pd_config;
+
+/* Launch tuning of a handle (pd_set_tuning / pd_get_tuning; ABI 9).  Results never depend on it:
+ * every setting steps the same envs through the same arithmetic. */
+typedef struct {
+    int32_t step_fuse;        /* env-steps per pd_step_n / pd_rollout launch, 1..256 (default 128) */
+    int32_t policy_fuse;      /* policy steps per pd_rollout_policy launch: a power of two 1..64 (default 64) */
+    int32_t policy_lanes;     /* lanes per env of the policy rollouts: 2 (default), 4 or 8 */
+    int32_t policy_list;      /* live-list launches of the policy rollouts: -1 = when the grid exceeds
+                                 one chip round (default), 0 = never, 1 = from the first launch */
+    double policy_list_at;    /* > 0 (with policy_list -1 or 0): switch the list on once the live count
+                                 read back falls to this fraction of n_envs (default 0: never) */
+} pd_tuning;
 
 /* Info tap of pd_step: the quantities of the LAST physics sub-step that rocket_physics_fcn puts in
  * its info dict (rockets_physics.py:649-702, incl. acceleration_dict / moments_dict), the
@@ -187,6 +210,9 @@ int pd_device_count(void);
 
 pd_status pd_create(const pd_params* params, const pd_config* cfg, pd_env** out);
 pd_status pd_destroy(pd_env* env);
+/* Launch tuning (see pd_tuning); PD_ERR_INVALID, changing nothing, for out-of-range fields. */
+pd_status pd_set_tuning(pd_env* env, const pd_tuning* tuning);
+pd_status pd_get_tuning(const pd_env* env, pd_tuning* tuning);
 /* Reset envs (mask: device uint8[N], NULL = all).  obs may be NULL. */
 pd_status pd_reset(pd_env* env, const uint8_t* mask, void* obs, void* stream);
 /* One env step for all N envs.
@@ -202,7 +228,7 @@ pd_status pd_step(pd_env* env, const void* actions, void* obs, void* reward, uin
  * phases: obs [n_steps][N][O], reward [n_steps][N], done/truncated/trunc_id [n_steps][N] receive
  * every step's outputs (any may be NULL).  Replaces a Python loop over
  * rocket_environment_pre_wrap.step (base_environment.py:99-154) with fused launches: each launch
- * runs up to 128 steps (PDENV_FUSE, 1..256) of every env in one kernel, so the LDS table staging and the
+ * runs up to 128 steps (pd_tuning.step_fuse, 1..256) of every env in one kernel, so the LDS table staging and the
  * launch tail are paid once per launch, followed by the miss flush.  Results are bit-identical
  * to n_steps pd_step calls.  No host synchronisation. */
 pd_status pd_step_n(pd_env* env, const void* actions, int32_t n_steps, void* obs, void* reward, uint8_t* done,
@@ -250,8 +276,9 @@ pd_status pd_step_sac_ring(pd_env* env, const float* heads, int32_t deterministi
  * unclamped: pd_step_sac_ring clamps).  params: a host array of 2 (n_hidden_layers + 2) device
  * pointers, the torch parameters in named_parameters() order (weight [out][in] row-major, bias):
  * shared_net layers, then mean, then log_std.  hidden 128, 256 or 512 (else PD_ERR_UNSUPPORTED),
- * state_dim <= 16, action_dim <= 8, n_hidden_layers <= 8.  f32 sums in another order than
- * torch's GEMMs: equal to f32 rounding.  Runs on the current HIP device. */
+ * state_dim <= 16, action_dim <= 8, n_hidden_layers <= 8; every parameter 16-byte aligned (else
+ * PD_ERR_UNSUPPORTED).  f32 sums in another order than torch's GEMMs: equal to f32 rounding.  Runs
+ * on the current HIP device. */
 pd_status pd_sac_actor(int64_t n, int32_t state_dim, int32_t hidden, int32_t n_hidden_layers, int32_t action_dim,
                        const float* obs, const float* const* params, float* heads, void* stream);
 /* The whole SAC collection step (sac_pytorch_powered_descent.py:160-183: actor.sample on the
@@ -259,11 +286,13 @@ pd_status pd_sac_actor(int64_t n, int32_t state_dim, int32_t hidden, int32_t n_h
  * (sac_pytorch.py:129-159) runs in the step kernel's prologue for each workgroup's 16 envs, on
  * obs32 [N][S] as the previous step (or pd_observe) left it, then pd_step_sac_ring follows with
  * those heads (same arguments and semantics; obs32 is overwritten with the next observation).
- * hidden / n_hidden_layers / params as pd_sac_actor; heads [N][2A] (may be NULL) receives the
- * heads.  Handles stepping 16 lanes per env (the default up to 4 096 envs) with hidden <= 256
- * take the single launch; others run pd_sac_actor + pd_step_sac_ring (two launches, the same
- * bits).  No host synchronisation. */
-pd_status pd_step_sac_fused(pd_env* env, int32_t hidden, int32_t n_hidden_layers, const float* const* params,
+ * state_dim / action_dim / hidden / n_hidden_layers / params as pd_sac_actor (state_dim and
+ * action_dim must equal the handle's pd_obs_dim / pd_action_dim: PD_ERR_INVALID otherwise); heads
+ * [N][2A] (may be NULL) receives the heads.  Handles stepping 16 lanes per env (the default up to
+ * 4 096 envs) with hidden <= 256 take the single launch; others run pd_sac_actor +
+ * pd_step_sac_ring (two launches, the same bits).  No host synchronisation. */
+pd_status pd_step_sac_fused(pd_env* env, int32_t state_dim, int32_t action_dim, int32_t hidden,
+                            int32_t n_hidden_layers, const float* const* params,
                             float* heads, int32_t deterministic, float log_std_min, float log_std_max,
                             float max_action, float* eps_out, float* action, float* ring, int64_t capacity,
                             long long* ring_state, float* priorities, const float* max_priority, float* obs32,
@@ -283,10 +312,10 @@ pd_status pd_rollout(pd_env* env, const void* actions, int32_t n_steps, void* re
  *  check_every: >0 = read the live-env count every that many steps (at least once per launch),
  *            stop early when all envs are done, and size later launches to the live count (one
  *            host sync per check); 0 = always max_steps steps over the full grid.
- * Each launch runs up to 64 fused steps (PDENV_PFUSE); a finished episode's lanes freeze and a
- * wave whose episodes have all ended leaves the launch.  Grids beyond one chip round of lanes
- * step only the live envs: a compacted index list, rebuilt inside the step kernel (wave ballot
- * + prefix count, one atomic per wave).  Results do not depend on either. */
+ * Each launch runs up to 64 fused steps (pd_tuning.policy_fuse); a finished episode's lanes freeze
+ * and a wave whose episodes have all ended leaves the launch.  Grids beyond one chip round of lanes
+ * step only the live envs (pd_tuning.policy_list): a compacted index list, rebuilt inside the step
+ * kernel (wave ballot + prefix count, one atomic per wave).  Results do not depend on either. */
 pd_status pd_rollout_policy(pd_env* env, const float* weights, int32_t n_params, int32_t max_steps,
                             void* fitness, int32_t* steps, int32_t check_every, void* stream);
 /* One PSO generation's particle update on the device (particle_swarm_optimisation.py:437-441
@@ -308,10 +337,13 @@ pd_status pd_pso_step(int64_t n_particles, int32_t dim, const double* fitness, d
  * subswarm_best` over the subswarm's particles in order (a NaN fitness never wins, ties keep the
  * lower index): min_fitness [n_swarms] and its position min_position [n_swarms][dim] (from
  * position [dim][n_particles]); +inf and zeros for a subswarm with no particle of non-NaN fitness.
- * A two-pass segmented argmin over blocks of 1 024 particles; no host synchronisation. */
+ * A two-pass segmented argmin over blocks of 1 024 particles; no host synchronisation.  scratch:
+ * a device buffer of at least pd_pso_swarm_minima_scratch_bytes(n_particles, n_swarms) bytes for
+ * the first pass's partials, owned by the caller (calls that may overlap need their own). */
+size_t pd_pso_swarm_minima_scratch_bytes(int64_t n_particles, int32_t n_swarms);
 pd_status pd_pso_swarm_minima(int64_t n_particles, int32_t dim, int32_t n_swarms, const double* fitness,
                               const int32_t* swarm, const double* position, double* min_fitness,
-                              double* min_position, void* stream);
+                              double* min_position, void* scratch, size_t scratch_bytes, void* stream);
 /* The subswarm and global bests after a generation (particle_swarm_optimisation.py:442-444,
  * :474-477), on the device: subswarm s takes (min_fitness[s], min_position[s]) if strictly better;
  * then the first subswarm holding the smallest best replaces global_best(_fitness) if strictly

@@ -127,6 +127,11 @@ def lib():
         L.orc_rollout_mt.argtypes = [P(OrcParams), C.c_int, C.c_int, C.c_int, C.c_int, P(C.c_float),
                                      C.c_int, C.c_int, D, C.c_uint64, C.c_int, P(C.c_int64)]
         L.orc_actor.argtypes = [P(OrcParams), C.c_int, P(C.c_float), P(D), P(C.c_float)]
+        L.orc_rollout_policy_mt.argtypes = [P(OrcParams), C.c_int, C.c_int, P(C.c_float), C.c_int, P(D),
+                                            P(C.c_int32), C.c_int]
+        L.orc_sac_collect_mt.restype = D
+        L.orc_sac_collect_mt.argtypes = [P(OrcParams), C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                         C.c_void_p, C.c_uint64, C.c_int, P(C.c_int64)]
         L.orc_rollout_policy.argtypes = [P(OrcParams), C.c_int, C.c_int, P(C.c_float), C.c_int, P(D),
                                          P(C.c_int32)]
         L.orc_reset_philox.restype = None
@@ -375,12 +380,30 @@ def actor(phase, w, state):
     return out[:1] if phase == 0 else out
 
 
-def rollout_policy(phase, W, max_steps=2200):
-    """PSO objective of every particle row of W (no wind): (fitness, steps)."""
+def rollout_policy(phase, W, max_steps=2200, threads=1):
+    """PSO objective of every particle row of W (no wind): (fitness, steps); threads > 1: the
+    particles split over that many host threads (the c4 cpu_baseline)."""
     W = np.ascontiguousarray(W, dtype=np.float32)
     n = W.shape[0]
     fit = np.zeros(n)
     steps = np.zeros(n, dtype=np.int32)
-    lib().orc_rollout_policy(C.byref(params()), phase, n, W.ctypes.data_as(C.POINTER(C.c_float)), int(max_steps),
-                             fit.ctypes.data_as(C.POINTER(C.c_double)), steps.ctypes.data_as(C.POINTER(C.c_int32)))
+    args = (C.byref(params()), phase, n, W.ctypes.data_as(C.POINTER(C.c_float)), int(max_steps),
+            fit.ctypes.data_as(C.POINTER(C.c_double)), steps.ctypes.data_as(C.POINTER(C.c_int32)))
+    if threads > 1:
+        lib().orc_rollout_policy_mt(*args, int(threads))
+    else:
+        lib().orc_rollout_policy(*args)
     return fit, steps
+
+
+def sac_collect(n_env, n_steps, params_f32, hidden, n_layers, state_dim=2, action_dim=1, seed=1234, threads=1):
+    """c5's collection step on the host (the c5 cpu_baseline): the SAC actor's forward pass and
+    sampling in binary32, the env step, the transition row, for n_env envs x n_steps steps;
+    params_f32: the actor's 2 (n_layers + 2) float32 arrays in torch's named_parameters() order.
+    Returns (sum of rewards, env-steps)."""
+    arrs = [np.ascontiguousarray(a, dtype=np.float32) for a in params_f32]
+    ptrs = (C.c_void_p * len(arrs))(*[a.ctypes.data for a in arrs])
+    steps = C.c_int64()
+    acc = lib().orc_sac_collect_mt(C.byref(params()), int(n_env), int(n_steps), int(state_dim), int(hidden),
+                                   int(n_layers), int(action_dim), ptrs, int(seed), int(threads), C.byref(steps))
+    return acc, steps.value

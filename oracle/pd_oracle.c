@@ -1242,3 +1242,139 @@ void orc_rollout_policy(const orc_params* P, int phase, int n, const float* w, i
         steps[i] = t;
     }
 }
+
+/* ---------------------------------------------------------------- CPU baselines (bench.py)
+ * The oracle is test infrastructure; these two drivers exist only as bench.py's cpu_baseline legs
+ * for BASELINE configs c4 and c5, timed on the host's cores over a static partition. */
+typedef struct { const orc_params* P; int phase, n, max_steps; const float* w; double* fit; int32_t* steps; } pol_job;
+static void* pol_worker(void* p) {
+    pol_job* j = (pol_job*)p;
+    orc_rollout_policy(j->P, j->phase, j->n, j->w, j->max_steps, j->fit, j->steps);
+    return NULL;
+}
+
+/* orc_rollout_policy on n_threads host threads, particles split in contiguous blocks */
+void orc_rollout_policy_mt(const orc_params* P, int phase, int n, const float* w, int max_steps, double* fitness,
+                           int32_t* steps, int n_threads) {
+    pthread_once(&g_log_once, log_cells_fill);
+    if (n_threads < 1) n_threads = 1;
+    if (n_threads > n) n_threads = n > 0 ? n : 1;
+    const int np_ = orc_actor_params(phase);
+    pol_job* jobs = (pol_job*)calloc((size_t)n_threads, sizeof(pol_job));
+    pthread_t* th = (pthread_t*)calloc((size_t)n_threads, sizeof(pthread_t));
+    for (int k = 0; k < n_threads; ++k) {
+        const int i0 = (int)((int64_t)n * k / n_threads), i1 = (int)((int64_t)n * (k + 1) / n_threads);
+        pol_job* j = &jobs[k];
+        j->P = P; j->phase = phase; j->n = i1 - i0; j->max_steps = max_steps; j->w = w + (size_t)i0 * np_;
+        j->fit = fitness + i0; j->steps = steps + i0;
+        if (n_threads > 1) pthread_create(&th[k], NULL, pol_worker, j);
+        else pol_worker(j);
+    }
+    if (n_threads > 1)
+        for (int k = 0; k < n_threads; ++k) pthread_join(th[k], NULL);
+    free(jobs); free(th);
+}
+
+/* c5's collection step per env (sac_pytorch_powered_descent.py:160-183), pure throttle, rtd RL,
+ * no wind, auto-reset: the Actor's forward pass (sac_pytorch.py:129-159: Linear(S, H) ReLU,
+ * (L - 1) x [Linear(H, H) ReLU], the mean and log_std heads; torch's named_parameters() order and
+ * [out][in] weights) in binary32 with sequential sums, Actor.sample (sac_pytorch.py:161-179: log_std
+ * clamped to [-20, 2], std = exp, tanh(mean + std eps), max_action 1) with eps drawn as the device
+ * draws it (Philox tag 19: (env, episode, step)), the env step, and the transition row
+ * state | action | reward | next_state | done into the thread's ring of `ring_rows` rows. */
+#define ORC_SAC_MAXH 512
+typedef struct {
+    const orc_params* P; int i0, i1, n_steps, S, H, L, A, ring_rows; const float* const* prm; uint64_t seed;
+    int64_t steps; double acc;
+} sac_job;
+static void sac_dense(const float* w, const float* b, int in, int out, const float* x, float* y, int relu) {
+    for (int j = 0; j < out; ++j) {
+        float acc = 0.f;
+        const float* wr = w + (size_t)j * in;
+        for (int k = 0; k < in; ++k) acc = acc + wr[k] * x[k];
+        acc = acc + b[j];
+        y[j] = relu && acc < 0.f ? 0.f : acc;
+    }
+}
+static void sac_range(sac_job* j) {
+    const orc_params* P = j->P;
+    const int S = j->S, H = j->H, L = j->L, A = j->A, W = 2 * S + A + 2;
+    float* ring = (float*)calloc((size_t)j->ring_rows * W, sizeof(float));
+    float h0[ORC_SAC_MAXH], h1[ORC_SAC_MAXH];
+    int64_t steps = 0, row = 0;
+    double acc = 0.0;
+    orc_env E;
+    orc_out o;
+    for (int i = j->i0; i < j->i1; ++i) {
+        uint32_t ep = 0;
+        orc_reset_philox(P, &E, ORC_PHASE_PURE_THROTTLE, j->seed, (uint64_t)i, ep, 0, 0, -1, 0.0);
+        double ob[8];
+        obs_rl(P, ORC_PHASE_PURE_THROTTLE, E.s, ob);
+        for (int t = 0; t < j->n_steps; ++t) {
+            float x[16], mean[8], lstd[8], a[8];
+            for (int k = 0; k < S; ++k) x[k] = (float)ob[k];
+            sac_dense(j->prm[0], j->prm[1], S, H, x, h0, 1);
+            for (int l = 1; l < L; ++l) {
+                sac_dense(j->prm[2 * l], j->prm[2 * l + 1], H, H, h0, h1, 1);
+                memcpy(h0, h1, (size_t)H * sizeof(float));
+            }
+            sac_dense(j->prm[2 * L], j->prm[2 * L + 1], H, A, h0, mean, 0);
+            sac_dense(j->prm[2 * L + 2], j->prm[2 * L + 3], H, A, h0, lstd, 0);
+            double u[4] = {0, 0, 0, 0};
+            for (int k = 0; k < A; k += 2) {
+                orc_u32x4 c = {(uint32_t)i, ep, (uint32_t)E.rng_ts, 19u + (uint32_t)(k >> 1)};
+                double z0, z1;
+                orc_gauss_pair(orc_philox(c, (uint32_t)j->seed, (uint32_t)(j->seed >> 32)), &z0, &z1);
+                for (int q = k; q < k + 2 && q < A; ++q) {
+                    float ls = lstd[q] < -20.f ? -20.f : (lstd[q] > 2.f ? 2.f : lstd[q]);
+                    a[q] = tanhf(mean[q] + expf(ls) * (float)(q == k ? z0 : z1));
+                    u[q] = a[q];
+                }
+            }
+            orc_step(P, &E, ORC_PHASE_PURE_THROTTLE, ORC_RTD_RL, u, 1, NULL, &o);
+            float* r = ring + (size_t)(row % j->ring_rows) * W;
+            for (int k = 0; k < S; ++k) r[k] = (float)ob[k];
+            for (int k = 0; k < A; ++k) r[S + k] = a[k];
+            r[S + A] = (float)o.reward;
+            for (int k = 0; k < S; ++k) r[S + A + 1 + k] = (float)o.obs[k];
+            r[2 * S + A + 1] = (float)o.done;
+            ++row; ++steps; acc += o.reward;
+            if (o.done || o.trunc) {
+                ++ep;
+                orc_reset_philox(P, &E, ORC_PHASE_PURE_THROTTLE, j->seed, (uint64_t)i, ep, 0, 0, -1, 0.0);
+                obs_rl(P, ORC_PHASE_PURE_THROTTLE, E.s, ob);
+            } else {
+                for (int k = 0; k < S; ++k) ob[k] = o.obs[k];
+            }
+        }
+    }
+    free(ring);
+    j->steps = steps; j->acc = acc;
+}
+static void* sac_worker(void* p) { sac_range((sac_job*)p); return NULL; }
+
+double orc_sac_collect_mt(const orc_params* P, int n_env, int n_steps, int S, int H, int L, int A,
+                          const float* const* prm, uint64_t seed, int n_threads, int64_t* env_steps_out) {
+    pthread_once(&g_log_once, log_cells_fill);
+    if (S > 16 || A > 8 || H > ORC_SAC_MAXH || L < 1) return 0.0;
+    if (n_threads < 1) n_threads = 1;
+    if (n_threads > n_env) n_threads = n_env > 0 ? n_env : 1;
+    sac_job* jobs = (sac_job*)calloc((size_t)n_threads, sizeof(sac_job));
+    pthread_t* th = (pthread_t*)calloc((size_t)n_threads, sizeof(pthread_t));
+    for (int k = 0; k < n_threads; ++k) {
+        sac_job* j = &jobs[k];
+        j->P = P; j->i0 = (int)((int64_t)n_env * k / n_threads); j->i1 = (int)((int64_t)n_env * (k + 1) / n_threads);
+        j->n_steps = n_steps; j->S = S; j->H = H; j->L = L; j->A = A; j->prm = prm; j->seed = seed;
+        j->ring_rows = 4096;
+        if (n_threads > 1) pthread_create(&th[k], NULL, sac_worker, j);
+        else sac_range(j);
+    }
+    double acc = 0.0; int64_t steps = 0;
+    for (int k = 0; k < n_threads; ++k) {
+        if (n_threads > 1) pthread_join(th[k], NULL);
+        acc += jobs[k].acc; steps += jobs[k].steps;
+    }
+    free(jobs); free(th);
+    if (env_steps_out) *env_steps_out = steps;
+    return acc;
+}

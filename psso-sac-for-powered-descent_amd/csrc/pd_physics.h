@@ -20,31 +20,50 @@ template <> struct Cst<float> {
 };
 
 // a / b for a divisor known ahead of the call -- a literal or a per-handle parameter -- given
-// rb = RN(1/b), its correctly rounded reciprocal (a compile-time or host division).  Markstein's
-// correction step returns the IEEE quotient RN(a / b): with rb within half an ulp of 1/b,
-// q = RN(a rb) is within one ulp of a/b, r = a - b q is exact (one FMA) and RN(q + r rb) = RN(a/b)
-// (Markstein's theorem; finite a and b away from underflow and overflow, as every divisor here
-// is).  The last step is computed negated, -RN(-r rb - q), so that a zero numerator keeps its
-// sign.  Three VALU operations, three deep, where a general division is the ten-deep
-// v_div_scale / v_rcp / Newton / v_div_fmas / v_div_fixup sequence.  tests/test_markstein.py
-// checks it bit for bit against IEEE division for every divisor it replaces.  PD_MARKSTEIN=0
-// (experiments) divides.
-#ifndef PD_MARKSTEIN
-#define PD_MARKSTEIN 1
-#endif
-template <typename R> __device__ __forceinline__ R div_known(R a, R b, R rb) {
-#if PD_MARKSTEIN
-    const R q = a * rb;
-    const R r = fma(-b, q, a);
+// rb = RN(1/b), its correctly rounded reciprocal (a compile-time or host division), as the IEEE
+// quotient RN(a / b) (finite a, b > 0, a / b away from underflow and overflow, as every quotient
+// here is).  Markstein's theorem: if rb is within half an ulp of 1/b and q is within one ulp of
+// a/b (faithful), then r = a - b q is exact (one FMA) and RN(q + r rb) = RN(a/b).  Whether
+// q = RN(a rb) is faithful depends on the divisor: with eps = b rb - 1 (exact), |a rb - a/b| =
+// |a/b| |eps| < 2^(e+1) |eps| for a/b in [2^e, 2^(e+1)), below half an ulp of a/b when
+// |eps| <= 2^-(p+1) (p = 53 / 24), and q is then faithful for every a (one_step_ok).  Other
+// divisors take one more correction first: q1 = RN(q + r rb) is within half an ulp plus
+// |a/b - q| 2^(1-p) of a/b, so faithful, and the final step is Markstein's.  Each step is
+// computed negated, -RN(-r rb - q), so that a zero numerator keeps its sign.  Three (five) VALU
+// operations where a general division is the ten-deep v_div_scale / v_rcp / Newton / v_div_fmas
+// / v_div_fixup sequence.  tests/test_markstein.py checks the classification in exact rational
+// arithmetic, every binary32 numerator of every divisor the kernel replaces, and sampled
+// binary64 numerators, bit for bit against IEEE division.
+template <typename R> constexpr R veltkamp_c() { return sizeof(R) == 8 ? R(134217729.0) : R(4097.0f); }
+// eps = b rb - 1 as (hi - 1) + lo, hi + lo = b rb exactly (Dekker's product; no FMA contraction
+// in this build), so both the compiler (literals) and the host (handle divisors) classify
+template <typename R> constexpr bool one_step_ok(R b, R rb) {
+    const R p = b * rb;
+    const R C = veltkamp_c<R>();
+    const R tb = C * b, bh = tb - (tb - b), bl = b - bh;
+    const R tr = C * rb, rh = tr - (tr - rb), rl = rb - rh;
+    const R lo = ((bh * rh - p) + bh * rl + bl * rh) + bl * rl;
+    const R eps = (p - R(1)) + lo;
+    // |eps| <= 2^-(p+1), with a 1 % margin for the rounding of the sum (conservative: a divisor
+    // at the bound takes the second correction)
+    const R lim = sizeof(R) == 8 ? R(0.99 * 0x1p-54) : R(0.99f * 0x1p-25f);
+    return eps <= lim && -eps <= lim;
+}
+template <typename R> __device__ __forceinline__ R div_known(R a, R b, R rb, bool two) {
+    R q = a * rb;
+    R r = fma(-b, q, a);
+    if (two) {
+        q = -fma(-r, rb, -q);
+        r = fma(-b, q, a);
+    }
     return -fma(-r, rb, -q);
-#else
-    (void)rb;
-    return a / b;
-#endif
 }
 // the reciprocal of a literal divisor, folded at compile time in R's precision
 template <typename R> constexpr R rcp_c(R b) { return R(1) / b; }
-#define PD_DIVC(R_, a, b) div_known<R_>((a), R_(b), rcp_c<R_>(R_(b)))
+// DevParams::div2 bits (the handle's divisors)
+constexpr uint32_t kDiv2MProp0 = 1, kDiv2Y0 = 2, kDiv2M0 = 4, kDiv2NormY = 8, kDiv2NormVy = 16, kDiv2NormX = 32,
+                   kDiv2NormVx = 64;
+#define PD_DIVC(R_, a, b) div_known<R_>((a), R_(b), rcp_c<R_>(R_(b)), !one_step_ok<R_>(R_(b), rcp_c<R_>(R_(b))))
 
 constexpr int kLineMax = 96;   // breakpoints per clamped query line
 // line search buckets: Mach [0, 10) in kLineBuckets; bucket b's breakpoint index range (lo, hi),
@@ -114,6 +133,8 @@ template <typename R> struct DevParams {
     // correctly rounded reciprocals of the divisors above (div_known): 1 / m_prop0, y0_rl, m0_rl,
     // norm_y, norm_vy, norm_x, norm_vx
     R inv_m_prop0, inv_y0_rl, inv_m0_rl, inv_norm_y, inv_norm_vy, inv_norm_x, inv_norm_vx;
+    // bit k set: divisor k of that list needs div_known's second correction (!one_step_ok)
+    uint32_t div2, pad_div2;
     // neighbourhood hash tables
     const unsigned long long* keys_cd;
     const unsigned long long* keys_cl;
@@ -244,16 +265,10 @@ template <> __device__ __forceinline__ void pd_sincos<double>(double x, double& 
 }
 
 // ---------------------------------------------------------------- flight-path angle
-// gamma = atan2(vy, vx) (rockets_physics.py:631): the device library's atan2.  PD_ATAN2_FD=1
-// (experiments) takes atan2_fd (pd_common.h; <= 1 ulp of glibc's, one division) for binary64:
-// measured 3 % slower on c3 and c3-descent, 5 % on c2 (profiles/r04_exp_s2_variants.jsonl).
-#ifndef PD_ATAN2_FD
-#define PD_ATAN2_FD 0
-#endif
+// gamma = atan2(vy, vx) (rockets_physics.py:631): the device library's atan2 (fdlibm's reduction
+// with one division, tools/experiments/atan2_fd.patch, measured 3 % slower on c3 and c3-descent,
+// 5 % on c2: profiles/r04_exp_s2_variants.jsonl)
 template <typename R> __device__ __forceinline__ R pd_atan2(R y, R x) { return atan2(y, x); }
-#if PD_ATAN2_FD
-template <> __device__ __forceinline__ double pd_atan2<double>(double y, double x) { return atan2_fd(y, x); }
-#endif
 
 // ---------------------------------------------------------------- atmosphere
 // atmosphere_dynamics.py:5-27 (ambiance ISA restated)
@@ -395,16 +410,16 @@ __host__ __device__ constexpr int obs_dim(int kind) {
 template <typename R, typename Put>
 __device__ __forceinline__ void obs_eval(DP<R>& P, int kind, const R* s, Put&& put) {
     // (divisions by the normalisers through their reciprocals: div_known, the same quotients)
-    auto ny = [&](R v) { return div_known<R>(v, P.norm_y, P.inv_norm_y); };
-    auto nvy = [&](R v) { return div_known<R>(v, P.norm_vy, P.inv_norm_vy); };
+    auto ny = [&](R v) { return div_known<R>(v, P.norm_y, P.inv_norm_y, P.div2 & kDiv2NormY); };
+    auto nvy = [&](R v) { return div_known<R>(v, P.norm_vy, P.inv_norm_vy, P.div2 & kDiv2NormVy); };
     if (kind == 0) {
         put(0, (R(1) - ny((R)(float)s[1])) * R(2) - R(1));
         put(1, (R(1) - nvy((R)(float)s[3])) * R(2) - R(1));
     } else if (kind == 1) {
         put(0, ny(s[1])); put(1, nvy(s[3]));
     } else if (kind == 2) {
-        put(0, div_known<R>(s[0], P.norm_x, P.inv_norm_x)); put(1, ny(s[1]));
-        put(2, div_known<R>(s[2], P.norm_vx, P.inv_norm_vx)); put(3, nvy(s[3]));
+        put(0, div_known<R>(s[0], P.norm_x, P.inv_norm_x, P.div2 & kDiv2NormX)); put(1, ny(s[1]));
+        put(2, div_known<R>(s[2], P.norm_vx, P.inv_norm_vx, P.div2 & kDiv2NormVx)); put(3, nvy(s[3]));
         put(4, tanh(P.k_theta_pso * (s[4] - Cst<R>::pi / R(2))));
     } else if (kind == 3) {
         put(0, ny((R)(float)s[1])); put(1, nvy((R)(float)s[3]));

@@ -653,16 +653,12 @@ __device__ __forceinline__ R cell_eval(const PD_AS1 R* __restrict__ rec, R M, R 
 // piece (one pass of the instruction stream for all of them) and part 0 returns it, the other
 // parts 0 -- the caller's shuffle sum then adds exact zeros.  The other queries split the payload
 // sum over the parts.  PCS = false: payload sums for every hit (the kernels where the piece code
-// would spill: wind, RK4, run-time-phase and landing-burn SAC instantiations); PD_PIECES_LPE=0
-// (experiments): false everywhere.
-#ifndef PD_PIECES_LPE
-#define PD_PIECES_LPE 1
-#endif
+// would spill: wind, RK4, run-time-phase and landing-burn SAC instantiations).
 template <bool PCS, typename R, typename AT>
 __device__ __forceinline__ R rbf(const AT& a, DP<R>& P, int table, const TabView<R>& t, const LineLds<R>& ln,
                                  RbfCache<R>& cache, R M, R aq, int part, int nparts) {
     TayRef tr{-1, 0, false, false, false, false, -1, 0.0, 0.0, false};
-    const int slot = rbf_lookup<R>(a, P, table, t, ln, cache, M, aq, (PCS && PD_PIECES_LPE) ? &tr : nullptr);
+    const int slot = rbf_lookup<R>(a, P, table, t, ln, cache, M, aq, PCS ? &tr : nullptr);
     const bool tay = tr.piece >= 0;
     const bool cel = tr.cp >= 0;
     R val = R(0);
@@ -899,12 +895,6 @@ template <typename R> __device__ __forceinline__ R cl_query(R ae, R& sgn, bool& 
 // 0-3 and half = 1 units 4-7 (each unit the same sequential sum from the same loads), then one DPP
 // swap per unit gives both lanes all eight; the output layer splits the same way when OUT is even.
 // Half the loads and arithmetic per lane, the same bits (which lane sums a unit does not enter).
-#ifndef PD_POL_EXIT
-#define PD_POL_EXIT 1   // (experiments: 0 = frozen waves run the launch's remaining steps)
-#endif
-#ifndef PD_ACTOR_SPLIT
-#define PD_ACTOR_SPLIT 1   // (experiments: 0 = every lane the whole actor)
-#endif
 template <int IN, int NL, int OUT, bool SPLIT = false>
 __device__ __forceinline__ void actor_forward(const float* __restrict__ W, int64_t N, uint32_t ui,
                                               int half, const float* x, float* y) {
@@ -1085,10 +1075,7 @@ __device__ __forceinline__ TabView<R> tab_view(DP<R>& P, const R* tab, int table
 template <typename R, int PHASE, int RTD, bool WIND, int LPE, int POL = 0, bool RK4 = false, bool CNT = false,
           bool SAC = false>
 // waves_per_eu(2): caps VGPR+AGPR at 256 so the f64 kernel keeps two waves per SIMD
-#ifndef PD_WPE
-#define PD_WPE 2
-#endif
-__global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_WPE))) void k_step(StepArgs<R> a_) {
+__global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(2))) void k_step(StepArgs<R> a_) {
     SA<R>& a = kargs<R>();
     static_assert(sizeof(a_) > 0);
     constexpr int EPB = kStepBlock / LPE;   // envs per workgroup
@@ -1337,11 +1324,11 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
         const float* W = wcopy ? a.policy_wc : a.policy_w;
         if constexpr (PHASE == 0) {
             float x[2] = {(float)(e.s[1] / Q.norm_y), (float)(e.s[3] / Q.norm_vy)};
-            actor_forward<2, 3, 1, (PD_ACTOR_SPLIT && LPE >= 2)>(W, N, uw, role & 1, x, uf);
+            actor_forward<2, 3, 1, (LPE >= 2)>(W, N, uw, role & 1, x, uf);
         } else {
             float x[5] = {(float)(e.s[0] / Q.norm_x), (float)(e.s[1] / Q.norm_y), (float)(e.s[2] / Q.norm_vx),
                           (float)(e.s[3] / Q.norm_vy), (float)tanh(Q.k_theta_pso * (e.s[4] - Cst<R>::pi / R(2)))};
-            actor_forward<5, 4, 4, (PD_ACTOR_SPLIT && LPE >= 2)>(W, N, uw, role & 1, x, uf);
+            actor_forward<5, 4, 4, (LPE >= 2)>(W, N, uw, role & 1, x, uf);
         }
     } else if constexpr (SAC) {
         // Actor.sample (sac_pytorch.py:161-179) on the caller's two heads, in binary32 as torch
@@ -1550,7 +1537,7 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
         PD_T(t_aero1);
         PD_ACC(3, t_aero1 - t_aero0);
         R q = R(0.5) * rho * (speed * speed);
-        R fpc = div_known<R>(P.m_prop0 - mp, P.m_prop0, P.inv_m_prop0);
+        R fpc = div_known<R>(P.m_prop0 - mp, P.m_prop0, P.inv_m_prop0, P.div2 & kDiv2MProp0);
         if (fpc == R(0)) fpc = R(1e-6);
         R x_cog, I;
         // subrocket_0 (full rocket) closures for the ascent, subrocket_2 after (:748-750, :772-774)
@@ -1897,12 +1884,12 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
             // (divisions by literals and by y0 / m0 through their reciprocals: div_known)
             if (qr > R(60000)) { R e_ = PD_DIVC(R, qr - R(60000), 5000); R e2 = e_ * e_; rew -= R(1) * (e2 > R(1) ? R(1) : e2); }
             if (gl > R(5.5)) { R e_ = (gl - R(5.5)) / (R(6) - R(5.5)); R e2 = e_ * e_; rew -= R(1) * (e2 > R(1) ? R(1) : e2); }
-            R prog = div_known<R>(P2.y0_rl - y, P2.y0_rl, P2.inv_y0_rl);
+            R prog = div_known<R>(P2.y0_rl - y, P2.y0_rl, P2.inv_y0_rl, P2.div2 & kDiv2Y0);
             R wp = (qr <= R(60000) && gl <= R(5.5)) ? R(0.5) : R(0.5) * R(0.1);
             rew += wp * prog;
             if (y < R(100)) rew += R(5.5) * (R(1) - PD_DIVC(R, fabs(vy), 50));
-            if (dn && !tr) rew += div_known<R>(R(400) * mp, P2.m0_rl, P2.inv_m0_rl);
-            else if (tr && y > R(0)) rew -= R(50) * div_known<R>(fabs(y), P2.y0_rl, P2.inv_y0_rl);
+            if (dn && !tr) rew += div_known<R>(R(400) * mp, P2.m0_rl, P2.inv_m0_rl, P2.div2 & kDiv2M0);
+            else if (tr && y > R(0)) rew -= R(50) * div_known<R>(fabs(y), P2.y0_rl, P2.inv_y0_rl, P2.div2 & kDiv2Y0);
             else if (tr && y < R(0)) rew -= R(50) * PD_DIVC(R, fabs(vy), 10);
             if (!dn || !(tr && y < R(0))) rew = rew < R(-10) ? R(-10) : (rew > R(10) ? R(10) : rew);
         } else {                      // landing_burn / ACS reward (rtd_rl.py:243-269), u0 = actions[0]
@@ -2084,7 +2071,7 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(PD_W
         // a wave whose episodes have all ended leaves the launch's remaining steps (no barrier
         // follows; its lanes write nothing more): the launch then ends with its last live wave,
         // not F steps after the swarm's last episode
-        if (PD_POL_EXIT && __ballot(live) == 0ull) break;
+        if (__ballot(live) == 0ull) break;
     }
     }   // fused steps
     if constexpr (POL) {

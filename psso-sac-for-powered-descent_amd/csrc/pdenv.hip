@@ -744,12 +744,7 @@ const GridKeys& grid_keys(const pd_aero_table& t, double a0, double a1, int nm, 
 // cells, refined cells in 8 x 8 sub-cells, two-region sub-cells split by their bisector: < 0.1 %
 // of queries verified (measured against 400 x 200 and 1600 x 800)
 void grid_geometry(int tb, int& nm, int& na, double& a0, double& a1) {
-    int d[4] = {800, 32, 800, 400};
-    if (const char* g = getenv("PDENV_GRID")) {   // experiments: "nm_cd,na_cd,nm_cl,na_cl"
-        int v[4];
-        if (sscanf(g, "%d,%d,%d,%d", &v[0], &v[1], &v[2], &v[3]) == 4 && v[0] > 0 && v[1] > 0 && v[2] > 0 && v[3] > 0)
-            for (int k = 0; k < 4; ++k) d[k] = v[k];
-    }
+    const int d[4] = {800, 32, 800, 400};
     nm = d[2 * tb]; na = d[2 * tb + 1];
     a0 = tb ? 0.0 : -10.0 * kDeg2Rad;
     a1 = tb ? 10.0 : 10.0 * kDeg2Rad;
@@ -1317,6 +1312,7 @@ struct pd_env {
     int count_work = 0; // workload counters on (pd_count_work)
     float* sac_heads = nullptr;   // pd_step_sac_fused's two-launch path: the actor heads [N][2A]
     float* pol_wc = nullptr;      // policy rollouts' list launches: the live envs' actor parameters
+    pd_tuning tune{128, 64, 2, -1, 0.0};   // launch tuning (pd_set_tuning)
 };
 
 namespace {
@@ -1444,6 +1440,12 @@ template <typename R> void fill_params(const pd_params* p, const pd_config* c, D
     D.inv_m_prop0 = R(1) / D.m_prop0; D.inv_y0_rl = R(1) / D.y0_rl; D.inv_m0_rl = R(1) / D.m0_rl;
     D.inv_norm_y = R(1) / D.norm_y; D.inv_norm_vy = R(1) / D.norm_vy; D.inv_norm_x = R(1) / D.norm_x;
     D.inv_norm_vx = R(1) / D.norm_vx;
+    {
+        const R b[7] = {D.m_prop0, D.y0_rl, D.m0_rl, D.norm_y, D.norm_vy, D.norm_x, D.norm_vx};
+        const R rb[7] = {D.inv_m_prop0, D.inv_y0_rl, D.inv_m0_rl, D.inv_norm_y, D.inv_norm_vy, D.inv_norm_x, D.inv_norm_vx};
+        D.div2 = 0;
+        for (int k = 0; k < 7; ++k) if (!one_step_ok<R>(b[k], rb[k])) D.div2 |= 1u << k;
+    }
     // ---- phase of the handle: its initial state, observation, and the constants of the
     // other compile_physics phases (rockets_physics.py:17-166,402-451,728-802,959-997)
     D.phase = c->phase;
@@ -1502,6 +1504,8 @@ pd_status validate(const pd_params* p, const pd_config* c) {
     }
     if (c->precision != PD_F64 && c->precision != PD_F32) return fail(PD_ERR_INVALID, "bad precision");
     if (c->integrator != PD_INTEG_REFERENCE && c->integrator != PD_INTEG_RK4) return fail(PD_ERR_INVALID, "bad integrator");
+    if (c->table_flags & ~(PD_TABLES_NO_CELL_PIECES | PD_TABLES_NO_FINE_INDEX | PD_TABLES_EXACT_ATMOSPHERE | PD_TABLES_VERBOSE))
+        return fail(PD_ERR_INVALID, "unknown table_flags bits");
     if (c->integrator == PD_INTEG_RK4 && (c->phase != PD_PHASE_PURE_THROTTLE || c->enable_wind))
         return fail(PD_ERR_UNSUPPORTED, "the RK4 integrator (non-parity, BASELINE c2) exists for "
                                         "landing_burn_pure_throttle without wind only");
@@ -1548,7 +1552,8 @@ template <typename R> pd_status create_impl(const pd_params* p, const pd_config*
     std::vector<R> tay;
     TayStats tst;
     for (int li = 0; li < 4; ++li) build_taylor<R>(li < 2 ? p->cd : p->cl, li, D, tay, tst);
-    if (getenv("PDENV_TAY_DEBUG"))
+    const bool verbose = (c->table_flags & PD_TABLES_VERBOSE) != 0;
+    if (verbose)
         fprintf(stderr, "pdenv taylor: %lld pieces, max abs err %.3g, max rel err %.3g, lines %d %d %d %d\n",
                 (long long)tst.pieces, tst.max_abs, tst.max_rel, D.tay_off[0], D.tay_off[1], D.tay_off[2], D.tay_off[3]);
     {
@@ -1557,13 +1562,13 @@ template <typename R> pd_status create_impl(const pd_params* p, const pd_config*
         if (!tay.empty()) PD_HIP(hipMemcpy(dt, tay.data(), tay.size() * sizeof(R), hipMemcpyHostToDevice));
         D.tay = (const R*)dt;
     }
-    // the atmosphere as piecewise polynomials (PDENV_ATM_TAB=0: the exact formulas on the device)
-    if (const char* at = getenv("PDENV_ATM_TAB"); !(at && at[0] == '0')) {
+    // the atmosphere as piecewise polynomials (PD_TABLES_EXACT_ATMOSPHERE: the exact formulas on the device)
+    if (!(c->table_flags & PD_TABLES_EXACT_ATMOSPHERE)) {
         std::vector<R> atm;
         int n_atm = 0;
         double err_atm = 0;
         build_atm_table<R>(p, atm, n_atm, err_atm);
-        if (getenv("PDENV_TAY_DEBUG")) fprintf(stderr, "pdenv atmosphere table: %d cells, max rel err %.3g\n", n_atm, err_atm);
+        if (verbose) fprintf(stderr, "pdenv atmosphere table: %d cells, max rel err %.3g\n", n_atm, err_atm);
         // (else: the exact formulas; binary32: its y rounds by 8 mm at 80 km, 1e-6 of p)
         if (err_atm <= (sizeof(R) == 8 ? 1e-14 : 4e-6)) {
             void* da;
@@ -1579,12 +1584,11 @@ template <typename R> pd_status create_impl(const pd_params* p, const pd_config*
     int gnm[2], gna[2];
     double ga0[2], ga1[2];
     for (int tb = 0; tb < 2; ++tb) grid_geometry(tb, gnm[tb], gna[tb], ga0[tb], ga1[tb]);
-    // cell pieces for the interior queries (PDENV_CELL_PIECES=0: payload sums only): binary64
+    // cell pieces for the interior queries (PD_TABLES_NO_CELL_PIECES: payload sums only): binary64
     // records for binary64 handles, their binary32 roundings (each checked in binary32,
     // ensure_f32) for binary32 handles
     const CellPieces* cps[2] = {nullptr, nullptr};
-    const char* cpe = getenv("PDENV_CELL_PIECES");
-    if (!(cpe && cpe[0] == '0')) {
+    if (!(c->table_flags & PD_TABLES_NO_CELL_PIECES)) {
         CellPieces* c0 = const_cast<CellPieces*>(&cell_pieces(p->cd, ga0[0], ga1[0], gnm[0], gna[0]));
         CellPieces* c1 = const_cast<CellPieces*>(&cell_pieces(p->cl, ga0[1], ga1[1], gnm[1], gna[1]));
         if (sizeof(R) == 4) { ensure_f32(*c0); ensure_f32(*c1); }
@@ -1592,14 +1596,13 @@ template <typename R> pd_status create_impl(const pd_params* p, const pd_config*
     }
     if ((st = build_grid<R>(p->cd, ga0[0], ga1[0], gnm[0], gna[0], tcd, gk[0], gs[0], sk[0], ss[0], bs[0], cps[0])) != PD_OK) return st;
     if ((st = build_grid<R>(p->cl, ga0[1], ga1[1], gnm[1], gna[1], tcl, gk[1], gs[1], sk[1], ss[1], bs[1], cps[1])) != PD_OK) return st;
-    // the fine index (PDENV_FINE=0: cell and sub-cell records only)
-    const char* fne = getenv("PDENV_FINE");
+    // the fine index (PD_TABLES_NO_FINE_INDEX: cell and sub-cell records only)
     for (int tb = 0; tb < 2; ++tb) {
         D.cell_pc[tb] = nullptr; D.sub_piece[tb] = nullptr; D.fine[tb] = nullptr;
         if (cps[tb] && (st = cell_pieces_device<R>(*cps[tb], &D.cell_pc[tb], &D.sub_piece[tb], &D.fine[tb])) != PD_OK) return st;
-        if (fne && fne[0] == '0') D.fine[tb] = nullptr;
+        if (c->table_flags & PD_TABLES_NO_FINE_INDEX) D.fine[tb] = nullptr;
     }
-    if (getenv("PDENV_TAY_DEBUG"))
+    if (verbose)
         for (int tb = 0; tb < 2; ++tb) {
             int64_t nref = 0, nne = 0, nce = 0;
             for (int v : gs[tb]) { nref += v >= 0 && (v & kGridRefine); nce += v >= 0 && !(v & kGridRefine) && !(v & kGridExact); }
@@ -1725,16 +1728,11 @@ template <typename R> void dispatch_step(const pd_env* e, const StepArgs<R>& a, 
 }
 
 // Policy rollouts run at 2 lanes per env whatever the handle's step LPE: the per-lane actor and
-// the LPE 2 table path (Taylor lines, cell pieces) fit 256 VGPRs without scratch.  PDENV_PLPE=4/8
-// (experiments, the c4 lanes-per-env sweep) runs the LPE 4/8 instantiations, whose tables take the
-// split payload sums.
-int policy_lpe() {
-    const char* v = getenv("PDENV_PLPE");
-    const int l = v && *v ? atoi(v) : 2;
-    return l == 4 || l == 8 ? l : 2;
-}
-template <typename R, int PH, bool W> void launch_policy(const StepArgs<R>& a, int64_t n_launch, hipStream_t s) {
-    switch (policy_lpe()) {
+// the LPE 2 table path (Taylor lines, cell pieces) fit 256 VGPRs without scratch.
+// pd_tuning.policy_lanes 4/8 (the c4 lanes-per-env sweep) runs the LPE 4/8 instantiations, whose
+// tables take the split payload sums.
+template <typename R, int PH, bool W> void launch_policy(int lpe, const StepArgs<R>& a, int64_t n_launch, hipStream_t s) {
+    switch (lpe) {
         case 4: launch_policy_lpe<R, PH, W, 4>(a, n_launch, s); break;
         case 8: launch_policy_lpe<R, PH, W, 8>(a, n_launch, s); break;
         default: launch_policy_lpe<R, PH, W, 2>(a, n_launch, s); break;
@@ -1768,6 +1766,16 @@ template <typename R>
 pd_status step_impl(pd_env* e, const void* actions, void* obs, void* reward, uint8_t* done, uint8_t* trunc,
                     int8_t* tid, const double* noise, void* info, void* reward_sum, hipStream_t s,
                     int n_fused = 1, const SacIO* sac = nullptr) {
+    // every caller's launch needs its inputs: actions (plain steps), the heads or the actor (SAC);
+    // the public entry points check them too, this keeps an internal caller from launching a
+    // kernel that would read through a null pointer
+    if (!sac && !actions) return fail(PD_ERR_INVALID, "step launch without actions");
+    if (sac && sac->mlp.H == 0 && !sac->mean) return fail(PD_ERR_INVALID, "SAC step launch without heads or actor");
+    if (sac && sac->mlp.H != 0 && (!sac->mlp.obs || !sac->mlp.wm || !sac->mlp.ws))
+        return fail(PD_ERR_INVALID, "SAC step launch with an incomplete actor");
+    if (sac && (e->cfg.rtd == PD_RTD_PSO || e->cfg.integrator != PD_INTEG_REFERENCE ||
+                (e->cfg.phase != PD_PHASE_PURE_THROTTLE && e->cfg.phase != PD_PHASE_LANDING_BURN)))
+        return fail(PD_ERR_UNSUPPORTED, "SAC step launch on a handle without a SAC kernel");
     StepArgs<R> a = make_args<R>(e);
     a.actions = actions; a.obs = (R*)obs; a.reward = (R*)reward; a.done = done; a.trunc = trunc; a.trunc_id = tid;
     a.noise = noise; a.info = (R*)info; a.reward_sum = (R*)reward_sum;
@@ -1793,8 +1801,6 @@ __global__ __launch_bounds__(kBlock) void k_live_init(int32_t* list, uint32_t* c
     if (i < 3) cnt[i] = i == 0 ? (uint32_t)n : 0u;
 }
 
-int policy_fuse();
-
 template <typename R>
 pd_status rollout_policy_impl(pd_env* e, const float* w, int32_t max_steps, void* fitness, int32_t* steps,
                               int32_t check_every, hipStream_t s) {
@@ -1818,24 +1824,23 @@ pd_status rollout_policy_impl(pd_env* e, const float* w, int32_t max_steps, void
     // state and actor weights through the list (gathers) only costs.  PDENV_COMPACT=0/1 forces.
     int dev_cus = 256;
     (void)hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, e->device);
-    const char* force = getenv("PDENV_COMPACT");
-    a.use_list = force && *force ? (atoi(force) != 0) : (N * policy_lpe() > (int64_t)dev_cus * 512);
+    const int plpe = e->tune.policy_lanes;
+    a.use_list = e->tune.policy_list >= 0 ? e->tune.policy_list : (N * plpe > (int64_t)dev_cus * 512);
     // every launch appends its survivors to the next list, so the rollout can switch to the list
-    // at any launch: once the live count read back falls to PDENV_COMPACT_AT x N (experiments;
-    // default off), the waves of the later launches hold live envs only
-    const char* cat = getenv("PDENV_COMPACT_AT");
-    const double compact_at = cat && *cat ? atof(cat) : 0.0;
+    // at any launch: once the live count read back falls to policy_list_at x N (default off), the
+    // waves of the later launches hold live envs only
+    const double compact_at = e->tune.policy_list_at;
     // the list launches' parameter copy (policy_wc): [P][N] floats, made at the first rollout
     if (!e->pol_wc) {
         PD_HIP(hipMalloc((void**)&e->pol_wc, (size_t)PD_ACTOR_PARAMS_LANDING_BURN * (size_t)N * sizeof(float)));
         e->allocs.push_back(e->pol_wc);
     }
-    a.policy_wc = getenv("PDENV_NO_WCOPY") ? nullptr : e->pol_wc;   // (experiments: gathered per step)
+    a.policy_wc = e->pol_wc;
     int64_t n_launch = N;
     int checks = 0;
     // F policy steps per launch (an episode that ends inside a launch is stored at its last step
     // and its lanes freeze); the live list is compacted once per launch
-    const int F = policy_fuse();
+    const int F = e->tune.policy_fuse;
     const int check_launches = check_every > 0 ? std::max(1, check_every / F) : 0;
     int32_t t = 0;
     for (int l = 0; t < max_steps; ++l) {
@@ -1843,8 +1848,8 @@ pd_status rollout_policy_impl(pd_env* e, const float* w, int32_t max_steps, void
         t += a.n_fused;
         a.list_in = e->live[l & 1]; a.list_out = e->live[(l + 1) & 1];
         a.cnt_in = e->live_cnt + l % 3; a.cnt_out = e->live_cnt + (l + 1) % 3; a.cnt_zero = e->live_cnt + (l + 2) % 3;
-        if (e->cfg.phase == PD_PHASE_PURE_THROTTLE) { if (wind) launch_policy<R, 0, true>(a, n_launch, s); else launch_policy<R, 0, false>(a, n_launch, s); }
-        else { if (wind) launch_policy<R, 1, true>(a, n_launch, s); else launch_policy<R, 1, false>(a, n_launch, s); }
+        if (e->cfg.phase == PD_PHASE_PURE_THROTTLE) { if (wind) launch_policy<R, 0, true>(plpe, a, n_launch, s); else launch_policy<R, 0, false>(plpe, a, n_launch, s); }
+        else { if (wind) launch_policy<R, 1, true>(plpe, a, n_launch, s); else launch_policy<R, 1, false>(plpe, a, n_launch, s); }
         PD_HIP(hipGetLastError());
         if (F >= 16 || (l & (16 / F - 1)) == 16 / F - 1) launch_insert<R>(e, s);
         if (check_launches > 0 && (l + 1) % check_launches == 0 && t < max_steps) {
@@ -1867,36 +1872,23 @@ pd_status rollout_policy_impl(pd_env* e, const float* w, int32_t max_steps, void
     return PD_OK;
 }
 
-// Policy steps per fused policy-rollout launch (PDENV_PFUSE overrides; a power of two <= 64).
-// A wave whose episodes have all ended leaves its launch (PD_POL_EXIT), so a longer launch costs
-// no frozen steps at the swarm's tail; it saves launches, their table staging and the count
-// checks between them (c4: 8 -> 1.66, 16 -> 1.57, 32 -> 1.53-1.57, 64 -> 1.49-1.50 ms per generation,
-// profiles/r04_exp_s16_pol_exit.jsonl, r04_exp_s17_pfuse.jsonl)
-int policy_fuse() {
-    const char* s = getenv("PDENV_PFUSE");
-    int k = s && *s ? atoi(s) : 64;
-    int f = 1;
-    while (f * 2 <= k && f < 64) f *= 2;
-    return f;
-}
+// Launch tuning defaults (pd_tuning).  policy_fuse 64: a wave whose episodes have all ended leaves
+// its launch, so a longer launch costs no frozen steps at the swarm's tail; it saves launches,
+// their table staging and the count checks between them (c4: 8 -> 1.66, 16 -> 1.57, 32 ->
+// 1.53-1.57, 64 -> 1.49-1.50 ms per generation, profiles/r04_exp_s16_pol_exit.jsonl,
+// r04_exp_s17_pfuse.jsonl).  step_fuse 128: the miss flush runs between launches, so a
+// neighbourhood solved on device is re-solved at most this many steps before it is in the tables
+// (c3 ms per env-step, payload sums: 16 -> 0.0450, 32 -> 0.0442, 64 -> 0.0421; cell pieces: 64 ->
+// 0.0341, 128 -> 0.0335, 256 -> 0.0337).
 
-// Steps per fused launch: the miss flush runs between launches, so a neighbourhood solved on
-// device is re-solved at most this many steps before it is in the tables (PDENV_FUSE overrides).
-int fuse_chunk() {
-    const char* s = getenv("PDENV_FUSE");
-    int k = s && *s ? atoi(s) : 128;   // (c3 ms per env-step, payload sums: 16 -> 0.0450, 32 -> 0.0442, 64 -> 0.0421;
-                                       //  cell pieces: 64 -> 0.0341, 128 -> 0.0335, 256 -> 0.0337)
-    return k < 1 ? 1 : (k > 256 ? 256 : k);
-}
-
-// n_steps env-steps in launches of fuse_chunk() fused steps, each followed by the miss flush.
+// n_steps env-steps in launches of pd_tuning.step_fuse fused steps, each followed by the miss flush.
 // Row t of every [n_steps][N...] array belongs to step t; NULL outputs are not written.
 pd_status step_n_impl(pd_env* e, const void* actions, int32_t n_steps, void* obs, void* reward, uint8_t* done,
                       uint8_t* trunc, int8_t* tid, void* reward_sum, hipStream_t s) {
     const size_t N = (size_t)e->cfg.n_envs;
     const size_t sa = N * e->act_dim * (e->cfg.action_f64 ? 8 : 4), so = N * e->obs_dim * e->rsize;
     const size_t sr = N * e->rsize;
-    const int K = fuse_chunk();
+    const int K = e->tune.step_fuse;
     for (int32_t t = 0; t < n_steps; t += K) {
         const int k = n_steps - t < K ? n_steps - t : K;
         auto at = [&](void* p, size_t stride) { return p ? (void*)((char*)p + stride * t) : nullptr; };
@@ -2011,7 +2003,6 @@ pd_status pd_create(const pd_params* params, const pd_config* cfg, pd_env** out)
     //  32 768: LPE 2 0.0263, 4 0.0352; 65 536: LPE 2
     e->lpe = cfg->lanes_per_env != 0 ? cfg->lanes_per_env
                                      : (cfg->n_envs <= 4096 ? 16 : (cfg->n_envs <= 8192 ? 8 : 2));
-    if (const char* lv = getenv("PDENV_LPE"); lv && *lv && cfg->lanes_per_env == 0) e->lpe = atoi(lv);   // experiments
     if (e->lpe != 1 && e->lpe != 2 && e->lpe != 4 && e->lpe != 8 && e->lpe != 16) { delete e; return fail(PD_ERR_INVALID, "lanes_per_env must be 0, 1, 2, 4, 8 or 16"); }
     if (cfg->integrator == PD_INTEG_RK4) e->lpe = e->lpe <= 2 ? 2 : 16;   // the RK4 instantiations
     st = cfg->precision == PD_F64 ? create_impl<double>(params, cfg, e) : create_impl<float>(params, cfg, e);
@@ -2027,6 +2018,26 @@ pd_status pd_destroy(pd_env* e) {
     if (e->host_cnt) (void)hipHostFree(e->host_cnt);
     for (hipEvent_t ev : e->cnt_ev) if (ev) (void)hipEventDestroy(ev);
     delete e;
+    return PD_OK;
+}
+
+pd_status pd_set_tuning(pd_env* e, const pd_tuning* t) {
+    if (!e || !t) return fail(PD_ERR_INVALID, "pd_set_tuning: null env/tuning");
+    const int pf = t->policy_fuse;
+    if (t->step_fuse < 1 || t->step_fuse > 256) return fail(PD_ERR_INVALID, "pd_set_tuning: step_fuse must be 1..256");
+    if (pf < 1 || pf > 64 || (pf & (pf - 1))) return fail(PD_ERR_INVALID, "pd_set_tuning: policy_fuse must be a power of two 1..64");
+    if (t->policy_lanes != 2 && t->policy_lanes != 4 && t->policy_lanes != 8)
+        return fail(PD_ERR_INVALID, "pd_set_tuning: policy_lanes must be 2, 4 or 8");
+    if (t->policy_list < -1 || t->policy_list > 1) return fail(PD_ERR_INVALID, "pd_set_tuning: policy_list must be -1, 0 or 1");
+    if (!(t->policy_list_at >= 0.0 && t->policy_list_at <= 1.0))
+        return fail(PD_ERR_INVALID, "pd_set_tuning: policy_list_at must be in [0, 1]");
+    e->tune = *t;
+    return PD_OK;
+}
+
+pd_status pd_get_tuning(const pd_env* e, pd_tuning* t) {
+    if (!e || !t) return fail(PD_ERR_INVALID, "pd_get_tuning: null env/tuning");
+    *t = e->tune;
     return PD_OK;
 }
 
@@ -2103,18 +2114,24 @@ pd_status pd_step_sac_ring(pd_env* e, const float* heads, int32_t deterministic,
                             (hipStream_t)stream, 1, &io);
 }
 
-pd_status pd_step_sac_fused(pd_env* e, int32_t hidden, int32_t n_hidden_layers, const float* const* params,
-                            float* heads, int32_t deterministic, float log_std_min, float log_std_max, float max_action,
-                            float* eps_out, float* action, float* ring, int64_t capacity, long long* ring_state,
-                            float* priorities, const float* max_priority, float* obs32, void* stream) {
+pd_status pd_step_sac_fused(pd_env* e, int32_t state_dim, int32_t action_dim, int32_t hidden, int32_t n_hidden_layers,
+                            const float* const* params, float* heads, int32_t deterministic, float log_std_min,
+                            float log_std_max, float max_action, float* eps_out, float* action, float* ring,
+                            int64_t capacity, long long* ring_state, float* priorities, const float* max_priority,
+                            float* obs32, void* stream) {
     if (!e || !params || !obs32) return fail(PD_ERR_INVALID, "pd_step_sac_fused: null env/params/obs32");
     const int S = e->obs_dim, A = e->act_dim;
+    // the actor's widths must be the handle's: its weights are read with the handle's row strides
+    if (state_dim != S || action_dim != A)
+        return fail(PD_ERR_INVALID, "pd_step_sac_fused: the actor's state_dim / action_dim differ from the handle's");
     if (n_hidden_layers < 1 || n_hidden_layers > kSacMaxLayers || A > 8 || S > 16)
         return fail(PD_ERR_INVALID, "pd_step_sac_fused: 1..8 hidden layers, state_dim <= 16, action_dim <= 8");
     if (hidden != 128 && hidden != 256 && hidden != 512)
         return fail(PD_ERR_UNSUPPORTED, "pd_step_sac_fused: hidden width 128, 256 or 512 only");
-    for (int k = 0; k < 2 * (n_hidden_layers + 2); ++k)
+    for (int k = 0; k < 2 * (n_hidden_layers + 2); ++k) {
         if (!params[k]) return fail(PD_ERR_INVALID, "pd_step_sac_fused: null parameter");
+        if ((uintptr_t)params[k] % 16 != 0) return fail(PD_ERR_UNSUPPORTED, "pd_step_sac_fused: parameter not 16-byte aligned");
+    }
     // one launch where the workgroup's envs are one MLP tile (16 lanes per env) and the tile's
     // activations fit the kernel's LDS (hidden <= 256); else pd_sac_actor into `heads` (or the
     // handle's scratch rows) and pd_step_sac_ring: two launches, the same heads bit for bit
@@ -2285,14 +2302,6 @@ pd_status pd_counters(pd_env* e, int64_t* misses, int64_t* ecd, int64_t* ecl, in
     PD_HIP(hipSetDevice(e->device));
     unsigned long long st[kStats];
     PD_HIP(hipMemcpy(st, e->pend.stats, sizeof(st), hipMemcpyDeviceToHost));
-    if (getenv("PDENV_DEBUG_COUNTERS")) {
-        fprintf(stderr, "[pdenv] knn calls %llu line-candidates %llu iterations %llu probes %llu\n", st[4], st[5], st[6], st[7]);
-        if (st[15])
-            fprintf(stderr, "[pdenv] k_step wave clocks (mean per wave): staging %.0f loads %.0f pre-aero %.0f aero %.0f "
-                    "post-aero %.0f rtd %.0f outputs %.0f (waves %llu)\n", (double)st[8] / st[15], (double)st[9] / st[15],
-                    (double)st[10] / st[15], (double)st[11] / st[15], (double)st[12] / st[15], (double)st[13] / st[15],
-                    (double)st[14] / st[15], st[15]);
-    }
     if (misses) *misses = (int64_t)st[0];
     if (nans) *nans = (int64_t)st[1];
     if (ecd) *ecd = (int64_t)st[2];

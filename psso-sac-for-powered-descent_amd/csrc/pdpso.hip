@@ -14,7 +14,7 @@
 // pd_rollout_policy reads.  HBM-bound: 52 B per (particle, parameter).
 #include <hip/hip_runtime.h>
 
-#include <mutex>
+
 
 #include "../../include/pdenv.h"
 #include "pd_common.h"
@@ -171,14 +171,6 @@ namespace pd {
 pd_status set_error(pd_status s, const char* m);   // pdenv.hip: the pd_last_error() message
 }
 
-namespace {
-// pd_pso_swarm_minima's pass-1 partials, per device
-constexpr int kMaxDevices = 64;
-struct MinScratch { double* f = nullptr; int64_t* i = nullptr; size_t cap = 0; };
-std::mutex g_min_mu;
-MinScratch g_min[kMaxDevices];
-}  // namespace
-
 extern "C" {
 
 pd_status pd_pso_step(int64_t n_particles, int32_t dim, const double* fitness, double* best_fitness, double* position,
@@ -199,37 +191,30 @@ pd_status pd_pso_step(int64_t n_particles, int32_t dim, const double* fitness, d
     return PD_OK;
 }
 
+size_t pd_pso_swarm_minima_scratch_bytes(int64_t n_particles, int32_t n_swarms) {
+    const int64_t G = n_particles > 0 ? (n_particles + kMinChunk - 1) / kMinChunk : 1;
+    return (size_t)G * (size_t)(n_swarms > 0 ? n_swarms : 1) * (sizeof(double) + sizeof(int64_t));
+}
+
 pd_status pd_pso_swarm_minima(int64_t n_particles, int32_t dim, int32_t n_swarms, const double* fitness,
                               const int32_t* swarm, const double* position, double* min_fitness, double* min_position,
-                              void* stream) {
+                              void* scratch, size_t scratch_bytes, void* stream) {
     if (n_particles < 0 || dim <= 0 || n_swarms <= 0 || n_swarms > 65535 || !min_fitness || !min_position ||
         (n_particles > 0 && (!fitness || !swarm || !position)))
         return set_error(PD_ERR_INVALID, "pd_pso_swarm_minima: bad arguments");
+    // pass-1 partials in the caller's scratch: [G][n_swarms] doubles, then [G][n_swarms] indices
     const int64_t G = (n_particles + kMinChunk - 1) / kMinChunk;
-    // pass-1 partials: a per-device scratch grown on demand (calls on one device are stream-ordered
-    // by the caller; the PSO driver issues them on one stream)
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices)
-        return set_error(PD_ERR_HIP, "pd_pso_swarm_minima: no device");
-    const size_t need = (size_t)(G > 0 ? G : 1) * (size_t)n_swarms;
-    {
-        std::lock_guard<std::mutex> lk(g_min_mu);
-        MinScratch& m = g_min[dev];
-        if (m.cap < need) {
-            if (m.f) { (void)hipFree(m.f); (void)hipFree(m.i); m.f = nullptr; m.i = nullptr; m.cap = 0; }
-            if (hipMalloc((void**)&m.f, need * sizeof(double)) != hipSuccess ||
-                hipMalloc((void**)&m.i, need * sizeof(int64_t)) != hipSuccess)
-                return set_error(PD_ERR_HIP, "pd_pso_swarm_minima: scratch allocation failed");
-            m.cap = need;
-        }
-    }
-    MinScratch& m = g_min[dev];
+    const size_t need = pd_pso_swarm_minima_scratch_bytes(n_particles, n_swarms);
+    if (!scratch || scratch_bytes < need || (uintptr_t)scratch % 8 != 0)
+        return set_error(PD_ERR_INVALID, "pd_pso_swarm_minima: scratch missing, too small or misaligned");
+    double* part_f = (double*)scratch;
+    int64_t* part_i = (int64_t*)((char*)scratch + (size_t)(G > 0 ? G : 1) * (size_t)n_swarms * sizeof(double));
     hipStream_t s = (hipStream_t)stream;
     if (G > 0)
         hipLaunchKernelGGL(k_swarm_minima_part, dim3((unsigned)G), dim3(kPsoBlock), 0, s, n_particles, n_swarms,
-                           fitness, swarm, m.f, m.i);
+                           fitness, swarm, part_f, part_i);
     hipLaunchKernelGGL(k_swarm_minima_final, dim3((unsigned)n_swarms), dim3(kPsoBlock), 0, s, n_particles, dim,
-                       n_swarms, G, m.f, m.i, position, min_fitness, min_position);
+                       n_swarms, G, part_f, part_i, position, min_fitness, min_position);
     if (hipGetLastError() != hipSuccess) return set_error(PD_ERR_HIP, "pd_pso_swarm_minima: launch failed");
     return PD_OK;
 }

@@ -47,6 +47,9 @@ pd_status pd_sac_actor(int64_t n, int32_t state_dim, int32_t hidden, int32_t n_h
     a.wm = params[2 * n_hidden_layers]; a.bm = params[2 * n_hidden_layers + 1];
     a.ws = params[2 * n_hidden_layers + 2]; a.bs = params[2 * n_hidden_layers + 3];
     if (!a.wm || !a.bm || !a.ws || !a.bs) return pd::set_error(PD_ERR_INVALID, "pd_sac_actor: null head parameter");
+    // the hidden layers' weights are read as 16-byte vectors (sac_mlp_tile)
+    for (int k = 0; k < 2 * (n_hidden_layers + 2); ++k)
+        if ((uintptr_t)params[k] % 16 != 0) return pd::set_error(PD_ERR_UNSUPPORTED, "pd_sac_actor: parameter not 16-byte aligned");
     const dim3 grid((unsigned)((n + kSacTile - 1) / kSacTile));
     hipStream_t s = (hipStream_t)stream;
     switch (hidden) {

@@ -77,7 +77,17 @@ class PdConfig(C.Structure):
                 ("seed", U64), ("env_offset", U64), ("enable_wind", I32), ("stochastic_wind", I32),
                 ("wind_percentile", I32), ("auto_reset", I32), ("tilt_sigma_rad", D),
                 ("action_f64", I32), ("lanes_per_env", I32),
-                ("dt", D), ("discount_factor", D), ("trajectory_length", I32), ("integrator", I32)]
+                ("dt", D), ("discount_factor", D), ("trajectory_length", I32), ("integrator", I32),
+                ("table_flags", I32), ("pad3", I32)]
+
+
+# pd_table_flags
+TABLES_NO_CELL_PIECES, TABLES_NO_FINE_INDEX, TABLES_EXACT_ATMOSPHERE, TABLES_VERBOSE = 1, 2, 4, 8
+
+
+class PdTuning(C.Structure):
+    _fields_ = [("step_fuse", I32), ("policy_fuse", I32), ("policy_lanes", I32), ("policy_list", I32),
+                ("policy_list_at", D)]
 
 
 EXPORTS = ["pd_abi_version", "pd_sizeof_params", "pd_sizeof_config", "pd_last_error", "pd_device_count", "pd_create",
@@ -87,8 +97,9 @@ EXPORTS = ["pd_abi_version", "pd_sizeof_params", "pd_sizeof_config", "pd_last_er
            "pd_set_wind_state", "pd_get_counters", "pd_set_counters", "pd_checkpoint_size", "pd_checkpoint_save",
            "pd_checkpoint_load", "pd_counters", "pd_stats", "pd_count_work", "pd_atmosphere", "pd_obs_dim",
            "pd_action_dim", "pd_step_sac", "pd_pso_swarm_minima", "pd_pso_update_bests", "pd_cell_piece_info",
-           "pd_step_sac_ring", "pd_sac_actor", "pd_step_sac_fused", "pd_atm_table"]
-ABI_VERSION = 8
+           "pd_step_sac_ring", "pd_sac_actor", "pd_step_sac_fused", "pd_atm_table", "pd_set_tuning", "pd_get_tuning",
+           "pd_pso_swarm_minima_scratch_bytes"]
+ABI_VERSION = 9
 
 _lib = None
 
@@ -120,12 +131,17 @@ def load(path=None):
     L.pd_step_sac.argtypes = [vp, vp, vp, I32, vp, F32, F32, F32, vp, vp, vp, vp]
     L.pd_step_sac_ring.argtypes = [vp, vp, I32, F32, F32, F32, vp, vp, vp, I64, vp, vp, vp, vp, vp]
     L.pd_sac_actor.argtypes = [I64, I32, I32, I32, I32, vp, vp, vp, vp]
-    L.pd_step_sac_fused.argtypes = [vp, I32, I32, vp, vp, I32, F32, F32, F32, vp, vp, vp, I64, vp, vp, vp, vp, vp]
+    L.pd_step_sac_fused.argtypes = [vp, I32, I32, I32, I32, vp, vp, I32, F32, F32, F32, vp, vp, vp, I64, vp, vp, vp,
+                                    vp, vp]
+    L.pd_set_tuning.argtypes = [vp, P(PdTuning)]
+    L.pd_get_tuning.argtypes = [vp, P(PdTuning)]
     L.pd_rollout.argtypes = [vp, vp, I32, vp, vp]
     L.pd_rollout_policy.argtypes = [vp, vp, I32, I32, vp, vp, I32, vp]
     L.pd_pso_step.argtypes = [I64, I32, vp, vp, vp, vp, vp, vp, vp, vp, vp, C.c_double, C.c_double, C.c_double,
                               U64, C.c_uint32, U64, vp, vp]
-    L.pd_pso_swarm_minima.argtypes = [I64, I32, I32, vp, vp, vp, vp, vp, vp]
+    L.pd_pso_swarm_minima.argtypes = [I64, I32, I32, vp, vp, vp, vp, vp, vp, C.c_size_t, vp]
+    L.pd_pso_swarm_minima_scratch_bytes.argtypes = [I64, I32]
+    L.pd_pso_swarm_minima_scratch_bytes.restype = C.c_size_t
     L.pd_pso_update_bests.argtypes = [I32, I32, vp, vp, vp, vp, vp, vp, vp]
     L.pd_observe.argtypes = [vp, vp, vp]
     L.pd_flush_misses.argtypes = [vp, vp]
@@ -157,7 +173,9 @@ def load(path=None):
                  "pd_set_wind_sigmas", "pd_set_gload_window", "pd_counters", "pd_stats", "pd_count_work",
                  "pd_get_gload_window",
                  "pd_get_wind_state", "pd_set_wind_state", "pd_get_counters", "pd_set_counters",
-                 "pd_checkpoint_save", "pd_checkpoint_load", "pd_atmosphere", "pd_cell_piece_info"):
+                 "pd_checkpoint_save", "pd_checkpoint_load", "pd_atmosphere", "pd_cell_piece_info",
+                 "pd_step_sac_ring", "pd_sac_actor", "pd_step_sac_fused", "pd_atm_table", "pd_set_tuning",
+                 "pd_get_tuning"):
         getattr(L, name).restype = C.c_int
     L.pd_sizeof_params.restype = C.c_size_t
     L.pd_sizeof_config.restype = C.c_size_t

@@ -41,7 +41,7 @@ class PoweredDescentEnv:
                  device=0, enable_wind=False, stochastic_wind=False, wind_percentile=50,
                  auto_reset=False, tilt_sigma_rad=0.0, seed=0, env_offset=0, action_f64=False,
                  params=None, lanes_per_env=0, dt=0.0, discount_factor=0.99, trajectory_length=100,
-                 integrator="reference"):
+                 integrator="reference", table_flags=0):
         # integrator "rk4": NOT the reference's (semi-implicit Euler) -- BASELINE config c2's
         # "RK4 dt=0.01 s", pure throttle without wind only; see include/pdenv.h pd_integrator
         if flight_phase not in PHASES:
@@ -86,6 +86,7 @@ class PoweredDescentEnv:
         if integrator not in INTEGRATORS:
             raise ValueError(f"integrator must be one of {list(INTEGRATORS)} (got {integrator!r})")
         cfg.integrator = INTEGRATORS[integrator]
+        cfg.table_flags = int(table_flags)   # pd_table_flags (L.TABLES_*): 0 = the defaults
         self.integrator = integrator
         self.cfg = cfg
         handle = C.c_void_p()
@@ -195,22 +196,42 @@ class PoweredDescentEnv:
                                           _ptr(max_priority), _ptr(obs32), _stream(self.device)))
         self._steps += 1
 
-    def step_sac_fused(self, hidden, n_hidden_layers, params, log_std_min=-20.0, log_std_max=2.0, max_action=1.0,
+    def step_sac_fused(self, state_dim, action_dim, hidden, n_hidden_layers, params, log_std_min=-20.0, log_std_max=2.0, max_action=1.0,
                        deterministic=False, ring=None, capacity=0, ring_state=None, priorities=None,
                        max_priority=None, action=None, obs32=None, eps_out=None, heads=None):
         """The whole SAC collection step in one launch (pd_step_sac_fused): the actor's forward pass
         in the step kernel's prologue on obs32 [N, S] (the observation the previous step left
         there), then step_sac_ring's sampling, env step and transition rows, and the next
         observation back into obs32.  params: a ctypes array of the actor's 2 (n_hidden_layers +
-        2) parameter pointers (pd_sac_actor's order); heads [N, 2A] receives the heads if given.
+        2) parameter pointers (pd_sac_actor's order) of an actor with state_dim inputs and action_dim
+        outputs (the library refuses widths other than the handle's); heads [N, 2A] receives the
+        heads if given.
         Handles that do not step 16 lanes per env run the actor as its own launch (same bits).
         No copies, allocations or syncs."""
-        L.check(self.lib.pd_step_sac_fused(self.h, int(hidden), int(n_hidden_layers), params, _ptr(heads),
+        L.check(self.lib.pd_step_sac_fused(self.h, int(state_dim), int(action_dim), int(hidden), int(n_hidden_layers),
+                                           params, _ptr(heads),
                                            int(bool(deterministic)), float(log_std_min), float(log_std_max),
                                            float(max_action), _ptr(eps_out), _ptr(action), _ptr(ring), int(capacity),
                                            _ptr(ring_state), _ptr(priorities), _ptr(max_priority), _ptr(obs32),
                                            _stream(self.device)))
         self._steps += 1
+
+    def tuning(self):
+        """The handle's launch tuning (pd_get_tuning) as a dict."""
+        t = L.PdTuning()
+        L.check(self.lib.pd_get_tuning(self.h, C.byref(t)))
+        return {k: getattr(t, k) for k, _ in L.PdTuning._fields_}
+
+    def set_tuning(self, **kw):
+        """Change launch tuning fields (pd_set_tuning: step_fuse, policy_fuse, policy_lanes,
+        policy_list, policy_list_at); results never depend on them."""
+        cur = self.tuning()
+        bad = set(kw) - set(cur)
+        if bad:
+            raise ValueError(f"unknown tuning fields {sorted(bad)}")
+        cur.update(kw)
+        t = L.PdTuning(**cur)
+        L.check(self.lib.pd_set_tuning(self.h, C.byref(t)))
 
     def observe_raw(self):
         """pd_observe into the preallocated obs buffer (no copy); returns that buffer."""

@@ -101,8 +101,9 @@ class ParticleSubswarmOptimisationGPU:
 
     def __init__(self, flight_phase="landing_burn", pso_params=None, pop_size=None, enable_wind=False,
                  stochastic_wind=False, horiontal_wind_percentile=50, device=0, precision="f64", seed=0,
-                 dist=None, max_steps=2200):
+                 dist=None, max_steps=2200, tuning=None):
         self.flight_phase = flight_phase
+        self.tuning = dict(tuning or {})     # pd_tuning fields of the rollout handles (PoweredDescentEnv.set_tuning)
         self.p = dict(PSO_PARAMS[flight_phase])
         if pso_params:
             self.p.update(pso_params)
@@ -150,16 +151,22 @@ class ParticleSubswarmOptimisationGPU:
         self.gb_t = torch.zeros(self.D, dtype=torch.float64, device=self.device)
         self._cols = torch.arange(self.S, device=self.device)
         self.w = self.p["w_start"]
-        self.env = PoweredDescentEnv(self.P, self.flight_phase, **self.env_kw) if self.P > 0 else None
+        self.env = self._new_env(self.P) if self.P > 0 else None
         # share_information evaluates 1..S-1 moved subswarm bests: one handle of S - 1 envs made
         # here (creating a handle inside a generation costs tens of ms), candidates padded to it
-        self._aux = {self.S - 1: PoweredDescentEnv(self.S - 1, self.flight_phase, **self.env_kw)} if self.S > 1 else {}
+        self._aux = {self.S - 1: self._new_env(self.S - 1)} if self.S > 1 else {}
         self.last_fitness = None
         self._pending = None           # a share's candidates, evaluated with the next generation
         self._share_log = None
         self.share_history = []        # (generation, moved subswarms, their candidates' fitness)
         self._make_merged_handle()
         self._warm_share_path()
+
+    def _new_env(self, n):
+        env = PoweredDescentEnv(n, self.flight_phase, **self.env_kw)
+        if self.tuning:
+            env.set_tuning(**self.tuning)
+        return env
 
     def _mergeable(self):
         """share_information's candidates ride along with the next generation's rollout (S - 1 more
@@ -173,7 +180,7 @@ class ParticleSubswarmOptimisationGPU:
         for k in [k for k in self._aux if k not in (self.S - 1, n)]:   # (a merged handle of an earlier P)
             self._aux.pop(k).close()
         if self._mergeable() and n not in self._aux:
-            self._aux[n] = PoweredDescentEnv(n, self.flight_phase, **self.env_kw)
+            self._aux[n] = self._new_env(n)
 
     def _warm_share_path(self):
         """share_information's tensor operations once on scratch copies (no rng draws, no state
@@ -202,7 +209,7 @@ class ParticleSubswarmOptimisationGPU:
         if self.env is not None and self.env.n == n:
             return self.env
         if n not in self._aux:                                  # share_information's candidates
-            self._aux[n] = PoweredDescentEnv(n, self.flight_phase, **self.env_kw)
+            self._aux[n] = self._new_env(n)
         return self._aux[n]
 
     def evaluate(self, x32):
@@ -266,9 +273,12 @@ class ParticleSubswarmOptimisationGPU:
         torch.argmin over the ranks picks the lowest rank among equal minima)."""
         f = torch.empty(self.S, dtype=torch.float64, device=self.device)
         pos = torch.empty(self.S, self.D, dtype=torch.float64, device=self.device)
+        need = int(self.lib.pd_pso_swarm_minima_scratch_bytes(self.P, self.S))
+        if getattr(self, "_min_scratch", None) is None or self._min_scratch.numel() < need:
+            self._min_scratch = torch.empty(need, dtype=torch.uint8, device=self.device)   # the first pass's partials
         L.check(self.lib.pd_pso_swarm_minima(self.P, self.D, self.S, _ptr(fit) if self.P else None,
                                              _ptr(self.swarm) if self.P else None, _ptr(self.x) if self.P else None,
-                                             _ptr(f), _ptr(pos), _stream(self.device)))
+                                             _ptr(f), _ptr(pos), _ptr(self._min_scratch), need, _stream(self.device)))
         if self.dist:
             fa = [torch.empty_like(f) for _ in range(self.world)]
             pa = [torch.empty_like(pos) for _ in range(self.world)]
@@ -366,5 +376,5 @@ class ParticleSubswarmOptimisationGPU:
         self.P = int(sel.numel())
         if self.env is not None:
             self.env.close()
-        self.env = PoweredDescentEnv(self.P, self.flight_phase, **self.env_kw) if self.P > 0 else None
+        self.env = self._new_env(self.P) if self.P > 0 else None
         self._make_merged_handle()

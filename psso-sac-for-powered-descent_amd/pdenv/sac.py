@@ -69,7 +69,10 @@ class DeviceReplayBuffer:
         self.state_dev = torch.zeros(3, dtype=torch.int64, device=device)
 
     def _sync_state_dev(self):
-        self.state_dev.copy_(torch.tensor([self.position, self.size, 0], dtype=torch.int64))
+        # device-side fills (no host tensor, so no blocking pageable copy on the step's stream)
+        self.state_dev[0].fill_(self.position)
+        self.state_dev[1].fill_(self.size)
+        self.state_dev[2].zero_()
 
     def note_appended(self, b):
         """The host mirror of b rows appended on the device (pd_step_sac_ring)."""
@@ -220,7 +223,8 @@ class ActorKernel:
         ps = [p for m in lins for p in (m.weight, m.bias)] + list(actor.mean.parameters()) + list(actor.log_std.parameters())
         return (H in (128, 256, 512) and lins[0].in_features <= 16 and actor.mean.out_features <= 8
                 and all(m.in_features == H and m.out_features == H for m in lins[1:])
-                and all(p.dtype == torch.float32 and p.is_cuda and p.is_contiguous() for p in ps))
+                and all(p.dtype == torch.float32 and p.is_cuda and p.is_contiguous() and p.data_ptr() % 16 == 0
+                        for p in ps))
 
     def ptrs(self):
         """The parameter pointers as pd_sac_actor / pd_step_sac_fused take them (read now: an
@@ -310,7 +314,7 @@ class SACCollector:
                 kw.update(ring=self._slab_buf)
             if self.kernel is not None:
                 k = self.kernel
-                self.env.step_sac_fused(k.H, k.nl, k.ptrs(), a.log_std_min, a.log_std_max, a.max_action,
+                self.env.step_sac_fused(k.S, k.A, k.H, k.nl, k.ptrs(), a.log_std_min, a.log_std_max, a.max_action,
                                         heads=self.heads_out, **kw)
             else:
                 self.env.step_sac_ring(self._heads(), a.log_std_min, a.log_std_max, a.max_action, **kw)

@@ -29,9 +29,33 @@ def test_struct_layout_and_abi():
     import pdenv
     from pdenv import _lib
     L = pdenv.load()
-    assert L.pd_abi_version() == _lib.ABI_VERSION == 8
+    assert L.pd_abi_version() == _lib.ABI_VERSION == 9
     assert L.pd_sizeof_params() == C.sizeof(_lib.PdParams)
     assert L.pd_sizeof_config() == C.sizeof(_lib.PdConfig)
+
+
+def test_argument_checks_before_any_launch():
+    """Entry points refuse bad arguments before touching the device (callable without a GPU;
+    the pointers below are never dereferenced): a misaligned SAC actor parameter, a missing or
+    short pd_pso_swarm_minima scratch, a null handle's tuning."""
+    import pdenv
+    from pdenv import _lib
+    L = pdenv.load()
+    vp = C.c_void_p
+    params = (vp * 8)(*([0x10000] * 7 + [0x10004]))          # the last one 4-byte aligned only
+    st = L.pd_sac_actor(64, 2, 256, 2, 1, vp(0x10000), params, vp(0x10000), None)
+    assert st == _lib.PD_ERR_UNSUPPORTED and b"aligned" in L.pd_last_error()
+    params[7] = 0
+    assert L.pd_sac_actor(64, 2, 256, 2, 1, vp(0x10000), params, vp(0x10000), None) == _lib.PD_ERR_INVALID
+    need = L.pd_pso_swarm_minima_scratch_bytes(5000, 3)
+    assert need == 5 * 3 * 16                                  # 5 blocks of 1 024 particles x 3 subswarms
+    for scratch, nb in ((None, 0), (vp(0x10000), need - 8), (vp(0x10004), need)):
+        st = L.pd_pso_swarm_minima(5000, 10, 3, vp(0x10000), vp(0x10000), vp(0x10000), vp(0x10000), vp(0x10000),
+                                   scratch, nb, None)
+        assert st == _lib.PD_ERR_INVALID and b"scratch" in L.pd_last_error()
+    t = _lib.PdTuning(128, 64, 2, -1, 0.0)
+    assert L.pd_set_tuning(None, C.byref(t)) == _lib.PD_ERR_INVALID
+    assert L.pd_get_tuning(None, C.byref(t)) == _lib.PD_ERR_INVALID
 
 
 def test_no_gpu_create_fails_loudly():

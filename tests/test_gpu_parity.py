@@ -12,6 +12,7 @@ import numpy as np
 import pytest
 
 from conftest import golden
+from pdenv import _lib as L
 
 pytestmark = pytest.mark.gpu
 
@@ -147,12 +148,9 @@ def test_device_solve_bit_identical(pd, precision, lpe):
               wind_percentile=None, auto_reset=True, tilt_sigma_rad=0.02, seed=9)
     # payload sums only: with cell pieces (binary64, the default) interior queries of both handles
     # would take the pieces whatever the tables hold
-    os.environ["PDENV_CELL_PIECES"] = "0"
-    try:
-        full = make(pd, N, **kw)
-        cut = make(pd, N, params=pd.Params().restrict_keys(4, 4), **kw)
-    finally:
-        del os.environ["PDENV_CELL_PIECES"]
+    kw["table_flags"] = L.TABLES_NO_CELL_PIECES
+    full = make(pd, N, **kw)
+    cut = make(pd, N, params=pd.Params().restrict_keys(4, 4), **kw)
     for t in range(T):
         o1, r1, d1, *_ = full.step(A[t])
         o2, r2, d2, *_ = cut.step(A[t])
@@ -165,7 +163,7 @@ def test_device_solve_bit_identical(pd, precision, lpe):
 def test_cell_pieces_match_payload_sums(pd):
     """Binary64 handles evaluate trusted interior queries from cell pieces: the
     same first steps with the pieces (default) and with the payload sums only
-    (PDENV_CELL_PIECES=0) from the same seeded states, |alpha| mostly inside the interior band
+    (PD_TABLES_NO_CELL_PIECES) from the same seeded states, |alpha| mostly inside the interior band
     (pitch tilt sigma 0.002 rad): C_D and C_L agree to rounding (1e-12 relative) on the first
     step, the states to the per-step tolerance after it; the counting launches report the piece
     path taken."""
@@ -175,11 +173,7 @@ def test_cell_pieces_match_payload_sums(pd):
     A = torch.rand(T, N, 1, device="cuda", generator=g) * 0.5 + 0.5
     kw = dict(lanes_per_env=2, enable_wind=False, auto_reset=False, tilt_sigma_rad=0.002, seed=5)
     pc = make(pd, N, **kw)
-    os.environ["PDENV_CELL_PIECES"] = "0"
-    try:
-        ps = make(pd, N, **kw)
-    finally:
-        del os.environ["PDENV_CELL_PIECES"]
+    ps = make(pd, N, table_flags=L.TABLES_NO_CELL_PIECES, **kw)
     pc.count_work(True)
     for t in range(T):
         _, r1, _, _, x1 = pc.step(A[t], info=True)
@@ -201,7 +195,7 @@ def test_cell_pieces_match_payload_sums(pd):
 def test_fine_index_bit_identical(pd):
     """The fine index (one word per sub-cell naming the piece or bisector that settles the query,
     read in place of the cell record) picks the same piece as the cell / sub-cell records, so
-    with and without it (PDENV_FINE=0) the c3 workload -- wind, gusts below 15 km, tilt,
+    with and without it (PD_TABLES_NO_FINE_INDEX) the c3 workload -- wind, gusts below 15 km, tilt,
     auto-reset -- is bit-identical over 2 fused launches of 64 steps."""
     import torch
     N, T = 16384, 128
@@ -211,11 +205,7 @@ def test_fine_index_bit_identical(pd):
     kw = dict(lanes_per_env=2, enable_wind=True, stochastic_wind=True, wind_percentile=None,
               auto_reset=True, tilt_sigma_rad=0.02, seed=13)
     fine = make(pd, N, **kw)
-    os.environ["PDENV_FINE"] = "0"
-    try:
-        rec = make(pd, N, **kw)
-    finally:
-        del os.environ["PDENV_FINE"]
+    rec = make(pd, N, table_flags=L.TABLES_NO_FINE_INDEX, **kw)
     for t0 in range(0, T, 64):
         o1 = fine.step_n(A[t0:t0 + 64])
         o2 = rec.step_n(A[t0:t0 + 64])
@@ -228,7 +218,7 @@ def test_fine_index_cell_edge_margins(pd):
     """Queries placed a fraction of the 1e-9 trust margin inside an interior cell's Mach edge
     (2e-10 .. 8e-10 cell widths, both edges, 120 cells): the fine index applies the record
     path's margin in the coordinates the record path uses (cell coordinates for a non-refined
-    cell), so one step from these states is bit-identical with and without it (PDENV_FINE=0).
+    cell), so one step from these states is bit-identical with and without it (PD_TABLES_NO_FINE_INDEX).
     With the sub-cell margin on every word (round 3) the queries in (1.25e-10, 1e-9] cell widths
     of a non-refined cell's edge took its piece with the index and the payload sums without."""
     import torch
@@ -247,12 +237,8 @@ def test_fine_index_cell_edge_margins(pd):
     s[:, 4] = s[:, 6] - np.pi - ae                              # alpha_eff = gamma - theta - pi
     s[:, 7] = s[:, 4] - s[:, 6]
     outs = []
-    for fine in ("1", "0"):
-        os.environ["PDENV_FINE"] = fine
-        try:
-            env = make(pd, n, lanes_per_env=2)
-        finally:
-            del os.environ["PDENV_FINE"]
+    for flags in (0, L.TABLES_NO_FINE_INDEX):
+        env = make(pd, n, lanes_per_env=2, table_flags=flags)
         env.set_state(torch.tensor(s, device="cuda"))
         o = env.step(torch.zeros(n, 1, device="cuda"))
         outs.append((env.state.clone(), o[1].clone()))
@@ -592,7 +578,15 @@ def test_pso_swarm_minima_and_bests_vs_numpy(pd):
         T = {k: torch.tensor(v, device="cuda") for k, v in dict(fit=fit, sw=sw, x=x).items()}
         mf = torch.empty(S, dtype=torch.float64, device="cuda")
         mp = torch.empty(S, D, dtype=torch.float64, device="cuda")
-        L.check(lib.pd_pso_swarm_minima(P, D, S, _ptr(T["fit"]), _ptr(T["sw"]), _ptr(T["x"]), _ptr(mf), _ptr(mp), None))
+        nb = int(lib.pd_pso_swarm_minima_scratch_bytes(P, S))
+        scratch = torch.empty(nb, dtype=torch.uint8, device="cuda")
+        if trial == 0:   # the caller's scratch is checked: missing or too small is refused
+            assert lib.pd_pso_swarm_minima(P, D, S, _ptr(T["fit"]), _ptr(T["sw"]), _ptr(T["x"]), _ptr(mf), _ptr(mp),
+                                           None, 0, None) == L.PD_ERR_INVALID
+            assert lib.pd_pso_swarm_minima(P, D, S, _ptr(T["fit"]), _ptr(T["sw"]), _ptr(T["x"]), _ptr(mf), _ptr(mp),
+                                           _ptr(scratch), nb - 8, None) == L.PD_ERR_INVALID
+        L.check(lib.pd_pso_swarm_minima(P, D, S, _ptr(T["fit"]), _ptr(T["sw"]), _ptr(T["x"]), _ptr(mf), _ptr(mp),
+                                        _ptr(scratch), nb, None))
         sbf = torch.tensor(rng.normal(size=S), device="cuda"); sb = torch.tensor(rng.normal(size=(S, D)), device="cuda")
         gbf = torch.tensor(0.5, dtype=torch.float64, device="cuda"); gb = torch.zeros(D, dtype=torch.float64, device="cuda")
         sbf0, sb0 = sbf.cpu().numpy().copy(), sb.cpu().numpy().copy()
@@ -849,7 +843,7 @@ def test_sac_fused_step_equals_two_launches(pd, S, A, H, L, lpe):
             kw = dict(ring=buf.data, capacity=cap, ring_state=buf.state_dev, priorities=buf.priorities,
                       max_priority=buf.max_prio_dev, action=act, obs32=obs, eps_out=eps)
             if fused:
-                env.step_sac_fused(H, L, kern.ptrs(), actor.log_std_min, actor.log_std_max, actor.max_action,
+                env.step_sac_fused(S, A, H, L, kern.ptrs(), actor.log_std_min, actor.log_std_max, actor.max_action,
                                    heads=heads, **kw)
             else:
                 kern(obs, heads)
@@ -889,23 +883,23 @@ def test_sac_collector_graph_equals_eager(pd, deterministic):
     assert torch.equal(bufs[0].data, bufs[1].data)
 
 
-def test_policy_rollout_compaction_invariant(pd, monkeypatch):
+def test_policy_rollout_compaction_invariant(pd):
     """Done-mask compaction: the live-env list is rebuilt inside every launch and, with the list
-    in use (PDENV_COMPACT=1; by default only for grids larger than one chip round), later
+    in use (pd_tuning.policy_list 1; by default only for grids larger than one chip round), later
     launches are sized to the live count read back every check_every steps, each launch copying
     its envs' actor parameters into list order once (policy_wc).  Fitness, episode lengths and
     final states must be bit-identical with and without the list, with the list switched on
-    mid-rollout (PDENV_COMPACT_AT), whatever the check interval (0 = never), and equal to those of
-    envs stepped in their own handle (the order of the list is irrelevant)."""
+    mid-rollout (policy_list_at), whatever the check interval (0 = never) and the steps per launch,
+    and equal to those of envs stepped in their own handle (the order of the list is irrelevant)."""
     import torch
     rng = np.random.default_rng(77)
     W = np.concatenate([rng.uniform(-1.5, 1.5, (700, 372)), rng.uniform(-0.3, 0.3, (324, 372))]).astype(np.float32)
     env = make(pd, len(W), phase="landing_burn", mode="pso")
     res = []
-    for force, ce, at in (("0", 8, ""), ("1", 0, ""), ("1", 1, ""), ("1", 3, ""), ("1", 8, ""), ("1", 64, ""),
-                          ("", 8, ""), ("0", 8, "0.5"), ("0", 8, "0.05")):
-        monkeypatch.setenv("PDENV_COMPACT", force)
-        monkeypatch.setenv("PDENV_COMPACT_AT", at)     # (switched on mid-rollout at that live fraction)
+    for lst, ce, at, pf in ((0, 8, 0.0, 64), (1, 0, 0.0, 64), (1, 1, 0.0, 64), (1, 3, 0.0, 8), (1, 8, 0.0, 4),
+                            (1, 64, 0.0, 64), (-1, 8, 0.0, 64), (0, 8, 0.5, 8), (0, 8, 0.05, 2), (0, 8, 0.0, 1)):
+        # (policy_list_at: switched on mid-rollout at that live fraction)
+        env.set_tuning(policy_list=lst, policy_list_at=at, policy_fuse=pf)
         fit, steps = env.rollout_policy(torch.tensor(W), max_steps=300, check_every=ce)
         res.append((fit.cpu().numpy(), steps.cpu().numpy(), env.state.cpu().numpy()))
     for f, s, S in res[1:]:
@@ -1005,3 +999,52 @@ def test_step_n_fused_equals_step_loop(pd, phase, precision, lpe):
     # the reward-only fused rollout matches the per-step rewards' sum
     r2 = make(pd, N, phase=phase, **kw).rollout(A)
     torch.testing.assert_close(r2, rew.sum(0), rtol=1e-12 if precision == "f64" else 1e-5, atol=1e-9)
+
+
+def test_launcher_refuses_mismatched_inputs(pd):
+    """Every launch checks its inputs before any kernel runs (the round-4 fault class: a launch
+    reaching the plain step kernel with a NULL action pointer): a step without actions, a SAC
+    step without heads, a SAC launch on a handle with no SAC kernel, a fused SAC step whose actor
+    widths differ from the handle's or whose parameters are misaligned, out-of-range tuning.
+    Each is refused with its status and the handle steps on unharmed."""
+    import ctypes as C
+    import torch
+    from pdenv.env import _ptr
+    env = make(pd, 256, lanes_per_env=16)
+    lib, h = env.lib, env.h
+    vp = C.c_void_p
+    assert lib.pd_step(h, None, None, None, None, None, None, None, None, None) == L.PD_ERR_INVALID
+    assert lib.pd_step_n(h, None, 4, None, None, None, None, None, None) == L.PD_ERR_INVALID
+    assert lib.pd_step_sac(h, None, None, 0, None, -20.0, 2.0, 1.0, None, None, None, None) == L.PD_ERR_INVALID
+    assert lib.pd_step_sac_ring(h, None, 0, -20.0, 2.0, 1.0, None, None, None, 0, None, None, None, None,
+                                None) == L.PD_ERR_INVALID
+    pso = make(pd, 256, mode="pso")
+    heads = torch.zeros(256, 2, device="cuda")
+    assert pso.lib.pd_step_sac_ring(pso.h, _ptr(heads), 1, -20.0, 2.0, 1.0, None, None, None, 0, None, None, None,
+                                    None, None) == L.PD_ERR_UNSUPPORTED
+    # a 2-256-256-1 actor: the right widths step, wrong ones and a misaligned parameter do not
+    H, S, A = 256, env.obs_dim, env.action_dim
+    ts = [torch.zeros(H, S), torch.zeros(H), torch.zeros(H, H), torch.zeros(H), torch.zeros(A, H), torch.zeros(A),
+          torch.zeros(A, H), torch.zeros(A)]
+    ts = [t.cuda() for t in ts]
+    params = (vp * 8)(*[t.data_ptr() for t in ts])
+    obs32 = torch.zeros(256, S, device="cuda")
+    act = torch.zeros(256, A, device="cuda")
+
+    def fused(s, a, p):
+        return lib.pd_step_sac_fused(h, s, a, H, 2, p, None, 1, -20.0, 2.0, 1.0, None, _ptr(act), None, 0, None, None,
+                                     None, _ptr(obs32), None)
+    assert fused(S + 1, A, params) == L.PD_ERR_INVALID
+    assert fused(S, A + 1, params) == L.PD_ERR_INVALID
+    bad = torch.zeros(A * H + 1, device="cuda")
+    params2 = (vp * 8)(*([t.data_ptr() for t in ts[:6]] + [bad.data_ptr() + 4, ts[7].data_ptr()]))
+    assert fused(S, A, params2) == L.PD_ERR_UNSUPPORTED
+    L.check(fused(S, A, params))
+    for kw in (dict(step_fuse=0), dict(step_fuse=257), dict(policy_fuse=3), dict(policy_lanes=16), dict(policy_list=2),
+               dict(policy_list_at=1.5)):
+        with pytest.raises(L.PdError):
+            env.set_tuning(**kw)
+    assert env.tuning() == dict(step_fuse=128, policy_fuse=64, policy_lanes=2, policy_list=-1, policy_list_at=0.0)
+    env.step(torch.zeros(256, 1, device="cuda"))
+    torch.cuda.synchronize()
+    assert torch.isfinite(env.state).all()

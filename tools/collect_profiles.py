@@ -40,7 +40,7 @@ def main(tag="r01"):
     summary = json.load(open(prev)) if os.path.exists(prev) else {}
     summary["source"] = ("tools/gpu_session.sh stages prof/prof32/pmc/pmc32/pmcv on one MI355X; "
                          "workload = bench.py defaults (c3, 65536 envs, 16 env-steps per k_step launch)")
-    summary["env_steps_per_launch"] = int(os.environ.get("PDENV_FUSE", "16"))
+    summary["env_steps_per_launch"] = int(os.environ.get("FUSE", "16"))
     for prec, d in (("f64", "prof"), ("f32", "prof32")):
         src = os.path.join(OUT, d, "run_kernel_stats.csv")
         if os.path.exists(src):

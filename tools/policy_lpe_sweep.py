@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Lanes-per-env sweep of the c4 policy rollouts (pd_rollout_policy: fused actor + landing_burn
-env + done-mask compaction) at P particles, interleaved rounds in one process: PDENV_PLPE 2/4/8
+env + done-mask compaction) at P particles, interleaved rounds in one process: pd_tuning.policy_lanes 2/4/8
 (read by the library at every rollout).  The same swarm (U(-1.5, 1.5) per parameter, as
 initialize_swarms draws it) each time.  Prints one JSON line per LPE: median rollout ms, the mean
 episode length, and the largest fitness difference against LPE 2 (LPE 4/8 evaluate the tables by
@@ -27,7 +27,7 @@ def main():
     fits = {}
     for r in range(rounds + 1):
         for l in lpes:
-            os.environ["PDENV_PLPE"] = str(l)
+            env.set_tuning(policy_lanes=l)
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             fit, steps = env.rollout_policy(W)
@@ -35,7 +35,6 @@ def main():
             if r > 0:                        # round 0 warms the tables and the kernels
                 times[l].append((time.perf_counter() - t0) * 1e3)
             fits[l] = (fit.cpu().numpy(), steps.cpu().numpy())
-    os.environ.pop("PDENV_PLPE", None)
     f2 = fits[lpes[0]][0]
     for l in lpes:
         t = sorted(times[l])

@@ -3,7 +3,7 @@
 library named by PDENV_LIB (default the in-tree one): one JSON line with the event-timed k_step
 launch average, the wall ms per env-step and the step kernel's workload counters over the timed
 launches.  N, LAUNCHES, PREC, LPE, PHASE from the environment; DESCENT=1: the c3-descent action
-mix (bench.py c3_actions) after bench.py's burn-in."""
+mix (bench.py c3_actions) after bench.py's burn-in; BURN overrides the untimed burn-in steps."""
 import json
 import math
 import os
@@ -18,11 +18,10 @@ import pdenv  # noqa: E402
 n = int(os.environ.get("N", "65536"))
 launches = int(os.environ.get("LAUNCHES", "24"))
 F = int(os.environ.get("FUSE", "16"))
-os.environ["PDENV_FUSE"] = str(F)
 descent = os.environ.get("DESCENT") == "1"
 sys.path.insert(0, REPO)
 import bench  # noqa: E402
-burn = bench.DESCENT_BURN_IN if descent else 0
+burn = int(os.environ.get("BURN", bench.DESCENT_BURN_IN if descent else 0))
 phase = os.environ.get("PHASE", "landing_burn_pure_throttle")
 t_c = time.perf_counter()
 wind = os.environ.get("WIND", "1") == "1"      # WIND=0 TILT=0: the c2 workload (INTEG=rk4: its RK4 mode)
@@ -30,8 +29,10 @@ env = pdenv.PoweredDescentEnv(n, flight_phase=phase, mode="rl" if phase == "land
                               precision=os.environ.get("PREC", "f64"), enable_wind=wind, stochastic_wind=wind,
                               wind_percentile=None, auto_reset=True,
                               tilt_sigma_rad=math.radians(1.0) if os.environ.get("TILT", "1") == "1" else 0.0, seed=1234,
-                              lanes_per_env=int(os.environ.get("LPE", "0")), integrator=os.environ.get("INTEG", "reference"))
+                              lanes_per_env=int(os.environ.get("LPE", "0")), integrator=os.environ.get("INTEG", "reference"),
+                              table_flags=int(os.environ.get("TABLE_FLAGS", "0")))
 t_create = time.perf_counter() - t_c
+env.set_tuning(step_fuse=F)
 g = torch.Generator(device="cuda").manual_seed(42)
 acts = bench.c3_actions(burn + (launches + 8) * F, n, g, "cuda", descent)
 kw = dict(device="cuda")
@@ -63,7 +64,7 @@ w1 = env.stats()
 work = {k: w1[k] - w0[k] for k in env.WORK_COUNTERS}
 work["gust_steps_frac"] = work["gust_substeps"] / (n * launches * F * 4)
 print(json.dumps({"lib": os.path.basename(os.environ.get("PDENV_LIB", "libpdenv.so")), "n": n, "fuse": F,
-                  "lpe": int(os.environ.get("LPE", "0")), "wind": wind, "integrator": os.environ.get("INTEG", "reference"), "cell_pieces": os.environ.get("PDENV_CELL_PIECES", "1") != "0", "fine": os.environ.get("PDENV_FINE", "1") != "0", "line_pieces": os.environ.get("PDENV_LINE_PIECES", "1") != "0",
+                  "lpe": int(os.environ.get("LPE", "0")), "wind": wind, "integrator": os.environ.get("INTEG", "reference"), "table_flags": int(os.environ.get("TABLE_FLAGS", "0")),
                   "descent": descent, "work": work,
                   "launch_ms_avg": sum(ms) / len(ms), "launch_ms_med": ms[len(ms) // 2],
                   "ms_per_step": sum(ms) / len(ms) / F, "wall_ms_per_step": wall * 1e3 / (launches * F),

@@ -20,11 +20,11 @@ import pdenv  # noqa: E402
 import bench  # noqa: E402
 
 F = int(os.environ.get("FUSE", "64"))
-os.environ["PDENV_FUSE"] = str(F)
 descent = os.environ.get("DESCENT") == "1"
 n = 65536
 env = pdenv.PoweredDescentEnv(n, enable_wind=True, stochastic_wind=True, wind_percentile=None, auto_reset=True,
                               tilt_sigma_rad=math.radians(1.0), seed=1234)
+env.set_tuning(step_fuse=F)
 burn = bench.DESCENT_BURN_IN if descent else 32
 L = 6
 g = torch.Generator(device="cuda").manual_seed(42)
