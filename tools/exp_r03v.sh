@@ -1,8 +1,9 @@
 #!/bin/bash
 # Round-3 session v: the grid-fin C_a / C_n interval slopes tabulated in LDS at staging (the same
-# division on the same operands: same bits; tools/experiments/grid_fin_slopes.patch,
-# libpdenv_gfs.so): c3 shadow + parity GPU tests on the variant, then c3 / c3-descent at 128
-# env-steps per launch, base and variant, two rounds.
+# division on the same operands: same bits; libpdenv_gfs.so, built then from a patch that is gone:
+# the change was kept and is in the product source since round 3): c3 shadow +
+# parity GPU tests on the variant, then c3 / c3-descent at 128 env-steps per launch, base and
+# variant, two rounds.  (A record of the round-3 session; it cannot be re-run as is.)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
