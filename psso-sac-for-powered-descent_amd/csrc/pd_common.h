@@ -159,7 +159,7 @@ struct LogTable { double invc[kLogCells], logc[kLogCells]; };
 // second entry is scaled by 4 (exactly) so that the Horner steps run on 4 log1p and every FMA
 // has at most one non-inline constant (pd_physics.h log_cell_poly4).
 constexpr int kLogBitsD = 10, kLogCellsD = 1 << kLogBitsD;
-struct LogTableD { double cell[2 * kLogCellsD]; };
+struct alignas(16) LogTableD { double cell[2 * kLogCellsD]; };   // (16-byte aligned: the step kernel copies it with 16-byte loads)
 inline void log_table_fill(LogTableD& t) {
     for (int i = 0; i < kLogCellsD; ++i) {
         long double c = 1.0L + (i + 0.5L) / kLogCellsD;

@@ -149,6 +149,7 @@ template <typename R> struct DevParams {
     uint16_t line_lb[4][kLineBuckets];
     // Taylor pieces of the four lines in one array; tay_off[li]: the line's first piece, -1 none
     const R* tay;
+    const void* stage_img;   // StepStatic<R, wind> of the handle (pd_step.h): the LDS tables' image
     int tay_off[4];
     // 2-D candidate grids over the interior query domain (Mach x AoA-abscissa), one per table:
     // the key/slot of the 50-NN set at each cell centre

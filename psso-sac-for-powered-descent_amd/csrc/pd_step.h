@@ -9,6 +9,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <cstring>
+
 #include "../../include/pdenv.h"
 #include "pd_physics.h"
 #include "pd_sac_mlp.h"
@@ -111,6 +113,65 @@ struct WaveCount {
         if (w && __lane_id() == 0) w[k] += v;
     }
 };
+
+// the clamped query lines' breakpoints, interval keys/slots and search buckets (staged into LDS)
+template <typename R> struct LineLds {
+    R bp[4][kLineMax];
+    int slot[4][kLineMax + 1];
+    unsigned long long key[4][kLineMax + 1];
+    R a[4];
+    int nbp[4];
+    int tay_off[4];
+    uint16_t lb[4][kLineBuckets];
+};
+
+// The tables every step workgroup stages into LDS, in the layout of its LDS (StepLds derives from
+// it): the handle keeps an image of it in HBM (pd_create, fill_step_static) and the kernel
+// prologue copies it with 16-byte loads.
+template <typename R, bool WIND> struct alignas(16) StepStatic {
+    // table points as (Mach_p, Mach_p+1) entries, C_D's 256 then C_L's: one 16-byte LDS read per
+    // payload pair slot (smach[2p] is point p's Mach for the neighbourhood search)
+    alignas(16) R tab[1024];
+    R gf[256];                    // grid fins: ca_x, ca_y, cn_x, cn_y (64 each)
+    R gfs[128];                   // their interval slopes: C_a at the upper index, C_n at the lower
+    uint16_t ca_lb[64];           // C_a search buckets
+    R isa[9 * kIsaCols];          // ISA layers
+    R walt[WIND ? 800 : 1];       // wind profiles [50][16]: altitude km, speed
+    R wsp[WIND ? 800 : 1];
+    LineLds<R> lines;
+};
+
+// The image's contents from the handle's parameter block (host): what the kernel prologue staged
+// field by field before round 5, the same values; the grid-fin interval slopes are the division
+// grid_fin_ca / np_interp would do, on the same operands (IEEE on host and device: same bits)
+template <typename R, bool WIND> void fill_step_static(const DevParams<R>& P, StepStatic<R, WIND>& L) {
+    std::memset(&L, 0, sizeof(L));
+    for (int t = 0; t < 256; ++t) {
+        L.tab[2 * t] = P.cd_mach[t]; L.tab[2 * t + 1] = t < 255 ? P.cd_mach[t + 1] : R(0);
+        L.tab[512 + 2 * t] = P.cl_mach[t]; L.tab[513 + 2 * t] = t < 255 ? P.cl_mach[t + 1] : R(0);
+    }
+    for (int i = 0; i < 64; ++i) {
+        L.gf[i] = P.ca_x[i]; L.gf[64 + i] = P.ca_y[i]; L.gf[128 + i] = P.cn_x[i]; L.gf[192 + i] = P.cn_y[i];
+        L.ca_lb[i] = P.ca_lb[i];
+        // (entries past a table's end are never read)
+        L.gfs[i] = i >= 1 ? (P.ca_y[i] - P.ca_y[i - 1]) / (P.ca_x[i] - P.ca_x[i - 1]) : R(0);
+        L.gfs[64 + i] = i < 63 ? (P.cn_y[i + 1] - P.cn_y[i]) / (P.cn_x[i + 1] - P.cn_x[i]) : R(0);
+    }
+    for (int k = 0; k < 9; ++k) {
+        R* r = L.isa + k * kIsaCols;
+        r[0] = P.isa_Hb[k]; r[1] = P.isa_Tb[k]; r[2] = P.isa_beta[k]; r[3] = P.isa_pb[k];
+        r[4] = P.isa_bt[k]; r[5] = P.isa_ex[k]; r[6] = P.isa_iso[k]; r[7] = R(0);
+    }
+    if (WIND)
+        for (int t = 0; t < 800; ++t) { L.walt[t] = (&P.wind_alt_km[0][0])[t]; L.wsp[t] = (&P.wind_speed[0][0])[t]; }
+    for (int t = 0; t < 4 * kLineMax; ++t) (&L.lines.bp[0][0])[t] = (&P.line_bp[0][0])[t];
+    for (int t = 0; t < 4 * (kLineMax + 1); ++t) {
+        (&L.lines.slot[0][0])[t] = (&P.line_slot[0][0])[t];
+        (&L.lines.key[0][0])[t] = (&P.line_key[0][0])[t];
+    }
+    for (int k = 0; k < 4; ++k) { L.lines.a[k] = P.line_a[k]; L.lines.nbp[k] = P.line_nbp[k]; L.lines.tay_off[k] = P.tay_off[k]; }
+    for (int t = 0; t < 4 * kLineBuckets; ++t) (&L.lines.lb[0][0])[t] = (&P.line_lb[0][0])[t];
+}
 
 // ---------------------------------------------------------------- per-env device buffers
 template <typename R> struct EnvBufs {

@@ -71,15 +71,6 @@ template <typename R> struct TabView {
 };
 
 // LDS copy of the clamped-line interval tables
-template <typename R> struct LineLds {
-    R bp[4][kLineMax];
-    int slot[4][kLineMax + 1];
-    unsigned long long key[4][kLineMax + 1];
-    R a[4];
-    int nbp[4];
-    int tay_off[4];
-    uint16_t lb[4][kLineBuckets];
-};
 
 // One chunk (five pair slots, ten terms) of sum_j c_j phi(|x - y_j|), phi(r) = r^2 log r =
 // d2 log(d2) / 2 with d2 = |x - y|^2 (thin_plate_spline, phi(0) = 0), times 8: the lane-
@@ -1010,17 +1001,9 @@ __device__ __forceinline__ void actor_forward(const float* __restrict__ W, int64
 #endif
 
 // ---------------------------------------------------------------- LDS of one step workgroup
-template <typename R, bool WIND, int EPB, bool BAL = false> struct StepLds {
-    // table points as (Mach_p, Mach_p+1) entries, C_D's 256 then C_L's: one 16-byte LDS read per
-    // payload pair slot (smach[2p] is point p's Mach for the neighbourhood search)
-    alignas(16) R tab[1024];
-    R gf[256];                    // grid fins: ca_x, ca_y, cn_x, cn_y (64 each)
-    R gfs[128];                   // their interval slopes: C_a at the upper index, C_n at the lower
-    uint16_t ca_lb[64];           // C_a search buckets
-    R isa[9 * kIsaCols];          // ISA layers
-    R walt[WIND ? 800 : 1];       // wind profiles [50][16]: altitude km, speed
-    R wsp[WIND ? 800 : 1];
-    LineLds<R> lines;
+// (the tables every workgroup stages come first: StepStatic, pd_step.h, copied from the handle's
+// image of it)
+template <typename R, bool WIND, int EPB, bool BAL = false> struct StepLds : StepStatic<R, WIND> {
     R gwin[10][EPB];              // the g-load ring of each env of the workgroup (register-resident launches)
     uint32_t work[kStepBlock / 64][kNWork];   // per-wave workload counts (counting launches)
     double wnx[WIND ? 2 : 1][WIND ? kStepBlock : 1];   // each lane's gust normals of the next (odd) sub-step
@@ -1119,45 +1102,28 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(2)))
         }
     }
     {
+        // the static tables: one 16-byte vector copy of the handle's image of them (pdenv.hip
+        // fill_step_static: the same values, the grid-fin slopes by the same division), every load
+        // of a thread issued before its first store; then the eval_log cells
         DP<R>& P = *params<R>(a.P);
-        for (int t = threadIdx.x; t < 256; t += kStepBlock) {
-            L.tab[2 * t] = P.cd_mach[t]; L.tab[2 * t + 1] = t < 255 ? P.cd_mach[t + 1] : R(0);
-            L.tab[512 + 2 * t] = P.cl_mach[t]; L.tab[513 + 2 * t] = t < 255 ? P.cl_mach[t + 1] : R(0);
+        constexpr int kImg = (int)(sizeof(StepStatic<R, WIND>) / 16);
+        constexpr int kLog = (int)(sizeof(LogTableD) / 16);
+        constexpr int kPer = (kImg + kLog + kStepBlock - 1) / kStepBlock;
+        using V4 = __attribute__((ext_vector_type(4))) unsigned int;
+        const PD_AS1 V4* img = (const PD_AS1 V4*)P.stage_img;
+        const PD_AS1 V4* lgt = (const PD_AS1 V4*)(uint64_t)&P.logtab_d.cell[0];
+        V4 v[kPer];
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) {
+            const int t = threadIdx.x + k * kStepBlock;
+            if (t < kImg) v[k] = img[t];
+            else if (t < kImg + kLog) v[k] = lgt[t - kImg];
         }
-        if (threadIdx.x < 64) {
-            L.gf[threadIdx.x] = P.ca_x[threadIdx.x]; L.gf[64 + threadIdx.x] = P.ca_y[threadIdx.x];
-            L.gf[128 + threadIdx.x] = P.cn_x[threadIdx.x]; L.gf[192 + threadIdx.x] = P.cn_y[threadIdx.x];
-            L.ca_lb[threadIdx.x] = P.ca_lb[threadIdx.x];
-            // the slopes grid_fin_ca / np_interp would compute, the same operation on the same
-            // operands (same bits); entries past a table's end are never read
-            const int i = threadIdx.x;
-            L.gfs[i] = i >= 1 ? (P.ca_y[i] - P.ca_y[i - 1]) / (P.ca_x[i] - P.ca_x[i - 1]) : R(0);
-            L.gfs[64 + i] = i < 63 ? (P.cn_y[i + 1] - P.cn_y[i]) / (P.cn_x[i + 1] - P.cn_x[i]) : R(0);
-        }
-        if (threadIdx.x < 9) {
-            const int k = threadIdx.x;
-            R* r = L.isa + k * kIsaCols;
-            r[0] = P.isa_Hb[k]; r[1] = P.isa_Tb[k]; r[2] = P.isa_beta[k]; r[3] = P.isa_pb[k];
-            r[4] = P.isa_bt[k]; r[5] = P.isa_ex[k]; r[6] = P.isa_iso[k]; r[7] = R(0);
-        }
-        if constexpr (WIND) {
-            for (int t = threadIdx.x; t < 800; t += kStepBlock) {
-                L.walt[t] = (&P.wind_alt_km[0][0])[t];
-                L.wsp[t] = (&P.wind_speed[0][0])[t];
-            }
-        }
-        for (int t = threadIdx.x; t < 4 * kLineMax; t += kStepBlock) (&L.lines.bp[0][0])[t] = (&P.line_bp[0][0])[t];
-        for (int t = threadIdx.x; t < 4 * (kLineMax + 1); t += kStepBlock) {
-            (&L.lines.slot[0][0])[t] = (&P.line_slot[0][0])[t];
-            (&L.lines.key[0][0])[t] = (&P.line_key[0][0])[t];
-        }
-        if (threadIdx.x < 4) {
-            L.lines.a[threadIdx.x] = P.line_a[threadIdx.x]; L.lines.nbp[threadIdx.x] = P.line_nbp[threadIdx.x];
-            L.lines.tay_off[threadIdx.x] = P.tay_off[threadIdx.x];
-        }
-        for (int t = threadIdx.x; t < 4 * kLineBuckets; t += kStepBlock) (&L.lines.lb[0][0])[t] = (&P.line_lb[0][0])[t];
-        for (int t = threadIdx.x; t < 2 * kLogCellsD; t += kStepBlock) {
-            s_logtab[t] = P.logtab_d.cell[t];
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) {
+            const int t = threadIdx.x + k * kStepBlock;
+            if (t < kImg) ((V4*)static_cast<StepStatic<R, WIND>*>(&L))[t] = v[k];
+            else if (t < kImg + kLog) ((V4*)s_logtab)[t - kImg] = v[k];
         }
         if (threadIdx.x < (kStepBlock / 64) * kNWork) (&L.work[0][0])[threadIdx.x] = 0u;
         if (threadIdx.x < 2) L.tdesc[threadIdx.x] = tab_view<R>(P, L.tab, (int)threadIdx.x);
@@ -1303,8 +1269,22 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(2)))
     // sub-step, to the step's rtd after the last one, and on to the next step's first sub-step
     // unless the env reset (same y, vx, vy: bit-identical).  RK4: the rtd's only, carried to the
     // next step's first stage
-    R k_rho = R(0), k_patm = R(0), k_asnd = R(0), k_speed = R(0);
+    R k_rho = R(0), k_patm = R(0), k_asnd = R(0);
+    double k_speed = 0.0;
     bool k_have = false;
+    // The state chain of the sub-steps (position, velocity, pitch and its rate, flight-path angle,
+    // alpha, masses, time) is integrated in binary64 in both precisions: a binary32 handle computes
+    // its forces in binary32 but carries the chain in binary64 through the env-step (alpha_eff =
+    // gamma - theta - pi, rockets_physics.py:498-501, is the difference of two O(1) angles: formed
+    // from binary32 angles it lost ~1e-4 of itself, which the aerodynamic moment turned into
+    // theta_dot) and rounds it to binary32 once, at the env-step's end -- the stored state, so
+    // fused and per-step launches give the same bits.  Binary64 handles: xs is e.s itself.
+    using RS = double;
+    RS xs[sizeof(R) == 8 ? 1 : 11];
+    auto SV = [&](int k) -> RS& {
+        if constexpr (sizeof(R) == 8) return e.s[k];
+        else return xs[k];
+    };
 #pragma unroll 1
     for (int f = 0; f < nf; ++f) {
     SA<R>& a = kargs<R>();
@@ -1410,7 +1390,13 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(2)))
     };
 
     bool wpre = false;   // the odd sub-step's gust normals are in L.wnx (drawn with the even one's)
-    R rkb[8], rka[8];   // RK4: the 0.01 s step's base state and its k1 + 2 k2 + 2 k3 + k4
+    RS rkb[8], rka[8];   // RK4: the 0.01 s step's base state and its k1 + 2 k2 + 2 k3 + k4
+    if constexpr (sizeof(R) == 4) {
+#pragma unroll
+        for (int k = 0; k < 11; ++k) xs[k] = (RS)e.s[k];
+    }
+    // the sub-step's dt in binary64 (the reference's literals; the binary64 handle's dt bits)
+    const RS dts = RK4 ? 0.01 : (PHASE == 0 ? 0.025 : (PHASE == 1 ? 0.1 : a.dt_aux));
 #pragma unroll 1
     for (int sub = 0; sub < NSUB; ++sub) {
         PD_T(t_sub);
@@ -1418,21 +1404,23 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(2)))
         SA<R>& a = kargs<R>();
         DP<R>& P = *params<R>(a.P);
         const bool tap_sub = tap && sub == NSUB - 1;
-        R x = e.s[0], y = e.s[1], vx = e.s[2], vy = e.s[3], th = e.s[4], thd = e.s[5], ga = e.s[6], al = e.s[7];
-        R m = e.s[8], mp = e.s[9];
+        RS x = SV(0), y = SV(1), vx = SV(2), vy = SV(3), th = SV(4), thd = SV(5), ga = SV(6), al = SV(7);
+        RS m = SV(8), mp = SV(9);
         if constexpr (WIND) wc.add(kStGust - kStWork, role == 0 && live && a.stochastic && y < P.vk_y_threshold);
         // rocket_physics_fcn (rockets_physics.py:455-704)
-        R rho, patm, asnd, speed;
+        R rho, patm, asnd;
+        RS speed;
         if (RK4 ? (sub == 0 && k_have) : k_have) { rho = k_rho; patm = k_patm; asnd = k_asnd; speed = k_speed; }
         else {
-            atmosphere<R, kAtmTab>(P, L.isa, y, rho, patm, asnd);
+            atmosphere<R, kAtmTab>(P, L.isa, (R)y, rho, patm, asnd);
             speed = sqrt(vx * vx + vy * vy);
         }
+        const R spR = (R)speed;
         R mach = R(0);
-        if (asnd != R(0)) { R mr = speed / asnd; mach = (R(10) < mr) ? R(10) : mr; }
+        if (asnd != R(0)) { R mr = spR / asnd; mach = (R(10) < mr) ? R(10) : mr; }
         // alpha_effective (rockets_physics.py:498-501) and Mach feed the aero tables; what the
         // tables do not need is computed after them (fewer values live across the RBF)
-        R ae = (vy < R(0)) ? ga - th - Cst<R>::pi : al;
+        const R ae = (R)((vy < RS(0)) ? ga - th - Cst<RS>::pi : al);
         // the horizontal wind and the gust filters (no table dependence): with LPE 2 run while
         // the aero lookup's grid loads are in flight, else after the tables
         R ug = R(0), vg = R(0);
@@ -1441,7 +1429,7 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(2)))
                 // WindModel.__call__ (full_wind_model.py:35-43)
                 const R* walt = L.walt + e.prof * 16;
                 const R* wsp = L.wsp + e.prof * 16;
-                R km = PD_DIVC(R, y, 1000);
+                R km = PD_DIVC(R, (R)y, 1000);
                 int wn = P.wind_n[e.prof];
                 ug = np_interp<R>(walt, wsp, wn, km);
                 const bool gust = y < P.vk_y_threshold && a.stochastic;
@@ -1536,8 +1524,8 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(2)))
         }
         PD_T(t_aero1);
         PD_ACC(3, t_aero1 - t_aero0);
-        R q = R(0.5) * rho * (speed * speed);
-        R fpc = div_known<R>(P.m_prop0 - mp, P.m_prop0, P.inv_m_prop0, P.div2 & kDiv2MProp0);
+        R q = R(0.5) * rho * (spR * spR);
+        R fpc = div_known<R>((R)(P.m_prop0 - mp), P.m_prop0, P.inv_m_prop0, P.div2 & kDiv2MProp0);
         if (fpc == R(0)) fpc = R(1e-6);
         R x_cog, I;
         // subrocket_0 (full rocket) closures for the ascent, subrocket_2 after (:748-750, :772-774)
@@ -1558,14 +1546,14 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(2)))
             info(PD_INFO_MACH, mach); info(PD_INFO_Q, q); info(PD_INFO_X_COG, x_cog); info(PD_INFO_INERTIA, I);
             info(PD_INFO_ALPHA_EFF, ae); info(PD_INFO_UG, ug); info(PD_INFO_VG, vg); info(PD_INFO_MACH_MAX, mmax);
             info(PD_INFO_D_CP_CG, d_cp_cg); info(PD_INFO_D_THRUST_CG, d_thrust); info(PD_INFO_FUEL_CONSUMED, fpc);
-            info(PD_INFO_F_WIND_X, Fwx); info(PD_INFO_F_WIND_Y, Fwy); info(PD_INFO_M_WIND, Mw); info(PD_INFO_THETA_IN, th);
+            info(PD_INFO_F_WIND_X, Fwx); info(PD_INFO_F_WIND_Y, Fwy); info(PD_INFO_M_WIND, Mw); info(PD_INFO_THETA_IN, (R)th);
         }
-        R drag = R(0.5) * rho * (speed * speed) * CD * P.A_front;
-        R lift = R(0.5) * rho * (speed * speed) * CL * P.A_front;
+        R drag = R(0.5) * rho * (spR * spR) * CD * P.A_front;
+        R lift = R(0.5) * rho * (spR * spR) * CL * P.A_front;
         R sae, cae, sth, cth;
-        sincos_pair<LPE, R>(ae, th, role, sae, cae, sth, cth);
+        sincos_pair<LPE, R>(ae, (R)th, role, sae, cae, sth, cth);
         R apar, aperp;
-        if (vy >= R(0)) { apar = lift * sae - drag * cae; aperp = -lift * cae - drag * sae; }
+        if (vy >= RS(0)) { apar = lift * sae - drag * cae; aperp = -lift * cae - drag * sae; }
         else { apar = drag * cae - lift * sae; aperp = -drag * sae - lift * cae; }
         R aero_x = apar * cth + aperp * sth;
         R aero_y = apar * sth - aperp * cth;
@@ -1591,7 +1579,7 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(2)))
                 // v_ref - speed (Kp -0.08, clip [0, 1]) into throttle_only as a list (binary64)
                 R u0;
                 if (a.act_f64) {
-                    R nt = ((R)ud[0] - speed) * P.kp_pc;
+                    R nt = ((R)ud[0] - spR) * P.kp_pc;
                     nt = nt < R(0) ? R(0) : (nt > R(1) ? R(1) : nt);
                     u0 = R(2) * (nt - R(0.5));
                 } else {
@@ -1783,58 +1771,62 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(2)))
 #ifdef PD_STAMP
         PD_T(t_p4); acc_[9 + 7] += t_p4 - t_p3;
 #endif
-        div_pair<LPE, R>(fx, m, fy, m, role, vxd, vyq);
-        div_pair<LPE, R>(mz, I, P.grav_R, P.grav_R + y, role, thdd, grq);
+        div_pair<LPE, R>(fx, (R)m, fy, (R)m, role, vxd, vyq);
+        div_pair<LPE, R>(mz, I, P.grav_R, P.grav_R + (R)y, role, thdd, grq);
         const R gr = P.grav_g0 * (grq * grq);
         const R vyd = vyq - gr;
         if constexpr (RK4) {
-            const R kd[8] = {vx, vy, vxd, vyd, thd, thdd, -md_info, -md_info};
-            R sv[8] = {x, y, vx, vy, th, thd, m, mp};
+            const RS kd[8] = {vx, vy, vxd, vyd, thd, thdd, -md_info, -md_info};
+            RS sv[8] = {x, y, vx, vy, th, thd, m, mp};
             if (stage == 0) {
 #pragma unroll
                 for (int k = 0; k < 8; ++k) rkb[k] = sv[k];
             }
 #pragma unroll
             for (int k = 0; k < 8; ++k) rka[k] = stage == 0 ? kd[k] : (stage == 3 ? rka[k] + kd[k] : rka[k] + R(2) * kd[k]);
-            const R c = stage == 3 ? dt / R(6) : (stage == 2 ? dt : R(0.5) * dt);
+            const RS c = stage == 3 ? dts / RS(6) : (stage == 2 ? dts : RS(0.5) * dts);
 #pragma unroll
             for (int k = 0; k < 8; ++k) sv[k] = rkb[k] + c * (stage == 3 ? rka[k] : kd[k]);
             x = sv[0]; y = sv[1]; vx = sv[2]; vy = sv[3]; th = sv[4]; thd = sv[5]; m = sv[6]; mp = sv[7];
-            if (stage == 3 && th > Cst<R>::two_pi) th -= Cst<R>::two_pi;
-            ga = pd_atan2<R>(vy, vx);
-            if (ga < R(0)) ga = Cst<R>::two_pi + ga;
+            if (stage == 3 && th > Cst<RS>::two_pi) th -= Cst<RS>::two_pi;
+            ga = pd_atan2<RS>(vy, vx);
+            if (ga < RS(0)) ga = Cst<RS>::two_pi + ga;
             al = th - ga;
         } else {
-        vx += vxd * dt; vy += vyd * dt; x += vx * dt; y += vy * dt;
-        thd += thdd * dt; th += thd * dt;
-        atmosphere<R, kAtmTab>(P, L.isa, y, k_rho, k_patm, k_asnd);
+        vx += (RS)vxd * dts; vy += (RS)vyd * dts; x += vx * dts; y += vy * dts;
+        thd += (RS)thdd * dts; th += thd * dts;
+        atmosphere<R, kAtmTab>(P, L.isa, (R)y, k_rho, k_patm, k_asnd);
         k_speed = sqrt(vx * vx + vy * vy);
         k_have = true;
-        ga = pd_atan2<R>(vy, vx);
-        if (th > Cst<R>::two_pi) th -= Cst<R>::two_pi;
-        if (ga < R(0)) ga = Cst<R>::two_pi + ga;
+        ga = pd_atan2<RS>(vy, vx);
+        if (th > Cst<RS>::two_pi) th -= Cst<RS>::two_pi;
+        if (ga < RS(0)) ga = Cst<RS>::two_pi + ga;
         al = th - ga;
-        mp -= mdot_dt; m -= mdot_dt;
+        mp -= (RS)mdot_dt; m -= (RS)mdot_dt;
         }
         if (tap_sub) {
             info(PD_INFO_CF_X, cfx); info(PD_INFO_CF_Y, cfy); info(PD_INFO_GRAVITY, gr); info(PD_INFO_VX_DOT, vxd);
             info(PD_INFO_VY_DOT, vyd); info(PD_INFO_MOMENTS, mz); info(PD_INFO_THETA_DDOT, thdd);
         }
-        e.s[0] = x; e.s[1] = y; e.s[2] = vx; e.s[3] = vy; e.s[4] = th; e.s[5] = thd; e.s[6] = ga; e.s[7] = al;
-        e.s[8] = m; e.s[9] = mp;
-        if (!RK4 || stage == 3) e.s[10] = e.s[10] + dt;
+        SV(0) = x; SV(1) = y; SV(2) = vx; SV(3) = vy; SV(4) = th; SV(5) = thd; SV(6) = ga; SV(7) = al;
+        SV(8) = m; SV(9) = mp;
+        if (!RK4 || stage == 3) SV(10) = SV(10) + dts;
         PD_T(t_subend);
         PD_ACC(4, t_subend - t_aero1);
     }
     if (nan_hit && role == 0 && live) atomicAdd(&a.pend.stats[kStNan], 1ull);
+    if constexpr (sizeof(R) == 4) {   // the env-step's state, rounded once
+#pragma unroll
+        for (int k = 0; k < 11; ++k) e.s[k] = (R)xs[k];
+    }
     PD_T(t_loop);
 
     // ---- g-load window (base_environment.py:136-149): ring of 10 in LDS, Python sum() from the
     // oldest; the new entry is written first, then the window is read back in summation order
     DP<R>& P2 = *params<R>(a.P);
     const R* s = e.s;
-    const R v = RK4 ? sqrt(s[2] * s[2] + s[3] * s[3]) : k_speed;   // (the same expression's bits)
-    R gl_new = PD_DIVC(R, PD_DIVC(R, fabs(v - e.vprev), 0.1) * R(1), 9.81);
+    const RS v = RK4 ? sqrt(SV(2) * SV(2) + SV(3) * SV(3)) : k_speed;   // (the same expression's bits)
+    R gl_new = (R)PD_DIVC(RS, PD_DIVC(RS, fabs(v - (RS)e.vprev), 0.1) * RS(1), 9.81);
     int glen = e.glen, ghead = e.ghead;
     int wslot;
     if (glen < 10) { wslot = glen; glen += 1; }
@@ -1863,7 +1855,7 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(2)))
     } else {
         rho = k_rho; pa_ = k_patm; as_ = k_asnd;   // (the last sub-step's, of this state)
     }
-    R speed = v;
+    R speed = (R)v;
     R q = R(0.5) * rho * (speed * speed);
     int tr = 0, id = 0, dn = 0;
     R rew = R(0);
@@ -1893,7 +1885,7 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(2)))
             else if (tr && y < R(0)) rew -= R(50) * PD_DIVC(R, fabs(vy), 10);
             if (!dn || !(tr && y < R(0))) rew = rew < R(-10) ? R(-10) : (rew > R(10) ? R(10) : rew);
         } else {                      // landing_burn / ACS reward (rtd_rl.py:243-269), u0 = actions[0]
-            R aef = fabs(ga - th - Cst<R>::pi);
+            R aef = (R)fabs(SV(6) - SV(4) - Cst<RS>::pi);   // (the chain's binary64 angles)
             R lead = R(1.5) - log(R(1) + aef) / P2.log_1p_max_ae;
             R X;
             if (a.act_f64) X = lead - ((R)ud[0] + R(1)) / R(2) * R(0.5);
@@ -1934,7 +1926,7 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(2)))
             rew = rew < R(-10) ? R(-10) : (rew > R(10) ? R(10) : rew);
         } else if (ph == PD_PHASE_BALLISTIC_ARC) {
             // compile_rtd_rl_ballistic_arc_descent (rtd_rl.py:153-188)
-            R aef = fabs(ga - th - Cst<R>::pi);
+            R aef = (R)fabs(SV(6) - SV(4) - Cst<RS>::pi);
             dn = (q > R(10000) && aef < (R)(3.0 * kDeg2Rad));
             if (q > R(10000 - 2000) && aef > (R)(5.0 * kDeg2Rad)) { tr = 1; id = 1; }
             rew = (Cst<R>::pi - aef) / Cst<R>::pi;
@@ -1993,7 +1985,7 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(2)))
             else if (x < R(0)) over = -x;
             else if (y < R(0)) over = -y;
             else over = R(0);
-            R aeff = (vy < R(0)) ? fabs(ga - th - Cst<R>::pi) : fabs(th - ga);
+            R aeff = (R)((vy < R(0)) ? fabs(SV(6) - SV(4) - Cst<RS>::pi) : fabs(SV(4) - SV(6)));
             if (over > R(0.5)) { tr = 1; id = 1; }
             else if (mp <= R(0)) { tr = 1; id = 2; }
             else if (aeff > (R)(10.0 * kDeg2Rad)) { tr = 1; id = 3; }
@@ -2014,6 +2006,9 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(2)))
     const bool ended = !POL && a.auto_reset && (dn || tr);
     wc.add(kStResets - kStWork, ended && role == 0 && live);
     k_have = !ended;
+    // (binary32: the next step starts from the rounded state; its speed from the rounded velocity,
+    // as a launch that loads it computes it; the atmosphere was evaluated at the rounded altitude)
+    if constexpr (sizeof(R) == 4) k_speed = sqrt((RS)e.s[2] * (RS)e.s[2] + (RS)e.s[3] * (RS)e.s[3]);
     if (role == 0 && live) {
         // (loop-invariant addresses from a laundered offset: formed here, not held across the loop)
         uint32_t uo = ui;
@@ -2053,7 +2048,7 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(2)))
         reset_values<R>(P2, a, g, e.ep + 1, (const double*)(uint64_t)&P2.logtab.invc[0],
                         (const double*)(uint64_t)&P2.logtab.logc[0], e);   // keeps the aero caches
     } else {
-        e.vprev = v;
+        e.vprev = (R)v;
         e.glen = glen; e.ghead = ghead;
         e.tid = id;
         e.ts = e.ts + 1;

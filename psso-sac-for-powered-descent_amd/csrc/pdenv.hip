@@ -1664,6 +1664,17 @@ template <typename R> pd_status create_impl(const pd_params* p, const pd_config*
             *dst[k] = (const R*)d;
         }
     }
+    {
+        // the step kernels' LDS tables as one image (pd_step.h StepStatic), copied by their prologue
+        void* img;
+        const size_t nb = c->enable_wind ? sizeof(StepStatic<R, true>) : sizeof(StepStatic<R, false>);
+        if ((st = dalloc(e, &img, nb))) return st;
+        std::vector<uint8_t> h(nb);
+        if (c->enable_wind) fill_step_static<R, true>(D, *(StepStatic<R, true>*)h.data());
+        else fill_step_static<R, false>(D, *(StepStatic<R, false>*)h.data());
+        PD_HIP(hipMemcpy(img, h.data(), nb, hipMemcpyHostToDevice));
+        D.stage_img = img;
+    }
     if ((st = dalloc(e, &e->dparams, sizeof(D)))) return st;
     PD_HIP(hipMemcpy(e->dparams, &D, sizeof(D), hipMemcpyHostToDevice));
     size_t R_ = sizeof(R);

@@ -217,9 +217,9 @@ def test_c3_f32_handle_shadowed(pd, oracle_mod):
     """The binary32 handle (the throughput precision: Taylor lines and binary32 cell pieces
     through the fine index) on the c3 workload at full size, 65 536 envs x 240
     steps; 96 sampled envs teacher-forced against the binary64 oracle at every step from the
-    handle's own (binary32) state: y, vy, mass, propellant and time within 1e-5 of max(|x|, 1)
-    (test_f32_teacher_forced's bound), x, vx, theta, gamma, alpha within 1e-3 and theta_dot
-    within 5e-2 (the chaotic attitude channels: see the bounds below), reward within 1e-4,
+    handle's own (binary32) state: every channel within 1e-5 of max(|x|, 1) and theta_dot within
+    1e-4 (SURVEY 8(d)'s fp32 tolerance; the handle integrates the state chain in binary64 within
+    the env-step, see the bounds below), reward within 1e-4,
     done/truncated/trunc_id equal in >= 99.5 % of the sampled steps (a binary32 quantity can sit
     on the other side of a threshold); auto-resets within 1e-6 of the oracle's (the same Philox
     draws; the binary32 reset adds the tilt in binary32) with the same wind percentile."""
@@ -262,17 +262,16 @@ def test_c3_f32_handle_shadowed(pd, oracle_mod):
                 so = np.array(E.s[:])
                 worst = np.maximum(worst, np.abs(after["s"][j].astype(np.float64) - so) / np.maximum(np.abs(so), 1.0))
         snap = after
-    # Bounds per channel group.  The attitude channels are where binary32 rounding is amplified
-    # most (round 4's first run: theta_dot 9.3e-3, theta 1.5e-4, alpha 6.9e-5, vx 4.5e-5 in one
-    # step): an env near max-q with |alpha_eff| ~ 1e-3 has alpha_eff = gamma - theta - pi as the
-    # difference of two O(1) binary32 angles (absolute error ~2e-7, relative ~1e-4 in alpha and
-    # in C_L, which is ~ deg(deg(alpha))), and the aerodynamic moment over the step turns that
-    # into theta_dot.  The binary64 handle has the same amplification at 2^-29 of the rounding
-    # (its theta_dot bound is 1e-8, s3 of DESIGN.md).
+    # Bounds.  The attitude channels are where binary32 rounding is amplified most: an env near
+    # max-q with |alpha_eff| ~ 1e-3 has alpha_eff = gamma - theta - pi as the difference of two
+    # O(1) angles, and the aerodynamic moment over the step turns its error into theta_dot.  With
+    # the angles in binary32 (round 4) one step lost theta_dot 9.3e-3, theta 1.5e-4, alpha
+    # 6.9e-5, vx 4.5e-5; the handle now carries the state chain in binary64 through the env-step
+    # and rounds it once, so only the binary32 forces and tables are left.
     att = [0, 2, 4, 6, 7]     # x, vx, theta, gamma, alpha
     res = dict(keep=float(worst[keep].max()), attitude=float(worst[att].max()), theta_dot=float(worst[5]),
                reward=wrew, flips=flips, steps=n, resets=resets, per_channel=dict(zip(ST, worst.tolist())))
     print("f32 shadow:", res)
-    assert (res["keep"] <= 1e-5 and res["attitude"] <= 1e-3 and res["theta_dot"] <= 5e-2 and wrew <= 1e-4
+    assert (res["keep"] <= 1e-5 and res["attitude"] <= 1e-5 and res["theta_dot"] <= 1e-4 and wrew <= 1e-4
             and flips <= 0.005 * n and resets >= len(idx) // 2), res
     assert env.counters()["nan_events"] == 0

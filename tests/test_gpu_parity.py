@@ -318,18 +318,28 @@ def test_wind_injected_noise_vs_oracle(pd, oracle_mod):
 
 
 def test_f32_teacher_forced(pd):
-    """fp32 handle: one step from recorded states vs the reference (fp32 tolerance)."""
+    """fp32 handle: one step from the reference's recorded states vs the reference, every channel
+    (SURVEY 8(d)'s fp32 tolerance, 1e-5 of max(|x|, 1); theta_dot 1e-4).  The handle computes its
+    forces in binary32 and integrates the state chain in binary64 within the step (alpha_eff =
+    gamma - theta - pi from binary64 angles), so what is left is the binary32 rounding of the
+    inputs and the forces."""
     import torch
     d = golden("ref_teacher_forced.npz")
-    S0, A = d["pt_state_in"], d["pt_action"]
-    env = make(pd, len(S0), mode="pso", precision="f32")
-    env.set_state(torch.tensor(S0))
-    env.step(torch.tensor(A))
-    S = env.state.double().cpu().numpy()
-    ref = d["pt_state_out"]
-    err = np.abs(S - ref) / np.maximum(np.abs(ref), 1.0)
-    keep = [1, 3, 8, 9, 10]   # y, vy, m, m_prop, t
-    assert err[:, keep].max() < 1e-5, dict(zip([ST[k] for k in keep], err[:, keep].max(0)))
+    for tag, phase in (("pt", "landing_burn_pure_throttle"), ("lb", "landing_burn")):
+        S0, A = d[f"{tag}_state_in"], d[f"{tag}_action"]
+        env = make(pd, len(S0), phase, mode="pso", precision="f32")
+        env.set_state(torch.tensor(S0))
+        if phase == "landing_burn":
+            env.set_actuators(torch.tensor(d["lb_prevs"]).float())
+        env.step(torch.tensor(A))
+        S = env.state.double().cpu().numpy()
+        ref = d[f"{tag}_state_out"]
+        err = np.abs(S - ref) / np.maximum(np.abs(ref), 1.0)
+        worst = dict(zip(ST, err.max(0).tolist()))
+        print(f"f32 teacher-forced {tag}:", worst)
+        tol = np.full(11, 1e-5)
+        tol[5] = 1e-4
+        assert (err.max(0) <= tol).all(), (tag, worst)
 
 
 def test_rl_facade_matches_reference_episode(pd):
@@ -910,6 +920,27 @@ def test_policy_rollout_compaction_invariant(pd):
     f2, s2 = env2.rollout_policy(torch.tensor(W[sub]), max_steps=300)
     assert np.array_equal(s2.cpu().numpy(), res[0][1][sub])
     np.testing.assert_allclose(f2.cpu().numpy(), res[0][0][sub], rtol=1e-12)
+
+
+@pytest.mark.parametrize("P", [65536, 262144])
+def test_policy_rollout_compaction_invariant_full_swarm(pd, P):
+    """The live list in the regime it is built for (N x 2 lanes beyond one chip round: the list is
+    the default there): BASELINE c4's whole 262 144-particle swarm on one device, and a quarter
+    of it, with the list (from the first launch; from 50 % live) and without, at 64 and at 8 policy
+    steps per launch, check every 8 steps: fitness, episode lengths and final states bit-identical."""
+    import torch
+    g = torch.Generator(device="cuda").manual_seed(5)
+    W = (torch.rand(P, 372, generator=g, device="cuda") * 3 - 1.5).contiguous()
+    env = make(pd, P, phase="landing_burn", mode="pso")
+    assert env.tuning()["policy_list"] == -1
+    res = []
+    for lst, at, pf in ((0, 0.0, 64), (-1, 0.0, 64), (1, 0.0, 8), (0, 0.5, 8)):
+        env.set_tuning(policy_list=lst, policy_list_at=at, policy_fuse=pf)
+        fit, steps = env.rollout_policy(W, max_steps=400, check_every=8)
+        res.append((fit.clone(), steps.clone(), env.state.clone()))
+    for f, s, S in res[1:]:
+        assert torch.equal(f, res[0][0]) and torch.equal(s, res[0][1]) and torch.equal(S, res[0][2])
+    assert int(res[0][1].max()) > 2 * int(res[0][1].float().mean())     # ragged: the list shrinks
 
 
 @pytest.mark.parametrize("lpe", [1, 2, 4, 8, 16])

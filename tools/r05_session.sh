@@ -6,6 +6,9 @@
 #      c4 at the config's whole swarm on one GPU (262 144 particles, live list on / off), and the
 #      driver's command on the current build.
 #   2: the GPU suite and the smoke.
+#   3: the binary32 handle with the binary64 state chain: its tests and timing.
+#   4: c3 / c3-descent traffic and time with and without the fine index (PMC passes).
+#   5: the suite, smoke, fixed cost, driver command, c5 and c4-262k on the round-5 build.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -37,6 +40,41 @@ case "${PART:-1}" in
   # table flags through the ABI): the GPU suite and the smoke
   run gpu_tests 900 python -u -m pytest tests/ -m gpu -x -q --timeout 200 --timeout-method thread
   run smoke 200 python -c "import __graft_entry__ as g; g.smoke()"
+  ;;
+3)
+  # binary32 handles with the binary64 state chain: their tests (teacher-forced against the
+  # reference on every channel, the c3 shadow at the fp32 tolerance, fused == per-step, device
+  # solve, RK4), then c3 at F = 128 in both precisions
+  run gpu_f32 900 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_c3.py tests/test_gpu_rk4.py -m gpu -x -v \
+      --timeout 300 --timeout-method thread -k "f32 or fused_equals or device_solve or rk4 or full_swarm or launcher" -s
+  for p in f32 f64; do
+    BURN=640 FUSE=128 LAUNCHES=6 PREC=$p run t_$p 200 python tools/time_fused.py
+  done
+  ;;
+4)
+  # where c3-descent's traffic comes from: the fine index against the cell / sub-cell records
+  # (PD_TABLES_NO_FINE_INDEX = 2), c3 and c3-descent, PMC traffic + L2 hits, then the timing
+  CASES="d_fine:1:0 d_rec:1:2 c_fine:0:0 c_rec:0:2" run pmc5 900 bash tools/pmc_r05.sh
+  for c in "1 0" "1 2" "0 0" "0 2"; do
+    set -- $c
+    DESCENT=$1 TABLE_FLAGS=$2 BURN=640 FUSE=128 LAUNCHES=6 run t_d$1_f$2 200 python tools/time_fused.py
+  done
+  ;;
+5)
+  # the build with the binary64 state chain (binary32 handles), the SAC actor's latency plan and
+  # the LDS tables staged from one image: the GPU suite (with the new f32 bounds, the launcher
+  # checks and the full-swarm compaction test) and the smoke, then the per-launch fixed cost
+  # (F = 1 / 20 / 128, binary64 and binary32), the driver's command, c5, c4 at the whole swarm
+  run gpu_tests 1000 python -u -m pytest tests/ -m gpu -x -q --timeout 300 --timeout-method thread -s
+  run smoke 200 python -c "import __graft_entry__ as g; g.smoke()"
+  for f in 20 128 1; do
+    L=$(( f >= 20 ? 6 : 24 ))
+    BURN=640 FUSE=$f LAUNCHES=$L run fix5_f$f 200 python tools/time_fused.py
+  done
+  BURN=640 FUSE=128 LAUNCHES=6 PREC=f32 run t5_f32 200 python tools/time_fused.py
+  run benchdrv5 300 python bench.py --steps 20 --warmup 5
+  run c5_5 300 python bench.py --workload c5
+  run c4_262k_5 300 python bench.py --workload c4 --particles 262144 --steps 6 --warmup 2 --policy-list 0
   ;;
 esac
 echo "=== done"
