@@ -315,6 +315,7 @@ def other_workloads(args, local):
     return res
 
 
+KERNEL_REPLAYS = 3      # replays of the timed launches for the kernel time (per-launch median)
 DESCENT_BURN_IN = 640   # c3-descent: untimed steps before the warmup (a steady mix of episode phases)
 # c3: untimed steps before the warmup, so that the timed window sees resets at their stationary
 # rate (every episode of the uniform-action law ends within ~200 steps); --c3-burn-in 0 gives the
@@ -417,14 +418,19 @@ def run_c3(args, precision, local, rank, dist, descent=False, launch_base=0, bur
     # actions and per-env state; the aero tables keep what the timed region inserted, so the
     # replay solves fewer misses -- both counts are reported), each launch with its miss flush
     # between a pair of HIP events on the stream the kernel runs on
-    env.restore(blob)
+    # (three replays; each launch's median: one launch of the driver's 20-step window varies by
+    # up to 20 % between identical replays -- clocks, the chip's other traffic)
     first_replay = launch_base + launches[0]
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in tb]
-    for k, b in enumerate(tb):
-        ev[k][0].record()
-        chunk(*b)
-        ev[k][1].record()
-    torch.cuda.synchronize()
+    reps = []
+    for _ in range(KERNEL_REPLAYS):
+        env.restore(blob)
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in tb]
+        for k, b in enumerate(tb):
+            ev[k][0].record()
+            chunk(*b)
+            ev[k][1].record()
+        torch.cuda.synchronize()
+        reps.append([a.elapsed_time(b) for a, b in ev])
     s2 = env.stats()
     # workload counts: the same launches once more with the step kernel's counters on (counting
     # costs a few per cent, so neither timed pass counts)
@@ -435,11 +441,11 @@ def run_c3(args, precision, local, rank, dist, descent=False, launch_base=0, bur
     torch.cuda.synchronize()
     env.count_work(False)
     s3 = env.stats()
-    kern = [a.elapsed_time(b) for a, b in ev]
+    kern = [sorted(r[k] for r in reps)[len(reps) // 2] for k in range(len(tb))]
     full = [m for m, (t0, t1) in zip(kern, tb) if t1 - t0 == F]
     d = {k: s3[k] - s2[k] for k in env.WORK_COUNTERS}
     d["rbf_misses"] = s1["rbf_misses"] - s0["rbf_misses"]     # solved in the timed region itself
-    res = dict(wall=wall, dev_ms=dev_ms, kern_total_ms=sum(kern), kern_launches=len(kern),
+    res = dict(wall=wall, dev_ms=dev_ms, kern_total_ms=sum(kern), kern_launches=len(kern), kern_replays=KERNEL_REPLAYS,
                kern_avg_full_ms=(sum(full) / len(full)) if full else None, fuse=F, n=n,
                obs_dim=env.obs_dim, act_dim=env.action_dim, burn_in=burn,
                # (lanes per env: pd_create's default, 2 above 8 192 envs)
@@ -447,9 +453,10 @@ def run_c3(args, precision, local, rank, dist, descent=False, launch_base=0, bur
                replay_misses=s2["rbf_misses"] - s1["rbf_misses"],
                launch_index={"kernel": f"k_step<{'double' if precision == 'f64' else 'float'}>",
                              "timed": [first_timed, first_timed + len(tb)],
-                             "replay": [first_replay, first_replay + len(tb)]},
+                             "replay": [first_replay, first_replay + KERNEL_REPLAYS * len(tb)],
+                             "replays": KERNEL_REPLAYS},
                nan_events=s3["nan_events"])
-    res["launches_total"] = launches[0]
+    res["launches_total"] = launches[0]   # (every launch of this handle: the replays included)
     env.close()
     return res
 
@@ -490,8 +497,8 @@ def c3_summary(args, r, world, precision, pmc=None):
                      "kernel_avg_full_launch_ms": r["kern_avg_full_ms"], "kernel_launches_timed": r["kern_launches"],
                      "env_steps_per_launch": F, "env_steps_per_timed_launch": K / r["kern_launches"],
                      "envs_per_launch": n,
-                     "kernel_timing": "the timed region's launches replayed from its checkpoint, HIP events per "
-                                      "launch (k_step + its miss flush) on the launch stream",
+                     "kernel_timing": "the timed region's launches replayed from its checkpoint three times, HIP events "
+                                      "per launch (k_step + its miss flush) on the launch stream, each launch's median",
                      "note": "VALU/latency-bound elementwise ODE (no MFMA); see DESIGN.md"},
         "workload_counts": r["counts"],
         "replay_rbf_misses": r["replay_misses"],

@@ -233,6 +233,12 @@ pd_status pd_step(pd_env* env, const void* actions, void* obs, void* reward, uin
  * to n_steps pd_step calls.  No host synchronisation. */
 pd_status pd_step_n(pd_env* env, const void* actions, int32_t n_steps, void* obs, void* reward, uint8_t* done,
                     uint8_t* truncated, int8_t* trunc_id, void* stream);
+/* pd_step_n with the info tap in the fused launches (ABI 9): info [n_steps][k][N] (handle
+ * precision) receives, for every step, the k = popcount(info_mask) fields of pd_info_field whose
+ * bit is set in info_mask, in pd_info_field order -- the visualisation episodes' selected keys
+ * (rockets_physics.py:649-702) without a launch per step.  The same values as pd_step's info. */
+pd_status pd_step_n_info(pd_env* env, const void* actions, int32_t n_steps, void* obs, void* reward, uint8_t* done,
+                         uint8_t* truncated, int8_t* trunc_id, void* info, uint64_t info_mask, void* stream);
 /* One SAC data-collection step (sac_pytorch_powered_descent.py:160-183 for N envs) in one
  * launch.  The action is sampled in the kernel from the caller's actor heads, as Actor.sample
  * does it (sac_pytorch.py:161-179) in binary32: a = tanh(mean + exp(clamp(log_std, log_std_min,

@@ -212,7 +212,9 @@ template <typename R> struct StepArgs {
     const void* actions;
     R* obs; R* reward; uint8_t* done; uint8_t* trunc; int8_t* trunc_id;
     const double* noise;
-    R* info;                         // [PD_N_INFO][N] (single-step launches)
+    R* info;                         // [n_fused][nsel][N]: the info fields of info_mask, in pd_info_field order
+    uint64_t info_mask;              // (pd_step: every field, nsel = PD_N_INFO)
+    int info_nsel;
     R* reward_sum;
     const float* policy_w;           // policy rollouts: actor parameters [P][N] float32
     // policy rollouts: the live envs as a compacted index list; a launch steps list_in[0, *cnt_in)

@@ -66,6 +66,8 @@ template <typename R> struct TabView {
     const PD_AS1 R* cell_pc;        // cell pieces (cell_stride<R>() words each; nullptr: none)
     const PD_AS1 int* sub_piece;
     const PD_AS1 uint32_t* fine;    // fine index (nullptr: none)
+    const PD_AS1 uint32_t* cellw;   // its two-level form (PD_IDX2)
+    const PD_AS1 uint32_t* rfine;
     int grid_nm, grid_na;
     R grid_a0, grid_inv_da, grid_inv_dm;
 };
@@ -435,6 +437,11 @@ __device__ __forceinline__ int rbf_lookup(const AT& a, DP<R>& P, int table, cons
     const bool fine_path = tay != nullptr && t.fine != nullptr;
     uint32_t fe = 0u;
     R fsm = R(0), fsa = R(0);
+#ifndef PD_IDX2
+#define PD_IDX2 0
+#endif
+    uint32_t fsub = 0u;
+    (void)fsub;
     if (use_grid) {
         R fm = M * t.grid_inv_dm, fa = (aq - t.grid_a0) * t.grid_inv_da;
         int im = fm < R(0) ? 0 : (fm >= R(t.grid_nm) ? t.grid_nm - 1 : (int)fm);
@@ -447,7 +454,14 @@ __device__ __forceinline__ int rbf_lookup(const AT& a, DP<R>& P, int table, cons
             int jm = (int)sm, ja = (int)sa;
             jm = jm < 0 ? 0 : (jm > kGridSub - 1 ? kGridSub - 1 : jm);
             ja = ja < 0 ? 0 : (ja > kGridSub - 1 ? kGridSub - 1 : ja);
+#if PD_IDX2
+            // the cell's word (the per-cell array stays in L2); a refined cell's sub-cell word
+            // below, once the cell word has said which refined cell it is
+            fe = t.cellw[gcell];
+            fsub = (uint32_t)(jm * kGridSub + ja);
+#else
             fe = t.fine[(uint32_t)(im * kGridSub + jm) * (uint32_t)(t.grid_na * kGridSub) + (uint32_t)(ia * kGridSub + ja)];
+#endif
             fsm = sm - (R)jm; fsa = sa - (R)ja;
         } else {
             gkey = t.grid_key[gcell];
@@ -491,6 +505,10 @@ __device__ __forceinline__ int rbf_lookup(const AT& a, DP<R>& P, int table, cons
             // Binary32 handles: 1e-4 cell widths as their record path, and 1e-3 sub-cell widths
             // (the binary32 position's rounding is ~5e-5 cell widths at the grid's far end)
             const R eps = sizeof(R) == 8 ? R(1e-9) : R(1e-4), eps_sub = sizeof(R) == 8 ? R(1e-9) : R(1e-3);
+#if PD_IDX2
+            if ((fe & kFineRefined) && !(fe & (kFinePiece | kFineBisect)))
+                fe = t.rfine[(fe & kFineIndex) * (uint32_t)(kGridSub * kGridSub) + fsub];
+#endif
             const bool inside = (fe & kFineRefined)
                 ? (fsm > eps_sub && R(1) - fsm > eps_sub && fsa > eps_sub && R(1) - fsa > eps_sub)
                 : (um > eps && R(1) - um > eps && ua > eps && R(1) - ua > eps);
@@ -1035,6 +1053,8 @@ __device__ __forceinline__ TabView<R> tab_view(DP<R>& P, const R* tab, int table
     t.cell_pc = gbl(P.cell_pc[table]);
     t.sub_piece = gbl(P.sub_piece[table]);
     t.fine = gbl(P.fine[table]);
+    t.cellw = gbl(P.cellw[table]);
+    t.rfine = gbl(P.rfine[table]);
     t.grid_nm = P.grid_nm[table];
     t.grid_na = P.grid_na[table];
     t.grid_a0 = P.grid_a0[table];
@@ -1074,26 +1094,6 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(2)))
     // reads it before the last one advances it, see the end of the kernel)
     int64_t ring_pos0 = 0;
     if constexpr (SAC) { if (a.ring_state) ring_pos0 = (int64_t)__atomic_load_n(a.ring_state, __ATOMIC_RELAXED); }
-    // pd_step_sac_fused (16 lanes per env: the workgroup's 16 envs are one MLP tile): the actor's
-    // heads of this step from the observation the previous step left in obs32, into s_sach (read
-    // by the sampling below; the staging barrier orders them), before anything else of the step
-    constexpr bool kSacMlp = SAC && LPE == 16;
-    __shared__ __attribute__((aligned(16))) float s_mlp[kSacMlp ? sac_mlp_lds_floats<256>() : 1];
-    __shared__ float s_sach[kSacMlp ? kSacTile * 16 : 1];
-    if constexpr (kSacMlp) {
-        const int H = a.sac_mlp.H;   // (grid-uniform: the barriers inside are reached by every thread)
-        if (H) {
-            const int64_t e0 = (int64_t)blockIdx.x * kSacTile;
-            const int A2 = a.sac_mlp.A;
-            auto put = [&](int e, int o, float v) {
-                s_sach[e * 16 + (o < A2 ? o : 8 + o - A2)] = v;
-                if (a.sac_heads_out && e0 + e < a.n) a.sac_heads_out[(e0 + e) * 2 * A2 + o] = v;
-            };
-            if (H == 128) sac_mlp_tile<128>(a.sac_mlp, a.n, e0, s_mlp, put);
-            else sac_mlp_tile<256>(a.sac_mlp, a.n, e0, s_mlp, put);
-            __syncthreads();   // (s_mlp is free again; the heads wait for the staging barrier)
-        }
-    }
     if constexpr (POL) {
         if (blockIdx.x == 0 && threadIdx.x == 0) *a.cnt_zero = 0u;
         if (a.use_list) {
@@ -1101,36 +1101,6 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(2)))
             if ((int64_t)blockIdx.x * EPB >= n_act) return;
         }
     }
-    {
-        // the static tables: one 16-byte vector copy of the handle's image of them (pdenv.hip
-        // fill_step_static: the same values, the grid-fin slopes by the same division), every load
-        // of a thread issued before its first store; then the eval_log cells
-        DP<R>& P = *params<R>(a.P);
-        constexpr int kImg = (int)(sizeof(StepStatic<R, WIND>) / 16);
-        constexpr int kLog = (int)(sizeof(LogTableD) / 16);
-        constexpr int kPer = (kImg + kLog + kStepBlock - 1) / kStepBlock;
-        using V4 = __attribute__((ext_vector_type(4))) unsigned int;
-        const PD_AS1 V4* img = (const PD_AS1 V4*)P.stage_img;
-        const PD_AS1 V4* lgt = (const PD_AS1 V4*)(uint64_t)&P.logtab_d.cell[0];
-        V4 v[kPer];
-#pragma unroll
-        for (int k = 0; k < kPer; ++k) {
-            const int t = threadIdx.x + k * kStepBlock;
-            if (t < kImg) v[k] = img[t];
-            else if (t < kImg + kLog) v[k] = lgt[t - kImg];
-        }
-#pragma unroll
-        for (int k = 0; k < kPer; ++k) {
-            const int t = threadIdx.x + k * kStepBlock;
-            if (t < kImg) ((V4*)static_cast<StepStatic<R, WIND>*>(&L))[t] = v[k];
-            else if (t < kImg + kLog) ((V4*)s_logtab)[t - kImg] = v[k];
-        }
-        if (threadIdx.x < (kStepBlock / 64) * kNWork) (&L.work[0][0])[threadIdx.x] = 0u;
-        if (threadIdx.x < 2) L.tdesc[threadIdx.x] = tab_view<R>(P, L.tab, (int)threadIdx.x);
-    }
-    __syncthreads();
-    PD_T(t_staged);
-    PD_ACC(0, t_staged - t_start);
     const int64_t N = a.n;
     const int64_t gt = (int64_t)blockIdx.x * kStepBlock + threadIdx.x;
     // Every lane stays active (the cooperative miss solve needs converged waves).  Lanes past the
@@ -1145,10 +1115,7 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(2)))
     // envs stay frozen and a wave with none left exits (wave-uniform, after the only barrier)
     bool live = valid;
     if constexpr (POL) {
-        if (!a.use_list) {
-            live = live && ev(a.b.fin, ui) == 0;
-            if (__ballot(live) == 0) return;
-        }
+        if (!a.use_list) live = live && ev(a.b.fin, ui) == 0;
     }
     // role -> (table, part): LPE 1: both tables on one lane; else table = role / (LPE/2)
     constexpr int nparts = LPE >= 2 ? LPE / 2 : 1;
@@ -1157,7 +1124,9 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(2)))
     const int gbase = (int)__lane_id() & ~(LPE - 1);
     const uint64_t g = a.env_offset + (uint64_t)i;
 
-    // ---- the env's state into registers (its g-load ring into LDS)
+    // ---- the env's state into registers (its g-load ring into LDS; the ring is not part of the
+    // staged tables, so its stores may precede the staging barrier): requested ahead of the actor
+    // prologue and the table staging, whose latencies then overlap it
     EnvRegs<R> e;
     RbfCache<R> cA, cB;   // LPE 1: A = C_D, B = C_L; LPE >= 2: A = own table
     {
@@ -1191,6 +1160,60 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(2)))
         cA.slot = valid ? ldv(a.b.slot + (my_table) * N, ui) : -1;
         if constexpr (LPE == 1) { cB.key = valid ? ldv(a.b.key + N, ui) : P.init_key_cl; cB.slot = valid ? ldv(a.b.slot + N, ui) : -1; }
         else { cB.key = 0; cB.slot = -1; }
+    }
+    // pd_step_sac_fused (16 lanes per env: the workgroup's 16 envs are one MLP tile): the actor's
+    // heads of this step from the observation the previous step left in obs32, into s_sach (read
+    // by the sampling below; the staging barrier orders them), before anything else of the step
+    constexpr bool kSacMlp = SAC && LPE == 16;
+    __shared__ __attribute__((aligned(16))) float s_mlp[kSacMlp ? sac_mlp_lds_floats<256>() : 1];
+    __shared__ float s_sach[kSacMlp ? kSacTile * 16 : 1];
+    if constexpr (kSacMlp) {
+        const int H = a.sac_mlp.H;   // (grid-uniform: the barriers inside are reached by every thread)
+        if (H) {
+            const int64_t e0 = (int64_t)blockIdx.x * kSacTile;
+            const int A2 = a.sac_mlp.A;
+            auto put = [&](int e, int o, float v) {
+                s_sach[e * 16 + (o < A2 ? o : 8 + o - A2)] = v;
+                if (a.sac_heads_out && e0 + e < a.n) a.sac_heads_out[(e0 + e) * 2 * A2 + o] = v;
+            };
+            if (H == 128) sac_mlp_tile<128>(a.sac_mlp, a.n, e0, s_mlp, put);
+            else sac_mlp_tile<256>(a.sac_mlp, a.n, e0, s_mlp, put);
+            __syncthreads();   // (s_mlp is free again; the heads wait for the staging barrier)
+        }
+    }
+    {
+        // the static tables: one 16-byte vector copy of the handle's image of them (pdenv.hip
+        // fill_step_static: the same values, the grid-fin slopes by the same division), every load
+        // of a thread issued before its first store; then the eval_log cells
+        DP<R>& P = *params<R>(a.P);
+        constexpr int kImg = (int)(sizeof(StepStatic<R, WIND>) / 16);
+        constexpr int kLog = (int)(sizeof(LogTableD) / 16);
+        constexpr int kPer = (kImg + kLog + kStepBlock - 1) / kStepBlock;
+        using V4 = __attribute__((ext_vector_type(4))) unsigned int;
+        const PD_AS1 V4* img = (const PD_AS1 V4*)P.stage_img;
+        const PD_AS1 V4* lgt = (const PD_AS1 V4*)(uint64_t)&P.logtab_d.cell[0];
+        V4 v[kPer];
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) {
+            const int t = threadIdx.x + k * kStepBlock;
+            if (t < kImg) v[k] = img[t];
+            else if (t < kImg + kLog) v[k] = lgt[t - kImg];
+        }
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) {
+            const int t = threadIdx.x + k * kStepBlock;
+            if (t < kImg) ((V4*)static_cast<StepStatic<R, WIND>*>(&L))[t] = v[k];
+            else if (t < kImg + kLog) ((V4*)s_logtab)[t - kImg] = v[k];
+        }
+        if (threadIdx.x < (kStepBlock / 64) * kNWork) (&L.work[0][0])[threadIdx.x] = 0u;
+        if (threadIdx.x < 2) L.tdesc[threadIdx.x] = tab_view<R>(P, L.tab, (int)threadIdx.x);
+    }
+    __syncthreads();
+    PD_T(t_staged);
+    PD_ACC(0, t_staged - t_start);
+    if constexpr (POL) {
+        // a wave whose envs have all finished leaves (wave-uniform, after the only barrier)
+        if (!a.use_list && __ballot(live) == 0) return;
     }
     // PHASE 2 = the other compile_physics phases, chosen at run time by P.phase (wave-uniform)
     const int aux = PHASE == 2 ? params<R>(a.P)->phase : PHASE;
@@ -1375,18 +1398,22 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(2)))
     R gdeg_out = e.act0, dcmdl_out = e.act1, dcmdr_out = e.act2;
     const R gprev = e.act0, dlprev = e.act1, drprev = e.act2;
     bool nan_hit = false;
-    // info tap (single-step launches): the last sub-step's quantities (rockets_physics.py:649-702)
+    // info tap: the last sub-step's quantities (rockets_physics.py:649-702) of the fields in
+    // info_mask, row f of the [n_fused][nsel][N] array (pd_step: every field, one row)
     const bool tap = a.info != nullptr && role == 0 && live;
     // (the lane offset is laundered per use so that the 49 loop-invariant store addresses are
     // formed inside the taken branch, not hoisted out of the loops and kept live: 92 VGPRs)
     // (and the row base is laundered too: hoisted, the 49 uniform row bases a.info + k N were
     // kept in scalar registers -- spilled into VGPR lanes from the prologue on)
     auto info = [&](int k, R v) {
+        const uint64_t m = a.info_mask;
+        if (!((m >> k) & 1ull)) return;   // (uniform)
+        const size_t row = (size_t)f * (size_t)a.info_nsel + (size_t)__popcll(m & ((1ull << k) - 1ull));
         uint32_t u = ui;
         uint32_t blo = (uint32_t)(uint64_t)a.info, bhi = (uint32_t)((uint64_t)a.info >> 32);
         asm volatile("" : "+v"(u), "+s"(blo), "+s"(bhi));
         R* base = (R*)(((uint64_t)bhi << 32) | blo);
-        ev(base + (size_t)k * (size_t)N, u) = v;
+        ev(base + row * (size_t)N, u) = v;
     };
 
     bool wpre = false;   // the odd sub-step's gust normals are in L.wnx (drawn with the even one's)
@@ -2029,7 +2056,7 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(2)))
         if (a.done) ev(a.done + fo, ui) = (uint8_t)dn;
         if (a.trunc) ev(a.trunc + fo, ui) = (uint8_t)tr;
         if (a.trunc_id) ev(a.trunc_id + fo, ui) = (int8_t)id;
-        if (a.info) ev(a.info + (PD_INFO_GLOAD) * N, uo) = gl;
+        if (a.info) info(PD_INFO_GLOAD, gl);
         if (SAC && a.slab) {
             // state | action | reward | next_state (terminal, before any reset) | done: the
             // replay buffer's row (sac_pytorch.py:27-35; done without truncation, as the driver

@@ -835,6 +835,10 @@ struct CellPieces {
     std::vector<int> sub_piece;       // [refined][S][S] piece of an exact sub-cell's key (-1 none)
     std::vector<int> bis_a, bis_b;    // per GridKeys bisector record: each trusted side's piece
     std::vector<uint32_t> fine;       // [nm S][na S] fine index (pd_step.h kFinePiece)
+    // the two-level form of the same index (PD_IDX2): one word per cell -- an exact cell's fine
+    // word (its piece, or 0), or kFineRefined | the refined cell's number -- and the refined
+    // cells' sub-cell words, [refined][S][S]
+    std::vector<uint32_t> cellw, rfine, cellw32, rfine32;
     double max_rel = 0, build_s = 0;
     int64_t pieces = 0, rejected = 0;
     std::vector<double> err;          // per piece: the binary64 check's error (INFINITY: unused slot)
@@ -1093,6 +1097,24 @@ void build_fine(const CellPieces& cp, const std::vector<uint8_t>& cell_ok, const
     });
 }
 
+// The two-level index from the fine index (CellPieces::cellw / rfine): the same words
+void build_cell_index(const CellPieces& cp, const std::vector<uint32_t>& fine, std::vector<uint32_t>& cellw,
+                      std::vector<uint32_t>& rfine) {
+    const int S = kGridSub, nm = cp.nm, na = cp.na;
+    int64_t nr = 0;
+    for (int v : cp.ridx) nr = std::max<int64_t>(nr, (int64_t)v + 1);
+    cellw.assign((size_t)nm * na, 0u);
+    rfine.assign((size_t)std::max<int64_t>(nr, 1) * S * S, 0u);
+    for (int64_t c = 0; c < (int64_t)nm * na; ++c) {
+        const int64_t im = c / na, ia = c % na;
+        if (!cp.refined[c]) { cellw[c] = fine[(size_t)(im * S) * ((size_t)na * S) + (size_t)ia * S]; continue; }
+        cellw[c] = kFineRefined | (uint32_t)cp.ridx[c];
+        for (int jm = 0; jm < S; ++jm)
+            for (int ja = 0; ja < S; ++ja)
+                rfine[(size_t)cp.ridx[c] * S * S + jm * S + ja] = fine[(size_t)(im * S + jm) * ((size_t)na * S) + (size_t)ia * S + ja];
+    }
+}
+
 const CellPieces& cell_pieces(const pd_aero_table& t, double a0, double a1, int nm, int na) {
     static std::mutex mu;
     static std::map<uint64_t, CellPieces> cache;
@@ -1201,6 +1223,7 @@ const CellPieces& cell_pieces(const pd_aero_table& t, double a0, double a1, int 
             }
     }
     build_fine(cp, cp.cell_ok, cp.sub_piece, cp.fine);
+    build_cell_index(cp, cp.fine, cp.cellw, cp.rfine);
     cp.build_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     return cp;
 }
@@ -1247,38 +1270,44 @@ void ensure_f32(CellPieces& cp) {
         else ++cp.rejected32;
     }
     build_fine(cp, cp.cell_ok32, cp.sub_piece32, cp.fine32);
+    build_cell_index(cp, cp.fine32, cp.cellw32, cp.rfine32);
     cp.have32 = true;
 }
 
 // The device copy of a table's cell pieces: one per device and process, shared read-only by the
 // handles (never freed; ~0.2 GB of the 288 GB)
 template <typename R>
-pd_status cell_pieces_device(const CellPieces& cp, const R** rec, const int** sub, const uint32_t** fine) {
+pd_status cell_pieces_device(const CellPieces& cp, const R** rec, const int** sub, const uint32_t** fine,
+                             const uint32_t** cellw, const uint32_t** rfine) {
     static std::mutex mu;
-    static std::map<std::pair<const void*, int>, std::array<void*, 3>> m;
+    static std::map<std::pair<const void*, int>, std::array<void*, 5>> m;
     const bool f32 = sizeof(R) == 4;
     const auto& rv = f32 ? (const void*)cp.rec32.data() : (const void*)cp.rec.data();
     const size_t rbytes = f32 ? cp.rec32.size() * 4 : cp.rec.size() * 8;
     const std::vector<int>& sp = f32 ? cp.sub_piece32 : cp.sub_piece;
     const std::vector<uint32_t>& fn = f32 ? cp.fine32 : cp.fine;
+    const std::vector<uint32_t>& cw = f32 ? cp.cellw32 : cp.cellw;
+    const std::vector<uint32_t>& rf = f32 ? cp.rfine32 : cp.rfine;
     int dev = 0;
     PD_HIP(hipGetDevice(&dev));
     std::lock_guard<std::mutex> lock(mu);
     auto k = std::make_pair((const void*)(f32 ? (const void*)&cp.rec32 : (const void*)&cp.rec), dev);
     auto it = m.find(k);
     if (it == m.end()) {
-        void *dr = nullptr, *ds = nullptr, *df = nullptr;
-        PD_HIP(hipMalloc(&dr, std::max<size_t>(rbytes, 8)));
-        PD_HIP(hipMalloc(&ds, std::max<size_t>(sp.size(), 1) * 4));
-        PD_HIP(hipMalloc(&df, std::max<size_t>(fn.size(), 1) * 4));
-        if (rbytes) PD_HIP(hipMemcpy(dr, rv, rbytes, hipMemcpyHostToDevice));
-        if (!sp.empty()) PD_HIP(hipMemcpy(ds, sp.data(), sp.size() * 4, hipMemcpyHostToDevice));
-        if (!fn.empty()) PD_HIP(hipMemcpy(df, fn.data(), fn.size() * 4, hipMemcpyHostToDevice));
-        it = m.emplace(k, std::array<void*, 3>{dr, ds, df}).first;
+        std::array<void*, 5> d{};
+        const void* src[5] = {rv, sp.data(), fn.data(), cw.data(), rf.data()};
+        const size_t nb[5] = {rbytes, sp.size() * 4, fn.size() * 4, cw.size() * 4, rf.size() * 4};
+        for (int q = 0; q < 5; ++q) {
+            PD_HIP(hipMalloc(&d[q], std::max<size_t>(nb[q], 8)));
+            if (nb[q]) PD_HIP(hipMemcpy(d[q], src[q], nb[q], hipMemcpyHostToDevice));
+        }
+        it = m.emplace(k, d).first;
     }
     *rec = (const R*)it->second[0];
     *sub = (const int*)it->second[1];
     *fine = (const uint32_t*)it->second[2];
+    *cellw = (const uint32_t*)it->second[3];
+    *rfine = (const uint32_t*)it->second[4];
     return PD_OK;
 }
 
@@ -1598,9 +1627,10 @@ template <typename R> pd_status create_impl(const pd_params* p, const pd_config*
     if ((st = build_grid<R>(p->cl, ga0[1], ga1[1], gnm[1], gna[1], tcl, gk[1], gs[1], sk[1], ss[1], bs[1], cps[1])) != PD_OK) return st;
     // the fine index (PD_TABLES_NO_FINE_INDEX: cell and sub-cell records only)
     for (int tb = 0; tb < 2; ++tb) {
-        D.cell_pc[tb] = nullptr; D.sub_piece[tb] = nullptr; D.fine[tb] = nullptr;
-        if (cps[tb] && (st = cell_pieces_device<R>(*cps[tb], &D.cell_pc[tb], &D.sub_piece[tb], &D.fine[tb])) != PD_OK) return st;
-        if (c->table_flags & PD_TABLES_NO_FINE_INDEX) D.fine[tb] = nullptr;
+        D.cell_pc[tb] = nullptr; D.sub_piece[tb] = nullptr; D.fine[tb] = nullptr; D.cellw[tb] = nullptr; D.rfine[tb] = nullptr;
+        if (cps[tb] && (st = cell_pieces_device<R>(*cps[tb], &D.cell_pc[tb], &D.sub_piece[tb], &D.fine[tb], &D.cellw[tb],
+                                                   &D.rfine[tb])) != PD_OK) return st;
+        if (c->table_flags & PD_TABLES_NO_FINE_INDEX) { D.fine[tb] = nullptr; D.cellw[tb] = nullptr; D.rfine[tb] = nullptr; }
     }
     if (verbose)
         for (int tb = 0; tb < 2; ++tb) {
@@ -1776,7 +1806,7 @@ struct SacIO {
 template <typename R>
 pd_status step_impl(pd_env* e, const void* actions, void* obs, void* reward, uint8_t* done, uint8_t* trunc,
                     int8_t* tid, const double* noise, void* info, void* reward_sum, hipStream_t s,
-                    int n_fused = 1, const SacIO* sac = nullptr) {
+                    int n_fused = 1, const SacIO* sac = nullptr, uint64_t info_mask = (1ull << PD_N_INFO) - 1ull) {
     // every caller's launch needs its inputs: actions (plain steps), the heads or the actor (SAC);
     // the public entry points check them too, this keeps an internal caller from launching a
     // kernel that would read through a null pointer
@@ -1790,6 +1820,7 @@ pd_status step_impl(pd_env* e, const void* actions, void* obs, void* reward, uin
     StepArgs<R> a = make_args<R>(e);
     a.actions = actions; a.obs = (R*)obs; a.reward = (R*)reward; a.done = done; a.trunc = trunc; a.trunc_id = tid;
     a.noise = noise; a.info = (R*)info; a.reward_sum = (R*)reward_sum;
+    a.info_mask = info_mask; a.info_nsel = __builtin_popcountll(info_mask);
     a.n_fused = n_fused;
     if (sac) {
         a.sac_mean = sac->mean; a.sac_logstd = sac->log_std; a.sac_eps = sac->eps;
@@ -1895,10 +1926,12 @@ pd_status rollout_policy_impl(pd_env* e, const float* w, int32_t max_steps, void
 // n_steps env-steps in launches of pd_tuning.step_fuse fused steps, each followed by the miss flush.
 // Row t of every [n_steps][N...] array belongs to step t; NULL outputs are not written.
 pd_status step_n_impl(pd_env* e, const void* actions, int32_t n_steps, void* obs, void* reward, uint8_t* done,
-                      uint8_t* trunc, int8_t* tid, void* reward_sum, hipStream_t s) {
+                      uint8_t* trunc, int8_t* tid, void* reward_sum, hipStream_t s, void* info = nullptr,
+                      uint64_t info_mask = 0) {
     const size_t N = (size_t)e->cfg.n_envs;
     const size_t sa = N * e->act_dim * (e->cfg.action_f64 ? 8 : 4), so = N * e->obs_dim * e->rsize;
     const size_t sr = N * e->rsize;
+    const size_t si = N * e->rsize * (size_t)__builtin_popcountll(info_mask);   // one step's info rows
     const int K = e->tune.step_fuse;
     for (int32_t t = 0; t < n_steps; t += K) {
         const int k = n_steps - t < K ? n_steps - t : K;
@@ -1906,9 +1939,9 @@ pd_status step_n_impl(pd_env* e, const void* actions, int32_t n_steps, void* obs
         const void* act = (const char*)actions + sa * t;
         pd_status st = e->rsize == 8
             ? step_impl<double>(e, act, at(obs, so), at(reward, sr), (uint8_t*)at(done, N), (uint8_t*)at(trunc, N),
-                                (int8_t*)at(tid, N), nullptr, nullptr, reward_sum, s, k)
+                                (int8_t*)at(tid, N), nullptr, at(info, si), reward_sum, s, k, nullptr, info_mask)
             : step_impl<float>(e, act, at(obs, so), at(reward, sr), (uint8_t*)at(done, N), (uint8_t*)at(trunc, N),
-                               (int8_t*)at(tid, N), nullptr, nullptr, reward_sum, s, k);
+                               (int8_t*)at(tid, N), nullptr, at(info, si), reward_sum, s, k, nullptr, info_mask);
         if (st != PD_OK) return st;
         if ((st = pd_flush_misses(e, s)) != PD_OK) return st;
     }
@@ -2201,6 +2234,18 @@ pd_status pd_step_n(pd_env* e, const void* actions, int32_t n_steps, void* obs, 
         return fail(PD_ERR_UNSUPPORTED, "pd_step_n: landing-burn phases only (use pd_step)");
     PD_HIP(hipSetDevice(e->device));
     return step_n_impl(e, actions, n_steps, obs, reward, done, truncated, trunc_id, nullptr, (hipStream_t)stream);
+}
+
+pd_status pd_step_n_info(pd_env* e, const void* actions, int32_t n_steps, void* obs, void* reward, uint8_t* done,
+                         uint8_t* truncated, int8_t* trunc_id, void* info, uint64_t info_mask, void* stream) {
+    if (!e || !actions || n_steps < 0) return fail(PD_ERR_INVALID, "bad step_n_info args");
+    if (e->cfg.phase != PD_PHASE_PURE_THROTTLE && e->cfg.phase != PD_PHASE_LANDING_BURN)
+        return fail(PD_ERR_UNSUPPORTED, "pd_step_n_info: landing-burn phases only (use pd_step)");
+    if (info && (info_mask == 0 || (info_mask >> PD_N_INFO) != 0))
+        return fail(PD_ERR_INVALID, "pd_step_n_info: info_mask must select 1..PD_N_INFO fields of pd_info_field");
+    PD_HIP(hipSetDevice(e->device));
+    return step_n_impl(e, actions, n_steps, obs, reward, done, truncated, trunc_id, nullptr, (hipStream_t)stream,
+                       info, info ? info_mask : 0);
 }
 
 pd_status pd_rollout(pd_env* e, const void* actions, int32_t n_steps, void* reward_sum, void* stream) {

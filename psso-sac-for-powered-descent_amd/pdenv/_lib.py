@@ -98,7 +98,7 @@ EXPORTS = ["pd_abi_version", "pd_sizeof_params", "pd_sizeof_config", "pd_last_er
            "pd_checkpoint_load", "pd_counters", "pd_stats", "pd_count_work", "pd_atmosphere", "pd_obs_dim",
            "pd_action_dim", "pd_step_sac", "pd_pso_swarm_minima", "pd_pso_update_bests", "pd_cell_piece_info",
            "pd_step_sac_ring", "pd_sac_actor", "pd_step_sac_fused", "pd_atm_table", "pd_set_tuning", "pd_get_tuning",
-           "pd_pso_swarm_minima_scratch_bytes"]
+           "pd_pso_swarm_minima_scratch_bytes", "pd_step_n_info"]
 ABI_VERSION = 9
 
 _lib = None
@@ -127,6 +127,8 @@ def load(path=None):
     L.pd_reset.argtypes = [vp, vp, vp, vp]
     L.pd_step.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
     L.pd_step_n.argtypes = [vp, vp, I32, vp, vp, vp, vp, vp, vp]
+    L.pd_step_n_info.argtypes = [vp, vp, I32, vp, vp, vp, vp, vp, vp, U64, vp]
+    L.pd_step_n_info.restype = C.c_int
     F32 = C.c_float
     L.pd_step_sac.argtypes = [vp, vp, vp, I32, vp, F32, F32, F32, vp, vp, vp, vp]
     L.pd_step_sac_ring.argtypes = [vp, vp, I32, F32, F32, F32, vp, vp, vp, I64, vp, vp, vp, vp, vp]

@@ -274,12 +274,14 @@ class PoweredDescentEnv:
         L.check(self.lib.pd_rollout(self.h, _ptr(a), int(T), _ptr(rs), _stream(self.device)))
         return rs
 
-    def step_n(self, actions, outputs=True):
+    def step_n(self, actions, outputs=True, info_keys=None):
         """T consecutive env-steps over device-resident actions [T, N, A] (pd_step_n: fused
         launches of up to 128 steps each, then the miss flush), the same results as T step()
         calls.  Landing-burn phases only.  outputs=True returns per-step
         (obs [T, N, O], reward [T, N], done [T, N], truncated [T, N], trunc_id [T, N]);
-        outputs=False writes nothing per step and returns None."""
+        outputs=False writes nothing per step and returns None.  info_keys: names of
+        L.INFO_FIELDS to tap in the fused launches (pd_step_n_info); the result then ends with a
+        dict of [T, N] tensors, one per key."""
         self._check_steppable()
         a = actions.to(device=self.device, dtype=self.action_dtype).contiguous()
         self._check_actions(a)
@@ -294,13 +296,22 @@ class PoweredDescentEnv:
             ptrs = [_ptr(x) for x in (obs, rew, dn, tr, tid)]
         else:
             ptrs = [None] * 5
-        L.check(self.lib.pd_step_n(self.h, _ptr(a), T, *ptrs, _stream(self.device)))
+        if info_keys:
+            idx = sorted(L.INFO_FIELDS.index(k) for k in info_keys)
+            mask = sum(1 << j for j in idx)
+            inf = torch.empty(T, len(idx), self.n, dtype=self.dtype, device=self.device)
+            L.check(self.lib.pd_step_n_info(self.h, _ptr(a), T, *ptrs, _ptr(inf), mask, _stream(self.device)))
+        else:
+            L.check(self.lib.pd_step_n(self.h, _ptr(a), T, *ptrs, _stream(self.device)))
         self._steps += T
+        tap = {L.INFO_FIELDS[j]: inf[:, r] for r, j in enumerate(idx)} if info_keys else None
         if outputs:
             if T > 0:   # the handle's step buffers (obs_buf, ...) hold the last step, as after step()
                 for dst, src in zip((self._obs, self._rew, self._done, self._trunc, self._tid), (obs, rew, dn, tr, tid)):
                     dst.copy_(src[-1])
-            return obs, rew, dn.bool(), tr.bool(), tid
+            res = (obs, rew, dn.bool(), tr.bool(), tid)
+            return res + (tap,) if info_keys else res
+        return tap
 
     def step_n_raw(self, actions, outputs=None):
         """Hot-loop pd_step_n: actions a contiguous [T, N, A] device tensor of action_dtype (the

@@ -319,7 +319,7 @@ def test_wind_injected_noise_vs_oracle(pd, oracle_mod):
 
 def test_f32_teacher_forced(pd):
     """fp32 handle: one step from the reference's recorded states vs the reference, every channel
-    (SURVEY 8(d)'s fp32 tolerance, 1e-5 of max(|x|, 1); theta_dot 1e-4).  The handle computes its
+    (SURVEY 8(d)'s fp32 tolerance, 1e-5 of max(|x|, 1); theta_dot 2.5e-4, test_c3_f32_handle_shadowed).  The handle computes its
     forces in binary32 and integrates the state chain in binary64 within the step (alpha_eff =
     gamma - theta - pi from binary64 angles), so what is left is the binary32 rounding of the
     inputs and the forces."""
@@ -338,7 +338,7 @@ def test_f32_teacher_forced(pd):
         worst = dict(zip(ST, err.max(0).tolist()))
         print(f"f32 teacher-forced {tag}:", worst)
         tol = np.full(11, 1e-5)
-        tol[5] = 1e-4
+        tol[5] = 2.5e-4
         assert (err.max(0) <= tol).all(), (tag, worst)
 
 
@@ -1079,3 +1079,31 @@ def test_launcher_refuses_mismatched_inputs(pd):
     env.step(torch.zeros(256, 1, device="cuda"))
     torch.cuda.synchronize()
     assert torch.isfinite(env.state).all()
+
+
+@pytest.mark.parametrize("precision", ["f64", "f32"])
+def test_step_n_info_tap_matches_step(pd, precision):
+    """The info tap in fused launches (pd_step_n_info, a key mask): 40 steps of 512 envs with wind,
+    gusts, tilt and auto-reset through two fused launches (step_fuse 24) with a subset of the keys
+    equal, bit for bit, to the same keys of 40 pd_step calls with the full tap; the states too."""
+    import torch
+    N, T = 512, 40
+    g = torch.Generator(device="cuda").manual_seed(41)
+    A = torch.rand(T, N, 1, device="cuda", generator=g) * 2 - 1
+    A[:, : N // 2] = A[:, : N // 2] * 0.25 + 0.75
+    kw = dict(precision=precision, lanes_per_env=2, enable_wind=True, stochastic_wind=True, wind_percentile=None,
+              auto_reset=True, tilt_sigma_rad=0.02, seed=17)
+    keys = ["air_density", "mach_number", "CL", "CD", "alpha_effective", "g_load_1_sec_window", "ug", "vg",
+            "theta_dot_dot", "gf_Mz", "theta_in"]
+    one, fused = make(pd, N, **kw), make(pd, N, **kw)
+    fused.set_tuning(step_fuse=24)
+    ref = {k: [] for k in keys}
+    for t in range(T):
+        *_, ex = one.step(A[t], info=True)
+        for k in keys:
+            ref[k].append(ex[k].clone())
+    obs, rew, dn, tr, tid, tap = fused.step_n(A, info_keys=keys)
+    assert set(tap) == set(keys)
+    for k in keys:
+        assert torch.equal(tap[k], torch.stack(ref[k])), k
+    assert torch.equal(one.state, fused.state)

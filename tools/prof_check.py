@@ -34,8 +34,9 @@ def check(trace, line):
         for rng in ("timed", "replay"):
             a, b = li[rng]
             sel = d[a:b]
+            reps = li.get("replays", 1) if rng == "replay" else 1     # (the replay range holds every replay)
             res[rng] = {"launches": len(sel), "rocprof_total_ms": sum(sel),
-                        "rocprof_ms_per_step": sum(sel) / steps,
+                        "rocprof_ms_per_step": sum(sel) / steps / reps,
                         "rocprof_avg_ms_per_launch": sum(sel) / len(sel) if sel else None}
         rf = part["roofline"]
         res["line_kernel_ms_per_step"] = rf["kernel_ms_per_step"]

@@ -9,6 +9,7 @@
 #   3: the binary32 handle with the binary64 state chain: its tests and timing.
 #   4: c3 / c3-descent traffic and time with and without the fine index (PMC passes).
 #   5: the suite, smoke, fixed cost, driver command, c5 and c4-262k on the round-5 build.
+#   6: the suite, smoke, c5 breakdown, fixed cost and driver command of the reordered prologue, then 4.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -53,11 +54,19 @@ case "${PART:-1}" in
   ;;
 4)
   # where c3-descent's traffic comes from: the fine index against the cell / sub-cell records
-  # (PD_TABLES_NO_FINE_INDEX = 2), c3 and c3-descent, PMC traffic + L2 hits, then the timing
-  CASES="d_fine:1:0 d_rec:1:2 c_fine:0:0 c_rec:0:2" run pmc5 900 bash tools/pmc_r05.sh
-  for c in "1 0" "1 2" "0 0" "0 2"; do
-    set -- $c
-    DESCENT=$1 TABLE_FLAGS=$2 BURN=640 FUSE=128 LAUNCHES=6 run t_d$1_f$2 200 python tools/time_fused.py
+  # (PD_TABLES_NO_FINE_INDEX = 2) and against the two-level index (libpdenv_idx2.so: a word per
+  # cell, L2-resident, and the refined cells' sub-cell words), c3 and c3-descent: the variant's
+  # bit-identity tests, PMC traffic + L2 hits, then the timing (two interleaved rounds)
+  V=psso-sac-for-powered-descent_amd/pdenv/libpdenv_idx2.so
+  PDENV_LIB=$V run idx2_tests 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_c3.py -m gpu -x -q \
+      --timeout 300 --timeout-method thread -k "fine_index or c3_shadowed or cell_pieces"
+  CASES="d_fine:1:0 d_rec:1:2 d_idx2:1:0:$V c_fine:0:0 c_idx2:0:0:$V" run pmc5 900 bash tools/pmc_r05.sh
+  for r in 1 2; do
+    for c in "1 0 base" "1 0 idx2" "0 0 base" "0 0 idx2" "1 2 base"; do
+      set -- $c
+      lib=psso-sac-for-powered-descent_amd/pdenv/libpdenv.so; [ "$3" = idx2 ] && lib=$V
+      PDENV_LIB=$lib DESCENT=$1 TABLE_FLAGS=$2 BURN=640 FUSE=128 LAUNCHES=6 run t4_r${r}_d$1_f$2_$3 200 python tools/time_fused.py
+    done
   done
   ;;
 5)
@@ -75,6 +84,20 @@ case "${PART:-1}" in
   run benchdrv5 300 python bench.py --steps 20 --warmup 5
   run c5_5 300 python bench.py --workload c5
   run c4_262k_5 300 python bench.py --workload c4 --particles 262144 --steps 6 --warmup 2 --policy-list 0
+  ;;
+6)
+  # the build with the env state requested ahead of the table staging (and of the SAC actor):
+  # the GPU suite and the smoke, the c5 breakdown, the fixed cost, the driver's command; then
+  # part 4 (the index experiment)
+  run gpu_tests 1000 python -u -m pytest tests/ -m gpu -x -q --timeout 300 --timeout-method thread -s
+  run smoke 200 python -c "import __graft_entry__ as g; g.smoke()"
+  run c5_breakdown 300 python tools/c5_breakdown.py
+  for f in 20 1; do
+    L=$(( f >= 20 ? 6 : 24 ))
+    BURN=640 FUSE=$f LAUNCHES=$L run fix6_f$f 200 python tools/time_fused.py
+  done
+  run benchdrv6 300 python bench.py --steps 20 --warmup 5
+  PART=4 bash tools/r05_session.sh
   ;;
 esac
 echo "=== done"
