@@ -229,7 +229,7 @@ def bench_pso(args, world, rank, local, dist):
     P = args.particles
     opt = ParticleSubswarmOptimisationGPU("landing_burn", pop_size=P * world, device=local, seed=1234,
                                           precision=args.precision, dist=dist,
-                                          tuning=dict(policy_list=args.policy_list),
+                                          tuning=dict(policy_list=args.policy_list, policy_refill=args.policy_refill),
                                           pso_params=dict(generations=args.warmup + args.steps,
                                                           re_initialise_generation=-1))
     for g in range(args.warmup):
@@ -547,6 +547,8 @@ def main():
                     help="c3: env-steps per k_step launch (pd_step_n; 1 = one pd_step launch per step)")
     ap.add_argument("--policy-list", type=int, default=-1, choices=[-1, 0, 1],
                     help="c4: the policy rollouts' live-list launches (pd_tuning.policy_list: -1 auto, 0 off, 1 on)")
+    ap.add_argument("--policy-refill", type=int, default=-1,
+                    help="c4: refill rollouts (pd_tuning.policy_refill: -1 auto, 0 off, k = batch of k waiting slots)")
     ap.add_argument("--graph", type=int, default=1, help="c5: replay the collection step as a HIP graph")
     ap.add_argument("--c3-burn-in", type=int, default=C3_BURN_IN,
                     help="c3: untimed env-steps before the warmup (steady state: resets at their stationary rate)")

@@ -173,6 +173,12 @@ typedef struct {
                                  one chip round (default), 0 = never, 1 = from the first launch */
     double policy_list_at;    /* > 0 (with policy_list -1 or 0): switch the list on once the live count
                                  read back falls to this fraction of n_envs (default 0: never) */
+    int32_t policy_refill;    /* refill rollouts: -1 = when n_envs exceeds the chip's resident env slots
+                                 (default, batch: half a wave's slots), 0 = never, k in 1..64 = always, batch k.  One launch of
+                                 policy_slots env slots (0: the resident capacity) steps the whole swarm:
+                                 an ended episode's lanes wait until k of their wave's slots wait (or none
+                                 is live), then take the next particles (a wave ballot, one atomic) */
+    int32_t policy_slots;     /* env slots of a refill rollout (0 = the chip's resident capacity) */
 } pd_tuning;
 
 /* Info tap of pd_step: the quantities of the LAST physics sub-step that rocket_physics_fcn puts in

@@ -166,8 +166,6 @@ template <typename R> struct DevParams {
     const R* cell_pc[2];
     const int* sub_piece[2];
     const uint32_t* fine[2];           // fine index (pd_step.h kFinePiece; nullptr: none)
-    const uint32_t* cellw[2];          // its two-level form: a word per cell, then the refined cells' (pdenv.hip)
-    const uint32_t* rfine[2];
     R line_bp[4][kLineMax];
     int line_slot[4][kLineMax + 1];
     unsigned long long line_key[4][kLineMax + 1];

@@ -255,6 +255,13 @@ template <typename R> struct StepArgs {
     // list launches of a policy rollout: the live envs' parameters in list order, [P][N] (the
     // launch copies them there once, so that its fused steps read them coalesced, not gathered)
     float* policy_wc;
+    // refill rollouts (pd_tuning.policy_refill): the grid holds refill_base env slots; an env whose
+    // episode ends (or reaches refill_max steps) is stored and its lanes wait for the next particle,
+    // which a wave hands out once `refill` of its slots wait (or none is live): refill_base + the
+    // launch's count of handed-out particles so far (*refill_next, one atomic per hand-out), until
+    // every particle of the swarm has run
+    uint32_t* refill_next;
+    int refill, refill_base, refill_max;
 };
 
 // Kernel launchers, explicitly instantiated in the kstep_*.hip translation units.

@@ -66,8 +66,6 @@ template <typename R> struct TabView {
     const PD_AS1 R* cell_pc;        // cell pieces (cell_stride<R>() words each; nullptr: none)
     const PD_AS1 int* sub_piece;
     const PD_AS1 uint32_t* fine;    // fine index (nullptr: none)
-    const PD_AS1 uint32_t* cellw;   // its two-level form (PD_IDX2)
-    const PD_AS1 uint32_t* rfine;
     int grid_nm, grid_na;
     R grid_a0, grid_inv_da, grid_inv_dm;
 };
@@ -437,11 +435,6 @@ __device__ __forceinline__ int rbf_lookup(const AT& a, DP<R>& P, int table, cons
     const bool fine_path = tay != nullptr && t.fine != nullptr;
     uint32_t fe = 0u;
     R fsm = R(0), fsa = R(0);
-#ifndef PD_IDX2
-#define PD_IDX2 0
-#endif
-    uint32_t fsub = 0u;
-    (void)fsub;
     if (use_grid) {
         R fm = M * t.grid_inv_dm, fa = (aq - t.grid_a0) * t.grid_inv_da;
         int im = fm < R(0) ? 0 : (fm >= R(t.grid_nm) ? t.grid_nm - 1 : (int)fm);
@@ -454,14 +447,7 @@ __device__ __forceinline__ int rbf_lookup(const AT& a, DP<R>& P, int table, cons
             int jm = (int)sm, ja = (int)sa;
             jm = jm < 0 ? 0 : (jm > kGridSub - 1 ? kGridSub - 1 : jm);
             ja = ja < 0 ? 0 : (ja > kGridSub - 1 ? kGridSub - 1 : ja);
-#if PD_IDX2
-            // the cell's word (the per-cell array stays in L2); a refined cell's sub-cell word
-            // below, once the cell word has said which refined cell it is
-            fe = t.cellw[gcell];
-            fsub = (uint32_t)(jm * kGridSub + ja);
-#else
             fe = t.fine[(uint32_t)(im * kGridSub + jm) * (uint32_t)(t.grid_na * kGridSub) + (uint32_t)(ia * kGridSub + ja)];
-#endif
             fsm = sm - (R)jm; fsa = sa - (R)ja;
         } else {
             gkey = t.grid_key[gcell];
@@ -505,10 +491,6 @@ __device__ __forceinline__ int rbf_lookup(const AT& a, DP<R>& P, int table, cons
             // Binary32 handles: 1e-4 cell widths as their record path, and 1e-3 sub-cell widths
             // (the binary32 position's rounding is ~5e-5 cell widths at the grid's far end)
             const R eps = sizeof(R) == 8 ? R(1e-9) : R(1e-4), eps_sub = sizeof(R) == 8 ? R(1e-9) : R(1e-3);
-#if PD_IDX2
-            if ((fe & kFineRefined) && !(fe & (kFinePiece | kFineBisect)))
-                fe = t.rfine[(fe & kFineIndex) * (uint32_t)(kGridSub * kGridSub) + fsub];
-#endif
             const bool inside = (fe & kFineRefined)
                 ? (fsm > eps_sub && R(1) - fsm > eps_sub && fsa > eps_sub && R(1) - fsa > eps_sub)
                 : (um > eps && R(1) - um > eps && ua > eps && R(1) - ua > eps);
@@ -1053,8 +1035,6 @@ __device__ __forceinline__ TabView<R> tab_view(DP<R>& P, const R* tab, int table
     t.cell_pc = gbl(P.cell_pc[table]);
     t.sub_piece = gbl(P.sub_piece[table]);
     t.fine = gbl(P.fine[table]);
-    t.cellw = gbl(P.cellw[table]);
-    t.rfine = gbl(P.rfine[table]);
     t.grid_nm = P.grid_nm[table];
     t.grid_na = P.grid_na[table];
     t.grid_a0 = P.grid_a0[table];
@@ -1096,6 +1076,9 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(2)))
     if constexpr (SAC) { if (a.ring_state) ring_pos0 = (int64_t)__atomic_load_n(a.ring_state, __ATOMIC_RELAXED); }
     if constexpr (POL) {
         if (blockIdx.x == 0 && threadIdx.x == 0) *a.cnt_zero = 0u;
+        // (refill: the grid's first refill_base envs are the slots; the rest of its last
+        // workgroup runs private copies, as past the end of any grid)
+        if (a.refill) n_act = a.refill_base;
         if (a.use_list) {
             n_act = (int64_t)*a.cnt_in;
             if ((int64_t)blockIdx.x * EPB >= n_act) return;
@@ -1105,12 +1088,15 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(2)))
     const int64_t gt = (int64_t)blockIdx.x * kStepBlock + threadIdx.x;
     // Every lane stays active (the cooperative miss solve needs converged waves).  Lanes past the
     // end run a private copy of the initial state (no loads of another env's state, no stores).
-    const bool valid = gt / LPE < n_act;
-    const int64_t e_act = valid ? gt / LPE : n_act - 1;
-    const int64_t i = (POL && a.use_list) ? (int64_t)a.list_in[e_act] : e_act;
+    // (mutable: a refill rollout hands the lanes of an ended episode the next particle)
+    bool valid = gt / LPE < n_act;
+    const bool slot = valid;   // (refill: the lanes of one of the launch's env slots)
+    bool drained = false;      // (refill: the swarm's particles all handed out; wave-uniform)
+    int64_t e_act = valid ? gt / LPE : n_act - 1;
+    int64_t i = (POL && a.use_list) ? (int64_t)a.list_in[e_act] : e_act;
     const int role = (int)(gt % LPE);
     const int le = (int)threadIdx.x / LPE;   // the env's column of the workgroup's LDS g-load ring
-    const uint32_t ui = (uint32_t)i;   // N <= 2^25 (validated): 32-bit per-lane byte offsets
+    uint32_t ui = (uint32_t)i;   // N <= 2^25 (validated): 32-bit per-lane byte offsets
     // POL (policy rollout): with the list, only live envs are stepped; without it, finished
     // envs stay frozen and a wave with none left exits (wave-uniform, after the only barrier)
     bool live = valid;
@@ -1122,14 +1108,14 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(2)))
     const int my_table = LPE >= 2 ? role / nparts : 0;   // 0 = C_D, 1 = C_L
     const int part = LPE >= 2 ? role % nparts : 0;
     const int gbase = (int)__lane_id() & ~(LPE - 1);
-    const uint64_t g = a.env_offset + (uint64_t)i;
+    uint64_t g = a.env_offset + (uint64_t)i;
 
     // ---- the env's state into registers (its g-load ring into LDS; the ring is not part of the
     // staged tables, so its stores may precede the staging barrier): requested ahead of the actor
     // prologue and the table staging, whose latencies then overlap it
     EnvRegs<R> e;
     RbfCache<R> cA, cB;   // LPE 1: A = C_D, B = C_L; LPE >= 2: A = own table
-    {
+    auto load_env = [&]() {
         DP<R>& P = *params<R>(a.P);
 #pragma unroll
         for (int k = 0; k < 11; ++k) e.s[k] = valid ? ldv(a.b.st + (k) * N, ui) : P.state0[k];
@@ -1160,7 +1146,8 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(2)))
         cA.slot = valid ? ldv(a.b.slot + (my_table) * N, ui) : -1;
         if constexpr (LPE == 1) { cB.key = valid ? ldv(a.b.key + N, ui) : P.init_key_cl; cB.slot = valid ? ldv(a.b.slot + N, ui) : -1; }
         else { cB.key = 0; cB.slot = -1; }
-    }
+    };
+    load_env();
     // pd_step_sac_fused (16 lanes per env: the workgroup's 16 envs are one MLP tile): the actor's
     // heads of this step from the observation the previous step left in obs32, into s_sach (read
     // by the sampling below; the staging barrier orders them), before anything else of the step
@@ -2089,7 +2076,34 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(2)))
     if constexpr (POL) {
         // an episode that ended is stored now and its lanes freeze (they go on computing in step
         // with the wave, convergent for the cooperative miss solve, but write nothing)
-        if (live && (dn || tr)) { store_all(); live = false; }
+        const bool ended_now = live && (dn || tr || (a.refill && e.ts >= (uint32_t)a.refill_max));
+        if (ended_now) { store_all(); live = false; }
+        if (a.refill && !drained) {
+            // refill: once `refill` of the wave's slots wait (or none is live), they take the next
+            // particles of the swarm, one atomic per hand-out and the ballot's prefix count per env
+            // (its role-0 lane's rank); each loads the particle's reset state as the first launch
+            // of a rollout does (same bits).  Batched, the swarm's one counter sees a few
+            // hand-outs per wave and episode length, not one per wave and step, and a wave pays
+            // the loads' latency once per batch
+            const unsigned long long mk = __ballot(slot && !live && role == 0);
+            const int nw = __popcll(mk);
+            if (nw >= a.refill || (nw > 0 && __ballot(live) == 0ull)) {
+                const int lane = (int)__lane_id();
+                const int leader = __ffsll((long long)mk) - 1;
+                uint32_t base = 0;
+                if (lane == leader) base = atomicAdd(a.refill_next, (uint32_t)nw);
+                base = (uint32_t)__shfl((int)base, leader);
+                // (wave-uniform: once a hand-out reaches the swarm's end, no later one can start)
+                drained = (int64_t)a.refill_base + (int64_t)base + nw >= N;
+                const int64_t nx = (int64_t)a.refill_base + (int64_t)base + (int64_t)__popcll(mk & ((1ull << gbase) - 1ull));
+                if (slot && !live && nx < N) {
+                    e_act = nx; i = nx; ui = (uint32_t)nx; g = a.env_offset + (uint64_t)nx; valid = true;
+                    load_env();
+                    live = true;
+                    k_have = false;
+                }
+            }
+        }
         // a wave whose episodes have all ended leaves the launch's remaining steps (no barrier
         // follows; its lanes write nothing more): the launch then ends with its last live wave,
         // not F steps after the swarm's last episode

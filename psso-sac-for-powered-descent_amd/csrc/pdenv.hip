@@ -835,10 +835,6 @@ struct CellPieces {
     std::vector<int> sub_piece;       // [refined][S][S] piece of an exact sub-cell's key (-1 none)
     std::vector<int> bis_a, bis_b;    // per GridKeys bisector record: each trusted side's piece
     std::vector<uint32_t> fine;       // [nm S][na S] fine index (pd_step.h kFinePiece)
-    // the two-level form of the same index (PD_IDX2): one word per cell -- an exact cell's fine
-    // word (its piece, or 0), or kFineRefined | the refined cell's number -- and the refined
-    // cells' sub-cell words, [refined][S][S]
-    std::vector<uint32_t> cellw, rfine, cellw32, rfine32;
     double max_rel = 0, build_s = 0;
     int64_t pieces = 0, rejected = 0;
     std::vector<double> err;          // per piece: the binary64 check's error (INFINITY: unused slot)
@@ -1097,24 +1093,6 @@ void build_fine(const CellPieces& cp, const std::vector<uint8_t>& cell_ok, const
     });
 }
 
-// The two-level index from the fine index (CellPieces::cellw / rfine): the same words
-void build_cell_index(const CellPieces& cp, const std::vector<uint32_t>& fine, std::vector<uint32_t>& cellw,
-                      std::vector<uint32_t>& rfine) {
-    const int S = kGridSub, nm = cp.nm, na = cp.na;
-    int64_t nr = 0;
-    for (int v : cp.ridx) nr = std::max<int64_t>(nr, (int64_t)v + 1);
-    cellw.assign((size_t)nm * na, 0u);
-    rfine.assign((size_t)std::max<int64_t>(nr, 1) * S * S, 0u);
-    for (int64_t c = 0; c < (int64_t)nm * na; ++c) {
-        const int64_t im = c / na, ia = c % na;
-        if (!cp.refined[c]) { cellw[c] = fine[(size_t)(im * S) * ((size_t)na * S) + (size_t)ia * S]; continue; }
-        cellw[c] = kFineRefined | (uint32_t)cp.ridx[c];
-        for (int jm = 0; jm < S; ++jm)
-            for (int ja = 0; ja < S; ++ja)
-                rfine[(size_t)cp.ridx[c] * S * S + jm * S + ja] = fine[(size_t)(im * S + jm) * ((size_t)na * S) + (size_t)ia * S + ja];
-    }
-}
-
 const CellPieces& cell_pieces(const pd_aero_table& t, double a0, double a1, int nm, int na) {
     static std::mutex mu;
     static std::map<uint64_t, CellPieces> cache;
@@ -1223,7 +1201,6 @@ const CellPieces& cell_pieces(const pd_aero_table& t, double a0, double a1, int 
             }
     }
     build_fine(cp, cp.cell_ok, cp.sub_piece, cp.fine);
-    build_cell_index(cp, cp.fine, cp.cellw, cp.rfine);
     cp.build_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     return cp;
 }
@@ -1270,34 +1247,30 @@ void ensure_f32(CellPieces& cp) {
         else ++cp.rejected32;
     }
     build_fine(cp, cp.cell_ok32, cp.sub_piece32, cp.fine32);
-    build_cell_index(cp, cp.fine32, cp.cellw32, cp.rfine32);
     cp.have32 = true;
 }
 
 // The device copy of a table's cell pieces: one per device and process, shared read-only by the
 // handles (never freed; ~0.2 GB of the 288 GB)
 template <typename R>
-pd_status cell_pieces_device(const CellPieces& cp, const R** rec, const int** sub, const uint32_t** fine,
-                             const uint32_t** cellw, const uint32_t** rfine) {
+pd_status cell_pieces_device(const CellPieces& cp, const R** rec, const int** sub, const uint32_t** fine) {
     static std::mutex mu;
-    static std::map<std::pair<const void*, int>, std::array<void*, 5>> m;
+    static std::map<std::pair<const void*, int>, std::array<void*, 3>> m;
     const bool f32 = sizeof(R) == 4;
     const auto& rv = f32 ? (const void*)cp.rec32.data() : (const void*)cp.rec.data();
     const size_t rbytes = f32 ? cp.rec32.size() * 4 : cp.rec.size() * 8;
     const std::vector<int>& sp = f32 ? cp.sub_piece32 : cp.sub_piece;
     const std::vector<uint32_t>& fn = f32 ? cp.fine32 : cp.fine;
-    const std::vector<uint32_t>& cw = f32 ? cp.cellw32 : cp.cellw;
-    const std::vector<uint32_t>& rf = f32 ? cp.rfine32 : cp.rfine;
     int dev = 0;
     PD_HIP(hipGetDevice(&dev));
     std::lock_guard<std::mutex> lock(mu);
     auto k = std::make_pair((const void*)(f32 ? (const void*)&cp.rec32 : (const void*)&cp.rec), dev);
     auto it = m.find(k);
     if (it == m.end()) {
-        std::array<void*, 5> d{};
-        const void* src[5] = {rv, sp.data(), fn.data(), cw.data(), rf.data()};
-        const size_t nb[5] = {rbytes, sp.size() * 4, fn.size() * 4, cw.size() * 4, rf.size() * 4};
-        for (int q = 0; q < 5; ++q) {
+        std::array<void*, 3> d{};
+        const void* src[3] = {rv, sp.data(), fn.data()};
+        const size_t nb[3] = {rbytes, sp.size() * 4, fn.size() * 4};
+        for (int q = 0; q < 3; ++q) {
             PD_HIP(hipMalloc(&d[q], std::max<size_t>(nb[q], 8)));
             if (nb[q]) PD_HIP(hipMemcpy(d[q], src[q], nb[q], hipMemcpyHostToDevice));
         }
@@ -1306,8 +1279,6 @@ pd_status cell_pieces_device(const CellPieces& cp, const R** rec, const int** su
     *rec = (const R*)it->second[0];
     *sub = (const int*)it->second[1];
     *fine = (const uint32_t*)it->second[2];
-    *cellw = (const uint32_t*)it->second[3];
-    *rfine = (const uint32_t*)it->second[4];
     return PD_OK;
 }
 
@@ -1341,7 +1312,7 @@ struct pd_env {
     int count_work = 0; // workload counters on (pd_count_work)
     float* sac_heads = nullptr;   // pd_step_sac_fused's two-launch path: the actor heads [N][2A]
     float* pol_wc = nullptr;      // policy rollouts' list launches: the live envs' actor parameters
-    pd_tuning tune{128, 64, 2, -1, 0.0};   // launch tuning (pd_set_tuning)
+    pd_tuning tune{128, 64, 2, -1, 0.0, -1, 0};   // launch tuning (pd_set_tuning)
 };
 
 namespace {
@@ -1627,10 +1598,9 @@ template <typename R> pd_status create_impl(const pd_params* p, const pd_config*
     if ((st = build_grid<R>(p->cl, ga0[1], ga1[1], gnm[1], gna[1], tcl, gk[1], gs[1], sk[1], ss[1], bs[1], cps[1])) != PD_OK) return st;
     // the fine index (PD_TABLES_NO_FINE_INDEX: cell and sub-cell records only)
     for (int tb = 0; tb < 2; ++tb) {
-        D.cell_pc[tb] = nullptr; D.sub_piece[tb] = nullptr; D.fine[tb] = nullptr; D.cellw[tb] = nullptr; D.rfine[tb] = nullptr;
-        if (cps[tb] && (st = cell_pieces_device<R>(*cps[tb], &D.cell_pc[tb], &D.sub_piece[tb], &D.fine[tb], &D.cellw[tb],
-                                                   &D.rfine[tb])) != PD_OK) return st;
-        if (c->table_flags & PD_TABLES_NO_FINE_INDEX) { D.fine[tb] = nullptr; D.cellw[tb] = nullptr; D.rfine[tb] = nullptr; }
+        D.cell_pc[tb] = nullptr; D.sub_piece[tb] = nullptr; D.fine[tb] = nullptr;
+        if (cps[tb] && (st = cell_pieces_device<R>(*cps[tb], &D.cell_pc[tb], &D.sub_piece[tb], &D.fine[tb])) != PD_OK) return st;
+        if (c->table_flags & PD_TABLES_NO_FINE_INDEX) D.fine[tb] = nullptr;
     }
     if (verbose)
         for (int tb = 0; tb < 2; ++tb) {
@@ -1863,10 +1833,40 @@ pd_status rollout_policy_impl(pd_env* e, const float* w, int32_t max_steps, void
     if (check_every > 0 && !e->host_cnt) return fail(PD_ERR_HIP, "policy rollout: no pinned live-count words");
     // The list pays off once the grid no longer fits the chip in one round (a launch then costs
     // the rounds its waves need); below that the launch time is one wave's, and reading the
-    // state and actor weights through the list (gathers) only costs.  PDENV_COMPACT=0/1 forces.
+    // state and actor weights through the list (gathers) only costs.  pd_tuning.policy_list forces.
     int dev_cus = 256;
     (void)hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, e->device);
     const int plpe = e->tune.policy_lanes;
+    // refill: one launch of the chip's resident env slots (two waves per SIMD) steps the whole
+    // swarm, the lanes of an ended episode taking the next particle -- the grid's lanes stay busy
+    // until the swarm's last particles, where a launch per live-list check leaves most of a
+    // workgroup's lanes idle behind its longest episode
+    const int64_t cap = (int64_t)dev_cus * 512 / plpe;
+    // (auto: a wave's slots are handed particles once half of them wait -- 16 of the 32 at two
+    // lanes per env: c4 at 262 144 particles 5.04 ms a rollout, against 12.4 / 8.6 / 6.5 / 5.01 ms
+    // at batches of 1 / 4 / 8 / 32 and 5.94 ms for the rollout without refill)
+    const int kRefillBatch = 32 / plpe;
+    const bool refill = e->tune.policy_refill > 0 || (e->tune.policy_refill < 0 && N > cap);
+    if (refill) {
+        const int64_t slots = std::min<int64_t>(N, e->tune.policy_slots > 0 ? e->tune.policy_slots : cap);
+        PD_HIP(hipMemsetAsync(e->live_cnt, 0, 3 * sizeof(uint32_t), s));
+        a.use_list = 0; a.policy_wc = nullptr;
+        a.refill = e->tune.policy_refill > 0 ? e->tune.policy_refill : kRefillBatch;
+        a.refill_next = e->live_cnt; a.refill_base = (int)slots; a.refill_max = max_steps;
+        a.list_in = e->live[0]; a.list_out = e->live[1];
+        a.cnt_in = e->live_cnt + 1; a.cnt_out = e->live_cnt + 1; a.cnt_zero = e->live_cnt + 2;
+        // (a bound every wave reaches: each slot runs at most ceil(N / slots) + 1 episodes of at
+        // most max_steps steps; the waves leave when their lanes have none left)
+        const int64_t bound = (int64_t)max_steps * ((N + slots - 1) / slots + 1);
+        a.n_fused = (int)std::min<int64_t>(bound, INT32_MAX);
+        if (e->cfg.phase == PD_PHASE_PURE_THROTTLE) { if (wind) launch_policy<R, 0, true>(plpe, a, slots, s); else launch_policy<R, 0, false>(plpe, a, slots, s); }
+        else { if (wind) launch_policy<R, 1, true>(plpe, a, slots, s); else launch_policy<R, 1, false>(plpe, a, slots, s); }
+        PD_HIP(hipGetLastError());
+        launch_insert<R>(e, s);
+        if (steps) PD_HIP(hipMemcpyAsync(steps, e->tstep, (size_t)N * 4, hipMemcpyDeviceToDevice, s));
+        PD_HIP(hipGetLastError());
+        return PD_OK;
+    }
     a.use_list = e->tune.policy_list >= 0 ? e->tune.policy_list : (N * plpe > (int64_t)dev_cus * 512);
     // every launch appends its survivors to the next list, so the rollout can switch to the list
     // at any launch: once the live count read back falls to policy_list_at x N (default off), the
@@ -2075,6 +2075,9 @@ pd_status pd_set_tuning(pd_env* e, const pd_tuning* t) {
     if (t->policy_list < -1 || t->policy_list > 1) return fail(PD_ERR_INVALID, "pd_set_tuning: policy_list must be -1, 0 or 1");
     if (!(t->policy_list_at >= 0.0 && t->policy_list_at <= 1.0))
         return fail(PD_ERR_INVALID, "pd_set_tuning: policy_list_at must be in [0, 1]");
+    if (t->policy_refill < -1 || t->policy_refill > 64)
+        return fail(PD_ERR_INVALID, "pd_set_tuning: policy_refill must be -1 (auto), 0 (off) or a batch of 1..64 slots");
+    if (t->policy_slots < 0) return fail(PD_ERR_INVALID, "pd_set_tuning: policy_slots must be >= 0");
     e->tune = *t;
     return PD_OK;
 }

@@ -11,7 +11,7 @@ for c in ${CASES}; do
   for pass in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum"; do
     pn=$(echo "$pass" | cut -d' ' -f1 | tr 'A-Z' 'a-z')
     out=gpurun_out/pmc5_${tag}_${pn}
-    DESCENT=$d TABLE_FLAGS=$flags ${lib:+PDENV_LIB=$lib} timeout -s KILL 150 rocprofv3 --pmc $pass --output-format csv \
+    DESCENT=$d TABLE_FLAGS=$flags PDENV_LIB=${lib:-psso-sac-for-powered-descent_amd/pdenv/libpdenv.so} timeout -s KILL 150 rocprofv3 --pmc $pass --output-format csv \
       -d $out -o run -- python3 tools/time_fused.py > $out.log 2>&1 || { echo "case $c pass $pass failed rc=$?"; exit 1; }
     echo "case $c pass $pass ok"
   done

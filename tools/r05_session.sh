@@ -10,6 +10,9 @@
 #   4: c3 / c3-descent traffic and time with and without the fine index (PMC passes).
 #   5: the suite, smoke, fixed cost, driver command, c5 and c4-262k on the round-5 build.
 #   6: the suite, smoke, c5 breakdown, fixed cost and driver command of the reordered prologue, then 4.
+#   7: refill rollouts and the fused info tap: tests, c4 timings; the binary32 landing_burn diagnostic.
+#   8: batched refill (slots handed particles once k of a wave's wait): tests, c4 timings per batch.
+#   9: the auto batch (half a wave): tests, c4 at the whole swarm by default and at batches 12 / 24.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -54,7 +57,8 @@ case "${PART:-1}" in
   ;;
 4)
   # where c3-descent's traffic comes from: the fine index against the cell / sub-cell records
-  # (PD_TABLES_NO_FINE_INDEX = 2) and against the two-level index (libpdenv_idx2.so: a word per
+  # (PD_TABLES_NO_FINE_INDEX = 2) and against the two-level index (libpdenv_idx2.so, built by
+  # python tools/variants.py idx2=patch:tools/experiments/two_level_index.patch,-DPD_IDX2=1,host: a word per
   # cell, L2-resident, and the refined cells' sub-cell words), c3 and c3-descent: the variant's
   # bit-identity tests, PMC traffic + L2 hits, then the timing (two interleaved rounds)
   V=psso-sac-for-powered-descent_amd/pdenv/libpdenv_idx2.so
@@ -98,6 +102,40 @@ case "${PART:-1}" in
   done
   run benchdrv6 300 python bench.py --steps 20 --warmup 5
   PART=4 bash tools/r05_session.sh
+  ;;
+7)
+  # refill rollouts (c4) and the info tap in fused launches: their tests; the landing_burn binary32
+  # diagnostic; c4 at the whole swarm with refill against the one-launch-per-check rollout; the
+  # two-level index's traffic (PMC)
+  run gpu_t7 900 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -v --timeout 300 --timeout-method thread \
+      -k "compaction or info_tap or launcher" -s
+  run diag_lb 200 python tools/diag_f32_lb.py
+  run c4_262k_refill 300 python bench.py --workload c4 --particles 262144 --steps 6 --warmup 2 --cpu-baseline 0
+  run c4_32k 300 python bench.py --workload c4 --steps 8 --warmup 2 --cpu-baseline 0
+  V=psso-sac-for-powered-descent_amd/pdenv/libpdenv_idx2.so
+  CASES="d_idx2:1:0:$V c_idx2:0:0:$V c_fine:0:0" run pmc7 900 bash tools/pmc_r05.sh
+  ;;
+8)
+  # refill in batches (the first refill handed one particle per ended env, one atomic per wave
+  # and step on the swarm's one counter: 12.5 ms a generation at 262 144 particles against 6.4 ms
+  # without): the tests (incl. the binary32 teacher-forced bound by the step's conditioning), then
+  # c4 at the whole swarm per batch size and off, c4 at 32 768 with refill forced on
+  run gpu_t8 900 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -v --timeout 300 --timeout-method thread \
+      -k "compaction or info_tap or launcher or f32_teacher" -s
+  for b in 0 1 4 8 16 32; do
+    run c4_262k_rf$b 300 python bench.py --workload c4 --particles 262144 --steps 6 --warmup 2 --cpu-baseline 0 --policy-refill $b
+  done
+  for b in 0 8; do
+    run c4_32k_rf$b 300 python bench.py --workload c4 --steps 8 --warmup 2 --cpu-baseline 0 --policy-refill $b
+  done
+  ;;
+9)
+  run gpu_t9 900 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -v --timeout 300 --timeout-method thread \
+      -k "compaction or info_tap or launcher or f32_teacher" -s
+  run c4_262k_auto 300 python bench.py --workload c4 --particles 262144 --steps 6 --warmup 2 --cpu-baseline 0
+  for b in 12 24; do
+    run c4_262k_rf$b 300 python bench.py --workload c4 --particles 262144 --steps 6 --warmup 2 --cpu-baseline 0 --policy-refill $b
+  done
   ;;
 esac
 echo "=== done"

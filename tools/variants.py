@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
 """Build experiment variants of libpdenv (c3 step-kernel object only) in parallel:
 python tools/variants.py name=-DFOO,-DBAR name2=patch:tools/experiments/no_gust.patch ...
-(patch:<file> compiles a patched copy of csrc/; the product sources are never modified)"""
+(patch:<file> compiles a patched copy of csrc/; the product sources are never modified; the item
+"host" also compiles the host unit from it, e.g.
+idx2=patch:tools/experiments/two_level_index.patch,-DPD_IDX2=1,host)"""
 import concurrent.futures as cf
 import os
 import sys
@@ -17,6 +19,7 @@ if __name__ == "__main__":
         def one(sp):
             items = [d for d in sp[1].split(",") if d]
             patch = next((d[6:] for d in items if d.startswith("patch:")), None)
-            return b.build_variant(sp[0], [d for d in items if not d.startswith("patch:")], patch=patch)
+            defs = [d for d in items if not d.startswith("patch:") and d != "host"]
+            return b.build_variant(sp[0], defs, patch=patch, host="host" in items)
         for p in ex.map(one, specs):
             print(p)
