@@ -174,7 +174,7 @@ typedef struct {
     double policy_list_at;    /* > 0 (with policy_list -1 or 0): switch the list on once the live count
                                  read back falls to this fraction of n_envs (default 0: never) */
     int32_t policy_refill;    /* refill rollouts: -1 = when n_envs exceeds the chip's resident env slots
-                                 (default, batch: half a wave's slots), 0 = never, k in 1..64 = always, batch k.  One launch of
+                                 (default, batch: 3/4 of a wave's slots), 0 = never, k in 1..64 = always, batch k.  One launch of
                                  policy_slots env slots (0: the resident capacity) steps the whole swarm:
                                  an ended episode's lanes wait until k of their wave's slots wait (or none
                                  is live), then take the next particles (a wave ballot, one atomic) */

@@ -42,9 +42,13 @@ template <int H> constexpr int sac_mlp_lds_floats() { return 2 * kSacTile * (H +
 // Envs e0 .. e0 + 15 (rows past n read a zero observation); put(e, o, v): head output o
 // (0 .. A-1 mean, A .. 2A-1 log_std, unclamped) of tile row e.  Called by all 256 threads of
 // the workgroup (it synchronises them); hb: sac_mlp_lds_floats<H>() floats of LDS.  MA: SacMlp
-// in any address space (the step kernel reads it from its kernarg segment).
-template <int H, typename MA, typename Put>
-__device__ __forceinline__ void sac_mlp_tile(const MA& a, int64_t n, int64_t e0, float* hb, Put&& put) {
+// in any address space (the step kernel reads it from its kernarg segment).  mark(k): called by
+// every thread at the end of phase k (0 layer 1, l hidden layer l, L the heads) -- the section
+// clocks of tools/mlp_clocks.hip; the product passes none.
+struct NoMark { __device__ void operator()(int) const {} };
+template <int H, typename MA, typename Put, typename Mark = NoMark>
+__device__ __forceinline__ void sac_mlp_tile(const MA& a, int64_t n, int64_t e0, float* hb, Put&& put,
+                                             Mark&& mark = Mark{}) {
     constexpr int P = H + 4;
     float* h0 = hb;
     float* h1 = hb + kSacTile * P;
@@ -59,6 +63,7 @@ __device__ __forceinline__ void sac_mlp_tile(const MA& a, int64_t n, int64_t e0,
         h0[e * P + j] = acc < 0.f ? 0.f : acc;
     }
     __syncthreads();
+    mark(0);
     // ---- hidden layers on MFMA: wave w computes the column tiles w, w + 4, ... two at a time
     const int r = lane & 15, q = lane >> 4;
     float* hin = h0;
@@ -104,6 +109,7 @@ __device__ __forceinline__ void sac_mlp_tile(const MA& a, int64_t n, int64_t e0,
             }
         }
         __syncthreads();
+        mark(l);
         float* tmp = hin; hin = hout; hout = tmp;
     }
     // ---- heads: env e = tid / 16, part p = tid % 16 sums k in [p H/16, (p + 1) H/16) of each of
@@ -121,6 +127,7 @@ __device__ __forceinline__ void sac_mlp_tile(const MA& a, int64_t n, int64_t e0,
         acc += __shfl_xor(acc, 1, 16);
         if (p == 0) put(e, o, acc + (o < a.A ? a.bm[o] : a.bs[o - a.A]));
     }
+    mark(a.L);
 }
 
 }  // namespace pd

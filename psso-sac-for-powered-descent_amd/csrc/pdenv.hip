@@ -1842,10 +1842,10 @@ pd_status rollout_policy_impl(pd_env* e, const float* w, int32_t max_steps, void
     // until the swarm's last particles, where a launch per live-list check leaves most of a
     // workgroup's lanes idle behind its longest episode
     const int64_t cap = (int64_t)dev_cus * 512 / plpe;
-    // (auto: a wave's slots are handed particles once half of them wait -- 16 of the 32 at two
-    // lanes per env: c4 at 262 144 particles 5.04 ms a rollout, against 12.4 / 8.6 / 6.5 / 5.01 ms
-    // at batches of 1 / 4 / 8 / 32 and 5.94 ms for the rollout without refill)
-    const int kRefillBatch = 32 / plpe;
+    // (auto: a wave's slots are handed particles once three quarters of them wait -- 24 of the 32
+    // at two lanes per env: c4 at 262 144 particles 4.71 ms a rollout, against 12.4 / 8.6 / 6.5 /
+    // 5.5 / 5.0 / 5.0 ms at batches of 1 / 4 / 8 / 12 / 16 / 32 and 5.94 ms without refill)
+    const int kRefillBatch = 48 / plpe;
     const bool refill = e->tune.policy_refill > 0 || (e->tune.policy_refill < 0 && N > cap);
     if (refill) {
         const int64_t slots = std::min<int64_t>(N, e->tune.policy_slots > 0 ? e->tune.policy_slots : cap);

@@ -327,10 +327,14 @@ def test_f32_teacher_forced(pd):
     landing_burn's recorded states include tumbling ones (theta_ddot ~16 rad/s^2 with the
     aerodynamic moment's slope ~200 rad/s^2 per rad: an error grows ~2x per 0.1 s sub-step) and
     queries near a change of the 50-nearest set (the reference's k-NN RBF is discontinuous there),
-    where no binary32 computation can hold 1e-5: the bound is the larger of the tolerance and the
-    step's own conditioning -- the binary64 handle's spread over inputs perturbed by one binary32
-    rounding (2^-24 relative, four draws) -- times 16; the test asserts that states whose input
-    rounding alone exceeds the tolerance are few."""
+    where no binary32 computation can hold 1e-5: the bound is the larger of the tolerance and 8x
+    the step's own conditioning -- the binary64 handle's spread over inputs perturbed by one
+    binary32 rounding (2^-24 relative, four draws).  Measured (profiles/r05_f32_teacher_forced.log):
+    for 71 % of the 600 recorded landing_burn states that input rounding alone moves the binary64
+    step beyond the tolerance (theta_dot spread: median 6.7e-5, 90 % 2.2e-3, max 0.35); the
+    binary32 handle stays within 0.32 of 16x the spread on every channel, i.e. within ~5x what
+    rounding its inputs costs; the states the rounding leaves within the tolerance hold it on every
+    channel but theta (1.4e-5).  pure throttle: every state, every channel, at the tolerance."""
     import torch
     d = golden("ref_teacher_forced.npz")
     rng = np.random.default_rng(5)
@@ -359,14 +363,13 @@ def test_f32_teacher_forced(pd):
                 sg = lambda x: x * (1.0 + rng.choice([-1.0, 1.0], x.shape) * 2.0 ** -24)
                 spread = np.maximum(spread, np.abs(run("f64", sg(S0), sg(prevs)) - s64) / scale)
             ill = (spread > tol).any(1)
-            bound = np.maximum(bound, 16 * spread)
+            bound = np.maximum(bound, 8 * spread)
             print(f"f32 teacher-forced lb: {int(ill.sum())} of {len(S0)} states whose binary32 input rounding alone "
                   f"moves the binary64 step beyond the fp32 tolerance; spread quantiles (50/90/99/100 %) per channel:")
             for k, q in zip(ST, np.quantile(spread, [0.5, 0.9, 0.99, 1.0], axis=0).T):
                 print(f"   {k:10s} spread {q}  err/bound max {np.max(err[:, ST.index(k)] / bound[:, ST.index(k)]):.3g}")
             wc = dict(zip(ST, err[~ill].max(0).tolist()))
             print("f32 teacher-forced lb, the other states:", wc)
-            assert ill.mean() <= 0.1
         worst = dict(zip(ST, err.max(0).tolist()))
         print(f"f32 teacher-forced {tag}:", worst)
         bad = np.argwhere(err > bound)
@@ -966,7 +969,7 @@ def test_policy_rollout_compaction_invariant_full_swarm(pd, P):
     """Done-mask compaction in the regime it is built for (N x 2 lanes beyond one chip round):
     BASELINE c4's whole 262 144-particle swarm on one device, and a quarter of it, through the
     refill rollout (the default beyond the chip's resident env slots: one launch, the lanes of an
-    ended episode take the next particle by a wave ballot and prefix count, in batches of 16 waiting
+    ended episode take the next particle by a wave ballot and prefix count, in batches of 24 waiting
     slots (the auto batch at two lanes per env) or of 1, 32), the live list (from
     the first launch; from 50 % live) and neither, at 64 and at 8 policy steps per launch, check
     every 8 steps: fitness, episode lengths and final states bit-identical."""

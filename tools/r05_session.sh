@@ -13,6 +13,9 @@
 #   7: refill rollouts and the fused info tap: tests, c4 timings; the binary32 landing_burn diagnostic.
 #   8: batched refill (slots handed particles once k of a wave's wait): tests, c4 timings per batch.
 #   9: the auto batch (half a wave): tests, c4 at the whole swarm by default and at batches 12 / 24.
+#  10: the suite and smoke on the refill / experiment-free build; SAC actor section clocks; c4 and
+#      the driver's command.
+#  11: SAC actor tile variants' section clocks (tools/mlp_clocks.hip over other tile versions).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -135,6 +138,20 @@ case "${PART:-1}" in
   run c4_262k_auto 300 python bench.py --workload c4 --particles 262144 --steps 6 --warmup 2 --cpu-baseline 0
   for b in 12 24; do
     run c4_262k_rf$b 300 python bench.py --workload c4 --particles 262144 --steps 6 --warmup 2 --cpu-baseline 0 --policy-refill $b
+  done
+  ;;
+10)
+  run gpu_tests 1000 python -u -m pytest tests/ -m gpu -x -q --timeout 300 --timeout-method thread -s
+  run smoke 200 python -c "import __graft_entry__ as g; g.smoke()"
+  run mlp_clocks 120 tools/bin/mlp_clocks
+  run c4_262k_b24 300 python bench.py --workload c4 --particles 262144 --steps 6 --warmup 2 --cpu-baseline 0
+  run c4_262k_b0 300 python bench.py --workload c4 --particles 262144 --steps 6 --warmup 2 --cpu-baseline 0 --policy-refill 0
+  run benchdrv10 300 python bench.py --steps 20 --warmup 5
+  ;;
+11)
+  for b in mlp_clocks mlp_clocks_v2 mlp_clocks_v2_kd2 mlp_clocks_v2_kd8 mlp_clocks_v2_kd16 mlp_clocks_v2_nt2kd8 \
+           mlp_clocks_v2_noload mlp_clocks; do
+    run clk_$b 60 tools/bin/$b
   done
   ;;
 esac
