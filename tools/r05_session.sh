@@ -16,6 +16,22 @@
 #  10: the suite and smoke on the refill / experiment-free build; SAC actor section clocks; c4 and
 #      the driver's command.
 #  11: SAC actor tile variants' section clocks (tools/mlp_clocks.hip over other tile versions).
+#  12: the actor tile with whole-line weight fragments (v3): clocks against v1 (cold and warm),
+#      the SAC tests, c5 and its breakdown.
+#  13: v4 (layer 1 with the state width at compile time): clocks.
+#  14: v4's hidden layer: fewer workgroups (shared L2 or per-CU bound?), tiles in flight, prefetch.
+#  15: v5 (rotating fragment buffers behind scheduling barriers): clocks.
+#  16: the hidden layer taken apart: loads only, loads beside independent MFMAs, v6 (A fragments
+#      double-buffered from LDS).
+#  17: loads only, the MFMA fragment pattern against 1 KB contiguous per wave load.
+#  18: v7 (weights through a wave-private LDS ring by LDS DMA) against v5, with the heads checked
+#      against a host forward pass.
+#  19: v7's ring depth and tiles in flight.
+#  20: v8 (the next block's fragments read from LDS during this block's MFMAs).
+#  21: v8 taken apart: without the DMA, without the weight-fragment reads, without both.
+#  22: v9 (whole-line loads into registers, swizzled into the LDS ring by the wave) against v7.
+#  23: the product actor tile (v7: LDS DMA ring, layer 1 at compile-time width, head biases
+#      early): the SAC tests, c5, its breakdown, the tile's clocks.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -153,6 +169,53 @@ case "${PART:-1}" in
            mlp_clocks_v2_noload mlp_clocks; do
     run clk_$b 60 tools/bin/$b
   done
+  ;;
+12)
+  for b in mlp_clocks_v1 mlp_clocks_v3 mlp_clocks_v1_twice mlp_clocks_v2_twice mlp_clocks_v3_twice; do
+    run clk12_$b 60 tools/bin/$b
+  done
+  run gpu_sac 600 python -u -m pytest tests/ -m gpu -x -q --timeout 300 --timeout-method thread -k "sac or actor or c5" -s
+  run c5_12 300 python bench.py --workload c5
+  run c5_breakdown12 300 python tools/c5_breakdown.py
+  ;;
+13)
+  for b in mlp_clocks_v3 mlp_clocks_v4 mlp_clocks_v4_twice; do
+    run clk13_$b 60 tools/bin/$b
+  done
+  ;;
+14)
+  for n in 4096 2048 1024 512 128; do run clk14_v4_n$n 60 tools/bin/mlp_clocks_v4 $n; done
+  for b in mlp_clocks_v4_nt2 mlp_clocks_v4_kd1 mlp_clocks_v4_kd3 mlp_clocks_v4_nt1kd4; do run clk14_$b 60 tools/bin/$b; done
+  ;;
+15)
+  for b in mlp_clocks_v4 mlp_clocks_v5 mlp_clocks_v5; do run clk15_$b 60 tools/bin/$b; done
+  ;;
+16)
+  for b in mlp_clocks_v5_loadonly mlp_clocks_v5_indep mlp_clocks_v6 mlp_clocks_v2_noload; do run clk16_$b 60 tools/bin/$b; done
+  ;;
+17)
+  for b in mlp_clocks_v5_loadonly mlp_clocks_v5_loadonly_contig; do run clk17_$b 60 tools/bin/$b; done
+  ;;
+18)
+  for b in mlp_clocks_v5 mlp_clocks_v7 mlp_clocks_v5 mlp_clocks_v7; do run clk18_$b 60 tools/bin/$b; done
+  ;;
+19)
+  for b in n2r2 n2r3 n2r4 n4r2 n4r3 n1r4 n2r4; do run clk19_v7_$b 60 tools/bin/mlp_clocks_v7_$b; done
+  ;;
+20)
+  for b in v7_n2r2 v8_n2r3 v8_n4r3 v8_n2r4 v8_n2r3; do run clk20_$b 60 tools/bin/mlp_clocks_$b; done
+  ;;
+21)
+  for b in v8_nodma v8_nowread v8_nodma_nowread v8_n2r3; do run clk21_$b 60 tools/bin/mlp_clocks_$b; done
+  ;;
+22)
+  for b in v7_n2r2 v9_n2 v9_n4 v9_n2; do run clk22_$b 60 tools/bin/mlp_clocks_$b; done
+  ;;
+23)
+  run gpu_sac23 600 python -u -m pytest tests/ -m gpu -x -q --timeout 300 --timeout-method thread -k "sac or actor or c5" -s
+  run clk23_product 60 tools/bin/mlp_clocks
+  run c5_23 300 python bench.py --workload c5
+  run c5_breakdown23 300 python tools/c5_breakdown.py
   ;;
 esac
 echo "=== done"
