@@ -229,7 +229,8 @@ def bench_pso(args, world, rank, local, dist):
     P = args.particles
     opt = ParticleSubswarmOptimisationGPU("landing_burn", pop_size=P * world, device=local, seed=1234,
                                           precision=args.precision, dist=dist,
-                                          tuning=dict(policy_list=args.policy_list, policy_refill=args.policy_refill),
+                                          tuning=dict(policy_list=args.policy_list, policy_refill=args.policy_refill,
+                                                      policy_refill_own=args.policy_refill_own),
                                           pso_params=dict(generations=args.warmup + args.steps,
                                                           re_initialise_generation=-1))
     for g in range(args.warmup):
@@ -549,6 +550,8 @@ def main():
                     help="c4: the policy rollouts' live-list launches (pd_tuning.policy_list: -1 auto, 0 off, 1 on)")
     ap.add_argument("--policy-refill", type=int, default=-1,
                     help="c4: refill rollouts (pd_tuning.policy_refill: -1 auto, 0 off, k = batch of k waiting slots)")
+    ap.add_argument("--policy-refill-own", type=int, default=-1,
+                    help="c4: percent of the swarm refilled from the waves' own ranges (pd_tuning.policy_refill_own; -1 auto)")
     ap.add_argument("--graph", type=int, default=1, help="c5: replay the collection step as a HIP graph")
     ap.add_argument("--c3-burn-in", type=int, default=C3_BURN_IN,
                     help="c3: untimed env-steps before the warmup (steady state: resets at their stationary rate)")

@@ -178,7 +178,11 @@ typedef struct {
                                  policy_slots env slots (0: the resident capacity) steps the whole swarm:
                                  an ended episode's lanes wait until k of their wave's slots wait (or none
                                  is live), then take the next particles (a wave ballot, one atomic) */
-    int32_t policy_slots;     /* env slots of a refill rollout (0 = the chip's resident capacity) */
+    int32_t policy_slots;     /* env slots of a refill rollout (0 = the chip's resident capacity; rounded
+                                 down to whole waves) */
+    int32_t policy_refill_own;/* refill rollouts: percent of the swarm handed out from the waves' own
+                                 particle ranges (no atomic), the rest from the shared pool; -1 = 100 */
+    int32_t pad_tuning;
 } pd_tuning;
 
 /* Info tap of pd_step: the quantities of the LAST physics sub-step that rocket_physics_fcn puts in

@@ -262,6 +262,7 @@ template <typename R> struct StepArgs {
     // every particle of the swarm has run
     uint32_t* refill_next;
     int refill, refill_base, refill_max;
+    int refill_slots, refill_q;   // (the slots; particles of a wave's own range, [w Q, (w + 1) Q))
 };
 
 // Kernel launchers, explicitly instantiated in the kstep_*.hip translation units.

@@ -1070,15 +1070,18 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(2)))
     // envs this launch steps: all N, or (POL) the compacted live list; a workgroup past its end
     // leaves before staging the tables (workgroup-uniform)
     int64_t n_act = a.n;
+    // (refill rollouts in the windless policy kernels only: the windy ones have no registers to
+    // spare for the particle reload; the host steps windy swarms by per-check launches)
+    constexpr bool kRefill = POL && !WIND;
     // ring mode of pd_step_sac_ring: the ring position this launch writes at (every workgroup
     // reads it before the last one advances it, see the end of the kernel)
     int64_t ring_pos0 = 0;
     if constexpr (SAC) { if (a.ring_state) ring_pos0 = (int64_t)__atomic_load_n(a.ring_state, __ATOMIC_RELAXED); }
     if constexpr (POL) {
         if (blockIdx.x == 0 && threadIdx.x == 0) *a.cnt_zero = 0u;
-        // (refill: the grid's first refill_base envs are the slots; the rest of its last
+        // (refill: the grid's first refill_slots envs are the slots; the rest of its last
         // workgroup runs private copies, as past the end of any grid)
-        if (a.refill) n_act = a.refill_base;
+        if (kRefill && a.refill) n_act = a.refill_slots;
         if (a.use_list) {
             n_act = (int64_t)*a.cnt_in;
             if ((int64_t)blockIdx.x * EPB >= n_act) return;
@@ -1093,6 +1096,18 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(2)))
     const bool slot = valid;   // (refill: the lanes of one of the launch's env slots)
     bool drained = false;      // (refill: the swarm's particles all handed out; wave-uniform)
     int64_t e_act = valid ? gt / LPE : n_act - 1;
+    // refill: wave w of the grid owns particles [w Q, (w + 1) Q) (refill_q = Q), its slots
+    // starting on the first of them and taking the rest without any atomic; the particles from
+    // refill_base on are the shared pool
+    int rq_next = 0;   // (refill: this wave's next own particle, wave-uniform)
+    if constexpr (kRefill) {
+        if (a.refill && valid) {
+            constexpr int kEpw = 64 / LPE;
+            const int64_t gw = gt >> 6;
+            e_act = gw * (int64_t)a.refill_q + (int64_t)(((int)gt & 63) / LPE);
+            rq_next = kEpw;
+        }
+    }
     int64_t i = (POL && a.use_list) ? (int64_t)a.list_in[e_act] : e_act;
     const int role = (int)(gt % LPE);
     const int le = (int)threadIdx.x / LPE;   // the env's column of the workgroup's LDS g-load ring
@@ -1148,6 +1163,26 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(2)))
         else { cB.key = 0; cB.slot = -1; }
     };
     load_env();
+    // the static tables: one 16-byte vector copy of the handle's image of them (pdenv.hip
+    // fill_step_static: the same values, the grid-fin slopes by the same division), every load of
+    // a thread issued here -- ahead of the SAC actor's prologue, whose first waits then cover
+    // their latency -- and stored after it; then the eval_log cells
+    constexpr int kImg = (int)(sizeof(StepStatic<R, WIND>) / 16);
+    constexpr int kLog = (int)(sizeof(LogTableD) / 16);
+    constexpr int kPer = (kImg + kLog + kStepBlock - 1) / kStepBlock;
+    using V4 = __attribute__((ext_vector_type(4))) unsigned int;
+    V4 stg[kPer];
+    {
+        DP<R>& P = *params<R>(a.P);
+        const PD_AS1 V4* img = (const PD_AS1 V4*)P.stage_img;
+        const PD_AS1 V4* lgt = (const PD_AS1 V4*)(uint64_t)&P.logtab_d.cell[0];
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) {
+            const int t = threadIdx.x + k * kStepBlock;
+            if (t < kImg) stg[k] = img[t];
+            else if (t < kImg + kLog) stg[k] = lgt[t - kImg];
+        }
+    }
     // pd_step_sac_fused (16 lanes per env: the workgroup's 16 envs are one MLP tile): the actor's
     // heads of this step from the observation the previous step left in obs32, into s_sach (read
     // by the sampling below; the staging barrier orders them), before anything else of the step
@@ -1169,28 +1204,12 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(2)))
         }
     }
     {
-        // the static tables: one 16-byte vector copy of the handle's image of them (pdenv.hip
-        // fill_step_static: the same values, the grid-fin slopes by the same division), every load
-        // of a thread issued before its first store; then the eval_log cells
         DP<R>& P = *params<R>(a.P);
-        constexpr int kImg = (int)(sizeof(StepStatic<R, WIND>) / 16);
-        constexpr int kLog = (int)(sizeof(LogTableD) / 16);
-        constexpr int kPer = (kImg + kLog + kStepBlock - 1) / kStepBlock;
-        using V4 = __attribute__((ext_vector_type(4))) unsigned int;
-        const PD_AS1 V4* img = (const PD_AS1 V4*)P.stage_img;
-        const PD_AS1 V4* lgt = (const PD_AS1 V4*)(uint64_t)&P.logtab_d.cell[0];
-        V4 v[kPer];
 #pragma unroll
         for (int k = 0; k < kPer; ++k) {
             const int t = threadIdx.x + k * kStepBlock;
-            if (t < kImg) v[k] = img[t];
-            else if (t < kImg + kLog) v[k] = lgt[t - kImg];
-        }
-#pragma unroll
-        for (int k = 0; k < kPer; ++k) {
-            const int t = threadIdx.x + k * kStepBlock;
-            if (t < kImg) ((V4*)static_cast<StepStatic<R, WIND>*>(&L))[t] = v[k];
-            else if (t < kImg + kLog) ((V4*)s_logtab)[t - kImg] = v[k];
+            if (t < kImg) ((V4*)static_cast<StepStatic<R, WIND>*>(&L))[t] = stg[k];
+            else if (t < kImg + kLog) ((V4*)s_logtab)[t - kImg] = stg[k];
         }
         if (threadIdx.x < (kStepBlock / 64) * kNWork) (&L.work[0][0])[threadIdx.x] = 0u;
         if (threadIdx.x < 2) L.tdesc[threadIdx.x] = tab_view<R>(P, L.tab, (int)threadIdx.x);
@@ -2076,15 +2095,33 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(2)))
     if constexpr (POL) {
         // an episode that ended is stored now and its lanes freeze (they go on computing in step
         // with the wave, convergent for the cooperative miss solve, but write nothing)
-        const bool ended_now = live && (dn || tr || (a.refill && e.ts >= (uint32_t)a.refill_max));
+        const bool ended_now = live && (dn || tr || (kRefill && a.refill && e.ts >= (uint32_t)a.refill_max));
         if (ended_now) { store_all(); live = false; }
-        if (a.refill && !drained) {
-            // refill: once `refill` of the wave's slots wait (or none is live), they take the next
-            // particles of the swarm, one atomic per hand-out and the ballot's prefix count per env
-            // (its role-0 lane's rank); each loads the particle's reset state as the first launch
-            // of a rollout does (same bits).  Batched, the swarm's one counter sees a few
-            // hand-outs per wave and episode length, not one per wave and step, and a wave pays
-            // the loads' latency once per batch
+        if (kRefill && a.refill && rq_next < a.refill_q) {
+            // refill from the wave's own particles: every waiting slot at once, its rank in the
+            // ballot (of its role-0 lane) the offset -- no atomic, no wait
+            const unsigned long long mk = __ballot(slot && !live && role == 0);
+            if (mk) {
+                const int nw = __popcll(mk);
+                const int take = nw < a.refill_q - rq_next ? nw : a.refill_q - rq_next;
+                const int rank = __popcll(mk & ((1ull << gbase) - 1ull));
+                if (slot && !live && rank < take) {
+                    const int64_t nx = (gt >> 6) * (int64_t)a.refill_q + (int64_t)(rq_next + rank);
+                    e_act = nx; i = nx; ui = (uint32_t)nx; g = a.env_offset + (uint64_t)nx; valid = true;
+                    load_env();
+                    live = true;
+                    k_have = false;
+                }
+                rq_next += take;
+            }
+        }
+        if (kRefill && a.refill && !drained && rq_next >= a.refill_q) {
+            // then the shared pool: once `refill` of the wave's slots wait (or none is live), they
+            // take its next particles, one atomic per hand-out and the ballot's prefix count per
+            // env (its role-0 lane's rank); each loads the particle's reset state as the first
+            // launch of a rollout does (same bits).  Batched, the pool's one counter sees a few
+            // hand-outs per wave, not one per wave and step, and a wave pays the loads' latency
+            // once per batch
             const unsigned long long mk = __ballot(slot && !live && role == 0);
             const int nw = __popcll(mk);
             if (nw >= a.refill || (nw > 0 && __ballot(live) == 0ull)) {

@@ -1312,7 +1312,7 @@ struct pd_env {
     int count_work = 0; // workload counters on (pd_count_work)
     float* sac_heads = nullptr;   // pd_step_sac_fused's two-launch path: the actor heads [N][2A]
     float* pol_wc = nullptr;      // policy rollouts' list launches: the live envs' actor parameters
-    pd_tuning tune{128, 64, 2, -1, 0.0, -1, 0};   // launch tuning (pd_set_tuning)
+    pd_tuning tune{128, 64, 2, -1, 0.0, -1, 0, -1, 0};   // launch tuning (pd_set_tuning)
 };
 
 namespace {
@@ -1846,18 +1846,35 @@ pd_status rollout_policy_impl(pd_env* e, const float* w, int32_t max_steps, void
     // at two lanes per env: c4 at 262 144 particles 4.71 ms a rollout, against 12.4 / 8.6 / 6.5 /
     // 5.5 / 5.0 / 5.0 ms at batches of 1 / 4 / 8 / 12 / 16 / 32 and 5.94 ms without refill)
     const int kRefillBatch = 48 / plpe;
-    const bool refill = e->tune.policy_refill > 0 || (e->tune.policy_refill < 0 && N > cap);
+    // (windless handles only: the windy policy kernels compile no refill, see pd_step_impl.h)
+    const bool refill = !wind && (e->tune.policy_refill > 0 || (e->tune.policy_refill < 0 && N > cap));
     if (refill) {
-        const int64_t slots = std::min<int64_t>(N, e->tune.policy_slots > 0 ? e->tune.policy_slots : cap);
+        // slots: whole waves (epw envs each), at most the swarm; wave w owns particles
+        // [w Q, (w + 1) Q) -- its first epw are its slots' first episodes -- and takes them
+        // without atomics; the rest, from waves x Q on, is the shared pool (batched hand-outs).
+        // Q: policy_refill_own percent of the swarm over the waves, whole waves' worth of envs
+        // (default 100: c4 at 262 144 particles, 128 per wave, no pool -- 3.97 ms a rollout against
+        // 4.22 / 4.18 / 4.54 / 4.75 ms with 90 / 75 / 50 / 0 % own, the rest from the pool in
+        // batches of 24: the pool's batching idles more lanes than the waves' uneven work does)
+        const int64_t epw = 64 / plpe;
+        int64_t slots = std::min<int64_t>(N, e->tune.policy_slots > 0 ? e->tune.policy_slots : cap);
+        slots = std::max<int64_t>(epw, slots / epw * epw);
+        const int64_t waves = slots / epw;
+        const int own = e->tune.policy_refill_own >= 0 ? e->tune.policy_refill_own : 100;
+        int64_t q = (int64_t)((double)N * own / 100.0 / (double)waves) / epw * epw;
+        q = std::max<int64_t>(epw, std::min<int64_t>(q, N / waves / epw * epw));
+        if (waves * q > N) q = epw;   // (a swarm smaller than one wave per slot group)
         PD_HIP(hipMemsetAsync(e->live_cnt, 0, 3 * sizeof(uint32_t), s));
         a.use_list = 0; a.policy_wc = nullptr;
         a.refill = e->tune.policy_refill > 0 ? e->tune.policy_refill : kRefillBatch;
-        a.refill_next = e->live_cnt; a.refill_base = (int)slots; a.refill_max = max_steps;
+        a.refill_next = e->live_cnt; a.refill_max = max_steps;
+        a.refill_slots = (int)slots; a.refill_q = (int)q; a.refill_base = (int)(waves * q);
         a.list_in = e->live[0]; a.list_out = e->live[1];
         a.cnt_in = e->live_cnt + 1; a.cnt_out = e->live_cnt + 1; a.cnt_zero = e->live_cnt + 2;
-        // (a bound every wave reaches: each slot runs at most ceil(N / slots) + 1 episodes of at
-        // most max_steps steps; the waves leave when their lanes have none left)
-        const int64_t bound = (int64_t)max_steps * ((N + slots - 1) / slots + 1);
+        // (a bound every wave reaches: a wave runs at most its own q particles and the pool's,
+        // one of its slots live at every step until they are all handed out, each episode at most
+        // max_steps steps; the waves leave when their lanes have none left)
+        const int64_t bound = (int64_t)max_steps * (q + (N - waves * q) + 1);
         a.n_fused = (int)std::min<int64_t>(bound, INT32_MAX);
         if (e->cfg.phase == PD_PHASE_PURE_THROTTLE) { if (wind) launch_policy<R, 0, true>(plpe, a, slots, s); else launch_policy<R, 0, false>(plpe, a, slots, s); }
         else { if (wind) launch_policy<R, 1, true>(plpe, a, slots, s); else launch_policy<R, 1, false>(plpe, a, slots, s); }
@@ -2078,6 +2095,8 @@ pd_status pd_set_tuning(pd_env* e, const pd_tuning* t) {
     if (t->policy_refill < -1 || t->policy_refill > 64)
         return fail(PD_ERR_INVALID, "pd_set_tuning: policy_refill must be -1 (auto), 0 (off) or a batch of 1..64 slots");
     if (t->policy_slots < 0) return fail(PD_ERR_INVALID, "pd_set_tuning: policy_slots must be >= 0");
+    if (t->policy_refill_own < -1 || t->policy_refill_own > 100)
+        return fail(PD_ERR_INVALID, "pd_set_tuning: policy_refill_own must be -1 (auto) or a percentage 0..100");
     e->tune = *t;
     return PD_OK;
 }

@@ -87,7 +87,8 @@ TABLES_NO_CELL_PIECES, TABLES_NO_FINE_INDEX, TABLES_EXACT_ATMOSPHERE, TABLES_VER
 
 class PdTuning(C.Structure):
     _fields_ = [("step_fuse", I32), ("policy_fuse", I32), ("policy_lanes", I32), ("policy_list", I32),
-                ("policy_list_at", D), ("policy_refill", I32), ("policy_slots", I32)]
+                ("policy_list_at", D), ("policy_refill", I32), ("policy_slots", I32),
+                ("policy_refill_own", I32), ("pad_tuning", I32)]
 
 
 EXPORTS = ["pd_abi_version", "pd_sizeof_params", "pd_sizeof_config", "pd_last_error", "pd_device_count", "pd_create",

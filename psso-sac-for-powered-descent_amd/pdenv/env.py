@@ -224,7 +224,8 @@ class PoweredDescentEnv:
 
     def set_tuning(self, **kw):
         """Change launch tuning fields (pd_set_tuning: step_fuse, policy_fuse, policy_lanes,
-        policy_list, policy_list_at); results never depend on them."""
+        policy_list, policy_list_at, policy_refill, policy_slots, policy_refill_own); results never
+        depend on them."""
         cur = self.tuning()
         bad = set(kw) - set(cur)
         if bad:

@@ -53,7 +53,7 @@ def test_argument_checks_before_any_launch():
         st = L.pd_pso_swarm_minima(5000, 10, 3, vp(0x10000), vp(0x10000), vp(0x10000), vp(0x10000), vp(0x10000),
                                    scratch, nb, None)
         assert st == _lib.PD_ERR_INVALID and b"scratch" in L.pd_last_error()
-    t = _lib.PdTuning(128, 64, 2, -1, 0.0, -1, 0)
+    t = _lib.PdTuning(128, 64, 2, -1, 0.0, -1, 0, -1, 0)
     assert L.pd_set_tuning(None, C.byref(t)) == _lib.PD_ERR_INVALID
     assert L.pd_get_tuning(None, C.byref(t)) == _lib.PD_ERR_INVALID
 

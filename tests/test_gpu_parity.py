@@ -944,13 +944,18 @@ def test_policy_rollout_compaction_invariant(pd):
              (1, 3, 0.0, 8, 0, 0), (1, 8, 0.0, 4, 0, 0), (1, 64, 0.0, 64, 0, 0),
              (-1, 8, 0.0, 64, -1, 0), (0, 8, 0.5, 8, 0, 0), (0, 8, 0.05, 2, 0, 0),
              (0, 8, 0.0, 1, 0, 0), (0, 8, 0.0, 64, 1, 256), (0, 8, 0.0, 64, 8, 97),
-             (0, 8, 0.0, 64, 32, 0), (0, 8, 0.0, 64, 3, 1))
-    for lst, ce, at, pf, rf, sl in cases:
+             (0, 8, 0.0, 64, 32, 0), (0, 8, 0.0, 64, 3, 1), (0, 8, 0.0, 64, 24, 64, 0), (0, 8, 0.0, 64, 24, 64, 100),
+             (0, 8, 0.0, 64, 5, 96, 50))
+    for c in cases:
+        lst, ce, at, pf, rf, sl = c[:6]
+        own = c[6] if len(c) > 6 else -1
         # (policy_list_at: switched on mid-rollout at that live fraction; policy_refill with
-        # policy_slots env slots, handed the next particles in batches of policy_refill waiting slots
-        # of a wave -- 97 slots leave most of the last workgroup without one, 32 waits for a whole
-        # wave, 1 slot steps the swarm one particle after another)
-        env.set_tuning(policy_list=lst, policy_list_at=at, policy_fuse=pf, policy_refill=rf, policy_slots=sl)
+        # policy_slots env slots (rounded down to whole waves, at least one), each wave's own
+        # particles (policy_refill_own percent of the swarm) without atomics, then the shared pool in
+        # batches of policy_refill waiting slots of a wave -- 97 slots round to 96 (three waves, less
+        # than one workgroup), 32 waits for a whole wave, 1 is one wave; own 0 / 100: pool / own only)
+        env.set_tuning(policy_list=lst, policy_list_at=at, policy_fuse=pf, policy_refill=rf, policy_slots=sl,
+                       policy_refill_own=own)
         fit, steps = env.rollout_policy(torch.tensor(W), max_steps=300, check_every=ce)
         res.append((fit.cpu().numpy(), steps.cpu().numpy(), env.state.cpu().numpy()))
     for c, (f, s, S) in zip(cases[1:], res[1:]):
@@ -969,8 +974,9 @@ def test_policy_rollout_compaction_invariant_full_swarm(pd, P):
     """Done-mask compaction in the regime it is built for (N x 2 lanes beyond one chip round):
     BASELINE c4's whole 262 144-particle swarm on one device, and a quarter of it, through the
     refill rollout (the default beyond the chip's resident env slots: one launch, the lanes of an
-    ended episode take the next particle by a wave ballot and prefix count, in batches of 24 waiting
-    slots (the auto batch at two lanes per env) or of 1, 32), the live list (from
+    ended episode take the next particle -- first from their wave's own range, then from the shared
+    pool by a wave ballot and prefix count in batches of waiting slots; own share 100 % (default),
+    0 and 90 %, batches 24 (the auto batch at two lanes per env), 1, 32), the live list (from
     the first launch; from 50 % live) and neither, at 64 and at 8 policy steps per launch, check
     every 8 steps: fitness, episode lengths and final states bit-identical."""
     import torch
@@ -979,9 +985,10 @@ def test_policy_rollout_compaction_invariant_full_swarm(pd, P):
     env = make(pd, P, phase="landing_burn", mode="pso")
     assert env.tuning()["policy_list"] == -1 and env.tuning()["policy_refill"] == -1
     res = []
-    for lst, at, pf, rf, sl in ((0, 0.0, 64, 0, 0), (-1, 0.0, 64, -1, 0), (1, 0.0, 8, 0, 0), (0, 0.5, 8, 0, 0),
-                                (0, 0.0, 64, 1, 0), (0, 0.0, 64, 32, 20000)):
-        env.set_tuning(policy_list=lst, policy_list_at=at, policy_fuse=pf, policy_refill=rf, policy_slots=sl)
+    for lst, at, pf, rf, sl, own in ((0, 0.0, 64, 0, 0, -1), (-1, 0.0, 64, -1, 0, -1), (1, 0.0, 8, 0, 0, -1),
+                                     (0, 0.5, 8, 0, 0, -1), (0, 0.0, 64, 1, 0, 0), (0, 0.0, 64, 32, 20000, 90)):
+        env.set_tuning(policy_list=lst, policy_list_at=at, policy_fuse=pf, policy_refill=rf, policy_slots=sl,
+                       policy_refill_own=own)
         fit, steps = env.rollout_policy(W, max_steps=400, check_every=8)
         res.append((fit.clone(), steps.clone(), env.state.clone()))
     for f, s, S in res[1:]:
@@ -1118,11 +1125,11 @@ def test_launcher_refuses_mismatched_inputs(pd):
     assert fused(S, A, params2) == L.PD_ERR_UNSUPPORTED
     L.check(fused(S, A, params))
     for kw in (dict(step_fuse=0), dict(step_fuse=257), dict(policy_fuse=3), dict(policy_lanes=16), dict(policy_list=2),
-               dict(policy_list_at=1.5)):
+               dict(policy_list_at=1.5), dict(policy_refill=65), dict(policy_refill_own=101)):
         with pytest.raises(L.PdError):
             env.set_tuning(**kw)
     assert env.tuning() == dict(step_fuse=128, policy_fuse=64, policy_lanes=2, policy_list=-1, policy_list_at=0.0,
-                                policy_refill=-1, policy_slots=0)
+                                policy_refill=-1, policy_slots=0, policy_refill_own=-1, pad_tuning=0)
     env.step(torch.zeros(256, 1, device="cuda"))
     torch.cuda.synchronize()
     assert torch.isfinite(env.state).all()

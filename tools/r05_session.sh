@@ -32,6 +32,9 @@
 #  22: v9 (whole-line loads into registers, swizzled into the LDS ring by the wave) against v7.
 #  23: the product actor tile (v7: LDS DMA ring, layer 1 at compile-time width, head biases
 #      early): the SAC tests, c5, its breakdown, the tile's clocks.
+#  24: the staging loads issued ahead of the actor prologue: SAC tests, c5, breakdown, c3 fixed cost.
+#  25: refill from the waves' own particle ranges: the compaction tests, c4 at the whole swarm by
+#      own share and batch.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -216,6 +219,21 @@ case "${PART:-1}" in
   run clk23_product 60 tools/bin/mlp_clocks
   run c5_23 300 python bench.py --workload c5
   run c5_breakdown23 300 python tools/c5_breakdown.py
+  ;;
+24)
+  run gpu_sac24 600 python -u -m pytest tests/ -m gpu -x -q --timeout 300 --timeout-method thread -k "sac or actor or c5 or fused" -s
+  run c5_24 300 python bench.py --workload c5
+  run c5_breakdown24 300 python tools/c5_breakdown.py
+  BURN=640 FUSE=1 LAUNCHES=24 run fix24_f1 200 python tools/time_fused.py
+  ;;
+25)
+  run gpu_t25 900 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -v --timeout 300 --timeout-method thread \
+      -k "compaction or launcher" -s
+  for c in "-1 -1" "0 24" "50 24" "90 24" "100 24" "75 8" "90 8" "90 16"; do
+    set -- $c
+    run c4_262k_own$1_b$2 300 python bench.py --workload c4 --particles 262144 --steps 6 --warmup 2 --cpu-baseline 0 \
+        --policy-refill-own $1 --policy-refill $2
+  done
   ;;
 esac
 echo "=== done"
