@@ -35,6 +35,12 @@
 #  24: the staging loads issued ahead of the actor prologue: SAC tests, c5, breakdown, c3 fixed cost.
 #  25: refill from the waves' own particle ranges: the compaction tests, c4 at the whole swarm by
 #      own share and batch.
+#  26: the round's measurement, part 1: the GPU suite, the smoke, the bench lines (default, the
+#      driver's command, c4 at 32 768 and 262 144 particles, c5, c2).
+#  27: part 2: rocprofv3 kernel traces (default, driver command, c4, c5) and the PMC passes
+#      (tools/collect_r03.py r05 reduces both into profiles/).
+#  28: the c3 kernel under other compiler scheduling strategies (tools/variants.py: max-memory-clause,
+#      iterative-ilp, max-ilp, metric bias 0), c3 and c3-descent, two interleaved rounds.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -233,6 +239,31 @@ case "${PART:-1}" in
     set -- $c
     run c4_262k_own$1_b$2 300 python bench.py --workload c4 --particles 262144 --steps 6 --warmup 2 --cpu-baseline 0 \
         --policy-refill-own $1 --policy-refill $2
+  done
+  ;;
+26)
+  run gpu_tests 1000 python -u -m pytest tests/ -m gpu -x -q --timeout 300 --timeout-method thread
+  run smoke 200 python -c "import __graft_entry__ as g; g.smoke()"
+  run bench 300 python bench.py
+  run benchdrv 200 python bench.py --steps 20 --warmup 5
+  run c4 200 python bench.py --workload c4
+  run c4_262k 300 python bench.py --workload c4 --particles 262144 --steps 8 --warmup 2
+  run c5 200 python bench.py --workload c5
+  run c2 200 python bench.py --workload c2 --cpu-baseline 0
+  ;;
+27)
+  STAGES="prof profdrv profc4 profc5" run profs 800 bash tools/gpu_session.sh
+  run pmc 500 bash tools/pmc_r03b.sh
+  ;;
+28)
+  P=psso-sac-for-powered-descent_amd/pdenv
+  for r in 1 2; do
+    for v in base smem sitilp silp sbias0; do
+      lib=$P/libpdenv.so; [ $v != base ] && lib=$P/libpdenv_$v.so
+      for d in 0 1; do
+        PDENV_LIB=$lib DESCENT=$d BURN=640 FUSE=128 LAUNCHES=6 run t28_r${r}_${v}_d$d 200 python tools/time_fused.py
+      done
+    done
   done
   ;;
 esac
