@@ -1847,7 +1847,8 @@ pd_status rollout_policy_impl(pd_env* e, const float* w, int32_t max_steps, void
     // 5.5 / 5.0 / 5.0 ms at batches of 1 / 4 / 8 / 12 / 16 / 32 and 5.94 ms without refill)
     const int kRefillBatch = 48 / plpe;
     // (windless handles only: the windy policy kernels compile no refill, see pd_step_impl.h)
-    const bool refill = !wind && (e->tune.policy_refill > 0 || (e->tune.policy_refill < 0 && N > cap));
+    // (and a swarm of at least one wave's slots: the slots are whole waves, none past the swarm)
+    const bool refill = !wind && N >= 64 / plpe && (e->tune.policy_refill > 0 || (e->tune.policy_refill < 0 && N > cap));
     if (refill) {
         // slots: whole waves (epw envs each), at most the swarm; wave w owns particles
         // [w Q, (w + 1) Q) -- its first epw are its slots' first episodes -- and takes them
@@ -1858,12 +1859,11 @@ pd_status rollout_policy_impl(pd_env* e, const float* w, int32_t max_steps, void
         // batches of 24: the pool's batching idles more lanes than the waves' uneven work does)
         const int64_t epw = 64 / plpe;
         int64_t slots = std::min<int64_t>(N, e->tune.policy_slots > 0 ? e->tune.policy_slots : cap);
-        slots = std::max<int64_t>(epw, slots / epw * epw);
+        slots = std::max<int64_t>(epw, slots / epw * epw);   // (<= N: N >= epw)
         const int64_t waves = slots / epw;
         const int own = e->tune.policy_refill_own >= 0 ? e->tune.policy_refill_own : 100;
         int64_t q = (int64_t)((double)N * own / 100.0 / (double)waves) / epw * epw;
-        q = std::max<int64_t>(epw, std::min<int64_t>(q, N / waves / epw * epw));
-        if (waves * q > N) q = epw;   // (a swarm smaller than one wave per slot group)
+        q = std::max<int64_t>(epw, std::min<int64_t>(q, N / waves / epw * epw));   // (waves q <= N: N >= slots)
         PD_HIP(hipMemsetAsync(e->live_cnt, 0, 3 * sizeof(uint32_t), s));
         a.use_list = 0; a.policy_wc = nullptr;
         a.refill = e->tune.policy_refill > 0 ? e->tune.policy_refill : kRefillBatch;

@@ -964,6 +964,7 @@ def test_policy_rollout_compaction_invariant(pd):
     assert len(set(res[0][1].tolist())) > 5            # ragged episode lengths: compaction exercised
     sub = np.arange(0, len(W), 97)
     env2 = make(pd, len(sub), phase="landing_burn", mode="pso")
+    env2.set_tuning(policy_refill=8)   # (11 particles: fewer than a wave's slots, refill cannot run)
     f2, s2 = env2.rollout_policy(torch.tensor(W[sub]), max_steps=300)
     assert np.array_equal(s2.cpu().numpy(), res[0][1][sub])
     np.testing.assert_allclose(f2.cpu().numpy(), res[0][0][sub], rtol=1e-12)

@@ -41,6 +41,11 @@
 #      (tools/collect_r03.py r05 reduces both into profiles/).
 #  28: the c3 kernel under other compiler scheduling strategies (tools/variants.py: max-memory-clause,
 #      iterative-ilp, max-ilp, metric bias 0), c3 and c3-descent, two interleaved rounds.
+#  29: refill rollouts in a given hand-out order (the previous generation's longest episodes first):
+#      the compaction tests, c4 at the whole swarm with and without the order; then part 28.
+#  30: where a 4 096-env launch's fixed cost goes (c5's shape without the actor: LPE 16, no wind):
+#      PD_STAMP section clocks at 1 and 128 steps per launch.
+#  31: parts 28 and 30 (part 29's run of 28 used a binding the variants did not export).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -265,6 +270,27 @@ case "${PART:-1}" in
       done
     done
   done
+  ;;
+29)
+  run gpu_t29 900 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -v --timeout 300 --timeout-method thread \
+      -k "compaction or launcher" -s
+  for r in 1 2; do
+    for o in 1 0; do
+      run c4_262k_order${o}_r$r 300 python bench.py --workload c4 --particles 262144 --steps 8 --warmup 3 --cpu-baseline 0 --policy-order $o
+    done
+  done
+  PART=28 bash tools/r05_session.sh
+  ;;
+30)
+  V=psso-sac-for-powered-descent_amd/pdenv/libpdenv_stamp0.so
+  for f in 1 128; do
+    L=$(( f > 1 ? 6 : 40 ))
+    PDENV_LIB=$V N=4096 LPE=16 WIND=0 TILT=0 STATS=1 FUSE=$f LAUNCHES=$L BURN=256 run st30_f$f 200 python tools/time_fused.py
+    N=4096 LPE=16 WIND=0 TILT=0 FUSE=$f LAUNCHES=$L BURN=256 run t30_f$f 200 python tools/time_fused.py
+  done
+  ;;
+31)
+  PART=28 bash tools/r05_session.sh && PART=30 bash tools/r05_session.sh
   ;;
 esac
 echo "=== done"
