@@ -24,13 +24,20 @@ FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fP
 KSTEP = [(r, ph, w) for r in (0, 1) for ph in (0, 1, 2) for w in (0, 1)]
 
 
+# per-unit compiler flags: the c3 unit (binary64, pure throttle, wind) is scheduled for memory
+# clauses -- c3 -1.0 %, c3-descent -1.3 % against the default scheduler, two interleaved rounds
+# (profiles/r05_exp_sched.jsonl; max-ilp -1.2 / -1.0 %, iterative-ilp +0.8 %, metric bias 0 +-0),
+# the same registers and no scratch
+KSTEP_FLAGS = {(0, 0, 1): ["-mllvm", "-amdgpu-sched-strategy=max-memory-clause"]}
+
+
 def units():
     """(object path, source, defines) of every translation unit."""
     u = [(os.path.join(OBJ, "pdenv.o"), "pdenv.hip", []), (os.path.join(OBJ, "pdpso.o"), "pdpso.hip", []),
          (os.path.join(OBJ, "pdsac.o"), "pdsac.hip", [])]
     for r, ph, w in KSTEP:
         u.append((os.path.join(OBJ, f"kstep_r{r}_p{ph}_w{w}.o"), "kstep.hip",
-                  [f"-DPD_KR={r}", f"-DPD_KPH={ph}", f"-DPD_KW={w}"]))
+                  [f"-DPD_KR={r}", f"-DPD_KPH={ph}", f"-DPD_KW={w}"] + KSTEP_FLAGS.get((r, ph, w), [])))
     for r in (0, 1):   # the non-parity RK4 kernels (pure throttle, no wind) in units of their own
         u.append((os.path.join(OBJ, f"kstep_r{r}_rk4.o"), "kstep.hip", [f"-DPD_KR={r}", "-DPD_KPH=0", "-DPD_KW=0",
                                                                         "-DPD_KRK4=1"]))

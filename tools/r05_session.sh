@@ -46,6 +46,7 @@
 #  30: where a 4 096-env launch's fixed cost goes (c5's shape without the actor: LPE 16, no wind):
 #      PD_STAMP section clocks at 1 and 128 steps per launch.
 #  31: parts 28 and 30 (part 29's run of 28 used a binding the variants did not export).
+#  32: the build with the c3 unit scheduled for memory clauses: the c3 tests, c3 / c3-descent timing.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -291,6 +292,14 @@ case "${PART:-1}" in
   ;;
 31)
   PART=28 bash tools/r05_session.sh && PART=30 bash tools/r05_session.sh
+  ;;
+32)
+  run gpu_c3_32 900 python -u -m pytest tests/test_gpu_c3.py tests/test_gpu_parity.py -m gpu -x -q --timeout 300 \
+      --timeout-method thread -k "c3 or fused or ragged or teacher"
+  for r in 1 2; do for d in 0 1; do
+    DESCENT=$d BURN=640 FUSE=128 LAUNCHES=6 run t32_r${r}_d$d 200 python tools/time_fused.py
+  done; done
+  run benchdrv32 200 python bench.py --steps 20 --warmup 5
   ;;
 esac
 echo "=== done"
