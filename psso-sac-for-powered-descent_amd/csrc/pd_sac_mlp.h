@@ -56,7 +56,8 @@ template <int H> constexpr int sac_mlp_lds_floats() {
 
 // Envs e0 .. e0 + 15 (rows past n read a zero observation); put(e, o, v): head output o
 // (0 .. A-1 mean, A .. 2A-1 log_std, unclamped) of tile row e.  Called by all 256 threads of
-// the workgroup (it synchronises them); hb: sac_mlp_lds_floats<H>() floats of LDS.  MA: SacMlp
+// the workgroup (it synchronises them); hb: sac_mlp_lds_floats<H>() floats of LDS (a __shared__
+// array: the LDS DMA of the hidden layers addresses it as LDS).  MA: SacMlp
 // in any address space (the step kernel reads it from its kernarg segment).  mark(k): called by
 // every thread at the end of phase k (0 layer 1, l hidden layer l, L the heads) -- the section
 // clocks of tools/mlp_clocks.hip; the product passes none.

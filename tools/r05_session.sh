@@ -47,6 +47,7 @@
 #      PD_STAMP section clocks at 1 and 128 steps per launch.
 #  31: parts 28 and 30 (part 29's run of 28 used a binding the variants did not export).
 #  32: the build with the c3 unit scheduled for memory clauses: the c3 tests, c3 / c3-descent timing.
+#  33: the final build: part 26 again (suite, smoke, bench lines); 34: part 27 again (traces, PMC).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -300,6 +301,12 @@ case "${PART:-1}" in
     DESCENT=$d BURN=640 FUSE=128 LAUNCHES=6 run t32_r${r}_d$d 200 python tools/time_fused.py
   done; done
   run benchdrv32 200 python bench.py --steps 20 --warmup 5
+  ;;
+33)
+  PART=26 bash tools/r05_session.sh
+  ;;
+34)
+  PART=27 bash tools/r05_session.sh
   ;;
 esac
 echo "=== done"
