@@ -48,6 +48,8 @@
 #  31: parts 28 and 30 (part 29's run of 28 used a binding the variants did not export).
 #  32: the build with the c3 unit scheduled for memory clauses: the c3 tests, c3 / c3-descent timing.
 #  33: the final build: part 26 again (suite, smoke, bench lines); 34: part 27 again (traces, PMC).
+#  35: more scheduler flags on top of max-memory-clause (clause length 32, the AMDGPU pressure
+#      trackers, no high-pressure rescheduling) and max-ilp with trackers: c3 / c3-descent.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -307,6 +309,17 @@ case "${PART:-1}" in
   ;;
 34)
   PART=27 bash tools/r05_session.sh
+  ;;
+35)
+  P=psso-sac-for-powered-descent_amd/pdenv
+  for r in 1 2; do
+    for v in base mc32 mctrk mcnorp ilptrk; do
+      lib=$P/libpdenv.so; [ $v != base ] && lib=$P/libpdenv_$v.so
+      for d in 0 1; do
+        PDENV_LIB=$lib DESCENT=$d BURN=640 FUSE=128 LAUNCHES=6 run t35_r${r}_${v}_d$d 200 python tools/time_fused.py
+      done
+    done
+  done
   ;;
 esac
 echo "=== done"
