@@ -173,11 +173,13 @@ typedef struct {
                                  one chip round (default), 0 = never, 1 = from the first launch */
     double policy_list_at;    /* > 0 (with policy_list -1 or 0): switch the list on once the live count
                                  read back falls to this fraction of n_envs (default 0: never) */
-    int32_t policy_refill;    /* refill rollouts: -1 = when n_envs exceeds the chip's resident env slots
-                                 (default, batch: 3/4 of a wave's slots), 0 = never, k in 1..64 = always, batch k.  One launch of
-                                 policy_slots env slots (0: the resident capacity) steps the whole swarm:
-                                 an ended episode's lanes wait until k of their wave's slots wait (or none
-                                 is live), then take the next particles (a wave ballot, one atomic) */
+    int32_t policy_refill;    /* refill rollouts: -1 = every windless swarm of at least one wave's slots
+                                 (default; pool batch 3/4 of a wave's slots), 0 = never, k in 1..64 = on,
+                                 pool batch k.  One launch of policy_slots env slots (0: the resident
+                                 capacity) steps the whole swarm: a wave's slots take the next particles
+                                 of its own range as their episodes end (no atomic; policy_refill_own),
+                                 then the shared pool's once k of them wait (or none is live: a wave
+                                 ballot, one atomic).  Windy handles: the per-check launches */
     int32_t policy_slots;     /* env slots of a refill rollout (0 = the chip's resident capacity; rounded
                                  down to whole waves) */
     int32_t policy_refill_own;/* refill rollouts: percent of the swarm handed out from the waves' own

@@ -1847,8 +1847,11 @@ pd_status rollout_policy_impl(pd_env* e, const float* w, int32_t max_steps, void
     // 5.5 / 5.0 / 5.0 ms at batches of 1 / 4 / 8 / 12 / 16 / 32 and 5.94 ms without refill)
     const int kRefillBatch = 48 / plpe;
     // (windless handles only: the windy policy kernels compile no refill, see pd_step_impl.h)
-    // (and a swarm of at least one wave's slots: the slots are whole waves, none past the swarm)
-    const bool refill = !wind && N >= 64 / plpe && (e->tune.policy_refill > 0 || (e->tune.policy_refill < 0 && N > cap));
+    // (and a swarm of at least one wave's slots: the slots are whole waves, none past the swarm).
+    // Auto: every windless swarm -- beyond the resident slots for the refills, and within them for
+    // the one launch without live-count reads (c4 at 32 768 particles: 1.452 ms a generation
+    // against 1.476 with the per-check launches, profiles/r05_c4_refill.jsonl)
+    const bool refill = !wind && N >= 64 / plpe && e->tune.policy_refill != 0;
     if (refill) {
         // slots: whole waves (epw envs each), at most the swarm; wave w owns particles
         // [w Q, (w + 1) Q) -- its first epw are its slots' first episodes -- and takes them

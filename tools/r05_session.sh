@@ -50,6 +50,12 @@
 #  33: the final build: part 26 again (suite, smoke, bench lines); 34: part 27 again (traces, PMC).
 #  35: more scheduler flags on top of max-memory-clause (clause length 32, the AMDGPU pressure
 #      trackers, no high-pressure rescheduling) and max-ilp with trackers: c3 / c3-descent.
+#  36: c4 at the config's 32 768 particles per GPU: refill (one launch, no live-count reads)
+#      against the per-check launches, two rounds.
+#  37: the actor tile's weight blocks requested one block ahead across tile groups and layers (the
+#      first before layer 1): clocks, the SAC tests, c5.
+#  38: refill by default for every windless swarm: the policy / PSO / compaction / c4 shadow tests,
+#      c4 at 32 768 and 262 144 particles.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -320,6 +326,25 @@ case "${PART:-1}" in
       done
     done
   done
+  ;;
+36)
+  for r in 1 2; do
+    for b in 0 24; do
+      run c4_32k_36_rf${b}_r$r 300 python bench.py --workload c4 --steps 32 --warmup 4 --cpu-baseline 0 --policy-refill $b
+    done
+  done
+  ;;
+37)
+  run clk37_v10 60 tools/bin/mlp_clocks_v10
+  run gpu_sac37 600 python -u -m pytest tests/ -m gpu -x -q --timeout 300 --timeout-method thread -k "sac or actor or c5 or fused" -s
+  run c5_37 300 python bench.py --workload c5
+  run c5_breakdown37 300 python tools/c5_breakdown.py
+  ;;
+38)
+  run gpu_pol38 900 python -u -m pytest tests/ -m gpu -x -q --timeout 300 --timeout-method thread \
+      -k "policy or pso or compaction or c4 or drivers or swarm" -s
+  run c4_38 300 python bench.py --workload c4
+  run c4_262k_38 300 python bench.py --workload c4 --particles 262144 --steps 8 --warmup 2 --cpu-baseline 0
   ;;
 esac
 echo "=== done"
