@@ -56,6 +56,7 @@
 #      first before layer 1): clocks, the SAC tests, c5.
 #  38: refill by default for every windless swarm: the policy / PSO / compaction / c4 shadow tests,
 #      c4 at 32 768 and 262 144 particles.
+#  39 / 40: the final build: part 26 (suite, smoke, bench lines) and part 27 (traces, PMC) again.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -345,6 +346,12 @@ case "${PART:-1}" in
       -k "policy or pso or compaction or c4 or drivers or swarm" -s
   run c4_38 300 python bench.py --workload c4
   run c4_262k_38 300 python bench.py --workload c4 --particles 262144 --steps 8 --warmup 2 --cpu-baseline 0
+  ;;
+39)
+  PART=26 bash tools/r05_session.sh
+  ;;
+40)
+  PART=27 bash tools/r05_session.sh
   ;;
 esac
 echo "=== done"
