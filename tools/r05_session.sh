@@ -57,6 +57,9 @@
 #  38: refill by default for every windless swarm: the policy / PSO / compaction / c4 shadow tests,
 #      c4 at 32 768 and 262 144 particles.
 #  39 / 40: the final build: part 26 (suite, smoke, bench lines) and part 27 (traces, PMC) again.
+#  41: the driver window's launch/sync gap: the driver's command (c3 only) with the host spinning
+#      on completion (tools/spin_probe.py) and/or kernel arguments in device memory
+#      (HIP_FORCE_DEV_KERNARG=1), three interleaved rounds.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -352,6 +355,15 @@ case "${PART:-1}" in
   ;;
 40)
   PART=27 bash tools/r05_session.sh
+  ;;
+41)
+  A="--steps 20 --warmup 5 --cpu-baseline 0 --secondary 0 --descent 0 --fresh 0 --others 0"
+  for r in 1 2 3; do
+    run sp41_base_$r 200 python tools/spin_probe.py --spin 0 -- $A
+    run sp41_spin_$r 200 python tools/spin_probe.py --spin 1 -- $A
+    HIP_FORCE_DEV_KERNARG=1 run sp41_karg_$r 200 python tools/spin_probe.py --spin 0 -- $A
+    HIP_FORCE_DEV_KERNARG=1 run sp41_both_$r 200 python tools/spin_probe.py --spin 1 -- $A
+  done
   ;;
 esac
 echo "=== done"
