@@ -155,10 +155,16 @@ def bench_sac(args, world, rank, local, dist):
     col = SACCollector(env, actor, buf, dist, use_graph=args.graph == 1)
     for _ in range(args.warmup):
         col.step()
-    wall = timed_region(lambda k: col.step(), args.steps, torch.cuda.synchronize, dist, env.device)
-    # the dominant kernel's device time: the same step replayed with a HIP event pair per step on
-    # the stream the graph (one k_step<SAC> launch) runs on; the miss flush every 16th step is
-    # outside the graph and outside the pairs
+    r0, r1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    wall = timed_region(lambda k: col.step(), args.steps, torch.cuda.synchronize, dist, env.device,
+                        pre=r0.record, post=r1.record)
+    region_ms = r0.elapsed_time(r1) / args.steps
+    # the dominant kernel's device time.  Eager (the default): the timed region's own event pair
+    # on the stream the k_step<SAC> launches run on, per step -- the launches run back to back
+    # there (rocprofv3: no gap between them), so this is their average duration with the miss
+    # flush every 16th step included (an upper bound).  With a graph the region also holds the
+    # gaps its replays leave, so the kernel time is the same step run again with a HIP event pair
+    # per step (the flush outside the pairs).  The pairs are reported in both modes.
     kern = []
     for _ in range(min(args.steps, 64)):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -168,7 +174,13 @@ def bench_sac(args, world, rank, local, dist):
         kern.append((e0, e1))
     torch.cuda.synchronize()
     kern_ms = sorted(a.elapsed_time(b) for a, b in kern)
-    kern_avg = sum(kern_ms) / len(kern_ms)
+    # a pair also spans any host stall between its first event and the launch (the GPU idles
+    # there): pairs beyond 1.5x the median are such stalls (rocprofv3's k_step average agrees with
+    # the rest), left out of the average and counted
+    kern_med = kern_ms[len(kern_ms) // 2]
+    kern_in = [k for k in kern_ms if k <= 1.5 * kern_med]
+    pairs_avg = sum(kern_in) / len(kern_in)
+    kern_avg = pairs_avg if args.graph == 1 else region_ms
     if rank != 0:
         return None
     # per env-step: the env's algorithmic bytes (f64 pure throttle, no wind: SURVEY 8(d)), the
@@ -192,8 +204,15 @@ def bench_sac(args, world, rank, local, dist):
         "roofline": {"bound": "hbm", "achieved": bpe * n / (kern_avg * 1e-3) / 1e9, "peak": 8000.0, "unit": "GB/s",
                      "frac": bpe * n / (kern_avg * 1e-3) / 1e9 / 8000.0, "traffic": None,
                      "bytes_per_env_step": round(bpe, 1), "kernel": "k_step<SAC> (pd_step_sac_fused: actor MLP + step)",
-                     "kernel_avg_ms": kern_avg, "kernel_med_ms": kern_ms[len(kern_ms) // 2], "kernel_launches": len(kern_ms),
-                     "kernel_timing": "HIP events around each replayed collection step (its graph: one k_step launch)",
+                     "kernel_avg_ms": kern_avg, "kernel_launches": args.steps if args.graph != 1 else len(kern_in),
+                     "kernel_timing": ("the timed region's HIP event pair per step (back-to-back launches, the miss "
+                                       "flushes included)" if args.graph != 1 else
+                                       "HIP events around each replayed step (pairs beyond 1.5x the median, host "
+                                       "stalls, left out)"),
+                     "event_pairs": {"avg_ms": pairs_avg, "med_ms": kern_med, "pairs": len(kern_in),
+                                     "host_stalled": len(kern_ms) - len(kern_in),
+                                     "note": "a HIP event pair around each step run again: each pair adds its "
+                                             "events' own device time"},
                      "bytes_source": "SURVEY 8(d) env bytes + transition row + next obs32 + actor parameters / n"},
         "mfma_roofline": {"bound": "mfma", "achieved": fpe * n / (kern_avg * 1e-3) / 1e12, "peak": 157.3,
                           "unit": "TFLOP/s", "frac": fpe * n / (kern_avg * 1e-3) / 1e12 / 157.3,
@@ -567,7 +586,10 @@ def main():
                     help="c4: refill rollouts (pd_tuning.policy_refill: -1 auto, 0 off, k = batch of k waiting slots)")
     ap.add_argument("--policy-refill-own", type=int, default=-1,
                     help="c4: percent of the swarm refilled from the waves' own ranges (pd_tuning.policy_refill_own; -1 auto)")
-    ap.add_argument("--graph", type=int, default=1, help="c5: replay the collection step as a HIP graph")
+    ap.add_argument("--graph", type=int, default=0,
+                    help="c5: replay the collection step as a HIP graph (off: each replay left an 8.6 us gap "
+                         "between step kernels, eager launches none -- 0.0434 against 0.0392 ms per step, "
+                         "profiles/r05_exp_c5_graph.jsonl)")
     ap.add_argument("--c3-burn-in", type=int, default=C3_BURN_IN,
                     help="c3: untimed env-steps before the warmup (steady state: resets at their stationary rate)")
     ap.add_argument("--fresh", type=int, default=1,

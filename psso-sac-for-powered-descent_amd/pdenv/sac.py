@@ -257,8 +257,10 @@ class SACCollector:
     on the learner rank.
     fused=False: Actor.sample, pd_step, transition_slab, pd_observe, buffer.add_batch (the unfused
     reference path, eps from torch.randn with `generator`).
-    use_graph=True captures the step into one HIP graph (replaying removes the launch gaps; the
-    ring position lives on the device, so replays append in order).  The gather runs eagerly after
+    use_graph=True captures the step into one HIP graph (the ring position lives on the device, so
+    replays append in order).  Off by default: on ROCm 7 each replay of the one-kernel graph left
+    an 8.6 us gap before its step kernel, where eager launches from a host that keeps ahead of
+    the GPU run back to back (c5: 0.0434 against 0.0392 ms per step, profiles/r05_exp_c5_graph.jsonl).  The gather runs eagerly after
     each replay; the aero-miss flush every flush_every steps.
     step() returns the step's transition rows: a view of the replay ring's rows (valid until the
     ring wraps onto them) in ring mode, else a fresh tensor."""

@@ -60,6 +60,12 @@
 #  41: the driver window's launch/sync gap: the driver's command (c3 only) with the host spinning
 #      on completion (tools/spin_probe.py) and/or kernel arguments in device memory
 #      (HIP_FORCE_DEV_KERNARG=1), three interleaved rounds.
+#  42: c5 with and without the HIP graph (one pd_step_sac_fused launch per step either way), three
+#      interleaved rounds, and a rocprofv3 kernel trace of each (the gaps between the step kernels).
+#  43: eager c5 by default: the SAC / collector tests, bench.py --workload c5 (twice) and the
+#      default line (with its other_workloads).
+#  44: the c5 line with its kernel time from the timed region's events: twice, plus the rocprofv3
+#      stats of the same command (the k_step<SAC> average to compare).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -364,6 +370,26 @@ case "${PART:-1}" in
     HIP_FORCE_DEV_KERNARG=1 run sp41_karg_$r 200 python tools/spin_probe.py --spin 0 -- $A
     HIP_FORCE_DEV_KERNARG=1 run sp41_both_$r 200 python tools/spin_probe.py --spin 1 -- $A
   done
+  ;;
+42)
+  for r in 1 2 3; do
+    run c5g1_$r 200 python bench.py --workload c5 --cpu-baseline 0 --graph 1
+    run c5g0_$r 200 python bench.py --workload c5 --cpu-baseline 0 --graph 0
+  done
+  for g in 1 0; do
+    run c5trace_g$g 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/c5trace_g$g -o run -- python3 bench.py --workload c5 --cpu-baseline 0 --steps 192 --warmup 32 --graph $g
+  done
+  ;;
+43)
+  run gpu_sac43 600 python -u -m pytest tests/ -m gpu -x -q --timeout 300 --timeout-method thread -k "sac or actor or c5 or collector" -s
+  run c5_43a 300 python bench.py --workload c5
+  run c5_43b 300 python bench.py --workload c5
+  run bench43 600 python bench.py
+  ;;
+44)
+  run c5_44a 300 python bench.py --workload c5
+  run c5_44b 300 python bench.py --workload c5
+  run c5prof44 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/c5prof44 -o run -- python3 bench.py --workload c5
   ;;
 esac
 echo "=== done"
