@@ -66,6 +66,13 @@
 #      default line (with its other_workloads).
 #  44: the c5 line with its kernel time from the timed region's events: twice, plus the rocprofv3
 #      stats of the same command (the k_step<SAC> average to compare).
+#  45: c4 with the subswarm membership mirrored on the host (a migration no longer reads the
+#      device back) and pinned index copies: the PSO tests, c4 twice, the rocprofv3 trace.
+#  46: part 45 again with share_information on the device (no read-back of the subswarm bests).
+#  47: part 45 again: the share draws and the migration writes as kernel scalars (no host copies).
+#  48: part 45 again: the best subswarm's row taken without indexing by a 0-d tensor (a read-back).
+#  49: part 45 again: the migration mirror and scalar writes kept, share_information back on the host
+#      path (the device path measured no better: its ~25 small kernels cost what the read-back did).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -390,6 +397,16 @@ case "${PART:-1}" in
   run c5_44a 300 python bench.py --workload c5
   run c5_44b 300 python bench.py --workload c5
   run c5prof44 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/c5prof44 -o run -- python3 bench.py --workload c5
+  ;;
+45)
+  run gpu_pso45 900 python -u -m pytest tests/ -m gpu -x -q --timeout 300 --timeout-method thread \
+      -k "policy or pso or compaction or c4 or drivers or swarm or migrat or share" -s
+  run c4_45a 300 python bench.py --workload c4
+  run c4_45b 300 python bench.py --workload c4
+  STAGES="profc4" run profs45 800 bash tools/gpu_session.sh
+  ;;
+46|47|48|49)
+  PART=45 bash tools/r05_session.sh
   ;;
 esac
 echo "=== done"
