@@ -71,6 +71,7 @@
 #  46: part 45 again with share_information on the device (no read-back of the subswarm bests).
 #  47: part 45 again: the share draws and the migration writes as kernel scalars (no host copies).
 #  48: part 45 again: the best subswarm's row taken without indexing by a 0-d tensor (a read-back).
+#  50: the final build again: part 26 (suite, smoke, bench lines).
 #  49: part 45 again: the migration mirror and scalar writes kept, share_information back on the host
 #      path (the device path measured no better: its ~25 small kernels cost what the read-back did).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -368,6 +369,9 @@ case "${PART:-1}" in
   ;;
 40)
   PART=27 bash tools/r05_session.sh
+  ;;
+50)
+  PART=26 bash tools/r05_session.sh
   ;;
 41)
   A="--steps 20 --warmup 5 --cpu-baseline 0 --secondary 0 --descent 0 --fresh 0 --others 0"
