@@ -72,6 +72,7 @@
 #  47: part 45 again: the share draws and the migration writes as kernel scalars (no host copies).
 #  48: part 45 again: the best subswarm's row taken without indexing by a 0-d tensor (a read-back).
 #  50: the final build again: part 26 (suite, smoke, bench lines).
+#  51: part 45 again: the PSO update with four parameters per thread (one Philox draw, loads first).
 #  49: part 45 again: the migration mirror and scalar writes kept, share_information back on the host
 #      path (the device path measured no better: its ~25 small kernels cost what the read-back did).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -409,7 +410,7 @@ case "${PART:-1}" in
   run c4_45b 300 python bench.py --workload c4
   STAGES="profc4" run profs45 800 bash tools/gpu_session.sh
   ;;
-46|47|48|49)
+46|47|48|49|51)
   PART=45 bash tools/r05_session.sh
   ;;
 esac
