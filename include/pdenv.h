@@ -174,7 +174,9 @@ typedef struct {
     double policy_list_at;    /* > 0 (with policy_list -1 or 0): switch the list on once the live count
                                  read back falls to this fraction of n_envs (default 0: never) */
     int32_t policy_refill;    /* refill rollouts: -1 = every windless swarm of at least one wave's slots
-                                 (default; pool batch 3/4 of a wave's slots), 0 = never, k in 1..64 = on,
+                                 unless policy_list >= 0 or policy_list_at > 0 asks for the per-check
+                                 launches (default; pool batch 3/4 of a wave's slots), 0 = never, k in
+                                 1..64 = on (policy_list, policy_list_at and check_every then do nothing),
                                  pool batch k.  One launch of policy_slots env slots (0: the resident
                                  capacity) steps the whole swarm: a wave's slots take the next particles
                                  of its own range as their episodes end (no atomic; policy_refill_own),
@@ -333,7 +335,11 @@ pd_status pd_rollout(pd_env* env, const void* actions, int32_t n_steps, void* re
  * Each launch runs up to 64 fused steps (pd_tuning.policy_fuse); a finished episode's lanes freeze
  * and a wave whose episodes have all ended leaves the launch.  Grids beyond one chip round of lanes
  * step only the live envs (pd_tuning.policy_list): a compacted index list, rebuilt inside the step
- * kernel (wave ballot + prefix count, one atomic per wave).  Results do not depend on either. */
+ * kernel (wave ballot + prefix count, one atomic per wave).  Results do not depend on either.
+ * A refill rollout (pd_tuning.policy_refill; the default for windless swarms) is ONE launch that
+ * steps the whole swarm: it reads no live count, so check_every, policy_list and policy_list_at
+ * apply only when refill is off (an explicit policy_list >= 0 or policy_list_at > 0 with
+ * policy_refill -1 turns it off). */
 pd_status pd_rollout_policy(pd_env* env, const float* weights, int32_t n_params, int32_t max_steps,
                             void* fitness, int32_t* steps, int32_t check_every, void* stream);
 /* One PSO generation's particle update on the device (particle_swarm_optimisation.py:437-441

@@ -1356,7 +1356,9 @@ static void* sac_worker(void* p) { sac_range((sac_job*)p); return NULL; }
 double orc_sac_collect_mt(const orc_params* P, int n_env, int n_steps, int S, int H, int L, int A,
                           const float* const* prm, uint64_t seed, int n_threads, int64_t* env_steps_out) {
     pthread_once(&g_log_once, log_cells_fill);
-    if (S > 16 || A > 8 || H > ORC_SAC_MAXH || L < 1) return 0.0;
+    /* the pure-throttle SAC task only (sac_range hard-codes that phase: S = 2 observations, A = 1
+     * action); anything else is refused rather than run on fixed-size buffers */
+    if (S != 2 || A != 1 || H > ORC_SAC_MAXH || H < 1 || L < 1) return 0.0;
     if (n_threads < 1) n_threads = 1;
     if (n_threads > n_env) n_threads = n_env > 0 ? n_env : 1;
     sac_job* jobs = (sac_job*)calloc((size_t)n_threads, sizeof(sac_job));

@@ -22,6 +22,12 @@
 //   heads (A outputs each): 16 lanes per env split the H-term dots (their weights and biases
 //                           requested at the start and held in registers when they fit), a
 //                           shuffle tree adds them.
+// Occupancy and waits: in the fused c5 step kernel (LPE 16, binary32 state I/O) the ring takes
+// the workgroup's LDS to ~100 KB, so a CU holds one such workgroup: one wave per SIMD
+// (profiles/r05_resource_usage.txt, the SAC LPE-16 rows).  Each k-block waits for its ring
+// fill with s_waitcnt vmcnt(0), which also drains the env-state and table-staging loads the
+// step kernel issued ahead of the actor; the c5 gain of the ring was measured with both costs
+// in it.
 // Numerics: f32 throughout (the reference's dtype); the sums run in another order than
 // hipBLASLt's (both are f32 GEMMs of the same Linear layers), so the heads agree with torch's to
 // f32 rounding, not bit for bit (tests/test_gpu_parity.py bounds it).  pd_sac_actor and the fused

@@ -40,15 +40,10 @@ constexpr uint32_t kFineIndex = kFineRefined - 1u;
 // coefficients row by row (u^i, i = kCellDeg .. 0; within a row v^j, j = kCellDeg - i .. 0), then
 // per exact term (Mach, coefficient / 8, AoA), then the neighbourhood's key (its bits), padded to 16
 // bytes.
-#ifndef PD_CELL_DEG
-#define PD_CELL_DEG 8
-#endif
-#ifndef PD_CELL_EXACT
-#define PD_CELL_EXACT 4
-#endif
-constexpr int kCellDeg = PD_CELL_DEG;
+// (degree 7 and 3 exact terms were measured in round 3 and dropped: DESIGN.md s9)
+constexpr int kCellDeg = 8;
 constexpr int kCellCoef = (kCellDeg + 1) * (kCellDeg + 2) / 2;
-constexpr int kCellExact = PD_CELL_EXACT;
+constexpr int kCellExact = 4;
 constexpr int kCellKey = kCellCoef + 3 * kCellExact;
 constexpr int kCellStride = (kCellKey + 2) & ~1;
 // binary32 handles: the same record in floats, the key's 8 bytes at an 8-byte aligned float index,
@@ -68,10 +63,7 @@ struct GridBisect {
     int slot_a, slot_b;
     int piece_a, piece_b;   // each side's cell piece (binary64 handles; -1: none)
 };
-#ifndef PD_GRID_SUB
-#define PD_GRID_SUB 8
-#endif
-constexpr int kGridSub = PD_GRID_SUB;   // sub-cells per refined cell side
+constexpr int kGridSub = 8;   // sub-cells per refined cell side
 constexpr int kStats = 48;            // pend.stats words (see Stat)
 
 // pend.stats[] words
@@ -198,7 +190,42 @@ struct Pending {
     unsigned long long* stats;   // [kStats]
     double* solve_ws;            // [kSolveSlots][kScratch] exact-solve scratch (global memory)
     int* solve_lock;             // [kSolveSlots]
+    unsigned int* ticket;        // [1] workgroups of the step launch that have finished (0 between launches)
 };
+
+// Insert the queued neighbourhoods into the device tables and empty the queue; one thread, with
+// nothing else reading the tables (k_insert after a launch, or the last workgroup of a step launch
+// once every other workgroup has finished).  Open addressing, load factor <= 1/2; a key already
+// present is skipped.
+template <typename R>
+__device__ void insert_pending(unsigned long long* count, const unsigned long long* pkeys, const double* ppay,
+                               unsigned long long* stats, unsigned long long* keys_cd, R* pay_cd, int lc_cd,
+                               unsigned long long* keys_cl, R* pay_cl, int lc_cl) {
+    unsigned long long cnt = *count;
+    if (cnt == 0) return;
+    if (cnt > (unsigned long long)kPendingCap) cnt = kPendingCap;
+    for (unsigned long long e = 0; e < cnt; ++e) {
+        const unsigned long long kk = pkeys[e];
+        const int table = (int)(kk >> 63);
+        const unsigned long long key = kk & ~(1ull << 63);
+        unsigned long long* keys = table ? keys_cl : keys_cd;
+        const int lc = table ? lc_cl : lc_cd;
+        uint32_t mask = (1u << lc) - 1u, h = key_hash(key, lc);
+        int slot = -1;
+        for (uint32_t p = 0; p <= mask; ++p) {
+            const unsigned long long k = keys[h];
+            if (k == key) { slot = -1; break; }
+            if (k == kEmptyKey) { slot = (int)h; break; }
+            h = (h + 1) & mask;
+        }
+        if (slot >= 0 && stats[kStInsCd + table] * 2 + 2 > (1ull << lc)) slot = -1;
+        if (slot < 0) continue;
+        stats[kStInsCd + table] += 1;
+        keys[slot] = key;
+        pay_store<R>(ppay + e * kPay, (table ? pay_cl : pay_cd) + (int64_t)slot * pay_stride<R>());
+    }
+    *count = 0;
+}
 
 template <typename R> struct StepArgs {
     uint64_t P;                      // const DevParams<R>* (read through a constant-AS view)

@@ -378,6 +378,9 @@ __device__ __forceinline__ R rbf_miss_wave(const AT& a, DP<R>& P, int table, con
             if (idx < (unsigned long long)kPendingCap) {
                 for (int j = 0; j < kPay; ++j) a.pend.pay[idx * kPay + j] = pay[j];
                 a.pend.keys[idx] = lk | ((unsigned long long)lt << 63);
+                // (release, device scope: the entry reaches memory before this workgroup takes
+                // its end-of-launch ticket, so the inserting workgroup on any XCD reads it)
+                __threadfence();
             } else {
                 atomicAdd(&a.pend.stats[kStDropped], 1ull);   // solved again until a later flush
             }
@@ -2179,6 +2182,24 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(2)))
                     a.ring_state[1] = (long long)(sz > a.ring_cap ? a.ring_cap : sz);
                     a.ring_state[2] = 0;
                 }
+            }
+        }
+    }
+    if constexpr (!POL) {
+        // the launch's last workgroup inserts the neighbourhoods its launch solved (no k_insert
+        // launch after every step launch): a ticket per workgroup, taken once all of its waves are
+        // past their table reads; the other workgroups' queued entries were released by their
+        // writers (rbf_miss_wave), the acquire below makes them visible here.  (Policy launches
+        // have waves that leave early, so no workgroup barrier here: they keep k_insert.)
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const unsigned int t = atomicAdd(a.pend.ticket, 1u);
+            if (t == gridDim.x - 1u) {
+                __threadfence();
+                DP<R>& P = *params<R>(a.P);
+                insert_pending<R>(a.pend.count, a.pend.keys, a.pend.pay, a.pend.stats, (unsigned long long*)P.keys_cd, (R*)P.pay_cd, P.logcap_cd,
+                                  (unsigned long long*)P.keys_cl, (R*)P.pay_cl, P.logcap_cl);
+                *a.pend.ticket = 0u;
             }
         }
     }

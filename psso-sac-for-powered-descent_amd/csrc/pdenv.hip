@@ -77,46 +77,14 @@ __global__ __launch_bounds__(kBlock) void k_reset(StepArgs<R> a, const uint8_t* 
     store_env<R>(a, P, ui, e, true);
 }
 
-// Insert the neighbourhoods solved on device during the last launch (single block; the only
-// writer of the tables, stream-ordered between step launches, so readers never race it).
+// Insert the neighbourhoods solved on device during the last launch (single thread; the only
+// writer of the tables, stream-ordered between launches, so readers never race it).  The step
+// launches insert their own (their last workgroup, k_step); this serves the policy rollouts and
+// pd_flush_misses.
 template <typename R>
 __global__ void k_insert(Pending pend, unsigned long long* keys_cd, R* pay_cd, int lc_cd,
                          unsigned long long* keys_cl, R* pay_cl, int lc_cl) {
-    __shared__ int s_slot;
-    unsigned long long cnt = *pend.count;
-    if (cnt == 0) return;
-    if (cnt > (unsigned long long)kPendingCap) cnt = kPendingCap;
-    for (unsigned long long e = 0; e < cnt; ++e) {
-        if (threadIdx.x == 0) {
-            unsigned long long kk = pend.keys[e];
-            int table = (int)(kk >> 63);
-            unsigned long long key = kk & ~(1ull << 63);
-            unsigned long long* keys = table ? keys_cl : keys_cd;
-            int lc = table ? lc_cl : lc_cd;
-            uint32_t mask = (1u << lc) - 1u, h = key_hash(key, lc);
-            int slot = -1;
-            for (uint32_t p = 0; p <= mask; ++p) {
-                unsigned long long k = keys[h];
-                if (k == key) { slot = -1; break; }
-                if (k == kEmptyKey) { slot = (int)h; break; }
-                h = (h + 1) & mask;
-            }
-            // keep the load factor <= 1/2
-            if (slot >= 0 && pend.stats[kStInsCd + table] * 2 + 2 > (1ull << lc)) slot = -1;
-            if (slot >= 0) { pend.stats[kStInsCd + table] += 1; }
-            s_slot = slot >= 0 ? (slot | (table << 30)) : -1;
-            if (slot >= 0) keys[slot] = key;
-        }
-        __syncthreads();
-        int sl = s_slot;
-        if (sl >= 0) {
-            int table = sl >> 30, slot = sl & ((1 << 30) - 1);
-            R* pay = (table ? pay_cl : pay_cd) + (int64_t)slot * pay_stride<R>();
-            if (threadIdx.x == 0) pay_store<R>(pend.pay + e * kPay, pay);
-        }
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) *pend.count = 0;
+    if (threadIdx.x == 0) insert_pending<R>(pend.count, pend.keys, pend.pay, pend.stats, keys_cd, pay_cd, lc_cd, keys_cl, pay_cl, lc_cl);
 }
 
 template <typename R>
@@ -1694,9 +1662,11 @@ template <typename R> pd_status create_impl(const pd_params* p, const pd_config*
         (st = dalloc(e, (void**)&e->pend.pay, (size_t)kPendingCap * kPay * 8)) ||
         (st = dalloc(e, (void**)&e->pend.stats, kStats * 8)) ||
         (st = dalloc(e, (void**)&e->pend.solve_ws, (size_t)kSolveSlots * kScratch * 8)) ||
-        (st = dalloc(e, (void**)&e->pend.solve_lock, (size_t)kSolveSlots * 4)))
+        (st = dalloc(e, (void**)&e->pend.solve_lock, (size_t)kSolveSlots * 4)) ||
+        (st = dalloc(e, (void**)&e->pend.ticket, 4)))
         return st;
     PD_HIP(hipMemset(e->pend.count, 0, 8));
+    PD_HIP(hipMemset(e->pend.ticket, 0, 4));
     PD_HIP(hipMemset(e->pend.solve_lock, 0, (size_t)kSolveSlots * 4));
     unsigned long long stats0[kStats] = {0, 0, (unsigned long long)tcd.entries, (unsigned long long)tcl.entries};
     PD_HIP(hipMemcpy(e->pend.stats, stats0, sizeof(stats0), hipMemcpyHostToDevice));
@@ -1751,7 +1721,7 @@ template <typename R, int PH, bool W> void launch_policy(int lpe, const StepArgs
 }
 
 template <typename R> void launch_insert(pd_env* e, hipStream_t s) {
-    hipLaunchKernelGGL(k_insert<R>, dim3(1), dim3(kPay), 0, s, e->pend, e->keys_cd, (R*)e->pay_cd, e->logcap_cd,
+    hipLaunchKernelGGL(k_insert<R>, dim3(1), dim3(64), 0, s, e->pend, e->keys_cd, (R*)e->pay_cd, e->logcap_cd,
                        e->keys_cl, (R*)e->pay_cl, e->logcap_cl);
 }
 
@@ -1851,7 +1821,11 @@ pd_status rollout_policy_impl(pd_env* e, const float* w, int32_t max_steps, void
     // Auto: every windless swarm -- beyond the resident slots for the refills, and within them for
     // the one launch without live-count reads (c4 at 32 768 particles: 1.452 ms a generation
     // against 1.476 with the per-check launches, profiles/r05_c4_refill.jsonl)
-    const bool refill = !wind && N >= 64 / plpe && e->tune.policy_refill != 0;
+    // (auto refill yields to an explicit request for the per-check launches: policy_list >= 0 or
+    // policy_list_at > 0 with policy_refill -1; check_every and the list apply to those only)
+    const bool refill_on = e->tune.policy_refill > 0 ||
+                           (e->tune.policy_refill < 0 && e->tune.policy_list < 0 && !(e->tune.policy_list_at > 0.0));
+    const bool refill = !wind && N >= 64 / plpe && refill_on;
     if (refill) {
         // slots: whole waves (epw envs each), at most the swarm; wave w owns particles
         // [w Q, (w + 1) Q) -- its first epw are its slots' first episodes -- and takes them
@@ -1943,7 +1917,7 @@ pd_status rollout_policy_impl(pd_env* e, const float* w, int32_t max_steps, void
 // (c3 ms per env-step, payload sums: 16 -> 0.0450, 32 -> 0.0442, 64 -> 0.0421; cell pieces: 64 ->
 // 0.0341, 128 -> 0.0335, 256 -> 0.0337).
 
-// n_steps env-steps in launches of pd_tuning.step_fuse fused steps, each followed by the miss flush.
+// n_steps env-steps in launches of pd_tuning.step_fuse fused steps (each inserts its own misses).
 // Row t of every [n_steps][N...] array belongs to step t; NULL outputs are not written.
 pd_status step_n_impl(pd_env* e, const void* actions, int32_t n_steps, void* obs, void* reward, uint8_t* done,
                       uint8_t* trunc, int8_t* tid, void* reward_sum, hipStream_t s, void* info = nullptr,
@@ -1963,7 +1937,8 @@ pd_status step_n_impl(pd_env* e, const void* actions, int32_t n_steps, void* obs
             : step_impl<float>(e, act, at(obs, so), at(reward, sr), (uint8_t*)at(done, N), (uint8_t*)at(trunc, N),
                                (int8_t*)at(tid, N), nullptr, at(info, si), reward_sum, s, k, nullptr, info_mask);
         if (st != PD_OK) return st;
-        if ((st = pd_flush_misses(e, s)) != PD_OK) return st;
+        // (no miss flush between the launches: each step launch's last workgroup inserts the
+        // neighbourhoods its launch solved, k_step's tail)
     }
     return PD_OK;
 }
@@ -2286,7 +2261,6 @@ pd_status pd_rollout(pd_env* e, const void* actions, int32_t n_steps, void* rewa
             ? step_impl<double>(e, at, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, reward_sum, (hipStream_t)stream)
             : step_impl<float>(e, at, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, reward_sum, (hipStream_t)stream);
         if (st != PD_OK) return st;
-        if ((t & 15) == 15 || t + 1 == n_steps) { if ((st = pd_flush_misses(e, stream)) != PD_OK) return st; }
     }
     return PD_OK;
 }

@@ -298,8 +298,16 @@ class PoweredDescentEnv:
         else:
             ptrs = [None] * 5
         if info_keys:
-            idx = sorted(L.INFO_FIELDS.index(k) for k in info_keys)
-            mask = sum(1 << j for j in idx)
+            keys = list(info_keys)
+            bad = [k for k in keys if k not in L.INFO_FIELDS]
+            if bad:
+                raise ValueError(f"unknown info keys {bad} (pdenv._lib.INFO_FIELDS)")
+            if len(set(keys)) != len(keys):
+                raise ValueError(f"info_keys holds a key more than once: {keys}")
+            idx = sorted(L.INFO_FIELDS.index(k) for k in keys)
+            mask = 0
+            for j in idx:
+                mask |= 1 << j
             inf = torch.empty(T, len(idx), self.n, dtype=self.dtype, device=self.device)
             L.check(self.lib.pd_step_n_info(self.h, _ptr(a), T, *ptrs, _ptr(inf), mask, _stream(self.device)))
         else:

@@ -142,9 +142,14 @@ class ParticleSubswarmOptimisationGPU:
 
     # ------------------------------------------------------------------ state
     def initialize_swarms(self):
-        g = torch.Generator(device=self.device).manual_seed(self.seed * 1000003 + self.rank)
-        u = torch.rand(self.D, self.P, generator=g, device=self.device, dtype=torch.float64)
+        # the GLOBAL swarm's uniforms from one seed on every rank, this rank's columns kept: a
+        # particle's start position depends on its global index only, so any world size starts
+        # from the same swarm (and world 1 draws exactly what it always drew)
+        g = torch.Generator(device=self.device).manual_seed(self.seed * 1000003)
+        u = torch.rand(self.D, self.P * self.world, generator=g, device=self.device, dtype=torch.float64)
+        u = u[:, self.offset:self.offset + self.P]
         self.x = (self.lower[:, None] + (self.upper - self.lower)[:, None] * u).contiguous()
+        del u
         self.v = torch.zeros_like(self.x)
         self.pb = torch.zeros_like(self.x)
         self.pbf = torch.full((self.P,), math.inf, dtype=torch.float64, device=self.device)
@@ -163,7 +168,7 @@ class ParticleSubswarmOptimisationGPU:
         self.gb_t = torch.zeros(self.D, dtype=torch.float64, device=self.device)
         self._cols = torch.arange(self.S, device=self.device)
         self.w = self.p["w_start"]
-        self.env = self._new_env(self.P) if self.P > 0 else None
+        self.env = self._new_env(self.P, self.offset) if self.P > 0 else None
         # share_information evaluates 1..S-1 moved subswarm bests: one handle of S - 1 envs made
         # here (creating a handle inside a generation costs tens of ms), candidates padded to it
         self._aux = {self.S - 1: self._new_env(self.S - 1)} if self.S > 1 else {}
@@ -174,8 +179,10 @@ class ParticleSubswarmOptimisationGPU:
         self._make_merged_handle()
         self._warm_share_path()
 
-    def _new_env(self, n):
-        env = PoweredDescentEnv(n, self.flight_phase, **self.env_kw)
+    def _new_env(self, n, offset=0):
+        """A rollout handle of n envs whose env i is global particle offset + i (the Philox key
+        of a stochastic-wind episode: the same draws at any world size)."""
+        env = PoweredDescentEnv(n, self.flight_phase, env_offset=offset, **self.env_kw)
         if self.tuning:
             env.set_tuning(**self.tuning)
         return env
@@ -192,7 +199,7 @@ class ParticleSubswarmOptimisationGPU:
         for k in [k for k in self._aux if k not in (self.S - 1, n)]:   # (a merged handle of an earlier P)
             self._aux.pop(k).close()
         if self._mergeable() and n not in self._aux:
-            self._aux[n] = self._new_env(n)
+            self._aux[n] = self._new_env(n, self.offset)
 
     def _warm_share_path(self):
         """share_information's tensor operations once on scratch copies (no rng draws, no state
@@ -388,5 +395,5 @@ class ParticleSubswarmOptimisationGPU:
         self.P = int(sel.numel())
         if self.env is not None:
             self.env.close()
-        self.env = self._new_env(self.P) if self.P > 0 else None
+        self.env = self._new_env(self.P, self.offset) if self.P > 0 else None
         self._make_merged_handle()

@@ -1162,3 +1162,8 @@ def test_step_n_info_tap_matches_step(pd, precision):
     for k in keys:
         assert torch.equal(tap[k], torch.stack(ref[k])), k
     assert torch.equal(one.state, fused.state)
+    #  a repeated or unknown key is refused before any launch: a repeated key's bit
+    # would carry into the next field's and the tap would return unwritten rows
+    for bad in (["mach_number", "mach_number"], ["no_such_key"]):
+        with pytest.raises(ValueError):
+            fused.step_n(A[:2], info_keys=bad)

@@ -98,8 +98,11 @@ case "${PART:-1}" in
   for f in 20 128; do
     STATS=1 BURN=640 FUSE=$f LAUNCHES=6 PDENV_LIB=$PKG/libpdenv_stamp.so run stamp_f$f 200 python tools/time_fused.py
   done
-  PDENV_COMPACT=1 run c4_262k_list 300 python bench.py --workload c4 --particles 262144 --steps 6 --warmup 2 --cpu-baseline 0
-  PDENV_COMPACT=0 run c4_262k_nolist 300 python bench.py --workload c4 --particles 262144 --steps 6 --warmup 2 --cpu-baseline 0
+  # (the records of part 1 came from the pre-ABI-9 library, where the PDENV_COMPACT environment
+  # switch chose the live list; ABI 9 removed every getenv switch, so the same comparison is now
+  # made with the tuning flags below -- refill off, list on / off)
+  run c4_262k_list 300 python bench.py --workload c4 --particles 262144 --steps 6 --warmup 2 --cpu-baseline 0 --policy-list 1 --policy-refill 0
+  run c4_262k_nolist 300 python bench.py --workload c4 --particles 262144 --steps 6 --warmup 2 --cpu-baseline 0 --policy-list 0 --policy-refill 0
   ;;
 2)
   # the ABI-9 build (launcher checks, two-step divisions where the divisor needs them, tuning and
