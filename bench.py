@@ -192,17 +192,25 @@ def bench_sac(args, world, rank, local, dist):
         + 4.0 * n_par / n
     fpe = 2.0 * (S * H + H * H + 2 * H * A)
     out = {
-        "metric": "SAC collection env-steps/sec (c5: actor + env + RCCL gather + prioritized replay buffer)",
+        "metric": ("SAC collection env-steps/sec (c5: actor + env + RCCL all_gather of the transition rows + "
+                   "prioritized replay buffer)" if dist else
+                   "SAC collection env-steps/sec (c5: actor + env + prioritized replay buffer, one launch per step; "
+                   "one process, no collective)"),
         "value": whole_job_rate(n, world, args.steps, wall), "unit": "env-steps/s",
         "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": wall / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": args.precision,
         "data": "synthetic (random-init SAC actor 2-256-256-1, reference initial state, no wind)",
         "config": {"workload": "c5: SAC collection, landing_burn_pure_throttle, rtd_rl, auto-reset",
-                   "envs_per_gpu": n, "global_envs": n * world, "parallelism": f"env-shard x{world} + all_gather"},
+                   "envs_per_gpu": n, "global_envs": n * world,
+                   "parallelism": f"env-shard x{world} + all_gather" if dist else "one process (no process group)"},
         "replay_buffer_size": len(buf), "hip_graph": args.graph == 1,
         "roofline": {"bound": "hbm", "achieved": bpe * n / (kern_avg * 1e-3) / 1e9, "peak": 8000.0, "unit": "GB/s",
-                     "frac": bpe * n / (kern_avg * 1e-3) / 1e9 / 8000.0, "traffic": None,
+                     "frac": bpe * n / (kern_avg * 1e-3) / 1e9 / 8000.0,
+                     "traffic": pmc_traffic("c5", n) if n == 4096 else None,
+                     "traffic_bytes_per_env_step": pmc_traffic("c5", 1) if n == 4096 else None,
+                     "traffic_source": PMC_C4C5 + " (case c5: 2 FETCH_SIZE + WRITE_SIZE of the k_step<SAC> launch, "
+                                       "per launch of n env-steps)",
                      "bytes_per_env_step": round(bpe, 1), "kernel": "k_step<SAC> (pd_step_sac_fused: actor MLP + step)",
                      "kernel_avg_ms": kern_avg, "kernel_launches": args.steps if args.graph != 1 else len(kern_in),
                      "kernel_timing": ("the timed region's HIP event pair per step (back-to-back launches, the miss "
@@ -295,7 +303,10 @@ def bench_pso(args, world, rank, local, dist):
         "env_steps_per_s_est": eps * mean_len, "mean_episode_len_after": mean_len,
         "global_best_fitness": opt.gbf,
         "roofline": {"bound": "hbm", "achieved": bpp * P / (kern_avg * 1e-3) / 1e9, "peak": 8000.0, "unit": "GB/s",
-                     "frac": bpp * P / (kern_avg * 1e-3) / 1e9 / 8000.0, "traffic": None,
+                     "frac": bpp * P / (kern_avg * 1e-3) / 1e9 / 8000.0,
+                     "traffic": pmc_traffic(f"c4_{P}", P), "traffic_bytes_per_particle_episode": pmc_traffic(f"c4_{P}", 1),
+                     "traffic_source": PMC_C4C5 + f" (case c4_{P}: 2 FETCH_SIZE + WRITE_SIZE of the policy k_step "
+                                       f"launches of one rollout, per rollout of {P} particles; null: no pass at this size)",
                      "bytes_per_particle_episode": round(bpp, 1), "kernel": "k_step<POL> (pd_rollout_policy)",
                      "kernel_avg_ms": kern_avg, "kernel_med_ms": kern_ms[len(kern_ms) // 2], "rollouts": len(kern_ms),
                      "kernel_timing": "HIP events around each replayed rollout of the swarm's positions (its reset, "
@@ -550,6 +561,19 @@ def c3_summary(args, r, world, precision, pmc=None):
     return out
 
 
+PMC_C4C5 = "profiles/r06_pmc_c4c5.json"
+
+
+def pmc_traffic(case, units):
+    """HBM-side bytes of `units` units of a c4 / c5 case from the committed rocprofv3 PMC passes
+    (tools/pmc_r06.sh, reduced by tools/pmc_r06.py: bytes per unit); None without a pass."""
+    d = load_pmc(os.path.basename(PMC_C4C5))
+    c = (d or {}).get("cases", {}).get(case)
+    if not c or c.get("bytes_per_unit") is None:
+        return None
+    return c["bytes_per_unit"] * units
+
+
 def load_pmc(name):
     p = os.path.join(REPO, "profiles", name)
     try:
@@ -568,7 +592,9 @@ def main():
     ap.add_argument("--phase", default="landing_burn_pure_throttle")
     ap.add_argument("--no-wind", action="store_true")
     ap.add_argument("--cpu-baseline", type=int, default=1)
-    ap.add_argument("--secondary", type=int, default=1, help="also time the other precision")
+    ap.add_argument("--secondary", type=int, default=0,
+                    help="also time the other precision (off by default: the binary32 handle is 1.2x binary64 on c3 "
+                         "and slower on c2, DESIGN.md s8)")
     ap.add_argument("--descent", type=int, default=1, help="c3: also measure c3-descent (nested in the line)")
     ap.add_argument("--workload", choices=["c2", "c3", "c3-descent", "c4", "c5"], default="c3",
                     help="c3: env-steps/s headline (uniform random actions); c3-descent: c3 with the 3:1 "
@@ -669,8 +695,12 @@ def main():
                 f"auto-reset, integrator {args.integrator}" +
                 (" (RK4 dt=0.01 s: NOT the reference's integrator, non-parity)" if args.integrator == "rk4"
                  else " (semi-implicit Euler 4 x 0.025 s)")}[args.workload]
+    metric = "env-steps/sec at 65 536 parallel envs; achieved HBM GB/s vs peak"    # BASELINE.json's (c3)
+    if args.workload == "c2":
+        metric = (f"env-steps/sec at {main_res['n']} parallel envs (c2, no wind" +
+                  (", RK4 dt=0.01 s: non-parity" if args.integrator == "rk4" else "") + "); achieved HBM GB/s vs peak")
     out = {
-        "metric": "env-steps/sec at 65 536 parallel envs; achieved HBM GB/s vs peak",
+        "metric": metric,
         "value": summ["value"],
         "unit": "env-steps/s",
         "n_gpus": world,
@@ -709,22 +739,29 @@ def main():
     # (before the CPU baseline: its host threads must not share the CPU with these launch-bound runs)
     if args.others and world == 1 and args.workload == "c3" and args.envs == 65536:
         out["other_workloads"] = other_workloads(args, local)
-    if args.cpu_baseline and world == 1 and args.workload in ("c3", "c3-descent"):
+    if args.cpu_baseline and world == 1 and args.workload == "c2" and args.integrator == "rk4":
+        out["cpu_baseline"] = None
+        out["cpu_baseline_note"] = ("the RK4 mode is not the reference's integrator and the oracle's threaded rollout "
+                                    "runs the reference integrator only: no CPU line for it")
+    elif args.cpu_baseline and world == 1 and args.workload in ("c2", "c3", "c3-descent"):
         sys.path.insert(0, os.path.join(REPO, "oracle"))
         import numpy as np
         import oracle
         # all host threads this job may use (the GPU box exports OMP_NUM_THREADS = its CPU share)
         thr = max(1, min(int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)), os.cpu_count() or 1, 64))
+        c2 = args.workload == "c2"
+        tilt = 0.0 if c2 else math.radians(1.0)
         ne, ns = 64 * thr, 600
         acts = np.random.default_rng(0).uniform(-1, 1, (ns, ne, 1)).astype(np.float32)
-        oracle.rollout(0, 0, 2, 2, acts[:2, :2], True, wind, math.radians(1.0))
+        oracle.rollout(0, 0, 2, 2, acts[:2, :2], True, wind, tilt)
         t0 = time.perf_counter()
-        _, nsteps = oracle.rollout(0, 0, ne, ns, acts, True, wind, math.radians(1.0), threads=thr)
+        _, nsteps = oracle.rollout(0, 0, ne, ns, acts, True, wind, tilt, threads=thr)
         dt = time.perf_counter() - t0
+        what = ("the c2 workload (no wind, no tilt, auto-reset, uniform random actions)" if c2 else
+                "the c3 workload (wind+tilt+auto-reset, uniform random actions)")
         out["cpu_baseline"] = {"value": nsteps / dt, "unit": "env-steps/s", "cores": thr, "kind": "port",
                                "sample": f"oracle/pd_oracle.c scalar port on {thr} host threads (static env "
-                                         f"partition), {ne} envs x {ns} steps of the c3 workload "
-                                         f"(wind+tilt+auto-reset, uniform random actions), {dt:.1f} s"}
+                                         f"partition), {ne} envs x {ns} steps of {what}, {dt:.1f} s"}
     print(json.dumps(out))
     if dist:
         dist.destroy_process_group()
