@@ -6,6 +6,14 @@
 #      step launches insert their own aero misses (no k_insert launch after each); the driver's
 #      command and the fixed cost against the round-5 library (libpdenv_r05.so), interleaved;
 #      the RCCL path of bench.py (torchrun, one rank, PD_BENCH_DIST=1: c3, c4, c5).
+#   2: the c4 / c5 traffic (tools/pmc_r06.sh: FETCH_SIZE, WRITE_SIZE, TCC hits of the policy and SAC
+#      step launches at 32 768 / 262 144 particles and 4 096 envs); then a PC-sampling trial of the
+#      c3 kernel (rocprofv3 --pc-sampling-beta-enabled, host_trap): where its issue slots go.
+#      (The pool refuses PC sampling: that step never ran.)
+#   3: non-temporal loads against L2 pollution, two interleaved rounds: the c4 actor weights
+#      (libpdenv_pnt.so, tools/experiments/policy_nt.patch; c4 at 32 768 and 262 144 particles) and
+#      the c3 fine-index word (libpdenv_fnt.so, fine_nt.patch; c3 and c3-descent); then the c2
+#      lines (reference integrator with its CPU baseline, RK4) and the c5 line.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -41,6 +49,30 @@ case "${PART:-1}" in
   rccl c3 --steps 32 --warmup 16 --cpu-baseline 0 --secondary 0 --descent 0 --fresh 0 --others 0
   rccl c5 --workload c5 --steps 32 --warmup 8 --cpu-baseline 0
   rccl c4 --workload c4 --steps 4 --warmup 2 --cpu-baseline 0
+  ;;
+2)
+  run pmc6 900 bash tools/pmc_r06.sh
+  run avail 120 rocprofv3 -L
+  FUSE=128 LAUNCHES=3 BURN=128 run pcs_c3 180 rocprofv3 --pc-sampling-beta-enabled 1 --pc-sampling-method host_trap \
+      --pc-sampling-unit time --pc-sampling-interval 10 --output-format csv -d gpurun_out/pcs_c3 -o run -- python3 tools/time_fused.py
+  ;;
+3)
+  for r in 1 2; do
+    for v in base pnt; do
+      lib=$PKG/libpdenv.so; [ $v != base ] && lib=$PKG/libpdenv_$v.so
+      PDENV_LIB=$lib run c4_${v}_r$r 300 python bench.py --workload c4 --steps 8 --warmup 2 --cpu-baseline 0
+      PDENV_LIB=$lib run c4big_${v}_r$r 300 python bench.py --workload c4 --particles 262144 --steps 4 --warmup 1 --cpu-baseline 0
+    done
+    for v in base fnt; do
+      lib=$PKG/libpdenv.so; [ $v != base ] && lib=$PKG/libpdenv_$v.so
+      for d in 0 1; do
+        PDENV_LIB=$lib DESCENT=$d BURN=640 FUSE=128 LAUNCHES=6 run t3_${v}_d${d}_r$r 200 python tools/time_fused.py
+      done
+    done
+  done
+  run c2 300 python bench.py --workload c2
+  run c2rk4 300 python bench.py --workload c2 --integrator rk4
+  run c5 300 python bench.py --workload c5
   ;;
 esac
 echo "=== done"
