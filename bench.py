@@ -233,7 +233,7 @@ def bench_sac(args, world, rank, local, dist):
         thr = max(1, min(int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)), os.cpu_count() or 1, 64))
         ps = [p.detach().float().cpu().numpy() for p in actor.parameters()]
         L_ = sum(1 for m in actor.shared_net if isinstance(m, torch.nn.Linear))
-        ne, ns = 16 * thr, 300
+        ne, ns = 64 * thr, 600          # (about 10 s of host work at 16 threads)
         t0 = time.perf_counter()
         _, nsteps = oracle.sac_collect(ne, ns, ps, H, L_, S, A, seed=1234, threads=thr)
         dt = time.perf_counter() - t0
@@ -349,9 +349,18 @@ def other_workloads(args, local):
 KERNEL_REPLAYS = 3      # replays of the timed launches for the kernel time (per-launch median)
 DESCENT_BURN_IN = 640   # c3-descent: untimed steps before the warmup (a steady mix of episode phases)
 # c3: untimed steps before the warmup, so that the timed window sees resets at their stationary
-# rate (every episode of the uniform-action law ends within ~200 steps); --c3-burn-in 0 gives the
-# fresh-episode window of rounds 1-3, which the line also reports as `c3_fresh`
+# rate; --c3-burn-in 0 gives the fresh-episode window of rounds 1-3, which the line also reports as
+# `c3_fresh`
 C3_BURN_IN = 640
+# Staggered starts: under the uniform-action law every episode lasts 131 +- 2.4 steps (oracle,
+# 1 024 envs x 3 000 steps), so envs that all start at step 0 keep resetting together for
+# thousands of steps -- a 20-step window lands on a reset wave (47 resets per 1 000 env-steps in
+# the driver's window) or between two (0), where the stationary rate is 7.6.  Before the burn-in,
+# env i is reset once more at prologue step i mod STAGGER (pd_reset with a mask, as
+# rocket_environment_pre_wrap.reset of that env), which spreads the episodes' phases over the
+# period as a training run's independent envs are; --stagger 0 gives the synchronized starts of
+# rounds 4-5, which the line also reports as `c3_sync`
+C3_STAGGER = 128
 
 
 def c3_actions(T, n, gen, device, descent):
@@ -393,8 +402,9 @@ def workload_counts(d, n, steps, lpe):
     return out
 
 
-def run_c3(args, precision, local, rank, dist, descent=False, launch_base=0, burn=None):
-    """One c3 (or c3-descent) measurement on this rank's handle, after `burn` untimed steps
+def run_c3(args, precision, local, rank, dist, descent=False, launch_base=0, burn=None, stagger=None):
+    """One c3 (or c3-descent) measurement on this rank's handle, after the staggered prologue
+    (`stagger` steps, default --stagger when there is a burn-in) and `burn` untimed steps
     (default: c3-descent's, or --c3-burn-in).  Returns the raw timings."""
     import torch
     import pdenv
@@ -408,10 +418,21 @@ def run_c3(args, precision, local, rank, dist, descent=False, launch_base=0, bur
     env.flush_every = 16
     if burn is None:
         burn = DESCENT_BURN_IN if descent else args.c3_burn_in
+    stagger = args.stagger if (stagger is None and burn > 0) else (stagger or 0)
     W = burn + args.warmup
     T = W + args.steps
     F = max(1, args.fuse)
     g = torch.Generator(device=env.device).manual_seed(42 + rank)
+    if stagger > 0:
+        # the staggered prologue (C3_STAGGER): one step of every env, then the envs of phase t
+        # reset, for t = 0 .. stagger - 1 (untimed; its own draws of the same action law)
+        ph = torch.arange(n, device=env.device) % stagger
+        pro = c3_actions(stagger, n, g, env.device, descent)
+        for t in range(stagger):
+            env.step_raw(pro[t].contiguous())
+            env.reset(mask=ph == t)
+        torch.cuda.synchronize()
+        del pro, ph
     acts = c3_actions(T, n, g, env.device, descent)
     launches = [0]
     if F > 1:
@@ -493,7 +514,7 @@ def run_c3(args, precision, local, rank, dist, descent=False, launch_base=0, bur
     d["rbf_misses"] = s1["rbf_misses"] - s0["rbf_misses"]     # solved in the timed region itself
     res = dict(wall=wall, dev_ms=dev_ms, kern_total_ms=sum(kern), kern_launches=len(kern), kern_replays=KERNEL_REPLAYS,
                kern_avg_full_ms=(sum(full) / len(full)) if full else None, fuse=F, n=n,
-               obs_dim=env.obs_dim, act_dim=env.action_dim, burn_in=burn,
+               obs_dim=env.obs_dim, act_dim=env.action_dim, burn_in=burn, stagger=stagger,
                # (lanes per env: pd_create's default, 2 above 8 192 envs)
                counts=workload_counts(d, n, args.steps, 2 if n > 8192 else 0),
                replay_misses=s2["rbf_misses"] - s1["rbf_misses"],
@@ -616,6 +637,11 @@ def main():
                     help="c5: replay the collection step as a HIP graph (off: each replay left an 8.6 us gap "
                          "between step kernels, eager launches none -- 0.0434 against 0.0392 ms per step, "
                          "profiles/r05_exp_c5_graph.jsonl)")
+    ap.add_argument("--stagger", type=int, default=C3_STAGGER,
+                    help="c3: staggered starts before the burn-in (env i reset at prologue step i mod STAGGER; "
+                         "0 = every env starts at step 0, the synchronized starts of rounds 4-5)")
+    ap.add_argument("--sync", type=int, default=1,
+                    help="c3: also measure the synchronized-starts window (--stagger 0), reported as c3_sync")
     ap.add_argument("--c3-burn-in", type=int, default=C3_BURN_IN,
                     help="c3: untimed env-steps before the warmup (steady state: resets at their stationary rate)")
     ap.add_argument("--fresh", type=int, default=1,
@@ -669,6 +695,10 @@ def main():
     if args.workload == "c3" and args.fresh and args.c3_burn_in > 0:
         fresh = run_c3(args, args.precision, local, rank, dist, launch_base=base, burn=0)
         base += fresh["launches_total"]
+    sync = None
+    if args.workload == "c3" and args.sync and args.stagger > 0 and args.c3_burn_in > 0:
+        sync = run_c3(args, args.precision, local, rank, dist, launch_base=base, stagger=0)
+        base += sync["launches_total"]
     other = None
     if args.secondary:
         other = run_c3(args, "f32" if args.precision == "f64" else "f64", local, rank, dist, descent=descent_main)
@@ -686,8 +716,8 @@ def main():
     summ = c3_summary(args, main_res, world, args.precision, pmc)
     wl = {"c3": "c3: 65536 envs/GPU, landing_burn_pure_throttle, rtd_rl reward, wind (percentile profile drawn "
                 "per reset + VK gusts below 15 km) + tilt, auto-reset, uniform random actions" +
-                (f"; timed at steady state after {args.c3_burn_in} untimed burn-in + {args.warmup} warmup steps"
-                 if args.c3_burn_in > 0 else "; timed on fresh episodes (no burn-in)"),
+                (f"; timed at steady state after {args.stagger} staggered-start + {args.c3_burn_in} untimed burn-in + "
+                 f"{args.warmup} warmup steps" if args.c3_burn_in > 0 else "; timed on fresh episodes (no burn-in)"),
           "c3-descent": f"c3-descent: the c3 configuration with the 3:1 high-throttle action mix, timed after "
                         f"{DESCENT_BURN_IN} burn-in + {args.warmup} warmup steps (episodes in every phase of the "
                         f"descent: gust band, landing logic)",
@@ -731,6 +761,15 @@ def main():
                            "launch_index": fs["launch_index"],
                            "workload": f"c3 on fresh episodes: no burn-in, {args.warmup} warmup steps, then "
                                        f"{args.steps} timed (every env's first episode, 30 km down)"}
+    if sync is not None:
+        ss = c3_summary(args, sync, world, args.precision)
+        out["c3_sync"] = {"value": ss["value"], "ms_per_step": ss["ms_per_step"],
+                          "kernel_ms_per_step": ss["roofline"]["kernel_ms_per_step"],
+                          "roofline_frac": ss["roofline"]["frac"], "workload_counts": ss["workload_counts"],
+                          "launch_index": ss["launch_index"],
+                          "workload": f"c3 with synchronized starts (no stagger; rounds 4-5): {args.c3_burn_in} burn-in + "
+                                      f"{args.warmup} warmup steps, then {args.steps} timed -- the window's position "
+                                      f"against the envs' common reset waves sets its reset count"}
     if other is not None:
         op = "f32" if args.precision == "f64" else "f64"
         out["secondary"] = {"dtype": op, "value": whole_job_rate(other["n"], world, args.steps, other["wall"]),

@@ -14,6 +14,16 @@
 #      (libpdenv_pnt.so, tools/experiments/policy_nt.patch; c4 at 32 768 and 262 144 particles) and
 #      the c3 fine-index word (libpdenv_fnt.so, fine_nt.patch; c3 and c3-descent); then the c2
 #      lines (reference integrator with its CPU baseline, RK4) and the c5 line.
+#   4: the c3 kernel's instruction stream by class: two rocprofv3 --pmc passes
+#      over tools/time_fused.py (F = 128, after the burn-in) for c3 and c3-descent -- VALU by type
+#      (INT32, INT64, CVT, F32 classes; F64 from the committed mix) and SALU / SMEM / LDS / VMEM /
+#      branch counts with the VALU lane utilisation (SQ_THREAD_CYCLES_VALU / SQ_ACTIVE_INST_VALU).
+#   5: what the c3 kernel's cold code costs its hot path: variants without the info tap (notap.patch,
+#      productisable as a no-tap instantiation), without the miss solve (nomiss) and without the
+#      neighbourhood verification (noverify; both wrong on the queries that need them, timing
+#      only): a PMC pass (VALU, SALU, cycles) and two interleaved timing rounds, c3 and c3-descent.
+#   6: staggered starts in the c3 windows (bench.py --stagger 128, the c3_sync sub-line the
+#      synchronized starts): the driver's command twice and the default line.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -73,6 +83,38 @@ case "${PART:-1}" in
   run c2 300 python bench.py --workload c2
   run c2rk4 300 python bench.py --workload c2 --integrator rk4
   run c5 300 python bench.py --workload c5
+  ;;
+4)
+  PA="SQ_INSTS_VALU SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_INSTS_VALU_CVT SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_TRANS_F32"
+  PB="SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_BRANCH SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU"
+  for d in 0 1; do
+    for pass in a b; do
+      cs=$PA; [ $pass = b ] && cs=$PB
+      DESCENT=$d BURN=640 FUSE=128 LAUNCHES=3 run pmc6mix_${pass}_d$d 120 rocprofv3 --pmc $cs --output-format csv \
+          -d gpurun_out/pmc6mix_${pass}_d$d -o run -- python3 tools/time_fused.py
+    done
+  done
+  ;;
+5)
+  for v in base notap nomiss noverify; do
+    lib=$PKG/libpdenv.so; [ $v != base ] && lib=$PKG/libpdenv_$v.so
+    PDENV_LIB=$lib DESCENT=0 BURN=640 FUSE=128 LAUNCHES=3 run pmc5v_$v 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU \
+        SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS --output-format csv \
+        -d gpurun_out/pmc5v_$v -o run -- python3 tools/time_fused.py
+  done
+  for r in 1 2; do
+    for v in base notap nomiss noverify; do
+      lib=$PKG/libpdenv.so; [ $v != base ] && lib=$PKG/libpdenv_$v.so
+      for d in 0 1; do
+        PDENV_LIB=$lib DESCENT=$d BURN=640 FUSE=128 LAUNCHES=6 run t5_${v}_d${d}_r$r 200 python tools/time_fused.py
+      done
+    done
+  done
+  ;;
+6)
+  run benchdrv6a 400 python bench.py --steps 20 --warmup 5
+  run benchdrv6b 400 python bench.py --steps 20 --warmup 5
+  run bench6 400 python bench.py
   ;;
 esac
 echo "=== done"
