@@ -352,15 +352,19 @@ DESCENT_BURN_IN = 640   # c3-descent: untimed steps before the warmup (a steady 
 # rate; --c3-burn-in 0 gives the fresh-episode window of rounds 1-3, which the line also reports as
 # `c3_fresh`
 C3_BURN_IN = 640
-# Staggered starts: under the uniform-action law every episode lasts 131 +- 2.4 steps (oracle,
-# 1 024 envs x 3 000 steps), so envs that all start at step 0 keep resetting together for
-# thousands of steps -- a 20-step window lands on a reset wave (47 resets per 1 000 env-steps in
-# the driver's window) or between two (0), where the stationary rate is 7.6.  Before the burn-in,
-# env i is reset once more at prologue step i mod STAGGER (pd_reset with a mask, as
-# rocket_environment_pre_wrap.reset of that env), which spreads the episodes' phases over the
-# period as a training run's independent envs are; --stagger 0 gives the synchronized starts of
-# rounds 4-5, which the line also reports as `c3_sync`
-C3_STAGGER = 128
+# Staggered starts (--stagger K, off by default): under the uniform-action law every episode lasts
+# 131 +- 2.4 steps (oracle, 1 024 envs x 3 000 steps), so envs that all start at step 0 keep
+# resetting together for thousands of steps -- a 20-step window lands on a reset wave (47 resets
+# per 1 000 env-steps in the driver's window) or between two (0; the stationary rate is 7.6).
+# With --stagger K env i is reset once more at prologue step i mod K before the burn-in (pd_reset
+# with a mask, rocket_environment_pre_wrap.reset of that env), which spreads the episodes' phases
+# over the period as a training run's independent envs are.  Measured (round 6): resets cost
+# little, but a wave's 32 envs then sit at 32 different phases of their descent and take more
+# divergent paths: c3 3 % slower than with the synchronized starts (profiles/r06_bench_stagger.jsonl).
+# The default keeps the synchronized starts (every env reset together, as pd_reset / the
+# reference's reset() leave a batch); the line reports the staggered window as `c3_staggered`.
+C3_STAGGER = 0
+C3_STAGGER_SUB = 128
 
 
 def c3_actions(T, n, gen, device, descent):
@@ -639,9 +643,10 @@ def main():
                          "profiles/r05_exp_c5_graph.jsonl)")
     ap.add_argument("--stagger", type=int, default=C3_STAGGER,
                     help="c3: staggered starts before the burn-in (env i reset at prologue step i mod STAGGER; "
-                         "0 = every env starts at step 0, the synchronized starts of rounds 4-5)")
-    ap.add_argument("--sync", type=int, default=1,
-                    help="c3: also measure the synchronized-starts window (--stagger 0), reported as c3_sync")
+                         "0 = every env starts at step 0, the synchronized starts, the default)")
+    ap.add_argument("--staggered", type=int, default=C3_STAGGER_SUB,
+                    help="c3: also measure the window with staggered starts (this K), reported as c3_staggered "
+                         "(0: not measured)")
     ap.add_argument("--c3-burn-in", type=int, default=C3_BURN_IN,
                     help="c3: untimed env-steps before the warmup (steady state: resets at their stationary rate)")
     ap.add_argument("--fresh", type=int, default=1,
@@ -695,10 +700,10 @@ def main():
     if args.workload == "c3" and args.fresh and args.c3_burn_in > 0:
         fresh = run_c3(args, args.precision, local, rank, dist, launch_base=base, burn=0)
         base += fresh["launches_total"]
-    sync = None
-    if args.workload == "c3" and args.sync and args.stagger > 0 and args.c3_burn_in > 0:
-        sync = run_c3(args, args.precision, local, rank, dist, launch_base=base, stagger=0)
-        base += sync["launches_total"]
+    stag = None
+    if args.workload == "c3" and args.staggered > 0 and args.stagger == 0 and args.c3_burn_in > 0:
+        stag = run_c3(args, args.precision, local, rank, dist, launch_base=base, stagger=args.staggered)
+        base += stag["launches_total"]
     other = None
     if args.secondary:
         other = run_c3(args, "f32" if args.precision == "f64" else "f64", local, rank, dist, descent=descent_main)
@@ -716,8 +721,9 @@ def main():
     summ = c3_summary(args, main_res, world, args.precision, pmc)
     wl = {"c3": "c3: 65536 envs/GPU, landing_burn_pure_throttle, rtd_rl reward, wind (percentile profile drawn "
                 "per reset + VK gusts below 15 km) + tilt, auto-reset, uniform random actions" +
-                (f"; timed at steady state after {args.stagger} staggered-start + {args.c3_burn_in} untimed burn-in + "
-                 f"{args.warmup} warmup steps" if args.c3_burn_in > 0 else "; timed on fresh episodes (no burn-in)"),
+                ((f"; timed after {args.stagger} staggered-start steps" if args.stagger > 0 else "; synchronized starts") +
+                 f", {args.c3_burn_in} untimed burn-in + {args.warmup} warmup steps" if args.c3_burn_in > 0
+                 else "; timed on fresh episodes (no burn-in)"),
           "c3-descent": f"c3-descent: the c3 configuration with the 3:1 high-throttle action mix, timed after "
                         f"{DESCENT_BURN_IN} burn-in + {args.warmup} warmup steps (episodes in every phase of the "
                         f"descent: gust band, landing logic)",
@@ -761,15 +767,16 @@ def main():
                            "launch_index": fs["launch_index"],
                            "workload": f"c3 on fresh episodes: no burn-in, {args.warmup} warmup steps, then "
                                        f"{args.steps} timed (every env's first episode, 30 km down)"}
-    if sync is not None:
-        ss = c3_summary(args, sync, world, args.precision)
-        out["c3_sync"] = {"value": ss["value"], "ms_per_step": ss["ms_per_step"],
-                          "kernel_ms_per_step": ss["roofline"]["kernel_ms_per_step"],
-                          "roofline_frac": ss["roofline"]["frac"], "workload_counts": ss["workload_counts"],
-                          "launch_index": ss["launch_index"],
-                          "workload": f"c3 with synchronized starts (no stagger; rounds 4-5): {args.c3_burn_in} burn-in + "
-                                      f"{args.warmup} warmup steps, then {args.steps} timed -- the window's position "
-                                      f"against the envs' common reset waves sets its reset count"}
+    if stag is not None:
+        ss = c3_summary(args, stag, world, args.precision)
+        out["c3_staggered"] = {"value": ss["value"], "ms_per_step": ss["ms_per_step"],
+                               "kernel_ms_per_step": ss["roofline"]["kernel_ms_per_step"],
+                               "roofline_frac": ss["roofline"]["frac"], "workload_counts": ss["workload_counts"],
+                               "launch_index": ss["launch_index"],
+                               "workload": f"c3 with staggered starts: env i reset once more at prologue step i mod "
+                                           f"{args.staggered}, then {args.c3_burn_in} burn-in + {args.warmup} warmup steps, "
+                                           f"then {args.steps} timed (resets at their stationary rate; each wave's envs at "
+                                           f"different phases of their episodes)"}
     if other is not None:
         op = "f32" if args.precision == "f64" else "f64"
         out["secondary"] = {"dtype": op, "value": whole_job_rate(other["n"], world, args.steps, other["wall"]),
