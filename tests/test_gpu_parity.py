@@ -160,6 +160,34 @@ def test_device_solve_bit_identical(pd, precision, lpe):
     assert full.counters()["rbf_misses"] < cut.counters()["rbf_misses"]
 
 
+def test_step_launch_inserts_its_misses(pd):
+    """The misses a step launch solves are inserted by the launch's last workgroup (k_step's tail:
+    a ticket per workgroup), with no k_insert launch or pd_flush_misses call after pd_step_n: with
+    the tables cut to 4 keys, launches of 10 fused steps grow the tables launch by launch, the later
+    launches solve fewer misses than the first (the inserted neighbourhoods are found), and the
+    trajectory equals the full-table handle's bit for bit."""
+    import torch
+    N, T, F = 2048, 40, 10
+    g = torch.Generator(device="cuda").manual_seed(12)
+    A = (torch.rand(T, N, 1, device="cuda", generator=g) * 2 - 1).contiguous()
+    kw = dict(lanes_per_env=2, enable_wind=True, stochastic_wind=True, wind_percentile=None, auto_reset=True,
+              tilt_sigma_rad=0.02, seed=9, table_flags=L.TABLES_NO_CELL_PIECES)
+    full = make(pd, N, **kw)
+    cut = make(pd, N, params=pd.Params().restrict_keys(4, 4), **kw)
+    misses, entries = [], []
+    for c in range(T // F):
+        c0 = cut.counters()
+        for env in (full, cut):
+            env.set_tuning(step_fuse=F)
+            env.step_n_raw(A[c * F:(c + 1) * F])
+        c1 = cut.counters()
+        misses.append(c1["rbf_misses"] - c0["rbf_misses"])
+        entries.append(c1["table_entries_cd"] + c1["table_entries_cl"])
+    assert misses[0] > 100 and misses[-1] < misses[0], misses
+    assert entries[0] > 8 and all(b >= a for a, b in zip(entries, entries[1:])), entries
+    assert torch.equal(full.state, cut.state)
+
+
 def test_cell_pieces_match_payload_sums(pd):
     """Binary64 handles evaluate trusted interior queries from cell pieces: the
     same first steps with the pieces (default) and with the payload sums only

@@ -24,6 +24,11 @@
 #      only): a PMC pass (VALU, SALU, cycles) and two interleaved timing rounds, c3 and c3-descent.
 #   6: staggered starts in the c3 windows (bench.py --stagger 128, the c3_sync sub-line the
 #      synchronized starts): the driver's command twice and the default line.
+#   7: the final build, part 1: the GPU suite (the two-rank test included), the smoke, the bench
+#      lines (default, the driver's command, c4 at 32 768 and 262 144 particles, c5, c2, c2 RK4)
+#      and a two-rank gloo rehearsal of the c3 line with both ranks on the one GPU.
+#   8: the final build, part 2: rocprofv3 kernel traces (default, driver command, c4, c5) and the
+#      c3 / c3-descent PMC passes (tools/pmc_r03b.sh); tools/collect_r03.py r06 reduces both.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -115,6 +120,23 @@ case "${PART:-1}" in
   run benchdrv6a 400 python bench.py --steps 20 --warmup 5
   run benchdrv6b 400 python bench.py --steps 20 --warmup 5
   run bench6 400 python bench.py
+  ;;
+7)
+  run gpu_tests 1200 python -u -m pytest tests/ -m gpu -x -q --timeout 600 --timeout-method thread
+  run smoke 200 python -c "import __graft_entry__ as g; g.smoke()"
+  run bench 400 python bench.py
+  run benchdrv 400 python bench.py --steps 20 --warmup 5
+  run c4 300 python bench.py --workload c4
+  run c4_262k 300 python bench.py --workload c4 --particles 262144 --steps 8 --warmup 2
+  run c5 300 python bench.py --workload c5
+  run c2 300 python bench.py --workload c2
+  run c2rk4 300 python bench.py --workload c2 --integrator rk4
+  PD_BENCH_BACKEND=gloo run gloo2 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+      --master-addr 127.0.0.1 --master-port 29519 bench.py --gpus 2 --steps 32 --warmup 8 --descent 0 --fresh 0 --staggered 0
+  ;;
+8)
+  STAGES="prof profdrv profc4 profc5" run profs 900 bash tools/gpu_session.sh
+  run pmc 600 bash tools/pmc_r03b.sh
   ;;
 esac
 echo "=== done"
