@@ -147,7 +147,6 @@ def bench_sac(args, world, rank, local, dist):
     env = pdenv.PoweredDescentEnv(n, flight_phase="landing_burn_pure_throttle", mode="rl",
                                   precision=args.precision, device=local, auto_reset=True, seed=1234,
                                   env_offset=shard_offset(rank, n))
-    env.flush_every = 16
     torch.manual_seed(0)
     actor = Actor(2, 1).to(env.device)
     # the driver's buffer: PrioritizedReplayBuffer, 1e6 transitions (sac_pytorch_powered_descent.py:62-70)
@@ -213,8 +212,8 @@ def bench_sac(args, world, rank, local, dist):
                                        "per launch of n env-steps)",
                      "bytes_per_env_step": round(bpe, 1), "kernel": "k_step<SAC> (pd_step_sac_fused: actor MLP + step)",
                      "kernel_avg_ms": kern_avg, "kernel_launches": args.steps if args.graph != 1 else len(kern_in),
-                     "kernel_timing": ("the timed region's HIP event pair per step (back-to-back launches, the miss "
-                                       "flushes included)" if args.graph != 1 else
+                     "kernel_timing": ("the timed region's HIP event pair per step (back-to-back launches)"
+                                       if args.graph != 1 else
                                        "HIP events around each replayed step (pairs beyond 1.5x the median, host "
                                        "stalls, left out)"),
                      "event_pairs": {"avg_ms": pairs_avg, "med_ms": kern_med, "pairs": len(kern_in),
@@ -419,7 +418,6 @@ def run_c3(args, precision, local, rank, dist, descent=False, launch_base=0, bur
         enable_wind=not args.no_wind, stochastic_wind=not args.no_wind, wind_percentile=None,
         auto_reset=True, tilt_sigma_rad=0.0 if args.workload == "c2" else math.radians(1.0), seed=1234,
         env_offset=shard_offset(rank, n), integrator=args.integrator)
-    env.flush_every = 16
     if burn is None:
         burn = DESCENT_BURN_IN if descent else args.c3_burn_in
     stagger = args.stagger if (stagger is None and burn > 0) else (stagger or 0)

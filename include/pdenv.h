@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define PD_ABI_VERSION 9   /* 4: pd_config.integrator (was padding); 5: pd_count_work, pd_step_sac; 6: cell pieces (pd_cell_piece_info, stats word 44); 7: pd_step_sac_ring, pd_sac_actor, stats word 45; 8: pd_step_sac_fused, pd_atm_table; 9: pd_config.table_flags, pd_tuning, caller scratch for pd_pso_swarm_minima, state/action dims of pd_step_sac_fused */
+#define PD_ABI_VERSION 10  /* 4: pd_config.integrator (was padding); 5: pd_count_work, pd_step_sac; 6: cell pieces (pd_cell_piece_info, stats word 44); 7: pd_step_sac_ring, pd_sac_actor, stats word 45; 8: pd_step_sac_fused, pd_atm_table; 9: pd_config.table_flags, pd_tuning, caller scratch for pd_pso_swarm_minima, state/action dims of pd_step_sac_fused; 10: step launches insert their own solved misses (pd_flush_misses optional), explicit list settings turn the auto refill off */
 #define PD_MAX_PTS 256      /* aero scatter points per table */
 #define PD_MAX_COLS 5       /* AoA columns per aero table */
 #define PD_MAX_TAB 64       /* grid-fin table length */
@@ -375,9 +375,11 @@ pd_status pd_pso_swarm_minima(int64_t n_particles, int32_t dim, int32_t n_swarms
 pd_status pd_pso_update_bests(int32_t n_swarms, int32_t dim, const double* min_fitness, const double* min_position,
                               double* swarm_best_fitness, double* swarm_best, double* global_best_fitness,
                               double* global_best, void* stream);
-/* Insert the aero neighbourhoods solved on device since the last flush into the handle's
- * tables (one tiny kernel; a no-op when nothing missed).  Call every few steps: a missed
- * neighbourhood is solved exactly on every lookup until it is flushed. */
+/* Insert the aero neighbourhoods solved on device and still queued into the handle's tables
+ * (one tiny kernel; a no-op when nothing is queued).  Since ABI 10 every step launch (pd_step,
+ * pd_step_n, pd_step_sac*, pd_rollout) inserts the neighbourhoods it solved itself, by its last
+ * workgroup, and pd_rollout_policy flushes its own: a caller never needs this call any more.
+ * It stays for callers written against ABI <= 9 (their periodic flush finds the queue empty). */
 pd_status pd_flush_misses(pd_env* env, void* stream);
 /* Current observation (post-reset) [N][O]. */
 pd_status pd_observe(pd_env* env, void* obs, void* stream);

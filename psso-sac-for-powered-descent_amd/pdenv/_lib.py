@@ -100,7 +100,7 @@ EXPORTS = ["pd_abi_version", "pd_sizeof_params", "pd_sizeof_config", "pd_last_er
            "pd_action_dim", "pd_step_sac", "pd_pso_swarm_minima", "pd_pso_update_bests", "pd_cell_piece_info",
            "pd_step_sac_ring", "pd_sac_actor", "pd_step_sac_fused", "pd_atm_table", "pd_set_tuning", "pd_get_tuning",
            "pd_pso_swarm_minima_scratch_bytes", "pd_step_n_info"]
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 _lib = None
 

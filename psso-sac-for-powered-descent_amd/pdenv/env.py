@@ -103,7 +103,9 @@ class PoweredDescentEnv:
         self._trunc = torch.empty(self.n, dtype=torch.uint8, **kw)
         self._tid = torch.empty(self.n, dtype=torch.int8, **kw)
         self._steps = 0
-        self.flush_every = 1
+        # pd_flush_misses every flush_every steps (0: never -- since ABI 10 every step launch inserts
+        # the neighbourhoods it solved itself; the call is kept for ABI <= 9 habits)
+        self.flush_every = 0
 
     # ------------------------------------------------------------------ reference surface
     def reset(self, mask=None):
@@ -129,7 +131,7 @@ class PoweredDescentEnv:
         L.check(self.lib.pd_step(self.h, _ptr(a), _ptr(self._obs), _ptr(self._rew), _ptr(self._done),
                                  _ptr(self._trunc), _ptr(self._tid), _ptr(nz), _ptr(inf), _stream(self.device)))
         self._steps += 1
-        if self._steps % self.flush_every == 0:
+        if self.flush_every and self._steps % self.flush_every == 0:
             self.flush()
         extras = {"trunc_id": self._tid.clone()}
         if info:
@@ -149,11 +151,11 @@ class PoweredDescentEnv:
                                  _ptr(self._done), _ptr(self._trunc), _ptr(self._tid), None, None,
                                  _stream(self.device)))
         self._steps += 1
-        if self._steps % self.flush_every == 0:
+        if self.flush_every and self._steps % self.flush_every == 0:
             self.flush()
 
     def step_raw_noflush(self, actions):
-        """step_raw without the periodic aero-miss flush (graph capture: the caller flushes)."""
+        """step_raw without any pd_flush_misses call (graph capture)."""
         L.check(self.lib.pd_step(self.h, C.c_void_p(actions.data_ptr()), _ptr(self._obs), _ptr(self._rew),
                                  _ptr(self._done), _ptr(self._trunc), _ptr(self._tid), None, None,
                                  _stream(self.device)))
@@ -277,7 +279,7 @@ class PoweredDescentEnv:
 
     def step_n(self, actions, outputs=True, info_keys=None):
         """T consecutive env-steps over device-resident actions [T, N, A] (pd_step_n: fused
-        launches of up to 128 steps each, then the miss flush), the same results as T step()
+        launches of up to 128 steps each, each inserting its solved misses), the same results as T step()
         calls.  Landing-burn phases only.  outputs=True returns per-step
         (obs [T, N, O], reward [T, N], done [T, N], truncated [T, N], trunc_id [T, N]);
         outputs=False writes nothing per step and returns None.  info_keys: names of
@@ -333,7 +335,8 @@ class PoweredDescentEnv:
         self._steps += int(actions.shape[0])
 
     def flush(self):
-        """Insert device-solved aero neighbourhoods into the tables (pd_flush_misses)."""
+        """Insert queued device-solved aero neighbourhoods into the tables (pd_flush_misses; since
+        ABI 10 the step launches insert their own, so the queue is normally empty)."""
         L.check(self.lib.pd_flush_misses(self.h, _stream(self.device)))
 
     def observe(self):

@@ -261,12 +261,13 @@ class SACCollector:
     replays append in order).  Off by default: on ROCm 7 each replay of the one-kernel graph left
     an 8.6 us gap before its step kernel, where eager launches from a host that keeps ahead of
     the GPU run back to back (c5: 0.0434 against 0.0392 ms per step, profiles/r05_exp_c5_graph.jsonl).  The gather runs eagerly after
-    each replay; the aero-miss flush every flush_every steps.
+    each replay.  flush_every > 0: a pd_flush_misses call every that many steps (0, the default:
+    none -- the step launch inserts the neighbourhoods it solved itself, ABI 10).
     step() returns the step's transition rows: a view of the replay ring's rows (valid until the
     ring wraps onto them) in ring mode, else a fresh tensor."""
 
     def __init__(self, env, actor, buffer=None, dist=None, learner_rank=0, generator=None,
-                 deterministic=False, use_graph=False, flush_every=16, fused=True):
+                 deterministic=False, use_graph=False, flush_every=0, fused=True):
         self.env, self.actor, self.buffer, self.dist = env, actor, buffer, dist
         self.learner_rank, self.generator, self.deterministic = learner_rank, generator, deterministic
         self.rank = dist.get_rank() if dist is not None and dist.is_initialized() else 0
@@ -331,7 +332,7 @@ class SACCollector:
 
     def _finish(self, slab):
         self.steps += 1
-        if self.steps % self.flush_every == 0:
+        if self.flush_every and self.steps % self.flush_every == 0:
             self.env.flush()
         if slab is None:                                       # ring mode: the rows are in place
             start = self.buffer.position

@@ -29,7 +29,7 @@ def test_struct_layout_and_abi():
     import pdenv
     from pdenv import _lib
     L = pdenv.load()
-    assert L.pd_abi_version() == _lib.ABI_VERSION == 9
+    assert L.pd_abi_version() == _lib.ABI_VERSION == 10
     assert L.pd_sizeof_params() == C.sizeof(_lib.PdParams)
     assert L.pd_sizeof_config() == C.sizeof(_lib.PdConfig)
 

@@ -135,6 +135,7 @@ case "${PART:-1}" in
       --master-addr 127.0.0.1 --master-port 29519 bench.py --gpus 2 --steps 32 --warmup 8 --descent 0 --fresh 0 --staggered 0
   ;;
 8)
+  run gpu_ins 300 python -u -m pytest tests/test_gpu_parity.py -x -v --timeout 200 --timeout-method thread -k "inserts_its_misses or device_solve"
   STAGES="prof profdrv profc4 profc5" run profs 900 bash tools/gpu_session.sh
   run pmc 600 bash tools/pmc_r03b.sh
   ;;
