@@ -524,7 +524,7 @@ def run_c3(args, precision, local, rank, dist, descent=False, launch_base=0, bur
                              "timed": [first_timed, first_timed + len(tb)],
                              "replay": [first_replay, first_replay + KERNEL_REPLAYS * len(tb)],
                              "replays": KERNEL_REPLAYS},
-               nan_events=s3["nan_events"])
+               nan_events=s3["nan_events"], descent=descent)
     res["launches_total"] = launches[0]   # (every launch of this handle: the replays included)
     env.close()
     return res
@@ -577,6 +577,14 @@ def c3_summary(args, r, world, precision, pmc=None):
         # over exactly the timed launches' env-steps and kernel time (a short timed region may be
         # one partial launch)
         out["valu_roofline"] = valu_roofline(mix, K, r["kern_total_ms"])
+        cm = load_pmc("r06_pmc_c3_mix.json")
+        case = (cm or {}).get("cases", {}).get("c3_descent" if r.get("descent") else "c3")
+        if case and precision == "f64":
+            # rocprof's VALUUtilization: the share of a VALU instruction's 64 lanes
+            # active, SQ_THREAD_CYCLES_VALU / (64 SQ_ACTIVE_INST_VALU), and the VALU stream by type
+            out["valu_roofline"]["lane_utilisation"] = case["valu_lane_utilisation"]
+            out["valu_roofline"]["valu_shares"] = case["valu_shares"]
+            out["valu_roofline"]["class_source"] = "profiles/r06_pmc_c3_mix.json (rocprofv3 --pmc, the same workload)"
     oc = load_pmc("opcount.json")
     if oc and precision == "f64" and args.phase == "landing_burn_pure_throttle" and not args.no_wind \
             and "q_taylor_frac" in r["counts"]:

@@ -29,6 +29,9 @@
 #      and a two-rank gloo rehearsal of the c3 line with both ranks on the one GPU.
 #   8: the final build, part 2: rocprofv3 kernel traces (default, driver command, c4, c5) and the
 #      c3 / c3-descent PMC passes (tools/pmc_r03b.sh); tools/collect_r03.py r06 reduces both.
+#   9: the c3 unit under other compiler flags (tools/variants.py: loop strength reduction off,
+#      -O2, both, no vectorizers; a static sweep of the ISA picked them: 1 % fewer VALU
+#      instructions and up to 7 fewer VGPRs): a PMC pass each and two interleaved timing rounds.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -138,6 +141,22 @@ case "${PART:-1}" in
   run gpu_ins 300 python -u -m pytest tests/test_gpu_parity.py -x -v --timeout 200 --timeout-method thread -k "inserts_its_misses or device_solve"
   STAGES="prof profdrv profc4 profc5" run profs 900 bash tools/gpu_session.sh
   run pmc 600 bash tools/pmc_r03b.sh
+  ;;
+9)
+  for v in base nolsr nolsro2 o2 novec; do
+    lib=$PKG/libpdenv.so; [ $v != base ] && lib=$PKG/libpdenv_$v.so
+    PDENV_LIB=$lib DESCENT=0 BURN=640 FUSE=128 LAUNCHES=3 run pmc9_$v 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU \
+        SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS --output-format csv \
+        -d gpurun_out/pmc9_$v -o run -- python3 tools/time_fused.py
+  done
+  for r in 1 2; do
+    for v in base nolsr nolsro2 o2 novec; do
+      lib=$PKG/libpdenv.so; [ $v != base ] && lib=$PKG/libpdenv_$v.so
+      for d in 0 1; do
+        PDENV_LIB=$lib DESCENT=$d BURN=640 FUSE=128 LAUNCHES=6 run t9_${v}_d${d}_r$r 200 python tools/time_fused.py
+      done
+    done
+  done
   ;;
 esac
 echo "=== done"
