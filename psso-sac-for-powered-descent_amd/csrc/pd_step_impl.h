@@ -892,27 +892,34 @@ template <typename R> __device__ __forceinline__ R cl_query(R ae, R& sgn, bool& 
 template <int IN, int NL, int OUT, bool SPLIT = false>
 __device__ __forceinline__ void actor_forward(const float* __restrict__ W, int64_t N, uint32_t ui,
                                               int half, const float* x, float* y) {
+    // W: the parameters in chunks of four, [ceil(P / 4)][N][4] (pdenv.hip k_wchunk): chunk c of
+    // env ui holds parameters 4c .. 4c + 3 of its particle, 16 bytes, so one 16-byte load per lane
+    // (512 contiguous bytes per wave) brings four parameters -- a quarter of the load instructions
+    // of the parameter-major [P][N] layout, the same bytes.  Every block a lane reads starts at a
+    // multiple of four parameters (the hidden rows are 8 long, the layer-1 blocks 4 IN, the biases
+    // start at multiples of 4); the sums run in the same order as before: the same bits.
     constexpr int H = 8;
     constexpr int HS = SPLIT ? H / 2 : H;                          // hidden units per lane
     constexpr bool OSPLIT = SPLIT && OUT % 2 == 0;
     constexpr int OS = OSPLIT ? OUT / 2 : OUT;                     // outputs per lane
+    static_assert((HS * IN) % 4 == 0 && (H * IN) % 4 == 0, "layer-1 blocks of whole chunks");
+    using F4 = __attribute__((ext_vector_type(4))) float;
     float h[H], g[H];
-    uint32_t sv = (uint32_t)N * 4u;
-    uint32_t o0 = ui * 4u;
+    uint32_t sv = (uint32_t)N * 16u;                               // one chunk row
+    uint32_t o0 = ui * 16u;
     uint32_t hv = SPLIT ? (uint32_t)half : 0u;
     asm volatile("" : "+v"(sv), "+v"(o0), "+v"(hv));
-    uint32_t off = o0;
-    // the lane's running offset set to parameter p (+ its half's rows: `rows` parameters each)
-    auto seek = [&](int p, int rows) {
-        off = o0 + (uint32_t)p * sv;
-        if constexpr (SPLIT) off += hv * ((uint32_t)rows * sv);
+    // n parameters from parameter p (a multiple of 4) + this lane's half (`rows` parameters)
+    auto load = [&](float* dst, int p, int rows, int n) {
+        uint32_t off = o0 + (uint32_t)(p >> 2) * sv;
+        if constexpr (SPLIT) off += hv * ((uint32_t)(rows >> 2) * sv);
         asm volatile("" : "+v"(off));
-    };
-    auto next = [&]() {
-        const float v = *(const PD_AS1 float*)((const PD_AS1 char*)(uint64_t)W + off);
-        off += sv;
-        asm volatile("" : "+v"(off));
-        return v;
+#pragma unroll
+        for (int c = 0; c < (n + 3) / 4; ++c) {
+            const F4 v = *(const PD_AS1 F4*)((const PD_AS1 char*)(uint64_t)W + off + (uint32_t)c * sv);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) if (4 * c + k < n) dst[4 * c + k] = v[k];
+        }
     };
     // both halves of a split layer on both lanes: own[j] is unit hs * HS + j of this lane's half
     auto gather = [&](const float* own, float* full, int n) {
@@ -931,19 +938,22 @@ __device__ __forceinline__ void actor_forward(const float* __restrict__ W, int64
     int p = 0;
     float hs[HS];
     // layer 1: Linear(IN, 8)
-    seek(p, HS * IN);
+    {
+        float w[HS * IN], b[HS];
+        load(w, p, HS * IN, HS * IN);
+        load(b, p + H * IN, HS, HS);
 #pragma unroll
-    for (int j = 0; j < HS; ++j) {
-        float acc = 0.f;
+        for (int j = 0; j < HS; ++j) {
+            float acc = 0.f;
 #pragma unroll
-        for (int k = 0; k < IN; ++k) acc = acc + next() * x[k];
-        g[j] = acc;
-    }
-    seek(p + H * IN, HS);
+            for (int k = 0; k < IN; ++k) acc = acc + w[j * IN + k] * x[k];
+            g[j] = acc;
+        }
 #pragma unroll
-    for (int j = 0; j < HS; ++j) {
-        const float acc = g[j] + next();
-        hs[j] = acc < 0.f ? 0.f : acc;
+        for (int j = 0; j < HS; ++j) {
+            const float acc = g[j] + b[j];
+            hs[j] = acc < 0.f ? 0.f : acc;
+        }
     }
     p += H * IN + H;
     if constexpr (SPLIT) gather(hs, h, HS);
@@ -953,18 +963,20 @@ __device__ __forceinline__ void actor_forward(const float* __restrict__ W, int64
     }
 #pragma unroll
     for (int l = 0; l < NL; ++l) {
-        seek(p, HS * H);
 #pragma unroll
         for (int j = 0; j < HS; ++j) {
+            float w[H];
+            load(w, p + j * H, HS * H, H);
             float acc = 0.f;
 #pragma unroll
-            for (int k = 0; k < H; ++k) acc = acc + next() * h[k];
+            for (int k = 0; k < H; ++k) acc = acc + w[k] * h[k];
             g[j] = acc;
         }
-        seek(p + H * H, HS);
+        float b[HS];
+        load(b, p + H * H, HS, HS);
 #pragma unroll
         for (int j = 0; j < HS; ++j) {
-            const float acc = g[j] + next();
+            const float acc = g[j] + b[j];
             hs[j] = acc < 0.f ? 0.f : acc;
         }
         p += H * H + H;
@@ -975,17 +987,24 @@ __device__ __forceinline__ void actor_forward(const float* __restrict__ W, int64
         }
     }
     float o[OS], ys[OS];
-    seek(p, OSPLIT ? OS * H : 0);
 #pragma unroll
     for (int j = 0; j < OS; ++j) {
+        float w[H];
+        load(w, p + j * H, OSPLIT ? OS * H : 0, H);
         float acc = 0.f;
 #pragma unroll
-        for (int k = 0; k < H; ++k) acc = acc + next() * h[k];
+        for (int k = 0; k < H; ++k) acc = acc + w[k] * h[k];
         o[j] = acc;
     }
-    seek(p + OUT * H, OSPLIT ? OS : 0);
+    // the output biases: parameters p + OUT H + hv OS .. (+ OS), inside one chunk (OUT <= 4)
+    {
+        const int pb = p + OUT * H;
+        float bb[4];
+        load(bb, pb, 0, 4);
+        const int sh = OSPLIT ? (int)hv * OS : 0;
 #pragma unroll
-    for (int j = 0; j < OS; ++j) ys[j] = (float)tanh((double)(o[j] + next()));
+        for (int j = 0; j < OS; ++j) ys[j] = (float)tanh((double)(o[j] + (sh ? bb[OS + j] : bb[j])));
+    }
     if constexpr (OSPLIT) gather(ys, y, OS);
     else {
 #pragma unroll
@@ -1286,12 +1305,14 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(2)))
     const bool wcopy = POL && a.use_list && a.policy_wc != nullptr;
     if constexpr (POL) {
         if (wcopy) {
-            constexpr int kP = PHASE == 0 ? PD_ACTOR_PARAMS_PURE_THROTTLE : PD_ACTOR_PARAMS_LANDING_BURN;
+            // (the chunked layout of actor_forward: ceil(P / 4) rows of 16-byte chunks)
+            constexpr int kC = ((PHASE == 0 ? PD_ACTOR_PARAMS_PURE_THROTTLE : PD_ACTOR_PARAMS_LANDING_BURN) + 3) / 4;
+            using F4 = __attribute__((ext_vector_type(4))) float;
             uint32_t src = ui, dst = (uint32_t)e_act;
             asm volatile("" : "+v"(src), "+v"(dst));
 #pragma unroll 8
-            for (int q = 0; q < kP; ++q)
-                ev(a.policy_wc + (size_t)q * (size_t)N, dst) = ldv(a.policy_w + (size_t)q * (size_t)N, src);
+            for (int q = 0; q < kC; ++q)
+                ev((F4*)a.policy_wc + (size_t)q * (size_t)N, dst) = ldv((const F4*)a.policy_w + (size_t)q * (size_t)N, src);
         }
     }
     const int nf = a.n_fused;   // policy rollouts: finished envs freeze, stored at their last step

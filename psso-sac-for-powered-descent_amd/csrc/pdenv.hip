@@ -1279,6 +1279,7 @@ struct pd_env {
     int obs_kind = 0;   // obs_write layout of the handle's observation
     int count_work = 0; // workload counters on (pd_count_work)
     float* sac_heads = nullptr;   // pd_step_sac_fused's two-launch path: the actor heads [N][2A]
+    float* pol_w4 = nullptr;      // policy rollouts: the actor parameters in chunks of four ([P/4][N][4])
     float* pol_wc = nullptr;      // policy rollouts' list launches: the live envs' actor parameters
     pd_tuning tune{128, 64, 2, -1, 0.0, -1, 0, -1, 0};   // launch tuning (pd_set_tuning)
 };
@@ -1776,6 +1777,22 @@ pd_status step_impl(pd_env* e, const void* actions, void* obs, void* reward, uin
     return PD_OK;
 }
 
+// policy rollouts: the caller's parameter-major weights [P][N] in chunks of four parameters,
+// [ceil(P / 4)][N][4] (zeros past P), the layout actor_forward reads with one 16-byte load per
+// chunk (pd_step_impl.h)
+__global__ __launch_bounds__(kBlock) void k_wchunk(const float* __restrict__ w, float4* __restrict__ out, int P,
+                                                   int64_t N) {
+    const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const int64_t C = (P + 3) / 4;
+    if (t >= C * N) return;
+    const int c = (int)(t / N);
+    const int64_t i = t - (int64_t)c * N;
+    float v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = 4 * c + k < P ? w[(int64_t)(4 * c + k) * N + i] : 0.f;
+    out[t] = make_float4(v[0], v[1], v[2], v[3]);
+}
+
 // policy rollouts: every env live, in index order
 __global__ __launch_bounds__(kBlock) void k_live_init(int32_t* list, uint32_t* cnt, int64_t n) {
     int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -1791,8 +1808,20 @@ pd_status rollout_policy_impl(pd_env* e, const float* w, int32_t max_steps, void
     hipLaunchKernelGGL(k_reset<R>, dim3(grid), dim3(kBlock), 0, s, make_args<R>(e), (const uint8_t*)nullptr);
     PD_HIP(hipMemsetAsync(fitness, 0, (size_t)N * sizeof(R), s));
     hipLaunchKernelGGL(k_live_init, dim3(grid), dim3(kBlock), 0, s, e->live[0], e->live_cnt, N);
+    // the weights in the chunked layout of the step kernel's actor (one pass over them: 2 x 1.5 KB
+    // per particle, against the 1.5 KB per policy step the rollout reads)
+    const int P = e->cfg.phase == PD_PHASE_PURE_THROTTLE ? PD_ACTOR_PARAMS_PURE_THROTTLE : PD_ACTOR_PARAMS_LANDING_BURN;
+    if (!e->pol_w4) {
+        PD_HIP(hipMalloc((void**)&e->pol_w4, (size_t)PD_ACTOR_PARAMS_LANDING_BURN * (size_t)N * sizeof(float)));
+        e->allocs.push_back(e->pol_w4);
+    }
+    {
+        const int64_t tot = (int64_t)((P + 3) / 4) * N;
+        hipLaunchKernelGGL(k_wchunk, dim3((unsigned)((tot + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, w,
+                           (float4*)e->pol_w4, P, N);
+    }
     StepArgs<R> a = make_args<R>(e);
-    a.policy_w = w; a.reward_sum = (R*)fitness; a.auto_reset = 0;
+    a.policy_w = e->pol_w4; a.reward_sum = (R*)fitness; a.auto_reset = 0;
     const bool wind = e->cfg.enable_wind != 0;
     // launch t steps live[t & 1][0, live_cnt[t % 3]) and appends the survivors to the other list;
     // the grid covers the live count last read back (a workgroup past the device count leaves
@@ -1866,7 +1895,7 @@ pd_status rollout_policy_impl(pd_env* e, const float* w, int32_t max_steps, void
     // at any launch: once the live count read back falls to policy_list_at x N (default off), the
     // waves of the later launches hold live envs only
     const double compact_at = e->tune.policy_list_at;
-    // the list launches' parameter copy (policy_wc): [P][N] floats, made at the first rollout
+    // the list launches' parameter copy (policy_wc, chunked as pol_w4): made at the first rollout
     if (!e->pol_wc) {
         PD_HIP(hipMalloc((void**)&e->pol_wc, (size_t)PD_ACTOR_PARAMS_LANDING_BURN * (size_t)N * sizeof(float)));
         e->allocs.push_back(e->pol_wc);

@@ -32,6 +32,10 @@
 #   9: the c3 unit under other compiler flags (tools/variants.py: loop strength reduction off,
 #      -O2, both, no vectorizers; a static sweep of the ISA picked them: 1 % fewer VALU
 #      instructions and up to 7 fewer VGPRs): a PMC pass each and two interleaved timing rounds.
+#  10: the policy actor's weights in chunks of four parameters (one 16-byte load per lane for four
+#      parameters; k_wchunk before each rollout): the policy, PSO, compaction and c4 shadow tests,
+#      then c4 at 32 768 and 262 144 particles against the previous library (libpdenv_base.so),
+#      two interleaved rounds.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -155,6 +159,17 @@ case "${PART:-1}" in
       for d in 0 1; do
         PDENV_LIB=$lib DESCENT=$d BURN=640 FUSE=128 LAUNCHES=6 run t9_${v}_d${d}_r$r 200 python tools/time_fused.py
       done
+    done
+  done
+  ;;
+10)
+  run gpu_pol 900 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_drivers.py tests/test_gpu_multi_rank.py -x -q \
+      --timeout 600 --timeout-method thread -k "policy or pso or compaction or c4 or rollout or swarm or two_ranks"
+  for r in 1 2; do
+    for v in new base; do
+      lib=$PKG/libpdenv.so; [ $v = base ] && lib=$PKG/libpdenv_base.so
+      PDENV_LIB=$lib run c4_${v}_r$r 300 python bench.py --workload c4 --steps 8 --warmup 2 --cpu-baseline 0
+      PDENV_LIB=$lib run c4big_${v}_r$r 300 python bench.py --workload c4 --particles 262144 --steps 4 --warmup 1 --cpu-baseline 0
     done
   done
   ;;
