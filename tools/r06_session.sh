@@ -36,6 +36,8 @@
 #      parameters; k_wchunk before each rollout): the policy, PSO, compaction and c4 shadow tests,
 #      then c4 at 32 768 and 262 144 particles against the previous library (libpdenv_base.so),
 #      two interleaved rounds.
+#  11: the final build (chunked actor), part 1: the GPU suite, the smoke, the bench lines; part 12
+#      (part 2): the c4 / c5 PMC passes and the rocprofv3 traces again.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -172,6 +174,13 @@ case "${PART:-1}" in
       PDENV_LIB=$lib run c4big_${v}_r$r 300 python bench.py --workload c4 --particles 262144 --steps 4 --warmup 1 --cpu-baseline 0
     done
   done
+  ;;
+11)
+  PART=7 bash tools/r06_session.sh
+  ;;
+12)
+  run pmc6 900 bash tools/pmc_r06.sh
+  STAGES="prof profdrv profc4 profc5" run profs 900 bash tools/gpu_session.sh
   ;;
 esac
 echo "=== done"
