@@ -326,7 +326,9 @@ pd_status pd_rollout(pd_env* env, const void* actions, int32_t n_steps, void* re
  * pso_wrapped_env.objective_function (env_wrapped_ea.py:200-222) driven by simple_actor
  * (env_wrapped_ea.py:18-44) evaluated inside the step kernel.  Resets every env, then steps
  * each until done or truncated (or max_steps), accumulating fitness = -sum(reward).
- *  weights : [n_params][N] float32, parameter-major (named_parameters() order per particle)
+ *  weights : [n_params][N] float32, parameter-major (named_parameters() order per particle);
+ *            the rollout first copies them into chunks of four parameters ([ceil(P/4)][N][4],
+ *            handle-owned) that the step kernel's actor reads with 16-byte loads
  *  n_params: PD_ACTOR_PARAMS_* for the handle's phase; the handle must have rtd = PD_RTD_PSO
  *  fitness : [N] (handle precision); steps: [N] int32 episode lengths (may be NULL)
  *  check_every: >0 = read the live-env count every that many steps (at least once per launch),

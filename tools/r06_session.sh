@@ -36,6 +36,10 @@
 #      parameters; k_wchunk before each rollout): the policy, PSO, compaction and c4 shadow tests,
 #      then c4 at 32 768 and 262 144 particles against the previous library (libpdenv_base.so),
 #      two interleaved rounds.
+#  13: c2's shape (4 096 envs, no wind, no tilt) at 8 against 16 lanes per env, 1 and 128 steps per
+#      launch, two interleaved rounds: does LPE 8 (cell pieces) run the step as fast as LPE 16
+#      (split payload sums)?  (A 32-env SAC actor tile at LPE 8 would read the hidden weights half
+#      as often.)
 #  11: the final build (chunked actor), part 1: the GPU suite, the smoke, the bench lines; part 12
 #      (part 2): the c4 / c5 PMC passes and the rocprofv3 traces again.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -181,6 +185,16 @@ case "${PART:-1}" in
 12)
   run pmc6 900 bash tools/pmc_r06.sh
   STAGES="prof profdrv profc4 profc5" run profs 900 bash tools/gpu_session.sh
+  ;;
+13)
+  for r in 1 2; do
+    for l in 16 8; do
+      for f in 128 1; do
+        L=$(( f > 1 ? 6 : 60 ))
+        N=4096 LPE=$l WIND=0 TILT=0 FUSE=$f LAUNCHES=$L BURN=256 run t13_l${l}_f${f}_r$r 200 python tools/time_fused.py
+      done
+    done
+  done
   ;;
 esac
 echo "=== done"
