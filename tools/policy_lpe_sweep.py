@@ -41,6 +41,9 @@ def main():
         f, s = fits[l]
         print(json.dumps({"plpe": l, "particles": P, "rollout_ms_med": t[len(t) // 2], "rollout_ms_min": t[0],
                           "mean_episode_len": float(s.mean()),
+                          "episode_len_p50_p90_p99_max": [float(np.percentile(s, q)) for q in (50, 90, 99, 100)],
+                          # (the longest episode of each wave's 64 / LPE particles: the wave's life)
+                          "wave_life_mean": float(s[:len(s) // (64 // l) * (64 // l)].reshape(-1, 64 // l).max(1).mean()),
                           "max_rel_fitness_diff_vs_first": float(np.max(np.abs(f - f2) / (np.abs(f2) + 1.0)))}))
 
 
