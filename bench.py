@@ -274,7 +274,7 @@ def bench_pso(args, world, rank, local, dist):
     for _ in range(max(1, min(args.steps, 8))):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
-        _, steps = opt.evaluate(opt.x32)
+        _, steps = opt.evaluate(opt.x32c)
         e1.record()
         kern.append((e0, e1))
     torch.cuda.synchronize()

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define PD_ABI_VERSION 10  /* 4: pd_config.integrator (was padding); 5: pd_count_work, pd_step_sac; 6: cell pieces (pd_cell_piece_info, stats word 44); 7: pd_step_sac_ring, pd_sac_actor, stats word 45; 8: pd_step_sac_fused, pd_atm_table; 9: pd_config.table_flags, pd_tuning, caller scratch for pd_pso_swarm_minima, state/action dims of pd_step_sac_fused; 10: step launches insert their own solved misses (pd_flush_misses optional), explicit list settings turn the auto refill off */
+#define PD_ABI_VERSION 11  /* 4: pd_config.integrator (was padding); 5: pd_count_work, pd_step_sac; 6: cell pieces (pd_cell_piece_info, stats word 44); 7: pd_step_sac_ring, pd_sac_actor, stats word 45; 8: pd_step_sac_fused, pd_atm_table; 9: pd_config.table_flags, pd_tuning, caller scratch for pd_pso_swarm_minima, state/action dims of pd_step_sac_fused; 10: step launches insert their own solved misses (pd_flush_misses optional), explicit list settings turn the auto refill off; 11: pd_pso_step_chunked, pd_rollout_policy_chunked */
 #define PD_MAX_PTS 256      /* aero scatter points per table */
 #define PD_MAX_COLS 5       /* AoA columns per aero table */
 #define PD_MAX_TAB 64       /* grid-fin table length */
@@ -344,6 +344,11 @@ pd_status pd_rollout(pd_env* env, const void* actions, int32_t n_steps, void* re
  * policy_refill -1 turns it off). */
 pd_status pd_rollout_policy(pd_env* env, const float* weights, int32_t n_params, int32_t max_steps,
                             void* fitness, int32_t* steps, int32_t check_every, void* stream);
+/* pd_rollout_policy with the weights already in the chunked layout, weights4 [ceil(n_params/4)][N][4]
+ * float32 (chunk c of particle i holds parameters 4c .. 4c+3, zeros past n_params; 16-byte aligned):
+ * the layout pd_pso_step_chunked writes, so the rollout skips its copy pass.  Same results. (ABI 11) */
+pd_status pd_rollout_policy_chunked(pd_env* env, const float* weights4, int32_t n_params, int32_t max_steps,
+                                    void* fitness, int32_t* steps, int32_t check_every, void* stream);
 /* One PSO generation's particle update on the device (particle_swarm_optimisation.py:437-441
  * personal best, :515-519 update_velocity_with_local_best, :112-118 update_position), binary64:
  *   if fitness < best_fitness: best_position = position;  best_fitness = min(best_fitness, fitness)
@@ -358,6 +363,16 @@ pd_status pd_pso_step(int64_t n_particles, int32_t dim, const double* fitness, d
                       const int32_t* swarm, const double* lower, const double* upper, double w, double c1,
                       double c2, uint64_t seed, uint32_t generation, uint64_t particle_offset,
                       float* position_f32, void* stream);
+/* pd_pso_step with the float32 copy in the chunked layout of pd_rollout_policy_chunked:
+ * position_f32_chunked (required) [ceil(dim/4)][n_particles][4], zeros past dim.  One thread per
+ * (chunk, particle) updates its four parameters with the same operations as pd_pso_step (the same
+ * bits in position, velocity, best_position and best_fitness) and stores the chunk with one 16-byte
+ * store. (ABI 11) */
+pd_status pd_pso_step_chunked(int64_t n_particles, int32_t dim, const double* fitness, double* best_fitness,
+                              double* position, double* velocity, double* best_position, const double* swarm_best,
+                              const int32_t* swarm, const double* lower, const double* upper, double w, double c1,
+                              double c2, uint64_t seed, uint32_t generation, uint64_t particle_offset,
+                              float* position_f32_chunked, void* stream);
 /* Per subswarm s < n_swarms, the first particle of minimal fitness among those with swarm[p] ==
  * s: the result of particle_swarm_optimisation.py:437-441's sequential `if fitness <
  * subswarm_best` over the subswarm's particles in order (a NaN fitness never wins, ties keep the

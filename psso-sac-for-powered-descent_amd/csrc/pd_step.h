@@ -243,7 +243,7 @@ template <typename R> struct StepArgs {
     uint64_t info_mask;              // (pd_step: every field, nsel = PD_N_INFO)
     int info_nsel;
     R* reward_sum;
-    const float* policy_w;           // policy rollouts: actor parameters [P][N] float32
+    const float* policy_w;           // policy rollouts: actor parameters in chunks of four, [ceil(P/4)][N][4] float32
     // policy rollouts: the live envs as a compacted index list; a launch steps list_in[0, *cnt_in)
     // and appends the envs whose episode goes on to list_out (wave ballot + prefix count, one
     // atomic per wave), then the next launch steps those only (triple-buffered counts: this

@@ -1802,26 +1802,27 @@ __global__ __launch_bounds__(kBlock) void k_live_init(int32_t* list, uint32_t* c
 
 template <typename R>
 pd_status rollout_policy_impl(pd_env* e, const float* w, int32_t max_steps, void* fitness, int32_t* steps,
-                              int32_t check_every, hipStream_t s) {
+                              int32_t check_every, hipStream_t s, bool chunked = false) {
     const int64_t N = e->cfg.n_envs;
     unsigned grid = (unsigned)((N + kBlock - 1) / kBlock);
     hipLaunchKernelGGL(k_reset<R>, dim3(grid), dim3(kBlock), 0, s, make_args<R>(e), (const uint8_t*)nullptr);
     PD_HIP(hipMemsetAsync(fitness, 0, (size_t)N * sizeof(R), s));
     hipLaunchKernelGGL(k_live_init, dim3(grid), dim3(kBlock), 0, s, e->live[0], e->live_cnt, N);
     // the weights in the chunked layout of the step kernel's actor (one pass over them: 2 x 1.5 KB
-    // per particle, against the 1.5 KB per policy step the rollout reads)
+    // per particle, against the 1.5 KB per policy step the rollout reads), unless the caller's
+    // are chunked already (pd_rollout_policy_chunked: pd_pso_step_chunked writes that layout)
     const int P = e->cfg.phase == PD_PHASE_PURE_THROTTLE ? PD_ACTOR_PARAMS_PURE_THROTTLE : PD_ACTOR_PARAMS_LANDING_BURN;
-    if (!e->pol_w4) {
-        PD_HIP(hipMalloc((void**)&e->pol_w4, (size_t)PD_ACTOR_PARAMS_LANDING_BURN * (size_t)N * sizeof(float)));
-        e->allocs.push_back(e->pol_w4);
-    }
-    {
+    if (!chunked) {
+        if (!e->pol_w4) {
+            PD_HIP(hipMalloc((void**)&e->pol_w4, (size_t)PD_ACTOR_PARAMS_LANDING_BURN * (size_t)N * sizeof(float)));
+            e->allocs.push_back(e->pol_w4);
+        }
         const int64_t tot = (int64_t)((P + 3) / 4) * N;
         hipLaunchKernelGGL(k_wchunk, dim3((unsigned)((tot + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, w,
                            (float4*)e->pol_w4, P, N);
     }
     StepArgs<R> a = make_args<R>(e);
-    a.policy_w = e->pol_w4; a.reward_sum = (R*)fitness; a.auto_reset = 0;
+    a.policy_w = chunked ? w : e->pol_w4; a.reward_sum = (R*)fitness; a.auto_reset = 0;
     const bool wind = e->cfg.enable_wind != 0;
     // launch t steps live[t & 1][0, live_cnt[t % 3]) and appends the survivors to the other list;
     // the grid covers the live count last read back (a workgroup past the device count leaves
@@ -2294,19 +2295,34 @@ pd_status pd_rollout(pd_env* e, const void* actions, int32_t n_steps, void* rewa
     return PD_OK;
 }
 
-pd_status pd_rollout_policy(pd_env* e, const float* weights, int32_t n_params, int32_t max_steps, void* fitness,
-                            int32_t* steps, int32_t check_every, void* stream) {
+extern "C++" {
+namespace {
+pd_status rollout_policy_entry(pd_env* e, const float* weights, int32_t n_params, int32_t max_steps, void* fitness,
+                               int32_t* steps, int32_t check_every, void* stream, bool chunked) {
     if (!e || !weights || !fitness || max_steps < 0) return fail(PD_ERR_INVALID, "bad policy rollout args");
     if (e->cfg.rtd != PD_RTD_PSO) return fail(PD_ERR_UNSUPPORTED, "policy rollouts need rtd = PD_RTD_PSO");
     if (e->cfg.integrator != PD_INTEG_REFERENCE) return fail(PD_ERR_UNSUPPORTED, "policy rollouts use the reference integrator");
     int want = e->cfg.phase == PD_PHASE_PURE_THROTTLE ? PD_ACTOR_PARAMS_PURE_THROTTLE : PD_ACTOR_PARAMS_LANDING_BURN;
     if (n_params != want) return fail(PD_ERR_INVALID, "n_params does not match the phase's actor");
-    // the kernel addresses the parameter-major weights [P][N] with 32-bit per-lane byte offsets
-    if ((uint64_t)e->cfg.n_envs * (uint64_t)n_params * 4ull >= (1ull << 32))
-        return fail(PD_ERR_INVALID, "policy rollouts: n_envs x n_params x 4 must be below 2^32 bytes");
+    if (chunked && (uintptr_t)weights % 16 != 0) return fail(PD_ERR_INVALID, "chunked policy weights must be 16-byte aligned");
+    // the kernel addresses the chunked weights [ceil(P/4)][N][4] with 32-bit per-lane byte offsets
+    if ((uint64_t)e->cfg.n_envs * (uint64_t)((n_params + 3) / 4) * 16ull >= (1ull << 32))
+        return fail(PD_ERR_INVALID, "policy rollouts: n_envs x ceil(n_params / 4) x 16 must be below 2^32 bytes");
     PD_HIP(hipSetDevice(e->device));
-    return e->rsize == 8 ? rollout_policy_impl<double>(e, weights, max_steps, fitness, steps, check_every, (hipStream_t)stream)
-                         : rollout_policy_impl<float>(e, weights, max_steps, fitness, steps, check_every, (hipStream_t)stream);
+    return e->rsize == 8 ? rollout_policy_impl<double>(e, weights, max_steps, fitness, steps, check_every, (hipStream_t)stream, chunked)
+                         : rollout_policy_impl<float>(e, weights, max_steps, fitness, steps, check_every, (hipStream_t)stream, chunked);
+}
+}  // namespace
+}  // extern "C++"
+
+pd_status pd_rollout_policy(pd_env* e, const float* weights, int32_t n_params, int32_t max_steps, void* fitness,
+                            int32_t* steps, int32_t check_every, void* stream) {
+    return rollout_policy_entry(e, weights, n_params, max_steps, fitness, steps, check_every, stream, false);
+}
+
+pd_status pd_rollout_policy_chunked(pd_env* e, const float* weights4, int32_t n_params, int32_t max_steps,
+                                    void* fitness, int32_t* steps, int32_t check_every, void* stream) {
+    return rollout_policy_entry(e, weights4, n_params, max_steps, fitness, steps, check_every, stream, true);
 }
 
 pd_status pd_flush_misses(pd_env* e, void* stream) {

@@ -10,8 +10,10 @@
 // Everything is binary64 as NumPy computes it, operation by operation (left-to-right
 // products, (inertia + cognitive) + social), so a NumPy restatement with the same r1, r2 is
 // bit-identical.  Layout is parameter-major [D][P] (lane = particle): every access coalesces,
-// and the float32 copy written alongside is exactly the [P_params][N] weight layout that
-// pd_rollout_policy reads.  HBM-bound: 52 B per (particle, parameter).
+// and the float32 copy written alongside is the [P_params][N] weight layout that
+// pd_rollout_policy reads, or (pd_pso_step_chunked, k_pso_step4) the chunked layout
+// [ceil(P_params/4)][N][4] that the step kernel's actor reads, so a rollout makes no copy pass.
+// HBM-bound: 44 B per (particle, parameter).
 #include <hip/hip_runtime.h>
 
 
@@ -52,6 +54,57 @@ __global__ __launch_bounds__(kPsoBlock) void k_pso_step(
     v[e] = vn;
     x[e] = xn;
     if (x32) x32[e] = (float)xn;
+}
+
+// pd_pso_step_chunked: thread (chunk c, particle p) updates parameters 4c .. 4c+3 of particle p
+// with k_pso_step's operations in its order (one Philox draw, reused for the four: r1, r2 are per
+// particle), and stores their float32 copy as one 16-byte chunk of [ceil(D/4)][P][4], the layout
+// the step kernel's actor reads (pd_step_impl.h actor_forward), zeros past D.
+__global__ __launch_bounds__(kPsoBlock) void k_pso_step4(
+    int64_t P, int D, const double* __restrict__ fit, const double* __restrict__ pbf, double* __restrict__ x,
+    double* __restrict__ v, double* __restrict__ pb, const double* __restrict__ sb, const int32_t* __restrict__ swarm,
+    const double* __restrict__ lo, const double* __restrict__ hi, double w, double c1, double c2, uint32_t seed_lo,
+    uint32_t seed_hi, uint32_t gen, uint64_t p_offset, float4* __restrict__ x32c) {
+    const int c = blockIdx.y;
+    const int64_t p = (int64_t)blockIdx.x * kPsoBlock + threadIdx.x;
+    if (p >= P) return;
+    const bool better = fit[p] < pbf[p];
+    const uint64_t g = p_offset + (uint64_t)p;
+    u32x4 r = philox({(uint32_t)g, (uint32_t)(g >> 32), gen, kTagPso}, seed_lo, seed_hi);
+    const double r1 = u01(r.x, r.y), r2 = u01(r.z, r.w);
+    const double* sbp = sb + (int64_t)swarm[p] * D;
+    // every load of the four parameters first (the update of one does not wait on the stores of
+    // the one before), then the arithmetic in k_pso_step's order, then the stores
+    double xv[4], vv[4], pbv[4], sv[4], lv[4], hv[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int d = 4 * c + k < D ? 4 * c + k : D - 1;   // (past D: a valid address, result unused)
+        const int64_t e = (int64_t)d * P + p;
+        xv[k] = x[e]; vv[k] = v[e];
+        pbv[k] = better ? 0.0 : pb[e];
+        sv[k] = sbp[d]; lv[k] = lo[d]; hv[k] = hi[d];
+    }
+    float o[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int d = 4 * c + k;
+        o[k] = 0.f;
+        if (d < D) {
+            const int64_t e = (int64_t)d * P + p;
+            if (better) { pbv[k] = xv[k]; pb[e] = xv[k]; }
+            const double inertia = w * vv[k];
+            const double cognitive = c1 * r1 * (pbv[k] - xv[k]);
+            const double social = c2 * r2 * (sv[k] - xv[k]);
+            const double vn = inertia + cognitive + social;
+            double xn = xv[k] + vn;
+            if (xn < lv[k]) xn = lv[k];
+            else if (xn > hv[k]) xn = hv[k];
+            v[e] = vn;
+            x[e] = xn;
+            o[k] = (float)xn;
+        }
+    }
+    x32c[(int64_t)c * P + p] = make_float4(o[0], o[1], o[2], o[3]);
 }
 
 __global__ __launch_bounds__(kPsoBlock) void k_pso_best(int64_t P, const double* __restrict__ fit,
@@ -188,6 +241,26 @@ pd_status pd_pso_step(int64_t n_particles, int32_t dim, const double* fitness, d
     hipLaunchKernelGGL(k_pso_best, dim3((unsigned)((n_particles + kPsoBlock - 1) / kPsoBlock)), dim3(kPsoBlock), 0, s,
                        n_particles, fitness, best_fitness);
     if (hipGetLastError() != hipSuccess) return set_error(PD_ERR_HIP, "pd_pso_step: launch failed");
+    return PD_OK;
+}
+
+pd_status pd_pso_step_chunked(int64_t n_particles, int32_t dim, const double* fitness, double* best_fitness,
+                              double* position, double* velocity, double* best_position, const double* swarm_best,
+                              const int32_t* swarm, const double* lower, const double* upper, double w, double c1,
+                              double c2, uint64_t seed, uint32_t generation, uint64_t particle_offset,
+                              float* position_f32_chunked, void* stream) {
+    if (n_particles <= 0 || dim <= 0 || dim > 65535 || !fitness || !best_fitness || !position || !velocity ||
+        !best_position || !swarm_best || !swarm || !lower || !upper || !position_f32_chunked ||
+        (uintptr_t)position_f32_chunked % 16 != 0)
+        return set_error(PD_ERR_INVALID, "pd_pso_step_chunked: bad arguments (the chunked copy is required, 16-byte aligned)");
+    hipStream_t s = (hipStream_t)stream;
+    dim3 grid((unsigned)((n_particles + kPsoBlock - 1) / kPsoBlock), (unsigned)((dim + 3) / 4));
+    hipLaunchKernelGGL(k_pso_step4, grid, dim3(kPsoBlock), 0, s, n_particles, dim, fitness, best_fitness, position,
+                       velocity, best_position, swarm_best, swarm, lower, upper, w, c1, c2, (uint32_t)seed,
+                       (uint32_t)(seed >> 32), generation, particle_offset, (float4*)position_f32_chunked);
+    hipLaunchKernelGGL(k_pso_best, dim3((unsigned)((n_particles + kPsoBlock - 1) / kPsoBlock)), dim3(kPsoBlock), 0, s,
+                       n_particles, fitness, best_fitness);
+    if (hipGetLastError() != hipSuccess) return set_error(PD_ERR_HIP, "pd_pso_step_chunked: launch failed");
     return PD_OK;
 }
 

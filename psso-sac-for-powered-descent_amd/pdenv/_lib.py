@@ -99,8 +99,8 @@ EXPORTS = ["pd_abi_version", "pd_sizeof_params", "pd_sizeof_config", "pd_last_er
            "pd_checkpoint_load", "pd_counters", "pd_stats", "pd_count_work", "pd_atmosphere", "pd_obs_dim",
            "pd_action_dim", "pd_step_sac", "pd_pso_swarm_minima", "pd_pso_update_bests", "pd_cell_piece_info",
            "pd_step_sac_ring", "pd_sac_actor", "pd_step_sac_fused", "pd_atm_table", "pd_set_tuning", "pd_get_tuning",
-           "pd_pso_swarm_minima_scratch_bytes", "pd_step_n_info"]
-ABI_VERSION = 10
+           "pd_pso_swarm_minima_scratch_bytes", "pd_step_n_info", "pd_pso_step_chunked", "pd_rollout_policy_chunked"]
+ABI_VERSION = 11
 
 _lib = None
 
@@ -140,8 +140,10 @@ def load(path=None):
     L.pd_get_tuning.argtypes = [vp, P(PdTuning)]
     L.pd_rollout.argtypes = [vp, vp, I32, vp, vp]
     L.pd_rollout_policy.argtypes = [vp, vp, I32, I32, vp, vp, I32, vp]
+    L.pd_rollout_policy_chunked.argtypes = [vp, vp, I32, I32, vp, vp, I32, vp]
     L.pd_pso_step.argtypes = [I64, I32, vp, vp, vp, vp, vp, vp, vp, vp, vp, C.c_double, C.c_double, C.c_double,
                               U64, C.c_uint32, U64, vp, vp]
+    L.pd_pso_step_chunked.argtypes = L.pd_pso_step.argtypes
     L.pd_pso_swarm_minima.argtypes = [I64, I32, I32, vp, vp, vp, vp, vp, vp, C.c_size_t, vp]
     L.pd_pso_swarm_minima_scratch_bytes.argtypes = [I64, I32]
     L.pd_pso_swarm_minima_scratch_bytes.restype = C.c_size_t
@@ -171,7 +173,7 @@ def load(path=None):
     L.pd_obs_dim.argtypes = [vp]; L.pd_obs_dim.restype = C.c_int
     L.pd_action_dim.argtypes = [vp]; L.pd_action_dim.restype = C.c_int
     for name in ("pd_create", "pd_destroy", "pd_reset", "pd_step", "pd_step_n", "pd_step_sac", "pd_rollout", "pd_rollout_policy", "pd_pso_step",
-                 "pd_pso_swarm_minima", "pd_pso_update_bests", "pd_flush_misses", "pd_observe",
+                 "pd_rollout_policy_chunked", "pd_pso_step_chunked", "pd_pso_swarm_minima", "pd_pso_update_bests", "pd_flush_misses", "pd_observe",
                  "pd_get_state", "pd_set_state", "pd_get_actuators", "pd_set_actuators",
                  "pd_set_wind_sigmas", "pd_set_gload_window", "pd_counters", "pd_stats", "pd_count_work",
                  "pd_get_gload_window",

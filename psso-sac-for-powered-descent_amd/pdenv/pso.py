@@ -2,9 +2,10 @@
 
 ParticleSubswarmOptimisation.run (src/particle_swarm_optimisation/particle_swarm_optimisation.py
 :285-520) with the swarm kept on the GPU between generations: particles are evaluated by
-pd_rollout_policy (the actor fused into the step kernel), the personal-best / velocity /
-position update is pd_pso_step (binary64, parameter-major [D][P]), and only per-subswarm
-minima cross ranks.  The reference's parameters (configs/evolutionary_algorithms_config.py)
+pd_rollout_policy_chunked (the actor fused into the step kernel), the personal-best / velocity /
+position update is pd_pso_step_chunked (binary64, parameter-major [D][P]; its float32 copy is
+written in the rollout's chunked weight layout, so a generation makes no copy pass), and only
+per-subswarm minima cross ranks.  The reference's parameters (configs/evolutionary_algorithms_config.py)
 are the defaults; the population can be scaled to config c4's 262 144 particles.
 
 Randomness: positions U(bounds) at init, r1/r2 per particle and generation (Philox, in the
@@ -38,6 +39,23 @@ def _to_device(values, dtype, device):
     pageable copy would wait for the queue: a generation that draws host-side decisions must not
     drain it)."""
     return torch.tensor(values, dtype=dtype).pin_memory().to(device, non_blocking=True)
+
+
+def chunk4(w):
+    """float32 actor weights [D][n] -> the chunked layout [ceil(D/4)][n][4] (chunk c of column i
+    holds parameters 4c .. 4c+3, zeros past D) that pd_rollout_policy_chunked reads and
+    pd_pso_step_chunked writes."""
+    D, n = w.shape
+    C = (D + 3) // 4
+    if C * 4 != D:
+        w = torch.cat([w, torch.zeros(C * 4 - D, n, dtype=w.dtype, device=w.device)])
+    return w.reshape(C, 4, n).permute(0, 2, 1).contiguous()
+
+
+def unchunk4(w4, D):
+    """The inverse of chunk4: [C][n][4] -> [D][n]."""
+    C, n, _ = w4.shape
+    return w4.permute(0, 2, 1).reshape(C * 4, n)[:D].contiguous()
 
 
 def all_gather_var(t, dist):
@@ -153,7 +171,8 @@ class ParticleSubswarmOptimisationGPU:
         self.v = torch.zeros_like(self.x)
         self.pb = torch.zeros_like(self.x)
         self.pbf = torch.full((self.P,), math.inf, dtype=torch.float64, device=self.device)
-        self.x32 = self.x.float().contiguous()
+        # the float32 actor weights in the rollout's chunked layout (pd_pso_step_chunked keeps it)
+        self.x32c = chunk4(self.x.float())
         gid = torch.arange(self.offset, self.offset + self.P, device=self.device)
         self.swarm = (gid // self.sub_size).to(torch.int32).contiguous()
         # the GLOBAL membership mirrored on the host: only migrate_particles (host-drawn moves) and
@@ -211,14 +230,14 @@ class ParticleSubswarmOptimisationGPU:
         moved = [0]
         sb[0] = (1 - 0.3) * sb[0] + 0.3 * sb[self.S - 1]
         pad = moved + [moved[0]] * (self.S - 1 - len(moved))
-        cand = sb[pad].t().float().contiguous()
+        cand = chunk4(sb[pad].t().float())
         fit = torch.zeros(cand.shape[1], dtype=torch.float64, device=self.device)[:len(moved)]
         mv = _to_device(moved, torch.int64, self.device)
         old = sbf[mv]
         sbf[mv] = torch.where(fit < old, fit, old)
         sb[mv] = (1 - 0.3) * sb[mv] + 0.3 * sb[self.S - 1]
         if self._mergeable():
-            torch.cat([self.x32, cand], dim=1)
+            torch.cat([self.x32c, cand], dim=1)
         if self.P > 0:
             sw = self.swarm.clone()
             sw[0] = 0
@@ -231,16 +250,23 @@ class ParticleSubswarmOptimisationGPU:
             self._aux[n] = self._new_env(n)
         return self._aux[n]
 
+    @property
+    def x32(self):
+        """The swarm's float32 positions [D][P] (a copy of the chunked weights the rollouts read)."""
+        return unchunk4(self.x32c, self.D)
+
     def evaluate(self, x32):
-        """pso_wrapped_env.objective_function for every column of x32 [D][n] (fused actor)."""
+        """pso_wrapped_env.objective_function for every particle of x32 (fused actor): chunked
+        weights [ceil(D/4)][n][4] (chunk4; pd_rollout_policy_chunked) or plain [D][n]
+        (pd_rollout_policy, which chunks them itself)."""
         n = x32.shape[1]
         if n == 0:
             return torch.empty(0, dtype=torch.float64, device=self.device), torch.empty(0, dtype=torch.int32)
         env = self._env_for(n)
         fit = torch.empty(n, dtype=env.dtype, device=self.device)
         steps = torch.empty(n, dtype=torch.int32, device=self.device)
-        L.check(self.lib.pd_rollout_policy(env.h, _ptr(x32), self.D, self.max_steps, _ptr(fit), _ptr(steps), 8,
-                                           _stream(self.device)))
+        roll = self.lib.pd_rollout_policy_chunked if x32.dim() == 3 else self.lib.pd_rollout_policy
+        L.check(roll(env.h, _ptr(x32), self.D, self.max_steps, _ptr(fit), _ptr(steps), 8, _stream(self.device)))
         return fit.double(), steps
 
     # ------------------------------------------------------------------ one generation
@@ -316,12 +342,12 @@ class ParticleSubswarmOptimisationGPU:
             # env's episode is independent of the batch: the same fitness bits as on their own);
             # their bests are updated before this generation's (the reference's order)
             cand = self._pending[2]
-            fit_all, _ = self.evaluate(torch.cat([self.x32, cand], dim=1))
+            fit_all, _ = self.evaluate(torch.cat([self.x32c, cand], dim=1))
             fit = fit_all[:self.P]
             self.flush_share(fit_all[self.P:])
         else:
             self.flush_share()
-            fit, _ = self.evaluate(self.x32)
+            fit, _ = self.evaluate(self.x32c)
         self.last_fitness = fit
         f, pos = self._swarm_minima(fit)
         # :442-444 per subswarm: a strictly better minimum replaces the subswarm best; :474-477
@@ -331,10 +357,10 @@ class ParticleSubswarmOptimisationGPU:
                                              _ptr(self.gbf_t), _ptr(self.gb_t), _stream(self.device)))
         self.w = self.p["w_start"] - (self.p["w_start"] - self.p["w_end"]) * gen / self.p["generations"]
         if self.P > 0:
-            L.check(self.lib.pd_pso_step(self.P, self.D, _ptr(fit), _ptr(self.pbf), _ptr(self.x), _ptr(self.v),
+            L.check(self.lib.pd_pso_step_chunked(self.P, self.D, _ptr(fit), _ptr(self.pbf), _ptr(self.x), _ptr(self.v),
                                          _ptr(self.pb), _ptr(self.sb), _ptr(self.swarm), _ptr(self.lower),
                                          _ptr(self.upper), float(self.w), float(self.p["c1"]), float(self.p["c2"]),
-                                         self.seed, gen, self.offset, _ptr(self.x32), _stream(self.device)))
+                                         self.seed, gen, self.offset, _ptr(self.x32c), _stream(self.device)))
         self._gen = gen
         if gen % self.p["communication_freq"] == 0 and gen > 0:
             self.share_information()
@@ -362,7 +388,7 @@ class ParticleSubswarmOptimisationGPU:
         mv = _to_device(moved, torch.int64, self.device)
         self.sb[mv] = (1 - 0.3) * self.sb[mv] + 0.3 * self.sb[best]
         pad = moved + [moved[0]] * (self.S - 1 - len(moved))  # (padded to the share handle's size)
-        cand = self.sb[pad].t().float().contiguous()            # [D][S-1]
+        cand = chunk4(self.sb[pad].t().float())                 # [ceil(D/4)][S-1][4]
         # evaluated with the next generation's rollout (or on the next read of the bests)
         self._pending = (getattr(self, "_gen", None), moved, cand)
 
@@ -389,7 +415,7 @@ class ParticleSubswarmOptimisationGPU:
         sel = torch.nonzero(mine).flatten()
         self.x, self.v, self.pb = (t[:, sel].contiguous() for t in (self.x, self.v, self.pb))
         self.pbf, self.swarm = self.pbf[sel].contiguous(), self.swarm[sel].contiguous()
-        self.x32 = self.x.float().contiguous()
+        self.x32c = chunk4(self.x.float())
         gids = torch.nonzero(keep).flatten()
         self.offset = int((gids < self.offset).sum()) if self.P else 0
         self.P = int(sel.numel())

@@ -29,7 +29,7 @@ def test_struct_layout_and_abi():
     import pdenv
     from pdenv import _lib
     L = pdenv.load()
-    assert L.pd_abi_version() == _lib.ABI_VERSION == 10
+    assert L.pd_abi_version() == _lib.ABI_VERSION == 11
     assert L.pd_sizeof_params() == C.sizeof(_lib.PdParams)
     assert L.pd_sizeof_config() == C.sizeof(_lib.PdConfig)
 
@@ -53,6 +53,12 @@ def test_argument_checks_before_any_launch():
         st = L.pd_pso_swarm_minima(5000, 10, 3, vp(0x10000), vp(0x10000), vp(0x10000), vp(0x10000), vp(0x10000),
                                    scratch, nb, None)
         assert st == _lib.PD_ERR_INVALID and b"scratch" in L.pd_last_error()
+    # pd_pso_step_chunked: the chunked copy is required and 16-byte aligned
+    a = [vp(0x10000)] * 9
+    for x32c in (None, vp(0x10008)):
+        st = L.pd_pso_step_chunked(5000, 372, *a, 0.7, 1.5, 1.5, 1, 0, 0, x32c, None)
+        assert st == _lib.PD_ERR_INVALID and b"chunked" in L.pd_last_error()
+    assert L.pd_rollout_policy_chunked(None, vp(0x10000), 372, 10, vp(0x10000), None, 0, None) == _lib.PD_ERR_INVALID
     t = _lib.PdTuning(128, 64, 2, -1, 0.0, -1, 0, -1, 0)
     assert L.pd_set_tuning(None, C.byref(t)) == _lib.PD_ERR_INVALID
     assert L.pd_get_tuning(None, C.byref(t)) == _lib.PD_ERR_INVALID

@@ -622,6 +622,71 @@ def test_pso_step_matches_numpy(pd):
     assert np.array_equal(x32.cpu().numpy(), xn.astype(np.float32))
 
 
+@pytest.mark.parametrize("D", [372, 249, 10])
+def test_pso_step_chunked_matches_numpy(pd, D):
+    """pd_pso_step_chunked: the same update bit for bit (one thread per four parameters), its
+    float32 copy in the chunked layout [ceil(D/4)][P][4] with zeros past D (D = 249, the pure
+    throttle actor, and 10 end inside a chunk)."""
+    import torch
+    from pdenv import _lib as L
+    from pdenv.env import _ptr
+    from pdenv.pso import chunk4, unchunk4
+    rng = np.random.default_rng(5)
+    P, S = 777, 4
+    x = rng.uniform(-1.5, 1.5, (D, P)); v = rng.normal(0, 0.2, (D, P)); pb = rng.uniform(-1.5, 1.5, (D, P))
+    pbf = rng.uniform(0, 10, P); pbf[::5] = np.inf
+    fit = rng.uniform(0, 10, P); fit[::11] = np.nan
+    sb = rng.uniform(-1.5, 1.5, (S, D))
+    swarm = rng.integers(0, S, P).astype(np.int32)
+    lo, hi = np.full(D, -1.5), np.full(D, 1.5)
+    w, c1, c2, seed, gen, off = 0.61, 1.0, 1.0, 0xABCDEF01234, 3, 77
+    T = {k: torch.tensor(a).cuda() for k, a in dict(x=x, v=v, pb=pb, pbf=pbf, fit=fit, sb=sb, swarm=swarm,
+                                                      lo=lo, hi=hi).items()}
+    C = (D + 3) // 4
+    x32c = torch.full((C, P, 4), 7.0, dtype=torch.float32, device="cuda")   # (the pad lanes must be written)
+    lib = L.load()
+    L.check(lib.pd_pso_step_chunked(P, D, _ptr(T["fit"]), _ptr(T["pbf"]), _ptr(T["x"]), _ptr(T["v"]), _ptr(T["pb"]),
+                                    _ptr(T["sb"]), _ptr(T["swarm"]), _ptr(T["lo"]), _ptr(T["hi"]), w, c1, c2, seed,
+                                    gen, off, _ptr(x32c), None))
+    torch.cuda.synchronize()
+    xn, vn, pbn, pbfn = _np_pso_step(x, v, pb, pbf, fit, sb, swarm, lo, hi, w, c1, c2, seed, gen, off)
+    assert np.array_equal(T["x"].cpu().numpy(), xn) and np.array_equal(T["v"].cpu().numpy(), vn)
+    assert np.array_equal(T["pb"].cpu().numpy(), pbn)
+    assert np.array_equal(T["pbf"].cpu().numpy(), pbfn, equal_nan=True)
+    ref = chunk4(torch.tensor(xn.astype(np.float32)))
+    assert torch.equal(x32c.cpu(), ref)
+    assert np.array_equal(unchunk4(x32c, D).cpu().numpy(), xn.astype(np.float32))
+
+
+@pytest.mark.parametrize("phase", ["landing_burn", "landing_burn_pure_throttle"])
+def test_rollout_policy_chunked_same_bits(pd, phase):
+    """pd_rollout_policy_chunked on chunk4'd weights gives pd_rollout_policy's fitness and
+    episode lengths bit for bit (refill launch and the compacted list)."""
+    import torch
+    from pdenv.env import _ptr, _stream
+    from pdenv import _lib as L
+    from pdenv.pso import chunk4
+    n = 3000
+    env = pd.PoweredDescentEnv(n, flight_phase=phase, mode="pso", device=0)
+    D = 372 if phase == "landing_burn" else 249
+    W = torch.from_numpy(np.random.default_rng(11).uniform(-1.5, 1.5, (D, n)).astype(np.float32)).cuda()
+    W4 = chunk4(W)
+    lib = L.load()
+    for tune in (dict(), dict(policy_refill=-1, policy_list=1)):
+        if tune:
+            env.set_tuning(**tune)
+        out = []
+        for fn, w in ((lib.pd_rollout_policy, W), (lib.pd_rollout_policy_chunked, W4)):
+            fit = torch.empty(n, dtype=torch.float64, device="cuda")
+            steps = torch.empty(n, dtype=torch.int32, device="cuda")
+            L.check(fn(env.h, _ptr(w), D, 400, _ptr(fit), _ptr(steps), 8, _stream(env.device)))
+            torch.cuda.synchronize()
+            out.append((fit.cpu().numpy(), steps.cpu().numpy()))
+        assert np.array_equal(out[0][0], out[1][0]) and np.array_equal(out[0][1], out[1][1]), tune
+        assert (out[0][1] >= 1).all()
+    env.close()
+
+
 def test_pso_swarm_minima_and_bests_vs_numpy(pd):
     """pd_pso_swarm_minima (the reference's sequential `if fitness < subswarm_best` per subswarm,
     particle_swarm_optimisation.py:437-441: a NaN never wins, ties keep the lower index, +inf for

@@ -44,3 +44,24 @@ def test_migration_moves_equal_list_restatement():
             except ValueError as e:    # a subswarm emptied by its own migrants: both raise
                 out.append(type(e))
         assert out[0] == out[1], seed
+
+
+def test_chunk4_layout_and_inverse():
+    """chunk4: chunk c of column i holds parameters 4c .. 4c+3 (zeros past D), the layout
+    pd_rollout_policy_chunked reads; unchunk4 inverts it; concatenating chunked batches along
+    the particle axis equals chunking the concatenation (the merged share rollout relies on it)."""
+    from pdenv.pso import chunk4, unchunk4
+    g = torch.Generator().manual_seed(0)
+    for D, n in ((372, 33), (249, 5), (10, 7), (4, 1)):
+        w = torch.rand(D, n, generator=g)
+        w4 = chunk4(w)
+        C = (D + 3) // 4
+        assert w4.shape == (C, n, 4) and w4.is_contiguous()
+        for c in range(C):
+            for k in range(4):
+                d = 4 * c + k
+                exp = w[d] if d < D else torch.zeros(n)
+                assert torch.equal(w4[c, :, k], exp)
+        assert torch.equal(unchunk4(w4, D), w)
+        v = torch.rand(D, 3, generator=g)
+        assert torch.equal(torch.cat([w4, chunk4(v)], dim=1), chunk4(torch.cat([w, v], dim=1)))
