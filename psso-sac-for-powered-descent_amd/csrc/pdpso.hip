@@ -65,6 +65,9 @@ __global__ __launch_bounds__(kPsoBlock) void k_pso_step4(
     double* __restrict__ v, double* __restrict__ pb, const double* __restrict__ sb, const int32_t* __restrict__ swarm,
     const double* __restrict__ lo, const double* __restrict__ hi, double w, double c1, double c2, uint32_t seed_lo,
     uint32_t seed_hi, uint32_t gen, uint64_t p_offset, float4* __restrict__ x32c) {
+    // (grid: the particle range fastest, as k_pso_step's.  Chunk-major and tiled orders keep the
+    // range's fit / pbf / swarm words in L2 across its chunks, 0.4 GB fewer fetches at 262 144
+    // particles, and measured 5-8 % slower: tools/pso_grid_ab.py, profiles/r06_exp_pso_chunked.jsonl)
     const int c = blockIdx.y;
     const int64_t p = (int64_t)blockIdx.x * kPsoBlock + threadIdx.x;
     if (p >= P) return;

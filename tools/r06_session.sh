@@ -42,6 +42,11 @@
 #      as often.)
 #  11: the final build (chunked actor), part 1: the GPU suite, the smoke, the bench lines; part 12
 #      (part 2): the c4 / c5 PMC passes and the rocprofv3 traces again.
+#  14: the PSO driver on the chunked copy (ABI 11: pd_pso_step_chunked writes the rollout's weight
+#      layout, pd_rollout_policy_chunked skips k_wchunk): the PSO / policy / c4 / two-rank tests,
+#      then tools/c4_chunked_ab.py (the chunked path against the plain copy, interleaved in one
+#      process, swarms bit-identical) at 32 768 and 262 144 particles, and a kernel trace of it;
+#      the update call alone: tools/pso_grid_ab.py.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -185,6 +190,16 @@ case "${PART:-1}" in
 12)
   run pmc6 900 bash tools/pmc_r06.sh
   STAGES="prof profdrv profc4 profc5" run profs 900 bash tools/gpu_session.sh
+  ;;
+14)
+  run gpu_chunk 900 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_drivers.py tests/test_gpu_multi_rank.py -x -q \
+      --timeout 600 --timeout-method thread -k "policy or pso or compaction or c4 or rollout or swarm or two_ranks or chunked"
+  P=32768 G=8 ROUNDS=6 run ab14_32k 300 python -u tools/c4_chunked_ab.py
+  P=262144 G=4 ROUNDS=6 run ab14_262k 300 python -u tools/c4_chunked_ab.py
+  P=262144 G=2 ROUNDS=2 run kt14 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/kt14 -o p -- \
+      python3 -u tools/c4_chunked_ab.py
+  P=262144 run grid14_262k 120 python -u tools/pso_grid_ab.py
+  P=32768 ROUNDS=20 run grid14_32k 120 python -u tools/pso_grid_ab.py
   ;;
 13)
   for r in 1 2; do
