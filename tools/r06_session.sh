@@ -47,6 +47,8 @@
 #      then tools/c4_chunked_ab.py (the chunked path against the plain copy, interleaved in one
 #      process, swarms bit-identical) at 32 768 and 262 144 particles, and a kernel trace of it;
 #      the update call alone: tools/pso_grid_ab.py.
+#  15: the RCCL path again on the final build (torchrun, one rank, PD_BENCH_DIST=1: c4 with the
+#      chunked swarm copy, c5, c3).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -200,6 +202,11 @@ case "${PART:-1}" in
       python3 -u tools/c4_chunked_ab.py
   P=262144 run grid14_262k 120 python -u tools/pso_grid_ab.py
   P=32768 ROUNDS=20 run grid14_32k 120 python -u tools/pso_grid_ab.py
+  ;;
+15)
+  rccl c4 --workload c4 --steps 4 --warmup 2 --cpu-baseline 0
+  rccl c5 --workload c5 --steps 32 --warmup 8 --cpu-baseline 0
+  rccl c3 --steps 32 --warmup 16 --cpu-baseline 0 --secondary 0 --descent 0 --fresh 0 --others 0
   ;;
 13)
   for r in 1 2; do
