@@ -1800,14 +1800,50 @@ __global__ __launch_bounds__(kBlock) void k_live_init(int32_t* list, uint32_t* c
     if (i < 3) cnt[i] = i == 0 ? (uint32_t)n : 0u;
 }
 
+// policy rollouts' prologue in one launch: k_reset of every env, its fitness zeroed, and the live
+// list / counts of k_live_init (refill: the three counts zero, the refill launch's hand-out
+// counter among them) -- the four launches a rollout used to start with
+template <typename R>
+__global__ __launch_bounds__(kBlock) void k_policy_init(StepArgs<R> a, R* __restrict__ fitness, int32_t* list,
+                                                        uint32_t* cnt, int refill) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i < 3) cnt[i] = (i == 0 && !refill) ? (uint32_t)a.n : 0u;
+    if (i >= a.n) return;
+    list[i] = (int32_t)i;
+    fitness[i] = R(0);
+    DP<R>& P = *params<R>(a.P);
+    const uint32_t ui = (uint32_t)i;
+    EnvRegs<R> e;
+    reset_values<R>(P, a, a.env_offset + (uint64_t)i, ev(a.b.epi, ui) + 1u,
+                    (const double*)(uint64_t)&P.logtab.invc[0], (const double*)(uint64_t)&P.logtab.logc[0], e);
+    store_env<R>(a, P, ui, e, true);
+}
+
+// policy rollouts' epilogue in one launch: k_insert (thread 0 of block 0) and the episode lengths
+// copied to the caller's steps (the tstep words), which used a copy of its own
+template <typename R>
+__global__ __launch_bounds__(kBlock) void k_policy_finish(Pending pend, unsigned long long* keys_cd, R* pay_cd,
+                                                          int lc_cd, unsigned long long* keys_cl, R* pay_cl, int lc_cl,
+                                                          const uint32_t* __restrict__ tstep, int32_t* __restrict__ steps,
+                                                          int64_t n) {
+    if (blockIdx.x == 0 && threadIdx.x == 0)
+        insert_pending<R>(pend.count, pend.keys, pend.pay, pend.stats, keys_cd, pay_cd, lc_cd, keys_cl, pay_cl, lc_cl);
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (steps && i < n) steps[i] = (int32_t)tstep[i];
+}
+
+template <typename R> void launch_policy_finish(pd_env* e, int32_t* steps, hipStream_t s) {
+    const int64_t N = e->cfg.n_envs;
+    hipLaunchKernelGGL(k_policy_finish<R>, dim3((unsigned)((N + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, e->pend,
+                       e->keys_cd, (R*)e->pay_cd, e->logcap_cd, e->keys_cl, (R*)e->pay_cl, e->logcap_cl,
+                       (const uint32_t*)e->tstep, steps, N);
+}
+
 template <typename R>
 pd_status rollout_policy_impl(pd_env* e, const float* w, int32_t max_steps, void* fitness, int32_t* steps,
                               int32_t check_every, hipStream_t s, bool chunked = false) {
     const int64_t N = e->cfg.n_envs;
     unsigned grid = (unsigned)((N + kBlock - 1) / kBlock);
-    hipLaunchKernelGGL(k_reset<R>, dim3(grid), dim3(kBlock), 0, s, make_args<R>(e), (const uint8_t*)nullptr);
-    PD_HIP(hipMemsetAsync(fitness, 0, (size_t)N * sizeof(R), s));
-    hipLaunchKernelGGL(k_live_init, dim3(grid), dim3(kBlock), 0, s, e->live[0], e->live_cnt, N);
     // the weights in the chunked layout of the step kernel's actor (one pass over them: 2 x 1.5 KB
     // per particle, against the 1.5 KB per policy step the rollout reads), unless the caller's
     // are chunked already (pd_rollout_policy_chunked: pd_pso_step_chunked writes that layout)
@@ -1856,6 +1892,9 @@ pd_status rollout_policy_impl(pd_env* e, const float* w, int32_t max_steps, void
     const bool refill_on = e->tune.policy_refill > 0 ||
                            (e->tune.policy_refill < 0 && e->tune.policy_list < 0 && !(e->tune.policy_list_at > 0.0));
     const bool refill = !wind && N >= 64 / plpe && refill_on;
+    // every env reset, fitness zeroed, the live list and counts initialised: one launch
+    hipLaunchKernelGGL(k_policy_init<R>, dim3(grid), dim3(kBlock), 0, s, make_args<R>(e), (R*)fitness, e->live[0],
+                       e->live_cnt, refill ? 1 : 0);
     if (refill) {
         // slots: whole waves (epw envs each), at most the swarm; wave w owns particles
         // [w Q, (w + 1) Q) -- its first epw are its slots' first episodes -- and takes them
@@ -1871,7 +1910,6 @@ pd_status rollout_policy_impl(pd_env* e, const float* w, int32_t max_steps, void
         const int own = e->tune.policy_refill_own >= 0 ? e->tune.policy_refill_own : 100;
         int64_t q = (int64_t)((double)N * own / 100.0 / (double)waves) / epw * epw;
         q = std::max<int64_t>(epw, std::min<int64_t>(q, N / waves / epw * epw));   // (waves q <= N: N >= slots)
-        PD_HIP(hipMemsetAsync(e->live_cnt, 0, 3 * sizeof(uint32_t), s));
         a.use_list = 0; a.policy_wc = nullptr;
         a.refill = e->tune.policy_refill > 0 ? e->tune.policy_refill : kRefillBatch;
         a.refill_next = e->live_cnt; a.refill_max = max_steps;
@@ -1886,8 +1924,7 @@ pd_status rollout_policy_impl(pd_env* e, const float* w, int32_t max_steps, void
         if (e->cfg.phase == PD_PHASE_PURE_THROTTLE) { if (wind) launch_policy<R, 0, true>(plpe, a, slots, s); else launch_policy<R, 0, false>(plpe, a, slots, s); }
         else { if (wind) launch_policy<R, 1, true>(plpe, a, slots, s); else launch_policy<R, 1, false>(plpe, a, slots, s); }
         PD_HIP(hipGetLastError());
-        launch_insert<R>(e, s);
-        if (steps) PD_HIP(hipMemcpyAsync(steps, e->tstep, (size_t)N * 4, hipMemcpyDeviceToDevice, s));
+        launch_policy_finish<R>(e, steps, s);
         PD_HIP(hipGetLastError());
         return PD_OK;
     }
@@ -1932,8 +1969,7 @@ pd_status rollout_policy_impl(pd_env* e, const float* w, int32_t max_steps, void
             ++checks;
         }
     }
-    launch_insert<R>(e, s);
-    if (steps) PD_HIP(hipMemcpyAsync(steps, e->tstep, (size_t)N * 4, hipMemcpyDeviceToDevice, s));
+    launch_policy_finish<R>(e, steps, s);
     PD_HIP(hipGetLastError());
     return PD_OK;
 }
