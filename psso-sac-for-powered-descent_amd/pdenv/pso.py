@@ -193,8 +193,10 @@ class ParticleSubswarmOptimisationGPU:
         self._aux = {self.S - 1: self._new_env(self.S - 1)} if self.S > 1 else {}
         self.last_fitness = None
         self._pending = None           # a share's candidates, evaluated with the next generation
-        self._share_log = None
-        self.share_history = []        # (generation, moved subswarms, their candidates' fitness)
+        # every completed share: (generation, moved subswarms, count, candidates' fitness), the
+        # moved subswarms a host list (count None) or, for a share decided on the device, the padded
+        # device index tensor and a device count (share_history / share_log read them back)
+        self._share_raw = []
         self._make_merged_handle()
         self._warm_share_path()
 
@@ -226,6 +228,11 @@ class ParticleSubswarmOptimisationGPU:
         timed generation 50-180 ms when the first non-empty share came."""
         if self.S < 2:
             return
+        if self._mergeable():
+            sb, sbf = self.sb.clone(), self.sbf_t.clone()
+            u = _to_device([0.25] * (self.S - 1), torch.float64, self.device)
+            pad, count, _ = self._share_on_device(sb, sbf, u)
+            self._flush_on_device(sbf, pad, count, torch.zeros(self.S - 1, dtype=torch.float64, device=self.device))
         sb, sbf = self.sb.clone(), self.sbf_t.clone()
         moved = [0]
         sb[0] = (1 - 0.3) * sb[0] + 0.3 * sb[self.S - 1]
@@ -240,7 +247,7 @@ class ParticleSubswarmOptimisationGPU:
             torch.cat([self.x32c, cand], dim=1)
         if self.P > 0:
             sw = self.swarm.clone()
-            sw[0] = 0
+            sw.index_put_((_to_device([0], torch.int64, self.device),), _to_device([0], torch.int32, self.device))
         torch.cuda.synchronize(self.device)
 
     def _env_for(self, n):
@@ -288,10 +295,27 @@ class ParticleSubswarmOptimisationGPU:
         return None if not math.isfinite(self.gbf) else self.gb_t.clone()
 
     @property
-    def share_log(self):
-        """(moved subswarms, their candidates' fitness) of the last share_information."""
+    def share_history(self):
+        """[(generation, moved subswarms, their candidates' fitness)] of every share_information
+        that moved a subswarm (reads the device decisions back)."""
         self.flush_share()
-        return self._share_log
+        out = []
+        for gen, moved, count, fit in self._share_raw:
+            if count is not None:
+                c = int(count)
+                if c == 0:
+                    continue
+                moved = [int(i) for i in moved[:c].tolist()]
+                fit = fit[:c]
+            out.append((gen, moved, fit))
+        return out
+
+    @property
+    def share_log(self):
+        """(moved subswarms, their candidates' fitness) of the last share_information that moved
+        a subswarm."""
+        h = self.share_history
+        return (h[-1][1], h[-1][2]) if h else None
 
     def flush_share(self, fit=None):
         """Complete a pending share_information (:533-541): the candidates' fitness (`fit`, from
@@ -299,16 +323,32 @@ class ParticleSubswarmOptimisationGPU:
         fitness when strictly better."""
         if self._pending is None:
             return
-        gen, moved, cand = self._pending
+        gen, moved, count, cand = self._pending
         self._pending = None
+        if count is not None:                                    # decided on the device
+            if fit is None:
+                if int(count) == 0:                              # (a read: nothing moved)
+                    return
+                fit, _ = self.evaluate(cand)
+            fit = fit[:self.S - 1].clone()
+            self._share_raw.append((gen, moved, count, fit))
+            self._flush_on_device(self.sbf_t, moved, count, fit)
+            return
         if fit is None:
             fit, _ = self.evaluate(cand)
-        fit = fit[:len(moved)]
-        self._share_log = (moved, fit.clone())
-        self.share_history.append((gen, moved, self._share_log[1]))
+        fit = fit[:len(moved)].clone()
+        self._share_raw.append((gen, moved, None, fit))
         mv = _to_device(moved, torch.int64, self.device)
         old = self.sbf_t[mv]
         self.sbf_t[mv] = torch.where(fit < old, fit, old)
+
+    @staticmethod
+    def _flush_on_device(sbf, pad, count, fit):
+        """The strictly-better replacement of a device-decided share: every padded entry repeats
+        the first moved subswarm with its (same) candidate, so the duplicate writes agree; nothing
+        changes when nothing moved."""
+        old = sbf.index_select(0, pad)
+        sbf.index_put_((pad,), torch.where((count > 0) & (fit < old), fit, old))
 
     def _swarm_minima(self, fit):
         """Per subswarm: (min fitness, its position) over all ranks, first particle on ties, a NaN
@@ -341,7 +381,7 @@ class ParticleSubswarmOptimisationGPU:
             # the previous generation's share candidates as S - 1 more envs of this rollout (each
             # env's episode is independent of the batch: the same fitness bits as on their own);
             # their bests are updated before this generation's (the reference's order)
-            cand = self._pending[2]
+            cand = self._pending[3]
             fit_all, _ = self.evaluate(torch.cat([self.x32c, cand], dim=1))
             fit = fit_all[:self.P]
             self.flush_share(fit_all[self.P:])
@@ -377,10 +417,39 @@ class ParticleSubswarmOptimisationGPU:
         return self.gb, self.gbf
 
     # ------------------------------------------------------------------ share / migrate / re-init
+    def _share_on_device(self, sb, sbf, u):
+        """share_information's decisions on the device, from the S - 1 uniforms the reference's
+        loop draws (one per subswarm but the best, in order -- the count does not depend on which
+        is best): best = the first minimum of sbf (np.argmin), subswarm i != best moves when its
+        uniform (draw i, or i - 1 past best) is below 1/2, and moves 30 % toward the best's
+        position.  Returns the moved subswarms ascending, padded to S - 1 with the first (the
+        share handle's size), their count, and the candidates in the rollout's chunked layout."""
+        S = self.S
+        i = self._cols
+        best = torch.argmin(sbf)
+        k = (i - (i > best).long()).clamp(max=S - 2)
+        moved = (i != best) & (u.index_select(0, k) < 0.5)
+        toward = 0.3 * sb.index_select(0, best.view(1))
+        sb.copy_(torch.where(moved[:, None], (1 - 0.3) * sb + toward, sb))
+        order = torch.argsort(torch.where(moved, i, i + S))
+        count = moved.sum()
+        pos = torch.arange(S - 1, device=self.device)
+        pad = torch.where(pos < count, order[:S - 1], order[0])
+        return pad, count, chunk4(sb.index_select(0, pad).t().float())
+
     def share_information(self):
         """:521-543: for every subswarm but the best, with probability 1/2 its best position moves
         30 % toward the best subswarm's; the moved position is re-evaluated and its fitness kept
-        only if better (the position is kept either way, as in the reference)."""
+        only if better (the position is kept either way, as in the reference).  When the
+        candidates ride along with the next rollout the decisions are taken on the device from
+        the host's uniforms (no read-back: the host used to wait for the queue to read the bests,
+        idling the GPU ~250 us every communication_freq generations)."""
+        if self._mergeable():
+            self.flush_share()
+            u = _to_device([self.rng.random() for _ in range(self.S - 1)], torch.float64, self.device)
+            pad, count, cand = self._share_on_device(self.sb, self.sbf_t, u)
+            self._pending = (getattr(self, "_gen", None), pad, count, cand)
+            return
         best = int(np.argmin(self.sbf))                         # (one read-back: the rng draws depend on it)
         moved = [i for i in range(self.S) if i != best and self.rng.random() < 0.5]
         if not moved:
@@ -390,7 +459,7 @@ class ParticleSubswarmOptimisationGPU:
         pad = moved + [moved[0]] * (self.S - 1 - len(moved))  # (padded to the share handle's size)
         cand = chunk4(self.sb[pad].t().float())                 # [ceil(D/4)][S-1][4]
         # evaluated with the next generation's rollout (or on the next read of the bests)
-        self._pending = (getattr(self, "_gen", None), moved, cand)
+        self._pending = (getattr(self, "_gen", None), moved, None, cand)
 
     def migrate_particles(self):
         """:545-553: number_of_migrants random particles of every subswarm (with > 1 member) move
@@ -400,8 +469,13 @@ class ParticleSubswarmOptimisationGPU:
         for g, t in moves:
             self.swarm_host[g] = t
         mine = local_moves(moves, self.offset, self.P)
-        for g, t in mine.items():          # (scalar writes: no host-to-device copy, no wait)
-            self.swarm[g] = t
+        if mine:
+            # one pinned, stream-ordered copy of the (index, subswarm) pairs and one scatter: a
+            # Python-int item write is a pageable 4-byte copy, which waits for the queue (two of
+            # them idled the GPU 30-37 us each per migration, profiles/r06_exp_policy_init.json)
+            idx = _to_device(list(mine.keys()), torch.int64, self.device)
+            val = _to_device(list(mine.values()), torch.int32, self.device)
+            self.swarm.index_put_((idx,), val)
 
     def re_initialise_swarms(self):
         """:360-370: every subswarm keeps its re_initialise_number_of_particles // S best
