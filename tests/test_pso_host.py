@@ -65,3 +65,47 @@ def test_chunk4_layout_and_inverse():
         assert torch.equal(unchunk4(w4, D), w)
         v = torch.rand(D, 3, generator=g)
         assert torch.equal(torch.cat([w4, chunk4(v)], dim=1), chunk4(torch.cat([w, v], dim=1)))
+
+
+def test_share_decisions_on_device_equal_the_list_restatement():
+    """share_information's device path (_share_on_device, CPU tensors here) takes the reference's
+    decisions (particle_swarm_optimisation.py:521-543 as the host path states them): best = the
+    first minimum of the subswarm bests, one uniform per subswarm but the best, in order, moved
+    when below 1/2, moved positions 30 % toward the best's; the candidates are the moved subswarms
+    ascending, padded with the first; and the strictly-better replacement leaves nothing changed
+    when nothing moved (ties, +inf bests and S = 2..6 included)."""
+    from pdenv.pso import ParticleSubswarmOptimisationGPU, chunk4
+    rng = np.random.default_rng(3)
+    opt = object.__new__(ParticleSubswarmOptimisationGPU)
+    for trial in range(300):
+        S = int(rng.integers(2, 7))
+        D = int(rng.choice([5, 8, 372]))
+        opt.S, opt.device = S, torch.device("cpu")
+        opt._cols = torch.arange(S)
+        sbf = rng.choice([1.0, 2.0, 3.0, np.inf], S) if trial % 3 == 0 else rng.uniform(0, 10, S)
+        sb = rng.uniform(-1.5, 1.5, (S, D))
+        u = rng.uniform(0, 1, S - 1)
+        # the host path's list restatement, drawing the same uniforms in order
+        draws = iter(u.tolist())
+        best = int(np.argmin(sbf))
+        moved = [i for i in range(S) if i != best and next(draws) < 0.5]
+        sb_ref = sb.copy()
+        for i in moved:
+            sb_ref[i] = (1 - 0.3) * sb_ref[i] + 0.3 * sb_ref[best]
+        sb_t, sbf_t = torch.tensor(sb), torch.tensor(sbf)
+        pad, count, cand = opt._share_on_device(sb_t, sbf_t, torch.tensor(u))
+        assert int(count) == len(moved)
+        assert np.array_equal(sb_t.numpy(), sb_ref)
+        if moved:
+            want = moved + [moved[0]] * (S - 1 - len(moved))
+            assert pad.tolist() == want
+            assert torch.equal(cand, chunk4(torch.tensor(sb_ref[want]).t().float()))
+        fit = torch.tensor(rng.uniform(0, 10, S - 1))
+        if moved:                               # the padded entries repeat the first candidate
+            fit[len(moved):] = fit[0]
+        sbf_ref = sbf.copy()
+        for k, i in enumerate(moved):
+            if fit[k] < sbf_ref[i]:
+                sbf_ref[i] = float(fit[k])
+        opt._flush_on_device(sbf_t, pad, count, fit)
+        assert np.array_equal(sbf_t.numpy(), sbf_ref)
