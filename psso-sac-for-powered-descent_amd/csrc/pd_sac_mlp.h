@@ -27,7 +27,9 @@
 // (profiles/r05_resource_usage.txt, the SAC LPE-16 rows).  Each k-block waits for its ring
 // fill with s_waitcnt vmcnt(0), which also drains the env-state and table-staging loads the
 // step kernel issued ahead of the actor; the c5 gain of the ring was measured with both costs
-// in it.
+// in it.  A partial count cannot keep those loads in flight: vmcnt
+// counts vector-memory loads, the LDS DMA fills among them, retiring in issue order, so a wait
+// for a ring fill is a wait for every load issued before it.
 // Numerics: f32 throughout (the reference's dtype); the sums run in another order than
 // hipBLASLt's (both are f32 GEMMs of the same Linear layers), so the heads agree with torch's to
 // f32 rounding, not bit for bit (tests/test_gpu_parity.py bounds it).  pd_sac_actor and the fused
