@@ -247,9 +247,9 @@ def bench_pso(args, world, rank, local, dist):
     """Config c4: generations of the particle subswarm optimisation over P particles per GPU
     (phase landing_burn, 372-parameter simple_actor per particle, swarm initialised U(-1.5, 1.5)
     as initialize_swarms does).  One timed step = one generation: every particle's episode with
-    the actor fused into the step kernel (pd_rollout_policy, until done/truncated, cap 2200),
-    subswarm/global bests with the per-subswarm minima exchanged across ranks, and the
-    velocity/position update (pd_pso_step)."""
+    the actor fused into the step kernel (pd_rollout_policy_chunked, until done/truncated, cap
+    2200), subswarm/global bests with the per-subswarm minima exchanged across ranks, and the
+    velocity/position update (pd_pso_step_chunked, which writes the next rollout's weights)."""
     import torch
     from pdenv.pso import ParticleSubswarmOptimisationGPU
     P = args.particles
@@ -268,8 +268,9 @@ def bench_pso(args, world, rank, local, dist):
         opt.generation(args.warmup + k)
     # episode lengths of the timed generations (a separate evaluation pass is not timed)
     wall = timed_region(one, args.steps, torch.cuda.synchronize, dist, opt.device)
-    # the dominant kernel: the policy rollout of the swarm's current positions (pd_rollout_policy:
-    # k_step<POL> launches until every episode ended), replayed with a HIP event pair per rollout
+    # the dominant kernel: the policy rollout of the swarm's current positions
+    # (pd_rollout_policy_chunked: k_step<POL> launches until every episode ended), replayed with a
+    # HIP event pair per rollout
     kern = []
     for _ in range(max(1, min(args.steps, 8))):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -306,10 +307,10 @@ def bench_pso(args, world, rank, local, dist):
                      "traffic": pmc_traffic(f"c4_{P}", P), "traffic_bytes_per_particle_episode": pmc_traffic(f"c4_{P}", 1),
                      "traffic_source": PMC_C4C5 + f" (case c4_{P}: 2 FETCH_SIZE + WRITE_SIZE of the policy k_step "
                                        f"launches of one rollout, per rollout of {P} particles; null: no pass at this size)",
-                     "bytes_per_particle_episode": round(bpp, 1), "kernel": "k_step<POL> (pd_rollout_policy)",
+                     "bytes_per_particle_episode": round(bpp, 1), "kernel": "k_step<POL> (pd_rollout_policy_chunked)",
                      "kernel_avg_ms": kern_avg, "kernel_med_ms": kern_ms[len(kern_ms) // 2], "rollouts": len(kern_ms),
-                     "kernel_timing": "HIP events around each replayed rollout of the swarm's positions (its reset, "
-                                      "k_step launches, count checks and miss flush)",
+                     "kernel_timing": "HIP events around each replayed rollout of the swarm's positions "
+                                      "(k_policy_init, the k_step launches, k_policy_finish)",
                      "bytes_source": "SURVEY 8(d) landing_burn env bytes x mean episode length + the actor's parameters"},
     }
     if args.cpu_baseline and world == 1:
