@@ -5,8 +5,8 @@ ParticleSubswarmOptimisation.run (src/particle_swarm_optimisation/particle_swarm
 pd_rollout_policy_chunked (the actor fused into the step kernel), the personal-best / velocity /
 position update is pd_pso_step_chunked (binary64, parameter-major [D][P]; its float32 copy is
 written in the rollout's chunked weight layout, so a generation makes no copy pass), and only
-per-subswarm minima cross ranks.  The reference's parameters (configs/evolutionary_algorithms_config.py)
-are the defaults; the population can be scaled to config c4's 262 144 particles.
+per-subswarm minima cross ranks.  The reference's parameters
+(configs/evolutionary_algorithms_config.py) are the defaults; the population can be scaled to config c4's 262 144 particles.
 
 Randomness: positions U(bounds) at init, r1/r2 per particle and generation (Philox, in the
 kernel), and a seeded Python `random.Random` for the share/migrate decisions that the reference
@@ -397,10 +397,11 @@ class ParticleSubswarmOptimisationGPU:
                                              _ptr(self.gbf_t), _ptr(self.gb_t), _stream(self.device)))
         self.w = self.p["w_start"] - (self.p["w_start"] - self.p["w_end"]) * gen / self.p["generations"]
         if self.P > 0:
-            L.check(self.lib.pd_pso_step_chunked(self.P, self.D, _ptr(fit), _ptr(self.pbf), _ptr(self.x), _ptr(self.v),
-                                         _ptr(self.pb), _ptr(self.sb), _ptr(self.swarm), _ptr(self.lower),
-                                         _ptr(self.upper), float(self.w), float(self.p["c1"]), float(self.p["c2"]),
-                                         self.seed, gen, self.offset, _ptr(self.x32c), _stream(self.device)))
+            L.check(self.lib.pd_pso_step_chunked(self.P, self.D, _ptr(fit), _ptr(self.pbf), _ptr(self.x),
+                                                 _ptr(self.v), _ptr(self.pb), _ptr(self.sb), _ptr(self.swarm),
+                                                 _ptr(self.lower), _ptr(self.upper), float(self.w), float(self.p["c1"]),
+                                                 float(self.p["c2"]), self.seed, gen, self.offset, _ptr(self.x32c),
+                                                 _stream(self.device)))
         self._gen = gen
         if gen % self.p["communication_freq"] == 0 and gen > 0:
             self.share_information()
