@@ -6,6 +6,7 @@ Tolerances (fp64 handle): teacher-forced single env-step <= 1e-10 relative per c
 per-channel range; the attitude channels are chaotic).  fp32 handle:
 teacher-forced <= 1e-4 relative on non-attitude channels.
 """
+import math
 import os
 
 import numpy as np
@@ -658,16 +659,18 @@ def test_pso_step_chunked_matches_numpy(pd, D):
     assert np.array_equal(unchunk4(x32c, D).cpu().numpy(), xn.astype(np.float32))
 
 
-@pytest.mark.parametrize("phase", ["landing_burn", "landing_burn_pure_throttle"])
-def test_rollout_policy_chunked_same_bits(pd, phase):
+@pytest.mark.parametrize("phase,wind", [("landing_burn", False), ("landing_burn_pure_throttle", False),
+                                        ("landing_burn", True)])
+def test_rollout_policy_chunked_same_bits(pd, phase, wind):
     """pd_rollout_policy_chunked on chunk4'd weights gives pd_rollout_policy's fitness and
-    episode lengths bit for bit (refill launch and the compacted list)."""
+    episode lengths bit for bit (refill launch and the compacted list; with stochastic wind the
+    per-check launches)."""
     import torch
     from pdenv.env import _ptr, _stream
     from pdenv import _lib as L
     from pdenv.pso import chunk4
     n = 3000
-    env = pd.PoweredDescentEnv(n, flight_phase=phase, mode="pso", device=0)
+    env = pd.PoweredDescentEnv(n, flight_phase=phase, mode="pso", device=0, enable_wind=wind, stochastic_wind=wind)
     D = 372 if phase == "landing_burn" else 249
     W = torch.from_numpy(np.random.default_rng(11).uniform(-1.5, 1.5, (D, n)).astype(np.float32)).cuda()
     W4 = chunk4(W)
@@ -776,6 +779,34 @@ def test_pso_share_merged_into_next_rollout(pd):
         assert ga == gb and ma == mb and torch.equal(fa, fb)
     for k in ("x", "v", "pb", "pbf", "swarm", "sb", "sbf_t", "gbf_t", "gb_t"):
         assert torch.equal(getattr(a, k), getattr(b, k)), k
+
+
+def test_pso_driver_stochastic_wind_host_share_path(pd):
+    """The PSO driver on a windy swarm with stochastic gusts: its share candidates cannot ride
+    with the next rollout (a candidate's gusts depend on its env index), so share_information
+    takes the host path and evaluates them on the share handle; the policy rollouts run the windy
+    kernels' per-check launches.  Two runs of the same seed agree bit for bit; every share that
+    moved a subswarm is logged with its candidates' finite fitness."""
+    import torch
+    from pdenv.pso import ParticleSubswarmOptimisationGPU
+    prm = dict(generations=5, communication_freq=1, migration_freq=2, num_sub_swarms=3, re_initialise_generation=99)
+    runs = []
+    for _ in range(2):
+        opt = ParticleSubswarmOptimisationGPU("landing_burn", pso_params=prm, pop_size=96, seed=11, max_steps=300,
+                                              enable_wind=True, stochastic_wind=True)
+        assert not opt._mergeable()
+        for g in range(5):
+            opt.generation(g)
+        opt.flush_share()
+        runs.append(opt)
+    a, b = runs
+    ha, hb = a.share_history, b.share_history
+    assert len(ha) == len(hb) >= 1
+    for (ga, ma, fa), (gb, mb, fb) in zip(ha, hb):
+        assert ga == gb and ma == mb and torch.equal(fa, fb) and bool(torch.isfinite(fa).all())
+    for k in ("x", "v", "pb", "pbf", "swarm", "sb", "sbf_t", "gbf_t", "gb_t"):
+        assert torch.equal(getattr(a, k), getattr(b, k)), k
+    assert math.isfinite(a.gbf)
 
 
 def test_pso_driver_generations_vs_numpy(pd):
