@@ -1793,16 +1793,10 @@ __global__ __launch_bounds__(kBlock) void k_wchunk(const float* __restrict__ w, 
     out[t] = make_float4(v[0], v[1], v[2], v[3]);
 }
 
-// policy rollouts: every env live, in index order
-__global__ __launch_bounds__(kBlock) void k_live_init(int32_t* list, uint32_t* cnt, int64_t n) {
-    int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i < n) list[i] = (int32_t)i;
-    if (i < 3) cnt[i] = i == 0 ? (uint32_t)n : 0u;
-}
-
-// policy rollouts' prologue in one launch: k_reset of every env, its fitness zeroed, and the live
-// list / counts of k_live_init (refill: the three counts zero, the refill launch's hand-out
-// counter among them) -- the four launches a rollout used to start with
+// policy rollouts' prologue in one launch: k_reset of every env, its fitness zeroed, every env
+// live in index order (the list, count 0 = n and the other two counts zero; refill: the three
+// counts zero, the refill launch's hand-out counter among them) -- the four launches a rollout
+// used to start with
 template <typename R>
 __global__ __launch_bounds__(kBlock) void k_policy_init(StepArgs<R> a, R* __restrict__ fitness, int32_t* list,
                                                         uint32_t* cnt, int refill) {
