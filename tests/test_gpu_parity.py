@@ -690,6 +690,43 @@ def test_rollout_policy_chunked_same_bits(pd, phase, wind):
     env.close()
 
 
+def test_rollout_policy_repeat_and_null_steps(pd):
+    """A policy rollout starts from nothing its handle's previous rollouts left (k_policy_init:
+    every env reset, fitness zeroed, live list and counts re-initialised): the same weights on
+    the same handle give the same bits after a rollout of other weights, with and without the
+    episode-length output (k_policy_finish skips the copy when steps is NULL), on the refill
+    launch and on the per-check list launches."""
+    import torch
+    from pdenv.env import _ptr, _stream
+    from pdenv import _lib as L
+    from pdenv.pso import chunk4
+    n, D = 2500, 372
+    env = pd.PoweredDescentEnv(n, flight_phase="landing_burn", mode="pso", device=0)
+    g = np.random.default_rng(21)
+    W = chunk4(torch.from_numpy(g.uniform(-1.5, 1.5, (D, n)).astype(np.float32)).cuda())
+    W2 = chunk4(torch.from_numpy(g.uniform(-1.5, 1.5, (D, n)).astype(np.float32)).cuda())
+    lib = L.load()
+
+    def roll(w, with_steps=True):
+        fit = torch.full((n,), 123.0, dtype=torch.float64, device="cuda")
+        steps = torch.empty(n, dtype=torch.int32, device="cuda") if with_steps else None
+        L.check(lib.pd_rollout_policy_chunked(env.h, _ptr(w), D, 400, _ptr(fit), _ptr(steps) if with_steps else None,
+                                              8, _stream(env.device)))
+        torch.cuda.synchronize()
+        return fit.cpu().numpy(), (steps.cpu().numpy() if with_steps else None)
+
+    for tune in (dict(), dict(policy_refill=-1, policy_list=1)):
+        if tune:
+            env.set_tuning(**tune)
+        f0, s0 = roll(W)
+        roll(W2)
+        f1, s1 = roll(W)
+        f2, _ = roll(W, with_steps=False)
+        assert np.array_equal(f0, f1) and np.array_equal(s0, s1) and np.array_equal(f0, f2), tune
+        assert (s0 >= 1).all() and np.isfinite(f0).all()
+    env.close()
+
+
 def test_pso_swarm_minima_and_bests_vs_numpy(pd):
     """pd_pso_swarm_minima (the reference's sequential `if fitness < subswarm_best` per subswarm,
     particle_swarm_optimisation.py:437-441: a NaN never wins, ties keep the lower index, +inf for
